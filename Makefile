@@ -1,0 +1,23 @@
+# libsamplers_hip.so — MI355X (gfx950) hot path.  `make` builds in-tree so the
+# .so travels to the GPU box with the repo snapshot.
+HIPCC ?= /opt/rocm/bin/hipcc
+ARCH  ?= gfx950
+CXXFLAGS ?= -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -Wall -Wno-unused-result
+SRC := samplers_amd/csrc/sp_dps.hip samplers_amd/csrc/sp_blur.hip
+OBJ := $(patsubst samplers_amd/csrc/%.hip,build/%.o,$(SRC))
+LIB := samplers_amd/lib/libsamplers_hip.so
+
+all: $(LIB)
+
+build/%.o: samplers_amd/csrc/%.hip samplers_amd/csrc/sp_common.h include/samplers_hip.h
+	@mkdir -p build
+	$(HIPCC) $(CXXFLAGS) -c $< -o $@
+
+$(LIB): $(OBJ)
+	@mkdir -p samplers_amd/lib
+	$(HIPCC) -shared --offload-arch=$(ARCH) -o $@ $(OBJ)
+
+clean:
+	rm -rf build $(LIB)
+
+.PHONY: all clean

@@ -1,0 +1,263 @@
+"""Headline benchmark: posterior samples/sec of DPS on CelebA-HQ-256 (BASELINE.json).
+
+    python bench.py [--gpus N --steps K --warmup W]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
+
+Workload (BASELINE.json configs[1], "config 2"): DPS + 50 % random inpainting
+mask + GaussianNoise(sigma=0.05) on 3x256x256 images, prior = the
+ddpm-celebahq-256 UNet architecture (113.7 M parameters, random weights with a
+fixed seed — no checkpoint offline), fp32, 64 samples per GPU, DDPM schedule
+with 1000 steps.  One bench step = one guided DPS iteration over the whole
+per-GPU batch: UNet forward + HIP residual pass + UNet input-VJP + HIP update
+pass (``samplers_amd.samplers.dps.FusedDPSStep``), timesteps walking down from
+t = 999 as in the sampler.  Inputs are resident in HBM before timing starts.
+
+value = (samples per GPU x GPUs x K steps) / max-over-ranks wall time of the K
+timed steps (weak scaling: the per-GPU batch is fixed).  The sample batch is
+sharded over ranks with no data-path collective (DPS samples are independent,
+SURVEY.md F6); Philox noise is keyed by the global sample index.
+
+Also reported:
+  roofline      dominant HIP guidance kernel: algorithmic bytes per launch /
+                mean launch time from HIP events on the launch stream, against
+                the 8 TB/s HBM peak; traffic = PMC-measured HBM bytes per launch
+                (profiles/pmc_traffic.json, separate rocprofv3 --pmc passes)
+  cpu_baseline  oracle/dps_loop.py (torch-CPU restatement of dps.py) with the
+                same UNet, timed on this host's cores for a bounded sample
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent
+os.environ.setdefault("MIOPEN_USER_DB_PATH", str(ROOT / ".miopen_cache"))
+os.environ.setdefault("MIOPEN_CUSTOM_CACHE_DIR", str(ROOT / ".miopen_cache"))
+sys.path.insert(0, str(ROOT))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec, MI355X_MICROARCH.md
+METRIC = "posterior samples/sec (batch×steps/s), DPS CelebA-HQ-256 @1/2/4/8 GPU"
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=5)
+    p.add_argument("--warmup", type=int, default=2)
+    p.add_argument("--batch", type=int, default=64, help="samples per GPU")
+    p.add_argument("--image", type=int, default=256)
+    p.add_argument("--micro-batch", type=int, default=0)
+    p.add_argument("--cpu-seconds", type=float, default=15.0)
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    return p.parse_args()
+
+
+def log(msg: str) -> None:
+    print(f"[bench] {msg}", file=sys.stderr, flush=True)
+
+
+def setup_dist(gpus: int):
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != gpus:
+        raise SystemExit(f"--gpus {gpus} but WORLD_SIZE={world}")
+    torch.cuda.set_device(local)
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", rank=rank, world_size=world,
+                                device_id=torch.device("cuda", local))
+    return rank, world, torch.device("cuda", local)
+
+
+def build_workload(batch: int, image: int, rank: int, device):
+    from samplers_amd.inverse_problem import InverseProblem
+    from samplers_amd.networks.ddpm import DDPMNetwork
+    from samplers_amd.noise import GaussianNoise
+    from samplers_amd.operators import RandomInpaintingOperator
+
+    shape = (3, image, image)
+    op = RandomInpaintingOperator(shape, fraction=0.5, seed=1).to(device)
+    noise = GaussianNoise(0.05).to(device)
+    gen = torch.Generator().manual_seed(1000 + rank)  # per-rank shard of the synthetic dataset
+    x_true = torch.rand((batch, *shape), generator=gen) * 2 - 1
+    y_clean = op.apply(x_true.to(device))  # HIP gather
+    y = y_clean + (0.05 * torch.randn(tuple(y_clean.shape), generator=gen)).to(device)
+    net = DDPMNetwork.from_config(seed=0, device=device, torch_dtype=torch.float32)
+    net.set_sampling_parameters(1000, batch_size=batch)
+    return InverseProblem(op, y, noise), net, shape
+
+
+def guidance_bytes(n: int, m: int, words: int) -> dict[str, float]:
+    """Algorithmic HBM bytes per sample (fp32): SURVEY.md §8d, 4(7n + 2m) + index."""
+    return {
+        "dps_residual": 4.0 * (3 * n + m),  # read x, eps, y; write v
+        "dps_update": 4.0 * (4 * n + m),    # read x, eps, w, y; write x'
+        "index_per_launch": 12.0 * words,   # keep bits + word ranks, once per launch
+    }
+
+
+def cpu_baseline(image: int, seconds: float) -> dict:
+    """oracle/dps_loop.py on the host cores, B=1, same workload per sample."""
+    from oracle import dps_loop
+    from samplers_amd.networks.unet2d import build_unet
+    from samplers_amd.operators import get_mask_random
+
+    cores = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
+    cores = max(1, min(cores, 16))
+    torch.set_num_threads(cores)
+    shape = (3, image, image)
+    unet = build_unet(seed=0)
+    mask = get_mask_random(shape, 0.5, seed=1)
+    kept = torch.nonzero(~mask.flatten()).squeeze(1)
+    gen = torch.Generator().manual_seed(1000)
+    x_true = torch.rand((1, *shape), generator=gen) * 2 - 1
+    y = x_true.reshape(1, -1)[:, kept] + 0.05 * torch.randn(1, kept.numel(), generator=gen)
+    betas = torch.linspace(1e-4, 0.02, 1000, dtype=torch.float32)
+    acp = torch.cat([torch.ones(1), torch.cumprod(1 - betas, 0)]).clip(1e-6, 1)
+    ts = list(range(1000))
+    x = torch.randn((1, *shape), generator=gen)
+    apply_op = lambda v: v.reshape(v.shape[0], -1)[:, kept]  # noqa: E731
+    lp = dps_loop.gaussian_log_prob(0.05)
+    noise = lambda i: torch.randn((1, *shape), generator=gen)  # noqa: E731
+    # one warm-up iteration, then as many as fit in `seconds` (at least 2)
+    x = dps_loop.dps_reference(lambda v, t: unet(v, t), acp, ts, apply_op, lp, y, x, noise,
+                               gamma=1.0, eta=1.0, steps_limit=1, return_sample=True)
+    done, t0 = 0, time.perf_counter()
+    while done < 2 or time.perf_counter() - t0 < seconds:
+        x = dps_loop.dps_reference(lambda v, t: unet(v, t), acp, ts, apply_op, lp, y, x, noise,
+                                   gamma=1.0, eta=1.0, steps_limit=1, return_sample=True)
+        done += 1
+    dt = time.perf_counter() - t0
+    return {
+        "value": round(done / dt, 4),
+        "unit": "samples/sec (batch×steps/s)",
+        "cores": cores,
+        "kind": "port",
+        "sample": f"batch=1, {done} guided DPS iterations (t=999) of "
+                  f"oracle/dps_loop.py at 3x{image}x{image}, 50% random mask, same random-init "
+                  f"UNet, fp32, torch-CPU {torch.__version__}",
+    }
+
+
+def main():
+    args = parse()
+    rank, world, device = setup_dist(args.gpus)
+    torch.backends.cudnn.benchmark = False  # MIOpen immediate mode: no exhaustive search
+    from samplers_amd import _hip
+    from samplers_amd.samplers.dps import FusedDPSStep, KernelTimer
+
+    _hip.load_library()
+    problem, net, shape = build_workload(args.batch, args.image, rank, device)
+    n = int(np.prod(shape))
+    m = problem.operator.shape[0]
+    timer = KernelTimer()
+    step = FusedDPSStep(net, problem, problem.observation, 1, gamma=1.0, eta=1.0,
+                        micro_batch=args.micro_batch or None, timer=timer)
+    from samplers_amd.samplers.dps import initial_sample
+
+    seed = 20260101
+    x = initial_sample((args.batch, *shape), device, rng="philox", seed=seed,
+                       sample_offset=rank * args.batch, noise_fn=None)
+    ts = net.timesteps_host
+    it = iter(range(len(ts) - 1, 1, -1))
+
+    def one_step():
+        i = next(it)
+        step(x, i, ts[i], ts[i - 1], ts[0], seed=seed, sample_offset=rank * args.batch)
+
+    t_w = time.perf_counter()
+    for k in range(args.warmup):
+        one_step()
+        torch.cuda.synchronize()
+        log(f"warmup step {k + 1}/{args.warmup} done at {time.perf_counter() - t_w:.1f}s")
+    timer.clear()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        one_step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=device, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    if not torch.isfinite(x).all():
+        raise SystemExit("non-finite samples")
+
+    kern = timer.summary()
+    nbytes = guidance_bytes(n, m, (n + 63) // 64)
+    rl = {}
+    for name in ("dps_residual", "dps_update"):
+        d = kern[name]
+        avg_ms = d["ms"] / d["count"]
+        per_launch = nbytes[name] * d["samples"] / d["count"] + nbytes["index_per_launch"]
+        rl[name] = {"avg_ms": avg_ms, "bytes": per_launch, "gbs": per_launch / avg_ms / 1e6}
+    dominant = max(rl, key=lambda k: rl[k]["avg_ms"])
+    traffic = None
+    pmc = ROOT / "profiles" / "pmc_traffic.json"
+    if pmc.exists():
+        try:
+            traffic = json.loads(pmc.read_text()).get(f"{dominant}@B{args.batch}_{args.image}")
+        except (ValueError, OSError):
+            traffic = None
+
+    total = args.batch * world * args.steps
+    value = total / elapsed
+    result = {
+        "metric": METRIC,
+        "value": round(value, 3),
+        "unit": "samples/sec (batch×steps/s)",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (seeded U(-1,1) images, 50% random mask, sigma=0.05 Gaussian noise; "
+                "random-init ddpm-celebahq-256 UNet architecture)",
+        "config": {"workload": "DPS + InpaintingMask(50% random) + GaussianNoise(0.05), "
+                               f"3x{args.image}x{args.image}, ddpm-celebahq-256 prior, "
+                               "1000-step DDPM schedule (BASELINE configs[1])",
+                   "global_batch": args.batch * world, "per_gpu_batch": args.batch,
+                   "parallelism": f"sample-batch shards x{world}, no data-path collective"},
+        "roofline": {
+            "kernel": dominant,
+            "bound": "hbm",
+            "achieved": round(rl[dominant]["gbs"], 1),
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": round(rl[dominant]["gbs"] / HBM_PEAK_GBS, 4),
+            "traffic": traffic,
+            "algorithmic_bytes_per_launch": rl[dominant]["bytes"],
+            "avg_launch_ms": round(rl[dominant]["avg_ms"], 5),
+        },
+        "guidance_kernels": {k: {"avg_ms": round(v["avg_ms"], 5), "GB/s": round(v["gbs"], 1)}
+                             for k, v in rl.items()},
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        log("timing the CPU baseline ...")
+        result["cpu_baseline"] = cpu_baseline(args.image, args.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

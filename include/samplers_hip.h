@@ -1,0 +1,137 @@
+/*
+ * samplers_hip.h — C ABI of libsamplers_hip.so, the MI355X (gfx950) hot path of
+ * diffusion posterior sampling (DPS / PSLD / PGDM / ReSample guidance steps).
+ *
+ * The reference (thomashirtz/samplers) is pure Python over PyTorch; every entry
+ * point below replaces a group of eager ATen calls that the reference issues
+ * per reverse-diffusion step.  Each declaration cites the reference code it
+ * replaces (paths relative to the reference repository root).
+ *
+ * Conventions (all entry points):
+ *   - device pointers to contiguous fp32 data; a "sample" is one row of
+ *     n = C*H*W elements (x-space) or m elements (y-space, observation);
+ *   - `stream` is the caller's hipStream_t (PyTorch passes its current stream);
+ *     every call is asynchronous on that stream and never synchronises;
+ *   - the library allocates nothing; callers pass every buffer;
+ *   - return 0 on success, a negative SP_E* code on bad arguments or a failed
+ *     launch (the launch error is also readable through sp_last_error()).
+ *   - observation row for sample b is b / y_div (y_div = number of
+ *     reconstructions sharing one observation, >= 1).
+ */
+#ifndef SAMPLERS_HIP_H
+#define SAMPLERS_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef void* sp_stream_t; /* hipStream_t */
+
+enum {
+    SP_OK = 0,
+    SP_EINVAL = -1,   /* bad argument (null pointer, size, unsupported operator kind) */
+    SP_ELAUNCH = -2,  /* kernel launch failed */
+    SP_EUNSUPPORTED = -3
+};
+
+/* Operator kinds (reference: samplers/operators/). */
+enum {
+    SP_OP_IDENTITY = 0, /* identity.py:8-68        y = x                      */
+    SP_OP_INPAINT = 1,  /* inpainting.py:8-195     y = x.flat[kept]            */
+    SP_OP_BLUR = 2,     /* new (BASELINE config 3): depthwise separable Gaussian
+                           blur with reflect padding; adjoint = exact transpose */
+    SP_OP_MASK = 3      /* inpainting.py:106-109 (flatten=False): y = x with the
+                           masked pixels zeroed; uses keep_bits only, m == n   */
+};
+
+/* Forward-operator descriptor.  Device arrays are owned by the caller
+ * (the Python Operator's buffers) and must outlive every call using them. */
+typedef struct sp_op {
+    int32_t kind;
+    int32_t channels, height, width; /* x_shape = (C, H, W); n = C*H*W        */
+    int64_t n;                       /* elements per x sample                 */
+    int64_t m;                       /* elements per y sample                 */
+    const uint64_t* keep_bits;       /* INPAINT: ceil(n/64) words; bit (j%64) of
+                                        word j/64 set <=> x[j] observed (= ~mask) */
+    const int32_t* word_rank;        /* INPAINT: observed count before word w  */
+    const float* taps;               /* BLUR: 2*radius+1 normalised taps       */
+    int32_t radius;                  /* BLUR: 1..8                             */
+    int32_t reserved;
+} sp_op;
+
+/* Scalars of one DPS step (all fp32, computed on the host exactly as the
+ * reference computes them). */
+typedef struct sp_dps_coefs {
+    float a;          /* sqrt(alpha_bar[t])      networks/base.py:41-43          */
+    float k;          /* sqrt(1 - alpha_bar[t])                                   */
+    float grad_scale; /* d logp / d(Ax): 1/sigma^2 (noise.py:77-79) or
+                         2/(rate+1e-3) (noise.py:121-123)                          */
+    float c_ell;      /* bridge_coeff_ell        bridge_kernels.py:36            */
+    float c_s;        /* bridge_coeff_s          bridge_kernels.py:37            */
+    float std;        /* bridge_std              bridge_kernels.py:33-35         */
+    float gamma;      /* DPS step size           dps.py:121                      */
+    float norm_eps;   /* 1e-9                    dps.py:121                      */
+} sp_dps_coefs;
+
+/* Library / ABI version (major*10000 + minor*100 + patch). */
+int sp_version(void);
+/* Text of the last launch error on this thread ("" if none). */
+const char* sp_last_error(void);
+
+/* Number of per-sample partial sums written by sp_dps_residual for `op`
+ * (callers allocate batch * sp_rsq_partials(op) floats). */
+int64_t sp_rsq_partials(const sp_op* op);
+
+/* DPS pass 1 — replaces dps.py:99-103 up to the prior's VJP and dps.py:117-118:
+ *   x0  = (x - k*eps)/a                         (networks/base.py:41-43)
+ *   r   = y - A(x0)                             (inverse_problem.py:17-18)
+ *   v   = A^T(grad_scale * r)  -> v_out         (autograd of noise.log_prob through A)
+ *   rsq_partial[b][p] = partial sums of r^2 over sample b (dps.py:117-120).
+ * v_out is the cotangent of x0; the caller feeds it to the prior's VJP. */
+int sp_dps_residual(const sp_op* op, const float* x, const float* eps, const float* y,
+                    int64_t batch, int64_t y_div, const sp_dps_coefs* c,
+                    float* v_out, float* rsq_partial, sp_stream_t stream);
+
+/* DPS pass 2 — replaces dps.py:106-122 (ddim_step -> sample_bridge_kernel and
+ * the guidance correction):
+ *   g   = v/a - (k/a) * w          (w = J_eps^T v from the prior's VJP)
+ *   x'  = c_ell*x + c_s*x0 + std*xi + gamma/(sqrt(sum_p rsq_partial[b][p]) + norm_eps) * g
+ * v: pass NULL to recompute v from (x, eps, y) (IDENTITY/INPAINT only), else
+ *    the buffer written by sp_dps_residual (required for BLUR).
+ * xi: injected standard-normal noise (B*n) or NULL to draw Philox4x32-10
+ *    normals keyed by (seed, step, sample_offset + b, element) — invariant to
+ *    how the batch is sharded across GPUs.  x_out may alias x. */
+int sp_dps_update(const sp_op* op, const float* x, const float* eps, const float* y,
+                  const float* v, const float* w, const float* rsq_partial, const float* xi,
+                  uint64_t seed, int64_t step, int64_t sample_offset,
+                  int64_t batch, int64_t y_div, const sp_dps_coefs* c,
+                  float* x_out, sp_stream_t stream);
+
+/* x0 = (x - k*eps)/a over `count` elements (networks/base.py:41-43; final
+ * prediction dps.py:125-126). out may alias x. */
+int sp_predict_x0(const float* x, const float* eps, int64_t count, float a, float k,
+                  float* out, sp_stream_t stream);
+
+/* Standard normals, Philox4x32-10 keyed by (seed, step, sample_offset+b, j);
+ * replaces torch.randn / randn_like (dps.py:83-87, bridge_kernels.py:59). */
+int sp_randn(float* out, int64_t batch, int64_t n, uint64_t seed, int64_t step,
+             int64_t sample_offset, sp_stream_t stream);
+
+/* y = A x (operators/base.py:91-92; linear.py:141-152; inpainting.py:132-145). */
+int sp_op_apply(const sp_op* op, const float* x, float* y, int64_t batch, sp_stream_t stream);
+/* x = A^T y (linear.py:154-165; inpainting.py:169-187). */
+int sp_op_adjoint(const sp_op* op, const float* y, float* x, int64_t batch, sp_stream_t stream);
+
+/* Likelihood gradient in y-space (noise.py:19-27 score, 77-79, 121-123):
+ *   r = y[b/y_div] - z[b];  g[b] = grad_scale * r;  rsq_partial[b][p] += r^2 partials.
+ * g may be NULL (norm only).  Partials per sample: sp_vec_partials(m). */
+int64_t sp_vec_partials(int64_t count);
+int sp_residual_grad(const float* y, const float* z, int64_t batch, int64_t m, int64_t y_div,
+                     float grad_scale, float* g, float* rsq_partial, sp_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SAMPLERS_HIP_H */

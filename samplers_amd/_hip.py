@@ -1,0 +1,132 @@
+"""ctypes binding of ``libsamplers_hip.so`` (the C ABI in ``include/samplers_hip.h``).
+
+This is the only door from Python to the HIP kernels.  It fails loudly: if the
+library is missing or a call returns a non-zero status, an exception is raised;
+there is no silent fallback to eager PyTorch on the GPU path.
+"""
+
+from __future__ import annotations
+
+import ctypes
+import os
+from pathlib import Path
+
+import torch
+
+LIB_PATH = Path(__file__).resolve().parent / "lib" / "libsamplers_hip.so"
+
+SP_OP_IDENTITY, SP_OP_INPAINT, SP_OP_BLUR, SP_OP_MASK = 0, 1, 2, 3
+
+_ERRORS = {-1: "invalid argument", -2: "kernel launch failed", -3: "unsupported"}
+
+
+class HipLibraryError(RuntimeError):
+    """The HIP library is missing, failed to load, or a call returned an error."""
+
+
+class SpOp(ctypes.Structure):
+    _fields_ = [
+        ("kind", ctypes.c_int32),
+        ("channels", ctypes.c_int32),
+        ("height", ctypes.c_int32),
+        ("width", ctypes.c_int32),
+        ("n", ctypes.c_int64),
+        ("m", ctypes.c_int64),
+        ("keep_bits", ctypes.c_void_p),
+        ("word_rank", ctypes.c_void_p),
+        ("taps", ctypes.c_void_p),
+        ("radius", ctypes.c_int32),
+        ("reserved", ctypes.c_int32),
+    ]
+
+
+class SpDpsCoefs(ctypes.Structure):
+    _fields_ = [
+        ("a", ctypes.c_float),
+        ("k", ctypes.c_float),
+        ("grad_scale", ctypes.c_float),
+        ("c_ell", ctypes.c_float),
+        ("c_s", ctypes.c_float),
+        ("std", ctypes.c_float),
+        ("gamma", ctypes.c_float),
+        ("norm_eps", ctypes.c_float),
+    ]
+
+
+_P = ctypes.c_void_p
+_I64 = ctypes.c_int64
+_U64 = ctypes.c_uint64
+_F = ctypes.c_float
+_OPP = ctypes.POINTER(SpOp)
+_COP = ctypes.POINTER(SpDpsCoefs)
+
+# name -> (restype, argtypes); mirrors include/samplers_hip.h one-to-one
+SIGNATURES = {
+    "sp_version": (ctypes.c_int, []),
+    "sp_last_error": (ctypes.c_char_p, []),
+    "sp_rsq_partials": (_I64, [_OPP]),
+    "sp_vec_partials": (_I64, [_I64]),
+    "sp_dps_residual": (ctypes.c_int, [_OPP, _P, _P, _P, _I64, _I64, _COP, _P, _P, _P]),
+    "sp_dps_update": (ctypes.c_int, [_OPP, _P, _P, _P, _P, _P, _P, _P, _U64, _I64, _I64,
+                                     _I64, _I64, _COP, _P, _P]),
+    "sp_predict_x0": (ctypes.c_int, [_P, _P, _I64, _F, _F, _P, _P]),
+    "sp_randn": (ctypes.c_int, [_P, _I64, _I64, _U64, _I64, _I64, _P]),
+    "sp_op_apply": (ctypes.c_int, [_OPP, _P, _P, _I64, _P]),
+    "sp_op_adjoint": (ctypes.c_int, [_OPP, _P, _P, _I64, _P]),
+    "sp_residual_grad": (ctypes.c_int, [_P, _P, _I64, _I64, _I64, _F, _P, _P, _P]),
+}
+
+_lib = None
+
+
+def load_library() -> ctypes.CDLL:
+    """Load (once) and type the HIP library; raise HipLibraryError if unavailable."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    path = Path(os.environ.get("SAMPLERS_HIP_LIB", LIB_PATH))
+    if not path.exists():
+        raise HipLibraryError(
+            f"{path} not found: build it with `make` (or __graft_entry__.build()) before "
+            "running the GPU path; there is no CPU fallback."
+        )
+    # torch first: the library must bind to the HIP runtime torch already loaded
+    import torch  # noqa: F401
+
+    lib = ctypes.CDLL(str(path))
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def check(status: int, what: str) -> None:
+    if status != 0:
+        detail = load_library().sp_last_error().decode(errors="replace")
+        raise HipLibraryError(f"{what} failed: {_ERRORS.get(status, status)} {detail}".strip())
+
+
+def ptr(t: torch.Tensor | None) -> int | None:
+    if t is None:
+        return None
+    if not t.is_cuda:
+        raise HipLibraryError("HIP path needs device tensors")
+    if t.dtype != torch.float32 and t.dtype not in (torch.int32, torch.int64, torch.uint8):
+        raise HipLibraryError(f"HIP path computes in fp32, got {t.dtype}")
+    if not t.is_contiguous():
+        raise HipLibraryError("HIP path needs contiguous tensors")
+    return t.data_ptr()
+
+
+def stream_of(t: torch.Tensor) -> int:
+    return torch.cuda.current_stream(t.device).cuda_stream
+
+
+def require_cuda(t: torch.Tensor, what: str) -> None:
+    if not t.is_cuda:
+        raise HipLibraryError(
+            f"{what}: samplers_amd runs its hot path on MI355X (HIP); got a {t.device} tensor. "
+            "The CPU restatement lives in oracle/ and is test infrastructure only."
+        )

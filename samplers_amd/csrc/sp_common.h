@@ -1,0 +1,150 @@
+// Shared device helpers for libsamplers_hip: Philox4x32-10 normals, wave64 /
+// block reductions, vector load/store, launch-error bookkeeping.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/samplers_hip.h"
+
+namespace sp {
+
+constexpr int kBlock = 256;  // 4 waves of 64 lanes
+constexpr int kIter = 4;     // float4 groups per thread per block (elementwise kernels)
+
+// ---------------------------------------------------------------------------
+// Philox4x32-10 (Salmon et al., SC'11).  Counter = (element group, sample, step lo,
+// step hi), key = seed.  The same (seed, step, sample, element) gives the same
+// normal on every shard, so a batch split over N GPUs reproduces the 1-GPU draw.
+// ---------------------------------------------------------------------------
+struct u32x4 { uint32_t x, y, z, w; };
+
+__device__ __forceinline__ u32x4 philox4x32_10(u32x4 c, uint32_t k0, uint32_t k1) {
+    constexpr uint32_t M0 = 0xD2511F53u, M1 = 0xCD9E8D57u;
+    constexpr uint32_t W0 = 0x9E3779B9u, W1 = 0xBB67AE85u;
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+        const uint32_t lo0 = M0 * c.x, hi0 = __umulhi(M0, c.x);
+        const uint32_t lo1 = M1 * c.z, hi1 = __umulhi(M1, c.z);
+        c = u32x4{hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0};
+        k0 += W0;
+        k1 += W1;
+    }
+    return c;
+}
+
+// Uniform in (0,1), exactly representable: ((u >> 9) + 0.5) * 2^-23.
+__device__ __forceinline__ float u01(uint32_t u) {
+    return (static_cast<float>(u >> 9) + 0.5f) * 1.1920928955078125e-07f;
+}
+
+// Four standard normals for element group `grp` (elements 4*grp .. 4*grp+3).
+__device__ __forceinline__ void philox_normal4(uint64_t seed, int64_t step, int64_t sample,
+                                               int64_t grp, float out[4]) {
+    const u32x4 c{static_cast<uint32_t>(grp), static_cast<uint32_t>(sample),
+                  static_cast<uint32_t>(static_cast<uint64_t>(step)),
+                  static_cast<uint32_t>(static_cast<uint64_t>(step) >> 32)};
+    const u32x4 r = philox4x32_10(c, static_cast<uint32_t>(seed), static_cast<uint32_t>(seed >> 32));
+    const float rad0 = sqrtf(-2.0f * logf(u01(r.x)));
+    const float rad1 = sqrtf(-2.0f * logf(u01(r.z)));
+    float s0, c0, s1, c1;
+    sincosf(6.283185307179586f * u01(r.y), &s0, &c0);
+    sincosf(6.283185307179586f * u01(r.w), &s1, &c1);
+    out[0] = rad0 * c0;
+    out[1] = rad0 * s0;
+    out[2] = rad1 * c1;
+    out[3] = rad1 * s1;
+}
+
+// ---------------------------------------------------------------------------
+// Reductions (wave64 butterfly; fixed order -> deterministic).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+// Block sum for kBlock threads; result valid in thread 0.
+__device__ __forceinline__ float block_sum(float v, float* lds4) {
+    v = wave_sum(v);
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    if (lane == 0) lds4[wid] = v;
+    __syncthreads();
+    float t = 0.f;
+    if (threadIdx.x == 0) t = (lds4[0] + lds4[1]) + (lds4[2] + lds4[3]);
+    return t;
+}
+
+// Sum of the P partials of one sample, computed redundantly by every wave
+// (all lanes end with the total; no LDS, no barrier).
+__device__ __forceinline__ float sum_partials(const float* __restrict__ p, int P) {
+    float s = 0.f;
+    for (int i = threadIdx.x & 63; i < P; i += 64) s += p[i];
+    return wave_sum(s);
+}
+
+// ---------------------------------------------------------------------------
+// Vector access
+// ---------------------------------------------------------------------------
+template <int V>
+__device__ __forceinline__ void load_v(const float* __restrict__ p, float (&r)[V]) {
+    if constexpr (V == 4) {
+        const float4 t = *reinterpret_cast<const float4*>(p);
+        r[0] = t.x; r[1] = t.y; r[2] = t.z; r[3] = t.w;
+    } else {
+#pragma unroll
+        for (int e = 0; e < V; ++e) r[e] = p[e];
+    }
+}
+
+template <int V>
+__device__ __forceinline__ void store_v(float* __restrict__ p, const float (&r)[V]) {
+    if constexpr (V == 4) {
+        *reinterpret_cast<float4*>(p) = make_float4(r[0], r[1], r[2], r[3]);
+    } else {
+#pragma unroll
+        for (int e = 0; e < V; ++e) p[e] = r[e];
+    }
+}
+
+// Normals for elements j..j+V-1 of one sample (V = 4 with j % 4 == 0, or V = 1).
+template <int V>
+__device__ __forceinline__ void philox_normals(uint64_t seed, int64_t step, int64_t sample,
+                                               int64_t j, float (&z)[V]) {
+    float q[4];
+    philox_normal4(seed, step, sample, j >> 2, q);
+    if constexpr (V == 4) {
+        z[0] = q[0]; z[1] = q[1]; z[2] = q[2]; z[3] = q[3];
+    } else {
+        const int c = static_cast<int>(j & 3);
+        z[0] = c == 0 ? q[0] : c == 1 ? q[1] : c == 2 ? q[2] : q[3];
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Inpainting index: observed rank of element j (= its index in the packed y).
+// keep_bits bit (j & 63) of word (j >> 6) is 1 when x[j] is observed; the rank
+// is word_rank[j >> 6] + popcount of the lower bits of that word.  Equals the
+// position of j in torch.nonzero(~mask.flatten()) (inpainting.py:49-50).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void inpaint_lookup(const sp_op& op, int64_t j, uint32_t& bits4,
+                                               int64_t& rank0) {
+    const uint64_t word = op.keep_bits[j >> 6];
+    const int sh = static_cast<int>(j & 63);
+    bits4 = static_cast<uint32_t>(word >> sh) & 0xFu;
+    rank0 = op.word_rank[j >> 6] + __popcll(word & ((1ull << sh) - 1ull));
+}
+
+// Observed bits of elements j..j+3 (MASK operator: m == n, no ranks needed).
+__device__ __forceinline__ uint32_t mask_bits(const sp_op& op, int64_t j) {
+    return static_cast<uint32_t>(op.keep_bits[j >> 6] >> (j & 63)) & 0xFu;
+}
+
+// ---------------------------------------------------------------------------
+// host-side error bookkeeping
+// ---------------------------------------------------------------------------
+void set_error(const char* what, hipError_t e);
+int check_launch(const char* what);
+
+}  // namespace sp

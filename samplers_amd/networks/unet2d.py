@@ -1,0 +1,242 @@
+"""Pixel-space DDPM prior: a structural equivalent of diffusers' ``UNet2DModel``.
+
+The reference never builds this network itself; ``DDPMNetwork.forward`` is
+``self.unet(sample=sample, timestep=t).sample`` over a diffusers
+``UNet2DModel`` loaded by name (``/root/reference/samplers/networks/diffusers/
+ddpm.py:40-43``).  Neither diffusers nor the checkpoint is available here, so
+this module rebuilds the architecture of ``google/ddpm-celebahq-256`` (six
+levels of 128/128/256/256/512/512 channels, two residual blocks per level,
+single-head self-attention at 16x16, GroupNorm(32, eps=1e-6) + SiLU,
+sinusoidal time embedding with ``freq_shift=1``) with random weights.  It is
+the prior of the hot path, and it stays in PyTorch-ROCm (MIOpen convolutions,
+hipBLASLt projections); the guidance arithmetic around it is HIP
+(``samplers_amd/csrc``).
+
+Parameters can be loaded from a local safetensors file whose keys follow the
+diffusers naming (``load_state_dict`` accepts them unchanged), so a real
+checkpoint drops in without network access.
+"""
+
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field
+
+import torch
+import torch.nn.functional as F
+from torch import Tensor, nn
+
+
+@dataclass(frozen=True)
+class UNet2DConfig:
+    sample_size: int = 256
+    in_channels: int = 3
+    out_channels: int = 3
+    block_out_channels: tuple[int, ...] = (128, 128, 256, 256, 512, 512)
+    # index of the levels carrying self-attention (AttnDownBlock2D / AttnUpBlock2D)
+    attention_levels: tuple[int, ...] = (4,)
+    layers_per_block: int = 2
+    norm_num_groups: int = 32
+    norm_eps: float = 1e-6
+    freq_shift: int = 1
+    flip_sin_to_cos: bool = False
+    attention_head_dim: int | None = None  # None -> one head spanning all channels
+
+
+CELEBAHQ_256 = UNet2DConfig()
+
+
+def timestep_embedding(t: Tensor, dim: int, *, flip_sin_to_cos: bool, freq_shift: float) -> Tensor:
+    """Sinusoidal embedding of integer timesteps (``Timesteps`` in diffusers)."""
+    half = dim // 2
+    exponent = -math.log(10000.0) * torch.arange(half, dtype=torch.float32, device=t.device)
+    exponent = exponent / (half - freq_shift)
+    emb = t.float()[:, None] * torch.exp(exponent)[None, :]
+    emb = torch.cat([torch.sin(emb), torch.cos(emb)], dim=-1)
+    if flip_sin_to_cos:
+        emb = torch.cat([emb[:, half:], emb[:, :half]], dim=-1)
+    return emb
+
+
+class TimestepEmbedding(nn.Module):
+    def __init__(self, in_dim: int, out_dim: int) -> None:
+        super().__init__()
+        self.linear_1 = nn.Linear(in_dim, out_dim)
+        self.linear_2 = nn.Linear(out_dim, out_dim)
+
+    def forward(self, x: Tensor) -> Tensor:
+        return self.linear_2(F.silu(self.linear_1(x)))
+
+
+class ResnetBlock2D(nn.Module):
+    def __init__(self, cin: int, cout: int, temb: int, groups: int, eps: float) -> None:
+        super().__init__()
+        self.norm1 = nn.GroupNorm(groups, cin, eps=eps)
+        self.conv1 = nn.Conv2d(cin, cout, 3, padding=1)
+        self.time_emb_proj = nn.Linear(temb, cout)
+        self.norm2 = nn.GroupNorm(groups, cout, eps=eps)
+        self.conv2 = nn.Conv2d(cout, cout, 3, padding=1)
+        self.conv_shortcut = nn.Conv2d(cin, cout, 1) if cin != cout else None
+
+    def forward(self, x: Tensor, temb: Tensor) -> Tensor:
+        h = self.conv1(F.silu(self.norm1(x)))
+        h = h + self.time_emb_proj(F.silu(temb))[:, :, None, None]
+        h = self.conv2(F.silu(self.norm2(h)))
+        if self.conv_shortcut is not None:
+            x = self.conv_shortcut(x)
+        return x + h
+
+
+class SpatialSelfAttention(nn.Module):
+    """GroupNorm -> single/multi-head attention over H*W tokens -> residual."""
+
+    def __init__(self, channels: int, groups: int, eps: float, head_dim: int | None) -> None:
+        super().__init__()
+        self.heads = 1 if head_dim is None else channels // head_dim
+        self.group_norm = nn.GroupNorm(groups, channels, eps=eps)
+        self.to_q = nn.Linear(channels, channels)
+        self.to_k = nn.Linear(channels, channels)
+        self.to_v = nn.Linear(channels, channels)
+        self.to_out = nn.ModuleList([nn.Linear(channels, channels)])
+
+    def forward(self, x: Tensor) -> Tensor:
+        b, c, h, w = x.shape
+        tokens = self.group_norm(x).reshape(b, c, h * w).transpose(1, 2)
+        q, k, v = self.to_q(tokens), self.to_k(tokens), self.to_v(tokens)
+        nh = self.heads
+        q, k, v = (t.reshape(b, h * w, nh, c // nh).transpose(1, 2) for t in (q, k, v))
+        o = F.scaled_dot_product_attention(q, k, v)
+        o = self.to_out[0](o.transpose(1, 2).reshape(b, h * w, c))
+        return x + o.transpose(1, 2).reshape(b, c, h, w)
+
+
+class Downsample2D(nn.Module):
+    """Stride-2 3x3 conv with diffusers' ``downsample_padding=0`` (pad right/bottom by 1)."""
+
+    def __init__(self, channels: int) -> None:
+        super().__init__()
+        self.conv = nn.Conv2d(channels, channels, 3, stride=2, padding=0)
+
+    def forward(self, x: Tensor) -> Tensor:
+        return self.conv(F.pad(x, (0, 1, 0, 1)))
+
+
+class Upsample2D(nn.Module):
+    def __init__(self, channels: int) -> None:
+        super().__init__()
+        self.conv = nn.Conv2d(channels, channels, 3, padding=1)
+
+    def forward(self, x: Tensor) -> Tensor:
+        return self.conv(F.interpolate(x, scale_factor=2.0, mode="nearest"))
+
+
+class _Level(nn.Module):
+    def __init__(self) -> None:
+        super().__init__()
+        self.resnets = nn.ModuleList()
+        self.attentions = nn.ModuleList()
+
+
+class UNet2DModel(nn.Module):
+    """Epsilon-prediction UNet; ``forward(sample, timestep) -> eps`` (same shape as sample)."""
+
+    def __init__(self, config: UNet2DConfig = CELEBAHQ_256) -> None:
+        super().__init__()
+        self.config = config
+        ch = config.block_out_channels
+        g, eps = config.norm_num_groups, config.norm_eps
+        temb = ch[0] * 4
+        self.time_embedding = TimestepEmbedding(ch[0], temb)
+        self.conv_in = nn.Conv2d(config.in_channels, ch[0], 3, padding=1)
+
+        self.down_blocks = nn.ModuleList()
+        cout = ch[0]
+        for i, c in enumerate(ch):
+            cin, cout = cout, c
+            lvl = _Level()
+            for j in range(config.layers_per_block):
+                lvl.resnets.append(ResnetBlock2D(cin if j == 0 else cout, cout, temb, g, eps))
+                if i in config.attention_levels:
+                    lvl.attentions.append(SpatialSelfAttention(cout, g, eps, config.attention_head_dim))
+            lvl.downsamplers = nn.ModuleList([Downsample2D(cout)]) if i < len(ch) - 1 else None
+            self.down_blocks.append(lvl)
+
+        mid = ch[-1]
+        self.mid_block = _Level()
+        self.mid_block.resnets.append(ResnetBlock2D(mid, mid, temb, g, eps))
+        self.mid_block.attentions.append(SpatialSelfAttention(mid, g, eps, config.attention_head_dim))
+        self.mid_block.resnets.append(ResnetBlock2D(mid, mid, temb, g, eps))
+
+        self.up_blocks = nn.ModuleList()
+        rev = list(reversed(ch))
+        nlev = len(ch)
+        prev = rev[0]
+        for i, c in enumerate(rev):
+            skip_in = rev[min(i + 1, nlev - 1)]
+            lvl = _Level()
+            for j in range(config.layers_per_block + 1):
+                res_skip = skip_in if j == config.layers_per_block else c
+                res_in = prev if j == 0 else c
+                lvl.resnets.append(ResnetBlock2D(res_in + res_skip, c, temb, g, eps))
+                if (nlev - 1 - i) in config.attention_levels:
+                    lvl.attentions.append(SpatialSelfAttention(c, g, eps, config.attention_head_dim))
+            lvl.upsamplers = nn.ModuleList([Upsample2D(c)]) if i < nlev - 1 else None
+            self.up_blocks.append(lvl)
+            prev = c
+
+        self.conv_norm_out = nn.GroupNorm(g, ch[0], eps=eps)
+        self.conv_out = nn.Conv2d(ch[0], config.out_channels, 3, padding=1)
+
+    def forward(self, sample: Tensor, timestep: Tensor | int) -> Tensor:
+        cfg = self.config
+        b = sample.shape[0]
+        if not torch.is_tensor(timestep):
+            timestep = torch.tensor([timestep], dtype=torch.long, device=sample.device)
+        timestep = timestep.reshape(-1).to(sample.device).expand(b)
+        t_emb = timestep_embedding(
+            timestep, cfg.block_out_channels[0],
+            flip_sin_to_cos=cfg.flip_sin_to_cos, freq_shift=cfg.freq_shift,
+        ).to(sample.dtype)
+        emb = self.time_embedding(t_emb)
+
+        h = self.conv_in(sample)
+        skips = [h]
+        for lvl in self.down_blocks:
+            for j, res in enumerate(lvl.resnets):
+                h = res(h, emb)
+                if len(lvl.attentions):
+                    h = lvl.attentions[j](h)
+                skips.append(h)
+            if lvl.downsamplers is not None:
+                h = lvl.downsamplers[0](h)
+                skips.append(h)
+
+        h = self.mid_block.resnets[0](h, emb)
+        h = self.mid_block.attentions[0](h)
+        h = self.mid_block.resnets[1](h, emb)
+
+        for lvl in self.up_blocks:
+            for j, res in enumerate(lvl.resnets):
+                h = res(torch.cat([h, skips.pop()], dim=1), emb)
+                if len(lvl.attentions):
+                    h = lvl.attentions[j](h)
+            if lvl.upsamplers is not None:
+                h = lvl.upsamplers[0](h)
+
+        return self.conv_out(F.silu(self.conv_norm_out(h)))
+
+
+def build_unet(config: UNet2DConfig = CELEBAHQ_256, *, seed: int = 0, device=None,
+               dtype: torch.dtype = torch.float32) -> UNet2DModel:
+    """Random-init prior with a fixed seed (weights are deterministic across boxes)."""
+    gen_state = torch.random.get_rng_state()
+    torch.manual_seed(seed)
+    try:
+        net = UNet2DModel(config)
+    finally:
+        torch.random.set_rng_state(gen_state)
+    return net.to(device=device, dtype=dtype).eval().requires_grad_(False)
+
+
+def count_parameters(module: nn.Module) -> int:
+    return sum(p.numel() for p in module.parameters())

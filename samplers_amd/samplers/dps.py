@@ -1,0 +1,283 @@
+"""Diffusion Posterior Sampling on the MI355X hot path.
+
+Same call contract as ``DPSSampler.__call__`` of the reference
+(``/root/reference/samplers/samplers/dps.py:25-134``); the loop body
+(``dps.py:91-122``) is rebuilt around two fused HIP passes with the prior's
+input-VJP between them::
+
+    eps = unet(x, t)                               PyTorch-ROCm (MIOpen / hipBLASLt)
+    v, |r|^2 partials = sp_dps_residual(x, eps, y) HIP pass 1: x0, A x0, residual, A^T grad
+    w = J_eps^T v                                  PyTorch-ROCm autograd (input-VJP only)
+    x <- sp_dps_update(x, eps, y|v, w, noise)      HIP pass 2: bridge mean + std*xi + guidance
+
+which is algebraically the reference's ``autograd.grad(log_likelihood(predict_x0(x)).sum(), x)``
+followed by ``ddim_step`` and ``x += gamma / (||r_b|| + 1e-9) * grad``
+(closed form: SURVEY.md §8a A9).  Timesteps and schedule scalars stay on the
+host, so a step issues no device->host synchronisation.
+
+Noise (``rng=``):
+  * ``"philox"`` (default): standard normals drawn inside pass 2 by Philox4x32-10
+    keyed by (seed, step, global sample index, element) — identical whatever the
+    batch sharding or micro-batching;
+  * ``"torch"``: the reference's draw order — ``torch.randn`` for x_T and one
+    ``torch.randn_like`` per step on the sample's device;
+  * ``noise_fn(kind, step, shape)``: injected tensors (parity tests replay the
+    reference's captured noise).
+"""
+
+from __future__ import annotations
+
+from typing import Callable, Generic, TypeVar
+
+import torch
+from torch import Tensor
+
+from samplers_amd import _hip
+from samplers_amd.dtypes import Shape
+from samplers_amd.inverse_problem import InverseProblem
+from samplers_amd.networks.base import EpsilonNetwork
+from samplers_amd.samplers.base import PosteriorSampler
+from samplers_amd.samplers.utils.batch_view import BatchView
+from samplers_amd.samplers.utils.bridge_kernels import bridge_coefficients, x0_coefficients
+
+Condition_co = TypeVar("Condition_co", covariant=True)
+
+NoiseFn = Callable[[str, int, tuple], Tensor]
+
+
+def draw_seed() -> int:
+    """A 63-bit seed from torch's default CPU generator (reproducible under manual_seed)."""
+    return int(torch.randint(0, 2**62, (1,), dtype=torch.int64).item())
+
+
+class KernelTimer:
+    """Collects HIP-event pairs around the fused passes (on the launch stream)."""
+
+    def __init__(self) -> None:
+        self.records: list[tuple[str, torch.cuda.Event, torch.cuda.Event, int]] = []
+
+    def span(self, name: str, batch: int):
+        timer = self
+
+        class _Span:
+            def __enter__(self):
+                self.e0 = torch.cuda.Event(enable_timing=True)
+                self.e1 = torch.cuda.Event(enable_timing=True)
+                self.e0.record()
+                return self
+
+            def __exit__(self, *exc):
+                self.e1.record()
+                timer.records.append((name, self.e0, self.e1, batch))
+                return False
+
+        return _Span()
+
+    def summary(self) -> dict[str, dict[str, float]]:
+        torch.cuda.synchronize()
+        out: dict[str, dict[str, float]] = {}
+        for name, e0, e1, b in self.records:
+            d = out.setdefault(name, {"count": 0, "ms": 0.0, "samples": 0})
+            d["count"] += 1
+            d["ms"] += e0.elapsed_time(e1)
+            d["samples"] += b
+        return out
+
+    def clear(self) -> None:
+        self.records.clear()
+
+
+class FusedDPSStep:
+    """One guided DPS iteration (``dps.py:91-122``) over a flat batch, on HIP.
+
+    ``observation_rows``: ``(num_rows, *y_shape)`` fp32 device tensor; sample b
+    uses row ``b // y_div`` (``y_div`` = reconstructions per observation).
+    """
+
+    def __init__(self, network: EpsilonNetwork, inverse_problem: InverseProblem,
+                 observation_rows: Tensor, y_div: int, *, gamma: float = 1.0, eta: float = 1.0,
+                 micro_batch: int | None = None, timer: KernelTimer | None = None) -> None:
+        op = inverse_problem.operator
+        desc = op.hip_descriptor()
+        if desc is None:
+            raise NotImplementedError(
+                f"{type(op).__name__} has no native (HIP) implementation; the fused DPS path "
+                "supports IdentityOperator, InpaintingOperator (and subclasses) and "
+                "GaussianBlurOperator"
+            )
+        _hip.require_cuda(observation_rows, "DPSSampler")
+        if observation_rows.dtype != torch.float32:
+            raise TypeError("the HIP path computes in fp32; cast the observation to float32")
+        self.lib = _hip.load_library()
+        self.network = network
+        self.operator = op
+        self.desc = desc
+        self.y = observation_rows.contiguous()
+        self.y_div = int(y_div)
+        self.m = int(desc.m)
+        self.n = int(desc.n)
+        self.partials = int(self.lib.sp_rsq_partials(desc))
+        if self.partials <= 0:
+            raise _hip.HipLibraryError(f"operator descriptor rejected ({self.partials})")
+        self.grad_scale = float(inverse_problem.noise.grad_scale())
+        self.gamma, self.eta = float(gamma), float(eta)
+        self.needs_v = desc.kind == _hip.SP_OP_BLUR
+        self.micro_batch = micro_batch
+        self.timer = timer
+
+    def coefficients(self, t: int, t_prev: int, s: int) -> _hip.SpDpsCoefs:
+        acp = self.network.alphas_cumprod_host
+        a, k = x0_coefficients(acp, t)
+        br = bridge_coefficients(acp, ell=t, t=t_prev, s=s, eta=self.eta)
+        return _hip.SpDpsCoefs(a, k, self.grad_scale, br.c_ell, br.c_s, br.std, self.gamma, 1e-9)
+
+    def _chunks(self, batch: int):
+        mb = self.micro_batch or batch
+        mb = max(self.y_div, (mb // self.y_div) * self.y_div)  # chunks never split an observation
+        for b0 in range(0, batch, mb):
+            yield b0, min(batch, b0 + mb)
+
+    def __call__(self, x: Tensor, step: int, t: int, t_prev: int, s: int, *,
+                 xi: Tensor | None = None, seed: int = 0, sample_offset: int = 0) -> Tensor:
+        """Advance ``x`` (flat ``(B, *x_shape)``, contiguous fp32) one step, in place."""
+        lib, desc = self.lib, self.desc
+        coefs = self.coefficients(t, t_prev, s)
+        stream = _hip.stream_of(x)
+        batch = x.shape[0]
+        for b0, b1 in self._chunks(batch):
+            xc = x[b0:b1]
+            bc = b1 - b0
+            yc = self.y[b0 // self.y_div:]
+            with torch.enable_grad():
+                xr = xc.detach().requires_grad_(True)
+                eps = self.network.forward(xr, t)
+            eps_c = eps.detach()
+            if not eps_c.is_contiguous():
+                eps_c = eps_c.contiguous()
+            v = torch.empty_like(xc)
+            part = torch.empty((bc, self.partials), device=x.device, dtype=torch.float32)
+            span = self.timer.span("dps_residual", bc) if self.timer else None
+            if span:
+                span.__enter__()
+            _hip.check(lib.sp_dps_residual(desc, _hip.ptr(xc), _hip.ptr(eps_c), _hip.ptr(yc), bc,
+                                           self.y_div, coefs, _hip.ptr(v), _hip.ptr(part), stream),
+                       "sp_dps_residual")
+            if span:
+                span.__exit__(None, None, None)
+            (w,) = torch.autograd.grad(eps, xr, grad_outputs=v.view_as(eps))
+            del eps, xr
+            w = w.contiguous()
+            xic = None if xi is None else xi[b0:b1].contiguous()
+            span = self.timer.span("dps_update", bc) if self.timer else None
+            if span:
+                span.__enter__()
+            _hip.check(lib.sp_dps_update(desc, _hip.ptr(xc), _hip.ptr(eps_c), _hip.ptr(yc),
+                                         _hip.ptr(v) if self.needs_v else None, _hip.ptr(w),
+                                         _hip.ptr(part), _hip.ptr(xic), seed, step,
+                                         sample_offset + b0, bc, self.y_div, coefs, _hip.ptr(xc),
+                                         stream),
+                       "sp_dps_update")
+            if span:
+                span.__exit__(None, None, None)
+        return x
+
+    def predict_x0(self, x: Tensor, t: int) -> Tensor:
+        """Final ``predict_x0`` (``dps.py:125-126``): prior forward + HIP epilogue."""
+        a, k = x0_coefficients(self.network.alphas_cumprod_host, t)
+        out = torch.empty_like(x)
+        for b0, b1 in self._chunks(x.shape[0]):
+            with torch.no_grad():
+                eps = self.network.forward(x[b0:b1], t).contiguous()
+            _hip.check(self.lib.sp_predict_x0(_hip.ptr(x[b0:b1]), _hip.ptr(eps), eps.numel(), a, k,
+                                              _hip.ptr(out[b0:b1]), _hip.stream_of(x)),
+                       "sp_predict_x0")
+        return out
+
+
+def initial_sample(shape: tuple, device: torch.device, *, rng: str, seed: int, sample_offset: int,
+                   noise_fn: NoiseFn | None) -> Tensor:
+    """x_T ~ N(0, I) (``dps.py:83-87``)."""
+    if noise_fn is not None:
+        return noise_fn("init", -1, shape).to(device=device, dtype=torch.float32).contiguous()
+    if rng == "torch":
+        return torch.randn(size=shape, device=device, dtype=torch.float32)
+    if rng != "philox":
+        raise ValueError(f"rng must be 'philox' or 'torch', got {rng!r}")
+    lib = _hip.load_library()
+    x = torch.empty(shape, device=device, dtype=torch.float32)
+    n = x[0].numel() if shape[0] else 0
+    if shape[0]:
+        _hip.check(lib.sp_randn(_hip.ptr(x), shape[0], n, seed, -1, sample_offset,
+                                _hip.stream_of(x)), "sp_randn")
+    return x
+
+
+class DPSSampler(PosteriorSampler, Generic[Condition_co]):
+    """DPS (Chung et al., 2022) with the guided step fused into two HIP passes."""
+
+    def __call__(
+        self,
+        inverse_problem: InverseProblem,
+        num_sampling_steps: int = 50,
+        num_reconstructions: int = 1,
+        gamma: float = 1.0,
+        eta: float = 1.0,
+        condition: Condition_co | None = None,
+        keep_reconstruction_dim: bool = False,
+        *args,
+        rng: str = "philox",
+        seed: int | None = None,
+        noise_fn: NoiseFn | None = None,
+        sample_offset: int = 0,
+        micro_batch: int | None = None,
+        timer: KernelTimer | None = None,
+        **kwargs,
+    ) -> Tensor:
+        """Run DPS; returns ``(*batch_shape, R, *x_shape)`` (R squeezed when 1).
+
+        Extra keyword-only options (all default to the reference behaviour):
+        ``rng`` / ``seed`` / ``noise_fn`` choose the noise source (module
+        docstring); ``sample_offset`` is the global index of this shard's first
+        flat sample (multi-GPU, keeps Philox streams shard-invariant);
+        ``micro_batch`` bounds how many samples share one prior forward+VJP.
+        """
+        if args or kwargs:
+            print(f"Warning: Unused args={args}, kwargs={kwargs} in DPSSampler")
+
+        x_shape: Shape = inverse_problem.operator.x_shape
+        batch_shape: Shape = inverse_problem.batch_shape
+        view = BatchView(batch_shape=batch_shape, num_samples=num_reconstructions, data_shape=x_shape)
+
+        net = self._epsilon_network
+        net.set_sampling_parameters(num_sampling_steps=num_sampling_steps,
+                                    num_reconstructions=num_reconstructions,
+                                    batch_size=view.batch_size)
+        net.set_condition(condition=condition)
+        try:
+            obs = inverse_problem.observation
+            _hip.require_cuda(obs, "DPSSampler")
+            y_rows = obs.reshape(max(view.batch_size, 1), *inverse_problem.operator.y_shape)
+            step = FusedDPSStep(net, inverse_problem, y_rows.to(torch.float32), num_reconstructions,
+                                gamma=gamma, eta=eta, micro_batch=micro_batch, timer=timer)
+            if seed is None and noise_fn is None and rng == "philox":
+                seed = draw_seed()
+            seed = int(seed or 0)
+
+            x = initial_sample(view.flat_shape, net.device, rng=rng, seed=seed,
+                               sample_offset=sample_offset, noise_fn=noise_fn)
+            ts = net.timesteps_host
+            for i in range(len(ts) - 1, 1, -1):
+                xi = None
+                if noise_fn is not None:
+                    xi = noise_fn("step", i, tuple(x.shape)).to(device=x.device, dtype=torch.float32)
+                elif rng == "torch":
+                    xi = torch.randn_like(x)
+                step(x, i, ts[i], ts[i - 1], ts[0], xi=xi, seed=seed, sample_offset=sample_offset)
+
+            x0_final = view.unflatten(step.predict_x0(x, ts[1]))
+            if num_reconstructions == 1 and not keep_reconstruction_dim:
+                x0_final = x0_final.squeeze(len(batch_shape))
+            return x0_final
+        finally:
+            net.clear_condition()
+            net.clear_sampling_parameters()

@@ -1,0 +1,126 @@
+"""Deterministic stand-in ε-networks shared by the golden-vector generator
+(which drives the REFERENCE samplers in the survey container) and the tests
+(which drive this package on the GPU).
+
+The real priors (diffusers checkpoints) are unavailable offline, so parity of
+the hot path is pinned with priors whose Jacobian is either known in closed
+form (``linear``: eps = c * x) or small enough to differentiate exactly on any
+device (``conv``: a fixed-seed two-layer conv net).  The schedule is the DDPM
+linear-beta schedule with diffusers' ``leading`` spacing, restated in
+``samplers_amd.networks.ddpm.DDPMSchedule``.
+"""
+
+from __future__ import annotations
+
+import math
+
+import numpy as np
+import torch
+from torch import nn
+
+
+def ddpm_alphas_cumprod(num_train_timesteps: int = 1000) -> torch.Tensor:
+    betas = torch.linspace(1e-4, 0.02, num_train_timesteps, dtype=torch.float32)
+    return torch.cumprod(1.0 - betas, dim=0)
+
+
+def leading_timesteps_ascending(n: int, num_train_timesteps: int = 1000) -> torch.Tensor:
+    ratio = num_train_timesteps // n
+    ts = (np.arange(0, n) * ratio).round().astype(np.int64)
+    return torch.from_numpy(ts)
+
+
+class EpsCore(nn.Module):
+    """eps(x, t) for the stand-in priors."""
+
+    def __init__(self, kind: str, channels: int, coef: float = 0.1, seed: int = 1234) -> None:
+        super().__init__()
+        self.kind = kind
+        self.coef = coef
+        if kind == "conv":
+            gen = torch.Generator().manual_seed(seed)
+            hidden = 8
+            self.w1 = nn.Parameter(torch.randn(hidden, channels, 3, 3, generator=gen) * 0.15,
+                                   requires_grad=False)
+            self.b1 = nn.Parameter(torch.randn(hidden, generator=gen) * 0.05, requires_grad=False)
+            self.w2 = nn.Parameter(torch.randn(channels, hidden, 3, 3, generator=gen) * 0.15,
+                                   requires_grad=False)
+        elif kind != "linear":
+            raise ValueError(kind)
+
+    def forward(self, x: torch.Tensor, t) -> torch.Tensor:
+        if self.kind == "linear":
+            return self.coef * x
+        tt = float(t) / 1000.0
+        h = torch.tanh(nn.functional.conv2d(x, self.w1, self.b1, padding=1))
+        return nn.functional.conv2d(h, self.w2, padding=1) * (1.0 + tt) + self.coef * x
+
+
+def make_samplers_amd_net(kind: str, channels: int, coef: float = 0.1, device=None):
+    """Stand-in prior implementing :class:`samplers_amd.networks.base.EpsilonNetwork`."""
+    from samplers_amd.networks.base import EpsilonNetwork, NoCondition
+
+    class StandInNetwork(EpsilonNetwork[NoCondition]):
+        def __init__(self) -> None:
+            acp = ddpm_alphas_cumprod()
+            super().__init__(alphas_cumprod=torch.cat([acp.new_tensor([1.0]), acp]))
+            self.core = EpsCore(kind, channels, coef)
+
+        def forward(self, x, t):
+            if self._num_sampling_steps is None:
+                raise RuntimeError("Call `set_sampling_parameters()` before sampling.")
+            return self.core(x, t)
+
+        @classmethod
+        def from_pretrained(cls, *a, **k):
+            raise NotImplementedError
+
+        def set_sampling_parameters(self, num_sampling_steps, batch_size=1, num_reconstructions=1):
+            self._batch_size = batch_size
+            self._num_sampling_steps = num_sampling_steps
+            self._num_reconstructions = num_reconstructions
+            self._set_timesteps_buffer(leading_timesteps_ascending(num_sampling_steps))
+
+        @property
+        def is_condition_initialized(self) -> bool:
+            return True
+
+    net = StandInNetwork()
+    return net.to(device) if device is not None else net
+
+
+def fixture_x_true(batch: int, shape: tuple, seed: int = 0) -> torch.Tensor:
+    gen = torch.Generator().manual_seed(seed)
+    return torch.rand((batch, *shape), generator=gen) * 2 - 1
+
+
+def fixture_mask(shape: tuple, kind: str, seed: int = 1) -> torch.Tensor:
+    c, h, w = shape
+    if kind == "random":
+        gen = torch.Generator().manual_seed(seed)
+        return (torch.rand(h, w, generator=gen) < 0.5).expand(c, h, w).contiguous()
+    if kind == "center":
+        m = torch.zeros(shape, dtype=torch.bool)
+        m[..., int(h * 0.25):int(h * 0.75), int(w * 0.25):int(w * 0.75)] = True
+        return m
+    raise ValueError(kind)
+
+
+def replay_noise(seed: int, flat_shape: tuple, num_steps: int):
+    """The reference DPS RNG stream: randn(flat_shape), then one randn_like per step."""
+    gen = torch.Generator().manual_seed(seed)
+    init = torch.randn(flat_shape, generator=gen)
+    steps = {}
+    for i in range(num_steps - 1, 1, -1):
+        steps[i] = torch.randn(flat_shape, generator=gen)
+    return init, steps
+
+
+def relative_error(a: torch.Tensor, b: torch.Tensor) -> float:
+    a = a.double().reshape(-1)
+    b = b.double().reshape(-1)
+    return float((a - b).norm() / max(b.norm().item(), 1e-30))
+
+
+def count(shape) -> int:
+    return int(math.prod(shape))
