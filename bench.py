@@ -36,9 +36,8 @@ import time
 from pathlib import Path
 
 ROOT = Path(__file__).resolve().parent
-os.environ.setdefault("MIOPEN_USER_DB_PATH", str(ROOT / ".miopen_cache"))
-os.environ.setdefault("MIOPEN_CUSTOM_CACHE_DIR", str(ROOT / ".miopen_cache"))
 sys.path.insert(0, str(ROOT))
+import samplers_amd  # noqa: E402,F401  (configures the MIOpen find-db / kernel cache)
 
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
@@ -56,6 +55,8 @@ def parse():
     p.add_argument("--batch", type=int, default=64, help="samples per GPU")
     p.add_argument("--image", type=int, default=256)
     p.add_argument("--micro-batch", type=int, default=0)
+    p.add_argument("--recompute-v", action="store_true",
+                   help="pass 2 re-derives v from y (gather) instead of re-reading pass 1's v")
     p.add_argument("--cpu-seconds", type=float, default=15.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
     return p.parse_args()
@@ -102,6 +103,7 @@ def guidance_bytes(n: int, m: int, words: int) -> dict[str, float]:
     return {
         "dps_residual": 4.0 * (3 * n + m),  # read x, eps, y; write v
         "dps_update": 4.0 * (4 * n + m),    # read x, eps, w, y; write x'
+        "dps_update_reuse_v": 4.0 * 5 * n,  # read x, eps, w, v; write x'
         "index_per_launch": 12.0 * words,   # keep bits + word ranks, once per launch
     }
 
@@ -162,7 +164,7 @@ def main():
     m = problem.operator.shape[0]
     timer = KernelTimer()
     step = FusedDPSStep(net, problem, problem.observation, 1, gamma=1.0, eta=1.0,
-                        micro_batch=args.micro_batch or None, timer=timer)
+                        micro_batch=args.micro_batch or None, timer=timer, reuse_v=not args.recompute_v)
     from samplers_amd.samplers.dps import initial_sample
 
     seed = 20260101
@@ -204,14 +206,16 @@ def main():
     for name in ("dps_residual", "dps_update"):
         d = kern[name]
         avg_ms = d["ms"] / d["count"]
-        per_launch = nbytes[name] * d["samples"] / d["count"] + nbytes["index_per_launch"]
+        key = "dps_update_reuse_v" if (name == "dps_update" and step.needs_v) else name
+        per_launch = nbytes[key] * d["samples"] / d["count"] + nbytes["index_per_launch"]
         rl[name] = {"avg_ms": avg_ms, "bytes": per_launch, "gbs": per_launch / avg_ms / 1e6}
     dominant = max(rl, key=lambda k: rl[k]["avg_ms"])
     traffic = None
     pmc = ROOT / "profiles" / "pmc_traffic.json"
     if pmc.exists():
         try:
-            traffic = json.loads(pmc.read_text()).get(f"{dominant}@B{args.batch}_{args.image}")
+            rec = json.loads(pmc.read_text()).get(f"{dominant}@B{args.batch}_{args.image}")
+            traffic = rec["hbm_bytes_per_launch"] if rec else None
         except (ValueError, OSError):
             traffic = None
 

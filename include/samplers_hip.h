@@ -75,6 +75,15 @@ typedef struct sp_dps_coefs {
     float norm_eps;   /* 1e-9                    dps.py:121                      */
 } sp_dps_coefs;
 
+/* Kernel timing (instrumentation, off by default).  While enabled, every
+ * sp_dps_residual / sp_dps_update launch gets a start/stop hipEvent pair attached
+ * to its dispatch packet (hipExtLaunchKernel), i.e. the kernel's own execution
+ * interval.  sp_timing_collect waits for the recorded launches, writes up to
+ * max_records (kind, milliseconds) pairs — kind 1 = residual pass, 2 = update
+ * pass — clears the log and returns the number written. */
+int sp_timing_enable(int on);
+int sp_timing_collect(int32_t* kinds, float* ms, int max_records);
+
 /* Library / ABI version (major*10000 + minor*100 + patch). */
 int sp_version(void);
 /* Text of the last launch error on this thread ("" if none). */

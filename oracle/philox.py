@@ -3,7 +3,7 @@
 Restates ``samplers_amd/csrc/sp_common.h`` (philox4x32_10, u01, philox_normal4)
 so the in-kernel noise stream can be checked: the 32-bit Philox words
 bit-exactly (plus the Random123 known-answer vectors), the normals to a few
-ulp (device logf / sincosf vs fp64 here).
+ulp (device v_log_f32 / v_sin_f32 / v_cos_f32 vs fp64 here).
 """
 
 from __future__ import annotations
@@ -49,8 +49,9 @@ def normals(seed: int, step: int, sample: int, n: int) -> np.ndarray:
     u = u01(r).astype(np.float64)
     rad0 = np.sqrt(-2.0 * np.log(u[:, 0]))
     rad1 = np.sqrt(-2.0 * np.log(u[:, 2]))
-    th0 = np.float64(np.float32(6.283185307179586) * u01(r[:, 1]))
-    th1 = np.float64(np.float32(6.283185307179586) * u01(r[:, 3]))
+    # the device takes sin/cos of 2*pi*u exactly in revolutions (v_sin_f32 / v_cos_f32)
+    th0 = 2.0 * np.pi * u01(r[:, 1]).astype(np.float64)
+    th1 = 2.0 * np.pi * u01(r[:, 3]).astype(np.float64)
     z = np.stack([rad0 * np.cos(th0), rad0 * np.sin(th0), rad1 * np.cos(th1), rad1 * np.sin(th1)],
                  axis=1).reshape(-1)
     return z[:n].astype(np.float32)

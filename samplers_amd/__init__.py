@@ -7,3 +7,7 @@ reference; the per-step arithmetic runs in hand-written HIP kernels
 """
 
 __version__ = "0.1.0"
+
+from samplers_amd.runtime import configure_miopen as _configure_miopen
+
+_configure_miopen()

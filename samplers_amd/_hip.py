@@ -63,6 +63,9 @@ _COP = ctypes.POINTER(SpDpsCoefs)
 # name -> (restype, argtypes); mirrors include/samplers_hip.h one-to-one
 SIGNATURES = {
     "sp_version": (ctypes.c_int, []),
+    "sp_timing_enable": (ctypes.c_int, [ctypes.c_int]),
+    "sp_timing_collect": (ctypes.c_int, [ctypes.POINTER(ctypes.c_int32),
+                                         ctypes.POINTER(ctypes.c_float), ctypes.c_int]),
     "sp_last_error": (ctypes.c_char_p, []),
     "sp_rsq_partials": (_I64, [_OPP]),
     "sp_vec_partials": (_I64, [_I64]),

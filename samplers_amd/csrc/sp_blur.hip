@@ -231,8 +231,8 @@ static int launch_blur(const sp_op* op, const float* in, const float* eps, const
     switch (op->radius) {
 #define SP_BLUR_CASE(RR)                                                                       \
     case RR:                                                                                   \
-        hipLaunchKernelGGL((k_blur<RR, MODE>), grid, dim3(kBlock), 0, s, *op, in, eps, y, y_div, \
-                           a, k, gs, out, partial, P);                                         \
+        launch(MODE == MODE_DPS ? TK_DPS_RESIDUAL : 0, k_blur<RR, MODE>, grid, dim3(kBlock), s, \
+               *op, in, eps, y, y_div, a, k, gs, out, partial, P);                               \
         break;
         SP_BLUR_CASE(1) SP_BLUR_CASE(2) SP_BLUR_CASE(3) SP_BLUR_CASE(4)
         SP_BLUR_CASE(5) SP_BLUR_CASE(6) SP_BLUR_CASE(7) SP_BLUR_CASE(8)

@@ -2,6 +2,7 @@
 // block reductions, vector load/store, launch-error bookkeeping.
 #pragma once
 
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -9,8 +10,15 @@
 
 namespace sp {
 
-constexpr int kBlock = 256;  // 4 waves of 64 lanes
-constexpr int kIter = 4;     // float4 groups per thread per block (elementwise kernels)
+#ifndef SP_KITER
+#define SP_KITER 4
+#endif
+#ifndef SP_NT_STORE
+#define SP_NT_STORE 0
+#endif
+
+constexpr int kBlock = 256;       // 4 waves of 64 lanes
+constexpr int kIter = SP_KITER;   // float4 groups per thread per block (elementwise kernels)
 
 // ---------------------------------------------------------------------------
 // Philox4x32-10 (Salmon et al., SC'11).  Counter = (element group, sample, step lo,
@@ -39,21 +47,22 @@ __device__ __forceinline__ float u01(uint32_t u) {
 }
 
 // Four standard normals for element group `grp` (elements 4*grp .. 4*grp+3).
+// Box-Muller on the hardware transcendentals: v_log_f32 is log2, v_sin_f32 /
+// v_cos_f32 take revolutions, so sin(2*pi*u) = __builtin_amdgcn_sinf(u).
 __device__ __forceinline__ void philox_normal4(uint64_t seed, int64_t step, int64_t sample,
                                                int64_t grp, float out[4]) {
     const u32x4 c{static_cast<uint32_t>(grp), static_cast<uint32_t>(sample),
                   static_cast<uint32_t>(static_cast<uint64_t>(step)),
                   static_cast<uint32_t>(static_cast<uint64_t>(step) >> 32)};
     const u32x4 r = philox4x32_10(c, static_cast<uint32_t>(seed), static_cast<uint32_t>(seed >> 32));
-    const float rad0 = sqrtf(-2.0f * logf(u01(r.x)));
-    const float rad1 = sqrtf(-2.0f * logf(u01(r.z)));
-    float s0, c0, s1, c1;
-    sincosf(6.283185307179586f * u01(r.y), &s0, &c0);
-    sincosf(6.283185307179586f * u01(r.w), &s1, &c1);
-    out[0] = rad0 * c0;
-    out[1] = rad0 * s0;
-    out[2] = rad1 * c1;
-    out[3] = rad1 * s1;
+    constexpr float kM2Ln2 = -1.3862943611198906f;  // -2 ln 2
+    const float rad0 = __builtin_sqrtf(kM2Ln2 * __builtin_amdgcn_logf(u01(r.x)));
+    const float rad1 = __builtin_sqrtf(kM2Ln2 * __builtin_amdgcn_logf(u01(r.z)));
+    const float t0 = u01(r.y), t1 = u01(r.w);
+    out[0] = rad0 * __builtin_amdgcn_cosf(t0);
+    out[1] = rad0 * __builtin_amdgcn_sinf(t0);
+    out[2] = rad1 * __builtin_amdgcn_cosf(t1);
+    out[3] = rad1 * __builtin_amdgcn_sinf(t1);
 }
 
 // ---------------------------------------------------------------------------
@@ -98,10 +107,16 @@ __device__ __forceinline__ void load_v(const float* __restrict__ p, float (&r)[V
     }
 }
 
-template <int V>
+// NT = non-temporal (streamed-once outputs: the updated sample of the DPS step).
+template <int V, bool NT = false>
 __device__ __forceinline__ void store_v(float* __restrict__ p, const float (&r)[V]) {
     if constexpr (V == 4) {
-        *reinterpret_cast<float4*>(p) = make_float4(r[0], r[1], r[2], r[3]);
+        typedef float f4v __attribute__((ext_vector_type(4)));
+        const f4v t = {r[0], r[1], r[2], r[3]};
+        if constexpr (NT || SP_NT_STORE)
+            __builtin_nontemporal_store(t, reinterpret_cast<f4v*>(p));
+        else
+            *reinterpret_cast<f4v*>(p) = t;
     } else {
 #pragma unroll
         for (int e = 0; e < V; ++e) p[e] = r[e];
@@ -146,5 +161,20 @@ __device__ __forceinline__ uint32_t mask_bits(const sp_op& op, int64_t j) {
 // ---------------------------------------------------------------------------
 void set_error(const char* what, hipError_t e);
 int check_launch(const char* what);
+
+// Kernel timing (sp_timing_enable): the start/stop events of a timed launch are
+// attached to its dispatch packet (hipExtLaunchKernel), so they bracket the
+// kernel alone — the same interval rocprofv3's kernel trace reports.
+bool timing_on();
+void timing_events(int kind, hipEvent_t* start, hipEvent_t* stop);
+
+enum { TK_DPS_RESIDUAL = 1, TK_DPS_UPDATE = 2 };
+
+template <typename K, typename... Args>
+inline void launch(int kind, K kernel, dim3 grid, dim3 block, hipStream_t s, Args... args) {
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    if (kind && timing_on()) timing_events(kind, &e0, &e1);
+    hipExtLaunchKernelGGL(kernel, grid, block, 0, s, e0, e1, 0, args...);
+}
 
 }  // namespace sp

@@ -12,6 +12,8 @@
 
 #include <cstdio>
 #include <cstring>
+#include <mutex>
+#include <vector>
 
 #include "sp_common.h"
 
@@ -32,6 +34,35 @@ int check_launch(const char* what) {
     return SP_OK;
 }
 
+struct TimingRecord {
+    int kind;
+    hipEvent_t start, stop;
+};
+static std::mutex g_timing_mu;
+static bool g_timing = false;
+static std::vector<TimingRecord> g_records;
+static std::vector<hipEvent_t> g_event_pool;
+
+bool timing_on() { return g_timing; }
+
+static hipEvent_t take_event() {
+    if (!g_event_pool.empty()) {
+        hipEvent_t e = g_event_pool.back();
+        g_event_pool.pop_back();
+        return e;
+    }
+    hipEvent_t e = nullptr;
+    if (hipEventCreate(&e) != hipSuccess) return nullptr;
+    return e;
+}
+
+void timing_events(int kind, hipEvent_t* start, hipEvent_t* stop) {
+    std::lock_guard<std::mutex> lock(g_timing_mu);
+    *start = take_event();
+    *stop = take_event();
+    if (*start && *stop) g_records.push_back({kind, *start, *stop});
+}
+
 // ---------------------------------------------------------------------------
 // K1: x0 -> residual -> v = A^T(grad_scale * r), per-block sum r^2
 // ---------------------------------------------------------------------------
@@ -49,51 +80,53 @@ __global__ __launch_bounds__(kBlock) void k_dps_residual(sp_op op, const float* 
     const float* eb = eps + b * n;
     const float* yb = y + (b / y_div) * op.m;
     float* vb = v + b * n;
+    const int64_t j0 = (int64_t)blockIdx.x * kIter * (kBlock * V) + threadIdx.x * V;
+    // issue every load of the tile first (memory-level parallelism), then compute
+    float xv[kIter][V], ev[kIter][V], yv[kIter][V];
+    uint32_t bits[kIter];
+    int64_t rank[kIter];
+#pragma unroll
+    for (int it = 0; it < kIter; ++it) {
+        const int64_t j = j0 + it * (kBlock * V);
+        if (j < n) {
+            load_v<V>(xb + j, xv[it]);
+            load_v<V>(eb + j, ev[it]);
+            if constexpr (OPK == SP_OP_INPAINT) {
+                inpaint_lookup(op, j, bits[it], rank[it]);
+            } else {
+                load_v<V>(yb + j, yv[it]);
+                if constexpr (OPK == SP_OP_MASK) bits[it] = mask_bits(op, j);
+            }
+        }
+    }
+    if constexpr (OPK == SP_OP_INPAINT) {
+#pragma unroll
+        for (int it = 0; it < kIter; ++it) {
+            const int64_t j = j0 + it * (kBlock * V);
+            if (j < n) {
+                int64_t r = rank[it];
+#pragma unroll
+                for (int e = 0; e < V; ++e) {
+                    yv[it][e] = 0.f;
+                    if ((bits[it] >> e) & 1u) yv[it][e] = yb[r++];
+                }
+            }
+        }
+    }
     float acc = 0.f;
 #pragma unroll
     for (int it = 0; it < kIter; ++it) {
-        const int64_t j = ((int64_t)blockIdx.x * kIter + it) * (kBlock * V) + threadIdx.x * V;
+        const int64_t j = j0 + it * (kBlock * V);
         if (j < n) {
-            float xv[V], ev[V], vv[V];
-            load_v<V>(xb + j, xv);
-            load_v<V>(eb + j, ev);
-            if constexpr (OPK == SP_OP_IDENTITY) {
-                float yv[V];
-                load_v<V>(yb + j, yv);
+            float vv[V];
 #pragma unroll
-                for (int e = 0; e < V; ++e) {
-                    const float x0 = (xv[e] - k * ev[e]) / a;
-                    const float r = yv[e] - x0;
-                    vv[e] = gs * r;
-                    acc += r * r;
-                }
-            } else if constexpr (OPK == SP_OP_MASK) {
-                float yv[V];
-                load_v<V>(yb + j, yv);
-                const uint32_t bits = mask_bits(op, j);
-#pragma unroll
-                for (int e = 0; e < V; ++e) {
-                    const bool kept = (bits >> e) & 1u;
-                    const float x0 = kept ? (xv[e] - k * ev[e]) / a : 0.f;
-                    const float r = yv[e] - x0;
-                    vv[e] = kept ? gs * r : 0.f;
-                    acc += r * r;
-                }
-            } else {
-                uint32_t bits;
-                int64_t rank;
-                inpaint_lookup(op, j, bits, rank);
-#pragma unroll
-                for (int e = 0; e < V; ++e) {
-                    vv[e] = 0.f;
-                    if ((bits >> e) & 1u) {
-                        const float x0 = (xv[e] - k * ev[e]) / a;
-                        const float r = yb[rank] - x0;
-                        vv[e] = gs * r;
-                        acc += r * r;
-                        ++rank;
-                    }
-                }
+            for (int e = 0; e < V; ++e) {
+                const bool kept = OPK == SP_OP_IDENTITY || ((bits[it] >> e) & 1u);
+                const float x0 = (xv[it][e] - k * ev[it][e]) / a;
+                // MASK: unobserved pixels still add y^2 to the residual (A x0 = 0 there)
+                const float r = yv[it][e] - (kept ? x0 : 0.f);
+                vv[e] = kept ? gs * r : 0.f;
+                if (OPK != SP_OP_INPAINT || kept) acc += r * r;
             }
             store_v<V>(vb + j, vv);
         }
@@ -113,50 +146,53 @@ __global__ __launch_bounds__(kBlock) void k_dps_update(
     int64_t step, int64_t sample_offset, int64_t y_div, sp_dps_coefs c, float* __restrict__ xo) {
     const int64_t b = blockIdx.y;
     const int64_t n = op.n;
-    const float rsq = sum_partials(partial + b * P, P);
-    const float scale = c.gamma / (sqrtf(rsq) + c.norm_eps);
     const float* xb = x + b * n;
     const float* eb = eps + b * n;
     const float* wb = w + b * n;
     const float* yb = y + (b / y_div) * op.m;
     float* ob = xo + b * n;
+    const int64_t j0 = (int64_t)blockIdx.x * kIter * (kBlock * V) + threadIdx.x * V;
+    float xv[kIter][V], ev[kIter][V], wv[kIter][V], yv[kIter][V];
+    uint32_t bits[kIter];
+    int64_t rank[kIter];
 #pragma unroll
     for (int it = 0; it < kIter; ++it) {
-        const int64_t j = ((int64_t)blockIdx.x * kIter + it) * (kBlock * V) + threadIdx.x * V;
+        const int64_t j = j0 + it * (kBlock * V);
         if (j < n) {
-            float xv[V], ev[V], wv[V], vv[V], z[V], x0[V];
-            load_v<V>(xb + j, xv);
-            load_v<V>(eb + j, ev);
-            load_v<V>(wb + j, wv);
-#pragma unroll
-            for (int e = 0; e < V; ++e) x0[e] = (xv[e] - c.k * ev[e]) / c.a;
+            load_v<V>(xb + j, xv[it]);
+            load_v<V>(eb + j, ev[it]);
+            load_v<V>(wb + j, wv[it]);
             if constexpr (V_IN) {
-                load_v<V>(v + b * n + j, vv);
-            } else if constexpr (OPK == SP_OP_IDENTITY) {
-                float yv[V];
-                load_v<V>(yb + j, yv);
-#pragma unroll
-                for (int e = 0; e < V; ++e) vv[e] = c.grad_scale * (yv[e] - x0[e]);
-            } else if constexpr (OPK == SP_OP_MASK) {
-                float yv[V];
-                load_v<V>(yb + j, yv);
-                const uint32_t bits = mask_bits(op, j);
-#pragma unroll
-                for (int e = 0; e < V; ++e)
-                    vv[e] = ((bits >> e) & 1u) ? c.grad_scale * (yv[e] - x0[e]) : 0.f;
+                load_v<V>(v + b * n + j, yv[it]);  // yv holds v in this variant
+            } else if constexpr (OPK == SP_OP_INPAINT) {
+                inpaint_lookup(op, j, bits[it], rank[it]);
             } else {
-                uint32_t bits;
-                int64_t rank;
-                inpaint_lookup(op, j, bits, rank);
+                load_v<V>(yb + j, yv[it]);
+                if constexpr (OPK == SP_OP_MASK) bits[it] = mask_bits(op, j);
+            }
+        }
+    }
+    if constexpr (!V_IN && OPK == SP_OP_INPAINT) {
+#pragma unroll
+        for (int it = 0; it < kIter; ++it) {
+            const int64_t j = j0 + it * (kBlock * V);
+            if (j < n) {
+                int64_t r = rank[it];
 #pragma unroll
                 for (int e = 0; e < V; ++e) {
-                    vv[e] = 0.f;
-                    if ((bits >> e) & 1u) {
-                        vv[e] = c.grad_scale * (yb[rank] - x0[e]);
-                        ++rank;
-                    }
+                    yv[it][e] = 0.f;
+                    if ((bits[it] >> e) & 1u) yv[it][e] = yb[r++];
                 }
             }
+        }
+    }
+    const float rsq = sum_partials(partial + b * P, P);
+    const float scale = c.gamma / (sqrtf(rsq) + c.norm_eps);
+#pragma unroll
+    for (int it = 0; it < kIter; ++it) {
+        const int64_t j = j0 + it * (kBlock * V);
+        if (j < n) {
+            float z[V];
             if constexpr (XI_IN) {
                 load_v<V>(xi + b * n + j, z);
             } else {
@@ -165,11 +201,19 @@ __global__ __launch_bounds__(kBlock) void k_dps_update(
             float out[V];
 #pragma unroll
             for (int e = 0; e < V; ++e) {
-                const float mean = c.c_ell * xv[e] + c.c_s * x0[e];
-                const float g = (vv[e] - c.k * wv[e]) / c.a;
+                const float x0 = (xv[it][e] - c.k * ev[it][e]) / c.a;
+                float vv;
+                if constexpr (V_IN) {
+                    vv = yv[it][e];
+                } else {
+                    const bool kept = OPK == SP_OP_IDENTITY || ((bits[it] >> e) & 1u);
+                    vv = kept ? c.grad_scale * (yv[it][e] - x0) : 0.f;
+                }
+                const float mean = c.c_ell * xv[it][e] + c.c_s * x0;
+                const float g = (vv - c.k * wv[it][e]) / c.a;
                 out[e] = (mean + c.std * z[e]) + scale * g;
             }
-            store_v<V>(ob + j, out);
+            store_v<V, true>(ob + j, out);
         }
     }
 }
@@ -332,7 +376,31 @@ using namespace sp;
 
 extern "C" {
 
-int sp_version(void) { return 100; }
+int sp_version(void) { return 101; }
+
+int sp_timing_enable(int on) {
+    std::lock_guard<std::mutex> lock(g_timing_mu);
+    g_timing = on != 0;
+    return SP_OK;
+}
+
+int sp_timing_collect(int32_t* kinds, float* ms, int max_records) {
+    std::lock_guard<std::mutex> lock(g_timing_mu);
+    int n = 0;
+    for (const TimingRecord& r : g_records) {
+        float t = -1.f;
+        if (hipEventSynchronize(r.stop) == hipSuccess && hipEventElapsedTime(&t, r.start, r.stop) == hipSuccess &&
+            n < max_records && kinds && ms) {
+            kinds[n] = r.kind;
+            ms[n] = t;
+            ++n;
+        }
+        g_event_pool.push_back(r.start);
+        g_event_pool.push_back(r.stop);
+    }
+    g_records.clear();
+    return n;
+}
 
 const char* sp_last_error(void) { return g_err; }
 
@@ -357,9 +425,9 @@ int sp_dps_residual(const sp_op* op, const float* x, const float* eps, const flo
     const int P = static_cast<int>(tiles_elementwise(op->n));
     const dim3 grid(P, static_cast<unsigned>(batch));
     const bool v4 = op->n % 4 == 0;
-#define SP_K1(OPK, V)                                                                        \
-    hipLaunchKernelGGL((k_dps_residual<OPK, V>), grid, dim3(kBlock), 0, s, *op, x, eps, y, \
-                       y_div, c->a, c->k, c->grad_scale, v_out, rsq_partial, P)
+#define SP_K1(OPK, V)                                                                       \
+    launch(TK_DPS_RESIDUAL, k_dps_residual<OPK, V>, grid, dim3(kBlock), s, *op, x, eps, y, y_div, \
+           c->a, c->k, c->grad_scale, v_out, rsq_partial, P)
     if (op->kind == SP_OP_IDENTITY) {
         if (v4) SP_K1(SP_OP_IDENTITY, 4); else SP_K1(SP_OP_IDENTITY, 1);
     } else if (op->kind == SP_OP_MASK) {
@@ -385,10 +453,9 @@ int sp_dps_update(const sp_op* op, const float* x, const float* eps, const float
     const dim3 grid(Pw, static_cast<unsigned>(batch));
     const bool v4 = op->n % 4 == 0;
     const int opk = op->kind == SP_OP_BLUR ? SP_OP_IDENTITY : op->kind;  // BLUR reads v
-#define SP_K2(OPK, V, VIN, XIN)                                                              \
-    hipLaunchKernelGGL((k_dps_update<OPK, V, VIN, XIN>), grid, dim3(kBlock), 0, s, *op, x, \
-                       eps, y, v, w, rsq_partial, P, xi, seed, step, sample_offset, y_div, *c, \
-                       x_out)
+#define SP_K2(OPK, V, VIN, XIN)                                                            \
+    launch(TK_DPS_UPDATE, k_dps_update<OPK, V, VIN, XIN>, grid, dim3(kBlock), s, *op, x, eps, y, \
+           v, w, rsq_partial, P, xi, seed, step, sample_offset, y_div, *c, x_out)
 #define SP_K2_XI(OPK, V, VIN) \
     if (xi) SP_K2(OPK, V, VIN, true); else SP_K2(OPK, V, VIN, false)
 #define SP_K2_V(OPK, V) \

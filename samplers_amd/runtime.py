@@ -1,0 +1,57 @@
+"""Process-level runtime setup for the MI355X path.
+
+MIOpen (the convolution library behind the PyTorch-ROCm prior) picks a solver
+per convolution shape by timing candidates the first time it meets the shape,
+and compiles the winning kernels; on a fresh gfx950 box that costs minutes and,
+when the search is cut short, a slower solver.  ``configure_miopen`` points
+MIOpen's user find-db and kernel cache at a writable in-tree directory and
+seeds it with ``samplers_amd/miopen_db/*.ufdb.txt`` — solver choices measured
+on MI355X by this project's own runs (a text table of solver names and
+timings, not code).  Existing settings of MIOPEN_USER_DB_PATH /
+MIOPEN_CUSTOM_CACHE_DIR are respected.
+"""
+
+from __future__ import annotations
+
+import os
+import shutil
+from pathlib import Path
+
+PACKAGE = Path(__file__).resolve().parent
+SEED_DB = PACKAGE / "miopen_db"
+
+
+def _writable_cache_dir() -> Path:
+    for cand in (PACKAGE.parent / ".miopen_cache",
+                 Path(os.environ.get("XDG_CACHE_HOME", Path.home() / ".cache")) / "samplers_amd_miopen"):
+        try:
+            cand.mkdir(parents=True, exist_ok=True)
+            probe = cand / ".w"
+            probe.write_text("")
+            probe.unlink()
+            return cand
+        except OSError:
+            continue
+    raise OSError("no writable directory for the MIOpen cache")
+
+
+def configure_miopen() -> Path | None:
+    """Set MIOpen's user-db / kernel-cache directory (idempotent); returns it."""
+    if os.environ.get("MIOPEN_USER_DB_PATH"):
+        cache = Path(os.environ["MIOPEN_USER_DB_PATH"])
+    else:
+        try:
+            cache = _writable_cache_dir()
+        except OSError:
+            return None
+        os.environ["MIOPEN_USER_DB_PATH"] = str(cache)
+    os.environ.setdefault("MIOPEN_CUSTOM_CACHE_DIR", str(cache))
+    try:
+        cache.mkdir(parents=True, exist_ok=True)
+        for src in SEED_DB.glob("*.ufdb.txt"):
+            dst = cache / src.name
+            if not dst.exists():
+                shutil.copyfile(src, dst)
+    except OSError:
+        pass
+    return cache

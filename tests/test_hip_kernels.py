@@ -192,3 +192,33 @@ def test_bad_arguments_return_einval(cuda):
     assert lib.sp_rsq_partials(bad) == -1
     with pytest.raises(_hip.HipLibraryError):
         _hip.check(-1, "x")
+
+
+def test_dispatch_packet_timing(cuda):
+    from samplers_amd.samplers.dps import KernelTimer
+
+    lib = _hip.load_library()
+    op = IdentityOperator((3, 64, 64))
+    desc = op.hip_descriptor()
+    b, n = 8, 3 * 64 * 64
+    x, eps, y, w = (torch.randn(b, n, device=cuda) for _ in range(4))
+    v = torch.empty_like(x)
+    P = lib.sp_rsq_partials(desc)
+    part = torch.empty(b, P, device=cuda)
+    c = _hip.SpDpsCoefs(0.5, 0.8, 10.0, 0.9, 0.2, 0.3, 0.1, 1e-9)
+    timer = KernelTimer()
+    try:
+        for _ in range(3):
+            with timer.span("dps_residual", b):
+                _hip.check(lib.sp_dps_residual(desc, x.data_ptr(), eps.data_ptr(), y.data_ptr(), b, 1,
+                                               c, v.data_ptr(), part.data_ptr(), _stream()), "k1")
+            with timer.span("dps_update", b):
+                _hip.check(lib.sp_dps_update(desc, x.data_ptr(), eps.data_ptr(), y.data_ptr(),
+                                             v.data_ptr(), w.data_ptr(), part.data_ptr(), None, 1, 2,
+                                             0, b, 1, c, x.data_ptr(), _stream()), "k2")
+        s = timer.summary()
+    finally:
+        timer.close()
+    assert s["dps_residual"]["count"] == 3 and s["dps_update"]["count"] == 3
+    assert 0 < s["dps_residual"]["ms"] < 100 and 0 < s["dps_update"]["ms"] < 100
+    assert s["dps_update"]["samples"] == 3 * b
