@@ -75,6 +75,26 @@ typedef struct sp_dps_coefs {
     float norm_eps;   /* 1e-9                    dps.py:121                      */
 } sp_dps_coefs;
 
+/* Scalars of the epsilon-form DDIM step (bridge_kernels.py:82-115), fp32 as there. */
+typedef struct sp_eps_coefs {
+    float sqrt_oma;    /* sqrt(1 - acp_t)                                   */
+    float oma;         /* 1 - acp_t                  (pseudo-x0)            */
+    float sqrt_a;      /* sqrt(acp_t)                                       */
+    float sqrt_a_prev; /* sqrt(acp_prev)                                    */
+    float sigma;       /* eta*sqrt(clamp((1-acp_prev)/(1-acp_t)*(1-acp_t/acp_prev)))      */
+    float dir;         /* sqrt(clamp(1 - acp_prev - sigma^2))                */
+} sp_eps_coefs;
+
+/* One torch.optim.AdamW step (resample_kernels.py:32-93 optimisers). */
+typedef struct sp_adamw_coefs {
+    float decay;      /* 1 - lr*weight_decay                                 */
+    float beta1;      /* 0.9                                                 */
+    float beta2;      /* 0.999                                               */
+    float eps;        /* 1e-8                                                */
+    float step_size;  /* lr / (1 - beta1^step)                               */
+    float bc2_sqrt;   /* sqrt(1 - beta2^step)                                */
+} sp_adamw_coefs;
+
 /* Kernel timing (instrumentation, off by default).  While enabled, every
  * sp_dps_residual / sp_dps_update launch gets a start/stop hipEvent pair attached
  * to its dispatch packet (hipExtLaunchKernel), i.e. the kernel's own execution
@@ -107,8 +127,11 @@ int sp_dps_residual(const sp_op* op, const float* x, const float* eps, const flo
  * the guidance correction):
  *   g   = v/a - (k/a) * w          (w = J_eps^T v from the prior's VJP)
  *   x'  = c_ell*x + c_s*x0 + std*xi + gamma/(sqrt(sum_p rsq_partial[b][p]) + norm_eps) * g
- * v: pass NULL to recompute v from (x, eps, y) (IDENTITY/INPAINT only), else
+ * v: pass NULL to recompute v from (x, eps, y) (IDENTITY/INPAINT/MASK), else
  *    the buffer written by sp_dps_residual (required for BLUR).
+ * rsq_partial: NULL selects a fixed factor, x' = ... + gamma * g — the PGDM update
+ *    (pgdm.py:126-135, gamma = -guidance_weight*sqrt(1-acp_t), v = -2 A^T r) and the
+ *    PSLD update (psld.py:144-153, gamma = -1, v = the latent cotangent).
  * xi: injected standard-normal noise (B*n) or NULL to draw Philox4x32-10
  *    normals keyed by (seed, step, sample_offset + b, element) — invariant to
  *    how the batch is sharded across GPUs.  x_out may alias x. */
@@ -139,6 +162,38 @@ int sp_op_adjoint(const sp_op* op, const float* y, float* x, int64_t batch, sp_s
 int64_t sp_vec_partials(int64_t count);
 int sp_residual_grad(const float* y, const float* z, int64_t batch, int64_t m, int64_t y_div,
                      float grad_scale, float* g, float* rsq_partial, sp_stream_t stream);
+
+/* ---- latent samplers (PSLD psld.py:118-153, ReSample resample.py:131-228) ---------- */
+
+/* PSLD pixel pass for IDENTITY / INPAINT / MASK (BLUR returns SP_EUNSUPPORTED: the
+ * caller composes it from sp_op_apply / sp_op_adjoint):
+ *   r = y - A x0,  x_eff = A^T y + x0 - A^T A x0,  atr = A^T r,
+ *   rsq_partial[b][p] = partial sums of r^2 (sp_rsq_partials(op) per sample). */
+int sp_psld_pixel(const sp_op* op, const float* x0, const float* y, int64_t batch, int64_t y_div,
+                  float* x_eff, float* atr, float* rsq_partial, sp_stream_t stream);
+/* out[0] = sum of count partials (one workgroup, fixed order; a device scalar). */
+int sp_sum_partials(const float* partials, int64_t count, float* out, sp_stream_t stream);
+/* out = alpha*a + beta/sqrt(*norm_sq)*b  (a may be NULL; norm_sq NULL means 1; a zero norm
+ * gives 0, as torch's norm backward).  Gluing-term cotangents of psld.py:138-141. */
+int sp_scaled_combine(const float* a, float alpha, const float* b, float beta, const float* norm_sq,
+                      int64_t count, float* out, sp_stream_t stream);
+/* c_x0 = -omega * atr / sqrt(*norm_sq) + (I - A^T A) u   (ata_u = A^T A u, BLUR only). */
+int sp_psld_cotangent(const sp_op* op, const float* atr, const float* u, const float* ata_u,
+                      const float* norm_sq, float omega, int64_t batch, float* out,
+                      sp_stream_t stream);
+/* epsilon-form DDIM step: x_prev = sqrt_a_prev*x0 + dir*eps + sigma*xi, x0 and pseudo-x0;
+ * any output may be NULL; xi NULL = Philox(seed, step, sample_offset+b). */
+int sp_ddim_eps_step(const float* x, const float* eps, int64_t batch, int64_t n,
+                     const sp_eps_coefs* c, const float* xi, uint64_t seed, int64_t step,
+                     int64_t sample_offset, float* x_prev, float* x0, float* pseudo_x0,
+                     sp_stream_t stream);
+/* ReSample stochastic resample (resample_kernels.py:96-107), a_t / sigma scalars. */
+int sp_stochastic_resample(const float* pseudo_x0, const float* x_t, int64_t batch, int64_t n,
+                           float a_t, float sigma, const float* xi, uint64_t seed, int64_t step,
+                           int64_t sample_offset, float* out, sp_stream_t stream);
+/* In-place AdamW update of `count` parameters. */
+int sp_adamw_step(float* param, const float* grad, float* exp_avg, float* exp_avg_sq,
+                  int64_t count, const sp_adamw_coefs* c, sp_stream_t stream);
 
 #ifdef __cplusplus
 }

@@ -32,10 +32,13 @@ def blur(x: torch.Tensor, k1d: np.ndarray) -> torch.Tensor:
 
 
 def blur_adjoint(y: torch.Tensor, k1d: np.ndarray) -> torch.Tensor:
+    """A^T y by autograd of the forward map; differentiable in y (create_graph), so
+    loops that backpropagate through A^T (PSLD's x_eff) see the exact transpose."""
     x = torch.zeros_like(y, dtype=torch.float64, requires_grad=True)
     with torch.enable_grad():
         out = blur(x, k1d)
-        (g,) = torch.autograd.grad(out, x, grad_outputs=y.to(torch.float64))
+        (g,) = torch.autograd.grad(out, x, grad_outputs=y.to(torch.float64),
+                                   create_graph=y.requires_grad)
     return g
 
 

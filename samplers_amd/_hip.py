@@ -53,6 +53,14 @@ class SpDpsCoefs(ctypes.Structure):
     ]
 
 
+class SpEpsCoefs(ctypes.Structure):
+    _fields_ = [(f, ctypes.c_float) for f in ("sqrt_oma", "oma", "sqrt_a", "sqrt_a_prev", "sigma", "dir")]
+
+
+class SpAdamWCoefs(ctypes.Structure):
+    _fields_ = [(f, ctypes.c_float) for f in ("decay", "beta1", "beta2", "eps", "step_size", "bc2_sqrt")]
+
+
 _P = ctypes.c_void_p
 _I64 = ctypes.c_int64
 _U64 = ctypes.c_uint64
@@ -77,6 +85,15 @@ SIGNATURES = {
     "sp_op_apply": (ctypes.c_int, [_OPP, _P, _P, _I64, _P]),
     "sp_op_adjoint": (ctypes.c_int, [_OPP, _P, _P, _I64, _P]),
     "sp_residual_grad": (ctypes.c_int, [_P, _P, _I64, _I64, _I64, _F, _P, _P, _P]),
+    "sp_psld_pixel": (ctypes.c_int, [_OPP, _P, _P, _I64, _I64, _P, _P, _P, _P]),
+    "sp_sum_partials": (ctypes.c_int, [_P, _I64, _P, _P]),
+    "sp_scaled_combine": (ctypes.c_int, [_P, _F, _P, _F, _P, _I64, _P, _P]),
+    "sp_psld_cotangent": (ctypes.c_int, [_OPP, _P, _P, _P, _P, _F, _I64, _P, _P]),
+    "sp_ddim_eps_step": (ctypes.c_int, [_P, _P, _I64, _I64, ctypes.POINTER(SpEpsCoefs), _P, _U64,
+                                        _I64, _I64, _P, _P, _P, _P]),
+    "sp_stochastic_resample": (ctypes.c_int, [_P, _P, _I64, _I64, _F, _F, _P, _U64, _I64, _I64, _P,
+                                              _P]),
+    "sp_adamw_step": (ctypes.c_int, [_P, _P, _P, _P, _I64, ctypes.POINTER(SpAdamWCoefs), _P]),
 }
 
 _lib = None

@@ -186,8 +186,9 @@ __global__ __launch_bounds__(kBlock) void k_dps_update(
             }
         }
     }
-    const float rsq = sum_partials(partial + b * P, P);
-    const float scale = c.gamma / (sqrtf(rsq) + c.norm_eps);
+    // DPS: gamma / (||r_b|| + eps); without partials a fixed factor (PGDM, PSLD)
+    const float scale =
+        partial ? c.gamma / (sqrtf(sum_partials(partial + b * P, P)) + c.norm_eps) : c.gamma;
 #pragma unroll
     for (int it = 0; it < kIter; ++it) {
         const int64_t j = j0 + it * (kBlock * V);
@@ -443,8 +444,8 @@ int sp_dps_update(const sp_op* op, const float* x, const float* eps, const float
                   const float* v, const float* w, const float* rsq_partial, const float* xi,
                   uint64_t seed, int64_t step, int64_t sample_offset, int64_t batch, int64_t y_div,
                   const sp_dps_coefs* c, float* x_out, sp_stream_t stream) {
-    if (!valid_op(op) || !x || !eps || !w || !rsq_partial || !c || !x_out || batch <= 0 ||
-        y_div <= 0 || batch > 65535)
+    if (!valid_op(op) || !x || !eps || !w || !c || !x_out || batch <= 0 || y_div <= 0 ||
+        batch > 65535)
         return SP_EINVAL;
     if (!v && (op->kind == SP_OP_BLUR || !y)) return SP_EINVAL;
     hipStream_t s = static_cast<hipStream_t>(stream);

@@ -69,18 +69,21 @@ class TimestepEmbedding(nn.Module):
 
 
 class ResnetBlock2D(nn.Module):
-    def __init__(self, cin: int, cout: int, temb: int, groups: int, eps: float) -> None:
+    """GN-SiLU-conv x2 with an optional time-embedding bias (``temb=None``: VAE blocks)."""
+
+    def __init__(self, cin: int, cout: int, temb: int | None, groups: int, eps: float) -> None:
         super().__init__()
         self.norm1 = nn.GroupNorm(groups, cin, eps=eps)
         self.conv1 = nn.Conv2d(cin, cout, 3, padding=1)
-        self.time_emb_proj = nn.Linear(temb, cout)
+        self.time_emb_proj = nn.Linear(temb, cout) if temb else None
         self.norm2 = nn.GroupNorm(groups, cout, eps=eps)
         self.conv2 = nn.Conv2d(cout, cout, 3, padding=1)
         self.conv_shortcut = nn.Conv2d(cin, cout, 1) if cin != cout else None
 
-    def forward(self, x: Tensor, temb: Tensor) -> Tensor:
+    def forward(self, x: Tensor, temb: Tensor | None = None) -> Tensor:
         h = self.conv1(F.silu(self.norm1(x)))
-        h = h + self.time_emb_proj(F.silu(temb))[:, :, None, None]
+        if self.time_emb_proj is not None:
+            h = h + self.time_emb_proj(F.silu(temb))[:, :, None, None]
         h = self.conv2(F.silu(self.norm2(h)))
         if self.conv_shortcut is not None:
             x = self.conv_shortcut(x)

@@ -29,6 +29,7 @@ from __future__ import annotations
 
 from typing import Callable, Generic, TypeVar
 
+import numpy as np
 import torch
 from torch import Tensor
 
@@ -115,7 +116,7 @@ class FusedDPSStep:
     def __init__(self, network: EpsilonNetwork, inverse_problem: InverseProblem,
                  observation_rows: Tensor, y_div: int, *, gamma: float = 1.0, eta: float = 1.0,
                  micro_batch: int | None = None, timer: KernelTimer | None = None,
-                 reuse_v: bool = True) -> None:
+                 reuse_v: bool = True, mode: str = "dps", guidance_weight: float = 1.0) -> None:
         op = inverse_problem.operator
         desc = op.hip_descriptor()
         if desc is None:
@@ -138,7 +139,13 @@ class FusedDPSStep:
         self.partials = int(self.lib.sp_rsq_partials(desc))
         if self.partials <= 0:
             raise _hip.HipLibraryError(f"operator descriptor rejected ({self.partials})")
-        self.grad_scale = float(inverse_problem.noise.grad_scale())
+        if mode not in ("dps", "pgdm"):
+            raise ValueError(mode)
+        self.mode = mode
+        # DPS: d log p/d(Ax) = c r.  PGDM: d/dx0 of ||A^+ y - A^+ A x0||^2 = -2 A^T r for the
+        # partial isometries with a native kernel (A^+ = A^T: identity, inpainting, mask).
+        self.grad_scale = (float(inverse_problem.noise.grad_scale()) if mode == "dps" else -2.0)
+        self.guidance_weight = float(guidance_weight)
         self.gamma, self.eta = float(gamma), float(eta)
         # pass 2 re-reads pass 1's v (default: one coalesced float4 stream; measured 4 % faster
         # than re-deriving v from (x, eps, y) through the inpainting gather on MI355X) or
@@ -151,7 +158,10 @@ class FusedDPSStep:
         acp = self.network.alphas_cumprod_host
         a, k = x0_coefficients(acp, t)
         br = bridge_coefficients(acp, ell=t, t=t_prev, s=s, eta=self.eta)
-        return _hip.SpDpsCoefs(a, k, self.grad_scale, br.c_ell, br.c_s, br.std, self.gamma, 1e-9)
+        # PGDM: sample = ddim - guidance_weight * sqrt(1 - acp_t) * grad   (pgdm.py:131-135)
+        gamma = self.gamma if self.mode == "dps" else float(np.float32(-self.guidance_weight) *
+                                                                  np.float32(k))
+        return _hip.SpDpsCoefs(a, k, self.grad_scale, br.c_ell, br.c_s, br.std, gamma, 1e-9)
 
     def _chunks(self, batch: int):
         mb = self.micro_batch or batch
@@ -195,7 +205,8 @@ class FusedDPSStep:
                 span.__enter__()
             _hip.check(lib.sp_dps_update(desc, _hip.ptr(xc), _hip.ptr(eps_c), _hip.ptr(yc),
                                          _hip.ptr(v) if self.needs_v else None, _hip.ptr(w),
-                                         _hip.ptr(part), _hip.ptr(xic), seed, step,
+                                         _hip.ptr(part) if self.mode == "dps" else None,
+                                         _hip.ptr(xic), seed, step,
                                          sample_offset + b0, bc, self.y_div, coefs, _hip.ptr(xc),
                                          stream),
                        "sp_dps_update")

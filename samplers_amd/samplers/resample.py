@@ -1,0 +1,317 @@
+"""ReSample: latent diffusion with hard data consistency
+(mirrors ``/root/reference/samplers/samplers/resample.py:27-228`` and
+``utils/resample_kernels.py``).
+
+Same control flow as the reference (ε-form DDIM step, DPS-style conditioning
+with scale ½ᾱ_t, time-travel blocks every ``time_travel_interval`` indices in
+the later part of the trajectory, pixel-space or latent-space AdamW hard
+consistency, stochastic resample, a final latent optimisation); the arithmetic
+between the priors is HIP:
+
+* ``sp_ddim_eps_step``       ε-form DDIM (x_prev, x0, pseudo-x0) + noise
+* ``sp_residual_grad`` + ``sp_sum_partials``  y − A(x), ‖·‖² / MSE, ∂/∂(Ax)
+* ``sp_op_apply`` / ``sp_op_adjoint``        A and Aᵀ
+* ``sp_adamw_step``          fused torch.optim.AdamW update
+* ``sp_stochastic_resample`` the resample step
+
+Losses and norms are batch-global (MSE mean / Frobenius norm over the whole
+flat batch, as in the reference); with a process group they are
+all-reduced (8 bytes) before use.  The optimisers' early-stopping tests read the
+loss on the host once per iteration, exactly where the reference calls
+``.item()`` (``resample_kernels.py:51,81``).
+"""
+
+from __future__ import annotations
+
+import math
+from typing import Generic, TypeVar
+
+import numpy as np
+import torch
+import torch.distributed as dist
+from torch import Tensor
+
+from samplers_amd import _hip
+from samplers_amd.dtypes import Shape
+from samplers_amd.inverse_problem import InverseProblem
+from samplers_amd.networks.base import LatentEpsilonNetwork
+from samplers_amd.noise import GaussianNoise
+from samplers_amd.samplers.base import PosteriorSampler
+from samplers_amd.samplers.dps import NoiseFn, draw_seed, initial_sample
+from samplers_amd.samplers.utils.batch_view import BatchView
+from samplers_amd.samplers.utils.bridge_kernels import eps_step_coefficients
+
+Condition_co = TypeVar("Condition_co", covariant=True)
+
+# Philox stream keys of the draw sites (the main DDIM step uses the loop index)
+_TRAVEL, _RESAMPLE = 1 << 32, 2 << 32
+
+
+def adamw_coefficients(step: int, lr: float, beta1: float = 0.9, beta2: float = 0.999,
+                       eps: float = 1e-8, weight_decay: float = 1e-2) -> _hip.SpAdamWCoefs:
+    """Scalars of torch.optim.AdamW's single-tensor step ``step`` (1-based), fp32-rounded."""
+    f = np.float32
+    bc1 = 1 - beta1**step
+    bc2 = 1 - beta2**step
+    return _hip.SpAdamWCoefs(float(f(1 - lr * weight_decay)), beta1, beta2, eps,
+                             float(f(lr / bc1)), float(f(math.sqrt(bc2))))
+
+
+class _Consistency:
+    """Batch-global ``||y - A x||`` / MSE and their gradients w.r.t. x, on HIP."""
+
+    def __init__(self, operator, y_rows: Tensor, y_div: int, group=None) -> None:
+        self.lib = _hip.load_library()
+        self.op = operator
+        self.desc = operator.hip_descriptor()
+        if self.desc is None:
+            raise NotImplementedError(f"{type(operator).__name__} has no native (HIP) implementation")
+        self.y = y_rows.to(torch.float32).contiguous()
+        self.y_div = int(y_div)
+        self.m, self.n = int(self.desc.m), int(self.desc.n)
+        self.P = int(self.lib.sp_vec_partials(self.m))
+        self.group = group
+
+    def _reduce(self, part: Tensor, out: Tensor, stream: int) -> None:
+        _hip.check(self.lib.sp_sum_partials(_hip.ptr(part), part.numel(), out.data_ptr(), stream),
+                   "sp_sum_partials")
+        if dist.is_initialized() and dist.get_world_size(self.group) > 1:
+            dist.all_reduce(out, group=self.group)
+
+    def residual(self, x: Tensor, scale: float) -> tuple[Tensor, Tensor]:
+        """(g_y = scale * (y - A x), sum of squares (device scalar, global))."""
+        lib, b = self.lib, x.shape[0]
+        stream = _hip.stream_of(x)
+        xf = x.reshape(b, self.n).contiguous()
+        ax = torch.empty(b, self.m, device=x.device)
+        _hip.check(lib.sp_op_apply(self.desc, _hip.ptr(xf), _hip.ptr(ax), b, stream), "sp_op_apply")
+        g = torch.empty_like(ax)
+        part = torch.empty(b, self.P, device=x.device)
+        _hip.check(lib.sp_residual_grad(_hip.ptr(self.y), _hip.ptr(ax), b, self.m, self.y_div,
+                                        scale, _hip.ptr(g), _hip.ptr(part), stream),
+                   "sp_residual_grad")
+        ss = torch.empty(1, device=x.device)
+        self._reduce(part, ss, stream)
+        return g, ss
+
+    def adjoint(self, g: Tensor, like: Tensor) -> Tensor:
+        out = torch.empty(like.shape, device=like.device, dtype=torch.float32)
+        _hip.check(self.lib.sp_op_adjoint(self.desc, _hip.ptr(g), _hip.ptr(out), g.shape[0],
+                                          _hip.stream_of(g)), "sp_op_adjoint")
+        return out
+
+    def mse_grad(self, x: Tensor, total: int) -> tuple[Tensor, Tensor]:
+        """(∂ MSE/∂x, MSE) with MSE = mean over all `total` observation elements."""
+        g, ss = self.residual(x, float(np.float32(-2.0 / total)))  # mse_loss backward: 2(y-Ax)/M
+        return self.adjoint(g, x), ss / total
+
+    def norm_grad(self, x: Tensor) -> Tensor:
+        """∂ ||y - A x||_F / ∂x = -A^T r / ||r|| (0 at r = 0)."""
+        g, ss = self.residual(x, 1.0)
+        gs = torch.empty_like(g)
+        _hip.check(self.lib.sp_scaled_combine(None, 0.0, _hip.ptr(g), -1.0, ss.data_ptr(), g.numel(),
+                                              _hip.ptr(gs), _hip.stream_of(g)), "combine")
+        return self.adjoint(gs, x)
+
+
+class ReSampleSampler(PosteriorSampler, Generic[Condition_co]):
+    """ReSample (Song et al., 2023) on the HIP path."""
+
+    def __init__(self, network):
+        super().__init__(network)
+        if not isinstance(self._epsilon_network, LatentEpsilonNetwork):
+            raise TypeError(
+                f"{self.__class__.__name__} requires a latent diffusion model, but build_network "
+                f"returned a non-latent network ({type(self._epsilon_network).__name__})."
+            )
+
+    # --- pieces ------------------------------------------------------------
+    def _ddim_eps(self, z: Tensor, t: int, t_prev: int, eta: float, noise: Tensor | None,
+                  seed: int, key: int, offset: int, *, want_x0: bool = False):
+        """ε-form DDIM step (``bridge_kernels.py:82-115``) -> (z_prev, pseudo_x0[, x0])."""
+        net, lib = self._epsilon_network, _hip.load_library()
+        c = eps_step_coefficients(net.alphas_cumprod_host, t, t_prev, eta)
+        with torch.no_grad():
+            e = net.predict_noise(z, t).contiguous()
+        zp, pseudo = torch.empty_like(z), torch.empty_like(z)
+        x0 = torch.empty_like(z) if want_x0 else None
+        coefs = _hip.SpEpsCoefs(c["sqrt_oma"], c["oma"], c["sqrt_a"], c["sqrt_a_prev"], c["sigma"],
+                                c["dir"])
+        b = z.shape[0]
+        _hip.check(lib.sp_ddim_eps_step(_hip.ptr(z.detach().contiguous()), _hip.ptr(e), b,
+                                        z[0].numel(), coefs, _hip.ptr(noise), seed, key, offset,
+                                        _hip.ptr(zp), _hip.ptr(x0), _hip.ptr(pseudo),
+                                        _hip.stream_of(z)), "sp_ddim_eps_step")
+        return zp, pseudo, c["sqrt_a"]
+
+    def _dps_conditioning(self, z_next: Tensor, pseudo: Tensor, sqrt_a: float, a_t: float,
+                          cons: _Consistency) -> Tensor:
+        """``resample_kernels.py:15-29``: z_next - 0.5 a_t * ∇_z ||y - A D(pseudo)||."""
+        net = self._epsilon_network
+        with torch.enable_grad():
+            pr = pseudo.detach().requires_grad_(True)
+            x = net.decode(pr, differentiable=True)
+        gx = cons.norm_grad(x.detach())
+        (gp,) = torch.autograd.grad(x, pr, grad_outputs=gx.reshape(x.shape))
+        out = torch.empty_like(z_next)
+        scale = float(np.float32(a_t) * np.float32(0.5))
+        # d pseudo / d z = 1/sqrt(a_t) (eps is evaluated without grad, bridge_kernels.py:97-98)
+        _hip.check(cons.lib.sp_scaled_combine(_hip.ptr(z_next), 1.0, _hip.ptr(gp.contiguous()),
+                                              -scale / sqrt_a, None, out.numel(), _hip.ptr(out),
+                                              _hip.stream_of(out)), "combine")
+        return out
+
+    def _adamw(self, param: Tensor, grad: Tensor, state: dict, lr: float) -> None:
+        state["step"] += 1
+        c = adamw_coefficients(state["step"], lr)
+        _hip.check(_hip.load_library().sp_adamw_step(
+            _hip.ptr(param), _hip.ptr(grad.contiguous()), _hip.ptr(state["m"]), _hip.ptr(state["v"]),
+            param.numel(), c, _hip.stream_of(param)), "sp_adamw_step")
+
+    def _pixel_optimization(self, x0: Tensor, cons: _Consistency, total: int, eps: float,
+                            max_iters: int) -> Tensor:
+        """``resample_kernels.py:32-54``: AdamW(lr=1e-2) on x, MSE, stop below eps^2."""
+        x = x0.detach().clone().contiguous()
+        st = {"step": 0, "m": torch.zeros_like(x), "v": torch.zeros_like(x)}
+        for _ in range(max_iters):
+            g, loss = cons.mse_grad(x, total)
+            self._adamw(x, g, st, 1e-2)
+            if loss.item() < eps**2:
+                break
+        return x
+
+    def _latent_optimization(self, z0: Tensor, cons: _Consistency, total: int, eps: float,
+                             max_iters: int) -> Tensor:
+        """``resample_kernels.py:57-93``: AdamW(lr=5e-3) on z through the decoder."""
+        net = self._epsilon_network
+        z = z0.detach().clone().contiguous()
+        st = {"step": 0, "m": torch.zeros_like(z), "v": torch.zeros_like(z)}
+        losses: list[float] = []
+        for itr in range(max_iters):
+            with torch.enable_grad():
+                zr = z.detach().requires_grad_(True)
+                x = net.decode(zr, differentiable=True)
+            gx, loss = cons.mse_grad(x.detach(), total)
+            (gz,) = torch.autograd.grad(x, zr, grad_outputs=gx.reshape(x.shape))
+            self._adamw(z, gz, st, 5e-3)
+            cur = loss.item()
+            if itr >= 200:
+                losses.append(cur)
+                if len(losses) > 1 and losses[0] < cur:
+                    break
+                if len(losses) > 1:
+                    losses.pop(0)
+            if cur < eps**2:
+                break
+        return z
+
+    def _resample(self, z_opt: Tensor, snapshot: Tensor, a_prev: float, sigma: float,
+                  noise: Tensor | None, seed: int, key: int, offset: int) -> Tensor:
+        out = torch.empty_like(z_opt)
+        _hip.check(_hip.load_library().sp_stochastic_resample(
+            _hip.ptr(z_opt.contiguous()), _hip.ptr(snapshot.contiguous()), z_opt.shape[0],
+            z_opt[0].numel(), a_prev, sigma, _hip.ptr(noise), seed, key, offset, _hip.ptr(out),
+            _hip.stream_of(out)), "sp_stochastic_resample")
+        return out
+
+    # --- driver --------------------------------------------------------------
+    def __call__(
+        self,
+        inverse_problem: InverseProblem,
+        *,
+        num_sampling_steps: int = 100,
+        num_reconstructions: int = 1,
+        scale: float = 0.3,
+        sigma_scale: float = 40.0,
+        max_optimization_iters: int = 2000,
+        eta: float = 1.0,
+        inter_timesteps: int = 5,
+        time_travel_interval: int = 10,
+        stage_splits: int = 3,
+        decode_output: bool = True,
+        condition: Condition_co | None = None,
+        rng: str = "philox",
+        seed: int | None = None,
+        noise_fn: NoiseFn | None = None,
+        sample_offset: int = 0,
+        group=None,
+    ) -> Tensor:
+        """Run ReSample; ``scale`` is accepted and unused, as in the reference
+        (its DPS step size is ½ᾱ_t, ``resample.py:145-146``)."""
+        x_shape: Shape = inverse_problem.operator.x_shape
+        batch_shape: Shape = inverse_problem.batch_shape
+        x_view = BatchView(batch_shape, num_reconstructions, x_shape)
+        net: LatentEpsilonNetwork = self._epsilon_network
+        latent_shape: Shape = tuple(net.get_latent_shape(x_shape))
+        z_view = BatchView(batch_shape, num_reconstructions, latent_shape)
+        net.set_sampling_parameters(num_sampling_steps=num_sampling_steps,
+                                    num_reconstructions=num_reconstructions,
+                                    batch_size=x_view.batch_size)
+        net.set_condition(condition)
+        try:
+            obs = inverse_problem.observation
+            _hip.require_cuda(obs, "ReSampleSampler")
+            y_rows = obs.reshape(max(x_view.batch_size, 1), -1)
+            cons = _Consistency(inverse_problem.operator, y_rows, num_reconstructions, group)
+            total = z_view.leading_size * cons.m  # MSELoss mean over the tiled observation
+            if dist.is_initialized() and dist.get_world_size(group) > 1:
+                t = torch.tensor([float(total)], device=obs.device, dtype=torch.float64)
+                dist.all_reduce(t, group=group)
+                total = int(t.item())
+            if seed is None and noise_fn is None and rng == "philox":
+                seed = draw_seed()
+            seed = int(seed or 0)
+            off = sample_offset
+
+            def draw(kind: str, key: int, like: Tensor) -> Tensor | None:
+                if noise_fn is not None:
+                    return noise_fn(kind, key, tuple(like.shape)).to(device=like.device,
+                                                                     dtype=torch.float32)
+                if rng == "torch":
+                    return torch.randn_like(like)
+                return None  # Philox inside the kernel
+
+            z = initial_sample(z_view.flat_shape, net.device, rng=rng, seed=seed,
+                               sample_offset=off, noise_fn=noise_fn)
+            eps = float(inverse_problem.noise.sigma.item()) \
+                if isinstance(inverse_problem.noise, GaussianNoise) else 1e-3
+            ts = net.timesteps_host
+            acp = net.alphas_cumprod_host
+            total_steps = len(ts) - 1
+            index_split = total_steps // stage_splits
+            for idx in range(len(ts) - 1, 1, -1):
+                t, tp = ts[idx], ts[idx - 1]
+                z_next, pseudo, sqrt_a = self._ddim_eps(z, t, tp, eta, draw("step", idx, z), seed,
+                                                        idx, off)
+                a_t = float(np.float32(acp[t]))
+                z = self._dps_conditioning(z_next, pseudo, sqrt_a, a_t, cons)
+                if idx <= total_steps - index_split and idx > 0 and idx % time_travel_interval == 0:
+                    snapshot = z.clone()
+                    for kk in range(idx, max(idx - inter_timesteps, 1), -1):
+                        if kk <= 1:
+                            break
+                        key = _TRAVEL | (idx << 16) | kk
+                        z, pseudo, _ = self._ddim_eps(z, ts[kk], ts[kk - 1], eta,
+                                                      draw("travel", key, z), seed, key, off)
+                    a_prev = np.float32(acp[tp])
+                    f = np.float32
+                    sigma = float(f(sigma_scale) * (f(1) - a_prev) / (f(1) - f(a_t))
+                                  * (f(1) - f(a_t) / a_prev))
+                    if idx >= index_split:
+                        x_pix = net.decode(pseudo, differentiable=False)
+                        x_opt = self._pixel_optimization(x_pix, cons, total, eps,
+                                                         max_optimization_iters)
+                        z_opt = net.encode(x_opt.reshape(x_pix.shape), differentiable=False)
+                    else:
+                        z_opt = self._latent_optimization(pseudo, cons, total, eps,
+                                                          max_optimization_iters)
+                    key = _RESAMPLE | idx
+                    z = self._resample(z_opt, snapshot, float(a_prev), sigma,
+                                       draw("resample", key, z_opt), seed, key, off)
+            final_z0 = self._latent_optimization(z, cons, total, eps, max_optimization_iters)
+            if decode_output:
+                return x_view.unflatten(net.decode(final_z0, differentiable=False))
+            return z_view.unflatten(final_z0)
+        finally:
+            net.clear_condition()
+            net.clear_sampling_parameters()

@@ -33,11 +33,18 @@ class DpsCase:
         return (int(np.prod(bs)) if bs else 1) * self.meta["R"]
 
     def noise(self):
-        return si.replay_noise(self.meta["seed"], (self.lead, *self.shape), self.meta["N"])
+        shape = tuple(self.meta.get("latent_shape", self.shape))
+        return si.replay_noise(self.meta["seed"], (self.lead, *shape), self.meta["N"])
+
+    def observation_rows(self) -> torch.Tensor:
+        """y tiled to the flat batch (what the reference's repeat_observation produces)."""
+        bs = self.meta["batch_shape"]
+        rows = self.y.reshape(int(np.prod(bs)) if bs else 1, -1)
+        return rows.repeat_interleave(self.meta["R"], dim=0)
 
 
-def dps_case_names() -> list[str]:
-    return sorted(p.stem for p in GOLDEN.glob("dps_*.npz"))
+def dps_case_names(prefix: str = "dps") -> list[str]:
+    return sorted(p.stem for p in GOLDEN.glob(f"{prefix}_*.npz"))
 
 
 def load_dps_case(name: str) -> DpsCase:

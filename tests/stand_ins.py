@@ -56,6 +56,71 @@ class EpsCore(nn.Module):
         return nn.functional.conv2d(h, self.w2, padding=1) * (1.0 + tt) + self.coef * x
 
 
+class LatentCore(nn.Module):
+    """Linear stand-in VAE: decode = nearest-upsample(f) of a 1x1 conv (4 -> C),
+    encode = 1x1 conv (C -> 4) of avg_pool(f) (the posterior mean)."""
+
+    def __init__(self, channels: int = 3, latent: int = 4, factor: int = 4, seed: int = 77) -> None:
+        super().__init__()
+        gen = torch.Generator().manual_seed(seed)
+        self.factor, self.latent = factor, latent
+        self.wd = nn.Parameter(torch.randn(channels, latent, 1, 1, generator=gen) * 0.5,
+                               requires_grad=False)
+        self.we = nn.Parameter(torch.randn(latent, channels, 1, 1, generator=gen) * 0.5,
+                               requires_grad=False)
+
+    def decode(self, z: torch.Tensor) -> torch.Tensor:
+        x = nn.functional.conv2d(z, self.wd)
+        return nn.functional.interpolate(x, scale_factor=float(self.factor), mode="nearest")
+
+    def encode(self, x: torch.Tensor) -> torch.Tensor:
+        return nn.functional.conv2d(nn.functional.avg_pool2d(x, self.factor), self.we)
+
+    def latent_shape(self, x_shape):
+        c, h, w = x_shape
+        return (self.latent, h // self.factor, w // self.factor)
+
+
+def make_samplers_amd_latent_net(kind: str = "conv", coef: float = 0.1, device=None):
+    """Latent stand-in implementing :class:`samplers_amd.networks.base.LatentEpsilonNetwork`."""
+    from samplers_amd.networks.base import LatentEpsilonNetwork, NoCondition
+
+    class StandInLatent(LatentEpsilonNetwork[NoCondition]):
+        def __init__(self) -> None:
+            acp = ddpm_alphas_cumprod()
+            super().__init__(alphas_cumprod=torch.cat([acp.new_tensor([1.0]), acp]))
+            self.core = EpsCore(kind, 4, coef)
+            self.vae = LatentCore()
+
+        def forward(self, x, t):
+            return self.core(x, t)
+
+        @classmethod
+        def from_pretrained(cls, *a, **k):
+            raise NotImplementedError
+
+        def set_sampling_parameters(self, num_sampling_steps, batch_size=1, num_reconstructions=1):
+            self._batch_size = batch_size
+            self._num_sampling_steps = num_sampling_steps
+            self._set_timesteps_buffer(leading_timesteps_ascending(num_sampling_steps))
+
+        def get_latent_shape(self, x_shape):
+            return self.vae.latent_shape(x_shape)
+
+        def _decode(self, z, *, differentiable=False):
+            return self.vae.decode(z)
+
+        def _encode(self, x, *, differentiable=False):
+            return self.vae.encode(x)
+
+        @property
+        def is_condition_initialized(self) -> bool:
+            return True
+
+    net = StandInLatent()
+    return net.to(device) if device is not None else net
+
+
 def make_samplers_amd_net(kind: str, channels: int, coef: float = 0.1, device=None):
     """Stand-in prior implementing :class:`samplers_amd.networks.base.EpsilonNetwork`."""
     from samplers_amd.networks.base import EpsilonNetwork, NoCondition

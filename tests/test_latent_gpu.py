@@ -1,0 +1,224 @@
+"""PGDM and PSLD on the GPU against the reference's golden vectors and the oracle loops.
+
+Tolerance: relative L2 <= max(1e-5, 20 x the case's fp32-vs-fp64 sensitivity), the
+sensitivity measured here with the fp64 oracle (tests/test_oracle_latent.py pins the
+fp32 oracle to the reference bit-exactly).  PGDM amplifies perturbations strongly on
+these stand-in priors (its outputs reach 1e7), hence the per-case bound.
+"""
+
+import numpy as np
+import pytest
+import torch
+
+import stand_ins as si
+from golden_cases import dps_case_names, load_dps_case
+from oracle import blur as oblur
+from oracle.latent_loops import pgdm_reference, psld_reference
+from samplers_amd.inverse_problem import InverseProblem
+from samplers_amd.noise import GaussianNoise
+from samplers_amd.operators import GaussianBlurOperator, IdentityOperator, InpaintingOperator
+from samplers_amd.samplers.pgdm import PGDMSampler
+from samplers_amd.samplers.psld import PSLDSampler
+from test_oracle_latent import oracle_pgdm, oracle_psld
+
+pytestmark = pytest.mark.gpu
+
+
+def _problem(case, device):
+    op = (IdentityOperator(case.shape) if case.kept is None
+          else InpaintingOperator(case.shape, case.mask).to(device))
+    return InverseProblem(op, case.y.to(device), GaussianNoise(0.05).to(device))
+
+
+def _noise_fn(case, device):
+    init, steps = case.noise()
+    return lambda kind, i, s: (init if kind == "init" else steps[i]).to(device)
+
+
+def _tol(case, oracle_fn):
+    cond = si.relative_error(oracle_fn(case, torch.float64), case.out)
+    return max(1e-5, 20 * cond)
+
+
+@pytest.mark.parametrize("name", dps_case_names("pgdm"))
+def test_pgdm_matches_reference_golden(cuda, name):
+    case = load_dps_case(name)
+    m = case.meta
+    net = si.make_samplers_amd_net(m["prior"], case.shape[0], m["coef"], device=cuda)
+    out = PGDMSampler(net)(_problem(case, cuda), num_sampling_steps=m["N"],
+                           num_reconstructions=m["R"], guidance_weight=m["guidance_weight"],
+                           eta=m["eta"], noise_fn=_noise_fn(case, cuda))
+    assert tuple(out.shape) == tuple(m["out_shape"])
+    assert si.relative_error(out.cpu(), case.out) < _tol(case, oracle_pgdm)
+
+
+def test_pgdm_inpainting_matches_oracle(cuda):
+    """The reference cannot run PGDM with a flattened observation (F5); the oracle loop
+    with A^+ = A^T pins it."""
+    shape, b, N = (3, 32, 32), 2, 8
+    mask = si.fixture_mask(shape, "random")
+    op = InpaintingOperator(shape, mask)
+    kept = op._kept_indices
+    x_true = si.fixture_x_true(b, shape, 0)
+    y = op.apply(x_true) + 0.05 * torch.randn(b, kept.numel(), generator=torch.Generator().manual_seed(1))
+    init, steps = si.replay_noise(5, (b, *shape), N)
+    net = si.make_samplers_amd_net("conv", 3, 0.1, device=cuda)
+    fn = lambda kind, i, s: (init if kind == "init" else steps[i]).to(cuda)  # noqa: E731
+    out = PGDMSampler(net)(InverseProblem(op.to(cuda), y.to(cuda), GaussianNoise(0.05).to(cuda)),
+                           num_sampling_steps=N, guidance_weight=0.05, noise_fn=fn)
+    acp = torch.cat([torch.ones(1), si.ddpm_alphas_cumprod()]).clip(1e-6, 1)
+    kc = kept.cpu()
+
+    def apply(x):
+        return x.reshape(x.shape[0], -1)[:, kc]
+
+    def pinv(v):
+        o = torch.zeros(v.shape[0], int(np.prod(shape)), dtype=v.dtype)
+        o[:, kc] = v
+        return o.reshape(v.shape[0], *shape)
+
+    def run(dt):
+        c = si.EpsCore("conv", 3, 0.1).to(dt)
+        return pgdm_reference(lambda x, t: c(x, t), acp.to(dt),
+                              si.leading_timesteps_ascending(N).tolist(), apply, pinv, y.to(dt),
+                              init.to(dt), lambda i: steps[i].to(dt), guidance_weight=0.05, eta=1.0)
+
+    ref = run(torch.float32)
+    cond = si.relative_error(run(torch.float64), ref)  # PGDM amplifies rounding (outputs ~1e4)
+    assert si.relative_error(out.cpu(), ref) < max(1e-4, 20 * cond)
+
+
+def test_pgdm_rejects_operator_without_pinv(cuda):
+    net = si.make_samplers_amd_net("linear", 3, 0.1, device=cuda)
+    op = GaussianBlurOperator((3, 32, 32)).to(cuda)
+    ip = InverseProblem(op, torch.zeros(1, 3, 32, 32, device=cuda), GaussianNoise(0.1).to(cuda))
+    with pytest.raises(NotImplementedError):
+        PGDMSampler(net)(ip, num_sampling_steps=4)
+
+
+@pytest.mark.parametrize("name", dps_case_names("psld"))
+def test_psld_matches_reference_golden(cuda, name):
+    case = load_dps_case(name)
+    m = case.meta
+    net = si.make_samplers_amd_latent_net(m["prior"], m["coef"], device=cuda)
+    out = PSLDSampler(net)(_problem(case, cuda), num_sampling_steps=m["N"],
+                           num_reconstructions=m["R"], gamma=m["gamma"], omega=m["omega"],
+                           eta=m["eta"], noise_fn=_noise_fn(case, cuda))
+    assert tuple(out.shape) == tuple(m["out_shape"])
+    assert si.relative_error(out.cpu(), case.out) < _tol(case, oracle_psld)
+
+
+def test_psld_batched_inpainting_matches_oracle(cuda):
+    """Batch > 1 with a flattened observation (fails in the reference, F5)."""
+    shape, b, N = (3, 32, 32), 3, 8
+    mask = si.fixture_mask(shape, "center")
+    op = InpaintingOperator(shape, mask)
+    kc = op._kept_indices
+    x_true = si.fixture_x_true(b, shape, 2)
+    y = op.apply(x_true) + 0.05 * torch.randn(b, kc.numel(), generator=torch.Generator().manual_seed(3))
+    net = si.make_samplers_amd_latent_net("conv", 0.1, device=cuda)
+    lat = net.get_latent_shape(shape)
+    init, steps = si.replay_noise(9, (b, *lat), N)
+    fn = lambda kind, i, s: (init if kind == "init" else steps[i]).to(cuda)  # noqa: E731
+    out = PSLDSampler(net)(InverseProblem(op.to(cuda), y.to(cuda), GaussianNoise(0.05).to(cuda)),
+                           num_sampling_steps=N, noise_fn=fn)
+    core, vae = si.EpsCore("conv", 4, 0.1), si.LatentCore()
+    acp = torch.cat([torch.ones(1), si.ddpm_alphas_cumprod()]).clip(1e-6, 1)
+    n = int(np.prod(shape))
+
+    def apply(x):
+        return x.reshape(x.shape[0], -1)[:, kc]
+
+    def adjoint(v):
+        o = torch.zeros(v.shape[0], n, dtype=v.dtype)
+        o[:, kc] = v
+        return o.reshape(v.shape[0], *shape)
+
+    ref = psld_reference(lambda x, t: core(x, t), acp, si.leading_timesteps_ascending(N).tolist(),
+                         apply, adjoint, vae.decode, vae.encode, y, init, lambda i: steps[i])
+    assert si.relative_error(out.cpu(), ref) < 1e-4
+
+
+def test_psld_blur_matches_oracle(cuda):
+    shape, b, N = (3, 32, 32), 2, 6
+    k = oblur.taps(9, 3.0)
+    x_true = si.fixture_x_true(b, shape, 4)
+    y = oblur.blur(x_true, k).float() + 0.05 * torch.randn(b, *shape, generator=torch.Generator().manual_seed(4))
+    net = si.make_samplers_amd_latent_net("conv", 0.1, device=cuda)
+    lat = net.get_latent_shape(shape)
+    init, steps = si.replay_noise(13, (b, *lat), N)
+    fn = lambda kind, i, s: (init if kind == "init" else steps[i]).to(cuda)  # noqa: E731
+    op = GaussianBlurOperator(shape, 9, 3.0).to(cuda)
+    out = PSLDSampler(net)(InverseProblem(op, y.to(cuda), GaussianNoise(0.05).to(cuda)),
+                           num_sampling_steps=N, noise_fn=fn)
+    core, vae = si.EpsCore("conv", 4, 0.1), si.LatentCore()
+    acp = torch.cat([torch.ones(1), si.ddpm_alphas_cumprod()]).clip(1e-6, 1)
+    ref = psld_reference(lambda x, t: core(x, t), acp, si.leading_timesteps_ascending(N).tolist(),
+                         lambda x: oblur.blur(x, k).float(), lambda v: oblur.blur_adjoint(v, k).float(),
+                         vae.decode, vae.encode, y, init, lambda i: steps[i])
+    assert si.relative_error(out.cpu(), ref) < 1e-4
+
+
+def test_psld_requires_latent_network(cuda):
+    net = si.make_samplers_amd_net("linear", 3)
+    with pytest.raises(TypeError, match="latent diffusion model"):
+        PSLDSampler(net)
+
+
+@pytest.mark.parametrize("name", dps_case_names("rs"))
+def test_resample_matches_reference_golden(cuda, name):
+    from samplers_amd.noise import PoissonNoise
+    from samplers_amd.samplers.resample import ReSampleSampler
+    from test_oracle_latent import oracle_resample
+
+    case = load_dps_case(name)
+    m = case.meta
+    op = (IdentityOperator(case.shape) if case.kept is None
+          else InpaintingOperator(case.shape, case.mask).to(cuda))
+    noise = PoissonNoise(1.0) if m["noise"] == "poisson" else GaussianNoise(1e-3)
+    prob = InverseProblem(op, case.y.to(cuda), noise.to(cuda))
+    gen = torch.Generator().manual_seed(m["seed"])
+    drawn = []
+
+    def fn(kind, key, shape):  # the reference's sequential draw order
+        t = torch.randn(shape, generator=gen)
+        drawn.append(list(shape))
+        return t.to(cuda)
+
+    net = si.make_samplers_amd_latent_net("conv", 0.1, device=cuda)
+    out = ReSampleSampler(net)(prob, num_sampling_steps=m["N"], num_reconstructions=m["R"],
+                               max_optimization_iters=m["max_iters"], eta=m["eta"],
+                               inter_timesteps=m["inter_timesteps"],
+                               time_travel_interval=m["time_travel_interval"],
+                               stage_splits=m["stage_splits"], noise_fn=fn)
+    assert drawn == m["draw_shapes"]
+    assert tuple(out.shape) == tuple(m["out_shape"])
+    assert si.relative_error(out.cpu(), case.out) < _tol(case, oracle_resample)
+
+
+def test_adamw_step_matches_torch(cuda):
+    from samplers_amd import _hip
+    from samplers_amd.samplers.resample import adamw_coefficients
+
+    torch.manual_seed(0)
+    p0 = torch.randn(1003)
+    ref = p0.clone().requires_grad_()
+    opt = torch.optim.AdamW([ref], lr=5e-3)
+    p = p0.clone().to(cuda)
+    mm, vv = torch.zeros_like(p), torch.zeros_like(p)
+    lib = _hip.load_library()
+    for step in range(1, 6):
+        g = torch.randn(1003)
+        ref.grad = g.clone()
+        opt.step()
+        _hip.check(lib.sp_adamw_step(p.data_ptr(), g.to(cuda).data_ptr(), mm.data_ptr(),
+                                     vv.data_ptr(), p.numel(), adamw_coefficients(step, 5e-3),
+                                     torch.cuda.current_stream().cuda_stream), "adamw")
+    torch.testing.assert_close(p.cpu(), ref.detach(), rtol=1e-6, atol=1e-6)
+
+
+def test_resample_requires_latent_network(cuda):
+    from samplers_amd.samplers.resample import ReSampleSampler
+
+    with pytest.raises(TypeError, match="latent diffusion model"):
+        ReSampleSampler(si.make_samplers_amd_net("linear", 3))
