@@ -44,6 +44,13 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec, MI355X_MICROARCH.md
+
+# DPS workloads of BASELINE.json (configs[0..2]); inpaint is the headline metric's config
+CONFIGS = {
+    "inpaint": "DPS + InpaintingMask(50% random) + GaussianNoise(0.05) (BASELINE configs[1])",
+    "blur": "DPS + GaussianBlur(9x9, sigma=3) + GaussianNoise(0.05) (BASELINE configs[2])",
+    "identity": "DPS + IdentityOperator + GaussianNoise(0.05) (BASELINE configs[0] on the GPU)",
+}
 METRIC = "posterior samples/sec (batch×steps/s), DPS CelebA-HQ-256 @1/2/4/8 GPU"
 
 
@@ -54,6 +61,9 @@ def parse():
     p.add_argument("--warmup", type=int, default=2)
     p.add_argument("--batch", type=int, default=64, help="samples per GPU")
     p.add_argument("--image", type=int, default=256)
+    p.add_argument("--config", choices=sorted(CONFIGS), default="inpaint",
+                   help="DPS workload: inpaint = BASELINE configs[1] (headline), blur = configs[2] "
+                        "(64 per GPU of the 512 sharded over 8), identity = configs[0] on the GPU")
     p.add_argument("--micro-batch", type=int, default=0)
     p.add_argument("--recompute-v", action="store_true",
                    help="pass 2 re-derives v from y (gather) instead of re-reading pass 1's v")
@@ -80,31 +90,37 @@ def setup_dist(gpus: int):
     return rank, world, torch.device("cuda", local)
 
 
-def build_workload(batch: int, image: int, rank: int, device):
+def build_workload(config: str, batch: int, image: int, rank: int, device):
     from samplers_amd.inverse_problem import InverseProblem
     from samplers_amd.networks.ddpm import DDPMNetwork
     from samplers_amd.noise import GaussianNoise
-    from samplers_amd.operators import RandomInpaintingOperator
+    from samplers_amd.operators import (GaussianBlurOperator, IdentityOperator,
+                                        RandomInpaintingOperator)
 
     shape = (3, image, image)
-    op = RandomInpaintingOperator(shape, fraction=0.5, seed=1).to(device)
+    if config == "inpaint":
+        op = RandomInpaintingOperator(shape, fraction=0.5, seed=1).to(device)
+    elif config == "blur":
+        op = GaussianBlurOperator(shape, kernel_size=9, sigma=3.0).to(device)
+    else:
+        op = IdentityOperator(shape)
     noise = GaussianNoise(0.05).to(device)
     gen = torch.Generator().manual_seed(1000 + rank)  # per-rank shard of the synthetic dataset
     x_true = torch.rand((batch, *shape), generator=gen) * 2 - 1
-    y_clean = op.apply(x_true.to(device))  # HIP gather
+    y_clean = op.apply(x_true.to(device))  # HIP operator
     y = y_clean + (0.05 * torch.randn(tuple(y_clean.shape), generator=gen)).to(device)
     net = DDPMNetwork.from_config(seed=0, device=device, torch_dtype=torch.float32)
     net.set_sampling_parameters(1000, batch_size=batch)
     return InverseProblem(op, y, noise), net, shape
 
 
-def guidance_bytes(n: int, m: int, words: int) -> dict[str, float]:
+def guidance_bytes(n: int, m: int, index_bytes: int) -> dict[str, float]:
     """Algorithmic HBM bytes per sample (fp32): SURVEY.md §8d, 4(7n + 2m) + index."""
     return {
-        "dps_residual": 4.0 * (3 * n + m),  # read x, eps, y; write v
+        "dps_residual": 4.0 * (3 * n + m),  # read x, eps, y; write v (blur: halo re-reads excluded)
         "dps_update": 4.0 * (4 * n + m),    # read x, eps, w, y; write x'
         "dps_update_reuse_v": 4.0 * 5 * n,  # read x, eps, w, v; write x'
-        "index_per_launch": 12.0 * words,   # keep bits + word ranks, once per launch
+        "index_per_launch": float(index_bytes),  # inpaint keep bits + ranks / blur taps, per launch
     }
 
 
@@ -159,9 +175,10 @@ def main():
     from samplers_amd.samplers.dps import FusedDPSStep, KernelTimer
 
     _hip.load_library()
-    problem, net, shape = build_workload(args.batch, args.image, rank, device)
+    problem, net, shape = build_workload(args.config, args.batch, args.image, rank, device)
     n = int(np.prod(shape))
-    m = problem.operator.shape[0]
+    m = int(problem.operator.hip_descriptor().m)
+    index_bytes = 12 * ((n + 63) // 64) if args.config == "inpaint" else 0
     timer = KernelTimer()
     step = FusedDPSStep(net, problem, problem.observation, 1, gamma=1.0, eta=1.0,
                         micro_batch=args.micro_batch or None, timer=timer, reuse_v=not args.recompute_v)
@@ -201,7 +218,7 @@ def main():
         raise SystemExit("non-finite samples")
 
     kern = timer.summary()
-    nbytes = guidance_bytes(n, m, (n + 63) // 64)
+    nbytes = guidance_bytes(n, m, index_bytes)
     rl = {}
     for name in ("dps_residual", "dps_update"):
         d = kern[name]
@@ -214,7 +231,8 @@ def main():
     pmc = ROOT / "profiles" / "pmc_traffic.json"
     if pmc.exists():
         try:
-            rec = json.loads(pmc.read_text()).get(f"{dominant}@B{args.batch}_{args.image}")
+            tag = "" if args.config == "inpaint" else f"_{args.config}"
+            rec = json.loads(pmc.read_text()).get(f"{dominant}@B{args.batch}_{args.image}{tag}")
             traffic = rec["hbm_bytes_per_launch"] if rec else None
         except (ValueError, OSError):
             traffic = None
@@ -233,11 +251,10 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f32",
-        "data": "synthetic (seeded U(-1,1) images, 50% random mask, sigma=0.05 Gaussian noise; "
+        "data": "synthetic (seeded U(-1,1) images, sigma=0.05 Gaussian noise; "
                 "random-init ddpm-celebahq-256 UNet architecture)",
-        "config": {"workload": "DPS + InpaintingMask(50% random) + GaussianNoise(0.05), "
-                               f"3x{args.image}x{args.image}, ddpm-celebahq-256 prior, "
-                               "1000-step DDPM schedule (BASELINE configs[1])",
+        "config": {"workload": f"{CONFIGS[args.config]}, 3x{args.image}x{args.image}, "
+                               "ddpm-celebahq-256 prior, 1000-step DDPM schedule",
                    "global_batch": args.batch * world, "per_gpu_batch": args.batch,
                    "parallelism": f"sample-batch shards x{world}, no data-path collective"},
         "roofline": {

@@ -1,18 +1,26 @@
 // Depthwise separable Gaussian blur (BASELINE config 3) with reflect padding:
-//   A x  = conv_v(conv_h(reflect_pad(x)))   per channel plane, taps k[-R..R]
-//   A^T s = exact transpose: zero-extended correlation, then the padded halo
-//           folded back onto the reflected pixels (adjoint of reflect-pad).
-// The reference has no blur operator; the CPU oracle
-// (oracle/blur.py) pins these semantics with torch autograd of
-// F.pad(mode="reflect") + conv2d.
+//   A x   = conv_v(conv_h(reflect_pad(x)))   per channel plane, taps k[-R..R]
+//   A^T s = exact transpose of that map: a zero-extended correlation, then the
+//           padded halo folded back onto the pixels it was reflected from:
+//             U(p)  = sum_d k[d] s(p - d)                (s = 0 off the image)
+//             v(j)  = U(j) + [0 < j <= R] U(-j) + [N-1-R <= j < N-1] U(2N-2-j)
+//           applied per axis (vertical, then horizontal).
+// The reference has no blur operator; oracle/blur.py pins these
+// semantics with torch autograd of F.pad(mode="reflect") + conv2d.
 //
-// One workgroup owns a TH x TW output tile of one channel plane.  For the fused
-// DPS pass the tile needs x0 on T +- 2R (forward blur of the residual halo),
-// the residual s on T +- R and produces v on T: every intermediate lives in LDS
-// (two ping-pong buffers), HBM sees x, eps, y once plus the halo re-reads that
-// neighbouring tiles mostly serve from L2.
-
-#include <algorithm>
+// One workgroup owns a TH x TW output tile T of one channel plane.  The fused DPS
+// pass keeps every intermediate in LDS and register-blocks each stage so that LDS
+// traffic stays far below the HBM time of the pass:
+//   1  X  = x0 = (x - k eps)/a on T +- 2R (reflected)   x, eps from HBM, lane = column
+//   2  Hh = horizontal pass on T +- 2R rows, T +- R cols 4 adjacent outputs per thread
+//                                                       (ds_read_b128 of the 4+2R inputs)
+//   3  S  = c (y - vertical(Hh)) on T +- R, 0 off image column strips of 8 rows per
+//          + |r|^2 partial over T                       thread (sliding window), y from HBM
+//   4  V  = vertical adjoint of S (+ row fold) on T     column strips again
+//   5  v  = horizontal adjoint of V (+ column fold)     4-wide items, float4 stores to HBM
+// HBM traffic: x, eps, y, v once plus halo re-reads that neighbouring tiles serve
+// from the XCD's L2 (tiles are ordered so one XCD walks neighbouring tiles).
+// Taps live in SGPRs (uniform loads), not LDS.
 
 #include "sp_common.h"
 
@@ -20,6 +28,9 @@ namespace sp {
 
 constexpr int TH = 32;
 constexpr int TW = 64;
+constexpr int BX = 64;  // lanes per row in the load stage
+constexpr int BY = kBlock / BX;
+constexpr int STRIP = 8;  // rows per thread in the column stages
 
 __device__ __forceinline__ int reflect_clamp(int g, int L) {
     if (g < 0) g = -g;
@@ -27,192 +38,332 @@ __device__ __forceinline__ int reflect_clamp(int g, int L) {
     return g < 0 ? 0 : (g >= L ? L - 1 : g);
 }
 
+__host__ __device__ constexpr int round4(int v) { return (v + 3) & ~3; }
+
+typedef float f2v __attribute__((ext_vector_type(2)));
+
+// two FMAs in one v_pk_fma_f32 (scalar tap broadcast to both halves)
+__device__ __forceinline__ f2v pk_fma(float s, f2v a, f2v c) {
+    return __builtin_elementwise_fma(f2v{s, s}, a, c);
+}
+
 enum { MODE_APPLY = 0, MODE_ADJOINT = 1, MODE_DPS = 2 };
 
 template <int R>
-struct BlurLds {
-    static constexpr int XR = TH + 4 * R, XC = TW + 4 * R;  // x0 window (T +- 2R)
-    static constexpr int HR = TH + 4 * R, HC = TW + 2 * R;  // horizontal pass of it
-    static constexpr int SR = TH + 2 * R, SC = TW + 2 * R;  // residual window (T +- R)
-    static constexpr int UR = TH, UC = TW + 2 * R;          // vertical adjoint
-    static constexpr int A = (XR * XC > SR * SC) ? XR * XC : SR * SC;
-    static constexpr int B = (HR * HC > UR * UC) ? HR * HC : UR * UC;
+struct BlurGeom {
+    static constexpr int K = 2 * R + 1;
+    static constexpr int NB = (4 + 2 * R + 3) / 4;        // float4 reads per 4-wide item
+    static constexpr int WR = TH + 4 * R;                 // X / Hh rows (T +- 2R)
+    static constexpr int SR = TH + 2 * R;                 // S rows (T +- R)
+    static constexpr int HC = TW + 2 * R;                 // Hh / S / V columns (T +- R)
+    static constexpr int HCP = round4(HC);                // their row stride
+    static constexpr int XC = TW + 4 * R;                 // X columns (T +- 2R)
+    static constexpr int XCP = round4(HCP - 4 + 4 * NB > XC ? HCP - 4 + 4 * NB : XC);
+    static constexpr int LDS_A = WR * XCP;                // X, later S
+    static constexpr int LDS_B = WR * HCP;                // Hh, later V
 };
 
-// Vertical adjoint for rows of T, columns [C0-R, C0+TW+R): U = A_v^T S.
+// dst[r][q..q+3] = sum_d k[d] src[r][q + R + d] for 4-wide items over rows x cols4*4.
 template <int R>
-__device__ __forceinline__ void vertical_adjoint(const float* S, float* U, const float* tk, int R0,
-                                                 int C0, int H, int W) {
-    using L = BlurLds<R>;
-    for (int idx = threadIdx.x; idx < L::UR * L::UC; idx += kBlock) {
-        const int i = idx / L::UC, q = idx % L::UC;
-        const int gi = R0 + i, gj = C0 - R + q;
-        float acc = 0.f;
-        if (gi < H && gj >= 0 && gj < W) {
-            // S row index of global row g: g - (R0 - R)
-            const bool lo = gi > 0 && gi <= R;
-            const bool hi = gi < H - 1 && gi >= H - 1 - R;
+__device__ __forceinline__ void hpass(const float* src, int sstride, float* dst, int dstride,
+                                      int rows, int cols4, const float (&tk)[2 * R + 1]) {
+    using G = BlurGeom<R>;
+    for (int it = threadIdx.x; it < rows * cols4; it += kBlock) {
+        const int r = it / cols4, q = (it - r * cols4) * 4;
+        float w[4 * G::NB];
+        const float4* s4 = reinterpret_cast<const float4*>(src + r * sstride + q);
 #pragma unroll
-            for (int d = -R; d <= R; ++d) {
-                const float kd = tk[d + R];
-                float s = 0.f;
-                int g = gi - d;
-                if (g >= 0 && g < H) s += S[(g - R0 + R) * L::SC + q];
-                if (lo) {
-                    g = -gi - d;
-                    if (g >= 0) s += S[(g - R0 + R) * L::SC + q];
-                }
-                if (hi) {
-                    g = 2 * H - 2 - gi - d;
-                    if (g < H) s += S[(g - R0 + R) * L::SC + q];
-                }
-                acc += kd * s;
-            }
+        for (int j = 0; j < G::NB; ++j) {
+            const float4 t = s4[j];
+            w[4 * j] = t.x, w[4 * j + 1] = t.y, w[4 * j + 2] = t.z, w[4 * j + 3] = t.w;
         }
-        U[i * L::UC + q] = acc;
+        float o[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            float acc = 0.f;
+#pragma unroll
+            for (int d = 0; d < G::K; ++d) acc = fmaf(tk[d], w[e + d], acc);
+            o[e] = acc;
+        }
+        *reinterpret_cast<float4*>(dst + r * dstride + q) = make_float4(o[0], o[1], o[2], o[3]);
     }
 }
 
-// Horizontal adjoint for the output tile: out = A_h^T U (rows of T).
+// Vertical adjoint on T rows: V[i][q] = U(R0+i) + folds, with S on T +- R rows
+// (S row of global row g is g - R0 + R; rows outside S are zero / off the image).
+// Fold terms exist only in tiles within R rows of the top/bottom edge (a uniform
+// branch); there U(-g) = sum_{i=0}^{R-g} k[-g-i] S(i) and
+// U(2H-2-g) = sum_{i=2H-2-g-R}^{H-1} k[2H-2-g-i] S(i).
 template <int R>
-__device__ __forceinline__ void horizontal_adjoint_store(const float* U, const float* tk, int R0,
-                                                         int C0, int H, int W,
-                                                         float* __restrict__ plane_out) {
-    using L = BlurLds<R>;
-    for (int idx = threadIdx.x; idx < TH * TW; idx += kBlock) {
-        const int i = idx / TW, j = idx % TW;
-        const int gi = R0 + i, gj = C0 + j;
-        if (gi >= H || gj >= W) continue;
-        const bool lo = gj > 0 && gj <= R;
-        const bool hi = gj < W - 1 && gj >= W - 1 - R;
-        float acc = 0.f;
+__device__ __forceinline__ void vadjoint(const float* S, float* V, int R0, int H,
+                                         const float (&tk)[2 * R + 1], const float* tkl) {
+    using G = BlurGeom<R>;
+    constexpr int NS = TH / STRIP, HP = G::HC / 2;  // items: 8-row strips x column pairs
+    const bool rfold = R0 <= R || R0 + TH >= H - 1 - R;
+    for (int it = threadIdx.x; it < NS * HP; it += kBlock) {
+        const int s = it / HP, q = 2 * (it - s * HP);
+        const int i0 = s * STRIP;
+        f2v w[STRIP + 2 * R];
 #pragma unroll
-        for (int d = -R; d <= R; ++d) {
-            const float kd = tk[d + R];
-            float u = 0.f;
-            int g = gj - d;
-            if (g >= 0 && g < W) u += U[i * L::UC + (g - C0 + R)];
-            if (lo) {
-                g = -gj - d;
-                if (g >= 0) u += U[i * L::UC + (g - C0 + R)];
-            }
-            if (hi) {
-                g = 2 * W - 2 - gj - d;
-                if (g < W) u += U[i * L::UC + (g - C0 + R)];
-            }
-            acc += kd * u;
+        for (int j = 0; j < STRIP + 2 * R; ++j) w[j] = *reinterpret_cast<const f2v*>(S + (i0 + j) * G::HCP + q);
+        f2v u[STRIP];
+#pragma unroll
+        for (int e = 0; e < STRIP; ++e) {
+            // U(g) = sum_d k[d] S(g - d): S rows i0+e+R-d  ->  w[e + 2R - (d+R)]
+            f2v acc = {0.f, 0.f};
+#pragma unroll
+            for (int d = 0; d < G::K; ++d) acc = pk_fma(tk[d], w[e + 2 * R - d], acc);
+            u[e] = acc;
         }
-        plane_out[(int64_t)gi * W + gj] = acc;
+        if (rfold) {
+#pragma unroll
+            for (int e = 0; e < STRIP; ++e) {
+                const int gi = R0 + i0 + e;
+                if (gi > 0 && gi <= R)
+                    for (int i = 0; i <= R - gi; ++i)
+                        u[e] = pk_fma(tkl[R - gi - i],
+                                      *reinterpret_cast<const f2v*>(S + (i - R0 + R) * G::HCP + q), u[e]);
+                if (gi < H - 1 && gi >= H - 1 - R)
+                    for (int i = 2 * H - 2 - gi - R; i < H; ++i)
+                        u[e] = pk_fma(tkl[R + 2 * H - 2 - gi - i],
+                                      *reinterpret_cast<const f2v*>(S + (i - R0 + R) * G::HCP + q), u[e]);
+            }
+        }
+#pragma unroll
+        for (int e = 0; e < STRIP; ++e) *reinterpret_cast<f2v*>(V + (i0 + e) * G::HCP + q) = u[e];
+    }
+}
+
+// out[T] = horizontal adjoint of V (+ column folds in edge tiles); 4-wide items,
+// float4 stores.
+template <int R>
+__device__ __forceinline__ void hadjoint_store(const float* V, int R0, int C0, int H, int W,
+                                               const float (&tk)[2 * R + 1], const float* tkl,
+                                               float* __restrict__ plane_out) {
+    using G = BlurGeom<R>;
+    constexpr int C4 = TW / 4;
+    const bool cfold = C0 <= R || C0 + TW >= W - 1 - R;
+    const bool vec = (W & 3) == 0 && (reinterpret_cast<uintptr_t>(plane_out) & 15) == 0;
+    for (int it = threadIdx.x; it < TH * C4; it += kBlock) {
+        const int i = it / C4, j0 = (it - i * C4) * 4;
+        const int gi = R0 + i;
+        if (gi >= H) continue;
+        const float* row = V + i * G::HCP;
+        float w[4 * G::NB];
+        const float4* s4 = reinterpret_cast<const float4*>(row + j0);
+#pragma unroll
+        for (int j = 0; j < G::NB; ++j) {
+            const float4 t = s4[j];
+            w[4 * j] = t.x, w[4 * j + 1] = t.y, w[4 * j + 2] = t.z, w[4 * j + 3] = t.w;
+        }
+        float o[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            float u = 0.f;
+#pragma unroll
+            for (int d = 0; d < G::K; ++d) u = fmaf(tk[d], w[e + 2 * R - d], u);
+            o[e] = u;
+        }
+        if (cfold) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int gj = C0 + j0 + e;
+                if (gj > 0 && gj <= R)
+                    for (int c = 0; c <= R - gj; ++c)
+                        o[e] = fmaf(tkl[R - gj - c], row[c - C0 + R], o[e]);
+                if (gj < W - 1 && gj >= W - 1 - R)
+                    for (int c = 2 * W - 2 - gj - R; c < W; ++c)
+                        o[e] = fmaf(tkl[R + 2 * W - 2 - gj - c], row[c - C0 + R], o[e]);
+            }
+        }
+        float* dst = plane_out + (unsigned)(gi * W + C0 + j0);
+        if (vec && C0 + j0 + 4 <= W) {
+            *reinterpret_cast<float4*>(dst) = make_float4(o[0], o[1], o[2], o[3]);
+        } else {
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+                if (C0 + j0 + e < W) dst[e] = o[e];
+        }
     }
 }
 
 template <int R, int MODE>
 __global__ __launch_bounds__(kBlock) void k_blur(sp_op op, const float* __restrict__ in,
                                                  const float* __restrict__ eps,
-                                                 const float* __restrict__ y, int64_t y_div,
+                                                 const float* __restrict__ y, int y_div,
                                                  float a, float k, float gs,
                                                  float* __restrict__ out,
                                                  float* __restrict__ partial, int P) {
-    using L = BlurLds<R>;
-    __shared__ float bufA[L::A];
-    __shared__ float bufB[L::B];
-    __shared__ float tk[2 * R + 1];
+    using G = BlurGeom<R>;
+    __shared__ __attribute__((aligned(16))) float bufA[G::LDS_A];
+    __shared__ __attribute__((aligned(16))) float bufB[G::LDS_B];
     __shared__ float red[4];
+    __shared__ float tkl[2 * R + 1];  // taps for the (lane-indexed) fold terms
 
     const int H = op.height, W = op.width, C = op.channels;
     const int tilesW = (W + TW - 1) / TW;
-    const int R0 = (blockIdx.x / tilesW) * TH, C0 = (blockIdx.x % tilesW) * TW;
-    const int c = blockIdx.y;
-    const int64_t b = blockIdx.z;
+    const int tiles = tilesW * ((H + TH - 1) / TH);
+    // XCD-aware order: dispatch deals blocks round-robin over the 8 XCDs, so give each
+    // XCD a contiguous run of tiles (neighbours share halos through that XCD's L2).
+    const unsigned nblk = gridDim.x;
+    const unsigned q8 = nblk / 8, r8 = nblk % 8, xcd = blockIdx.x % 8, loc = blockIdx.x / 8;
+    const unsigned lin = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + loc;
+    const unsigned pl = lin / tiles;  // plane index b*C + c
+    const int tile = static_cast<int>(lin - pl * tiles);
+    const int c = static_cast<int>(pl % C);
+    const unsigned b = pl / C;
+    const int R0 = (tile / tilesW) * TH, C0 = (tile % tilesW) * TW;
     const int64_t plane = (int64_t)H * W;
-    const int64_t xoff = (b * C + c) * plane;
+    const int64_t xoff = (int64_t)pl * plane;
+    // uniform plane bases; per-element offsets are 32-bit (plane < 2^31 elements)
+    const float* __restrict__ xp = in + xoff;
+    const int tx = threadIdx.x % BX, ty = threadIdx.x / BX;
 
-    if (threadIdx.x < 2 * R + 1) tk[threadIdx.x] = op.taps[threadIdx.x];
+    float tk[2 * R + 1];  // uniform -> scalar loads
+#pragma unroll
+    for (int d = 0; d < 2 * R + 1; ++d) tk[d] = op.taps[d];
+    if (threadIdx.x < 2 * R + 1) tkl[threadIdx.x] = op.taps[threadIdx.x];
 
-    if constexpr (MODE == MODE_ADJOINT) {
-        // S = input s on T +- R, zero outside the image
-        float* S = bufA;
-        for (int idx = threadIdx.x; idx < L::SR * L::SC; idx += kBlock) {
-            const int p = idx / L::SC, q = idx % L::SC;
-            const int gi = R0 - R + p, gj = C0 - R + q;
-            S[idx] = (gi >= 0 && gi < H && gj >= 0 && gj < W) ? in[xoff + (int64_t)gi * W + gj] : 0.f;
-        }
-        __syncthreads();
-        vertical_adjoint<R>(S, bufB, tk, R0, C0, H, W);
-        __syncthreads();
-        horizontal_adjoint_store<R>(bufB, tk, R0, C0, H, W, out + xoff);
-        return;
-    } else if constexpr (MODE == MODE_APPLY) {
-        // X = x on T +- R (reflected), Hz = horizontal pass on rows T +- R, out = vertical pass on T
-        constexpr int XR = TH + 2 * R, XC = TW + 2 * R;
+    if constexpr (MODE == MODE_APPLY) {
+        // X = x on T +- R (reflected); Hh = horizontal pass on those rows; out = vertical
         float* X = bufA;
-        float* Hz = bufB;
-        for (int idx = threadIdx.x; idx < XR * XC; idx += kBlock) {
-            const int p = idx / XC, q = idx % XC;
-            const int gi = reflect_clamp(R0 - R + p, H), gj = reflect_clamp(C0 - R + q, W);
-            X[idx] = in[xoff + (int64_t)gi * W + gj];
+        float* Hh = bufB;
+        constexpr int XR = TH + 2 * R, XW = TW + 2 * R;
+        for (int r = ty; r < XR; r += BY) {
+            const unsigned gro = (unsigned)reflect_clamp(R0 - R + r, H) * W;
+            for (int q = tx; q < XW; q += BX) X[r * G::XCP + q] = xp[gro + reflect_clamp(C0 - R + q, W)];
         }
         __syncthreads();
-        for (int idx = threadIdx.x; idx < XR * TW; idx += kBlock) {
-            const int p = idx / TW, q = idx % TW;
-            float acc = 0.f;
-#pragma unroll
-            for (int d = -R; d <= R; ++d) acc += tk[d + R] * X[p * XC + q + R + d];
-            Hz[idx] = acc;
-        }
+        hpass<R>(X, G::XCP, Hh, G::HCP, XR, TW / 4, tk);
         __syncthreads();
-        for (int idx = threadIdx.x; idx < TH * TW; idx += kBlock) {
-            const int i = idx / TW, j = idx % TW;
-            const int gi = R0 + i, gj = C0 + j;
-            if (gi >= H || gj >= W) continue;
-            float acc = 0.f;
+        constexpr int NS = TH / STRIP;
+        for (int it = threadIdx.x; it < NS * TW; it += kBlock) {
+            const int s = it / TW, q = it - s * TW;
+            const int i0 = s * STRIP;
+            if (C0 + q >= W) continue;
+            float w[STRIP + 2 * R];
 #pragma unroll
-            for (int d = -R; d <= R; ++d) acc += tk[d + R] * Hz[(i + R + d) * TW + j];
-            out[xoff + (int64_t)gi * W + gj] = acc;
+            for (int j = 0; j < STRIP + 2 * R; ++j) w[j] = Hh[(i0 + j) * G::HCP + q];
+#pragma unroll
+            for (int e = 0; e < STRIP; ++e) {
+                const int gi = R0 + i0 + e;
+                if (gi >= H) break;
+                float acc = 0.f;
+#pragma unroll
+                for (int d = 0; d < G::K; ++d) acc = fmaf(tk[d], w[e + d], acc);
+                (out + xoff)[(unsigned)(gi * W + C0 + q)] = acc;
+            }
         }
         return;
     } else {
-        // fused DPS residual pass
-        const int64_t yoff = ((b / y_div) * C + c) * plane;
-        float* X = bufA;
-        float* Hz = bufB;
-        for (int idx = threadIdx.x; idx < L::XR * L::XC; idx += kBlock) {
-            const int p = idx / L::XC, q = idx % L::XC;
-            const int gi = reflect_clamp(R0 - 2 * R + p, H), gj = reflect_clamp(C0 - 2 * R + q, W);
-            const int64_t o = xoff + (int64_t)gi * W + gj;
-            X[idx] = (in[o] - k * eps[o]) / a;
-        }
-        __syncthreads();
-        for (int idx = threadIdx.x; idx < L::HR * L::HC; idx += kBlock) {
-            const int p = idx / L::HC, q = idx % L::HC;
-            float acc = 0.f;
-#pragma unroll
-            for (int d = -R; d <= R; ++d) acc += tk[d + R] * X[p * L::XC + q + R + d];
-            Hz[idx] = acc;
-        }
-        __syncthreads();
-        float* S = bufA;  // X is dead
+        float* S = bufA;  // T +- R rows x HC cols, stride HCP
         float racc = 0.f;
-        for (int idx = threadIdx.x; idx < L::SR * L::SC; idx += kBlock) {
-            const int p = idx / L::SC, q = idx % L::SC;
-            const int gi = R0 - R + p, gj = C0 - R + q;
-            float sv = 0.f;
-            if (gi >= 0 && gi < H && gj >= 0 && gj < W) {
-                float z = 0.f;
-#pragma unroll
-                for (int d = -R; d <= R; ++d) z += tk[d + R] * Hz[(p + R + d) * L::HC + q];
-                const float r = y[yoff + (int64_t)gi * W + gj] - z;
-                sv = gs * r;
-                if (p >= R && p < R + TH && q >= R && q < R + TW) racc += r * r;
+        if constexpr (MODE == MODE_ADJOINT) {
+            for (int r = ty; r < G::SR; r += BY) {
+                const int gi = R0 - R + r;
+                for (int q = tx; q < G::HC; q += BX) {
+                    const int gj = C0 - R + q;
+                    const bool ok = gi >= 0 && gi < H && gj >= 0 && gj < W;
+                    S[r * G::HCP + q] = ok ? xp[(unsigned)(gi * W + gj)] : 0.f;
+                }
             }
-            S[idx] = sv;
+            __syncthreads();
+        } else {
+            // ---- fused DPS residual pass ----
+            const float* __restrict__ yp = y + ((int64_t)(b / (unsigned)y_div) * C + c) * plane;
+            const float* __restrict__ ep = eps + xoff;
+            float* X = bufA;
+            float* Hh = bufB;
+            const float inv_a = 1.f / a;  // x0 to 1 ulp of the division K2 uses
+            static_assert(G::WR % BY == 0 && G::XC > BX && G::XC <= 2 * BX, "window layout");
+            constexpr int NI = G::WR / BY;
+            // Stage 1 loads: column tx for every window row, then column tx + 64 (a
+            // duplicate, unused load on lanes past the window).  Rows are wave-uniform,
+            // so the reflected row offset is a scalar (buffer-load soffset) and each
+            // lane's reflected column a fixed voffset: no per-load vector address math.
+            const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+            const int nbytes = static_cast<int>(plane * 4);
+            const auto xr = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(xp), (short)0, nbytes, 0x00020000);
+            const auto er = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(ep), (short)0, nbytes, 0x00020000);
+            const int vo0 = 4 * reflect_clamp(C0 - 2 * R + tx, W);
+            const int vo1 = 4 * reflect_clamp(C0 - 2 * R + tx + BX, W);
+            const bool has1 = tx < G::XC - BX;
+            float xv[NI][2], ev[NI][2];
+#pragma unroll
+            for (int it = 0; it < NI; ++it) {
+                const int so = 4 * W * reflect_clamp(R0 - 2 * R + wv + BY * it, H);
+                xv[it][0] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, vo0, so, 0));
+                ev[it][0] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(er, vo0, so, 0));
+                xv[it][1] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, vo1, so, 0));
+                ev[it][1] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(er, vo1, so, 0));
+            }
+            // observation for this thread's stage-3 items (strip x column pair), prefetched
+            // behind the window; addresses clamped into the image (off-image entries unused)
+            constexpr bool EXACT3 = G::SR % STRIP == 0;
+            constexpr int NS3 = (G::SR + STRIP - 1) / STRIP, HP = G::HC / 2;
+            constexpr int NIT3 = (NS3 * HP + kBlock - 1) / kBlock;
+            f2v yv[NIT3][STRIP];
+#pragma unroll
+            for (int u = 0; u < NIT3; ++u) {
+                const int it = min((int)threadIdx.x + u * kBlock, NS3 * HP - 1);
+                const int s = it / HP, q = 2 * (it - s * HP);
+                const int gj0 = min(max(C0 - R + q, 0), W - 1), gj1 = min(max(C0 - R + q + 1, 0), W - 1);
+#pragma unroll
+                for (int e = 0; e < STRIP; ++e) {
+                    const unsigned ro = (unsigned)min(max(R0 - R + s * STRIP + e, 0), H - 1) * W;
+                    yv[u][e] = f2v{yp[ro + gj0], yp[ro + gj1]};
+                }
+            }
+#pragma unroll
+            for (int it = 0; it < NI; ++it) {
+                const int r = wv + BY * it;
+                X[r * G::XCP + tx] = (xv[it][0] - k * ev[it][0]) * inv_a;
+                if (has1) X[r * G::XCP + tx + BX] = (xv[it][1] - k * ev[it][1]) * inv_a;
+            }
+            __syncthreads();
+            hpass<R>(X, G::XCP, Hh, G::HCP, G::WR, G::HCP / 4, tk);
+            __syncthreads();  // X is dead: S reuses bufA
+#pragma unroll
+            for (int u = 0; u < NIT3; ++u) {
+                const int it = threadIdx.x + u * kBlock;
+                if (it >= NS3 * HP) break;
+                const int s = it / HP, q = 2 * (it - s * HP);
+                const int i0 = s * STRIP;
+                const int gj = C0 - R + q;
+                const bool cin0 = gj >= 0 && gj < W, cin1 = gj + 1 >= 0 && gj + 1 < W;
+                const bool cT0 = q >= R && q < R + TW, cT1 = q + 1 >= R && q + 1 < R + TW;
+                f2v w[STRIP + 2 * R];
+#pragma unroll
+                for (int j = 0; j < STRIP + 2 * R; ++j)
+                    w[j] = (EXACT3 || i0 + j < G::WR) ? *reinterpret_cast<const f2v*>(Hh + (i0 + j) * G::HCP + q)
+                                                     : f2v{0.f, 0.f};
+#pragma unroll
+                for (int e = 0; e < STRIP; ++e) {
+                    const int i = i0 + e;
+                    if (!EXACT3 && i >= G::SR) break;
+                    const int gi = R0 - R + i;
+                    f2v z = {0.f, 0.f};
+#pragma unroll
+                    for (int d = 0; d < G::K; ++d) z = pk_fma(tk[d], w[e + d], z);
+                    const f2v rr = yv[u][e] - z;
+                    const bool rok = (unsigned)gi < (unsigned)H, rT = rok && i >= R && i < R + TH;
+                    const f2v sv = rr * gs;
+                    *reinterpret_cast<f2v*>(S + i * G::HCP + q) =
+                        f2v{(rok && cin0) ? sv.x : 0.f, (rok && cin1) ? sv.y : 0.f};
+                    racc += (rT && cT0 && cin0) ? rr.x * rr.x : 0.f;
+                    racc += (rT && cT1 && cin1) ? rr.y * rr.y : 0.f;
+                }
+            }
+            __syncthreads();  // Hh is dead: V reuses bufB
         }
-        __syncthreads();
-        vertical_adjoint<R>(S, bufB, tk, R0, C0, H, W);  // Hz is dead
-        const float t = block_sum(racc, red);            // contains a barrier
-        if (threadIdx.x == 0) partial[b * P + (int64_t)c * gridDim.x + blockIdx.x] = t;
-        __syncthreads();
-        horizontal_adjoint_store<R>(bufB, tk, R0, C0, H, W, out + xoff);
+        vadjoint<R>(S, bufB, R0, H, tk, tkl);
+        if constexpr (MODE == MODE_DPS) {
+            const float t = block_sum(racc, red);  // contains the barrier V needs
+            if (threadIdx.x == 0) partial[(int64_t)b * P + c * tiles + tile] = t;
+        } else {
+            __syncthreads();
+        }
+        hadjoint_store<R>(bufB, R0, C0, H, W, tk, tkl, out + xoff);
     }
 }
 
@@ -225,14 +376,20 @@ template <int MODE>
 static int launch_blur(const sp_op* op, const float* in, const float* eps, const float* y,
                        int64_t y_div, float a, float k, float gs, float* out, float* partial,
                        int64_t batch, hipStream_t s) {
-    const int tiles = ((op->height + TH - 1) / TH) * ((op->width + TW - 1) / TW);
-    const dim3 grid(tiles, op->channels, static_cast<unsigned>(batch));
+    const int64_t tiles = (int64_t)((op->height + TH - 1) / TH) * ((op->width + TW - 1) / TW);
+    const int64_t blocks = tiles * op->channels * batch;
+    // the kernel decodes blocks and in-plane offsets in 32 bits
+    if (blocks >= (int64_t(1) << 31) || (int64_t)op->height * op->width >= (int64_t(1) << 31) ||
+        y_div < 1 || y_div > batch)
+        return SP_EINVAL;
+    if (blocks == 0) return SP_OK;
+    const dim3 grid(static_cast<unsigned>(blocks));
     const int P = static_cast<int>(blur_partials(op));
     switch (op->radius) {
-#define SP_BLUR_CASE(RR)                                                                       \
-    case RR:                                                                                   \
+#define SP_BLUR_CASE(RR)                                                                        \
+    case RR:                                                                                    \
         launch(MODE == MODE_DPS ? TK_DPS_RESIDUAL : 0, k_blur<RR, MODE>, grid, dim3(kBlock), s, \
-               *op, in, eps, y, y_div, a, k, gs, out, partial, P);                               \
+               *op, in, eps, y, static_cast<int>(y_div), a, k, gs, out, partial, P);                              \
         break;
         SP_BLUR_CASE(1) SP_BLUR_CASE(2) SP_BLUR_CASE(3) SP_BLUR_CASE(4)
         SP_BLUR_CASE(5) SP_BLUR_CASE(6) SP_BLUR_CASE(7) SP_BLUR_CASE(8)

@@ -2,6 +2,8 @@
 
     SAMPLERS_HIP_LIB=build/variants/lib_k8.so python tools/bench_kernels.py [label]
 
+OPS=blur,inpaint restricts the operators; FLUSH=0 times warm-cache launches.
+
 Prints one JSON line per (operator, kernel): mean microseconds over 50 launches
 (HIP events on the launch stream) and algorithmic GB/s.
 """
@@ -29,8 +31,10 @@ def timeit(fn, reps=30):
     for _ in range(3):
         fn()
     total = 0.0
+    flush = os.environ.get("FLUSH", "1") == "1"
     for _ in range(reps):
-        _FLUSH.zero_()
+        if flush:
+            _FLUSH.zero_()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
         fn()
@@ -56,7 +60,10 @@ def main():
     ops = {"identity": IdentityOperator(shape),
            "inpaint": RandomInpaintingOperator(shape, 0.5, seed=1).to(dev),
            "blur": GaussianBlurOperator(shape, 9, 3.0).to(dev)}
+    only = os.environ.get("OPS")
     for name, op in ops.items():
+        if only and name not in only.split(","):
+            continue
         desc = op.hip_descriptor()
         m = int(desc.m)
         x, eps, w = (torch.randn(B, n, device=dev) for _ in range(3))
