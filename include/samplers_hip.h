@@ -195,6 +195,26 @@ int sp_stochastic_resample(const float* pseudo_x0, const float* x_t, int64_t bat
 int sp_adamw_step(float* param, const float* grad, float* exp_avg, float* exp_avg_sq,
                   int64_t count, const sp_adamw_coefs* c, sp_stream_t stream);
 
+/* ---- prior building blocks (SURVEY.md §8b "groupnorm_silu_fwd/bwd") -------------------
+ * GroupNorm over NCHW x (n, channels, hw = H*W) with `groups` groups, eps, optional
+ * per-(sample, channel) bias added to x first (chan_bias [n, channels] or NULL: the UNet's
+ * time-embedding add), optional affine (gamma/beta [channels] or NULL) and, if act != 0,
+ * SiLU on the output.  Replaces torch GroupNorm + SiLU inside diffusers' ResnetBlock2D /
+ * Attention / conv_norm_out (called from ddpm.py:40-43 and stable_diffusion.py:330-345).
+ * work: sp_groupnorm_workspace() floats.  mean/rstd [n*groups] are written by the
+ * forward and read by the backward, which returns the input VJP dx (= the VJP w.r.t.
+ * chan_bias after a sum over H*W). */
+int64_t sp_groupnorm_workspace(int64_t n, int32_t channels, int64_t hw, int32_t groups);
+int sp_groupnorm_silu_fwd(const float* x, const float* chan_bias, const float* gamma,
+                          const float* beta, int64_t n, int32_t channels, int64_t hw,
+                          int32_t groups, float eps, int32_t act, float* z, float* mean,
+                          float* rstd, float* work, sp_stream_t stream);
+int sp_groupnorm_silu_bwd(const float* dz, const float* x, const float* chan_bias,
+                          const float* gamma, const float* beta, const float* mean,
+                          const float* rstd, int64_t n, int32_t channels, int64_t hw,
+                          int32_t groups, int32_t act, float* dx, float* work,
+                          sp_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

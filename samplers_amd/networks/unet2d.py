@@ -26,6 +26,8 @@ import torch
 import torch.nn.functional as F
 from torch import Tensor, nn
 
+from .layers import GroupNormAct
+
 
 @dataclass(frozen=True)
 class UNet2DConfig:
@@ -73,18 +75,18 @@ class ResnetBlock2D(nn.Module):
 
     def __init__(self, cin: int, cout: int, temb: int | None, groups: int, eps: float) -> None:
         super().__init__()
-        self.norm1 = nn.GroupNorm(groups, cin, eps=eps)
+        self.norm1 = GroupNormAct(groups, cin, eps=eps, act=True)
         self.conv1 = nn.Conv2d(cin, cout, 3, padding=1)
         self.time_emb_proj = nn.Linear(temb, cout) if temb else None
-        self.norm2 = nn.GroupNorm(groups, cout, eps=eps)
+        self.norm2 = GroupNormAct(groups, cout, eps=eps, act=True)
         self.conv2 = nn.Conv2d(cout, cout, 3, padding=1)
         self.conv_shortcut = nn.Conv2d(cin, cout, 1) if cin != cout else None
 
     def forward(self, x: Tensor, temb: Tensor | None = None) -> Tensor:
-        h = self.conv1(F.silu(self.norm1(x)))
-        if self.time_emb_proj is not None:
-            h = h + self.time_emb_proj(F.silu(temb))[:, :, None, None]
-        h = self.conv2(F.silu(self.norm2(h)))
+        h = self.conv1(self.norm1(x))  # silu(norm1(x)), fused
+        # silu(norm2(h + temb_proj)): the time-embedding add rides in the fused norm
+        tb = self.time_emb_proj(F.silu(temb)) if self.time_emb_proj is not None else None
+        h = self.conv2(self.norm2(h, tb))
         if self.conv_shortcut is not None:
             x = self.conv_shortcut(x)
         return x + h
@@ -96,7 +98,7 @@ class SpatialSelfAttention(nn.Module):
     def __init__(self, channels: int, groups: int, eps: float, head_dim: int | None) -> None:
         super().__init__()
         self.heads = 1 if head_dim is None else channels // head_dim
-        self.group_norm = nn.GroupNorm(groups, channels, eps=eps)
+        self.group_norm = GroupNormAct(groups, channels, eps=eps)
         self.to_q = nn.Linear(channels, channels)
         self.to_k = nn.Linear(channels, channels)
         self.to_v = nn.Linear(channels, channels)
@@ -187,7 +189,7 @@ class UNet2DModel(nn.Module):
             self.up_blocks.append(lvl)
             prev = c
 
-        self.conv_norm_out = nn.GroupNorm(g, ch[0], eps=eps)
+        self.conv_norm_out = GroupNormAct(g, ch[0], eps=eps, act=True)
         self.conv_out = nn.Conv2d(ch[0], config.out_channels, 3, padding=1)
 
     def forward(self, sample: Tensor, timestep: Tensor | int) -> Tensor:
@@ -226,7 +228,7 @@ class UNet2DModel(nn.Module):
             if lvl.upsamplers is not None:
                 h = lvl.upsamplers[0](h)
 
-        return self.conv_out(F.silu(self.conv_norm_out(h)))
+        return self.conv_out(self.conv_norm_out(h))
 
 
 def build_unet(config: UNet2DConfig = CELEBAHQ_256, *, seed: int = 0, device=None,

@@ -19,6 +19,7 @@ import torch
 import torch.nn.functional as F
 from torch import Tensor, nn
 
+from .layers import GroupNormAct
 from .unet2d import Downsample2D, ResnetBlock2D, SpatialSelfAttention, Upsample2D
 
 
@@ -68,7 +69,7 @@ class Encoder(nn.Module):
             blk.downsamplers = nn.ModuleList([Downsample2D(cout)]) if i < len(ch) - 1 else None
             self.down_blocks.append(blk)
         self.mid_block = _Mid(ch[-1], g, eps)
-        self.conv_norm_out = nn.GroupNorm(g, ch[-1], eps=eps)
+        self.conv_norm_out = GroupNormAct(g, ch[-1], eps=eps, act=True)
         self.conv_out = nn.Conv2d(ch[-1], 2 * c.latent_channels, 3, padding=1)
 
     def forward(self, x: Tensor) -> Tensor:
@@ -79,7 +80,7 @@ class Encoder(nn.Module):
             if blk.downsamplers is not None:
                 h = blk.downsamplers[0](h)
         h = self.mid_block(h)
-        return self.conv_out(F.silu(self.conv_norm_out(h)))
+        return self.conv_out(self.conv_norm_out(h))
 
 
 class Decoder(nn.Module):
@@ -98,7 +99,7 @@ class Decoder(nn.Module):
             blk.upsamplers = nn.ModuleList([Upsample2D(co)]) if i < len(rev) - 1 else None
             self.up_blocks.append(blk)
             prev = co
-        self.conv_norm_out = nn.GroupNorm(g, ch[0], eps=eps)
+        self.conv_norm_out = GroupNormAct(g, ch[0], eps=eps, act=True)
         self.conv_out = nn.Conv2d(ch[0], c.out_channels, 3, padding=1)
 
     def forward(self, z: Tensor) -> Tensor:
@@ -108,7 +109,7 @@ class Decoder(nn.Module):
                 h = res(h)
             if blk.upsamplers is not None:
                 h = blk.upsamplers[0](h)
-        return self.conv_out(F.silu(self.conv_norm_out(h)))
+        return self.conv_out(self.conv_norm_out(h))
 
 
 class AutoencoderKL(nn.Module):
