@@ -1,0 +1,119 @@
+"""PSLD benchmark (BASELINE.json configs[3], "config 4"): latent-space inpainting at 512².
+
+    python tools/bench_psld.py [--batch 32 --steps 3 --warmup 1]
+
+Workload: PSLD (psld.py:118-153) with a centre-inpainting mask on 3x512x512 images,
+GaussianNoise(0.05), SD 1.5 VAE architecture (83.65 M parameters) + 4x64x64 latent
+UNet, random weights with fixed seeds, fp32, 100-step schedule (psld.py:50).  One
+step = one PSLD iteration over the batch: latent UNet forward, VAE decode forward,
+HIP pixel pass, VAE encode forward, encode/decode/UNet VJPs, HIP glue and update
+(samplers_amd.samplers.psld.FusedPSLDStep).  Prints one JSON line; "vae_tflops" is
+the algorithmic VAE work (7.13 TFLOP per sample-step) over the step
+time, an upper bound on what the VAE convolutions achieve.
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import sys
+import threading
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT))
+import samplers_amd  # noqa: E402,F401
+
+import torch  # noqa: E402
+
+VAE_FLOP_PER_SAMPLE = 7.13e12
+
+
+def heartbeat(path: Path, every: float = 30.0) -> None:
+    def beat():
+        while True:
+            time.sleep(every)
+            with open(path, "a") as f:
+                f.write(f"{time.time():.0f}\n")
+
+    threading.Thread(target=beat, daemon=True).start()
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("--batch", type=int, default=32)
+    p.add_argument("--image", type=int, default=512)
+    p.add_argument("--steps", type=int, default=3)
+    p.add_argument("--warmup", type=int, default=1)
+    p.add_argument("--heartbeat", default="gpurun_out/psld_heartbeat.log")
+    args = p.parse_args()
+    Path(args.heartbeat).parent.mkdir(parents=True, exist_ok=True)
+    heartbeat(Path(args.heartbeat))
+    torch.backends.cudnn.benchmark = False
+    dev = torch.device("cuda:0")
+
+    from samplers_amd import _hip
+    from samplers_amd.inverse_problem import InverseProblem
+    from samplers_amd.networks.latent import LatentDiffusionNetwork
+    from samplers_amd.noise import GaussianNoise
+    from samplers_amd.operators import CenterInpaintingOperator
+    from samplers_amd.samplers.dps import initial_sample
+    from samplers_amd.samplers.psld import FusedPSLDStep
+
+    _hip.load_library()
+    shape = (3, args.image, args.image)
+    op = CenterInpaintingOperator(shape, 0.5).to(dev)
+    gen = torch.Generator().manual_seed(1000)
+    x_true = (torch.rand((args.batch, *shape), generator=gen) * 2 - 1).to(dev)
+    y = op.apply(x_true)
+    y = y + (0.05 * torch.randn(tuple(y.shape), generator=gen)).to(dev)
+    net = LatentDiffusionNetwork.from_config(seed=0, device=dev)
+    net.set_sampling_parameters(100, batch_size=args.batch)
+    problem = InverseProblem(op, y, GaussianNoise(0.05).to(dev))
+    lat = tuple(net.get_latent_shape(shape))
+    step = FusedPSLDStep(net, problem, y.reshape(args.batch, -1), 1, lat)
+    seed = 20260101
+    z = initial_sample((args.batch, *lat), dev, rng="philox", seed=seed, sample_offset=0,
+                       noise_fn=None)
+    ts = net.timesteps_host
+    it = iter(range(len(ts) - 1, 1, -1))
+
+    def one():
+        i = next(it)
+        step(z, i, ts[i], ts[i - 1], ts[0], seed=seed)
+
+    t0 = time.perf_counter()
+    for k in range(args.warmup):
+        one()
+        torch.cuda.synchronize()
+        print(f"[psld] warmup {k + 1} done at {time.perf_counter() - t0:.1f}s", file=sys.stderr,
+              flush=True)
+    torch.cuda.reset_peak_memory_stats()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        one()
+        torch.cuda.synchronize()
+        print(f"[psld] step {k + 1} at {time.perf_counter() - t0:.1f}s", file=sys.stderr, flush=True)
+    dt = time.perf_counter() - t0
+    if not torch.isfinite(z).all():
+        raise SystemExit("non-finite latents")
+    ms = dt / args.steps * 1e3
+    print(json.dumps({
+        "metric": "posterior samples/sec (batch×steps/s), PSLD SD1.5 512² (BASELINE configs[3])",
+        "value": round(args.batch * args.steps / dt, 4),
+        "unit": "samples/sec (batch×steps/s)",
+        "n_gpus": 1, "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 2),
+        "higher_is_better": True, "dtype": "f32",
+        "data": "synthetic (seeded U(-1,1) images, centre mask, sigma=0.05); random-init SD1.5 "
+                "VAE architecture + 4x64x64 latent UNet",
+        "config": {"workload": f"PSLD + CenterInpainting(0.5) + GaussianNoise(0.05), 3x{args.image}²",
+                   "batch": args.batch, "schedule": "100-step PNDM (psld.py:50)"},
+        "vae_tflops": round(VAE_FLOP_PER_SAMPLE * args.batch / (ms / 1e3) / 1e12, 2),
+        "peak_gib": round(torch.cuda.max_memory_allocated() / 2**30, 1),
+    }), flush=True)
+
+
+if __name__ == "__main__":
+    main()
