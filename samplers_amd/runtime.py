@@ -49,9 +49,21 @@ def configure_miopen() -> Path | None:
     try:
         cache.mkdir(parents=True, exist_ok=True)
         for src in SEED_DB.glob("*.ufdb.txt"):
-            dst = cache / src.name
-            if not dst.exists():
-                shutil.copyfile(src, dst)
+            _merge_find_db(src, cache / src.name)
     except OSError:
         pass
     return cache
+
+
+def _merge_find_db(src: Path, dst: Path) -> None:
+    """Add the seed's entries (one ``key=solver:time,...`` line per convolution) that
+    ``dst`` lacks; entries MIOpen already measured on this machine are kept."""
+    if not dst.exists():
+        shutil.copyfile(src, dst)
+        return
+    have = {line.split("=", 1)[0] for line in dst.read_text().splitlines() if "=" in line}
+    extra = [line for line in src.read_text().splitlines()
+             if "=" in line and line.split("=", 1)[0] not in have]
+    if extra:
+        with open(dst, "a") as f:
+            f.write("\n".join(extra) + "\n")
