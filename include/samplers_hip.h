@@ -215,6 +215,21 @@ int sp_groupnorm_silu_bwd(const float* dz, const float* x, const float* chan_bia
                           int32_t groups, int32_t act, float* dx, float* work,
                           sp_stream_t stream);
 
+/* 3x3 / stride 1 / pad 1 convolution on fp32 MFMA (SURVEY.md §8b "vae_conv3x3_fwd/bwd_input",
+ * §8f f1): the ResnetBlock / mid / up-sampling convolutions of the SD VAE and DDPM UNet
+ * (diffusers Conv2d(k=3, p=1), reached from stable_diffusion.py:330-345, ddpm.py:40-43).
+ * Weights are packed once per layer (sp_conv3x3_pack; input_vjp=1 packs the transposed,
+ * flipped weights of the input VJP); NCHW fp32 activations.  Shapes: see _supported. */
+int sp_conv3x3_supported(int32_t cin, int32_t cout, int32_t height, int32_t width);
+int64_t sp_conv3x3_packed_size(int32_t cin, int32_t cout);
+int sp_conv3x3_pack(const float* w, int32_t cout, int32_t cin, int32_t input_vjp, float* wp,
+                    sp_stream_t stream);
+int sp_conv3x3_fwd(const float* x, const float* wp, const float* bias, int64_t n, int32_t cin,
+                   int32_t cout, int32_t height, int32_t width, float* y, sp_stream_t stream);
+int sp_conv3x3_bwd_input(const float* dy, const float* wp_vjp, int64_t n, int32_t cin,
+                         int32_t cout, int32_t height, int32_t width, float* dx,
+                         sp_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -108,3 +108,90 @@ class GroupNormAct(nn.GroupNorm):
 
     def extra_repr(self) -> str:
         return super().extra_repr() + f", act={'silu' if self.act else 'none'}"
+
+
+# ---------------------------------------------------------------------------------------
+# 3x3 convolution on fp32 MFMA
+# ---------------------------------------------------------------------------------------
+
+def conv_backend() -> str:
+    """``SAMPLERS_AMD_CONV``: ``hip`` (default: the MFMA kernel wherever its shape rules
+    hold, MIOpen elsewhere) or ``miopen`` (always torch/MIOpen)."""
+    import os
+
+    return os.environ.get("SAMPLERS_AMD_CONV", "hip").lower()
+
+
+class _Conv3x3Fn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias, wp, wp_vjp):
+        lib = _hip.load_library()
+        n, cin, h, w = x.shape
+        cout = weight.shape[0]
+        x = x.contiguous()
+        y = torch.empty(n, cout, h, w, device=x.device, dtype=torch.float32)
+        _hip.check(lib.sp_conv3x3_fwd(_hip.ptr(x), _hip.ptr(wp), _hip.ptr(bias), n, cin, cout, h, w,
+                                      _hip.ptr(y), _hip.stream_of(x)), "sp_conv3x3_fwd")
+        ctx.save_for_backward(x, weight, wp_vjp)
+        ctx.has_bias = bias is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, weight, wp_vjp = ctx.saved_tensors
+        n, cin, h, w = x.shape
+        cout = weight.shape[0]
+        dy = dy.contiguous()
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            lib = _hip.load_library()
+            if lib.sp_conv3x3_supported(cout, cin, h, w):
+                dx = torch.empty_like(x)
+                _hip.check(lib.sp_conv3x3_bwd_input(_hip.ptr(dy), _hip.ptr(wp_vjp), n, cin, cout, h,
+                                                    w, _hip.ptr(dx), _hip.stream_of(dy)),
+                           "sp_conv3x3_bwd_input")
+            else:  # input VJP shape outside the tile rules (cin % 128): MIOpen
+                dx = torch.nn.grad.conv2d_input(x.shape, weight, dy, padding=1)
+        if ctx.needs_input_grad[1]:
+            dw = torch.nn.grad.conv2d_weight(x, weight.shape, dy, padding=1)
+        if ctx.has_bias and ctx.needs_input_grad[2]:
+            db = dy.sum(dim=(0, 2, 3))
+        return dx, dw, db, None, None
+
+
+class Conv3x3(nn.Conv2d):
+    """``nn.Conv2d(cin, cout, 3, padding=1)`` whose device forward / input VJP run the
+    fp32-MFMA kernel of ``csrc/sp_conv.hip`` where its shape rules hold (cin % 4,
+    cout % 128, H % 4, W % 32) and MIOpen elsewhere.  Packed weights are cached and
+    rebuilt when the parameter changes."""
+
+    def __init__(self, cin: int, cout: int) -> None:
+        super().__init__(cin, cout, 3, padding=1)
+        self._packs = None
+        self._pack_key = None
+
+    def _packed(self):
+        w = self.weight
+        key = (w.data_ptr(), w._version, w.device)
+        if self._pack_key != key:
+            lib = _hip.load_library()
+            cout, cin = w.shape[0], w.shape[1]
+            wc = w.detach().contiguous()
+            wp = torch.empty(int(lib.sp_conv3x3_packed_size(cin, cout)), device=w.device)
+            _hip.check(lib.sp_conv3x3_pack(_hip.ptr(wc), cout, cin, 0, _hip.ptr(wp),
+                                           _hip.stream_of(wc)), "sp_conv3x3_pack")
+            wv = None
+            if cout % 4 == 0:
+                wv = torch.empty_like(wp)
+                _hip.check(lib.sp_conv3x3_pack(_hip.ptr(wc), cout, cin, 1, _hip.ptr(wv),
+                                               _hip.stream_of(wc)), "sp_conv3x3_pack")
+            self._packs, self._pack_key = (wp, wv), key
+        return self._packs
+
+    def forward(self, x: Tensor) -> Tensor:
+        if (x.is_cuda and x.dtype == torch.float32 and x.dim() == 4 and conv_backend() == "hip"
+                and _hip.load_library().sp_conv3x3_supported(x.shape[1], self.out_channels,
+                                                             x.shape[2], x.shape[3])):
+            wp, wv = self._packed()
+            return _Conv3x3Fn.apply(x, self.weight, self.bias, wp, wv)
+        return super().forward(x)

@@ -26,7 +26,7 @@ import torch
 import torch.nn.functional as F
 from torch import Tensor, nn
 
-from .layers import GroupNormAct
+from .layers import Conv3x3, GroupNormAct
 
 
 @dataclass(frozen=True)
@@ -76,10 +76,10 @@ class ResnetBlock2D(nn.Module):
     def __init__(self, cin: int, cout: int, temb: int | None, groups: int, eps: float) -> None:
         super().__init__()
         self.norm1 = GroupNormAct(groups, cin, eps=eps, act=True)
-        self.conv1 = nn.Conv2d(cin, cout, 3, padding=1)
+        self.conv1 = Conv3x3(cin, cout)
         self.time_emb_proj = nn.Linear(temb, cout) if temb else None
         self.norm2 = GroupNormAct(groups, cout, eps=eps, act=True)
-        self.conv2 = nn.Conv2d(cout, cout, 3, padding=1)
+        self.conv2 = Conv3x3(cout, cout)
         self.conv_shortcut = nn.Conv2d(cin, cout, 1) if cin != cout else None
 
     def forward(self, x: Tensor, temb: Tensor | None = None) -> Tensor:
@@ -129,7 +129,7 @@ class Downsample2D(nn.Module):
 class Upsample2D(nn.Module):
     def __init__(self, channels: int) -> None:
         super().__init__()
-        self.conv = nn.Conv2d(channels, channels, 3, padding=1)
+        self.conv = Conv3x3(channels, channels)
 
     def forward(self, x: Tensor) -> Tensor:
         return self.conv(F.interpolate(x, scale_factor=2.0, mode="nearest"))
