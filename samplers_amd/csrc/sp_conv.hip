@@ -5,26 +5,42 @@
 // and ddpm.py:40-43).  Input VJP = the same kernel on transposed + flipped weights.
 //
 // Implicit GEMM: out[n, co, p] = sum_{ci, r, s} W[co, ci, r, s] * x[n, ci, p + (r-1, s-1)]
-//   M = Cout (128 per workgroup), N = pixels (4 rows x 32 columns of one image per
+//   M = Cout (128 per workgroup), N = pixels (8 rows x 32 columns of one image per
 //   workgroup), K = Cin*9 walked in chunks of 4 input channels (36 k).
 // Per chunk the workgroup stages in LDS
 //   A: packed weights [36 k][128 co]          (host-packed once per layer: row k of a
 //                                              chunk = 128 contiguous co, float4 loads)
-//   P: input patch    [4 ci][6 rows][34 cols] (zero outside the image = the padding)
-// and each wave (2 x 2 tiles of 32 x 32: 64 co x 2 pixel rows) issues 72 MFMAs.  Lane
+//   P: input patch    [4 ci][10 rows][34 cols] (zero outside the image = the padding)
+// and each wave (2 x 4 tiles of 32 x 32: 64 co x 4 pixel rows) issues 144 MFMAs.  Lane
 // half h of an MFMA carries k-index kk + 18h, i.e. the same (r, s) and input channel
 // ci + 2h, so every LDS address is a per-lane base + a compile-time offset.  Chunks are
 // double-buffered: the next chunk's global loads are in flight during the MFMAs.
+// Measured on MI355X (tools/bench_conv.py): 136-137.5 TFLOP/s = 0.87 of the 157.3 TF
+// fp32-MFMA peak on the UNet/VAE layer shapes (MIOpen: 104-130); 4x8 / 8x4 / 8x8 /
+// 2x8 (channels x rows) tiles measured 133 / 114-121 / 126-129 / 132-136.
 
 #include "sp_common.h"
 
 namespace sp {
 
-constexpr int CV_M = 128;   // output channels per workgroup
-constexpr int CV_TPH = 4;   // pixel rows per workgroup
-constexpr int CV_TPW = 32;  // pixel columns per workgroup
-constexpr int CV_CI = 4;    // input channels per K chunk
+#ifndef SP_CONV_CI
+#define SP_CONV_CI 4
+#endif
+#ifndef SP_CONV_TPH
+#define SP_CONV_TPH 8
+#endif
+#ifndef SP_CONV_MINB
+#define SP_CONV_MINB 2
+#endif
+
+constexpr int CV_M = 128;            // output channels per workgroup
+constexpr int CV_TPH = SP_CONV_TPH;  // pixel rows per workgroup (each wave: TPH/2 rows)
+constexpr int CV_TPW = 32;           // pixel columns per workgroup
+constexpr int CV_CI = SP_CONV_CI;    // input channels per K chunk (even)
 constexpr int CV_K = CV_CI * 9;
+constexpr int CV_KH = CV_K / 2;      // k-steps per chunk: lane half h takes k = kk + KH*h
+constexpr int CV_NR = CV_TPH / 2;    // MFMA pixel tiles (rows) per wave
+static_assert(CV_CI % 2 == 0 && CV_TPH % 2 == 0, "conv tile");
 constexpr int CV_PW = CV_TPW + 2;
 constexpr int CV_PH = CV_TPH + 2;
 constexpr int CV_PATCH = CV_PH * CV_PW;                    // 204
@@ -74,7 +90,7 @@ __device__ __forceinline__ void cv_store(float* As, float* Ps, int tid, const f3
     }
 }
 
-__global__ __launch_bounds__(kBlock, 2) void k_conv3x3(const float* __restrict__ x,
+__global__ __launch_bounds__(kBlock, SP_CONV_MINB) void k_conv3x3(const float* __restrict__ x,
                                                        const float* __restrict__ wp,
                                                        const float* __restrict__ bias,
                                                        float* __restrict__ out, int cin,
@@ -89,16 +105,16 @@ __global__ __launch_bounds__(kBlock, 2) void k_conv3x3(const float* __restrict__
     const int64_t plane = (int64_t)H * W;
     const float* __restrict__ xn = x + (int64_t)n * cin * plane;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, hh = lane >> 5, l = lane & 31;
-    const int m_w = (wv & 1) * 64, prow = (wv >> 1) * 2;
+    const int m_w = (wv & 1) * 64, prow = (wv >> 1) * CV_NR;
     const int nchunks = cin / CV_CI;
 
     f32x4 ra[CV_NA];
     float rp[CV_NP];
-    f32x16 acc[2][2];
+    f32x16 acc[2][CV_NR];
 #pragma unroll
     for (int a = 0; a < 2; ++a)
 #pragma unroll
-        for (int b = 0; b < 2; ++b) acc[a][b] = f32x16{};
+        for (int b = 0; b < CV_NR; ++b) acc[a][b] = f32x16{};
 
     cv_load(wp, xn, 0, cout, co0, h0, w0, H, W, plane, tid, ra, rp);
     cv_store(As[0], Ps[0], tid, ra, rp);
@@ -106,17 +122,20 @@ __global__ __launch_bounds__(kBlock, 2) void k_conv3x3(const float* __restrict__
     for (int cc = 0; cc < nchunks; ++cc) {
         const int buf = cc & 1;
         if (cc + 1 < nchunks) cv_load(wp, xn, cc + 1, cout, co0, h0, w0, H, W, plane, tid, ra, rp);
-        const float* Ab = &As[buf][(18 * hh) * CV_M + m_w + l];
-        const float* Pb = &Ps[buf][(2 * hh) * CV_PATCH + prow * CV_PW + l];
+        const float* Ab = &As[buf][(CV_KH * hh) * CV_M + m_w + l];
+        const float* Pb = &Ps[buf][(CV_CI / 2 * hh) * CV_PATCH + prow * CV_PW + l];
 #pragma unroll
-        for (int kk = 0; kk < 18; ++kk) {
+        for (int kk = 0; kk < CV_KH; ++kk) {
             const int koff = (kk / 9) * CV_PATCH + ((kk % 9) / 3) * CV_PW + (kk % 3);
             const float a0 = Ab[kk * CV_M], a1 = Ab[kk * CV_M + 32];
-            const float b0 = Pb[koff], b1 = Pb[koff + CV_PW];
-            acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b0, acc[0][0], 0, 0, 0);
-            acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b1, acc[0][1], 0, 0, 0);
-            acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b0, acc[1][0], 0, 0, 0);
-            acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc[1][1], 0, 0, 0);
+            float b[CV_NR];
+#pragma unroll
+            for (int ni = 0; ni < CV_NR; ++ni) b[ni] = Pb[koff + ni * CV_PW];
+#pragma unroll
+            for (int ni = 0; ni < CV_NR; ++ni) {
+                acc[0][ni] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b[ni], acc[0][ni], 0, 0, 0);
+                acc[1][ni] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b[ni], acc[1][ni], 0, 0, 0);
+            }
         }
         if (cc + 1 < nchunks) cv_store(As[buf ^ 1], Ps[buf ^ 1], tid, ra, rp);
         __syncthreads();
@@ -131,7 +150,7 @@ __global__ __launch_bounds__(kBlock, 2) void k_conv3x3(const float* __restrict__
             const int co = co0 + m_w + mi * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
             const float bv = bias ? bias[co] : 0.f;
 #pragma unroll
-            for (int ni = 0; ni < 2; ++ni)
+            for (int ni = 0; ni < CV_NR; ++ni)
                 on[(int64_t)co * plane + (h0 + prow + ni) * W + w0 + l] = acc[mi][ni][r] + bv;
         }
     }

@@ -162,7 +162,7 @@ class _Conv3x3Fn(torch.autograd.Function):
 class Conv3x3(nn.Conv2d):
     """``nn.Conv2d(cin, cout, 3, padding=1)`` whose device forward / input VJP run the
     fp32-MFMA kernel of ``csrc/sp_conv.hip`` where its shape rules hold (cin % 4,
-    cout % 128, H % 4, W % 32) and MIOpen elsewhere.  Packed weights are cached and
+    cout % 128, H % 8, W % 32) and MIOpen elsewhere.  Packed weights are cached and
     rebuilt when the parameter changes."""
 
     def __init__(self, cin: int, cout: int) -> None:

@@ -18,7 +18,7 @@ SHAPES = [  # n, cin, cout, h, w
     (1, 4, 512, 8, 32),      # VAE decoder conv_in (forward only on the tile; VJP on MIOpen)
     (2, 384, 128, 16, 32),   # UNet up-block concat input
     (1, 256, 256, 64, 64),
-    (3, 132, 256, 4, 96),
+    (3, 132, 256, 8, 96),
 ]
 
 
@@ -72,6 +72,7 @@ def test_conv3x3_rejects_unsupported(cuda):
     assert not lib.sp_conv3x3_supported(3, 128, 32, 32)
     assert not lib.sp_conv3x3_supported(128, 64, 32, 32)
     assert not lib.sp_conv3x3_supported(128, 128, 16, 16)
+    assert not lib.sp_conv3x3_supported(128, 128, 4, 32)
     conv = Conv3x3(128, 128).to(cuda)  # falls back to MIOpen at 16x16
     x = torch.randn(1, 128, 16, 16, device=cuda)
     torch.testing.assert_close(conv(x), F.conv2d(x, conv.weight, conv.bias, padding=1))
