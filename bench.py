@@ -18,9 +18,15 @@ sharded over ranks with no data-path collective (DPS samples are independent,
 SURVEY.md F6); Philox noise is keyed by the global sample index.
 
 Also reported:
-  roofline      dominant HIP guidance kernel: algorithmic bytes per launch /
-                mean launch time from HIP events on the launch stream, against
-                the 8 TB/s HBM peak; traffic = PMC-measured HBM bytes per launch
+  roofline      the dominant HIP kernel of the step.  Since the prior's 3x3
+                convolutions run on this project's fp32-MFMA tile it is that
+                kernel: algorithmic FLOPs (2*9*N*Cin*Cout*H*W per launch, fwd and
+                input VJP) / its launch times from HIP events attached to the
+                dispatch packets on the launch stream, against the 157.3 TFLOP/s
+                dense fp32 MFMA peak
+  guidance_roofline  the dominant guidance pass (pass 1 / pass 2): algorithmic
+                bytes per launch / mean launch time, against the
+                8 TB/s HBM peak; traffic = PMC-measured HBM bytes per launch
                 (profiles/pmc_traffic.json, separate rocprofv3 --pmc passes)
   cpu_baseline  oracle/dps_loop.py (torch-CPU restatement of dps.py) with the
                 same UNet, timed on this host's cores for a bounded sample
@@ -44,6 +50,7 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec, MI355X_MICROARCH.md
+MFMA_F32_PEAK_TFLOPS = 157.3  # dense fp32 MFMA (v_mfma_f32_32x32x2_f32), MI355X_MICROARCH.md
 
 # DPS workloads of BASELINE.json (configs[0..2]); inpaint is the headline metric's config
 CONFIGS = {
@@ -122,6 +129,25 @@ def guidance_bytes(n: int, m: int, index_bytes: int) -> dict[str, float]:
         "dps_update_reuse_v": 4.0 * 5 * n,  # read x, eps, w, v; write x'
         "index_per_launch": float(index_bytes),  # inpaint keep bits + ranks / blur taps, per launch
     }
+
+
+def load_pmc() -> dict:
+    """PMC-measured HBM bytes per launch (profiles/pmc_traffic.json), keyed kernel@config."""
+    pmc = ROOT / "profiles" / "pmc_traffic.json"
+    try:
+        return json.loads(pmc.read_text()) if pmc.exists() else {}
+    except (ValueError, OSError):
+        return {}
+
+
+def conv_summary(kern: dict) -> dict | None:
+    """Both directions of the fp32-MFMA convolution tile (one kernel): count, ms, FLOPs."""
+    parts = [kern[k] for k in ("conv3x3_fwd", "conv3x3_bwd_input") if k in kern]
+    if not parts:
+        return None
+    out = {k: sum(p[k] for p in parts) for k in ("count", "ms", "flops")}
+    out["tflops"] = out["flops"] / out["ms"] / 1e9
+    return out
 
 
 def cpu_baseline(image: int, seconds: float) -> dict:
@@ -226,16 +252,33 @@ def main():
         key = "dps_update_reuse_v" if (name == "dps_update" and step.needs_v) else name
         per_launch = nbytes[key] * d["samples"] / d["count"] + nbytes["index_per_launch"]
         rl[name] = {"avg_ms": avg_ms, "bytes": per_launch, "gbs": per_launch / avg_ms / 1e6}
-    dominant = max(rl, key=lambda k: rl[k]["avg_ms"])
-    traffic = None
-    pmc = ROOT / "profiles" / "pmc_traffic.json"
-    if pmc.exists():
-        try:
-            tag = "" if args.config == "inpaint" else f"_{args.config}"
-            rec = json.loads(pmc.read_text()).get(f"{dominant}@B{args.batch}_{args.image}{tag}")
-            traffic = rec["hbm_bytes_per_launch"] if rec else None
-        except (ValueError, OSError):
-            traffic = None
+    g_dom = max(rl, key=lambda k: rl[k]["avg_ms"])
+    pmc = load_pmc()
+    tag = "" if args.config == "inpaint" else f"_{args.config}"
+    g_rec = pmc.get(f"{g_dom}@B{args.batch}_{args.image}{tag}")
+    guidance_roofline = {
+        "kernel": g_dom, "bound": "hbm", "achieved": round(rl[g_dom]["gbs"], 1),
+        "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(rl[g_dom]["gbs"] / HBM_PEAK_GBS, 4),
+        "traffic": g_rec["hbm_bytes_per_launch"] if g_rec else None,
+        "algorithmic_bytes_per_launch": rl[g_dom]["bytes"],
+        "avg_launch_ms": round(rl[g_dom]["avg_ms"], 5),
+    }
+    conv = conv_summary(kern)
+    if conv and conv["ms"] > sum(rl[k]["avg_ms"] * kern[k]["count"] for k in rl):
+        # the prior's fp32-MFMA convolution tile dominates the step
+        c_rec = pmc.get(f"conv3x3@B{args.batch}_{args.image}")
+        roofline = {
+            "kernel": "conv3x3 (sp_conv3x3_fwd + sp_conv3x3_bwd_input)", "bound": "mfma",
+            "achieved": round(conv["tflops"], 2), "peak": MFMA_F32_PEAK_TFLOPS, "unit": "TFLOP/s",
+            "frac": round(conv["tflops"] / MFMA_F32_PEAK_TFLOPS, 4),
+            "traffic": c_rec["hbm_bytes_per_launch"] if c_rec else None,
+            "algorithmic_flops_per_launch": conv["flops"] / conv["count"],
+            "avg_launch_ms": round(conv["ms"] / conv["count"], 4),
+            "launches_per_step": conv["count"] / args.steps,
+            "share_of_step": round(conv["ms"] / (elapsed * 1e3), 4),
+        }
+    else:
+        roofline = guidance_roofline
 
     total = args.batch * world * args.steps
     value = total / elapsed
@@ -257,17 +300,8 @@ def main():
                                "ddpm-celebahq-256 prior, 1000-step DDPM schedule",
                    "global_batch": args.batch * world, "per_gpu_batch": args.batch,
                    "parallelism": f"sample-batch shards x{world}, no data-path collective"},
-        "roofline": {
-            "kernel": dominant,
-            "bound": "hbm",
-            "achieved": round(rl[dominant]["gbs"], 1),
-            "peak": HBM_PEAK_GBS,
-            "unit": "GB/s",
-            "frac": round(rl[dominant]["gbs"] / HBM_PEAK_GBS, 4),
-            "traffic": traffic,
-            "algorithmic_bytes_per_launch": rl[dominant]["bytes"],
-            "avg_launch_ms": round(rl[dominant]["avg_ms"], 5),
-        },
+        "roofline": roofline,
+        "guidance_roofline": guidance_roofline,
         "guidance_kernels": {k: {"avg_ms": round(v["avg_ms"], 5), "GB/s": round(v["gbs"], 1)}
                              for k, v in rl.items()},
     }

@@ -103,6 +103,9 @@ typedef struct sp_adamw_coefs {
  * pass — clears the log and returns the number written. */
 int sp_timing_enable(int on);
 int sp_timing_collect(int32_t* kinds, float* ms, int max_records);
+/* As sp_timing_collect, plus each launch's algorithmic work: samples for kinds 1-2 (DPS
+ * passes), FLOPs for kinds 3-4 (sp_conv3x3_fwd / _bwd_input). */
+int sp_timing_collect_work(int32_t* kinds, float* ms, double* work, int max_records);
 
 /* Library / ABI version (major*10000 + minor*100 + patch). */
 int sp_version(void);

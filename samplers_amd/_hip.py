@@ -74,6 +74,9 @@ SIGNATURES = {
     "sp_timing_enable": (ctypes.c_int, [ctypes.c_int]),
     "sp_timing_collect": (ctypes.c_int, [ctypes.POINTER(ctypes.c_int32),
                                          ctypes.POINTER(ctypes.c_float), ctypes.c_int]),
+    "sp_timing_collect_work": (ctypes.c_int, [ctypes.POINTER(ctypes.c_int32),
+                                              ctypes.POINTER(ctypes.c_float),
+                                              ctypes.POINTER(ctypes.c_double), ctypes.c_int]),
     "sp_last_error": (ctypes.c_char_p, []),
     "sp_rsq_partials": (_I64, [_OPP]),
     "sp_vec_partials": (_I64, [_I64]),

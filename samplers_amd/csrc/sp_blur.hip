@@ -388,7 +388,7 @@ static int launch_blur(const sp_op* op, const float* in, const float* eps, const
     switch (op->radius) {
 #define SP_BLUR_CASE(RR)                                                                        \
     case RR:                                                                                    \
-        launch(MODE == MODE_DPS ? TK_DPS_RESIDUAL : 0, k_blur<RR, MODE>, grid, dim3(kBlock), s, \
+        launch_w(MODE == MODE_DPS ? TK_DPS_RESIDUAL : 0, (double)batch, k_blur<RR, MODE>, grid, dim3(kBlock), s, \
                *op, in, eps, y, static_cast<int>(y_div), a, k, gs, out, partial, P);                              \
         break;
         SP_BLUR_CASE(1) SP_BLUR_CASE(2) SP_BLUR_CASE(3) SP_BLUR_CASE(4)

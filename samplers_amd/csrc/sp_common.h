@@ -165,16 +165,24 @@ int check_launch(const char* what);
 // Kernel timing (sp_timing_enable): the start/stop events of a timed launch are
 // attached to its dispatch packet (hipExtLaunchKernel), so they bracket the
 // kernel alone — the same interval rocprofv3's kernel trace reports.
+// Each record carries the launch's algorithmic work (samples for the DPS passes,
+// FLOPs for the convolution tile) for sp_timing_collect_work.
 bool timing_on();
-void timing_events(int kind, hipEvent_t* start, hipEvent_t* stop);
+void timing_events(int kind, double work, hipEvent_t* start, hipEvent_t* stop);
 
-enum { TK_DPS_RESIDUAL = 1, TK_DPS_UPDATE = 2 };
+enum { TK_DPS_RESIDUAL = 1, TK_DPS_UPDATE = 2, TK_CONV3X3_FWD = 3, TK_CONV3X3_BWD_INPUT = 4 };
+
+template <typename K, typename... Args>
+inline void launch_w(int kind, double work, K kernel, dim3 grid, dim3 block, hipStream_t s,
+                     Args... args) {
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    if (kind && timing_on()) timing_events(kind, work, &e0, &e1);
+    hipExtLaunchKernelGGL(kernel, grid, block, 0, s, e0, e1, 0, args...);
+}
 
 template <typename K, typename... Args>
 inline void launch(int kind, K kernel, dim3 grid, dim3 block, hipStream_t s, Args... args) {
-    hipEvent_t e0 = nullptr, e1 = nullptr;
-    if (kind && timing_on()) timing_events(kind, &e0, &e1);
-    hipExtLaunchKernelGGL(kernel, grid, block, 0, s, e0, e1, 0, args...);
+    launch_w(kind, 0.0, kernel, grid, block, s, args...);
 }
 
 }  // namespace sp

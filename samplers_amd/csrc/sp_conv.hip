@@ -200,31 +200,34 @@ int sp_conv3x3_pack(const float* w, int32_t cout, int32_t cin, int32_t input_vjp
     return check_launch("sp_conv3x3_pack");
 }
 
-static int conv3x3(const float* x, const float* wp, const float* bias, int64_t n, int32_t cin,
-                   int32_t cout, int32_t height, int32_t width, float* y, sp_stream_t stream,
-                   const char* what) {
+static int conv3x3(int kind, const float* x, const float* wp, const float* bias, int64_t n,
+                   int32_t cin, int32_t cout, int32_t height, int32_t width, float* y,
+                   sp_stream_t stream, const char* what) {
     if (!sp_conv3x3_supported(cin, cout, height, width) || n < 0) return SP_EINVAL;
     if (n == 0) return SP_OK;
     if (!x || !wp || !y) return SP_EINVAL;
     const int64_t tiles = n * (height / CV_TPH) * (width / CV_TPW);
     if (tiles >= (int64_t(1) << 31) || (int64_t)cin * height * width >= (int64_t(1) << 31))
         return SP_EINVAL;
-    launch(0, k_conv3x3, dim3(static_cast<unsigned>(tiles), cout / CV_M), dim3(kBlock),
-           static_cast<hipStream_t>(stream), x, wp, bias, y, cin, cout, height, width);
+    const double flops = 18.0 * n * cin * cout * height * width;  // 2 * 9 MACs per tap
+    launch_w(kind, flops, k_conv3x3, dim3(static_cast<unsigned>(tiles), cout / CV_M),
+             dim3(kBlock), static_cast<hipStream_t>(stream), x, wp, bias, y, cin, cout, height,
+             width);
     return check_launch(what);
 }
 
 int sp_conv3x3_fwd(const float* x, const float* wp, const float* bias, int64_t n, int32_t cin,
                    int32_t cout, int32_t height, int32_t width, float* y, sp_stream_t stream) {
-    return conv3x3(x, wp, bias, n, cin, cout, height, width, y, stream, "sp_conv3x3_fwd");
+    return conv3x3(TK_CONV3X3_FWD, x, wp, bias, n, cin, cout, height, width, y, stream,
+                   "sp_conv3x3_fwd");
 }
 
 int sp_conv3x3_bwd_input(const float* dy, const float* wp_vjp, int64_t n, int32_t cin,
                          int32_t cout, int32_t height, int32_t width, float* dx,
                          sp_stream_t stream) {
     // dx (n, cin, h, w) = conv3x3(dy (n, cout, h, w), W') with W' packed by input_vjp=1
-    return conv3x3(dy, wp_vjp, nullptr, n, cout, cin, height, width, dx, stream,
-                   "sp_conv3x3_bwd_input");
+    return conv3x3(TK_CONV3X3_BWD_INPUT, dy, wp_vjp, nullptr, n, cout, cin, height, width, dx,
+                   stream, "sp_conv3x3_bwd_input");
 }
 
 }  // extern "C"

@@ -36,6 +36,7 @@ int check_launch(const char* what) {
 
 struct TimingRecord {
     int kind;
+    double work;
     hipEvent_t start, stop;
 };
 static std::mutex g_timing_mu;
@@ -56,11 +57,11 @@ static hipEvent_t take_event() {
     return e;
 }
 
-void timing_events(int kind, hipEvent_t* start, hipEvent_t* stop) {
+void timing_events(int kind, double work, hipEvent_t* start, hipEvent_t* stop) {
     std::lock_guard<std::mutex> lock(g_timing_mu);
     *start = take_event();
     *stop = take_event();
-    if (*start && *stop) g_records.push_back({kind, *start, *stop});
+    if (*start && *stop) g_records.push_back({kind, work, *start, *stop});
 }
 
 // ---------------------------------------------------------------------------
@@ -386,6 +387,10 @@ int sp_timing_enable(int on) {
 }
 
 int sp_timing_collect(int32_t* kinds, float* ms, int max_records) {
+    return sp_timing_collect_work(kinds, ms, nullptr, max_records);
+}
+
+int sp_timing_collect_work(int32_t* kinds, float* ms, double* work, int max_records) {
     std::lock_guard<std::mutex> lock(g_timing_mu);
     int n = 0;
     for (const TimingRecord& r : g_records) {
@@ -394,6 +399,7 @@ int sp_timing_collect(int32_t* kinds, float* ms, int max_records) {
             n < max_records && kinds && ms) {
             kinds[n] = r.kind;
             ms[n] = t;
+            if (work) work[n] = r.work;
             ++n;
         }
         g_event_pool.push_back(r.start);
@@ -427,7 +433,7 @@ int sp_dps_residual(const sp_op* op, const float* x, const float* eps, const flo
     const dim3 grid(P, static_cast<unsigned>(batch));
     const bool v4 = op->n % 4 == 0;
 #define SP_K1(OPK, V)                                                                       \
-    launch(TK_DPS_RESIDUAL, k_dps_residual<OPK, V>, grid, dim3(kBlock), s, *op, x, eps, y, y_div, \
+    launch_w(TK_DPS_RESIDUAL, (double)batch, k_dps_residual<OPK, V>, grid, dim3(kBlock), s, *op, x, eps, y, y_div, \
            c->a, c->k, c->grad_scale, v_out, rsq_partial, P)
     if (op->kind == SP_OP_IDENTITY) {
         if (v4) SP_K1(SP_OP_IDENTITY, 4); else SP_K1(SP_OP_IDENTITY, 1);
@@ -455,7 +461,7 @@ int sp_dps_update(const sp_op* op, const float* x, const float* eps, const float
     const bool v4 = op->n % 4 == 0;
     const int opk = op->kind == SP_OP_BLUR ? SP_OP_IDENTITY : op->kind;  // BLUR reads v
 #define SP_K2(OPK, V, VIN, XIN)                                                            \
-    launch(TK_DPS_UPDATE, k_dps_update<OPK, V, VIN, XIN>, grid, dim3(kBlock), s, *op, x, eps, y, \
+    launch_w(TK_DPS_UPDATE, (double)batch, k_dps_update<OPK, V, VIN, XIN>, grid, dim3(kBlock), s, *op, x, eps, y, \
            v, w, rsq_partial, P, xi, seed, step, sample_offset, y_div, *c, x_out)
 #define SP_K2_XI(OPK, V, VIN) \
     if (xi) SP_K2(OPK, V, VIN, true); else SP_K2(OPK, V, VIN, false)

@@ -52,15 +52,18 @@ def draw_seed() -> int:
 
 
 class KernelTimer:
-    """Per-launch durations of the two fused passes.
+    """Per-launch durations of the library's timed kernels.
 
     Uses the library's dispatch-packet events (``sp_timing_enable``: a start/stop
     hipEvent pair attached to each kernel's AQL packet via hipExtLaunchKernel),
     i.e. the kernel's own execution interval on its launch stream — the same
-    interval rocprofv3's kernel trace reports — not a host-side bracket.
+    interval rocprofv3's kernel trace reports — not a host-side bracket.  Each
+    record carries the launch's algorithmic work (``sp_timing_collect_work``):
+    samples for the two DPS passes, FLOPs for the fp32-MFMA convolution tile.
     """
 
-    _KIND = {1: "dps_residual", 2: "dps_update"}
+    _KIND = {1: "dps_residual", 2: "dps_update", 3: "conv3x3_fwd", 4: "conv3x3_bwd_input"}
+    _CAP = 1 << 16
 
     def __init__(self) -> None:
         self.batches: list[tuple[str, int]] = []
@@ -81,20 +84,23 @@ class KernelTimer:
         return _Span()
 
     def summary(self) -> dict[str, dict[str, float]]:
+        """{kind: {count, ms, work}} over the launches since the last call; ``samples`` is
+        the DPS passes' work, ``flops`` the convolutions'."""
         import ctypes
 
-        cap = max(len(self.batches), 1)
-        kinds = (ctypes.c_int32 * cap)()
-        ms = (ctypes.c_float * cap)()
-        n = self._lib.sp_timing_collect(kinds, ms, cap)
+        kinds = (ctypes.c_int32 * self._CAP)()
+        ms = (ctypes.c_float * self._CAP)()
+        work = (ctypes.c_double * self._CAP)()
+        n = self._lib.sp_timing_collect_work(kinds, ms, work, self._CAP)
         out: dict[str, dict[str, float]] = {}
-        for (name, b), kind, t in zip(self.batches, kinds[:n], ms[:n]):
-            if self._KIND.get(kind) != name:
-                raise RuntimeError(f"timing log out of order: {name} vs kind {kind}")
-            d = out.setdefault(name, {"count": 0, "ms": 0.0, "samples": 0})
+        for kind, t, w in zip(kinds[:n], ms[:n], work[:n]):
+            name = self._KIND.get(kind, f"kind{kind}")
+            d = out.setdefault(name, {"count": 0, "ms": 0.0, "work": 0.0})
             d["count"] += 1
             d["ms"] += float(t)
-            d["samples"] += b
+            d["work"] += float(w)
+        for name, d in out.items():
+            d["samples" if name.startswith("dps") else "flops"] = d["work"]
         self.batches.clear()
         return out
 

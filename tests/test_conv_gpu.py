@@ -76,3 +76,21 @@ def test_conv3x3_rejects_unsupported(cuda):
     conv = Conv3x3(128, 128).to(cuda)  # falls back to MIOpen at 16x16
     x = torch.randn(1, 128, 16, 16, device=cuda)
     torch.testing.assert_close(conv(x), F.conv2d(x, conv.weight, conv.bias, padding=1))
+
+
+def test_conv3x3_timing_records_flops(cuda):
+    from samplers_amd.samplers.dps import KernelTimer
+
+    conv = Conv3x3(128, 256).to(cuda)
+    x = torch.randn(2, 128, 8, 64, device=cuda, requires_grad=True)
+    timer = KernelTimer()
+    try:
+        out = conv(x)
+        torch.autograd.grad(out, x, torch.ones_like(out))
+        s = timer.summary()
+    finally:
+        timer.close()
+    flops = 18.0 * 2 * 128 * 256 * 8 * 64
+    assert s["conv3x3_fwd"]["count"] == 1 and s["conv3x3_fwd"]["flops"] == flops
+    assert s["conv3x3_bwd_input"]["count"] == 1 and s["conv3x3_bwd_input"]["flops"] == flops
+    assert 0 < s["conv3x3_fwd"]["ms"] < 100
