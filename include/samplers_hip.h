@@ -104,7 +104,8 @@ typedef struct sp_adamw_coefs {
 int sp_timing_enable(int on);
 int sp_timing_collect(int32_t* kinds, float* ms, int max_records);
 /* As sp_timing_collect, plus each launch's algorithmic work: samples for kinds 1-2 (DPS
- * passes), FLOPs for kinds 3-4 (sp_conv3x3_fwd / _bwd_input). */
+ * passes), FLOPs for kinds 3-4 (sp_conv3x3_fwd / _bwd_input: 18*N*Cin*Cout*H*W) and
+ * executed MFMA FLOPs for kinds 5-6 (sp_wino3x3_fwd / _bwd_input: 8*N*Cin*Cout*H*W). */
 int sp_timing_collect_work(int32_t* kinds, float* ms, double* work, int max_records);
 
 /* Library / ABI version (major*10000 + minor*100 + patch). */
@@ -230,6 +231,19 @@ int sp_conv3x3_pack(const float* w, int32_t cout, int32_t cin, int32_t input_vjp
 int sp_conv3x3_fwd(const float* x, const float* wp, const float* bias, int64_t n, int32_t cin,
                    int32_t cout, int32_t height, int32_t width, float* y, sp_stream_t stream);
 int sp_conv3x3_bwd_input(const float* dy, const float* wp_vjp, int64_t n, int32_t cin,
+                         int32_t cout, int32_t height, int32_t width, float* dx,
+                         sp_stream_t stream);
+
+/* The same layers by Winograd F(2x2,3x3) on fp32 MFMA (2.25x fewer multiplies; the
+ * transforms add F(2,3) rounding, as MIOpen's Winograd solver does).  up = U = G g G^T
+ * packed by sp_wino3x3_pack (input_vjp=1: of the transposed, flipped weights). */
+int sp_wino3x3_supported(int32_t cin, int32_t cout, int32_t height, int32_t width);
+int64_t sp_wino3x3_packed_size(int32_t cin, int32_t cout);
+int sp_wino3x3_pack(const float* w, int32_t cout, int32_t cin, int32_t input_vjp, float* up,
+                    sp_stream_t stream);
+int sp_wino3x3_fwd(const float* x, const float* up, const float* bias, int64_t n, int32_t cin,
+                   int32_t cout, int32_t height, int32_t width, float* y, sp_stream_t stream);
+int sp_wino3x3_bwd_input(const float* dy, const float* up_vjp, int64_t n, int32_t cin,
                          int32_t cout, int32_t height, int32_t width, float* dx,
                          sp_stream_t stream);
 

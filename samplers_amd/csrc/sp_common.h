@@ -170,7 +170,14 @@ int check_launch(const char* what);
 bool timing_on();
 void timing_events(int kind, double work, hipEvent_t* start, hipEvent_t* stop);
 
-enum { TK_DPS_RESIDUAL = 1, TK_DPS_UPDATE = 2, TK_CONV3X3_FWD = 3, TK_CONV3X3_BWD_INPUT = 4 };
+enum {
+    TK_DPS_RESIDUAL = 1,
+    TK_DPS_UPDATE = 2,
+    TK_CONV3X3_FWD = 3,
+    TK_CONV3X3_BWD_INPUT = 4,
+    TK_WINO3X3_FWD = 5,
+    TK_WINO3X3_BWD_INPUT = 6
+};
 
 template <typename K, typename... Args>
 inline void launch_w(int kind, double work, K kernel, dim3 grid, dim3 block, hipStream_t s,

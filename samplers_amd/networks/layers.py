@@ -115,83 +115,101 @@ class GroupNormAct(nn.GroupNorm):
 # ---------------------------------------------------------------------------------------
 
 def conv_backend() -> str:
-    """``SAMPLERS_AMD_CONV``: ``hip`` (default: the MFMA kernel wherever its shape rules
-    hold, MIOpen elsewhere) or ``miopen`` (always torch/MIOpen)."""
+    """``SAMPLERS_AMD_CONV``: ``auto`` (default: Winograd F(2x2,3x3) tile where its shape
+    rules hold, else the direct tile, else MIOpen), ``direct`` (direct tile or MIOpen),
+    ``miopen`` (always torch/MIOpen)."""
     import os
 
-    return os.environ.get("SAMPLERS_AMD_CONV", "hip").lower()
+    return os.environ.get("SAMPLERS_AMD_CONV", "auto").lower()
+
+
+def _conv_algo(lib, cin: int, cout: int, h: int, w: int, backend: str) -> str | None:
+    if backend == "miopen":
+        return None
+    if backend == "auto" and lib.sp_wino3x3_supported(cin, cout, h, w):
+        return "wino"
+    if lib.sp_conv3x3_supported(cin, cout, h, w):
+        return "direct"
+    return None
 
 
 class _Conv3x3Fn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, wp, wp_vjp):
+    def forward(ctx, x, weight, bias, module, algo_fwd, algo_bwd):
         lib = _hip.load_library()
         n, cin, h, w = x.shape
         cout = weight.shape[0]
         x = x.contiguous()
         y = torch.empty(n, cout, h, w, device=x.device, dtype=torch.float32)
-        _hip.check(lib.sp_conv3x3_fwd(_hip.ptr(x), _hip.ptr(wp), _hip.ptr(bias), n, cin, cout, h, w,
-                                      _hip.ptr(y), _hip.stream_of(x)), "sp_conv3x3_fwd")
-        ctx.save_for_backward(x, weight, wp_vjp)
+        pk = module._pack(algo_fwd, False)
+        fn = lib.sp_wino3x3_fwd if algo_fwd == "wino" else lib.sp_conv3x3_fwd
+        _hip.check(fn(_hip.ptr(x), _hip.ptr(pk), _hip.ptr(bias), n, cin, cout, h, w, _hip.ptr(y),
+                      _hip.stream_of(x)), f"sp_{algo_fwd}_conv3x3_fwd")
+        pv = module._pack(algo_bwd, True) if algo_bwd else None
+        ctx.save_for_backward(x, weight, pv)
         ctx.has_bias = bias is not None
+        ctx.algo_bwd = algo_bwd
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        x, weight, wp_vjp = ctx.saved_tensors
+        x, weight, pv = ctx.saved_tensors
         n, cin, h, w = x.shape
         cout = weight.shape[0]
         dy = dy.contiguous()
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
-            lib = _hip.load_library()
-            if lib.sp_conv3x3_supported(cout, cin, h, w):
+            if ctx.algo_bwd:
+                lib = _hip.load_library()
                 dx = torch.empty_like(x)
-                _hip.check(lib.sp_conv3x3_bwd_input(_hip.ptr(dy), _hip.ptr(wp_vjp), n, cin, cout, h,
-                                                    w, _hip.ptr(dx), _hip.stream_of(dy)),
-                           "sp_conv3x3_bwd_input")
-            else:  # input VJP shape outside the tile rules (cin % 128): MIOpen
+                fn = lib.sp_wino3x3_bwd_input if ctx.algo_bwd == "wino" else lib.sp_conv3x3_bwd_input
+                _hip.check(fn(_hip.ptr(dy), _hip.ptr(pv), n, cin, cout, h, w, _hip.ptr(dx),
+                              _hip.stream_of(dy)), f"sp_{ctx.algo_bwd}_conv3x3_bwd_input")
+            else:  # input VJP shape outside the tiles' rules (e.g. cin = 3 or 4): MIOpen
                 dx = torch.nn.grad.conv2d_input(x.shape, weight, dy, padding=1)
         if ctx.needs_input_grad[1]:
             dw = torch.nn.grad.conv2d_weight(x, weight.shape, dy, padding=1)
         if ctx.has_bias and ctx.needs_input_grad[2]:
             db = dy.sum(dim=(0, 2, 3))
-        return dx, dw, db, None, None
+        return dx, dw, db, None, None, None
 
 
 class Conv3x3(nn.Conv2d):
-    """``nn.Conv2d(cin, cout, 3, padding=1)`` whose device forward / input VJP run the
-    fp32-MFMA kernel of ``csrc/sp_conv.hip`` where its shape rules hold (cin % 4,
-    cout % 128, H % 8, W % 32) and MIOpen elsewhere.  Packed weights are cached and
-    rebuilt when the parameter changes."""
+    """``nn.Conv2d(cin, cout, 3, padding=1)`` whose device forward / input VJP run this
+    project's fp32-MFMA tiles: Winograd F(2x2,3x3) (``csrc/sp_wino.hip``; cin % 8,
+    cout % 64, H % 8, W % 32) or the direct implicit GEMM (``csrc/sp_conv.hip``; cin % 4,
+    cout % 128, H % 8, W % 32), MIOpen elsewhere.  Transformed / packed weights are cached
+    per algorithm and rebuilt when the parameter changes."""
 
     def __init__(self, cin: int, cout: int) -> None:
         super().__init__(cin, cout, 3, padding=1)
-        self._packs = None
+        self._packs: dict = {}
         self._pack_key = None
 
-    def _packed(self):
+    def _pack(self, algo: str, input_vjp: bool) -> Tensor:
         w = self.weight
         key = (w.data_ptr(), w._version, w.device)
         if self._pack_key != key:
+            self._packs, self._pack_key = {}, key
+        if (algo, input_vjp) not in self._packs:
             lib = _hip.load_library()
             cout, cin = w.shape[0], w.shape[1]
             wc = w.detach().contiguous()
-            wp = torch.empty(int(lib.sp_conv3x3_packed_size(cin, cout)), device=w.device)
-            _hip.check(lib.sp_conv3x3_pack(_hip.ptr(wc), cout, cin, 0, _hip.ptr(wp),
-                                           _hip.stream_of(wc)), "sp_conv3x3_pack")
-            wv = None
-            if cout % 4 == 0:
-                wv = torch.empty_like(wp)
-                _hip.check(lib.sp_conv3x3_pack(_hip.ptr(wc), cout, cin, 1, _hip.ptr(wv),
-                                               _hip.stream_of(wc)), "sp_conv3x3_pack")
-            self._packs, self._pack_key = (wp, wv), key
-        return self._packs
+            size = (lib.sp_wino3x3_packed_size if algo == "wino" else lib.sp_conv3x3_packed_size)(cin, cout)
+            out = torch.empty(int(size), device=w.device)
+            fn = lib.sp_wino3x3_pack if algo == "wino" else lib.sp_conv3x3_pack
+            _hip.check(fn(_hip.ptr(wc), cout, cin, int(input_vjp), _hip.ptr(out), _hip.stream_of(wc)),
+                       f"sp_{algo}3x3_pack")
+            self._packs[(algo, input_vjp)] = out
+        return self._packs[(algo, input_vjp)]
 
     def forward(self, x: Tensor) -> Tensor:
-        if (x.is_cuda and x.dtype == torch.float32 and x.dim() == 4 and conv_backend() == "hip"
-                and _hip.load_library().sp_conv3x3_supported(x.shape[1], self.out_channels,
-                                                             x.shape[2], x.shape[3])):
-            wp, wv = self._packed()
-            return _Conv3x3Fn.apply(x, self.weight, self.bias, wp, wv)
+        if x.is_cuda and x.dtype == torch.float32 and x.dim() == 4:
+            lib = _hip.load_library()
+            be = conv_backend()
+            n, cin, h, w = x.shape
+            algo = _conv_algo(lib, cin, self.out_channels, h, w, be)
+            if algo is not None:
+                algo_bwd = _conv_algo(lib, self.out_channels, cin, h, w, be)
+                return _Conv3x3Fn.apply(x, self.weight, self.bias, self, algo, algo_bwd)
         return super().forward(x)

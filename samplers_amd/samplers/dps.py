@@ -62,7 +62,8 @@ class KernelTimer:
     samples for the two DPS passes, FLOPs for the fp32-MFMA convolution tile.
     """
 
-    _KIND = {1: "dps_residual", 2: "dps_update", 3: "conv3x3_fwd", 4: "conv3x3_bwd_input"}
+    _KIND = {1: "dps_residual", 2: "dps_update", 3: "conv3x3_fwd", 4: "conv3x3_bwd_input",
+             5: "wino3x3_fwd", 6: "wino3x3_bwd_input"}
     _CAP = 1 << 16
 
     def __init__(self) -> None:

@@ -1,8 +1,9 @@
-"""fp32-MFMA 3x3 convolution (csrc/sp_conv.hip) against an fp64 torch reference.
+"""fp32-MFMA 3x3 convolution tiles (csrc/sp_conv.hip direct, csrc/sp_wino.hip Winograd)
+against an fp64 torch reference.
 
-The kernel is an exact-fp32 fmaf chain over K = Cin*9 (v_mfma_f32_32x32x2_f32), so the
+The direct tile is an exact-fp32 fmaf chain over K = Cin*9 (v_mfma_f32_32x32x2_f32), so the
 tolerance is the fp32 accumulation error: relative L2 <= 2e-6 and max |err| <= 1e-5 x the
-largest |output| for the forward and the input VJP."""
+largest |output|; the Winograd tile's fp32 transforms add F(2,3) rounding: 5x that."""
 
 import pytest
 import torch
@@ -22,15 +23,18 @@ SHAPES = [  # n, cin, cout, h, w
 ]
 
 
-def _check(got, ref):
+def _check(got, ref, slack=1):
+    """slack 5 for the Winograd tile (its fp32 transforms add F(2,3) rounding)."""
     ref = ref.double()
     rel = ((got.double().cpu() - ref).norm() / ref.norm()).item()
     mx = (got.double().cpu() - ref).abs().max().item() / ref.abs().max().item()
-    assert rel < 2e-6 and mx < 1e-5, (rel, mx)
+    assert rel < 2e-6 * slack and mx < 1e-5 * slack, (rel, mx)
 
 
+@pytest.mark.parametrize("backend", ["auto", "direct"])
 @pytest.mark.parametrize("shape", SHAPES)
-def test_conv3x3_forward_and_input_vjp(cuda, shape):
+def test_conv3x3_forward_and_input_vjp(cuda, shape, backend, monkeypatch):
+    monkeypatch.setenv("SAMPLERS_AMD_CONV", backend)
     n, cin, cout, h, w = shape
     g = torch.Generator().manual_seed(sum(shape))
     x = torch.randn(n, cin, h, w, generator=g)
@@ -45,12 +49,14 @@ def test_conv3x3_forward_and_input_vjp(cuda, shape):
 
     lib = _hip.load_library()
     assert lib.sp_conv3x3_supported(cin, cout, h, w)
+    import os
+    wino = os.environ.get("SAMPLERS_AMD_CONV", "auto") == "auto" and lib.sp_wino3x3_supported(cin, cout, h, w)
     cg = conv.to(cuda)
     xg = x.to(cuda).requires_grad_()
     out = cg(xg)
     (gx,) = torch.autograd.grad(out, xg, dy.to(cuda))
-    _check(out.detach(), ref.detach())
-    _check(gx, gref)
+    _check(out.detach(), ref.detach(), 5 if wino else 1)
+    _check(gx, gref, 5 if wino else 1)
 
 
 def test_conv3x3_matches_miopen_and_repacks(cuda, monkeypatch):
@@ -60,7 +66,7 @@ def test_conv3x3_matches_miopen_and_repacks(cuda, monkeypatch):
     monkeypatch.setenv("SAMPLERS_AMD_CONV", "miopen")
     b = conv(x)
     torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-4)
-    monkeypatch.setenv("SAMPLERS_AMD_CONV", "hip")
+    monkeypatch.setenv("SAMPLERS_AMD_CONV", "auto")
     with torch.no_grad():
         conv.weight.mul_(2)  # in-place update -> packed weights rebuilt
     torch.testing.assert_close(conv(x) - conv.bias.view(1, -1, 1, 1),
@@ -78,11 +84,12 @@ def test_conv3x3_rejects_unsupported(cuda):
     torch.testing.assert_close(conv(x), F.conv2d(x, conv.weight, conv.bias, padding=1))
 
 
-def test_conv3x3_timing_records_flops(cuda):
+def test_conv3x3_timing_records_flops(cuda, monkeypatch):
     from samplers_amd.samplers.dps import KernelTimer
 
     conv = Conv3x3(128, 256).to(cuda)
     x = torch.randn(2, 128, 8, 64, device=cuda, requires_grad=True)
+    monkeypatch.setenv("SAMPLERS_AMD_CONV", "direct")
     timer = KernelTimer()
     try:
         out = conv(x)
@@ -94,3 +101,47 @@ def test_conv3x3_timing_records_flops(cuda):
     assert s["conv3x3_fwd"]["count"] == 1 and s["conv3x3_fwd"]["flops"] == flops
     assert s["conv3x3_bwd_input"]["count"] == 1 and s["conv3x3_bwd_input"]["flops"] == flops
     assert 0 < s["conv3x3_fwd"]["ms"] < 100
+    monkeypatch.setenv("SAMPLERS_AMD_CONV", "auto")
+    timer = KernelTimer()
+    try:
+        out = conv(x)
+        torch.autograd.grad(out, x, torch.ones_like(out))
+        s = timer.summary()
+    finally:
+        timer.close()
+    assert s["wino3x3_fwd"]["flops"] == flops * 8 / 18  # executed MFMA work
+    assert s["wino3x3_bwd_input"]["count"] == 1
+
+
+@pytest.mark.parametrize("shape", [(2, 128, 128, 32, 64), (1, 256, 64, 16, 32), (2, 64, 128, 8, 96)])
+def test_winograd_forward_and_input_vjp(cuda, shape):
+    """Winograd F(2x2,3x3) tile: fp32 transforms + exact fp32 MFMA accumulation; the
+    transforms add F(2,3) rounding, so the bound is 1e-5 relative L2 (vs 2e-6 direct)."""
+    n, cin, cout, h, w = shape
+    lib = _hip.load_library()
+    assert lib.sp_wino3x3_supported(cin, cout, h, w)
+    g = torch.Generator().manual_seed(11 + sum(shape))
+    x = torch.randn(n, cin, h, w, generator=g)
+    wt = torch.randn(cout, cin, 3, 3, generator=g) * (cin * 9) ** -0.5
+    b = torch.randn(cout, generator=g)
+    dy = torch.randn(n, cout, h, w, generator=g)
+    xd = x.double().requires_grad_()
+    ref = F.conv2d(xd, wt.double(), b.double(), padding=1)
+    (gref,) = torch.autograd.grad(ref, xd, dy.double())
+    st = torch.cuda.current_stream().cuda_stream
+    xg, wg, bg, dyg = x.to(cuda), wt.to(cuda), b.to(cuda), dy.to(cuda)
+    up = torch.empty(int(lib.sp_wino3x3_packed_size(cin, cout)), device=cuda)
+    uv = torch.empty_like(up)
+    _hip.check(lib.sp_wino3x3_pack(wg.data_ptr(), cout, cin, 0, up.data_ptr(), st), "pack")
+    _hip.check(lib.sp_wino3x3_pack(wg.data_ptr(), cout, cin, 1, uv.data_ptr(), st), "pack")
+    y = torch.empty(n, cout, h, w, device=cuda)
+    dx = torch.empty_like(xg)
+    _hip.check(lib.sp_wino3x3_fwd(xg.data_ptr(), up.data_ptr(), bg.data_ptr(), n, cin, cout, h, w,
+                                  y.data_ptr(), st), "wino fwd")
+    if lib.sp_wino3x3_supported(cout, cin, h, w):
+        _hip.check(lib.sp_wino3x3_bwd_input(dyg.data_ptr(), uv.data_ptr(), n, cin, cout, h, w,
+                                            dx.data_ptr(), st), "wino bwd")
+        rel = ((dx.double().cpu() - gref).norm() / gref.norm()).item()
+        assert rel < 1e-5, rel
+    rel = ((y.double().cpu() - ref.detach()).norm() / ref.detach().norm()).item()
+    assert rel < 1e-5, rel

@@ -62,7 +62,16 @@ def main():
         wv = torch.empty_like(wp)
         _hip.check(lib.sp_conv3x3_pack(wt.data_ptr(), cout, cin, 0, wp.data_ptr(), st()), "pack")
         _hip.check(lib.sp_conv3x3_pack(wt.data_ptr(), cout, cin, 1, wv.data_ptr(), st()), "pack")
+        up = torch.empty(cin * cout * 16, device="cuda")
+        uv = torch.empty_like(up)
+        _hip.check(lib.sp_wino3x3_pack(wt.data_ptr(), cout, cin, 0, up.data_ptr(), st()), "pack")
+        _hip.check(lib.sp_wino3x3_pack(wt.data_ptr(), cout, cin, 1, uv.data_ptr(), st()), "pack")
+        y2 = torch.empty_like(y)
         rows = {
+            "wino_fwd": lambda: lib.sp_wino3x3_fwd(x.data_ptr(), up.data_ptr(), b.data_ptr(), n, cin,
+                                                   cout, h, w, y2.data_ptr(), st()),
+            "wino_bwd_input": lambda: lib.sp_wino3x3_bwd_input(dy.data_ptr(), uv.data_ptr(), n, cin,
+                                                               cout, h, w, dx.data_ptr(), st()),
             "hip_fwd": lambda: lib.sp_conv3x3_fwd(x.data_ptr(), wp.data_ptr(), b.data_ptr(), n, cin,
                                                   cout, h, w, y.data_ptr(), st()),
             "miopen_fwd": lambda: F.conv2d(x, wt, b, padding=1),
@@ -71,7 +80,7 @@ def main():
             "miopen_bwd_input": lambda: torch.nn.grad.conv2d_input(x.shape, wt, dy, padding=1),
         }
         for name, fn in rows.items():
-            if name == "hip_bwd_input" and not lib.sp_conv3x3_supported(cout, cin, h, w):
+            if name in ("hip_bwd_input", "wino_bwd_input") and not lib.sp_conv3x3_supported(cout, cin, h, w):
                 continue
             ms = timeit(fn)
             print(json.dumps({"shape": [n, cin, cout, h, w], "kernel": name, "ms": round(ms, 3),
@@ -80,7 +89,11 @@ def main():
         lib.sp_conv3x3_fwd(x.data_ptr(), wp.data_ptr(), b.data_ptr(), n, cin, cout, h, w,
                            y.data_ptr(), st())
         err = ((y - ref).norm() / ref.norm()).item()
-        print(json.dumps({"shape": [n, cin, cout, h, w], "hip_vs_miopen_rel_l2": err}), flush=True)
+        lib.sp_wino3x3_fwd(x.data_ptr(), up.data_ptr(), b.data_ptr(), n, cin, cout, h, w,
+                           y2.data_ptr(), st())
+        err2 = ((y2 - ref).norm() / ref.norm()).item()
+        print(json.dumps({"shape": [n, cin, cout, h, w], "hip_vs_miopen_rel_l2": err,
+                          "wino_vs_miopen_rel_l2": err2}), flush=True)
         del x, y, dy, dx, ref
         torch.cuda.empty_cache()
 

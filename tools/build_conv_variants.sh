@@ -4,7 +4,7 @@
 set -e
 cd "$(dirname "$0")/.."
 mkdir -p build/variants
-SRC="samplers_amd/csrc/sp_dps.hip samplers_amd/csrc/sp_blur.hip samplers_amd/csrc/sp_latent.hip samplers_amd/csrc/sp_groupnorm.hip samplers_amd/csrc/sp_conv.hip"
+SRC="samplers_amd/csrc/sp_dps.hip samplers_amd/csrc/sp_blur.hip samplers_amd/csrc/sp_latent.hip samplers_amd/csrc/sp_groupnorm.hip samplers_amd/csrc/sp_conv.hip samplers_amd/csrc/sp_wino.hip"
 VARIANTS=("c4t4:-DSP_CONV_CI=4 -DSP_CONV_TPH=4"
           "c4t8:-DSP_CONV_CI=4 -DSP_CONV_TPH=8"
           "c8t4:-DSP_CONV_CI=8 -DSP_CONV_TPH=4 -DSP_CONV_MINB=1"
