@@ -57,11 +57,9 @@ __device__ __forceinline__ void wino_in(const float (&d)[16], float (&v)[16]) {
     }
 }
 
-// Global -> registers for chunk cc: packed U (float4) and each thread's input windows.
-__device__ __forceinline__ void wg_load(const float* __restrict__ up, const float* __restrict__ xn,
-                                        int cc, int cout, int co0, int64_t plane,
-                                        int64_t ci_bytes, const int (&voff)[16], int tid,
-                                        f32x4 (&ru)[WG_U / 4 / kBlock], float (&rd)[16]) {
+// Global -> registers for chunk cc: packed U rows (float4).
+__device__ __forceinline__ void wg_load_u(const float* __restrict__ up, int cc, int cout, int co0,
+                                          int tid, f32x4 (&ru)[WG_U / 4 / kBlock]) {
     // U chunk layout: [xi][ci_l][cout] rows of cout floats; this workgroup takes co0..+63
     const float* src = up + (int64_t)cc * 16 * WG_CI * cout + co0;
 #pragma unroll
@@ -70,17 +68,30 @@ __device__ __forceinline__ void wg_load(const float* __restrict__ up, const floa
         const int row = idx >> 4, c4 = idx & 15;
         ru[i] = *reinterpret_cast<const f32x4*>(src + (int64_t)row * cout + c4 * 4);
     }
-    // Input windows by buffer loads: the channel offset is wave-uniform (scalar soffset),
-    // each lane's 16 pixel offsets are fixed per workgroup, and a pixel outside the image
-    // gets an out-of-range offset, which the hardware returns as 0 (the padding) — no
-    // branches, no clamping, no waits between the loads.
-    const auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(xn), (short)0,
-                                                      static_cast<int>(ci_bytes), 0x00020000);
-    if (tid < WG_NPAIR) {  // waves 0, 1: pair = tid, ci = tid / 32 (in voff), tile = tid % 32
+}
+
+// Global -> registers for chunk cc: this thread's 4x4 input window (threads < 128).
+// Buffer loads: the chunk offset is a scalar (soffset), each lane's 16 pixel offsets are
+// fixed per workgroup, and a pixel outside the image has an out-of-range offset, which
+// the hardware returns as 0 (the padding) — no branches, no clamping.
+struct WinWindow {  // a thread's 4x4 input window: byte offset of its corner + validity
+    int base;         // ((ci_l * H + gr) * W + gc) * 4
+    unsigned mask;    // bit r*4+c: pixel inside the image
+};
+
+__device__ __forceinline__ void wg_load_x(__amdgpu_buffer_rsrc_t rs, int cc, int64_t plane, int W,
+                                          WinWindow win, int tid, float (&rd)[16]) {
+    if (tid < WG_NPAIR) {  // waves 0, 1: pair = tid, ci = tid / 32 (in base), tile = tid % 32
         const int so = static_cast<int>((int64_t)cc * WG_CI * plane * 4);  // wave-uniform
 #pragma unroll
-        for (int e = 0; e < 16; ++e)
-            rd[e] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, voff[e], so, 0));
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                const int off = ((win.mask >> (r * 4 + c)) & 1u) ? win.base + (r * W + c) * 4
+                                                                 : 0x7FFFFFF0;  // OOB -> 0
+                rd[r * 4 + c] =
+                    __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, off, so, 0));
+            }
     }
 }
 
@@ -97,6 +108,42 @@ __device__ __forceinline__ void wg_store(float* Us, float* Vs, int tid,
 #pragma unroll
         for (int xi = 0; xi < 16; ++xi) Vs[(xi * WG_CI + ci) * WG_T + tile] = v[xi];
     }
+}
+
+// LDS-visibility barrier that leaves global loads in flight.
+__device__ __forceinline__ void lds_barrier() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+}
+
+// One K chunk: MFMAs on buffer `buf`, stage chunk cc+1 (loaded before the previous
+// barrier) into the other buffer, then issue the loads of chunk cc+2.
+__device__ __forceinline__ void wg_chunk(float* Us0, float* Vs0, int buf, int cc, int nchunks,
+                                         const float* __restrict__ up, int cout, int co0,
+                                         int64_t plane, int W, __amdgpu_buffer_rsrc_t rs,
+                                         WinWindow win, int tid, int xh, int hh, int cw,
+                                         int l, f32x4 (&ru)[WG_U / 4 / kBlock], float (&rnext)[16],
+                                         f32x16 (&acc)[8]) {
+    const bool more = cc + 1 < nchunks;
+    const float* Ub = Us0 + buf * WG_U + (8 * xh * WG_CI + hh) * WG_CO + cw + l;
+    const float* Vb = Vs0 + buf * WG_V + (8 * xh * WG_CI + hh) * WG_T + l;
+#pragma unroll
+    for (int kk = 0; kk < WG_CI / 2; ++kk) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const float a = Ub[(j * WG_CI + 2 * kk) * WG_CO];
+            const float b = Vb[(j * WG_CI + 2 * kk) * WG_T];
+            acc[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc[j], 0, 0, 0);
+        }
+    }
+    if (more) {
+        wg_store(Us0 + (buf ^ 1) * WG_U, Vs0 + (buf ^ 1) * WG_V, tid, ru, rnext);
+        if (cc + 2 < nchunks) {
+            wg_load_u(up, cc + 2, cout, co0, tid, ru);
+            wg_load_x(rs, cc + 2, plane, W, win, tid, rnext);
+        }
+    }
+    lds_barrier();
 }
 
 __global__ __launch_bounds__(kBlock, 2) void k_wino3x3(const float* __restrict__ x,
@@ -122,45 +169,41 @@ __global__ __launch_bounds__(kBlock, 2) void k_wino3x3(const float* __restrict__
     f32x4 ru[WG_U / 4 / kBlock];
     float rd[16];
     // the input window of this thread's tile (threads < 128: tile = tid % 32)
-    int voff[16];
+    WinWindow win;
     {
         const int tile = tid & 31;
         const int gr = oh0 + 2 * (tile / WG_TC) - 1, gc = ow0 + 2 * (tile % WG_TC) - 1;
+        win.base = (int)(((tid >> 5) & 3) * plane + gr * W + gc) * 4;
+        win.mask = 0;
 #pragma unroll
         for (int r = 0; r < 4; ++r)
 #pragma unroll
-            for (int c = 0; c < 4; ++c) {
-                const int h = gr + r, w = gc + c;
-                const bool ok = (unsigned)h < (unsigned)H && (unsigned)w < (unsigned)W;
-                // + this thread's channel within the chunk; outside the image -> OOB -> 0
-                voff[r * 4 + c] = ok ? (int)(((tid >> 5) & 3) * plane + h * W + w) * 4 : 0x7FFFFFF0;
-            }
+            for (int c = 0; c < 4; ++c)
+                if ((unsigned)(gr + r) < (unsigned)H && (unsigned)(gc + c) < (unsigned)W)
+                    win.mask |= 1u << (r * 4 + c);
     }
     const int64_t ci_bytes = (int64_t)cin * plane * 4;
     f32x16 acc[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) acc[j] = f32x16{};
 
-    wg_load(up, xn, 0, cout, co0, plane, ci_bytes, voff, tid, ru, rd);
+    const auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(xn), (short)0,
+                                                      static_cast<int>(ci_bytes), 0x00020000);
+    // The next chunk's U rows and input windows are loaded right after the previous
+    // chunk's stage was written, before the barrier, so their latency is covered by the
+    // barrier wait plus a whole MFMA phase.  The barrier is a raw s_barrier after an
+    // LDS-only wait: __syncthreads()'s release fence would also wait for these loads.
+    wg_load_u(up, 0, cout, co0, tid, ru);
+    wg_load_x(rs, 0, plane, W, win, tid, rd);
     wg_store(Us0, Vs0, tid, ru, rd);
-    __syncthreads();
-    for (int cc = 0; cc < nchunks; ++cc) {
-        const int buf = cc & 1;
-        if (cc + 1 < nchunks) wg_load(up, xn, cc + 1, cout, co0, plane, ci_bytes, voff, tid, ru, rd);
-        const float* Ub = Us0 + buf * WG_U + (8 * xh * WG_CI + hh) * WG_CO + cw + l;
-        const float* Vb = Vs0 + buf * WG_V + (8 * xh * WG_CI + hh) * WG_T + l;
-#pragma unroll
-        for (int kk = 0; kk < WG_CI / 2; ++kk) {
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                const float a = Ub[(j * WG_CI + 2 * kk) * WG_CO];
-                const float b = Vb[(j * WG_CI + 2 * kk) * WG_T];
-                acc[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc[j], 0, 0, 0);
-            }
-        }
-        if (cc + 1 < nchunks) wg_store(Us0 + (buf ^ 1) * WG_U, Vs0 + (buf ^ 1) * WG_V, tid, ru, rd);
-        __syncthreads();
+    if (nchunks > 1) {
+        wg_load_u(up, 1, cout, co0, tid, ru);
+        wg_load_x(rs, 1, plane, W, win, tid, rd);
     }
+    lds_barrier();
+    for (int cc = 0; cc < nchunks; ++cc)
+        wg_chunk(Us0, Vs0, cc & 1, cc, nchunks, up, cout, co0, plane, W, rs, win, tid, xh, hh, cw,
+                 l, ru, rd, acc);
 
     // output transform Y = A^T M A, A^T = [[1,1,1,0],[0,1,-1,-1]], split by M's rows:
     // xi half 0 = rows 0,1 of M, half 1 = rows 2,3.  Lane column = tile l, register r =

@@ -14,7 +14,6 @@ MIOPEN_CUSTOM_CACHE_DIR are respected.
 from __future__ import annotations
 
 import os
-import shutil
 from pathlib import Path
 
 PACKAGE = Path(__file__).resolve().parent
@@ -57,13 +56,15 @@ def configure_miopen() -> Path | None:
 
 def _merge_find_db(src: Path, dst: Path) -> None:
     """Add the seed's entries (one ``key=solver:time,...`` line per convolution) that
-    ``dst`` lacks; entries MIOpen already measured on this machine are kept."""
-    if not dst.exists():
-        shutil.copyfile(src, dst)
-        return
-    have = {line.split("=", 1)[0] for line in dst.read_text().splitlines() if "=" in line}
+    ``dst`` lacks; entries MIOpen already measured on this machine are kept.  The merged
+    file is written to a private temporary and renamed into place, so the ranks of a
+    multi-GPU launch starting together never see (or write) a half-written database."""
+    have_lines = dst.read_text().splitlines() if dst.exists() else []
+    have = {line.split("=", 1)[0] for line in have_lines if "=" in line}
     extra = [line for line in src.read_text().splitlines()
              if "=" in line and line.split("=", 1)[0] not in have]
-    if extra:
-        with open(dst, "a") as f:
-            f.write("\n".join(extra) + "\n")
+    if not extra and dst.exists():
+        return
+    tmp = dst.with_name(f"{dst.name}.{os.getpid()}.tmp")
+    tmp.write_text("\n".join(have_lines + extra) + "\n")
+    os.replace(tmp, dst)

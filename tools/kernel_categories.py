@@ -7,7 +7,7 @@ tot = sum(float(r["TotalDurationNs"]) for r in rows)
 cats = {}
 for r in rows:
     n, t = r["Name"], float(r["TotalDurationNs"])
-    if "Conv" in n or "igemm" in n or "conv" in n.lower():
+    if "Conv" in n or "igemm" in n or "conv" in n.lower() or "k_wino" in n:
         c = "conv"
     elif "k_gn_" in n:
         c = "sp groupnorm (HIP)"
