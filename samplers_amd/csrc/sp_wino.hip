@@ -7,12 +7,12 @@
 //   M_xi = sum_ci U_xi[co][ci] * V_xi[ci][tile]      16 GEMMs on v_mfma_f32_32x32x2_f32
 //   Y = A^T M A   (2x2 outputs per (co, tile))
 //
-// Workgroup: 64 output channels x 32 tiles (4 x 32 output pixels of one image), 4 waves
-// as 2 (co halves) x 2 (xi halves): each wave accumulates 8 of the 16 xi GEMMs of its
-// 32 co x 32 tiles (128 fp32 per lane), so two workgroups fit a CU (48 KB LDS, <= 256
-// registers per lane) and one workgroup's transforms / LDS stores overlap the other's
-// MFMAs.  The output transform is linear in M, so each wave applies A^T (.) A to its own
-// 8 xi and the two xi halves are summed through LDS.  K walks the input channels 4 at a
+// Workgroup: 64 output channels x 32 tiles (4 x 32 output pixels of one image), 4 waves,
+// wave r owning row r of the transformed 4x4 tile M (xi = 4r .. 4r+3) for all 64 co x 32
+// tiles (128 fp32 per lane), so two workgroups fit a CU (48 KB LDS, <= 256 registers per
+// lane) and one workgroup's transforms / LDS stores overlap the other's MFMAs.  The
+// output transform is linear in M, so each wave applies A^T (.) A to its own row and the
+// four shares are summed through LDS.  K walks the input channels 4 at a
 // time: per chunk the workgroup writes U (16 xi x 4 ci x 64 co) and V (16 xi x 4 ci x 32
 // tiles) to LDS (double-buffered: the next chunk's global loads are in flight during the
 // MFMAs).  MFMA lane half h carries input channel 2kk + h.
@@ -121,19 +121,23 @@ __device__ __forceinline__ void lds_barrier() {
 __device__ __forceinline__ void wg_chunk(float* Us0, float* Vs0, int buf, int cc, int nchunks,
                                          const float* __restrict__ up, int cout, int co0,
                                          int64_t plane, int W, __amdgpu_buffer_rsrc_t rs,
-                                         WinWindow win, int tid, int xh, int hh, int cw,
+                                         WinWindow win, int tid, int xr, int hh,
                                          int l, f32x4 (&ru)[WG_U / 4 / kBlock], float (&rnext)[16],
-                                         f32x16 (&acc)[8]) {
+                                         f32x16 (&acc)[4][2]) {
     const bool more = cc + 1 < nchunks;
-    const float* Ub = Us0 + buf * WG_U + (8 * xh * WG_CI + hh) * WG_CO + cw + l;
-    const float* Vb = Vs0 + buf * WG_V + (8 * xh * WG_CI + hh) * WG_T + l;
+    // wave xr owns row xr of M: xi = 4 xr + j, both 32-channel halves (one B read feeds
+    // two MFMAs: 1.5 LDS reads per MFMA)
+    const float* Ub = Us0 + buf * WG_U + (4 * xr * WG_CI + hh) * WG_CO + l;
+    const float* Vb = Vs0 + buf * WG_V + (4 * xr * WG_CI + hh) * WG_T + l;
 #pragma unroll
     for (int kk = 0; kk < WG_CI / 2; ++kk) {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            const float a = Ub[(j * WG_CI + 2 * kk) * WG_CO];
+        for (int j = 0; j < 4; ++j) {
+            const float a0 = Ub[(j * WG_CI + 2 * kk) * WG_CO];
+            const float a1 = Ub[(j * WG_CI + 2 * kk) * WG_CO + 32];
             const float b = Vb[(j * WG_CI + 2 * kk) * WG_T];
-            acc[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc[j], 0, 0, 0);
+            acc[j][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b, acc[j][0], 0, 0, 0);
+            acc[j][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b, acc[j][1], 0, 0, 0);
         }
     }
     if (more) {
@@ -144,6 +148,34 @@ __device__ __forceinline__ void wg_chunk(float* Us0, float* Vs0, int buf, int cc
         }
     }
     lds_barrier();
+}
+
+// One wave's share of the output transform: MODE 0 writes it to LDS, 1 adds the LDS value
+// and writes back, 2 adds the LDS value and the bias and stores the 2x2 outputs.
+template <int MODE>
+__device__ __forceinline__ void wg_share(const f32x16 (&acc)[4][2], float c0, float c1, int hh,
+                                         int tile, float* ex, const float* __restrict__ bias,
+                                         float* __restrict__ on, int co0, int64_t plane,
+                                         int64_t pix = 0, int W = 0) {
+#pragma unroll
+    for (int m = 0; m < 2; ++m)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const float u0 = acc[0][m][r] + acc[1][m][r] + acc[2][m][r];
+            const float u1 = acc[1][m][r] - acc[2][m][r] - acc[3][m][r];
+            f32x4 y = {c0 * u0, c0 * u1, c1 * u0, c1 * u1};
+            const int col = 32 * m + (r & 3) + 8 * (r >> 2) + 4 * hh;
+            f32x4* e = reinterpret_cast<f32x4*>(&ex[(col * WG_T + tile) * 4]);
+            if (MODE > 0) y += *e;
+            if (MODE < 2) {
+                *e = y;
+            } else {
+                const float bv = bias ? bias[co0 + col] : 0.f;
+                float* dst = on + (int64_t)(co0 + col) * plane + pix;
+                *reinterpret_cast<float2*>(dst) = make_float2(y[0] + bv, y[1] + bv);
+                *reinterpret_cast<float2*>(dst + W) = make_float2(y[2] + bv, y[3] + bv);
+            }
+        }
 }
 
 __global__ __launch_bounds__(kBlock, 2) void k_wino3x3(const float* __restrict__ x,
@@ -163,7 +195,7 @@ __global__ __launch_bounds__(kBlock, 2) void k_wino3x3(const float* __restrict__
     const int64_t plane = (int64_t)H * W;
     const float* __restrict__ xn = x + (int64_t)n * cin * plane;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, hh = lane >> 5, l = lane & 31;
-    const int cw = (wv & 1) * 32, xh = wv >> 1;  // wave's co offset and xi half
+    const int xr = wv;  // wave's row of the 4x4 transformed tile M
     const int nchunks = cin / WG_CI;
 
     f32x4 ru[WG_U / 4 / kBlock];
@@ -183,9 +215,9 @@ __global__ __launch_bounds__(kBlock, 2) void k_wino3x3(const float* __restrict__
                     win.mask |= 1u << (r * 4 + c);
     }
     const int64_t ci_bytes = (int64_t)cin * plane * 4;
-    f32x16 acc[8];
+    f32x16 acc[4][2];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) acc[j] = f32x16{};
+    for (int j = 0; j < 4; ++j) acc[j][0] = acc[j][1] = f32x16{};
 
     const auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(xn), (short)0,
                                                       static_cast<int>(ci_bytes), 0x00020000);
@@ -202,56 +234,26 @@ __global__ __launch_bounds__(kBlock, 2) void k_wino3x3(const float* __restrict__
     }
     lds_barrier();
     for (int cc = 0; cc < nchunks; ++cc)
-        wg_chunk(Us0, Vs0, cc & 1, cc, nchunks, up, cout, co0, plane, W, rs, win, tid, xh, hh, cw,
-                 l, ru, rd, acc);
+        wg_chunk(Us0, Vs0, cc & 1, cc, nchunks, up, cout, co0, plane, W, rs, win, tid, xr, hh, l,
+                 ru, rd, acc);
 
-    // output transform Y = A^T M A, A^T = [[1,1,1,0],[0,1,-1,-1]], split by M's rows:
-    // xi half 0 = rows 0,1 of M, half 1 = rows 2,3.  Lane column = tile l, register r =
-    // co row (r&3)+8(r>>2)+4h.  Half 1 hands its partial Y to half 0 through LDS.
-    float* ex = lds;  // [64 co][32 tiles][4] partial outputs (8192 floats of the 12288)
-    float part[16][4];
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-        float s0[4], s1[4];  // contributions of this half's two M rows to A^T M
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-            const float m0 = acc[c][r], m1 = acc[4 + c][r];  // M rows 2xh, 2xh+1
-            if (xh == 0) {  // rows 0, 1: A^T[0] = (1, 1), A^T[1] = (0, 1)
-                s0[c] = m0 + m1;
-                s1[c] = m1;
-            } else {        // rows 2, 3: A^T[0] = (1, 0), A^T[1] = (-1, -1)
-                s0[c] = m0;
-                s1[c] = -m0 - m1;
-            }
-        }
-        part[r][0] = s0[0] + s0[1] + s0[2];
-        part[r][1] = s0[1] - s0[2] - s0[3];
-        part[r][2] = s1[0] + s1[1] + s1[2];
-        part[r][3] = s1[1] - s1[2] - s1[3];
-    }
-    if (xh == 1) {
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const int col = cw + (r & 3) + 8 * (r >> 2) + 4 * hh;
-            *reinterpret_cast<f32x4*>(&ex[(col * WG_T + l) * 4]) =
-                f32x4{part[r][0], part[r][1], part[r][2], part[r][3]};
-        }
-    }
+    // output transform Y = A^T M A, A^T = [[1,1,1,0],[0,1,-1,-1]]: wave xr holds row xr of
+    // M, whose share of Y is A^T[:, xr] (x) (M[xr, :] A).  The four shares are summed in a
+    // fixed order through LDS (wave 3, then 2, 1, and 0 writes the output).  Lane column
+    // = tile l, register r = co row (r&3)+8(r>>2)+4h of channel half m.
+    float* ex = lds;  // [64 co][32 tiles][4] (8192 floats of the 12288)
+    const float c0 = xr == 3 ? 0.f : 1.f;                       // A^T[0][xr]
+    const float c1 = xr == 0 ? 0.f : (xr == 1 ? 1.f : -1.f);    // A^T[1][xr]
+    const int tile = l;
+    const int oh = oh0 + 2 * (tile / WG_TC), ow = ow0 + 2 * (tile % WG_TC);
+    float* on = out + (int64_t)n * cout * plane;
+    if (xr == 3) wg_share<0>(acc, c0, c1, hh, tile, ex, nullptr, nullptr, 0, 0, 0);
     __syncthreads();
-    if (xh == 0) {
-        const int tile = l;
-        const int oh = oh0 + 2 * (tile / WG_TC), ow = ow0 + 2 * (tile % WG_TC);
-        float* on = out + (int64_t)n * cout * plane;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const int col = cw + (r & 3) + 8 * (r >> 2) + 4 * hh;
-            const f32x4 o = *reinterpret_cast<const f32x4*>(&ex[(col * WG_T + tile) * 4]);
-            const float bv = bias ? bias[co0 + col] : 0.f;
-            float* dst = on + (int64_t)(co0 + col) * plane + (int64_t)oh * W + ow;
-            *reinterpret_cast<float2*>(dst) = make_float2(part[r][0] + o[0] + bv, part[r][1] + o[1] + bv);
-            *reinterpret_cast<float2*>(dst + W) = make_float2(part[r][2] + o[2] + bv, part[r][3] + o[3] + bv);
-        }
-    }
+    if (xr == 2) wg_share<1>(acc, c0, c1, hh, tile, ex, nullptr, nullptr, 0, 0, 0);
+    __syncthreads();
+    if (xr == 1) wg_share<1>(acc, c0, c1, hh, tile, ex, nullptr, nullptr, 0, 0, 0);
+    __syncthreads();
+    if (xr == 0) wg_share<2>(acc, c0, c1, hh, tile, ex, bias, on, co0, plane, (int64_t)oh * W + ow, W);
 }
 
 // U = G g G^T, G = [[1,0,0],[.5,.5,.5],[.5,-.5,.5],[0,0,1]], packed
