@@ -74,6 +74,9 @@ def parse():
     p.add_argument("--micro-batch", type=int, default=0)
     p.add_argument("--recompute-v", action="store_true",
                    help="pass 2 re-derives v from y (gather) instead of re-reading pass 1's v")
+    p.add_argument("--graph", action="store_true",
+                   help="replay one hipGraph-captured step (samplers/graph.py); kernel times and "
+                        "the roofline then come from the eager warmup steps")
     p.add_argument("--cpu-seconds", type=float, default=15.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
     return p.parse_args()
@@ -201,6 +204,8 @@ def cpu_baseline(image: int, seconds: float) -> dict:
 
 def main():
     args = parse()
+    if args.graph and args.warmup < 1:
+        raise SystemExit("--graph needs --warmup >= 1 (kernel records come from the warmup)")
     rank, world, device = setup_dist(args.gpus)
     torch.backends.cudnn.benchmark = False  # MIOpen immediate mode: no exhaustive search
     from samplers_amd import _hip
@@ -231,13 +236,31 @@ def main():
         one_step()
         torch.cuda.synchronize()
         log(f"warmup step {k + 1}/{args.warmup} done at {time.perf_counter() - t_w:.1f}s")
-    timer.clear()
+    graph = None
+    if args.graph:
+        # kernel times of the (eager) warmup steps stand in for the replays' (events cannot
+        # be captured); the timed region is K replays of the captured step
+        kern_warm = timer.summary()
+        timer.close()
+        step.timer = None
+        from samplers_amd.samplers.graph import GraphedStepLoop
+
+        rest = [next(it) for _ in range(args.steps)]
+        graph = GraphedStepLoop(step, x, [(i, ts[i], ts[i - 1], ts[0]) for i in rest], seed=seed,
+                                sample_offset=rank * args.batch)
+        graph.capture()
+        log("captured one step into a hipGraph")
+    else:
+        timer.clear()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        one_step()
+    if graph is not None:
+        graph.replay()
+    else:
+        for _ in range(args.steps):
+            one_step()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -249,7 +272,8 @@ def main():
     if not torch.isfinite(x).all():
         raise SystemExit("non-finite samples")
 
-    kern = timer.summary()
+    kern = kern_warm if graph is not None else timer.summary()
+    kern_steps = args.warmup if graph is not None else args.steps  # steps the records cover
     nbytes = guidance_bytes(n, m, index_bytes)
     rl = {}
     for name in ("dps_residual", "dps_update"):
@@ -282,8 +306,8 @@ def main():
             "flops_basis": "executed MFMA FLOPs (Winograd: 8*N*Cin*Cout*H*W, direct: 18*...)",
             "effective_tflops": round(conv["effective_tflops"], 2),
             "avg_launch_ms": round(conv["ms"] / conv["count"], 4),
-            "launches_per_step": conv["count"] / args.steps,
-            "share_of_step": round(conv["ms"] / (elapsed * 1e3), 4),
+            "launches_per_step": conv["count"] / kern_steps,
+            "share_of_step": round(conv["ms"] / kern_steps / (elapsed / args.steps * 1e3), 4),
         }
     else:
         roofline = guidance_roofline
@@ -307,7 +331,9 @@ def main():
         "config": {"workload": f"{CONFIGS[args.config]}, 3x{args.image}x{args.image}, "
                                "ddpm-celebahq-256 prior, 1000-step DDPM schedule",
                    "global_batch": args.batch * world, "per_gpu_batch": args.batch,
-                   "parallelism": f"sample-batch shards x{world}, no data-path collective"},
+                   "parallelism": f"sample-batch shards x{world}, no data-path collective",
+                   "execution": "hipGraph replay of one captured step" if graph is not None
+                   else "eager"},
         "roofline": roofline,
         "guidance_roofline": guidance_roofline,
         "guidance_kernels": {k: {"avg_ms": round(v["avg_ms"], 5), "GB/s": round(v["gbs"], 1)}

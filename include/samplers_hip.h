@@ -219,6 +219,33 @@ int sp_groupnorm_silu_bwd(const float* dz, const float* x, const float* chan_bia
                           int32_t groups, int32_t act, float* dx, float* work,
                           sp_stream_t stream);
 
+/* ---- device-resident step schedule (hipGraph capture of a step) ----
+ * One record per guided step, precomputed on the host in the same fp64->fp32 arithmetic
+ * as the by-value calls; a device cursor selects the current record, so a captured step
+ * (timestep write, UNet forward/VJP, both passes, cursor advance) replays unchanged. */
+typedef struct sp_step_rec {
+    sp_dps_coefs c;   /* this step's scalars                          */
+    int64_t step;     /* Philox step index (the sampler's loop index) */
+    int64_t t;        /* the prior's timestep                          */
+} sp_step_rec;       /* 48 bytes */
+
+/* *t_out = sched[*cursor].t (the prior's timestep tensor, int64) */
+int sp_sched_timestep(const sp_step_rec* sched, const int32_t* cursor, int64_t* t_out,
+                      sp_stream_t stream);
+/* *cursor += 1 */
+int sp_sched_advance(int32_t* cursor, sp_stream_t stream);
+/* sp_dps_residual / sp_dps_update with the scalars (and the Philox step) read from
+ * sched[*cursor] on the device. */
+int sp_dps_residual_sched(const sp_op* op, const float* x, const float* eps, const float* y,
+                          int64_t batch, int64_t y_div, const sp_step_rec* sched,
+                          const int32_t* cursor, float* v_out, float* rsq_partial,
+                          sp_stream_t stream);
+int sp_dps_update_sched(const sp_op* op, const float* x, const float* eps, const float* y,
+                        const float* v, const float* w, const float* rsq_partial,
+                        uint64_t seed, int64_t sample_offset, int64_t batch, int64_t y_div,
+                        const sp_step_rec* sched, const int32_t* cursor, float* x_out,
+                        sp_stream_t stream);
+
 /* 3x3 / stride 1 / pad 1 convolution on fp32 MFMA (SURVEY.md §8b "vae_conv3x3_fwd/bwd_input",
  * §8f f1): the ResnetBlock / mid / up-sampling convolutions of the SD VAE and DDPM UNet
  * (diffusers Conv2d(k=3, p=1), reached from stable_diffusion.py:330-345, ddpm.py:40-43).

@@ -53,6 +53,11 @@ class SpDpsCoefs(ctypes.Structure):
     ]
 
 
+class SpStepRec(ctypes.Structure):
+    """One record of the device-resident step schedule (include/samplers_hip.h)."""
+    _fields_ = [("c", SpDpsCoefs), ("step", ctypes.c_int64), ("t", ctypes.c_int64)]
+
+
 class SpEpsCoefs(ctypes.Structure):
     _fields_ = [(f, ctypes.c_float) for f in ("sqrt_oma", "oma", "sqrt_a", "sqrt_a_prev", "sigma", "dir")]
 
@@ -111,6 +116,11 @@ SIGNATURES = {
                                       ctypes.c_int32, ctypes.c_int32, _P, _P]),
     "sp_wino3x3_bwd_input": (ctypes.c_int, [_P, _P, _I64, ctypes.c_int32, ctypes.c_int32,
                                             ctypes.c_int32, ctypes.c_int32, _P, _P]),
+    "sp_sched_timestep": (ctypes.c_int, [_P, _P, _P, _P]),
+    "sp_sched_advance": (ctypes.c_int, [_P, _P]),
+    "sp_dps_residual_sched": (ctypes.c_int, [_OPP, _P, _P, _P, _I64, _I64, _P, _P, _P, _P, _P]),
+    "sp_dps_update_sched": (ctypes.c_int, [_OPP, _P, _P, _P, _P, _P, _P, _U64, _I64, _I64, _I64,
+                                           _P, _P, _P, _P]),
     "sp_groupnorm_workspace": (_I64, [_I64, ctypes.c_int32, _I64, ctypes.c_int32]),
     "sp_groupnorm_silu_fwd": (ctypes.c_int, [_P, _P, _P, _P, _I64, ctypes.c_int32, _I64,
                                              ctypes.c_int32, _F, ctypes.c_int32, _P, _P, _P, _P,

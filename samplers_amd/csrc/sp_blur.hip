@@ -193,8 +193,14 @@ __global__ __launch_bounds__(kBlock) void k_blur(sp_op op, const float* __restri
                                                  const float* __restrict__ y, int y_div,
                                                  float a, float k, float gs,
                                                  float* __restrict__ out,
-                                                 float* __restrict__ partial, int P) {
+                                                 float* __restrict__ partial, int P,
+                                                 const sp_step_rec* __restrict__ sched,
+                                                 const int32_t* __restrict__ cursor) {
     using G = BlurGeom<R>;
+    if (MODE == MODE_DPS && sched) {  // device-resident schedule (graph replay)
+        const sp_dps_coefs& c = sched[*cursor].c;
+        a = c.a, k = c.k, gs = c.grad_scale;
+    }
     __shared__ __attribute__((aligned(16))) float bufA[G::LDS_A];
     __shared__ __attribute__((aligned(16))) float bufB[G::LDS_B];
     __shared__ float red[4];
@@ -375,7 +381,8 @@ int64_t blur_partials(const sp_op* op) {
 template <int MODE>
 static int launch_blur(const sp_op* op, const float* in, const float* eps, const float* y,
                        int64_t y_div, float a, float k, float gs, float* out, float* partial,
-                       int64_t batch, hipStream_t s) {
+                       int64_t batch, hipStream_t s, const sp_step_rec* sched = nullptr,
+                       const int32_t* cursor = nullptr) {
     const int64_t tiles = (int64_t)((op->height + TH - 1) / TH) * ((op->width + TW - 1) / TW);
     const int64_t blocks = tiles * op->channels * batch;
     // the kernel decodes blocks and in-plane offsets in 32 bits
@@ -389,7 +396,7 @@ static int launch_blur(const sp_op* op, const float* in, const float* eps, const
 #define SP_BLUR_CASE(RR)                                                                        \
     case RR:                                                                                    \
         launch_w(MODE == MODE_DPS ? TK_DPS_RESIDUAL : 0, (double)batch, k_blur<RR, MODE>, grid, dim3(kBlock), s, \
-               *op, in, eps, y, static_cast<int>(y_div), a, k, gs, out, partial, P);                              \
+               *op, in, eps, y, static_cast<int>(y_div), a, k, gs, out, partial, P, sched, cursor); \
         break;
         SP_BLUR_CASE(1) SP_BLUR_CASE(2) SP_BLUR_CASE(3) SP_BLUR_CASE(4)
         SP_BLUR_CASE(5) SP_BLUR_CASE(6) SP_BLUR_CASE(7) SP_BLUR_CASE(8)
@@ -400,9 +407,11 @@ static int launch_blur(const sp_op* op, const float* in, const float* eps, const
 }
 
 int blur_dps_residual(const sp_op* op, const float* x, const float* eps, const float* y,
-                      int64_t batch, int64_t y_div, float a, float k, float gs, float* v,
-                      float* partial, hipStream_t s) {
-    return launch_blur<MODE_DPS>(op, x, eps, y, y_div, a, k, gs, v, partial, batch, s);
+                      int64_t batch, int64_t y_div, float a, float k, float gs,
+                      const sp_step_rec* sched, const int32_t* cursor, float* v, float* partial,
+                      hipStream_t s) {
+    return launch_blur<MODE_DPS>(op, x, eps, y, y_div, a, k, gs, v, partial, batch, s, sched,
+                                 cursor);
 }
 
 int blur_apply(const sp_op* op, const float* x, float* y, int64_t batch, hipStream_t s) {

@@ -73,8 +73,14 @@ __global__ __launch_bounds__(kBlock) void k_dps_residual(sp_op op, const float* 
                                                          const float* __restrict__ y, int64_t y_div,
                                                          float a, float k, float gs,
                                                          float* __restrict__ v,
-                                                         float* __restrict__ partial, int P) {
+                                                         float* __restrict__ partial, int P,
+                                                         const sp_step_rec* __restrict__ sched,
+                                                         const int32_t* __restrict__ cursor) {
     __shared__ float red[4];
+    if (sched) {  // device-resident schedule (graph replay): uniform scalar loads
+        const sp_dps_coefs& c = sched[*cursor].c;
+        a = c.a, k = c.k, gs = c.grad_scale;
+    }
     const int64_t b = blockIdx.y;
     const int64_t n = op.n;
     const float* xb = x + b * n;
@@ -144,7 +150,13 @@ __global__ __launch_bounds__(kBlock) void k_dps_update(
     sp_op op, const float* __restrict__ x, const float* __restrict__ eps,
     const float* __restrict__ y, const float* __restrict__ v, const float* __restrict__ w,
     const float* __restrict__ partial, int P, const float* __restrict__ xi, uint64_t seed,
-    int64_t step, int64_t sample_offset, int64_t y_div, sp_dps_coefs c, float* __restrict__ xo) {
+    int64_t step, int64_t sample_offset, int64_t y_div, sp_dps_coefs c, float* __restrict__ xo,
+    const sp_step_rec* __restrict__ sched, const int32_t* __restrict__ cursor) {
+    if (sched) {  // device-resident schedule (graph replay)
+        const sp_step_rec& rec = sched[*cursor];
+        c = rec.c;
+        step = rec.step;
+    }
     const int64_t b = blockIdx.y;
     const int64_t n = op.n;
     const float* xb = x + b * n;
@@ -367,8 +379,9 @@ bool valid_op(const sp_op* op) {
 // blur entry points (sp_blur.hip)
 int64_t blur_partials(const sp_op* op);
 int blur_dps_residual(const sp_op* op, const float* x, const float* eps, const float* y,
-                      int64_t batch, int64_t y_div, float a, float k, float gs, float* v,
-                      float* partial, hipStream_t s);
+                      int64_t batch, int64_t y_div, float a, float k, float gs,
+                      const sp_step_rec* sched, const int32_t* cursor, float* v, float* partial,
+                      hipStream_t s);
 int blur_apply(const sp_op* op, const float* x, float* y, int64_t batch, hipStream_t s);
 int blur_adjoint(const sp_op* op, const float* y, float* x, int64_t batch, hipStream_t s);
 
@@ -419,22 +432,23 @@ int64_t sp_rsq_partials(const sp_op* op) {
 
 int64_t sp_vec_partials(int64_t count) { return count > 0 ? tiles_elementwise(count) : SP_EINVAL; }
 
-int sp_dps_residual(const sp_op* op, const float* x, const float* eps, const float* y,
-                    int64_t batch, int64_t y_div, const sp_dps_coefs* c, float* v_out,
-                    float* rsq_partial, sp_stream_t stream) {
-    if (!valid_op(op) || !x || !eps || !y || !c || !v_out || !rsq_partial || batch <= 0 ||
+static int dps_residual_impl(const sp_op* op, const float* x, const float* eps, const float* y,
+                             int64_t batch, int64_t y_div, sp_dps_coefs c,
+                             const sp_step_rec* sched, const int32_t* cursor, float* v_out,
+                             float* rsq_partial, sp_stream_t stream) {
+    if (!valid_op(op) || !x || !eps || !y || !v_out || !rsq_partial || batch <= 0 ||
         y_div <= 0 || batch > 65535)
         return SP_EINVAL;
     hipStream_t s = static_cast<hipStream_t>(stream);
     if (op->kind == SP_OP_BLUR)
-        return blur_dps_residual(op, x, eps, y, batch, y_div, c->a, c->k, c->grad_scale, v_out,
-                                 rsq_partial, s);
+        return blur_dps_residual(op, x, eps, y, batch, y_div, c.a, c.k, c.grad_scale, sched,
+                                 cursor, v_out, rsq_partial, s);
     const int P = static_cast<int>(tiles_elementwise(op->n));
     const dim3 grid(P, static_cast<unsigned>(batch));
     const bool v4 = op->n % 4 == 0;
 #define SP_K1(OPK, V)                                                                       \
     launch_w(TK_DPS_RESIDUAL, (double)batch, k_dps_residual<OPK, V>, grid, dim3(kBlock), s, *op, x, eps, y, y_div, \
-           c->a, c->k, c->grad_scale, v_out, rsq_partial, P)
+           c.a, c.k, c.grad_scale, v_out, rsq_partial, P, sched, cursor)
     if (op->kind == SP_OP_IDENTITY) {
         if (v4) SP_K1(SP_OP_IDENTITY, 4); else SP_K1(SP_OP_IDENTITY, 1);
     } else if (op->kind == SP_OP_MASK) {
@@ -446,11 +460,30 @@ int sp_dps_residual(const sp_op* op, const float* x, const float* eps, const flo
     return check_launch("sp_dps_residual");
 }
 
-int sp_dps_update(const sp_op* op, const float* x, const float* eps, const float* y,
-                  const float* v, const float* w, const float* rsq_partial, const float* xi,
-                  uint64_t seed, int64_t step, int64_t sample_offset, int64_t batch, int64_t y_div,
-                  const sp_dps_coefs* c, float* x_out, sp_stream_t stream) {
-    if (!valid_op(op) || !x || !eps || !w || !c || !x_out || batch <= 0 || y_div <= 0 ||
+int sp_dps_residual(const sp_op* op, const float* x, const float* eps, const float* y,
+                    int64_t batch, int64_t y_div, const sp_dps_coefs* c, float* v_out,
+                    float* rsq_partial, sp_stream_t stream) {
+    if (!c) return SP_EINVAL;
+    return dps_residual_impl(op, x, eps, y, batch, y_div, *c, nullptr, nullptr, v_out, rsq_partial,
+                             stream);
+}
+
+int sp_dps_residual_sched(const sp_op* op, const float* x, const float* eps, const float* y,
+                          int64_t batch, int64_t y_div, const sp_step_rec* sched,
+                          const int32_t* cursor, float* v_out, float* rsq_partial,
+                          sp_stream_t stream) {
+    if (!sched || !cursor) return SP_EINVAL;
+    return dps_residual_impl(op, x, eps, y, batch, y_div, sp_dps_coefs{}, sched, cursor, v_out,
+                             rsq_partial, stream);
+}
+
+static int dps_update_impl(const sp_op* op, const float* x, const float* eps, const float* y,
+                           const float* v, const float* w, const float* rsq_partial,
+                           const float* xi, uint64_t seed, int64_t step, int64_t sample_offset,
+                           int64_t batch, int64_t y_div, sp_dps_coefs c,
+                           const sp_step_rec* sched, const int32_t* cursor, float* x_out,
+                           sp_stream_t stream) {
+    if (!valid_op(op) || !x || !eps || !w || !x_out || batch <= 0 || y_div <= 0 ||
         batch > 65535)
         return SP_EINVAL;
     if (!v && (op->kind == SP_OP_BLUR || !y)) return SP_EINVAL;
@@ -462,7 +495,7 @@ int sp_dps_update(const sp_op* op, const float* x, const float* eps, const float
     const int opk = op->kind == SP_OP_BLUR ? SP_OP_IDENTITY : op->kind;  // BLUR reads v
 #define SP_K2(OPK, V, VIN, XIN)                                                            \
     launch_w(TK_DPS_UPDATE, (double)batch, k_dps_update<OPK, V, VIN, XIN>, grid, dim3(kBlock), s, *op, x, eps, y, \
-           v, w, rsq_partial, P, xi, seed, step, sample_offset, y_div, *c, x_out)
+           v, w, rsq_partial, P, xi, seed, step, sample_offset, y_div, c, x_out, sched, cursor)
 #define SP_K2_XI(OPK, V, VIN) \
     if (xi) SP_K2(OPK, V, VIN, true); else SP_K2(OPK, V, VIN, false)
 #define SP_K2_V(OPK, V) \
@@ -478,6 +511,45 @@ int sp_dps_update(const sp_op* op, const float* x, const float* eps, const float
 #undef SP_K2_XI
 #undef SP_K2
     return check_launch("sp_dps_update");
+}
+
+int sp_dps_update(const sp_op* op, const float* x, const float* eps, const float* y,
+                  const float* v, const float* w, const float* rsq_partial, const float* xi,
+                  uint64_t seed, int64_t step, int64_t sample_offset, int64_t batch, int64_t y_div,
+                  const sp_dps_coefs* c, float* x_out, sp_stream_t stream) {
+    if (!c) return SP_EINVAL;
+    return dps_update_impl(op, x, eps, y, v, w, rsq_partial, xi, seed, step, sample_offset, batch,
+                           y_div, *c, nullptr, nullptr, x_out, stream);
+}
+
+int sp_dps_update_sched(const sp_op* op, const float* x, const float* eps, const float* y,
+                        const float* v, const float* w, const float* rsq_partial,
+                        uint64_t seed, int64_t sample_offset, int64_t batch, int64_t y_div,
+                        const sp_step_rec* sched, const int32_t* cursor, float* x_out,
+                        sp_stream_t stream) {
+    if (!sched || !cursor) return SP_EINVAL;
+    return dps_update_impl(op, x, eps, y, v, w, rsq_partial, nullptr, seed, 0, sample_offset,
+                           batch, y_div, sp_dps_coefs{}, sched, cursor, x_out, stream);
+}
+
+__global__ void k_sched_timestep(const sp_step_rec* sched, const int32_t* cursor, int64_t* t) {
+    *t = sched[*cursor].t;
+}
+
+__global__ void k_sched_advance(int32_t* cursor) { *cursor += 1; }
+
+int sp_sched_timestep(const sp_step_rec* sched, const int32_t* cursor, int64_t* t_out,
+                      sp_stream_t stream) {
+    if (!sched || !cursor || !t_out) return SP_EINVAL;
+    launch(0, k_sched_timestep, dim3(1), dim3(1), static_cast<hipStream_t>(stream), sched, cursor,
+           t_out);
+    return check_launch("sp_sched_timestep");
+}
+
+int sp_sched_advance(int32_t* cursor, sp_stream_t stream) {
+    if (!cursor) return SP_EINVAL;
+    launch(0, k_sched_advance, dim3(1), dim3(1), static_cast<hipStream_t>(stream), cursor);
+    return check_launch("sp_sched_advance");
 }
 
 int sp_predict_x0(const float* x, const float* eps, int64_t count, float a, float k, float* out,

@@ -271,6 +271,7 @@ class DPSSampler(PosteriorSampler, Generic[Condition_co]):
         sample_offset: int = 0,
         micro_batch: int | None = None,
         timer: KernelTimer | None = None,
+        graph: bool = False,
         **kwargs,
     ) -> Tensor:
         """Run DPS; returns ``(*batch_shape, R, *x_shape)`` (R squeezed when 1).
@@ -279,7 +280,9 @@ class DPSSampler(PosteriorSampler, Generic[Condition_co]):
         ``rng`` / ``seed`` / ``noise_fn`` choose the noise source (module
         docstring); ``sample_offset`` is the global index of this shard's first
         flat sample (multi-GPU, keeps Philox streams shard-invariant);
-        ``micro_batch`` bounds how many samples share one prior forward+VJP.
+        ``micro_batch`` bounds how many samples share one prior forward+VJP;
+        ``graph=True`` replays one hipGraph-captured step for every iteration
+        (``samplers.graph``; Philox noise only) — same samples, no per-launch host work.
         """
         if args or kwargs:
             print(f"Warning: Unused args={args}, kwargs={kwargs} in DPSSampler")
@@ -306,13 +309,23 @@ class DPSSampler(PosteriorSampler, Generic[Condition_co]):
             x = initial_sample(view.flat_shape, net.device, rng=rng, seed=seed,
                                sample_offset=sample_offset, noise_fn=noise_fn)
             ts = net.timesteps_host
-            for i in range(len(ts) - 1, 1, -1):
-                xi = None
-                if noise_fn is not None:
-                    xi = noise_fn("step", i, tuple(x.shape)).to(device=x.device, dtype=torch.float32)
-                elif rng == "torch":
-                    xi = torch.randn_like(x)
-                step(x, i, ts[i], ts[i - 1], ts[0], xi=xi, seed=seed, sample_offset=sample_offset)
+            if graph:
+                if noise_fn is not None or rng != "philox":
+                    raise ValueError("graph=True needs the in-kernel Philox noise (rng='philox')")
+                from .graph import GraphedStepLoop, schedule_for
+
+                GraphedStepLoop(step, x, schedule_for(ts), seed=seed,
+                                sample_offset=sample_offset).replay()
+            else:
+                for i in range(len(ts) - 1, 1, -1):
+                    xi = None
+                    if noise_fn is not None:
+                        xi = noise_fn("step", i, tuple(x.shape)).to(device=x.device,
+                                                                    dtype=torch.float32)
+                    elif rng == "torch":
+                        xi = torch.randn_like(x)
+                    step(x, i, ts[i], ts[i - 1], ts[0], xi=xi, seed=seed,
+                         sample_offset=sample_offset)
 
             x0_final = view.unflatten(step.predict_x0(x, ts[1]))
             if num_reconstructions == 1 and not keep_reconstruction_dim:

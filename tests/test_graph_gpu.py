@@ -1,0 +1,54 @@
+"""hipGraph capture of the guided step (samplers/graph.py): a captured-and-replayed DPS
+solve matches the eager loop through the UNet's HIP GroupNorm and MFMA conv tiles.
+
+The HIP kernels are deterministic, but the prior's attention backward (flash-attention
+kernels accumulating with atomics) is not, so two eager solves already differ at ~1e-6;
+the bound is 1e-5 relative L2 for eager-vs-eager and graph-vs-eager alike (these
+random-weight priors amplify rounding: |x| reaches 1e3 here)."""
+
+import pytest
+import torch
+
+from samplers_amd.inverse_problem import InverseProblem
+from samplers_amd.networks.ddpm import DDPMNetwork
+from samplers_amd.networks.unet2d import UNet2DConfig
+from samplers_amd.noise import GaussianNoise
+from samplers_amd.operators import GaussianBlurOperator, IdentityOperator, RandomInpaintingOperator
+from samplers_amd.samplers import DPSSampler
+
+pytestmark = pytest.mark.gpu
+
+CFG = UNet2DConfig(sample_size=32, block_out_channels=(64, 128), attention_levels=(1,),
+                   layers_per_block=1)
+
+
+def _problem(kind, dev, b=2):
+    shape = (3, 32, 32)
+    op = {"identity": IdentityOperator(shape),
+          "inpaint": RandomInpaintingOperator(shape, 0.5, seed=3),
+          "blur": GaussianBlurOperator(shape, 9, 3.0)}[kind].to(dev)
+    gen = torch.Generator().manual_seed(5)
+    x_true = (torch.rand((b, *shape), generator=gen) * 2 - 1).to(dev)
+    y = op.apply(x_true)
+    y = y + 0.05 * torch.randn(tuple(y.shape), generator=gen).to(dev)
+    return InverseProblem(op, y, GaussianNoise(0.05).to(dev))
+
+
+@pytest.mark.parametrize("kind", ["identity", "inpaint", "blur"])
+def test_graph_replay_matches_eager(cuda, kind):
+    net = DDPMNetwork.from_config(CFG, seed=0, device=cuda)
+    prob = _problem(kind, cuda)
+    eager = DPSSampler(net)(prob, num_sampling_steps=8, gamma=0.5, seed=1234)
+    again = DPSSampler(net)(prob, num_sampling_steps=8, gamma=0.5, seed=1234)
+    graphed = DPSSampler(net)(prob, num_sampling_steps=8, gamma=0.5, seed=1234, graph=True)
+    assert torch.isfinite(eager).all()
+    base = ((again - eager).norm() / eager.norm()).item()
+    rel = ((graphed - eager).norm() / eager.norm()).item()
+    assert base < 1e-5 and rel < 1e-5, (base, rel)
+
+
+def test_graph_requires_philox(cuda):
+    net = DDPMNetwork.from_config(CFG, seed=0, device=cuda)
+    prob = _problem("identity", cuda)
+    with pytest.raises(ValueError, match="Philox"):
+        DPSSampler(net)(prob, num_sampling_steps=4, rng="torch", graph=True)

@@ -41,6 +41,7 @@ def test_struct_layouts_match_header():
     # sp_op: 4*int32 + 2*int64 + 3 pointers + 2*int32 = 16 + 16 + 24 + 8
     assert ctypes.sizeof(_hip.SpOp) == 64
     assert ctypes.sizeof(_hip.SpDpsCoefs) == 32
+    assert ctypes.sizeof(_hip.SpStepRec) == 48
 
 
 def test_library_loads_without_gpu():
