@@ -113,7 +113,8 @@ def test_conv3x3_timing_records_flops(cuda, monkeypatch):
     assert s["wino3x3_bwd_input"]["count"] == 1
 
 
-@pytest.mark.parametrize("shape", [(2, 128, 128, 32, 64), (1, 256, 64, 16, 32), (2, 64, 128, 8, 96)])
+@pytest.mark.parametrize("shape", [(2, 128, 128, 32, 64), (1, 256, 64, 16, 32), (2, 64, 128, 8, 96),
+                                   (3, 64, 192, 24, 64)])
 def test_winograd_forward_and_input_vjp(cuda, shape):
     """Winograd F(2x2,3x3) tile: fp32 transforms + exact fp32 MFMA accumulation; the
     transforms add F(2,3) rounding, so the bound is 1e-5 relative L2 (vs 2e-6 direct)."""

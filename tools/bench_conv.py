@@ -79,12 +79,17 @@ def main():
                                                               cout, h, w, dx.data_ptr(), st()),
             "miopen_bwd_input": lambda: torch.nn.grad.conv2d_input(x.shape, wt, dy, padding=1),
         }
+        keep = os.environ.get("ROWS")
         for name, fn in rows.items():
+            if keep and name not in keep.split(","):
+                continue
             if name in ("hip_bwd_input", "wino_bwd_input") and not lib.sp_conv3x3_supported(cout, cin, h, w):
                 continue
             ms = timeit(fn)
             print(json.dumps({"shape": [n, cin, cout, h, w], "kernel": name, "ms": round(ms, 3),
                               "TFLOP/s": round(flop / ms / 1e9, 1)}), flush=True)
+        if os.environ.get("ROWS"):
+            continue
         ref = F.conv2d(x, wt, b, padding=1)
         lib.sp_conv3x3_fwd(x.data_ptr(), wp.data_ptr(), b.data_ptr(), n, cin, cout, h, w,
                            y.data_ptr(), st())
