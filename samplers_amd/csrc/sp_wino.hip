@@ -325,9 +325,7 @@ __global__ __launch_bounds__(kBlock, 2) void k_wino3x3(const float* __restrict__
 constexpr int WR_CO = 64;   // output channels per workgroup (2 waves x 32)
 constexpr int WR_TR = 4;    // tile rows per workgroup (2 per wave): 8 output rows
 constexpr int WR_TC = 16;   // tile columns: 32 output columns
-#ifndef WR_NS
-#define WR_NS 4             // unroll of the k-step ring (cin % (2 WR_NS) == 0)
-#endif
+constexpr int WR_NS = 4;    // unroll of the k-step ring (cin % (2 WR_NS) == 0)
 constexpr int WX_ROW = 40;           // LDS floats per block row: even columns 0..16, odd 19..35
 constexpr int WX_CI = 6 * WX_ROW;    // per input channel of the block
 constexpr int WX_WAVE = 2 * WX_CI;   // per wave
@@ -371,6 +369,60 @@ __device__ __forceinline__ void wr_window(const float* xw, const WxLane& xl, flo
         d[r * 4 + 2] = row[20];
         d[r * 4 + 3] = row[1];
     }
+}
+
+struct WrRing {          // k-steps in flight
+    WrX xs[4];
+    WrU us[4];
+    float v[2][16];      // V of the current and the next step
+};
+struct WrCtx {
+    __amdgpu_buffer_rsrc_t rs;
+    WxLane xl;
+    float* xw;
+    const float* ub;
+    int64_t u_step;
+    int so_step, nsteps;
+};
+
+// One k-step q (slot K = q mod 4), laid out by hand with scheduling walls between the
+// pieces — 4 MFMAs, stage the next block, 4 MFMAs, read the next windows, 4 MFMAs, the
+// next V and the block loads, 4 MFMAs, the U loads — so the waits land where the data is
+// due and the vector / LDS work issues in the MFMA pipe's shadow.  (Spreading the same
+// work over all 16 MFMA gaps with scheduling groups measured the same.)
+template <int K, bool FIRST>
+__device__ __forceinline__ void wr_step(const WrCtx& c, int q, WrRing& g, f32x16 (&acc)[16]) {
+    const int nx = min(q + 3, c.nsteps - 1);  // clamped: harmless re-loads at the end
+    const int nu = min(q + 2, c.nsteps - 1);
+    const WrU& u = g.us[K];
+    const float(&vc)[16] = g.v[K & 1];
+    float(&vn)[16] = g.v[(K + 1) & 1];
+    float d[16];
+    auto mfma = [&](int xi, float a) {
+        acc[xi] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, vc[xi], FIRST ? f32x16{} : acc[xi],
+                                                       0, 0, 0);
+    };
+#pragma unroll
+    for (int xi = 0; xi < 4; ++xi) mfma(xi, u.u[0][xi]);
+    __builtin_amdgcn_sched_barrier(0);
+    wr_stage_x(c.xw, c.xl, g.xs[(K + 1) % 4]);  // block of step q + 1
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int xi = 4; xi < 8; ++xi) mfma(xi, u.u[1][xi - 4]);
+    __builtin_amdgcn_sched_barrier(0);
+    wr_window(c.xw, c.xl, d);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int xi = 8; xi < 12; ++xi) mfma(xi, u.u[2][xi - 8]);
+    __builtin_amdgcn_sched_barrier(0);
+    wino_in(d, vn);
+    wr_load_x(c.rs, c.xl, nx * c.so_step, g.xs[(K + 3) % 4]);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int xi = 12; xi < 16; ++xi) mfma(xi, u.u[3][xi - 12]);
+    __builtin_amdgcn_sched_barrier(0);
+    wr_load_u(c.ub + nu * c.u_step, g.us[(K + 2) % 4]);
+    __builtin_amdgcn_sched_barrier(0);
 }
 
 __global__ __launch_bounds__(kBlock, 1) void k_wino3x3_r(const float* __restrict__ x,
@@ -426,76 +478,52 @@ __global__ __launch_bounds__(kBlock, 1) void k_wino3x3_r(const float* __restrict
     const float* ub = up + ((int64_t)(co0 >> 5) * 64 + lane) * 16;
     const int nsteps = cin / 2;  // a multiple of WR_NS (cin % (2 WR_NS) == 0)
 
-    f32x16 acc[16];
-#pragma unroll
-    for (int xi = 0; xi < 16; ++xi) acc[xi] = f32x16{};
     // Step q's input block is loaded during step q - 3 and staged + turned into V during
-    // step q - 1; its U rows are loaded at the end of step q - 2.  The step is laid out by
-    // hand — 4 MFMAs, stage the next block, 4 MFMAs, read the next windows, 4 MFMAs, the
-    // next V and the block loads, 4 MFMAs, the U loads — with scheduling walls between the
-    // pieces, so the waits land where the data is due and the vector / LDS work issues in
-    // the MFMA pipe's shadow.  The prologue issues loads in the loop's own order.
-    WrX xs[WR_NS];
-    WrU us[WR_NS];
-    wr_load_x(rs, xl, 0, xs[0]);
+    // step q - 1; its U rows are loaded at the end of step q - 2 (wr_step).  The prologue
+    // issues loads in the loop's own order, so the waits at the loop head are the same from
+    // either predecessor.
+    WrRing ring;
+    wr_load_x(rs, xl, 0, ring.xs[0]);
     __builtin_amdgcn_sched_barrier(0);
-    wr_load_x(rs, xl, so_step, xs[1]);
+    wr_load_x(rs, xl, so_step, ring.xs[1]);
     __builtin_amdgcn_sched_barrier(0);
-    wr_load_u(ub, us[0]);
+    wr_load_u(ub, ring.us[0]);
     __builtin_amdgcn_sched_barrier(0);
-    wr_load_x(rs, xl, 2 * so_step, xs[2]);
+    wr_load_x(rs, xl, 2 * so_step, ring.xs[2]);
     __builtin_amdgcn_sched_barrier(0);
-    wr_load_u(ub + u_step, us[1]);
+    wr_load_u(ub + u_step, ring.us[1]);
     __builtin_amdgcn_sched_barrier(0);
-    float v[2][16];
     {
         float d[16];
-        wr_stage_x(xw, xl, xs[0]);
+        wr_stage_x(xw, xl, ring.xs[0]);
         wr_window(xw, xl, d);
-        wino_in(d, v[0]);
+        wino_in(d, ring.v[0]);
     }
-    for (int p = 0; p < nsteps; p += WR_NS) {
-#pragma unroll
-        for (int k = 0; k < WR_NS; ++k) {
-            const int q = p + k;
-            const int nx = min(q + 3, nsteps - 1);  // clamped: harmless re-loads at the end
-            const int nu = min(q + 2, nsteps - 1);
-            const WrU& u = us[k];
-            const float(&vc)[16] = v[k & 1];
-            float(&vn)[16] = v[(k + 1) & 1];
-            float d[16];
-#pragma unroll
-            for (int xi = 0; xi < 4; ++xi)
-                acc[xi] = __builtin_amdgcn_mfma_f32_32x32x2f32(u.u[0][xi], vc[xi], acc[xi], 0, 0, 0);
-            __builtin_amdgcn_sched_barrier(0);
-            wr_stage_x(xw, xl, xs[(k + 1) % WR_NS]);  // block of step q + 1
-            __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-            for (int xi = 4; xi < 8; ++xi)
-                acc[xi] = __builtin_amdgcn_mfma_f32_32x32x2f32(u.u[1][xi - 4], vc[xi], acc[xi], 0, 0, 0);
-            __builtin_amdgcn_sched_barrier(0);
-            wr_window(xw, xl, d);
-            __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-            for (int xi = 8; xi < 12; ++xi)
-                acc[xi] = __builtin_amdgcn_mfma_f32_32x32x2f32(u.u[2][xi - 8], vc[xi], acc[xi], 0, 0, 0);
-            __builtin_amdgcn_sched_barrier(0);
-            wino_in(d, vn);
-            wr_load_x(rs, xl, nx * so_step, xs[(k + 3) % WR_NS]);
-            __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-            for (int xi = 12; xi < 16; ++xi)
-                acc[xi] = __builtin_amdgcn_mfma_f32_32x32x2f32(u.u[3][xi - 12], vc[xi], acc[xi], 0, 0, 0);
-            __builtin_amdgcn_sched_barrier(0);
-            wr_load_u(ub + nu * u_step, us[(k + 2) % WR_NS]);
-            __builtin_amdgcn_sched_barrier(0);
-        }
+    const WrCtx ctx{rs, xl, xw, ub, u_step, so_step, nsteps};
+    f32x16 acc[16];
+    // first round: step 0 starts the accumulators from zero (no 256 AGPR clears)
+    wr_step<0, true>(ctx, 0, ring, acc);
+    wr_step<1, false>(ctx, 1, ring, acc);
+    wr_step<2, false>(ctx, 2, ring, acc);
+    wr_step<3, false>(ctx, 3, ring, acc);
+    for (int p = WR_NS; p < nsteps; p += WR_NS) {
+        wr_step<0, false>(ctx, p + 0, ring, acc);
+        wr_step<1, false>(ctx, p + 1, ring, acc);
+        wr_step<2, false>(ctx, p + 2, ring, acc);
+        wr_step<3, false>(ctx, p + 3, ring, acc);
     }
 
     // Y = A^T M A, A^T = [[1,1,1,0],[0,1,-1,-1]], per (channel, tile) in registers:
     // register r of every accumulator is channel co0 + (r&3) + 8(r>>2) + 4hh, tile l
     const int oh = oh0 + 2 * tr, ow = ow0 + 2 * tc;
     float* on = out + (int64_t)n * cout * plane + (int64_t)oh * W + ow;
+    float bv[16];  // all bias loads in flight together (one wait, not sixteen)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) bv[r] = 0.f;
+    if (bias) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) bv[r] = bias[co0 + (r & 3) + 8 * (r >> 2) + 4 * hh];
+    }
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
         float s0[4], s1[4];
@@ -507,12 +535,11 @@ __global__ __launch_bounds__(kBlock, 1) void k_wino3x3_r(const float* __restrict
             s1[a] = m1 - m2 - m3;
         }
         const int co = co0 + (r & 3) + 8 * (r >> 2) + 4 * hh;
-        const float bv = bias ? bias[co] : 0.f;
         float* dst = on + (int64_t)co * plane;
         *reinterpret_cast<float2*>(dst) =
-            make_float2(s0[0] + s0[1] + s0[2] + bv, s1[0] + s1[1] + s1[2] + bv);
+            make_float2(s0[0] + s0[1] + s0[2] + bv[r], s1[0] + s1[1] + s1[2] + bv[r]);
         *reinterpret_cast<float2*>(dst + W) =
-            make_float2(s0[1] - s0[2] - s0[3] + bv, s1[1] - s1[2] - s1[3] + bv);
+            make_float2(s0[1] - s0[2] - s0[3] + bv[r], s1[1] - s1[2] - s1[3] + bv[r]);
     }
 }
 

@@ -48,7 +48,10 @@ def main():
     lib = _hip.load_library()
     st = lambda: torch.cuda.current_stream().cuda_stream  # noqa: E731
     only = os.environ.get("SHAPES")
-    for idx, (n, cin, cout, h, w) in enumerate(SHAPES):
+    shapes = SHAPES
+    if os.environ.get("CUSTOM"):  # "n,cin,cout,h,w;n,cin,cout,h,w"
+        shapes = [tuple(int(v) for v in c.split(",")) for c in os.environ["CUSTOM"].split(";")]
+    for idx, (n, cin, cout, h, w) in enumerate(shapes):
         if only and str(idx) not in only.split(","):
             continue
         flop = 2.0 * n * cout * cin * 9 * h * w
@@ -61,11 +64,13 @@ def main():
         wp = torch.empty(cin * cout * 9, device="cuda")
         wv = torch.empty_like(wp)
         _hip.check(lib.sp_conv3x3_pack(wt.data_ptr(), cout, cin, 0, wp.data_ptr(), st()), "pack")
-        _hip.check(lib.sp_conv3x3_pack(wt.data_ptr(), cout, cin, 1, wv.data_ptr(), st()), "pack")
+        if lib.sp_conv3x3_supported(cout, cin, h, w):
+            _hip.check(lib.sp_conv3x3_pack(wt.data_ptr(), cout, cin, 1, wv.data_ptr(), st()), "pack")
         up = torch.empty(cin * cout * 16, device="cuda")
         uv = torch.empty_like(up)
         _hip.check(lib.sp_wino3x3_pack(wt.data_ptr(), cout, cin, 0, up.data_ptr(), st()), "pack")
-        _hip.check(lib.sp_wino3x3_pack(wt.data_ptr(), cout, cin, 1, uv.data_ptr(), st()), "pack")
+        if lib.sp_wino3x3_supported(cout, cin, h, w):
+            _hip.check(lib.sp_wino3x3_pack(wt.data_ptr(), cout, cin, 1, uv.data_ptr(), st()), "pack")
         y2 = torch.empty_like(y)
         rows = {
             "wino_fwd": lambda: lib.sp_wino3x3_fwd(x.data_ptr(), up.data_ptr(), b.data_ptr(), n, cin,
