@@ -88,9 +88,11 @@ constexpr int WR_TC = 16;   // tile columns: 32 output columns
                        // 3 = no input transform (wrong results, timing only)
 #endif
 constexpr int WR_NS = 4;    // unroll of the k-step ring (cin % (2 WR_NS) == 0)
-constexpr int WX_ROW = 40;           // LDS floats per block row: even columns 0..16, odd 19..35
+constexpr int WX_ROW = 40;           // LDS floats per block row (columns -1..32 at 3..36)
 constexpr int WX_CI = 6 * WX_ROW;    // per input channel of the block
 constexpr int WX_WAVE = 2 * WX_CI;   // per wave
+
+__device__ __forceinline__ int wx_row(int r) { return r * WX_ROW + (r >> 1); }
 
 struct WrX { f32x4 a, b; float h; };  // a lane's share of one k-step's input block
 struct WrU { f32x4 u[4]; };           // a lane's 16 U values (xi = 0..15) for one k-step
@@ -161,24 +163,22 @@ __device__ __forceinline__ void wr_load_u(const float* __restrict__ src, WrU& u)
     for (int i = 0; i < 4; ++i) u.u[i] = reinterpret_cast<const f32x4*>(src)[i];
 }
 
-// Block piece -> LDS: columns 4k..4k+3 go to even slots 2k, 2k+1 and odd slots 20+2k, 21+2k.
+// Block piece -> LDS (columns in natural order; dword pairs, so no register shuffles).
 __device__ __forceinline__ void wr_stage_x(float* xw, const WxLane& xl, const WrX& x) {
-    *reinterpret_cast<float2*>(xw + xl.wa) = make_float2(x.a[0], x.a[2]);
-    *reinterpret_cast<float2*>(xw + xl.wa + 20) = make_float2(x.a[1], x.a[3]);
-    *reinterpret_cast<float2*>(xw + xl.wb) = make_float2(x.b[0], x.b[2]);
-    *reinterpret_cast<float2*>(xw + xl.wb + 20) = make_float2(x.b[1], x.b[3]);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) xw[xl.wa + i] = x.a[i];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) xw[xl.wb + i] = x.b[i];
     xw[xl.wh] = x.h;
 }
 
-// This lane's 4x4 window (columns 2tc-1 .. 2tc+2 = odd tc-1, even tc, odd tc, even tc+1).
+// This lane's 4x4 window: columns 2tc-1 .. 2tc+2 of the wave's rows 2tr .. 2tr+3.
 __device__ __forceinline__ void wr_window(const float* xw, const WxLane& xl, float (&d)[16]) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-        const float* row = xw + xl.rd + r * WX_ROW;
-        d[r * 4 + 0] = row[19];
-        d[r * 4 + 1] = row[0];
-        d[r * 4 + 2] = row[20];
-        d[r * 4 + 3] = row[1];
+        const float* row = xw + xl.rd + wx_row(r);
+#pragma unroll
+        for (int c = 0; c < 4; ++c) d[r * 4 + c] = row[c];
     }
 }
 
@@ -188,14 +188,19 @@ struct WrRing {          // k-steps in flight
     float v[2][16];      // V of the current and the next step
 };
 
-// One k-step q (slot K = q mod 4) of the current tile, laid out by hand with scheduling
-// walls between the pieces — 4 MFMAs, stage the next block, 4 MFMAs, read the next
-// windows, 4 MFMAs, the next V and a block load, 4 MFMAs, a U load — so the waits land
-// where the data is due and the vector / LDS work issues in the MFMA pipe's shadow.
-// (Spreading the same work over all 16 MFMA gaps with scheduling groups measured the
-// same.)  Loads run 3 steps ahead for the input block, 2 for U; near the end of a tile
-// they fetch the next tile's first steps (XN / UN), so its operands arrive during this
-// tile's epilogue.
+// One k-step q (slot K = q mod 4) of the current tile.  A wave issues in order and its
+// vector work does not overlap an MFMA it has to wait behind, so the step is laid out by
+// hand, one small piece of side work after each of the 16 MFMAs (each runs 64 cycles),
+// with scheduling walls in between:
+//   gap 0     input block loads for step q + 3
+//   gap 1, 2  U loads for step q + 2
+//   gap 3, 4  stage the block of step q + 1 in LDS
+//   gap 5, 6  read this lane's window of it
+//   gap 8-15  V = B^T d B of step q + 1, four operations per gap
+// (Four bursts after every fourth MFMA ran 12-14 % slower: the MFMA pipe idled while the
+// burst issued.)  Loads run 3 steps ahead for the input block, 2 for U; near the end of
+// a tile they fetch the next tile's first steps (XN / UN), so its operands arrive during
+// this tile's epilogue.
 template <int K, bool FIRST, bool XN, bool UN>
 __device__ __forceinline__ void wr_step(const WrGeom& g, const WrSrc& cur, const WrSrc& nxt,
                                         float* xw, const WxLane& xl, int q, WrRing& r,
@@ -203,39 +208,88 @@ __device__ __forceinline__ void wr_step(const WrGeom& g, const WrSrc& cur, const
     const WrU& u = r.us[K];
     const float(&vc)[16] = r.v[K & 1];
     float(&vn)[16] = r.v[(K + 1) & 1];
-    float d[16];
+    float d[16], t[16];
+    const WrX& xb = r.xs[(K + 1) % 4];  // block of step q + 1
+#define WR_MFMA(xi)                                                                          \
+    acc[xi] = __builtin_amdgcn_mfma_f32_32x32x2f32(u.u[(xi) >> 2][(xi) & 3], vc[xi],         \
+                                                   FIRST ? f32x16{} : acc[xi], 0, 0, 0);     \
+    __builtin_amdgcn_sched_barrier(0)
+#define WR_WALL                                \
+    asm volatile("" ::: "memory");             \
+    __builtin_amdgcn_sched_barrier(0)
+    WR_MFMA(0);
+#if SP_WINO_EXP != 1
+    wr_load_x(XN ? nxt : cur, (XN ? q + 3 - g.nsteps : q + 3) * g.so_step, r.xs[(K + 3) % 4]);
+#endif
+    WR_WALL;
+    WR_MFMA(1);
+    const float* usrc = (UN ? nxt.ub : cur.ub) + (UN ? q + 2 - g.nsteps : q + 2) * g.u_step;
+    WrU& un = r.us[(K + 2) % 4];
+#if SP_WINO_EXP != 1
+    un.u[0] = reinterpret_cast<const f32x4*>(usrc)[0];
+    un.u[1] = reinterpret_cast<const f32x4*>(usrc)[1];
+#endif
+    WR_WALL;
+    WR_MFMA(2);
+#if SP_WINO_EXP != 1
+    un.u[2] = reinterpret_cast<const f32x4*>(usrc)[2];
+    un.u[3] = reinterpret_cast<const f32x4*>(usrc)[3];
+#endif
+    WR_WALL;
+    WR_MFMA(3);
 #pragma unroll
-    for (int xi = 0; xi < 16; ++xi) {
-        if (xi == 4) {
-            __builtin_amdgcn_sched_barrier(0);
-            wr_stage_x(xw, xl, r.xs[(K + 1) % 4]);  // block of step q + 1
-            __builtin_amdgcn_sched_barrier(0);
-        } else if (xi == 8) {
-            __builtin_amdgcn_sched_barrier(0);
-            wr_window(xw, xl, d);
-            __builtin_amdgcn_sched_barrier(0);
-        } else if (xi == 12) {
-            __builtin_amdgcn_sched_barrier(0);
+    for (int i = 0; i < 4; ++i) xw[xl.wa + i] = xb.a[i];
+    WR_WALL;
+    WR_MFMA(4);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) xw[xl.wb + i] = xb.b[i];
+    xw[xl.wh] = xb.h;
+    WR_WALL;
+    WR_MFMA(5);
+#pragma unroll
+    for (int rr = 0; rr < 2; ++rr)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) d[rr * 4 + c] = xw[xl.rd + wx_row(rr) + c];
+    WR_WALL;
+    WR_MFMA(6);
+#pragma unroll
+    for (int rr = 2; rr < 4; ++rr)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) d[rr * 4 + c] = xw[xl.rd + wx_row(rr) + c];
+    WR_WALL;
+    WR_MFMA(7);
+    WR_MFMA(8);
+    // t = B^T d, B^T = [[1,0,-1,0],[0,1,1,0],[0,-1,1,0],[0,1,0,-1]], one column per gap
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        t[0 * 4 + c] = d[0 * 4 + c] - d[2 * 4 + c];
+        t[1 * 4 + c] = d[1 * 4 + c] + d[2 * 4 + c];
+        t[2 * 4 + c] = d[2 * 4 + c] - d[1 * 4 + c];
+        t[3 * 4 + c] = d[1 * 4 + c] - d[3 * 4 + c];
+        WR_WALL;
+        WR_MFMA(9 + c);
+    }
+    // v = t B, one row per gap
+#pragma unroll
+    for (int rr = 0; rr < 3; ++rr) {
+        vn[rr * 4 + 0] = t[rr * 4 + 0] - t[rr * 4 + 2];
+        vn[rr * 4 + 1] = t[rr * 4 + 1] + t[rr * 4 + 2];
+        vn[rr * 4 + 2] = t[rr * 4 + 2] - t[rr * 4 + 1];
+        vn[rr * 4 + 3] = t[rr * 4 + 1] - t[rr * 4 + 3];
+        WR_WALL;
+        WR_MFMA(13 + rr);
+    }
+    vn[12] = t[12] - t[14];
+    vn[13] = t[13] + t[14];
+    vn[14] = t[14] - t[13];
+    vn[15] = t[13] - t[15];
 #if SP_WINO_EXP == 3
 #pragma unroll
-            for (int i = 0; i < 16; ++i) vn[i] = d[i];  // diagnostics: no input transform
-#else
-            wino_in(d, vn);
+    for (int i = 0; i < 16; ++i) vn[i] = d[i];  // diagnostics: no input transform
 #endif
-#if SP_WINO_EXP != 1
-            wr_load_x(XN ? nxt : cur, (XN ? q + 3 - g.nsteps : q + 3) * g.so_step,
-                      r.xs[(K + 3) % 4]);
-#endif
-            __builtin_amdgcn_sched_barrier(0);
-        }
-        acc[xi] = __builtin_amdgcn_mfma_f32_32x32x2f32(u.u[xi >> 2][xi & 3], vc[xi],
-                                                       FIRST ? f32x16{} : acc[xi], 0, 0, 0);
-    }
-    __builtin_amdgcn_sched_barrier(0);
-#if SP_WINO_EXP != 1
-    wr_load_u((UN ? nxt.ub : cur.ub) + (UN ? q + 2 - g.nsteps : q + 2) * g.u_step, r.us[(K + 2) % 4]);
-#endif
-    __builtin_amdgcn_sched_barrier(0);
+    WR_WALL;
+#undef WR_MFMA
+#undef WR_WALL
 }
 
 // Y = A^T M A, A^T = [[1,1,1,0],[0,1,-1,-1]], per (channel, tile) in registers: register r
@@ -298,14 +352,16 @@ __global__ __launch_bounds__(kBlock, 1) void k_wino3x3_r(WrGeom g) {
     float* const xw = xlds + wv * WX_WAVE;
     WxLane xl;
     {
-        auto loff = [](int rc) { return (rc / 6) * WX_CI + (rc % 6) * WX_ROW; };
+        // row r of a channel at r * WX_ROW + r / 2: the two tile rows of a wave read rows
+        // two apart, 81 floats = an odd bank distance, so their lanes never collide
+        auto loff = [](int rc) { return (rc / 6) * WX_CI + wx_row(rc % 6); };
         const int ka = lane & 7, rca = lane >> 3, rcb = 8 + ((lane >> 3) & 3);
         const int rch = (lane % 24) >> 1, side = lane & 1;
-        xl.wa = loff(rca) + 2 * ka;
-        xl.wb = loff(rcb) + 2 * ka;
-        xl.wh = loff(rch) + (side ? 16 : 19);
+        xl.wa = loff(rca) + 4 + 4 * ka;
+        xl.wb = loff(rcb) + 4 + 4 * ka;
+        xl.wh = loff(rch) + (side ? 36 : 3);
         const int l = lane & 31;
-        xl.rd = (lane >> 5) * WX_CI + 2 * (l >> 4) * WX_ROW + (l & 15);
+        xl.rd = (lane >> 5) * WX_CI + wx_row(2 * (l >> 4)) + 3 + 2 * (l & 15);
     }
     int t = blockIdx.x;
     const int stride = gridDim.x;
