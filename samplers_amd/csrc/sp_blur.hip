@@ -373,7 +373,248 @@ __global__ __launch_bounds__(kBlock) void k_blur(sp_op op, const float* __restri
     }
 }
 
+// ---------------------------------------------------------------------------
+// Streaming DPS pass for 256-column planes (BASELINE config 3 and any H % SSEG == 0).
+//
+// One wave owns one SSEG-row segment of one channel plane and sweeps it top to
+// bottom; each lane owns 4 adjacent columns, so a wave-instruction moves one whole
+// 1 KiB image row.  The vertical stencils run on rolling register windows (no
+// vertical halo is recomputed inside a segment), the horizontal stencils exchange
+// a row through a wave-private LDS row with zero pads (no barrier: one wave writes
+// and reads it), and the next chunk's x / eps / y rows are in flight while the
+// current chunk computes.  Per chunk of SCH input rows g:
+//   1  x0(g) = (x - k eps)/a on reflected row g; Hh(g) = horizontal A   (LDS row)
+//   2  z(g-R) = vertical A over Hh; S = c (y - z), 0 off the image; |r|^2
+//   3  V(g-2R) = vertical A^T over S (edge rows: fold-corrected taps)
+//   4  v(g-2R) = horizontal A^T over V (per-lane fold-corrected taps)  (LDS row)
+// The only redundant work is the segment's vertical halo (4R input rows per
+// SSEG output rows, read from L2: the block's 4 waves are neighbouring segments).
+// ---------------------------------------------------------------------------
+#ifndef SP_BLUR_SEG
+#define SP_BLUR_SEG 32
+#endif
+#ifndef SP_BLUR_STREAM
+#define SP_BLUR_STREAM 1
+#endif
+#ifndef SP_BLUR_WPB
+#define SP_BLUR_WPB 4
+#endif
+constexpr int SWPB = SP_BLUR_WPB;  // waves (row segments) per workgroup
+constexpr int SSEG = SP_BLUR_SEG;  // output rows per wave
+constexpr int SWID = 256;          // plane width served: 64 lanes x 4 columns
+constexpr int SCH = 4;             // rows per chunk
+constexpr int SPAD = 4;            // zero columns each side of an exchange row
+constexpr int SROW = SWID + 2 * SPAD;
+
+typedef float f4v __attribute__((ext_vector_type(4)));
+
+__host__ __device__ inline bool blur_streams(const sp_op* op) {
+    return SP_BLUR_STREAM && op->width == SWID && op->radius <= SPAD && op->height % SSEG == 0 &&
+           op->height >= 2 * op->radius + 2;
+}
+
+// Tap of the fold-corrected adjoint: (A1^T s)(j) = sum_o T_j[o] s(j + o), |o| <= R,
+// for the 1-D reflect-padded correlation over an extent of N (s = 0 off [0, N)):
+// T_j[o] = t[R-o] + t[R-2j-o] (1 <= j <= R) + t[2N-2-2j+R-o] (N-1-R <= j <= N-2).
+__device__ __forceinline__ float adj_tap(const float* t, int R, int N, int j, int o) {
+    float v = t[R - o];
+    if (j >= 1 && j <= R) {
+        const int i = R - 2 * j - o;
+        if (i >= 0 && i <= 2 * R) v += t[i];
+    }
+    if (j >= N - 1 - R && j <= N - 2) {
+        const int i = 2 * N - 2 - 2 * j + R - o;
+        if (i >= 0 && i <= 2 * R) v += t[i];
+    }
+    return v;
+}
+
+// LDS written by some lanes of a wave and read by others of the same wave: DS
+// instructions of one wave execute in order, so only the compiler needs fencing.
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+template <int R>
+__global__ __launch_bounds__(64 * SWPB) void k_blur_dps_stream(
+    sp_op op, const float* __restrict__ x, const float* __restrict__ eps,
+    const float* __restrict__ y, int y_div, float a, float k, float gs, float* __restrict__ out,
+    float* __restrict__ partial, int P, unsigned units, const sp_step_rec* __restrict__ sched,
+    const int32_t* __restrict__ cursor) {
+    constexpr int K = 2 * R + 1, WIN = SCH + 2 * R, NCH = SSEG / SCH + R;
+    constexpr int C2 = (2 * R) / SCH;  // first chunk whose z rows reach s0 - R
+    static_assert(SSEG % SCH == 0 && R >= 1 && R <= SPAD, "stream geometry");
+    if (sched) {
+        const sp_dps_coefs& cf = sched[*cursor].c;
+        a = cf.a, k = cf.k, gs = cf.grad_scale;
+    }
+    __shared__ __attribute__((aligned(16))) float xch[SWPB][SCH][SROW];
+    __shared__ float tl[K];
+
+    const int H = op.height, C = op.channels, nseg = H / SSEG;
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    float (*xr)[SROW] = xch[wv];
+    if (threadIdx.x < K) tl[threadIdx.x] = op.taps[threadIdx.x];
+    if (lane < SCH * 2 * SPAD) {  // zero pads, never written again
+        const int r = lane / (2 * SPAD), q = lane % (2 * SPAD);
+        xr[r][q < SPAD ? q : SWID + q] = 0.f;
+    }
+    __syncthreads();
+
+    // XCD-contiguous block order: neighbouring segments (shared halo rows) on one L2
+    const unsigned nblk = gridDim.x;
+    const unsigned q8 = nblk / 8, r8 = nblk % 8, xcd = blockIdx.x % 8, loc = blockIdx.x / 8;
+    const unsigned lin = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + loc;
+    const unsigned u = lin * SWPB + wv;
+    if (u >= units) return;
+    const unsigned pl = u / nseg;
+    const int sg = static_cast<int>(u - pl * nseg);
+    const int c = static_cast<int>(pl % C);
+    const unsigned b = pl / C;
+    const int s0 = sg * SSEG;
+    const int64_t plane = (int64_t)H * SWID;
+    const float* __restrict__ xp = x + pl * plane;
+    const float* __restrict__ ep = eps + pl * plane;
+    const float* __restrict__ yp = y + ((int64_t)(b / (unsigned)y_div) * C + c) * plane;
+    float* __restrict__ op_out = out + pl * plane;
+    const int col = 4 * lane;
+
+    float tk[K];  // uniform -> SGPRs
+#pragma unroll
+    for (int d = 0; d < K; ++d) tk[d] = op.taps[d];
+    float th[4][K];  // per-lane horizontal adjoint taps (fold-corrected at the edge columns)
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+#pragma unroll
+        for (int o = -R; o <= R; ++o) th[e][o + R] = adj_tap(tl, R, SWID, col + e, o);
+    const float inv_a = 1.f / a;
+
+    f4v hw[WIN], sw[WIN];
+#pragma unroll
+    for (int j = 0; j < WIN; ++j) hw[j] = sw[j] = f4v{0.f, 0.f, 0.f, 0.f};
+    f4v xn[SCH], en[SCH], yn[SCH];
+    auto load_chunk = [&](int cc) {
+#pragma unroll
+        for (int e = 0; e < SCH; ++e) {
+            const int gi = s0 - 2 * R + SCH * cc + e;
+            const int gr = reflect_clamp(gi, H);
+            const int gy = min(max(gi - R, 0), H - 1);
+            xn[e] = *reinterpret_cast<const f4v*>(xp + gr * SWID + col);
+            en[e] = *reinterpret_cast<const f4v*>(ep + gr * SWID + col);
+            yn[e] = *reinterpret_cast<const f4v*>(yp + gy * SWID + col);
+        }
+    };
+    load_chunk(0);
+    float racc = 0.f;
+    for (int cc = 0; cc < NCH; ++cc) {
+        f4v xc[SCH], ec[SCH], yc[SCH];
+#pragma unroll
+        for (int e = 0; e < SCH; ++e) xc[e] = xn[e], ec[e] = en[e], yc[e] = yn[e];
+        if (cc + 1 < NCH) load_chunk(cc + 1);
+
+        // ---- 1: x0 rows through the exchange row, horizontal A ----
+#pragma unroll
+        for (int j = 0; j < 2 * R; ++j) hw[j] = hw[j + SCH];
+        wave_lds_sync();  // previous chunk's reads of xr are done before the overwrite
+#pragma unroll
+        for (int e = 0; e < SCH; ++e)
+            *reinterpret_cast<f4v*>(&xr[e][SPAD + col]) = (xc[e] - k * ec[e]) * inv_a;
+        wave_lds_sync();
+#pragma unroll
+        for (int e = 0; e < SCH; ++e) {
+            float w[12];
+#pragma unroll
+            for (int q = 0; q < 3; ++q) {
+                const f4v t = *reinterpret_cast<const f4v*>(&xr[e][col + 4 * q]);
+                w[4 * q] = t.x, w[4 * q + 1] = t.y, w[4 * q + 2] = t.z, w[4 * q + 3] = t.w;
+            }
+#pragma unroll
+            for (int i = 1; i <= R; ++i) {  // reflect padding at the plane's side edges
+                w[SPAD - i] = lane == 0 ? w[SPAD + i] : w[SPAD - i];
+                w[SPAD + 3 + i] = lane == 63 ? w[SPAD + 3 - i] : w[SPAD + 3 + i];
+            }
+            f4v h;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                float acc = 0.f;
+#pragma unroll
+                for (int d = 0; d < K; ++d) acc = fmaf(tk[d], w[SPAD - R + q + d], acc);
+                h[q] = acc;
+            }
+            hw[2 * R + e] = h;
+        }
+        if (cc < C2) continue;
+
+        // ---- 2: vertical A, residual, S = c r (0 off the image), |r|^2 ----
+#pragma unroll
+        for (int j = 0; j < 2 * R; ++j) sw[j] = sw[j + SCH];
+#pragma unroll
+        for (int e = 0; e < SCH; ++e) {
+            const int gz = s0 - 3 * R + SCH * cc + e;
+            f4v z = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int d = 0; d < K; ++d) z += tk[d] * hw[e + d];
+            const f4v rr = yc[e] - z;
+            const bool in = (unsigned)gz < (unsigned)H;
+            sw[2 * R + e] = in ? rr * gs : f4v{0.f, 0.f, 0.f, 0.f};
+            if (gz >= s0 && gz < s0 + SSEG)
+                racc += (rr.x * rr.x + rr.y * rr.y) + (rr.z * rr.z + rr.w * rr.w);
+        }
+        if (cc < R) continue;
+
+        // ---- 3: vertical A^T (fold-corrected taps on edge rows) ----
+        const int gv0 = s0 - 4 * R + SCH * cc;
+        f4v vv[SCH];
+        if (gv0 > R && gv0 + SCH - 1 < H - 1 - R) {
+#pragma unroll
+            for (int e = 0; e < SCH; ++e) {
+                f4v u4 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                for (int i = 0; i < K; ++i) u4 += tk[i] * sw[e + 2 * R - i];
+                vv[e] = u4;
+            }
+        } else {
+#pragma unroll
+            for (int e = 0; e < SCH; ++e) {
+                f4v u4 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                for (int o = -R; o <= R; ++o) u4 += adj_tap(tl, R, H, gv0 + e, o) * sw[e + R + o];
+                vv[e] = u4;
+            }
+        }
+
+        // ---- 4: horizontal A^T through the exchange row, store v ----
+        wave_lds_sync();
+#pragma unroll
+        for (int e = 0; e < SCH; ++e) *reinterpret_cast<f4v*>(&xr[e][SPAD + col]) = vv[e];
+        wave_lds_sync();
+#pragma unroll
+        for (int e = 0; e < SCH; ++e) {
+            float w[12];
+#pragma unroll
+            for (int q = 0; q < 3; ++q) {
+                const f4v t = *reinterpret_cast<const f4v*>(&xr[e][col + 4 * q]);
+                w[4 * q] = t.x, w[4 * q + 1] = t.y, w[4 * q + 2] = t.z, w[4 * q + 3] = t.w;
+            }
+            f4v o4;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                float acc = 0.f;
+#pragma unroll
+                for (int o = -R; o <= R; ++o) acc = fmaf(th[q][o + R], w[SPAD + q + o], acc);
+                o4[q] = acc;
+            }
+            *reinterpret_cast<f4v*>(op_out + (gv0 + e) * SWID + col) = o4;
+        }
+    }
+    racc = wave_sum(racc);
+    if (lane == 0) partial[(int64_t)b * P + c * nseg + sg] = racc;
+}
+
 int64_t blur_partials(const sp_op* op) {
+    if (blur_streams(op)) return (int64_t)op->channels * (op->height / SSEG);
     const int64_t tiles = (int64_t)((op->height + TH - 1) / TH) * ((op->width + TW - 1) / TW);
     return tiles * op->channels;
 }
@@ -390,8 +631,24 @@ static int launch_blur(const sp_op* op, const float* in, const float* eps, const
         y_div < 1 || y_div > batch)
         return SP_EINVAL;
     if (blocks == 0) return SP_OK;
-    const dim3 grid(static_cast<unsigned>(blocks));
     const int P = static_cast<int>(blur_partials(op));
+    if (MODE == MODE_DPS && blur_streams(op)) {
+        const int64_t units = (int64_t)op->channels * (op->height / SSEG) * batch;
+        const dim3 sgrid(static_cast<unsigned>((units + SWPB - 1) / SWPB));
+        switch (op->radius) {
+#define SP_STREAM_CASE(RR)                                                                      \
+    case RR:                                                                                    \
+        launch_w(TK_DPS_RESIDUAL, (double)batch, k_blur_dps_stream<RR>, sgrid, dim3(64 * SWPB), s, \
+                 *op, in, eps, y, static_cast<int>(y_div), a, k, gs, out, partial, P,          \
+                 static_cast<unsigned>(units), sched, cursor);                                  \
+        break;
+            SP_STREAM_CASE(1) SP_STREAM_CASE(2) SP_STREAM_CASE(3) SP_STREAM_CASE(4)
+#undef SP_STREAM_CASE
+            default: return SP_EINVAL;
+        }
+        return check_launch("blur_stream");
+    }
+    const dim3 grid(static_cast<unsigned>(blocks));
     switch (op->radius) {
 #define SP_BLUR_CASE(RR)                                                                        \
     case RR:                                                                                    \

@@ -222,3 +222,33 @@ def test_dispatch_packet_timing(cuda):
     assert s["dps_residual"]["count"] == 3 and s["dps_update"]["count"] == 3
     assert 0 < s["dps_residual"]["ms"] < 100 and 0 < s["dps_update"]["ms"] < 100
     assert s["dps_update"]["samples"] == 3 * b
+
+
+@pytest.mark.parametrize("shape,ks,batch,ydiv", [((3, 32, 256), 9, 2, 1), ((2, 64, 256), 9, 3, 3),
+                                                 ((1, 96, 256), 5, 2, 1), ((3, 32, 256), 3, 1, 1),
+                                                 ((1, 64, 256), 7, 2, 2), ((3, 256, 256), 9, 2, 1)])
+def test_blur_streaming_residual_pass(cuda, shape, ks, batch, ydiv):
+    """The streaming blur pass (256-column planes, one wave per row segment) against the
+    closed form with the fold-corrected reflect adjoint: every radius it serves, one and
+    several segments per plane, shared observations."""
+    torch.manual_seed(1)
+    op = GaussianBlurOperator(shape, ks, 3.0).to(cuda)
+    apply_np, adjoint_np = oblur.blur_ops(shape, oblur.taps(ks, 3.0))
+    lib = _hip.load_library()
+    desc = op.hip_descriptor()
+    n = math.prod(shape)
+    P = lib.sp_rsq_partials(desc)
+    assert P == shape[0] * (shape[1] // 32)  # streaming layout: one partial per segment
+    x, eps = torch.randn(batch, n), torch.randn(batch, n)
+    y = torch.randn(batch // ydiv, n)
+    a, k, gs = 0.3, math.sqrt(1 - 0.09), 400.0
+    coefs = _hip.SpDpsCoefs(a, k, gs, 0.9, 0.2, 0.1, 0.05, 1e-9)
+    xd, ed, yd = (t.to(cuda).contiguous() for t in (x, eps, y))
+    v = torch.full_like(xd, float("nan"))
+    part = torch.full((batch, P), float("nan"), device=cuda)
+    _hip.check(lib.sp_dps_residual(desc, xd.data_ptr(), ed.data_ptr(), yd.data_ptr(), batch, ydiv,
+                                   coefs, v.data_ptr(), part.data_ptr(), _stream()), "residual")
+    v_ref, rsq_ref = closed_form.residual_pass(x.numpy(), eps.numpy(), y.numpy(), ydiv, a, k, gs,
+                                               apply_np, adjoint_np)
+    np.testing.assert_allclose(v.cpu().numpy(), v_ref, rtol=0, atol=2e-5 * np.abs(v_ref).max())
+    np.testing.assert_allclose(part.sum(1).cpu().numpy(), rsq_ref, rtol=2e-5)

@@ -22,19 +22,21 @@ _FLUSH = None
 
 
 def timeit(fn, reps=30):
-    """Mean launch time with cold caches: 1 GiB is written between launches so the
+    """Mean launch time with cold caches: 1 GiB is READ between launches so the
     256 MiB Infinity Cache holds none of the operands (as in the sampler, where
-    the prior's VJP streams gigabytes between the two passes)."""
+    the prior's VJP streams gigabytes between the two passes).  A read, not a
+    write: a written flush leaves dirty lines whose write-back lands inside the
+    timed launch (measured: a device copy then reads 3.1 instead of ~5 TB/s)."""
     global _FLUSH
     if _FLUSH is None:
-        _FLUSH = torch.empty(2**28, device="cuda")
+        _FLUSH = torch.ones(2**28, device="cuda")
     for _ in range(3):
         fn()
     total = 0.0
     flush = os.environ.get("FLUSH", "1") == "1"
     for _ in range(reps):
         if flush:
-            _FLUSH.zero_()
+            _FLUSH.sum()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
         fn()
