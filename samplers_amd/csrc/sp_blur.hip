@@ -376,19 +376,19 @@ __global__ __launch_bounds__(kBlock) void k_blur(sp_op op, const float* __restri
 // ---------------------------------------------------------------------------
 // Streaming DPS pass for 256-column planes (BASELINE config 3 and any H % SSEG == 0).
 //
-// One wave owns one SSEG-row segment of one channel plane and sweeps it top to
-// bottom; each lane owns 4 adjacent columns, so a wave-instruction moves one whole
-// 1 KiB image row.  The vertical stencils run on rolling register windows (no
-// vertical halo is recomputed inside a segment), the horizontal stencils exchange
-// a row through a wave-private LDS row with zero pads (no barrier: one wave writes
-// and reads it), and the next chunk's x / eps / y rows are in flight while the
-// current chunk computes.  Per chunk of SCH input rows g:
-//   1  x0(g) = (x - k eps)/a on reflected row g; Hh(g) = horizontal A   (LDS row)
+// One wave owns one SSEG-row segment of one channel plane and sweeps it from one end
+// to the other; each lane owns 4 adjacent columns, so one wave-instruction moves one
+// whole 1 KiB image row.  The vertical stencils run on rolling register windows (no
+// vertical halo is recomputed inside a segment); the horizontal stencils exchange a
+// row through LDS (one wave writes and reads it: no barrier).  Per chunk of DCH input
+// rows g:
+//   1  x0(g) = (x - k eps)/a on reflected row g; Hh(g) = horizontal A
 //   2  z(g-R) = vertical A over Hh; S = c (y - z), 0 off the image; |r|^2
 //   3  V(g-2R) = vertical A^T over S (edge rows: fold-corrected taps)
-//   4  v(g-2R) = horizontal A^T over V (per-lane fold-corrected taps)  (LDS row)
-// The only redundant work is the segment's vertical halo (4R input rows per
-// SSEG output rows, read from L2: the block's 4 waves are neighbouring segments).
+//   4  v(g-2R) = horizontal A^T over V (per-lane fold-corrected taps)
+// The only redundant reads are the segment's vertical halo (4R rows of x / eps, 2R of
+// y per SSEG rows); neighbouring segments sweep in opposite directions so both reach
+// a shared boundary together and the second read of its halo hits L2.
 // ---------------------------------------------------------------------------
 #ifndef SP_BLUR_SEG
 #define SP_BLUR_SEG 32
@@ -396,15 +396,9 @@ __global__ __launch_bounds__(kBlock) void k_blur(sp_op op, const float* __restri
 #ifndef SP_BLUR_STREAM
 #define SP_BLUR_STREAM 1
 #endif
-#ifndef SP_BLUR_WPB
-#define SP_BLUR_WPB 4
-#endif
-constexpr int SWPB = SP_BLUR_WPB;  // waves (row segments) per workgroup
 constexpr int SSEG = SP_BLUR_SEG;  // output rows per wave
 constexpr int SWID = 256;          // plane width served: 64 lanes x 4 columns
-constexpr int SCH = 4;             // rows per chunk
-constexpr int SPAD = 4;            // zero columns each side of an exchange row
-constexpr int SROW = SWID + 2 * SPAD;
+constexpr int SPAD = 4;            // window columns each side of a lane's 4 (R <= SPAD)
 
 typedef float f4v __attribute__((ext_vector_type(4)));
 
@@ -437,101 +431,187 @@ __device__ __forceinline__ void wave_lds_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// ---------------------------------------------------------------------------
+// LDS-DMA ring: the x / eps / y rows of DSLOT-1 chunks are in flight as
+// buffer_load_dwordx4 ... lds (one 1 KiB image row per wave-instruction, straight into
+// a wave-private LDS ring, no VGPRs held).  The DMAs are issued from inline asm (the
+// compiler would otherwise wait vmcnt(0) before every ds_read of the ring) and retired
+// by counted s_waitcnt vmcnt(N) = the exact number of younger vector memory
+// operations (later DMAs and the v stores in between).  The exchange rows live in
+// place in the consumed slot's x rows.  Window rows rotate through the registers with
+// period WIN / gcd(WIN, DCH) (the chunk body is instantiated per phase), so no
+// register moves shift them.
+// ---------------------------------------------------------------------------
+constexpr int DCH = 2;            // rows per chunk
+constexpr int DSLOT = 4;          // ring slots: DSLOT - 1 chunks in flight
+constexpr int DROWS = 3 * DCH;    // x, eps, y rows per slot
+constexpr int DRING = DSLOT * DROWS * SWID;
+
+// one 1 KiB row: buffer_load_dwordx4 ... lds, row offset in soffset (scalar), lane offset
+// in a fixed VGPR, LDS destination = M0 + 16 * lane
+__device__ __forceinline__ void dma_row(__amdgpu_buffer_rsrc_t rsrc, uint32_t voff, uint32_t soff,
+                                        uint32_t lds_byte) {
+    uint32_t keep;
+    asm volatile(
+        "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %4\n\ts_nop 0\n\t"
+        "buffer_load_dwordx4 %1, %2, %3 offen lds\n\ts_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "v"(voff), "s"(rsrc), "s"(soff), "s"(lds_byte)
+        : "memory");
+}
+
+// s_waitcnt vmcnt(n) for the even n a chunk can leave younger (<= 24)
+__device__ __forceinline__ void wait_vm(int n) {
+    switch (n) {
+#define SP_VM(N) \
+    case N: asm volatile("s_waitcnt vmcnt(" #N ")" ::: "memory"); break;
+        SP_VM(0) SP_VM(2) SP_VM(4) SP_VM(6) SP_VM(8) SP_VM(10) SP_VM(12) SP_VM(14)
+        SP_VM(16) SP_VM(18) SP_VM(20) SP_VM(22) SP_VM(24)
+#undef SP_VM
+        default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+}
+
+constexpr int gcd_c(int a, int b) { return b == 0 ? a : gcd_c(b, a % b); }
+
+// f(phase P0), f(P0 + 1), ..., f(N - 1) on chunks cc + P0, ... (compile-time phases)
+template <int P0, int N, class F>
+__device__ __forceinline__ void phases(F& f, int cc) {
+    if constexpr (P0 < N) {
+        f(std::integral_constant<int, P0>{}, cc + P0);
+        phases<P0 + 1, N>(f, cc);
+    }
+}
+
 template <int R>
-__global__ __launch_bounds__(64 * SWPB) void k_blur_dps_stream(
+__global__ __launch_bounds__(64) void k_blur_dps_dma(
     sp_op op, const float* __restrict__ x, const float* __restrict__ eps,
     const float* __restrict__ y, int y_div, float a, float k, float gs, float* __restrict__ out,
     float* __restrict__ partial, int P, unsigned units, const sp_step_rec* __restrict__ sched,
     const int32_t* __restrict__ cursor) {
-    constexpr int K = 2 * R + 1, WIN = SCH + 2 * R, NCH = SSEG / SCH + R;
-    constexpr int C2 = (2 * R) / SCH;  // first chunk whose z rows reach s0 - R
-    static_assert(SSEG % SCH == 0 && R >= 1 && R <= SPAD, "stream geometry");
+    constexpr int K = 2 * R + 1, CH = DCH, WIN = CH + 2 * R, NCH = (SSEG + 4 * R) / CH;
+    constexpr int C2 = (2 * R) / CH, C3 = (4 * R) / CH, PER = WIN / gcd_c(WIN, CH);
+    static_assert(SSEG % CH == 0 && (4 * R) % CH == 0 && R >= 1 && R <= SPAD, "dma geometry");
+    static_assert(DROWS * (DSLOT - 1) + CH * (DSLOT - 1) <= 24 && DROWS % 2 == 0 && CH % 2 == 0, "vmcnt cases");
     if (sched) {
         const sp_dps_coefs& cf = sched[*cursor].c;
         a = cf.a, k = cf.k, gs = cf.grad_scale;
     }
-    __shared__ __attribute__((aligned(16))) float xch[SWPB][SCH][SROW];
-    __shared__ float tl[K];
-
-    const int H = op.height, C = op.channels, nseg = H / SSEG;
-    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    float (*xr)[SROW] = xch[wv];
-    if (threadIdx.x < K) tl[threadIdx.x] = op.taps[threadIdx.x];
-    if (lane < SCH * 2 * SPAD) {  // zero pads, never written again
-        const int r = lane / (2 * SPAD), q = lane % (2 * SPAD);
-        xr[r][q < SPAD ? q : SWID + q] = 0.f;
-    }
+    __shared__ __attribute__((aligned(16))) float lds[DRING + 8];
+    __shared__ float tl[2][K];  // taps, and reversed (vertical taps of a bottom-up sweep)
+    float* ring = lds + 4;  // guards either side: lanes 0 / 63 read one float4 past a row
+    const int lane = threadIdx.x;
+    if (lane < K) tl[0][lane] = tl[1][K - 1 - lane] = op.taps[lane];
     __syncthreads();
 
-    // XCD-contiguous block order: neighbouring segments (shared halo rows) on one L2
+    const int H = op.height, C = op.channels, nseg = H / SSEG;
     const unsigned nblk = gridDim.x;
     const unsigned q8 = nblk / 8, r8 = nblk % 8, xcd = blockIdx.x % 8, loc = blockIdx.x / 8;
-    const unsigned lin = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + loc;
-    const unsigned u = lin * SWPB + wv;
+    const unsigned u = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + loc;
     if (u >= units) return;
     const unsigned pl = u / nseg;
     const int sg = static_cast<int>(u - pl * nseg);
     const int c = static_cast<int>(pl % C);
     const unsigned b = pl / C;
-    const int s0 = sg * SSEG;
+    // Odd segments sweep bottom-up (mirrored rows and vertical taps; the reflect-padded
+    // blur is mirror-symmetric), so the two waves that read the halo rows of a segment
+    // boundary both reach it at the start, or both at the end, of their sweeps and the
+    // second read hits L2.  Row indices below are sweep coordinates; prow() maps them.
+    const bool flip = sg & 1;
+    const int s0 = flip ? H - (sg + 1) * SSEG : sg * SSEG;
+    auto prow = [&](int g) { return flip ? H - 1 - g : g; };
+    const float* tlv = tl[flip ? 1 : 0];
     const int64_t plane = (int64_t)H * SWID;
     const float* __restrict__ xp = x + pl * plane;
     const float* __restrict__ ep = eps + pl * plane;
     const float* __restrict__ yp = y + ((int64_t)(b / (unsigned)y_div) * C + c) * plane;
     float* __restrict__ op_out = out + pl * plane;
     const int col = 4 * lane;
+    const uint32_t voff = 16u * lane;
+    const uint32_t ring_b =
+        static_cast<uint32_t>(reinterpret_cast<uintptr_t>((__attribute__((address_space(3))) float*)ring));
 
-    float tk[K];  // uniform -> SGPRs
+    float tk[K];
 #pragma unroll
     for (int d = 0; d < K; ++d) tk[d] = op.taps[d];
-    float th[4][K];  // per-lane horizontal adjoint taps (fold-corrected at the edge columns)
+    float tv[K];  // vertical taps in sweep order
+#pragma unroll
+    for (int d = 0; d < K; ++d) tv[d] = flip ? tk[K - 1 - d] : tk[d];
+    float th[4][K];
 #pragma unroll
     for (int e = 0; e < 4; ++e)
 #pragma unroll
-        for (int o = -R; o <= R; ++o) th[e][o + R] = adj_tap(tl, R, SWID, col + e, o);
+        for (int o = -R; o <= R; ++o) th[e][o + R] = adj_tap(tl[0], R, SWID, col + e, o);
     const float inv_a = 1.f / a;
+
+    const int pbytes = static_cast<int>(plane * 4);
+    const auto xr = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(xp), (short)0, pbytes, 0x00020000);
+    const auto er = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(ep), (short)0, pbytes, 0x00020000);
+    const auto yr = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(yp), (short)0, pbytes, 0x00020000);
+    auto issue = [&](int cc) {
+        const int s = cc % DSLOT;
+#pragma unroll
+        for (int e = 0; e < CH; ++e) {
+            const int gi = s0 - 2 * R + CH * cc + e;
+            const int gr = reflect_clamp(gi, H);
+            const int gy = min(max(gi - R, 0), H - 1);
+            const uint32_t rb = ring_b + 4u * ((s * DROWS + e) * SWID);
+            const uint32_t ox = 4u * SWID * prow(gr), oy = 4u * SWID * prow(gy);
+            dma_row(xr, voff, ox, rb);
+            dma_row(er, voff, ox, rb + 4u * CH * SWID);
+            dma_row(yr, voff, oy, rb + 8u * CH * SWID);
+        }
+    };
+#pragma unroll
+    for (int cc = 0; cc < DSLOT - 1; ++cc)
+        if (cc < NCH) issue(cc);
 
     f4v hw[WIN], sw[WIN];
 #pragma unroll
     for (int j = 0; j < WIN; ++j) hw[j] = sw[j] = f4v{0.f, 0.f, 0.f, 0.f};
-    f4v xn[SCH], en[SCH], yn[SCH];
-    auto load_chunk = [&](int cc) {
+    float racc = 0.f;
+
+    auto read_win = [&](const float* row, float (&w)[12]) {
 #pragma unroll
-        for (int e = 0; e < SCH; ++e) {
-            const int gi = s0 - 2 * R + SCH * cc + e;
-            const int gr = reflect_clamp(gi, H);
-            const int gy = min(max(gi - R, 0), H - 1);
-            xn[e] = *reinterpret_cast<const f4v*>(xp + gr * SWID + col);
-            en[e] = *reinterpret_cast<const f4v*>(ep + gr * SWID + col);
-            yn[e] = *reinterpret_cast<const f4v*>(yp + gy * SWID + col);
+        for (int q = 0; q < 3; ++q) {
+            const f4v t = *reinterpret_cast<const f4v*>(row + col - SPAD + 4 * q);
+            w[4 * q] = t.x, w[4 * q + 1] = t.y, w[4 * q + 2] = t.z, w[4 * q + 3] = t.w;
         }
     };
-    load_chunk(0);
-    float racc = 0.f;
-    for (int cc = 0; cc < NCH; ++cc) {
-        f4v xc[SCH], ec[SCH], yc[SCH];
-#pragma unroll
-        for (int e = 0; e < SCH; ++e) xc[e] = xn[e], ec[e] = en[e], yc[e] = yn[e];
-        if (cc + 1 < NCH) load_chunk(cc + 1);
 
-        // ---- 1: x0 rows through the exchange row, horizontal A ----
+    auto body = [&](auto phc, int cc) {
+        constexpr int PH = decltype(phc)::value;
+        auto ix = [](int j) { return (j + PH * CH) % WIN; };  // logical window row -> register slot
+        // slot of chunk cc-1 is refilled below: its exchange reads must have returned
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (cc + DSLOT - 1 < NCH) issue(cc + DSLOT - 1);
+        {   // retire chunk cc's DMAs: younger = later chunks' DMAs + v stores issued since
+            const int later = min(DSLOT - 1, NCH - 1 - cc);
+            const int st = max(0, min(cc, DSLOT - 1) - max(0, C3 - (cc - min(cc, DSLOT - 1))));
+            wait_vm(DROWS * later + CH * st);
+        }
+        float* xrow = ring + (cc % DSLOT) * DROWS * SWID;  // x rows, then exchange rows
+        const float* erow = xrow + CH * SWID;
+        const float* yrow = xrow + 2 * CH * SWID;
+
+        // ---- 1: x0 (in place), horizontal A ----
+        f4v x0[CH];
 #pragma unroll
-        for (int j = 0; j < 2 * R; ++j) hw[j] = hw[j + SCH];
-        wave_lds_sync();  // previous chunk's reads of xr are done before the overwrite
-#pragma unroll
-        for (int e = 0; e < SCH; ++e)
-            *reinterpret_cast<f4v*>(&xr[e][SPAD + col]) = (xc[e] - k * ec[e]) * inv_a;
+        for (int e = 0; e < CH; ++e) {
+            const f4v xv = *reinterpret_cast<const f4v*>(xrow + e * SWID + col);
+            const f4v ev = *reinterpret_cast<const f4v*>(erow + e * SWID + col);
+            x0[e] = (xv - k * ev) * inv_a;
+        }
         wave_lds_sync();
 #pragma unroll
-        for (int e = 0; e < SCH; ++e) {
+        for (int e = 0; e < CH; ++e) *reinterpret_cast<f4v*>(xrow + e * SWID + col) = x0[e];
+        wave_lds_sync();
+#pragma unroll
+        for (int e = 0; e < CH; ++e) {
             float w[12];
+            read_win(xrow + e * SWID, w);
 #pragma unroll
-            for (int q = 0; q < 3; ++q) {
-                const f4v t = *reinterpret_cast<const f4v*>(&xr[e][col + 4 * q]);
-                w[4 * q] = t.x, w[4 * q + 1] = t.y, w[4 * q + 2] = t.z, w[4 * q + 3] = t.w;
-            }
-#pragma unroll
-            for (int i = 1; i <= R; ++i) {  // reflect padding at the plane's side edges
+            for (int i = 1; i <= R; ++i) {  // reflect padding at the side edges
                 w[SPAD - i] = lane == 0 ? w[SPAD + i] : w[SPAD - i];
                 w[SPAD + 3 + i] = lane == 63 ? w[SPAD + 3 - i] : w[SPAD + 3 + i];
             }
@@ -543,60 +623,59 @@ __global__ __launch_bounds__(64 * SWPB) void k_blur_dps_stream(
                 for (int d = 0; d < K; ++d) acc = fmaf(tk[d], w[SPAD - R + q + d], acc);
                 h[q] = acc;
             }
-            hw[2 * R + e] = h;
+            hw[ix(2 * R + e)] = h;
         }
-        if (cc < C2) continue;
+        if (cc < C2) return;
 
-        // ---- 2: vertical A, residual, S = c r (0 off the image), |r|^2 ----
+        // ---- 2: vertical A, residual, S, |r|^2 ----
 #pragma unroll
-        for (int j = 0; j < 2 * R; ++j) sw[j] = sw[j + SCH];
-#pragma unroll
-        for (int e = 0; e < SCH; ++e) {
-            const int gz = s0 - 3 * R + SCH * cc + e;
+        for (int e = 0; e < CH; ++e) {
+            const int gz = s0 - 3 * R + CH * cc + e;
             f4v z = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-            for (int d = 0; d < K; ++d) z += tk[d] * hw[e + d];
-            const f4v rr = yc[e] - z;
+            for (int d = 0; d < K; ++d) z += tv[d] * hw[ix(e + d)];
+            const f4v rr = *reinterpret_cast<const f4v*>(yrow + e * SWID + col) - z;
             const bool in = (unsigned)gz < (unsigned)H;
-            sw[2 * R + e] = in ? rr * gs : f4v{0.f, 0.f, 0.f, 0.f};
+            sw[ix(2 * R + e)] = in ? rr * gs : f4v{0.f, 0.f, 0.f, 0.f};
             if (gz >= s0 && gz < s0 + SSEG)
                 racc += (rr.x * rr.x + rr.y * rr.y) + (rr.z * rr.z + rr.w * rr.w);
         }
-        if (cc < R) continue;
+        if (cc < C3) return;
 
-        // ---- 3: vertical A^T (fold-corrected taps on edge rows) ----
-        const int gv0 = s0 - 4 * R + SCH * cc;
-        f4v vv[SCH];
-        if (gv0 > R && gv0 + SCH - 1 < H - 1 - R) {
+        // ---- 3: vertical A^T ----
+        const int gv0 = s0 - 4 * R + CH * cc;
+        f4v vv[CH];
+        if (gv0 > R && gv0 + CH - 1 < H - 1 - R) {
 #pragma unroll
-            for (int e = 0; e < SCH; ++e) {
+            for (int e = 0; e < CH; ++e) {
                 f4v u4 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-                for (int i = 0; i < K; ++i) u4 += tk[i] * sw[e + 2 * R - i];
+                for (int i = 0; i < K; ++i) u4 += tv[i] * sw[ix(e + 2 * R - i)];
                 vv[e] = u4;
             }
         } else {
 #pragma unroll
-            for (int e = 0; e < SCH; ++e) {
+            for (int e = 0; e < CH; ++e) {
                 f4v u4 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-                for (int o = -R; o <= R; ++o) u4 += adj_tap(tl, R, H, gv0 + e, o) * sw[e + R + o];
+                for (int o = -R; o <= R; ++o) u4 += adj_tap(tlv, R, H, gv0 + e, o) * sw[ix(e + R + o)];
                 vv[e] = u4;
             }
         }
 
-        // ---- 4: horizontal A^T through the exchange row, store v ----
+        // ---- 4: horizontal A^T through the exchange rows, store v ----
         wave_lds_sync();
 #pragma unroll
-        for (int e = 0; e < SCH; ++e) *reinterpret_cast<f4v*>(&xr[e][SPAD + col]) = vv[e];
+        for (int e = 0; e < CH; ++e) *reinterpret_cast<f4v*>(xrow + e * SWID + col) = vv[e];
         wave_lds_sync();
 #pragma unroll
-        for (int e = 0; e < SCH; ++e) {
+        for (int e = 0; e < CH; ++e) {
             float w[12];
+            read_win(xrow + e * SWID, w);
 #pragma unroll
-            for (int q = 0; q < 3; ++q) {
-                const f4v t = *reinterpret_cast<const f4v*>(&xr[e][col + 4 * q]);
-                w[4 * q] = t.x, w[4 * q + 1] = t.y, w[4 * q + 2] = t.z, w[4 * q + 3] = t.w;
+            for (int i = 0; i < SPAD; ++i) {  // V = 0 off the image
+                w[i] = lane == 0 ? 0.f : w[i];
+                w[SPAD + 4 + i] = lane == 63 ? 0.f : w[SPAD + 4 + i];
             }
             f4v o4;
 #pragma unroll
@@ -606,9 +685,13 @@ __global__ __launch_bounds__(64 * SWPB) void k_blur_dps_stream(
                 for (int o = -R; o <= R; ++o) acc = fmaf(th[q][o + R], w[SPAD + q + o], acc);
                 o4[q] = acc;
             }
-            *reinterpret_cast<f4v*>(op_out + (gv0 + e) * SWID + col) = o4;
+            *reinterpret_cast<f4v*>(op_out + prow(gv0 + e) * SWID + col) = o4;
         }
-    }
+    };
+
+    int cc = 0;
+    for (; cc + PER <= NCH; cc += PER) phases<0, PER>(body, cc);
+    phases<0, NCH % PER>(body, cc);
     racc = wave_sum(racc);
     if (lane == 0) partial[(int64_t)b * P + c * nseg + sg] = racc;
 }
@@ -634,12 +717,12 @@ static int launch_blur(const sp_op* op, const float* in, const float* eps, const
     const int P = static_cast<int>(blur_partials(op));
     if (MODE == MODE_DPS && blur_streams(op)) {
         const int64_t units = (int64_t)op->channels * (op->height / SSEG) * batch;
-        const dim3 sgrid(static_cast<unsigned>((units + SWPB - 1) / SWPB));
         switch (op->radius) {
 #define SP_STREAM_CASE(RR)                                                                      \
     case RR:                                                                                    \
-        launch_w(TK_DPS_RESIDUAL, (double)batch, k_blur_dps_stream<RR>, sgrid, dim3(64 * SWPB), s, \
-                 *op, in, eps, y, static_cast<int>(y_div), a, k, gs, out, partial, P,          \
+        launch_w(TK_DPS_RESIDUAL, (double)batch, k_blur_dps_dma<RR>,                            \
+                 dim3(static_cast<unsigned>(units)), dim3(64), s, *op, in, eps, y,              \
+                 static_cast<int>(y_div), a, k, gs, out, partial, P,                            \
                  static_cast<unsigned>(units), sched, cursor);                                  \
         break;
             SP_STREAM_CASE(1) SP_STREAM_CASE(2) SP_STREAM_CASE(3) SP_STREAM_CASE(4)

@@ -224,16 +224,23 @@ def test_dispatch_packet_timing(cuda):
     assert s["dps_update"]["samples"] == 3 * b
 
 
-@pytest.mark.parametrize("shape,ks,batch,ydiv", [((3, 32, 256), 9, 2, 1), ((2, 64, 256), 9, 3, 3),
-                                                 ((1, 96, 256), 5, 2, 1), ((3, 32, 256), 3, 1, 1),
-                                                 ((1, 64, 256), 7, 2, 2), ((3, 256, 256), 9, 2, 1)])
-def test_blur_streaming_residual_pass(cuda, shape, ks, batch, ydiv):
-    """The streaming blur pass (256-column planes, one wave per row segment) against the
-    closed form with the fold-corrected reflect adjoint: every radius it serves, one and
-    several segments per plane, shared observations."""
+@pytest.mark.parametrize("shape,ks,batch,ydiv,asym", [
+    ((3, 32, 256), 9, 2, 1, False), ((2, 64, 256), 9, 3, 3, False), ((1, 96, 256), 5, 2, 1, False),
+    ((3, 32, 256), 3, 1, 1, False), ((1, 64, 256), 7, 2, 2, False), ((3, 256, 256), 9, 2, 1, False),
+    ((2, 96, 256), 9, 2, 1, True), ((1, 64, 256), 5, 1, 1, True)])
+def test_blur_streaming_residual_pass(cuda, shape, ks, batch, ydiv, asym):
+    """The streaming blur pass (256-column planes, one wave per row segment, odd segments
+    swept bottom-up) against the closed form with the fold-corrected reflect adjoint: every
+    radius it serves, one and several segments per plane, shared observations, and
+    asymmetric taps (which a mirrored sweep must reverse in its vertical passes)."""
     torch.manual_seed(1)
     op = GaussianBlurOperator(shape, ks, 3.0).to(cuda)
-    apply_np, adjoint_np = oblur.blur_ops(shape, oblur.taps(ks, 3.0))
+    k1d = oblur.taps(ks, 3.0)
+    if asym:
+        k1d = np.random.default_rng(ks).uniform(0.05, 1.0, ks).astype(np.float32)
+        k1d /= k1d.sum()
+        op.taps.copy_(torch.from_numpy(k1d))
+    apply_np, adjoint_np = oblur.blur_ops(shape, k1d)
     lib = _hip.load_library()
     desc = op.hip_descriptor()
     n = math.prod(shape)

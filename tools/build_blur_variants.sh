@@ -6,7 +6,7 @@ cd "$(dirname "$0")/.."
 make -s
 mkdir -p build/variants
 OTHERS=$(ls build/*.o | grep -v sp_blur.o)
-for v in "tile:-DSP_BLUR_STREAM=0" "seg32:-DSP_BLUR_SEG=32" "seg64:-DSP_BLUR_SEG=64" "seg32w1:-DSP_BLUR_SEG=32 -DSP_BLUR_WPB=1" "seg64w1:-DSP_BLUR_SEG=64 -DSP_BLUR_WPB=1" "seg16w1:-DSP_BLUR_SEG=16 -DSP_BLUR_WPB=1"; do
+for v in "tile:-DSP_BLUR_STREAM=0" "seg32:-DSP_BLUR_SEG=32" "seg64:-DSP_BLUR_SEG=64"; do
   name=${v%%:*}; flags=${v#*:}
   ( /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 $flags -c samplers_amd/csrc/sp_blur.hip \
       -o build/variants/blur_$name.o &&
