@@ -198,6 +198,26 @@ int sp_stochastic_resample(const float* pseudo_x0, const float* x_t, int64_t bat
 /* In-place AdamW update of `count` parameters. */
 int sp_adamw_step(float* param, const float* grad, float* exp_avg, float* exp_avg_sq,
                   int64_t count, const sp_adamw_coefs* c, sp_stream_t stream);
+/* The same with a device-side stop flag: no-op once *stop != 0. */
+int sp_adamw_step_until(float* param, const float* grad, float* exp_avg, float* exp_avg_sq,
+                        int64_t count, const sp_adamw_coefs* c, const int32_t* stop,
+                        sp_stream_t stream);
+/* One iteration of ReSample's pixel-space hard data consistency (resample_kernels.py:32-54:
+ * AdamW(lr=1e-2) on MSELoss(y, A x)) for IDENTITY / INPAINT / MASK in one pass over x:
+ *   r = y[b/y_div] - A x,  g = A^T(grad_scale * r)  (grad_scale = -2/M, M = elements of the
+ *   MSE mean), AdamW update of x / exp_avg / exp_avg_sq in place, r^2 partials
+ *   (sp_rsq_partials(op) per sample) of the loss at x before the update.
+ * No-op once *stop != 0 (stop may be NULL).  BLUR: SP_EUNSUPPORTED (the caller composes
+ * sp_op_apply / sp_residual_grad / sp_op_adjoint / sp_adamw_step_until). */
+int sp_pixel_opt_step(const sp_op* op, float* x, float* exp_avg, float* exp_avg_sq,
+                      const float* y, int64_t batch, int64_t y_div, float grad_scale,
+                      const sp_adamw_coefs* c, const int32_t* stop, float* rsq_partial,
+                      sp_stream_t stream);
+/* Early-stop test of the optimisation loops (resample_kernels.py:50-51):
+ *   loss = (sum of count partials, fixed order) / total;  *loss_out = loss (may be NULL);
+ *   *stop = 1 if loss < threshold (compared in double).  Skipped once *stop != 0. */
+int sp_opt_check(const float* partials, int64_t count, float total, double threshold,
+                 int32_t* stop, float* loss_out, sp_stream_t stream);
 
 /* ---- prior building blocks (SURVEY.md §8b "groupnorm_silu_fwd/bwd") -------------------
  * GroupNorm over NCHW x (n, channels, hw = H*W) with `groups` groups, eps, optional

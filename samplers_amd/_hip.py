@@ -102,6 +102,11 @@ SIGNATURES = {
     "sp_stochastic_resample": (ctypes.c_int, [_P, _P, _I64, _I64, _F, _F, _P, _U64, _I64, _I64, _P,
                                               _P]),
     "sp_adamw_step": (ctypes.c_int, [_P, _P, _P, _P, _I64, ctypes.POINTER(SpAdamWCoefs), _P]),
+    "sp_adamw_step_until": (ctypes.c_int, [_P, _P, _P, _P, _I64, ctypes.POINTER(SpAdamWCoefs), _P,
+                                           _P]),
+    "sp_pixel_opt_step": (ctypes.c_int, [_OPP, _P, _P, _P, _P, _I64, _I64, _F,
+                                         ctypes.POINTER(SpAdamWCoefs), _P, _P, _P]),
+    "sp_opt_check": (ctypes.c_int, [_P, _I64, _F, ctypes.c_double, _P, _P, _P]),
     "sp_conv3x3_supported": (ctypes.c_int, [ctypes.c_int32] * 4),
     "sp_conv3x3_packed_size": (_I64, [ctypes.c_int32, ctypes.c_int32]),
     "sp_conv3x3_pack": (ctypes.c_int, [_P, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, _P, _P]),

@@ -184,11 +184,22 @@ __global__ __launch_bounds__(kBlock) void k_stochastic_resample(
     }
 }
 
-// torch.optim.AdamW step (decoupled weight decay, no amsgrad), in place
+// torch.optim.AdamW update of one parameter (decoupled weight decay, no amsgrad)
+__device__ __forceinline__ void adamw_1(float& p, float g, float& m, float& v, const sp_adamw_coefs& c) {
+    p = p * c.decay;                                // p *= 1 - lr * weight_decay
+    m = m + (1.f - c.beta1) * (g - m);              // exp_avg.lerp_(g, 1 - beta1)
+    v = v * c.beta2 + (1.f - c.beta2) * g * g;      // exp_avg_sq.mul_(beta2).addcmul_
+    const float denom = sqrtf(v) / c.bc2_sqrt + c.eps;
+    p = p - c.step_size * m / denom;
+}
+
+// torch.optim.AdamW step, in place; a set *stop makes it a no-op (device-side early stop)
 template <int V>
 __global__ __launch_bounds__(kBlock) void k_adamw(float* __restrict__ p, const float* __restrict__ g,
                                                   float* __restrict__ m, float* __restrict__ v,
-                                                  int64_t count, sp_adamw_coefs c) {
+                                                  int64_t count, sp_adamw_coefs c,
+                                                  const int32_t* __restrict__ stop) {
+    if (stop && *stop) return;
     const int64_t stride = (int64_t)gridDim.x * kBlock * V;
     for (int64_t j = ((int64_t)blockIdx.x * kBlock + threadIdx.x) * V; j < count; j += stride) {
         float pv[V], gv[V], mv[V], vv[V];
@@ -197,16 +208,84 @@ __global__ __launch_bounds__(kBlock) void k_adamw(float* __restrict__ p, const f
         load_v<V>(m + j, mv);
         load_v<V>(v + j, vv);
 #pragma unroll
-        for (int e = 0; e < V; ++e) {
-            pv[e] = pv[e] * c.decay;  // p *= 1 - lr * weight_decay
-            mv[e] = mv[e] + (1.f - c.beta1) * (gv[e] - mv[e]);         // exp_avg.lerp_(g, 1-b1)
-            vv[e] = vv[e] * c.beta2 + (1.f - c.beta2) * gv[e] * gv[e];  // mul_(b2).addcmul_
-            const float denom = sqrtf(vv[e]) / c.bc2_sqrt + c.eps;
-            pv[e] = pv[e] - c.step_size * mv[e] / denom;
-        }
+        for (int e = 0; e < V; ++e) adamw_1(pv[e], gv[e], mv[e], vv[e], c);
         store_v<V>(p + j, pv);
         store_v<V>(m + j, mv);
         store_v<V>(v + j, vv);
+    }
+}
+
+// One iteration of ReSample's pixel-space hard data consistency for the elementwise
+// operators (resample_kernels.py:32-54: AdamW(lr=1e-2) on MSE(y, A x)), one pass over x:
+// r = y - A x, g = A^T (gs r) with gs = -2/M (the MSE gradient w.r.t. A x), the AdamW
+// update of x in place, and the iteration's r^2 partials (the loss of x before the
+// update, as the reference's measurement_loss).  A set *stop makes it a no-op.
+template <int OPK, int V>
+__global__ __launch_bounds__(kBlock) void k_pixel_opt(sp_op op, float* __restrict__ x,
+                                                      float* __restrict__ m, float* __restrict__ v,
+                                                      const float* __restrict__ y, int64_t y_div,
+                                                      float gs, sp_adamw_coefs c,
+                                                      const int32_t* __restrict__ stop,
+                                                      float* __restrict__ partial, int P) {
+    __shared__ float red[4];
+    if (stop && *stop) return;
+    const int64_t b = blockIdx.y, n = op.n;
+    float* xb = x + b * n;
+    float* mb = m + b * n;
+    float* vb = v + b * n;
+    const float* yb = y + (b / y_div) * op.m;
+    const int64_t j0 = (int64_t)blockIdx.x * kIter * (kBlock * V) + threadIdx.x * V;
+    float acc = 0.f;
+#pragma unroll
+    for (int it = 0; it < kIter; ++it) {
+        const int64_t j = j0 + it * (kBlock * V);
+        if (j >= n) break;
+        float xv[V], mv[V], vv[V], yv[V];
+        load_v<V>(xb + j, xv);
+        load_v<V>(mb + j, mv);
+        load_v<V>(vb + j, vv);
+        uint32_t bits = 0xFu;
+        if constexpr (OPK == SP_OP_INPAINT) {
+            int64_t r;
+            inpaint_lookup(op, j, bits, r);
+#pragma unroll
+            for (int e = 0; e < V; ++e) yv[e] = ((bits >> e) & 1u) ? yb[r++] : 0.f;
+        } else {
+            load_v<V>(yb + j, yv);
+            if constexpr (OPK == SP_OP_MASK) bits = mask_bits(op, j);
+        }
+#pragma unroll
+        for (int e = 0; e < V; ++e) {
+            const bool kept = (bits >> e) & 1u;
+            const float r = yv[e] - (kept ? xv[e] : 0.f);
+            if (OPK != SP_OP_INPAINT || kept) acc += r * r;
+            adamw_1(xv[e], kept ? gs * r : 0.f, mv[e], vv[e], c);
+        }
+        store_v<V>(xb + j, xv);
+        store_v<V>(mb + j, mv);
+        store_v<V>(vb + j, vv);
+    }
+    const float t = block_sum(acc, red);
+    if (threadIdx.x == 0) partial[b * P + blockIdx.x] = t;
+}
+
+// Early-stop test of the optimisation loops (resample_kernels.py:50-51): loss = (sum of
+// the count partials) / total; *stop = 1 once loss < threshold (compared in double, as
+// the reference compares measurement_loss.item() with eps**2).  Runs after the
+// iteration's update, so the stopping iteration's step is kept, as in the reference.
+__global__ __launch_bounds__(kBlock) void k_opt_check(const float* __restrict__ p, int64_t count,
+                                                      float total, double threshold,
+                                                      int32_t* __restrict__ stop,
+                                                      float* __restrict__ loss_out) {
+    __shared__ float red[4];
+    if (*stop) return;
+    float s = 0.f;
+    for (int64_t i = threadIdx.x; i < count; i += kBlock) s += p[i];
+    const float t = block_sum(s, red);
+    if (threadIdx.x == 0) {
+        const float loss = t / total;
+        if (loss_out) *loss_out = loss;
+        if ((double)loss < threshold) *stop = 1;
     }
 }
 
@@ -320,17 +399,55 @@ int sp_stochastic_resample(const float* pseudo_x0, const float* x_t, int64_t bat
 
 int sp_adamw_step(float* param, const float* grad, float* exp_avg, float* exp_avg_sq,
                   int64_t count, const sp_adamw_coefs* c, sp_stream_t stream) {
+    return sp_adamw_step_until(param, grad, exp_avg, exp_avg_sq, count, c, nullptr, stream);
+}
+
+int sp_adamw_step_until(float* param, const float* grad, float* exp_avg, float* exp_avg_sq,
+                        int64_t count, const sp_adamw_coefs* c, const int32_t* stop,
+                        sp_stream_t stream) {
     if (!param || !grad || !exp_avg || !exp_avg_sq || !c || count <= 0) return SP_EINVAL;
     hipStream_t s = static_cast<hipStream_t>(stream);
     const bool v4 = count % 4 == 0 && aligned16(param) && aligned16(grad) && aligned16(exp_avg) &&
                     aligned16(exp_avg_sq);
     if (v4)
         launch(0, k_adamw<4>, dim3(grid_for(count, 4, 1)), dim3(kBlock), s, param, grad, exp_avg,
-               exp_avg_sq, count, *c);
+               exp_avg_sq, count, *c, stop);
     else
         launch(0, k_adamw<1>, dim3(grid_for(count, 1, 1)), dim3(kBlock), s, param, grad, exp_avg,
-               exp_avg_sq, count, *c);
+               exp_avg_sq, count, *c, stop);
     return check_launch("sp_adamw_step");
+}
+
+int sp_pixel_opt_step(const sp_op* op, float* x, float* exp_avg, float* exp_avg_sq,
+                      const float* y, int64_t batch, int64_t y_div, float grad_scale,
+                      const sp_adamw_coefs* c, const int32_t* stop, float* rsq_partial,
+                      sp_stream_t stream) {
+    if (!valid_op(op) || !x || !exp_avg || !exp_avg_sq || !y || !c || !rsq_partial ||
+        batch <= 0 || batch > 65535 || y_div <= 0)
+        return SP_EINVAL;
+    if (op->kind == SP_OP_BLUR) return SP_EUNSUPPORTED;  // composed by the caller
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const int P = static_cast<int>(tiles_elementwise(op->n));
+    const dim3 grid(P, static_cast<unsigned>(batch));
+    const bool v4 = op->n % 4 == 0;
+#define SP_PO(OPK, V)                                                                         \
+    launch(0, k_pixel_opt<OPK, V>, grid, dim3(kBlock), s, *op, x, exp_avg, exp_avg_sq, y, y_div, \
+           grad_scale, *c, stop, rsq_partial, P)
+    switch (op->kind) {
+        case SP_OP_IDENTITY: if (v4) SP_PO(SP_OP_IDENTITY, 4); else SP_PO(SP_OP_IDENTITY, 1); break;
+        case SP_OP_INPAINT: if (v4) SP_PO(SP_OP_INPAINT, 4); else SP_PO(SP_OP_INPAINT, 1); break;
+        default: if (v4) SP_PO(SP_OP_MASK, 4); else SP_PO(SP_OP_MASK, 1); break;
+    }
+#undef SP_PO
+    return check_launch("sp_pixel_opt_step");
+}
+
+int sp_opt_check(const float* partials, int64_t count, float total, double threshold,
+                 int32_t* stop, float* loss_out, sp_stream_t stream) {
+    if (!partials || !stop || count <= 0 || !(total > 0.f)) return SP_EINVAL;
+    launch(0, k_opt_check, dim3(1), dim3(kBlock), static_cast<hipStream_t>(stream), partials,
+           count, total, threshold, stop, loss_out);
+    return check_launch("sp_opt_check");
 }
 
 }  // extern "C"

@@ -222,3 +222,56 @@ def test_resample_requires_latent_network(cuda):
 
     with pytest.raises(TypeError, match="latent diffusion model"):
         ReSampleSampler(si.make_samplers_amd_net("linear", 3))
+
+
+@pytest.mark.parametrize("kind", ["identity", "inpaint", "mask", "blur"])
+def test_pixel_optimization_device_stop_matches_reference_loop(cuda, kind):
+    """ReSample's pixel-space hard consistency (resample_kernels.py:32-54) with the stopping
+    test on the device (sp_pixel_opt_step / sp_adamw_step_until + sp_opt_check) runs exactly
+    the iterations of the reference loop (torch AdamW + MSELoss + .item() per iteration):
+    the threshold is placed between two consecutive losses of the reference, at an
+    iteration that is not a multiple of the host's flag-check interval."""
+    from samplers_amd.operators import GaussianBlurOperator, get_mask_random
+    from samplers_amd.samplers.resample import ReSampleSampler, _Consistency
+
+    torch.manual_seed(0)
+    shape, b = (3, 16, 24), 2
+    if kind == "identity":
+        op = IdentityOperator(shape)
+    elif kind == "blur":
+        op = GaussianBlurOperator(shape, 5, 1.5).to(cuda)
+    else:
+        op = InpaintingOperator(shape, get_mask_random(shape, 0.4, seed=2),
+                                flatten=(kind == "inpaint")).to(cuda)
+    x_true = torch.rand(b, *shape) * 2 - 1
+    x0 = torch.randn(b, *shape)
+    y = op.apply(x_true.to(cuda)).reshape(b, -1).cpu()
+    total = y.numel()
+
+    def reference(n_iter, thr=None):
+        opt = x0.clone().requires_grad_()
+        adam = torch.optim.AdamW([opt], lr=1e-2)
+        losses = []
+        for _ in range(n_iter):
+            adam.zero_grad()
+            loss = torch.nn.MSELoss()(y, op.apply(opt.to(cuda)).reshape(b, -1).cpu())
+            loss.backward()
+            adam.step()
+            losses.append(loss.item())
+            if thr is not None and loss.item() < thr:
+                break
+        return opt.detach(), losses
+
+    _, losses = reference(40)
+    stop_at = 22  # 0-based iteration whose loss first falls below the threshold
+    assert losses[stop_at] < losses[stop_at - 1]
+    thr = 0.5 * (losses[stop_at] + losses[stop_at - 1])
+    assert all(v >= thr for v in losses[:stop_at])
+    ref, ref_losses = reference(2000, thr)
+    assert len(ref_losses) == stop_at + 1
+    cons = _Consistency(op, y.to(cuda), 1)
+    out = ReSampleSampler._pixel_optimization(None, x0.to(cuda), cons, total, thr ** 0.5, 2000)
+    err = float((out.cpu() - ref).norm() / ref.norm())
+    one_more, _ = reference(stop_at + 2)
+    assert err < 1e-5, err
+    assert float((one_more - ref).norm() / ref.norm()) > 100 * max(err, 1e-7)
