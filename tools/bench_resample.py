@@ -1,0 +1,148 @@
+"""ReSample benchmark (BASELINE.json configs[4], "config 5"): SD1.5 latent, 512², Poisson noise.
+
+    python tools/bench_resample.py [--batch 32 --steps 3 --warmup 2]
+
+Config 5 is 256 samples sharded over 8 GPUs: 32 per GPU, which is what one process here
+runs (the batch shards with no data-path collective; the batch-global losses are 8-byte
+all-reduces).  Workload: ReSample (resample.py:131-228) with IdentityOperator on 3x512x512,
+PoissonNoise(rate=1.0) (config 5 fixes no rate), the SD 1.5 VAE architecture
+(83.65 M parameters) + 4x64x64 latent UNet, random weights with fixed seeds, fp32.
+
+A full ReSample run (100 steps, default max_optimization_iters=2000) is 98 main-loop
+iterations plus time-travel blocks, three pixel-space and four latent-space hard
+consistency solves; at B = 32 it runs for tens of minutes, so this tool times its pieces
+on the same tensors and reports each:
+
+  step          one main-loop iteration over the batch: latent UNet (epsilon-form DDIM,
+                HIP sp_ddim_eps_step) + DPS conditioning (VAE decode forward + VJP, HIP
+                norm gradient).  "value" = batch x steps / s of these iterations, the
+                metric's unit (posterior samples/sec)
+  pixel_iter    one pixel-space AdamW iteration (sp_pixel_opt_step + sp_opt_check; the
+                host reads the device stop flag every 16 iterations)
+  latent_iter   one latent-space AdamW iteration (VAE decode forward + VJP, HIP MSE
+                gradient and AdamW)
+
+Prints one JSON line.
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT))
+import samplers_amd  # noqa: E402,F401
+
+import torch  # noqa: E402
+
+sys.path.insert(0, str(ROOT / "tools"))
+from bench_psld import VAE_FLOP_PER_SAMPLE, heartbeat  # noqa: E402
+
+DECODE_FLOP_PER_SAMPLE = 4.96e12  # decode forward + VJP at 512²
+
+
+def timed(fn, reps: int, label: str) -> float:
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(reps):
+        fn()
+        torch.cuda.synchronize()
+        print(f"[resample] {label} {k + 1}/{reps} at {time.perf_counter() - t0:.1f}s",
+              file=sys.stderr, flush=True)
+    return (time.perf_counter() - t0) / reps
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("--batch", type=int, default=32)
+    p.add_argument("--image", type=int, default=512)
+    p.add_argument("--steps", type=int, default=3)
+    p.add_argument("--warmup", type=int, default=2)
+    p.add_argument("--pixel-iters", type=int, default=200)
+    p.add_argument("--latent-iters", type=int, default=3)
+    p.add_argument("--heartbeat", default="gpurun_out/resample_heartbeat.log")
+    args = p.parse_args()
+    Path(args.heartbeat).parent.mkdir(parents=True, exist_ok=True)
+    heartbeat(Path(args.heartbeat))
+    dev = torch.device("cuda:0")
+
+    from samplers_amd import _hip
+    from samplers_amd.networks.latent import LatentDiffusionNetwork
+    from samplers_amd.noise import PoissonNoise
+    from samplers_amd.operators import IdentityOperator
+    from samplers_amd.samplers.dps import initial_sample
+    from samplers_amd.samplers.resample import ReSampleSampler, _Consistency
+
+    _hip.load_library()
+    shape = (3, args.image, args.image)
+    b = args.batch
+    op = IdentityOperator(shape)
+    gen = torch.Generator().manual_seed(1000)
+    x_true = torch.rand((b, *shape), generator=gen) * 2 - 1
+    noise = PoissonNoise(1.0)
+    y = noise.sample(tuple(x_true.shape), generator=gen) + x_true  # y = A x + Poisson noise
+    y = y.to(dev)
+    net = LatentDiffusionNetwork.from_config(seed=0, device=dev)
+    net.set_sampling_parameters(100, batch_size=b)
+    lat = tuple(net.get_latent_shape(shape))
+    sampler = ReSampleSampler(net)
+    cons = _Consistency(op, y.reshape(b, -1), 1)
+    total = b * cons.m
+    seed = 20260101
+    z = initial_sample((b, *lat), dev, rng="philox", seed=seed, sample_offset=0, noise_fn=None)
+    ts, acp = net.timesteps_host, net.alphas_cumprod_host
+    it = iter(range(len(ts) - 1, 1, -1))
+
+    def one():
+        nonlocal z
+        i = next(it)
+        z_next, pseudo, sqrt_a = sampler._ddim_eps(z, ts[i], ts[i - 1], 1.0, None, seed, i, 0)
+        z = sampler._dps_conditioning(z_next, pseudo, sqrt_a, float(acp[ts[i]]), cons)
+
+    t0 = time.perf_counter()
+    for k in range(args.warmup):
+        one()
+        torch.cuda.synchronize()
+        print(f"[resample] warmup {k + 1} done at {time.perf_counter() - t0:.1f}s",
+              file=sys.stderr, flush=True)
+    torch.cuda.reset_peak_memory_stats()
+    step_s = timed(one, args.steps, "step")
+    if not torch.isfinite(z).all():
+        raise SystemExit("non-finite latents")
+
+    x_pix = net.decode(z, differentiable=False).reshape(b, *shape).contiguous()
+    sampler._pixel_optimization(x_pix, cons, total, 1e-3, 16)  # warm
+    pix_s = timed(lambda: sampler._pixel_optimization(x_pix, cons, total, 0.0, args.pixel_iters),
+                  1, "pixel") / args.pixel_iters
+    sampler._latent_optimization(z, cons, total, 1e-3, 1)  # warm
+    lat_s = timed(lambda: sampler._latent_optimization(z, cons, total, 0.0, args.latent_iters),
+                  1, "latent") / args.latent_iters
+
+    n = b * shape[0] * args.image * args.image
+    print(json.dumps({
+        "metric": "posterior samples/sec (batch×steps/s), ReSample SD1.5 512² Poisson "
+                  "(BASELINE configs[4], 32 per GPU of 256 over 8)",
+        "value": round(b * args.steps / (step_s * args.steps), 4),
+        "unit": "samples/sec (batch×steps/s)",
+        "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(step_s * 1e3, 2), "higher_is_better": True, "dtype": "f32",
+        "data": "synthetic (seeded U(-1,1) images, Poisson(rate=1) noise); random-init SD1.5 VAE "
+                "architecture + 4x64x64 latent UNet",
+        "config": {"workload": f"ReSample + Identity + PoissonNoise(1.0), 3x{args.image}²",
+                   "batch": b, "schedule": "100-step PNDM (resample.py:52)"},
+        "decode_vjp_tflops": round(DECODE_FLOP_PER_SAMPLE * b / step_s / 1e12, 2),
+        "pixel_iter_ms": round(pix_s * 1e3, 4),
+        "pixel_iter_GBps": round(4 * 7 * n / pix_s / 1e9, 1),  # x,m,v,y read; x,m,v written
+        "latent_iter_ms": round(lat_s * 1e3, 2),
+        "latent_iter_tflops": round(DECODE_FLOP_PER_SAMPLE * b / lat_s / 1e12, 2),
+        "peak_gib": round(torch.cuda.max_memory_allocated() / 2**30, 1),
+        "vae_flop_per_sample_step": VAE_FLOP_PER_SAMPLE,
+    }), flush=True)
+
+
+if __name__ == "__main__":
+    main()
