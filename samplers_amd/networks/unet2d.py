@@ -92,6 +92,32 @@ class ResnetBlock2D(nn.Module):
         return x + h
 
 
+def attention_backend() -> str:
+    """``SAMPLERS_AMD_ATTN``: ``gemm`` (default: scores materialised, batched fp32 GEMMs +
+    softmax, autograd through them) or ``sdpa`` (``F.scaled_dot_product_attention``)."""
+    import os
+
+    return os.environ.get("SAMPLERS_AMD_ATTN", "gemm").lower()
+
+
+def attention(q: Tensor, k: Tensor, v: Tensor) -> Tensor:
+    """softmax(q k^T / sqrt(d)) v over (batch, heads, tokens, d).
+
+    The priors' attention has one head of d = 512 (the VAE mid blocks at 64x64 = 4096
+    tokens, the DDPM UNet at 16x16) or 8 heads of 64 (the latent UNet).  At d = 512 the
+    fused flash kernels of PyTorch-ROCm run fp32 at 54 TFLOP/s forward and 25 backward
+    (their Q/K/V tiles do not fit on chip); materialising the scores (B x N x N fp32:
+    2 GiB for 32 VAE samples, small beside 288 GB) turns both directions into large
+    batched GEMMs on hipBLASLt plus one softmax, forward and backward."""
+    if attention_backend() == "sdpa" or not q.is_cuda:
+        return F.scaled_dot_product_attention(q, k, v)
+    b, nh, n, d = q.shape
+    qf, kf, vf = (t.reshape(b * nh, n, d) for t in (q, k, v))
+    s = torch.baddbmm(torch.empty(b * nh, n, n, device=q.device, dtype=q.dtype), qf,
+                      kf.transpose(1, 2), beta=0.0, alpha=1.0 / math.sqrt(d))
+    return torch.bmm(torch.softmax(s, dim=-1), vf).reshape(b, nh, n, d)
+
+
 class SpatialSelfAttention(nn.Module):
     """GroupNorm -> single/multi-head attention over H*W tokens -> residual."""
 
@@ -110,7 +136,7 @@ class SpatialSelfAttention(nn.Module):
         q, k, v = self.to_q(tokens), self.to_k(tokens), self.to_v(tokens)
         nh = self.heads
         q, k, v = (t.reshape(b, h * w, nh, c // nh).transpose(1, 2) for t in (q, k, v))
-        o = F.scaled_dot_product_attention(q, k, v)
+        o = attention(q, k, v)
         o = self.to_out[0](o.transpose(1, 2).reshape(b, h * w, c))
         return x + o.transpose(1, 2).reshape(b, c, h, w)
 
