@@ -296,7 +296,7 @@ def main():
     conv = conv_summary(kern)
     if conv and conv["ms"] > sum(rl[k]["avg_ms"] * kern[k]["count"] for k in rl):
         # the prior's fp32-MFMA convolution tile dominates the step
-        c_rec = pmc.get(f"conv3x3_tiles@B{args.batch}_{args.image}")
+        c_rec = pmc.get(f"conv3x3_tiles@B{args.batch}_{args.image}{tag}")
         roofline = {
             "kernel": "3x3 conv tiles (" + " + ".join(conv["kernels"]) + ")", "bound": "mfma",
             "achieved": round(conv["tflops"], 2), "peak": MFMA_F32_PEAK_TFLOPS, "unit": "TFLOP/s",
