@@ -238,6 +238,21 @@ int sp_groupnorm_silu_bwd(const float* dz, const float* x, const float* chan_bia
                           const float* rstd, int64_t n, int32_t channels, int64_t hw,
                           int32_t groups, int32_t act, float* dx, float* work,
                           sp_stream_t stream);
+/* The same over a channel concatenation x = cat(x1, x2) (x1: c1 channels, x2: the other
+ * channels - c1; x2 NULL: one tensor), read in place — the up-path ResnetBlocks'
+ * torch.cat([h, skip]) is never materialised.  The backward writes the input VJP into the
+ * two parts (dx1, dx2) and adds the optional addends (add1, add2: e.g. the residual
+ * branch's gradient; an addend may alias its output). */
+int sp_groupnorm_silu_fwd2(const float* x1, const float* x2, int32_t c1, const float* chan_bias,
+                           const float* gamma, const float* beta, int64_t n, int32_t channels,
+                           int64_t hw, int32_t groups, float eps, int32_t act, float* z,
+                           float* mean, float* rstd, float* work, sp_stream_t stream);
+int sp_groupnorm_silu_bwd2(const float* dz, const float* x1, const float* x2, int32_t c1,
+                           const float* chan_bias, const float* gamma, const float* beta,
+                           const float* mean, const float* rstd, int64_t n, int32_t channels,
+                           int64_t hw, int32_t groups, int32_t act, float* dx1, float* dx2,
+                           const float* add1, const float* add2, float* work,
+                           sp_stream_t stream);
 
 /* ---- device-resident step schedule (hipGraph capture of a step) ----
  * One record per guided step, precomputed on the host in the same fp64->fp32 arithmetic
@@ -290,6 +305,11 @@ int sp_wino3x3_pack(const float* w, int32_t cout, int32_t cin, int32_t input_vjp
                     sp_stream_t stream);
 int sp_wino3x3_fwd(const float* x, const float* up, const float* bias, int64_t n, int32_t cin,
                    int32_t cout, int32_t height, int32_t width, float* y, sp_stream_t stream);
+/* y = conv(x) + bias + res: the ResnetBlock's residual added in the tile's epilogue
+ * (res shaped like y, not aliasing it). */
+int sp_wino3x3_fwd_res(const float* x, const float* up, const float* bias, const float* res,
+                       int64_t n, int32_t cin, int32_t cout, int32_t height, int32_t width,
+                       float* y, sp_stream_t stream);
 int sp_wino3x3_bwd_input(const float* dy, const float* up_vjp, int64_t n, int32_t cin,
                          int32_t cout, int32_t height, int32_t width, float* dx,
                          sp_stream_t stream);

@@ -132,6 +132,14 @@ SIGNATURES = {
                                              _P]),
     "sp_groupnorm_silu_bwd": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _P, _I64, ctypes.c_int32,
                                              _I64, ctypes.c_int32, ctypes.c_int32, _P, _P, _P]),
+    "sp_groupnorm_silu_fwd2": (ctypes.c_int, [_P, _P, ctypes.c_int32, _P, _P, _P, _I64,
+                                              ctypes.c_int32, _I64, ctypes.c_int32, _F,
+                                              ctypes.c_int32, _P, _P, _P, _P, _P]),
+    "sp_groupnorm_silu_bwd2": (ctypes.c_int, [_P, _P, _P, ctypes.c_int32, _P, _P, _P, _P, _P,
+                                              _I64, ctypes.c_int32, _I64, ctypes.c_int32,
+                                              ctypes.c_int32, _P, _P, _P, _P, _P, _P]),
+    "sp_wino3x3_fwd_res": (ctypes.c_int, [_P, _P, _P, _P, _I64, ctypes.c_int32, ctypes.c_int32,
+                                          ctypes.c_int32, ctypes.c_int32, _P, _P]),
 }
 
 _lib = None

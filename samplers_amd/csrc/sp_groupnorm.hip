@@ -47,7 +47,40 @@ struct GnGeom {
     int chunks;          // workgroups per group
     FastDiv hw_div;      // element (or float4) index in group -> channel in group
     float eps;
+    // The input may be the channel concatenation of two tensors, x = cat(x1, x2), x1 with
+    // c1 channels (c1hw = c1 * HW elements per sample), x2 with the rest; x2 == NULL: one
+    // tensor.  The same split applies to the input gradient (dx1, dx2) and its addends.
+    const float* x2;
+    uint32_t c1hw, s2;   // elements per sample of x1 and of x2
 };
+
+// Element e of group blockIdx.y of a (possibly two-part) NCHW tensor: p1 + e before the
+// group's split point, p2 + e after it (a float4 never straddles: HW % 4 == 0 when V = 4).
+template <typename T>
+struct Parts {
+    T* p1;
+    T* p2;
+    uint32_t split;
+    __device__ __forceinline__ T* at(uint32_t e) const { return (e < split ? p1 : p2) + e; }
+};
+
+template <typename T>
+__device__ __forceinline__ Parts<T> parts_of(T* x1, T* x2, const GnGeom& G) {
+    const int64_t gi = blockIdx.y;
+    const int64_t n = gi / G.G;
+    const int64_t g0 = (gi - n * G.G) * (int64_t)G.gs;  // group start within the sample
+    Parts<T> p;
+    if (!x2) {
+        p.p1 = p.p2 = x1 + gi * (int64_t)G.gs;
+        p.split = G.gs;
+        return p;
+    }
+    p.p1 = x1 + n * (int64_t)G.c1hw + g0;
+    p.p2 = x2 + n * (int64_t)G.s2 + (g0 - (int64_t)G.c1hw);
+    const int64_t sp = (int64_t)G.c1hw - g0;
+    p.split = static_cast<uint32_t>(sp < 0 ? 0 : (sp > (int64_t)G.gs ? G.gs : sp));
+    return p;
+}
 
 __device__ __forceinline__ float silu_f(float y) { return y / (1.f + __expf(-y)); }
 
@@ -59,10 +92,11 @@ __device__ __forceinline__ float silu_bwd(float y, float dz) {
 
 // Per-group quantities every kernel needs.
 struct GroupCtx {
-    int64_t n;       // sample
-    int g;           // group within sample
-    const float* x;  // group base
-    uint32_t lo, hi; // this chunk's vector range [lo, hi) in units of V elements
+    int64_t n;             // sample
+    int g;                 // group within sample
+    Parts<const float> x;  // the group's input elements
+    int64_t zoff;          // group base in the (one-part) output / dz tensors
+    uint32_t lo, hi;       // this chunk's vector range [lo, hi) in units of V elements
 };
 
 template <int V>
@@ -71,7 +105,8 @@ __device__ __forceinline__ GroupCtx group_ctx(const float* base, const GnGeom& G
     const int64_t gi = blockIdx.y;
     c.n = gi / G.G;
     c.g = static_cast<int>(gi - c.n * G.G);
-    c.x = base + gi * (int64_t)G.gs;
+    c.x = parts_of<const float>(base, G.x2, G);
+    c.zoff = gi * (int64_t)G.gs;
     const uint32_t nv = G.gs / V, per = GN_CHUNK / V;
     c.lo = blockIdx.x * per;
     c.hi = min(nv, c.lo + per);
@@ -91,14 +126,14 @@ __global__ __launch_bounds__(kBlock) void k_gn_stats(const float* __restrict__ x
                                                      float* __restrict__ partial) {
     __shared__ float red[8];
     const GroupCtx c = group_ctx<V>(x, G);
-    const float K = c.x[0] + (G.bias ? G.bias[c.n * G.C + c.g * G.Cg] : 0.f);
+    const float K = *c.x.at(0) + (G.bias ? G.bias[c.n * G.C + c.g * G.Cg] : 0.f);
     float s1 = 0.f, s2 = 0.f;
     for (uint32_t j0 = c.lo + threadIdx.x; j0 < c.hi; j0 += GN_UNROLL * kBlock) {
         float v[GN_UNROLL][V];
 #pragma unroll
         for (int u = 0; u < GN_UNROLL; ++u) {
             const uint32_t j = j0 + u * kBlock;
-            if (j < c.hi) load_v<V>(c.x + (size_t)j * V, v[u]);
+            if (j < c.hi) load_v<V>(c.x.at(j * V), v[u]);
         }
 #pragma unroll
         for (int u = 0; u < GN_UNROLL; ++u) {
@@ -146,20 +181,20 @@ __global__ __launch_bounds__(kBlock) void k_gn_apply(const float* __restrict__ x
     const GroupCtx c = group_ctx<V>(x, G);
     float S1, S2;
     group_sums(partial, G.chunks, S1, S2);
-    const float K = c.x[0] + (G.bias ? G.bias[c.n * G.C + c.g * G.Cg] : 0.f);
+    const float K = *c.x.at(0) + (G.bias ? G.bias[c.n * G.C + c.g * G.Cg] : 0.f);
     const float inv_n = 1.f / static_cast<float>(G.gs);
     const float m1 = S1 * inv_n;
     const float mean = K + m1;
     const float var = fmaxf(S2 * inv_n - m1 * m1, 0.f);
     const float rstd = rsqrtf(var + G.eps);
     if (blockIdx.x == 0 && threadIdx.x == 0) mean_out[blockIdx.y] = mean, rstd_out[blockIdx.y] = rstd;
-    float* zg = z + (c.x - x);
+    float* zg = z + c.zoff;
     for (uint32_t j0 = c.lo + threadIdx.x; j0 < c.hi; j0 += GN_UNROLL * kBlock) {
         float v[GN_UNROLL][V];
 #pragma unroll
         for (int u = 0; u < GN_UNROLL; ++u) {
             const uint32_t j = j0 + u * kBlock;
-            if (j < c.hi) load_v<V>(c.x + (size_t)j * V, v[u]);
+            if (j < c.hi) load_v<V>(c.x.at(j * V), v[u]);
         }
 #pragma unroll
         for (int u = 0; u < GN_UNROLL; ++u) {
@@ -206,7 +241,7 @@ __global__ __launch_bounds__(kBlock) void k_gn_bwd_stats(const float* __restrict
     __shared__ float red[8];
     const GroupCtx c = group_ctx<V>(x, G);
     const float mean = mean_in[blockIdx.y], rstd = rstd_in[blockIdx.y];
-    const float* dzg = dz + (c.x - x);
+    const float* dzg = dz + c.zoff;
     float sa = 0.f, sb = 0.f;
     for (uint32_t j0 = c.lo + threadIdx.x; j0 < c.hi; j0 += GN_UNROLL * kBlock) {
         float v[GN_UNROLL][V], g[GN_UNROLL][V];
@@ -214,7 +249,7 @@ __global__ __launch_bounds__(kBlock) void k_gn_bwd_stats(const float* __restrict
         for (int u = 0; u < GN_UNROLL; ++u) {
             const uint32_t j = j0 + u * kBlock;
             if (j < c.hi) {
-                load_v<V>(c.x + (size_t)j * V, v[u]);
+                load_v<V>(c.x.at(j * V), v[u]);
                 load_v<V>(dzg + (size_t)j * V, g[u]);
             }
         }
@@ -252,22 +287,26 @@ __global__ __launch_bounds__(kBlock) void k_gn_bwd_apply(const float* __restrict
                                                          const float* __restrict__ mean_in,
                                                          const float* __restrict__ rstd_in,
                                                          const float* __restrict__ partial,
-                                                         float* __restrict__ dx) {
+                                                         float* __restrict__ dx,
+                                                         float* __restrict__ dx2,
+                                                         const float* __restrict__ add1,
+                                                         const float* __restrict__ add2) {
     const GroupCtx c = group_ctx<V>(x, G);
     float A, B;
     group_sums(partial, G.chunks, A, B);
     const float inv_n = 1.f / static_cast<float>(G.gs);
     const float mA = A * inv_n, mB = B * inv_n;
     const float mean = mean_in[blockIdx.y], rstd = rstd_in[blockIdx.y];
-    const float* dzg = dz + (c.x - x);
-    float* dxg = dx + (c.x - x);
+    const float* dzg = dz + c.zoff;
+    const Parts<float> dxg = parts_of<float>(dx, G.x2 ? dx2 : nullptr, G);
+    const Parts<const float> adg = parts_of<const float>(add1, G.x2 ? add2 : nullptr, G);
     for (uint32_t j0 = c.lo + threadIdx.x; j0 < c.hi; j0 += GN_UNROLL * kBlock) {
         float v[GN_UNROLL][V], g[GN_UNROLL][V];
 #pragma unroll
         for (int u = 0; u < GN_UNROLL; ++u) {
             const uint32_t j = j0 + u * kBlock;
             if (j < c.hi) {
-                load_v<V>(c.x + (size_t)j * V, v[u]);
+                load_v<V>(c.x.at(j * V), v[u]);
                 load_v<V>(dzg + (size_t)j * V, g[u]);
             }
         }
@@ -281,7 +320,13 @@ __global__ __launch_bounds__(kBlock) void k_gn_bwd_apply(const float* __restrict
                                   G.gamma ? G.gamma[ch] : 1.f, G.beta ? G.beta[ch] : 0.f, gdy, xh);
 #pragma unroll
             for (int e = 0; e < V; ++e) o[e] = rstd * (gdy[e] - mA - xh[e] * mB);
-            store_v<V>(dxg + (size_t)j * V, o);
+            if (add1) {  // dx = GN input VJP + addend (a residual branch's gradient)
+                float ad[V];
+                load_v<V>(adg.at(j * V), ad);
+#pragma unroll
+                for (int e = 0; e < V; ++e) o[e] += ad[e];
+            }
+            store_v<V>(dxg.at(j * V), o);
         }
     }
 }
@@ -300,6 +345,9 @@ static int gn_geom(int64_t n, int32_t c, int64_t hw, int32_t groups, const float
     G->chunks = static_cast<int>((gs + GN_CHUNK - 1) / GN_CHUNK);
     G->hw_div = make_fastdiv(static_cast<uint32_t>(hw / *V));
     G->eps = eps;
+    G->x2 = nullptr;
+    G->c1hw = static_cast<uint32_t>(c * hw);
+    G->s2 = 0;
     *grid = dim3(G->chunks, static_cast<unsigned>(n * groups));
     return SP_OK;
 }
@@ -316,14 +364,33 @@ int64_t sp_groupnorm_workspace(int64_t n, int32_t channels, int64_t hw, int32_t 
     return n * groups * ((gs + GN_CHUNK - 1) / GN_CHUNK) * 2;
 }
 
+// second part of a channel-concatenated input: x2 != NULL holds channels c1 .. channels-1
+static int gn_split(GnGeom* G, const float* x2, int32_t c1, int32_t channels, int64_t hw) {
+    if (!x2) return SP_OK;
+    if (c1 <= 0 || c1 >= channels || (int64_t)channels * hw >= (int64_t(1) << 31)) return SP_EINVAL;
+    G->x2 = x2;
+    G->c1hw = static_cast<uint32_t>(c1 * hw);
+    G->s2 = static_cast<uint32_t>((channels - c1) * hw);
+    return SP_OK;
+}
+
 int sp_groupnorm_silu_fwd(const float* x, const float* chan_bias, const float* gamma,
                           const float* beta, int64_t n, int32_t channels, int64_t hw,
                           int32_t groups, float eps, int32_t act, float* z, float* mean,
                           float* rstd, float* work, sp_stream_t stream) {
+    return sp_groupnorm_silu_fwd2(x, nullptr, channels, chan_bias, gamma, beta, n, channels, hw,
+                                  groups, eps, act, z, mean, rstd, work, stream);
+}
+
+int sp_groupnorm_silu_fwd2(const float* x, const float* x2, int32_t c1, const float* chan_bias,
+                           const float* gamma, const float* beta, int64_t n, int32_t channels,
+                           int64_t hw, int32_t groups, float eps, int32_t act, float* z,
+                           float* mean, float* rstd, float* work, sp_stream_t stream) {
     GnGeom G;
     int V;
     dim3 grid;
-    const int rc = gn_geom(n, channels, hw, groups, chan_bias, gamma, beta, eps, &G, &V, &grid);
+    int rc = gn_geom(n, channels, hw, groups, chan_bias, gamma, beta, eps, &G, &V, &grid);
+    if (rc == SP_OK) rc = gn_split(&G, x2, c1, channels, hw);
     if (rc != SP_OK) return rc;
     if (n == 0) return SP_OK;  // empty batch: nothing to read or write
     if (!x || !z || !mean || !rstd || !work) return SP_EINVAL;
@@ -346,18 +413,32 @@ int sp_groupnorm_silu_bwd(const float* dz, const float* x, const float* chan_bia
                           const float* rstd, int64_t n, int32_t channels, int64_t hw,
                           int32_t groups, int32_t act, float* dx, float* work,
                           sp_stream_t stream) {
+    return sp_groupnorm_silu_bwd2(dz, x, nullptr, channels, chan_bias, gamma, beta, mean, rstd,
+                                  n, channels, hw, groups, act, dx, nullptr, nullptr, nullptr,
+                                  work, stream);
+}
+
+int sp_groupnorm_silu_bwd2(const float* dz, const float* x, const float* x2, int32_t c1,
+                           const float* chan_bias, const float* gamma, const float* beta,
+                           const float* mean, const float* rstd, int64_t n, int32_t channels,
+                           int64_t hw, int32_t groups, int32_t act, float* dx, float* dx2,
+                           const float* add1, const float* add2, float* work,
+                           sp_stream_t stream) {
     GnGeom G;
     int V;
     dim3 grid;
-    const int rc = gn_geom(n, channels, hw, groups, chan_bias, gamma, beta, 0.f, &G, &V, &grid);
+    int rc = gn_geom(n, channels, hw, groups, chan_bias, gamma, beta, 0.f, &G, &V, &grid);
+    if (rc == SP_OK) rc = gn_split(&G, x2, c1, channels, hw);
     if (rc != SP_OK) return rc;
     if (n == 0) return SP_OK;
-    if (!dz || !x || !mean || !rstd || !dx || !work) return SP_EINVAL;
+    if (!dz || !x || !mean || !rstd || !dx || !work || (x2 && !dx2) || (x2 && add1 && !add2))
+        return SP_EINVAL;
     hipStream_t s = static_cast<hipStream_t>(stream);
     const dim3 blk(kBlock);
 #define SP_GN_BWD(VV, AA)                                                                      \
     launch(0, k_gn_bwd_stats<VV, AA>, grid, blk, s, dz, x, G, mean, rstd, work);              \
-    launch(0, k_gn_bwd_apply<VV, AA>, grid, blk, s, dz, x, G, mean, rstd, (const float*)work, dx)
+    launch(0, k_gn_bwd_apply<VV, AA>, grid, blk, s, dz, x, G, mean, rstd, (const float*)work, dx, \
+           dx2, add1, add2)
     if (V == 4) {
         if (act) { SP_GN_BWD(4, true); } else { SP_GN_BWD(4, false); }
     } else {

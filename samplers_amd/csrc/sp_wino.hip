@@ -113,6 +113,7 @@ struct WrGeom {
     const float* up;
     float* out;
     const float* bias;
+    const float* res;   // NULL, or a tensor shaped like out added in the epilogue
     int cin, cout, H, W, plane;
     int ntiles, cob, tiles_w, per_img;
     int64_t u_step;                   // floats of packed U per k-step
@@ -295,14 +296,40 @@ __device__ __forceinline__ void wr_step(const WrGeom& g, const WrSrc& cur, const
 // Y = A^T M A, A^T = [[1,1,1,0],[0,1,-1,-1]], per (channel, tile) in registers: register r
 // of every accumulator is channel co0 + (r&3) + 8(r>>2) + 4hh, tile l.  Buffer stores:
 // one per-lane offset, the register row's channel offset as a scalar.
-__device__ __forceinline__ void wr_epilogue(const WrGeom& g, const WrTile& ti, int wv, int lane,
-                                            const f32x16 (&acc)[16]) {
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ int wr_out_voff(const WrGeom& g, const WrTile& ti, int wv, int lane) {
     const int hh = lane >> 5, l = lane & 31;
     const int tr = 2 * (wv >> 1) + (l >> 4), tc = l & 15;
-    const int oh = ti.oh0 + 2 * tr, ow = ti.ow0 + 2 * tc;
+    return ((ti.co0 + 4 * hh) * g.plane + (ti.oh0 + 2 * tr) * g.W + ti.ow0 + 2 * tc) * 4;
+}
+
+// The residual this lane adds to its 2x2 outputs of the tile (RES): loaded before the
+// tile's last k-steps so the loads land while the MFMAs finish.
+struct WrRes { f32x2 v[16][2]; };
+
+__device__ __forceinline__ void wr_load_res(const WrGeom& g, const WrTile& ti, int wv, int lane,
+                                            WrRes& rv) {
+    const auto rrs = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(g.res) + (int64_t)ti.n * g.cout * g.plane, (short)0,
+        g.cout * g.plane * 4, 0x00020000);
+    const int vo = wr_out_voff(g, ti, wv, lane);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const int so = ((r & 3) + 8 * (r >> 2)) * g.plane * 4;
+        rv.v[r][0] = __builtin_bit_cast(f32x2, __builtin_amdgcn_raw_buffer_load_b64(rrs, vo, so, 0));
+        rv.v[r][1] = __builtin_bit_cast(f32x2, __builtin_amdgcn_raw_buffer_load_b64(rrs, vo, so + g.W * 4, 0));
+    }
+}
+
+template <bool RES>
+__device__ __forceinline__ void wr_epilogue(const WrGeom& g, const WrTile& ti, int wv, int lane,
+                                            const f32x16 (&acc)[16], const WrRes& rv) {
+    const int hh = lane >> 5, l = lane & 31;
     const auto ors = __builtin_amdgcn_make_buffer_rsrc(
         g.out + (int64_t)ti.n * g.cout * g.plane, (short)0, g.cout * g.plane * 4, 0x00020000);
-    const int vo = ((ti.co0 + 4 * hh) * g.plane + oh * g.W + ow) * 4;
+    const int vo = wr_out_voff(g, ti, wv, lane);
     // bias[co0 + (lane & 31)] in one register, each row's two values (channels c and c + 4)
     // read out with v_readlane; no bias: a zero-length buffer, whose loads return 0.
     // (Sixteen vector bias registers here get hoisted and spilled while the next tile's
@@ -310,8 +337,6 @@ __device__ __forceinline__ void wr_epilogue(const WrGeom& g, const WrTile& ti, i
     const auto brs = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<float*>(g.bias ? g.bias : g.up), (short)0, g.bias ? g.cout * 4 : 0, 0x00020000);
     const float bl = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(brs, (ti.co0 + l) * 4, 0, 0));
-    typedef float f32x2 __attribute__((ext_vector_type(2)));
-    typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
         float s0[4], s1[4];
@@ -330,12 +355,11 @@ __device__ __forceinline__ void wr_epilogue(const WrGeom& g, const WrTile& ti, i
 #if SP_WINO_EXP == 2
         if (g.W >= 0) continue;  // never true at run time: the stores are skipped, all math kept
 #endif
-        __builtin_amdgcn_raw_buffer_store_b64(
-            __builtin_bit_cast(u32x2, f32x2{s0[0] + s0[1] + s0[2] + bv, s1[0] + s1[1] + s1[2] + bv}),
-            ors, vo, so, 0);
-        __builtin_amdgcn_raw_buffer_store_b64(
-            __builtin_bit_cast(u32x2, f32x2{s0[1] - s0[2] - s0[3] + bv, s1[1] - s1[2] - s1[3] + bv}),
-            ors, vo, so + g.W * 4, 0);
+        f32x2 y0 = {s0[0] + s0[1] + s0[2] + bv, s1[0] + s1[1] + s1[2] + bv};
+        f32x2 y1 = {s0[1] - s0[2] - s0[3] + bv, s1[1] - s1[2] - s1[3] + bv};
+        if constexpr (RES) y0 += rv.v[r][0], y1 += rv.v[r][1];
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, y0), ors, vo, so, 0);
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, y1), ors, vo, so + g.W * 4, 0);
         // one register row at a time: the next tile's operands are live across the
         // epilogue, so its accumulator reads must not all be hoisted
         __builtin_amdgcn_sched_barrier(0);
@@ -346,6 +370,7 @@ __device__ __forceinline__ void wr_epilogue(const WrGeom& g, const WrTile& ti, i
 // ring runs on across tile boundaries, so a tile's prologue latency and its predecessor's
 // store drain overlap MFMA work instead of leaving the CU idle (at one wave per SIMD no
 // other workgroup can fill those gaps).
+template <bool RES>
 __global__ __launch_bounds__(kBlock, 1) void k_wino3x3_r(WrGeom g) {
     __shared__ __attribute__((aligned(16))) float xlds[4 * WX_WAVE];
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -402,12 +427,17 @@ __global__ __launch_bounds__(kBlock, 1) void k_wino3x3_r(WrGeom g) {
             wr_step<2, false, false, false>(g, cur, nxt, xw, xl, p + 2, r, acc);
             wr_step<3, false, false, false>(g, cur, nxt, xw, xl, p + 3, r, acc);
         }
+        WrRes rv;
+        if constexpr (RES) {
+            wr_load_res(g, ti, wv, lane, rv);
+            __builtin_amdgcn_sched_barrier(0);
+        }
         // last four steps: the ring starts fetching the next tile's steps 0..2 / 0..1
         wr_step<0, false, false, false>(g, cur, nxt, xw, xl, last + 0, r, acc);
         wr_step<1, false, true, false>(g, cur, nxt, xw, xl, last + 1, r, acc);
         wr_step<2, false, true, true>(g, cur, nxt, xw, xl, last + 2, r, acc);
         wr_step<3, false, true, true>(g, cur, nxt, xw, xl, last + 3, r, acc);
-        wr_epilogue(g, ti, wv, lane, acc);
+        wr_epilogue<RES>(g, ti, wv, lane, acc, rv);
         t = tn;
         if (t >= g.ntiles) break;
         ti = tin;
@@ -476,9 +506,9 @@ static int cu_count() {
     return cached[dev];
 }
 
-static int wino3x3(int kind, const float* x, const float* up, const float* bias, int64_t n,
-                   int32_t cin, int32_t cout, int32_t height, int32_t width, float* y,
-                   sp_stream_t stream, const char* what) {
+static int wino3x3(int kind, const float* x, const float* up, const float* bias,
+                   const float* res, int64_t n, int32_t cin, int32_t cout, int32_t height,
+                   int32_t width, float* y, sp_stream_t stream, const char* what) {
     if (!sp_wino3x3_supported(cin, cout, height, width) || n < 0) return SP_EINVAL;
     if (n == 0) return SP_OK;
     if (!x || !up || !y) return SP_EINVAL;
@@ -492,6 +522,7 @@ static int wino3x3(int kind, const float* x, const float* up, const float* bias,
     g.up = up;
     g.out = y;
     g.bias = bias;
+    g.res = res;
     g.cin = cin;
     g.cout = cout;
     g.H = height;
@@ -509,22 +540,34 @@ static int wino3x3(int kind, const float* x, const float* up, const float* bias,
     // executed MFMA work: 16 GEMMs of 2*cin*cout per 2x2 tile = 8*cin*cout per pixel
     // (the direct-conv equivalent is 18*cin*cout per pixel, 2.25x more)
     const double flops = 8.0 * n * cin * cout * height * width;
-    launch_w(kind, flops, k_wino3x3_r, dim3(static_cast<unsigned>(grid)), dim3(kBlock),
-             static_cast<hipStream_t>(stream), g);
+    if (res)
+        launch_w(kind, flops, k_wino3x3_r<true>, dim3(static_cast<unsigned>(grid)), dim3(kBlock),
+                 static_cast<hipStream_t>(stream), g);
+    else
+        launch_w(kind, flops, k_wino3x3_r<false>, dim3(static_cast<unsigned>(grid)), dim3(kBlock),
+                 static_cast<hipStream_t>(stream), g);
     return check_launch(what);
 }
 
 int sp_wino3x3_fwd(const float* x, const float* up, const float* bias, int64_t n, int32_t cin,
                    int32_t cout, int32_t height, int32_t width, float* y, sp_stream_t stream) {
-    return wino3x3(TK_WINO3X3_FWD, x, up, bias, n, cin, cout, height, width, y, stream,
+    return wino3x3(TK_WINO3X3_FWD, x, up, bias, nullptr, n, cin, cout, height, width, y, stream,
                    "sp_wino3x3_fwd");
+}
+
+int sp_wino3x3_fwd_res(const float* x, const float* up, const float* bias, const float* res,
+                       int64_t n, int32_t cin, int32_t cout, int32_t height, int32_t width,
+                       float* y, sp_stream_t stream) {
+    if (!res || res == y) return SP_EINVAL;
+    return wino3x3(TK_WINO3X3_FWD, x, up, bias, res, n, cin, cout, height, width, y, stream,
+                   "sp_wino3x3_fwd_res");
 }
 
 int sp_wino3x3_bwd_input(const float* dy, const float* up_vjp, int64_t n, int32_t cin,
                          int32_t cout, int32_t height, int32_t width, float* dx,
                          sp_stream_t stream) {
-    return wino3x3(TK_WINO3X3_BWD_INPUT, dy, up_vjp, nullptr, n, cout, cin, height, width, dx,
-                   stream, "sp_wino3x3_bwd_input");
+    return wino3x3(TK_WINO3X3_BWD_INPUT, dy, up_vjp, nullptr, nullptr, n, cout, cin, height,
+                   width, dx, stream, "sp_wino3x3_bwd_input");
 }
 
 }  // extern "C"

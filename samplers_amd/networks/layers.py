@@ -1,4 +1,4 @@
-"""Fused GroupNorm (+ time-embedding bias) (+ SiLU) for the priors.
+"""Fused GroupNorm (+ time-embedding bias) (+ SiLU) and 3x3 convolutions for the priors.
 
 ``GroupNormAct`` is a drop-in ``nn.GroupNorm`` (same parameters, same state-dict
 keys) whose forward optionally adds a per-(sample, channel) bias to its input and
@@ -27,6 +27,48 @@ def group_norm_act_torch(x: Tensor, groups: int, weight: Tensor | None, bias: Te
         x = x + chan_bias[:, :, None, None]
     y = F.group_norm(x, groups, weight, bias, eps)
     return F.silu(y) if act else y
+
+
+def gn_forward(norm: "GroupNormAct", x1: Tensor, x2: Tensor | None = None,
+               chan_bias: Tensor | None = None) -> tuple[Tensor, Tensor]:
+    """HIP GroupNorm(+bias)(+SiLU) forward over x1, or over cat(x1, x2) along channels read in
+    place; returns (z, stats = [mean; rstd] per (sample, group))."""
+    lib = _hip.load_library()
+    n, c1 = x1.shape[0], x1.shape[1]
+    c = c1 + (x2.shape[1] if x2 is not None else 0)
+    hw = x1[0, 0].numel() if x1.numel() else 1
+    z = torch.empty((n, c) + tuple(x1.shape[2:]), device=x1.device, dtype=torch.float32)
+    stats = torch.empty(2, n * norm.num_groups, device=x1.device, dtype=torch.float32)
+    work = torch.empty(max(int(lib.sp_groupnorm_workspace(n, c, hw, norm.num_groups)), 1),
+                       device=x1.device, dtype=torch.float32)
+    _hip.check(lib.sp_groupnorm_silu_fwd2(
+        _hip.ptr(x1), _hip.ptr(x2), c1, _hip.ptr(chan_bias), _hip.ptr(norm.weight),
+        _hip.ptr(norm.bias), n, c, hw, norm.num_groups, float(norm.eps), int(norm.act),
+        _hip.ptr(z), _hip.ptr(stats[0]), _hip.ptr(stats[1]), _hip.ptr(work),
+        _hip.stream_of(x1)), "sp_groupnorm_silu_fwd2")
+    return z, stats
+
+
+def gn_backward(norm: "GroupNormAct", dz: Tensor, x1: Tensor, x2: Tensor | None,
+                chan_bias: Tensor | None, stats: Tensor, add1: Tensor | None = None,
+                add2: Tensor | None = None, out1: Tensor | None = None,
+                out2: Tensor | None = None) -> tuple[Tensor, Tensor | None]:
+    """Input VJP of ``gn_forward`` into the parts' shapes, plus the optional addends
+    (out1 / out2 may be the addends themselves: accumulate in place)."""
+    lib = _hip.load_library()
+    n, c1 = x1.shape[0], x1.shape[1]
+    c = dz.shape[1]
+    hw = x1[0, 0].numel() if x1.numel() else 1
+    dx1 = torch.empty_like(x1) if out1 is None else out1
+    dx2 = None if x2 is None else (torch.empty_like(x2) if out2 is None else out2)
+    work = torch.empty(max(int(lib.sp_groupnorm_workspace(n, c, hw, norm.num_groups)), 1),
+                       device=x1.device, dtype=torch.float32)
+    _hip.check(lib.sp_groupnorm_silu_bwd2(
+        _hip.ptr(dz.contiguous()), _hip.ptr(x1), _hip.ptr(x2), c1, _hip.ptr(chan_bias),
+        _hip.ptr(norm.weight), _hip.ptr(norm.bias), _hip.ptr(stats[0]), _hip.ptr(stats[1]), n, c,
+        hw, norm.num_groups, int(norm.act), _hip.ptr(dx1), _hip.ptr(dx2), _hip.ptr(add1),
+        _hip.ptr(add2), _hip.ptr(work), _hip.stream_of(x1)), "sp_groupnorm_silu_bwd2")
+    return dx1, dx2
 
 
 class _GroupNormActFn(torch.autograd.Function):
@@ -131,6 +173,46 @@ def _conv_algo(lib, cin: int, cout: int, h: int, w: int, backend: str) -> str | 
     if lib.sp_conv3x3_supported(cin, cout, h, w):
         return "direct"
     return None
+
+
+def conv3x3_forward(module: "Conv3x3", x: Tensor, res: Tensor | None = None) -> Tensor:
+    """conv(x) + bias (+ res) on the module's tile (the residual rides in the Winograd
+    epilogue), MIOpen + an add where no tile serves the shape."""
+    lib = _hip.load_library()
+    n, cin, h, w = x.shape
+    cout = module.out_channels
+    algo = _conv_algo(lib, cin, cout, h, w, conv_backend())
+    if algo is None:
+        y = F.conv2d(x, module.weight, module.bias, padding=1)
+        return y if res is None else y.add_(res)
+    x = x.contiguous()
+    y = torch.empty(n, cout, h, w, device=x.device, dtype=torch.float32)
+    pk = module._pack(algo, False)
+    if algo == "wino" and res is not None:
+        _hip.check(lib.sp_wino3x3_fwd_res(_hip.ptr(x), _hip.ptr(pk), _hip.ptr(module.bias),
+                                          _hip.ptr(res.contiguous()), n, cin, cout, h, w,
+                                          _hip.ptr(y), _hip.stream_of(x)), "sp_wino3x3_fwd_res")
+        return y
+    fn = lib.sp_wino3x3_fwd if algo == "wino" else lib.sp_conv3x3_fwd
+    _hip.check(fn(_hip.ptr(x), _hip.ptr(pk), _hip.ptr(module.bias), n, cin, cout, h, w, _hip.ptr(y),
+                  _hip.stream_of(x)), f"sp_{algo}_conv3x3_fwd")
+    return y if res is None else y.add_(res)
+
+
+def conv3x3_input_vjp(module: "Conv3x3", dy: Tensor, x_shape) -> Tensor:
+    """d conv(x) / dx applied to dy (weights frozen)."""
+    lib = _hip.load_library()
+    n, cin, h, w = x_shape
+    cout = module.out_channels
+    algo = _conv_algo(lib, cout, cin, h, w, conv_backend())
+    dy = dy.contiguous()
+    if algo is None:
+        return torch.nn.grad.conv2d_input(tuple(x_shape), module.weight, dy, padding=1)
+    dx = torch.empty(tuple(x_shape), device=dy.device, dtype=torch.float32)
+    fn = lib.sp_wino3x3_bwd_input if algo == "wino" else lib.sp_conv3x3_bwd_input
+    _hip.check(fn(_hip.ptr(dy), _hip.ptr(module._pack(algo, True)), n, cin, cout, h, w,
+                  _hip.ptr(dx), _hip.stream_of(dy)), f"sp_{algo}_conv3x3_bwd_input")
+    return dx
 
 
 class _Conv3x3Fn(torch.autograd.Function):

@@ -26,7 +26,7 @@ import torch
 import torch.nn.functional as F
 from torch import Tensor, nn
 
-from .layers import Conv3x3, GroupNormAct
+from .layers import Conv3x3, GroupNormAct, conv3x3_forward, conv3x3_input_vjp, gn_backward, gn_forward
 
 
 @dataclass(frozen=True)
@@ -70,8 +70,84 @@ class TimestepEmbedding(nn.Module):
         return self.linear_2(F.silu(self.linear_1(x)))
 
 
+def _shortcut_forward(conv: nn.Conv2d, x1: Tensor, x2: Tensor | None) -> Tensor:
+    """1x1 conv_shortcut over cat(x1, x2): W[:, :c1] x1 + W[:, c1:] x2 + b, the second
+    part accumulated in place by a batched GEMM (no concatenated input)."""
+    c1 = x1.shape[1]
+    y = F.conv2d(x1, conv.weight[:, :c1], conv.bias)
+    if x2 is not None:
+        n, cout = y.shape[:2]
+        w2 = conv.weight[:, c1:, 0, 0]
+        y.view(n, cout, -1).baddbmm_(w2.expand(n, *w2.shape), x2.reshape(n, x2.shape[1], -1))
+    return y
+
+
+def _shortcut_input_vjp(conv: nn.Conv2d, dy: Tensor, c1: int, c2: int) -> tuple[Tensor, Tensor | None]:
+    """(W[:, :c1]^T dy, W[:, c1:]^T dy) as batched GEMMs."""
+    n, cout = dy.shape[:2]
+    dyv = dy.reshape(n, cout, -1)
+    w = conv.weight[:, :, 0, 0]
+    d1 = torch.matmul(w[:, :c1].t(), dyv).reshape((n, c1) + tuple(dy.shape[2:]))
+    d2 = None if not c2 else torch.matmul(w[:, c1:].t(), dyv).reshape((n, c2) + tuple(dy.shape[2:]))
+    return d1, d2
+
+
+class _ResnetBlockFn(torch.autograd.Function):
+    """A whole ResnetBlock2D on the HIP kernels with its input VJP written by hand:
+
+    fwd  z1 = silu(GN1(cat(x1, x2)))   both parts read in place (no torch.cat)
+         h1 = conv1(z1)
+         z2 = silu(GN2(h1 + tb))
+         out = conv2(z2) + shortcut(x)   the residual added in the Winograd epilogue
+    bwd  dx = GN1^T(conv1^T(GN2^T(conv2^T dout))) + shortcut^T dout, the residual branch's
+         gradient added by GN1's backward kernel into the parts' gradients (no autograd
+         accumulation add, no contiguous copies of cat slices).
+    Saves x1, x2, h1 and the GroupNorm statistics (the conv inputs z1, z2 are only needed
+    for weight gradients, which the samplers never take: weights are frozen)."""
+
+    @staticmethod
+    def forward(ctx, block, tb, x1, x2):
+        z1, st1 = gn_forward(block.norm1, x1, x2)
+        h1 = conv3x3_forward(block.conv1, z1)
+        del z1
+        z2, st2 = gn_forward(block.norm2, h1, None, tb)
+        if block.conv_shortcut is None:
+            short = x1
+        else:
+            short = _shortcut_forward(block.conv_shortcut, x1, x2)
+        out = conv3x3_forward(block.conv2, z2, res=short)
+        ctx.block = block
+        ctx.save_for_backward(x1, x2, h1, tb, st1, st2)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        x1, x2, h1, tb, st1, st2 = ctx.saved_tensors
+        blk = ctx.block
+        dout = dout.contiguous()
+        dz2 = conv3x3_input_vjp(blk.conv2, dout, h1.shape)
+        dh1, _ = gn_backward(blk.norm2, dz2, h1, None, tb, st2)
+        del dz2
+        zshape = (x1.shape[0], blk.conv1.in_channels) + tuple(x1.shape[2:])
+        dz1 = conv3x3_input_vjp(blk.conv1, dh1, zshape)
+        del dh1
+        if blk.conv_shortcut is None:  # identity shortcut: dx1 = GN1^T dz1 + dout
+            dx1, dx2 = gn_backward(blk.norm1, dz1, x1, x2, None, st1, add1=dout)
+        else:  # dx = shortcut^T dout, then += GN1^T dz1 in place
+            s1, s2 = _shortcut_input_vjp(blk.conv_shortcut, dout, x1.shape[1],
+                                         0 if x2 is None else x2.shape[1])
+            dx1, dx2 = gn_backward(blk.norm1, dz1, x1, x2, None, st1, add1=s1, add2=s2,
+                                   out1=s1, out2=s2)
+        return None, None, dx1, dx2
+
+
 class ResnetBlock2D(nn.Module):
-    """GN-SiLU-conv x2 with an optional time-embedding bias (``temb=None``: VAE blocks)."""
+    """GN-SiLU-conv x2 with an optional time-embedding bias (``temb=None``: VAE blocks).
+
+    ``forward(x, temb, skip)`` takes the up path's skip tensor separately: on the device
+    with frozen fp32 weights the whole block runs as ``_ResnetBlockFn`` over cat(x, skip)
+    read in place; otherwise (CPU, training) it is the module-by-module graph on
+    ``torch.cat([x, skip], 1)``."""
 
     def __init__(self, cin: int, cout: int, temb: int | None, groups: int, eps: float) -> None:
         super().__init__()
@@ -82,10 +158,21 @@ class ResnetBlock2D(nn.Module):
         self.conv2 = Conv3x3(cout, cout)
         self.conv_shortcut = nn.Conv2d(cin, cout, 1) if cin != cout else None
 
-    def forward(self, x: Tensor, temb: Tensor | None = None) -> Tensor:
+    def _fusable(self, x: Tensor) -> bool:
+        return (x.is_cuda and x.dtype == torch.float32 and x.dim() == 4
+                and not any(p.requires_grad for p in self.parameters())
+                and x[0, 0].numel() % 4 == 0)
+
+    def forward(self, x: Tensor, temb: Tensor | None = None, skip: Tensor | None = None) -> Tensor:
+        tb = self.time_emb_proj(F.silu(temb)) if self.time_emb_proj is not None else None
+        if self._fusable(x) and (skip is None or skip.dtype == x.dtype):
+            x1 = x.contiguous()
+            x2 = None if skip is None else skip.contiguous()
+            return _ResnetBlockFn.apply(self, None if tb is None else tb.contiguous(), x1, x2)
+        if skip is not None:
+            x = torch.cat([x, skip], dim=1)
         h = self.conv1(self.norm1(x))  # silu(norm1(x)), fused
         # silu(norm2(h + temb_proj)): the time-embedding add rides in the fused norm
-        tb = self.time_emb_proj(F.silu(temb)) if self.time_emb_proj is not None else None
         h = self.conv2(self.norm2(h, tb))
         if self.conv_shortcut is not None:
             x = self.conv_shortcut(x)
@@ -248,7 +335,7 @@ class UNet2DModel(nn.Module):
 
         for lvl in self.up_blocks:
             for j, res in enumerate(lvl.resnets):
-                h = res(torch.cat([h, skips.pop()], dim=1), emb)
+                h = res(h, emb, skip=skips.pop())
                 if len(lvl.attentions):
                     h = lvl.attentions[j](h)
             if lvl.upsamplers is not None:

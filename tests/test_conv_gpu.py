@@ -146,3 +146,16 @@ def test_winograd_forward_and_input_vjp(cuda, shape):
         assert rel < 1e-5, rel
     rel = ((y.double().cpu() - ref.detach()).norm() / ref.detach().norm()).item()
     assert rel < 1e-5, rel
+
+
+def test_winograd_residual_epilogue(cuda):
+    """sp_wino3x3_fwd_res = sp_wino3x3_fwd + res, exactly (the add happens once, in fp32)."""
+    from samplers_amd.networks.layers import Conv3x3, conv3x3_forward
+
+    torch.manual_seed(3)
+    conv = Conv3x3(64, 128).to(cuda).requires_grad_(False)
+    x = torch.randn(2, 64, 16, 64, device=cuda)
+    res = torch.randn(2, 128, 16, 64, device=cuda)
+    y = conv3x3_forward(conv, x)
+    yr = conv3x3_forward(conv, x, res=res)
+    assert torch.equal(yr, y + res)

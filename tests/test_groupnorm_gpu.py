@@ -100,3 +100,56 @@ def test_unet_forward_vjp_matches_cpu(cuda):
     (gx,) = torch.autograd.grad(out, xg, v.to(cuda))
     assert _rel(out.detach().cpu(), ref.detach()) < 1e-4
     assert _rel(gx.cpu(), gref) < 1e-4
+
+
+@pytest.mark.parametrize("act", [True, False])
+def test_two_part_input_and_addends(cuda, act):
+    """sp_groupnorm_silu_fwd2 / bwd2 over cat(x1, x2) read in place (groups straddling the
+    split: c1 = 40 is not a multiple of Cg = 12) and the input VJP split into the parts
+    plus addends, accumulated in place for one part — against torch on the concatenation."""
+    from samplers_amd.networks.layers import gn_backward, gn_forward
+
+    gen = torch.Generator().manual_seed(11)
+    n, c1, c2, h, w, g = 3, 40, 56, 12, 20, 8
+    x1, x2 = torch.randn(n, c1, h, w, generator=gen), torch.randn(n, c2, h, w, generator=gen)
+    dz = torch.randn(n, c1 + c2, h, w, generator=gen)
+    a1, a2 = torch.randn(n, c1, h, w, generator=gen), torch.randn(n, c2, h, w, generator=gen)
+    layer = GroupNormAct(g, c1 + c2, eps=1e-6, act=act)
+    with torch.no_grad():
+        layer.weight.uniform_(0.5, 1.5, generator=gen)
+        layer.bias.uniform_(-0.5, 0.5, generator=gen)
+    xd = torch.cat([x1, x2], 1).double().requires_grad_()
+    ref = layer.double()(xd)
+    (gref,) = torch.autograd.grad(ref, xd, dz.double())
+    lg = layer.float().to(cuda)
+    z, st = gn_forward(lg, x1.to(cuda), x2.to(cuda))
+    assert _rel(z.cpu(), ref.detach()) < 2e-5
+    s2 = a2.to(cuda)
+    d1, d2 = gn_backward(lg, dz.to(cuda), x1.to(cuda), x2.to(cuda), None, st,
+                         add1=a1.to(cuda), add2=s2, out2=s2)
+    assert d2.data_ptr() == s2.data_ptr()
+    assert _rel(d1.cpu(), gref[:, :c1] + a1.double()) < 1e-4
+    assert _rel(d2.cpu(), gref[:, c1:] + a2.double()) < 1e-4
+
+
+def test_fused_resnet_blocks_match_cpu(cuda):
+    """The UNet with every ResnetBlock as one fused autograd function (GN over cat(h, skip)
+    in place, 1x1 shortcuts as GEMMs, the residual in the Winograd epilogue, the
+    residual's gradient added inside GN1's backward) against fp64 CPU, forward and input
+    VJP, at channel widths / sizes where the Winograd tile serves the 3x3 convs."""
+    from samplers_amd.networks.unet2d import UNet2DConfig, build_unet
+
+    cfg = UNet2DConfig(sample_size=64, block_out_channels=(64, 128), attention_levels=(1,),
+                       norm_num_groups=32)
+    net = build_unet(cfg, seed=5)
+    x = torch.randn(2, 3, 64, 64, generator=torch.Generator().manual_seed(1))
+    v = torch.randn_like(x)
+    xd = x.double().requires_grad_()
+    ref = net.double()(xd, 321)
+    (gref,) = torch.autograd.grad(ref, xd, v.double())
+    net = net.float().to(cuda)
+    xg = x.to(cuda).requires_grad_()
+    out = net(xg, 321)
+    (gx,) = torch.autograd.grad(out, xg, v.to(cuda))
+    assert _rel(out.detach().cpu(), ref.detach()) < 1e-4
+    assert _rel(gx.cpu(), gref) < 1e-4
