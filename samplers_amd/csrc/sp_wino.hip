@@ -81,18 +81,31 @@ __device__ __forceinline__ void wino_filter(const float (&g)[9], float (&u)[16])
 // uncoalesced; the address unit was 74 % busy and the MFMAs 48 %.)
 // ---------------------------------------------------------------------------------------
 constexpr int WR_CO = 64;   // output channels per workgroup (2 waves x 32)
-constexpr int WR_TR = 4;    // tile rows per workgroup (2 per wave): 8 output rows
-constexpr int WR_TC = 16;   // tile columns: 32 output columns
 #ifndef SP_WINO_EXP
 #define SP_WINO_EXP 0  // diagnostics only: 1 = no loads in the k loop, 2 = no output stores,
                        // 3 = no input transform (wrong results, timing only)
 #endif
 constexpr int WR_NS = 4;    // unroll of the k-step ring (cin % (2 WR_NS) == 0)
-constexpr int WX_ROW = 40;           // LDS floats per block row (columns -1..32 at 3..36)
-constexpr int WX_CI = 6 * WX_ROW;    // per input channel of the block
-constexpr int WX_WAVE = 2 * WX_CI;   // per wave
-
-__device__ __forceinline__ int wx_row(int r) { return r * WX_ROW + (r >> 1); }
+// Tile geometry of a wave: 32 tiles (the MFMA's N) as TRW tile rows x TCW tile columns.
+// TCW = 16 (images with W % 32 == 0): 2 x 16 tiles = 4 x 32 outputs; TCW = 8 (W = 16, the
+// UNet's 16x16 level): 4 x 8 tiles = 8 x 16 outputs.  A workgroup stacks two waves' rows
+// (and two 32-channel halves): 64 co x (4 TRW) x (2 TCW) outputs.
+template <int TCW_>
+struct WGeo {
+    static constexpr int TCW = TCW_;
+    static constexpr int TRW = 32 / TCW;
+    static constexpr int ROWS = 2 * TRW + 2;     // input block rows per channel
+    static constexpr int PPR = TCW / 2;          // 16-byte pieces per block row
+    static constexpr int RC = 2 * ROWS;          // block rows of the k-step's two channels
+    static constexpr int ROW = TCW == 16 ? 40 : 25;  // LDS floats per block row (cols -1.. at 3..)
+    static constexpr int CI = TCW == 16 ? 6 * 40 : 10 * 25 + 8;  // per input channel
+    static constexpr int WAVE = 2 * CI;
+    static constexpr int WG_ROWS = 4 * TRW;      // output rows per workgroup
+    static constexpr int WG_COLS = 2 * TCW;      // output columns per workgroup
+    static_assert(RC - 64 / PPR == 4 && 2 * RC <= 64, "piece / halo lane mapping");
+    // row r of a channel at r * ROW + r / 2: rows two apart sit an odd bank distance apart
+    __device__ static constexpr int row(int r) { return r * ROW + (r >> 1); }
+};
 
 struct WrX { f32x4 a, b; float h; };  // a lane's share of one k-step's input block
 struct WrU { f32x4 u[4]; };           // a lane's 16 U values (xi = 0..15) for one k-step
@@ -121,6 +134,7 @@ struct WrGeom {
     int nsteps;
 };
 
+template <class GE>
 __device__ __forceinline__ WrTile wr_tile(const WrGeom& g, int t, int wv) {
     // XCD-aware order: tiles t and t + 8 run on one XCD (persistent workgroups b and b + 8
     // share one), so consecutive logical tiles (the channel blocks of one tile group, then
@@ -129,16 +143,17 @@ __device__ __forceinline__ WrTile wr_tile(const WrGeom& g, int t, int wv) {
     const int co_blk = lb % g.cob, rest = lb / g.cob;
     const int n = rest / g.per_img, r = rest - n * g.per_img;
     const int ty = r / g.tiles_w;
-    return WrTile{n, ty * 2 * WR_TR, (r - ty * g.tiles_w) * 2 * WR_TC, co_blk * WR_CO + 32 * (wv & 1)};
+    return WrTile{n, ty * GE::WG_ROWS, (r - ty * g.tiles_w) * GE::WG_COLS, co_blk * WR_CO + 32 * (wv & 1)};
 }
 
+template <class GE>
 __device__ __forceinline__ WrSrc wr_src(const WrGeom& g, const WrTile& ti, int wv, int lane) {
     constexpr int OOB = 0x7FFFFFF0;  // outside the image: the buffer returns 0
-    const int row0 = ti.oh0 + 4 * (wv >> 1) - 1;  // the wave's first input row
-    const int ka = lane & 7, rca = lane >> 3, rcb = 8 + ((lane >> 3) & 3);
-    const int rch = (lane % 24) >> 1, side = lane & 1;
+    const int row0 = ti.oh0 + 2 * GE::TRW * (wv >> 1) - 1;  // the wave's first input row
+    const int ka = lane % GE::PPR, rca = lane / GE::PPR, rcb = 64 / GE::PPR + ((lane / GE::PPR) & 3);
+    const int rch = (lane % (2 * GE::RC)) >> 1, side = lane & 1;
     auto goff = [&](int rc, int col) {
-        const int ci = rc / 6, gr = row0 + rc % 6;
+        const int ci = rc / GE::ROWS, gr = row0 + rc % GE::ROWS;
         return ((unsigned)gr < (unsigned)g.H && (unsigned)col < (unsigned)g.W)
                    ? (ci * g.plane + gr * g.W + col) * 4 : OOB;
     };
@@ -148,7 +163,7 @@ __device__ __forceinline__ WrSrc wr_src(const WrGeom& g, const WrTile& ti, int w
         0x00020000);
     s.oa = goff(rca, ti.ow0 + 4 * ka);
     s.ob = goff(rcb, ti.ow0 + 4 * ka);
-    s.oh = goff(rch, side ? ti.ow0 + 32 : ti.ow0 - 1);
+    s.oh = goff(rch, side ? ti.ow0 + 2 * GE::TCW : ti.ow0 - 1);
     s.ub = g.up + ((int64_t)(ti.co0 >> 5) * 64 + lane) * 16;
     return s;
 }
@@ -174,10 +189,11 @@ __device__ __forceinline__ void wr_stage_x(float* xw, const WxLane& xl, const Wr
 }
 
 // This lane's 4x4 window: columns 2tc-1 .. 2tc+2 of the wave's rows 2tr .. 2tr+3.
+template <class GE>
 __device__ __forceinline__ void wr_window(const float* xw, const WxLane& xl, float (&d)[16]) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-        const float* row = xw + xl.rd + wx_row(r);
+        const float* row = xw + xl.rd + GE::row(r);
 #pragma unroll
         for (int c = 0; c < 4; ++c) d[r * 4 + c] = row[c];
     }
@@ -202,7 +218,7 @@ struct WrRing {          // k-steps in flight
 // burst issued.)  Loads run 3 steps ahead for the input block, 2 for U; near the end of
 // a tile they fetch the next tile's first steps (XN / UN), so its operands arrive during
 // this tile's epilogue.
-template <int K, bool FIRST, bool XN, bool UN>
+template <class GE, int K, bool FIRST, bool XN, bool UN>
 __device__ __forceinline__ void wr_step(const WrGeom& g, const WrSrc& cur, const WrSrc& nxt,
                                         float* xw, const WxLane& xl, int q, WrRing& r,
                                         f32x16 (&acc)[16]) {
@@ -250,13 +266,13 @@ __device__ __forceinline__ void wr_step(const WrGeom& g, const WrSrc& cur, const
 #pragma unroll
     for (int rr = 0; rr < 2; ++rr)
 #pragma unroll
-        for (int c = 0; c < 4; ++c) d[rr * 4 + c] = xw[xl.rd + wx_row(rr) + c];
+        for (int c = 0; c < 4; ++c) d[rr * 4 + c] = xw[xl.rd + GE::row(rr) + c];
     WR_WALL;
     WR_MFMA(6);
 #pragma unroll
     for (int rr = 2; rr < 4; ++rr)
 #pragma unroll
-        for (int c = 0; c < 4; ++c) d[rr * 4 + c] = xw[xl.rd + wx_row(rr) + c];
+        for (int c = 0; c < 4; ++c) d[rr * 4 + c] = xw[xl.rd + GE::row(rr) + c];
     WR_WALL;
     WR_MFMA(7);
     WR_MFMA(8);
@@ -299,9 +315,10 @@ __device__ __forceinline__ void wr_step(const WrGeom& g, const WrSrc& cur, const
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
 
+template <class GE>
 __device__ __forceinline__ int wr_out_voff(const WrGeom& g, const WrTile& ti, int wv, int lane) {
     const int hh = lane >> 5, l = lane & 31;
-    const int tr = 2 * (wv >> 1) + (l >> 4), tc = l & 15;
+    const int tr = GE::TRW * (wv >> 1) + l / GE::TCW, tc = l % GE::TCW;
     return ((ti.co0 + 4 * hh) * g.plane + (ti.oh0 + 2 * tr) * g.W + ti.ow0 + 2 * tc) * 4;
 }
 
@@ -309,12 +326,13 @@ __device__ __forceinline__ int wr_out_voff(const WrGeom& g, const WrTile& ti, in
 // tile's last k-steps so the loads land while the MFMAs finish.
 struct WrRes { f32x2 v[16][2]; };
 
+template <class GE>
 __device__ __forceinline__ void wr_load_res(const WrGeom& g, const WrTile& ti, int wv, int lane,
                                             WrRes& rv) {
     const auto rrs = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<float*>(g.res) + (int64_t)ti.n * g.cout * g.plane, (short)0,
         g.cout * g.plane * 4, 0x00020000);
-    const int vo = wr_out_voff(g, ti, wv, lane);
+    const int vo = wr_out_voff<GE>(g, ti, wv, lane);
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
         const int so = ((r & 3) + 8 * (r >> 2)) * g.plane * 4;
@@ -323,13 +341,13 @@ __device__ __forceinline__ void wr_load_res(const WrGeom& g, const WrTile& ti, i
     }
 }
 
-template <bool RES>
+template <class GE, bool RES>
 __device__ __forceinline__ void wr_epilogue(const WrGeom& g, const WrTile& ti, int wv, int lane,
                                             const f32x16 (&acc)[16], const WrRes& rv) {
     const int hh = lane >> 5, l = lane & 31;
     const auto ors = __builtin_amdgcn_make_buffer_rsrc(
         g.out + (int64_t)ti.n * g.cout * g.plane, (short)0, g.cout * g.plane * 4, 0x00020000);
-    const int vo = wr_out_voff(g, ti, wv, lane);
+    const int vo = wr_out_voff<GE>(g, ti, wv, lane);
     // bias[co0 + (lane & 31)] in one register, each row's two values (channels c and c + 4)
     // read out with v_readlane; no bias: a zero-length buffer, whose loads return 0.
     // (Sixteen vector bias registers here get hoisted and spilled while the next tile's
@@ -370,31 +388,30 @@ __device__ __forceinline__ void wr_epilogue(const WrGeom& g, const WrTile& ti, i
 // ring runs on across tile boundaries, so a tile's prologue latency and its predecessor's
 // store drain overlap MFMA work instead of leaving the CU idle (at one wave per SIMD no
 // other workgroup can fill those gaps).
-template <bool RES>
+template <bool RES, int TCW>
 __global__ __launch_bounds__(kBlock, 1) void k_wino3x3_r(WrGeom g) {
-    __shared__ __attribute__((aligned(16))) float xlds[4 * WX_WAVE];
+    using GE = WGeo<TCW>;
+    __shared__ __attribute__((aligned(16))) float xlds[4 * GE::WAVE];
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    float* const xw = xlds + wv * WX_WAVE;
+    float* const xw = xlds + wv * GE::WAVE;
     WxLane xl;
     {
-        // row r of a channel at r * WX_ROW + r / 2: the two tile rows of a wave read rows
-        // two apart, 81 floats = an odd bank distance, so their lanes never collide
-        auto loff = [](int rc) { return (rc / 6) * WX_CI + wx_row(rc % 6); };
-        const int ka = lane & 7, rca = lane >> 3, rcb = 8 + ((lane >> 3) & 3);
-        const int rch = (lane % 24) >> 1, side = lane & 1;
+        auto loff = [](int rc) { return (rc / GE::ROWS) * GE::CI + GE::row(rc % GE::ROWS); };
+        const int ka = lane % GE::PPR, rca = lane / GE::PPR, rcb = 64 / GE::PPR + ((lane / GE::PPR) & 3);
+        const int rch = (lane % (2 * GE::RC)) >> 1, side = lane & 1;
         xl.wa = loff(rca) + 4 + 4 * ka;
         xl.wb = loff(rcb) + 4 + 4 * ka;
-        xl.wh = loff(rch) + (side ? 36 : 3);
+        xl.wh = loff(rch) + (side ? 4 + 2 * GE::TCW : 3);
         const int l = lane & 31;
-        xl.rd = (lane >> 5) * WX_CI + wx_row(2 * (l >> 4)) + 3 + 2 * (l & 15);
+        xl.rd = (lane >> 5) * GE::CI + GE::row(2 * (l / GE::TCW)) + 3 + 2 * (l % GE::TCW);
     }
     int t = blockIdx.x;
     const int stride = gridDim.x;
-    WrTile ti = wr_tile(g, t, wv);
-    WrSrc cur = wr_src(g, ti, wv, lane);
+    WrTile ti = wr_tile<GE>(g, t, wv);
+    WrSrc cur = wr_src<GE>(g, ti, wv, lane);
     int tn = t + stride;
-    WrTile tin = wr_tile(g, tn < g.ntiles ? tn : t, wv);  // no next tile: harmless re-loads
-    WrSrc nxt = wr_src(g, tin, wv, lane);
+    WrTile tin = wr_tile<GE>(g, tn < g.ntiles ? tn : t, wv);  // no next tile: harmless re-loads
+    WrSrc nxt = wr_src<GE>(g, tin, wv, lane);
 
     // prologue in the loop's own issue order (..., X(q+1), U(q), X(q+2), U(q+1))
     WrRing r;
@@ -411,40 +428,40 @@ __global__ __launch_bounds__(kBlock, 1) void k_wino3x3_r(WrGeom g) {
     {
         float d[16];
         wr_stage_x(xw, xl, r.xs[0]);
-        wr_window(xw, xl, d);
+        wr_window<GE>(xw, xl, d);
         wino_in(d, r.v[0]);
     }
     f32x16 acc[16];
     const int last = g.nsteps - 4;  // >= 4 (cin >= 16)
     for (;;) {
-        wr_step<0, true, false, false>(g, cur, nxt, xw, xl, 0, r, acc);
-        wr_step<1, false, false, false>(g, cur, nxt, xw, xl, 1, r, acc);
-        wr_step<2, false, false, false>(g, cur, nxt, xw, xl, 2, r, acc);
-        wr_step<3, false, false, false>(g, cur, nxt, xw, xl, 3, r, acc);
+        wr_step<GE, 0, true, false, false>(g, cur, nxt, xw, xl, 0, r, acc);
+        wr_step<GE, 1, false, false, false>(g, cur, nxt, xw, xl, 1, r, acc);
+        wr_step<GE, 2, false, false, false>(g, cur, nxt, xw, xl, 2, r, acc);
+        wr_step<GE, 3, false, false, false>(g, cur, nxt, xw, xl, 3, r, acc);
         for (int p = 4; p < last; p += 4) {
-            wr_step<0, false, false, false>(g, cur, nxt, xw, xl, p + 0, r, acc);
-            wr_step<1, false, false, false>(g, cur, nxt, xw, xl, p + 1, r, acc);
-            wr_step<2, false, false, false>(g, cur, nxt, xw, xl, p + 2, r, acc);
-            wr_step<3, false, false, false>(g, cur, nxt, xw, xl, p + 3, r, acc);
+            wr_step<GE, 0, false, false, false>(g, cur, nxt, xw, xl, p + 0, r, acc);
+            wr_step<GE, 1, false, false, false>(g, cur, nxt, xw, xl, p + 1, r, acc);
+            wr_step<GE, 2, false, false, false>(g, cur, nxt, xw, xl, p + 2, r, acc);
+            wr_step<GE, 3, false, false, false>(g, cur, nxt, xw, xl, p + 3, r, acc);
         }
         WrRes rv;
         if constexpr (RES) {
-            wr_load_res(g, ti, wv, lane, rv);
+            wr_load_res<GE>(g, ti, wv, lane, rv);
             __builtin_amdgcn_sched_barrier(0);
         }
         // last four steps: the ring starts fetching the next tile's steps 0..2 / 0..1
-        wr_step<0, false, false, false>(g, cur, nxt, xw, xl, last + 0, r, acc);
-        wr_step<1, false, true, false>(g, cur, nxt, xw, xl, last + 1, r, acc);
-        wr_step<2, false, true, true>(g, cur, nxt, xw, xl, last + 2, r, acc);
-        wr_step<3, false, true, true>(g, cur, nxt, xw, xl, last + 3, r, acc);
-        wr_epilogue<RES>(g, ti, wv, lane, acc, rv);
+        wr_step<GE, 0, false, false, false>(g, cur, nxt, xw, xl, last + 0, r, acc);
+        wr_step<GE, 1, false, true, false>(g, cur, nxt, xw, xl, last + 1, r, acc);
+        wr_step<GE, 2, false, true, true>(g, cur, nxt, xw, xl, last + 2, r, acc);
+        wr_step<GE, 3, false, true, true>(g, cur, nxt, xw, xl, last + 3, r, acc);
+        wr_epilogue<GE, RES>(g, ti, wv, lane, acc, rv);
         t = tn;
         if (t >= g.ntiles) break;
         ti = tin;
         cur = nxt;
         tn = t + stride;
-        tin = wr_tile(g, tn < g.ntiles ? tn : t, wv);
-        nxt = wr_src(g, tin, wv, lane);
+        tin = wr_tile<GE>(g, tn < g.ntiles ? tn : t, wv);
+        nxt = wr_src<GE>(g, tin, wv, lane);
     }
 }
 
@@ -475,8 +492,11 @@ using namespace sp;
 extern "C" {
 
 int sp_wino3x3_supported(int32_t cin, int32_t cout, int32_t height, int32_t width) {
-    return cin >= 16 && cout > 0 && cin % (2 * WR_NS) == 0 && cout % WR_CO == 0 &&
-           height % (2 * WR_TR) == 0 && width % (2 * WR_TC) == 0 && height > 0 && width > 0;
+    // W % 32: 32-column workgroup tiles of 8 rows; W = 16 (UNet 16x16 level): 16 x 16
+    const bool geo = (width % WGeo<16>::WG_COLS == 0 && height % WGeo<16>::WG_ROWS == 0) ||
+                     (width == WGeo<8>::WG_COLS && height % WGeo<8>::WG_ROWS == 0);
+    return cin >= 16 && cout > 0 && cin % (2 * WR_NS) == 0 && cout % WR_CO == 0 && geo &&
+           height > 0 && width > 0;
 }
 
 int64_t sp_wino3x3_packed_size(int32_t cin, int32_t cout) { return (int64_t)cin * cout * 16; }
@@ -512,7 +532,10 @@ static int wino3x3(int kind, const float* x, const float* up, const float* bias,
     if (!sp_wino3x3_supported(cin, cout, height, width) || n < 0) return SP_EINVAL;
     if (n == 0) return SP_OK;
     if (!x || !up || !y) return SP_EINVAL;
-    const int64_t tiles = n * (height / (2 * WR_TR)) * (width / (2 * WR_TC)) * (cout / WR_CO);
+    const bool narrow = width % WGeo<16>::WG_COLS != 0;  // the W = 16 geometry
+    const int wg_rows = narrow ? WGeo<8>::WG_ROWS : WGeo<16>::WG_ROWS;
+    const int wg_cols = narrow ? WGeo<8>::WG_COLS : WGeo<16>::WG_COLS;
+    const int64_t tiles = n * (height / wg_rows) * (width / wg_cols) * (cout / WR_CO);
     // per-sample planes are addressed by 32-bit buffer offsets (bytes < 2^31)
     if (tiles >= (int64_t(1) << 31) || (int64_t)cin * height * width * 4 >= (int64_t(1) << 31) ||
         (int64_t)cout * height * width * 4 >= (int64_t(1) << 31))
@@ -530,8 +553,8 @@ static int wino3x3(int kind, const float* x, const float* up, const float* bias,
     g.plane = height * width;
     g.ntiles = static_cast<int>(tiles);
     g.cob = cout / WR_CO;
-    g.tiles_w = width / (2 * WR_TC);
-    g.per_img = g.tiles_w * (height / (2 * WR_TR));
+    g.tiles_w = width / wg_cols;
+    g.per_img = g.tiles_w * (height / wg_rows);
     g.u_step = (int64_t)cout * 32;
     g.so_step = 2 * height * width * 4;
     g.nsteps = cin / 2;
@@ -540,12 +563,15 @@ static int wino3x3(int kind, const float* x, const float* up, const float* bias,
     // executed MFMA work: 16 GEMMs of 2*cin*cout per 2x2 tile = 8*cin*cout per pixel
     // (the direct-conv equivalent is 18*cin*cout per pixel, 2.25x more)
     const double flops = 8.0 * n * cin * cout * height * width;
-    if (res)
-        launch_w(kind, flops, k_wino3x3_r<true>, dim3(static_cast<unsigned>(grid)), dim3(kBlock),
-                 static_cast<hipStream_t>(stream), g);
-    else
-        launch_w(kind, flops, k_wino3x3_r<false>, dim3(static_cast<unsigned>(grid)), dim3(kBlock),
-                 static_cast<hipStream_t>(stream), g);
+    const dim3 gd(static_cast<unsigned>(grid)), bd(kBlock);
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    if (narrow) {
+        if (res) launch_w(kind, flops, k_wino3x3_r<true, 8>, gd, bd, st, g);
+        else launch_w(kind, flops, k_wino3x3_r<false, 8>, gd, bd, st, g);
+    } else {
+        if (res) launch_w(kind, flops, k_wino3x3_r<true, 16>, gd, bd, st, g);
+        else launch_w(kind, flops, k_wino3x3_r<false, 16>, gd, bd, st, g);
+    }
     return check_launch(what);
 }
 

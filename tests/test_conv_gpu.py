@@ -114,10 +114,12 @@ def test_conv3x3_timing_records_flops(cuda, monkeypatch):
 
 
 @pytest.mark.parametrize("shape", [(2, 128, 128, 32, 64), (1, 256, 64, 16, 32), (2, 64, 128, 8, 96),
-                                   (3, 64, 192, 24, 64)])
+                                   (3, 64, 192, 24, 64), (3, 128, 64, 16, 16), (2, 64, 128, 32, 16),
+                                   (1, 512, 512, 16, 16)])
 def test_winograd_forward_and_input_vjp(cuda, shape):
     """Winograd F(2x2,3x3) tile: fp32 transforms + exact fp32 MFMA accumulation; the
-    transforms add F(2,3) rounding, so the bound is 1e-5 relative L2 (vs 2e-6 direct)."""
+    transforms add F(2,3) rounding, so the bound is 1e-5 relative L2 (vs 2e-6 direct).
+    W = 16 shapes run the 4 x 8-tile wave geometry (the UNet's 16x16 level)."""
     n, cin, cout, h, w = shape
     lib = _hip.load_library()
     assert lib.sp_wino3x3_supported(cin, cout, h, w)
@@ -159,3 +161,6 @@ def test_winograd_residual_epilogue(cuda):
     y = conv3x3_forward(conv, x)
     yr = conv3x3_forward(conv, x, res=res)
     assert torch.equal(yr, y + res)
+    x16 = torch.randn(2, 64, 16, 16, device=cuda)  # the W = 16 geometry
+    r16 = torch.randn(2, 128, 16, 16, device=cuda)
+    assert torch.equal(conv3x3_forward(conv, x16, res=r16), conv3x3_forward(conv, x16) + r16)
