@@ -175,26 +175,29 @@ def _conv_algo(lib, cin: int, cout: int, h: int, w: int, backend: str) -> str | 
     return None
 
 
-def conv3x3_forward(module: "Conv3x3", x: Tensor, res: Tensor | None = None) -> Tensor:
+def conv3x3_forward(module: "Conv3x3", x: Tensor, res: Tensor | None = None,
+                    bias: Tensor | None = None) -> Tensor:
     """conv(x) + bias (+ res) on the module's tile (the residual rides in the Winograd
-    epilogue), MIOpen + an add where no tile serves the shape."""
+    epilogue), MIOpen + an add where no tile serves the shape.  ``bias`` overrides the
+    module's (the fused ResnetBlock folds the shortcut's bias into it)."""
     lib = _hip.load_library()
     n, cin, h, w = x.shape
     cout = module.out_channels
+    bias = module.bias if bias is None else bias.contiguous()
     algo = _conv_algo(lib, cin, cout, h, w, conv_backend())
     if algo is None:
-        y = F.conv2d(x, module.weight, module.bias, padding=1)
+        y = F.conv2d(x, module.weight, bias, padding=1)
         return y if res is None else y.add_(res)
     x = x.contiguous()
     y = torch.empty(n, cout, h, w, device=x.device, dtype=torch.float32)
     pk = module._pack(algo, False)
     if algo == "wino" and res is not None:
-        _hip.check(lib.sp_wino3x3_fwd_res(_hip.ptr(x), _hip.ptr(pk), _hip.ptr(module.bias),
+        _hip.check(lib.sp_wino3x3_fwd_res(_hip.ptr(x), _hip.ptr(pk), _hip.ptr(bias),
                                           _hip.ptr(res.contiguous()), n, cin, cout, h, w,
                                           _hip.ptr(y), _hip.stream_of(x)), "sp_wino3x3_fwd_res")
         return y
     fn = lib.sp_wino3x3_fwd if algo == "wino" else lib.sp_conv3x3_fwd
-    _hip.check(fn(_hip.ptr(x), _hip.ptr(pk), _hip.ptr(module.bias), n, cin, cout, h, w, _hip.ptr(y),
+    _hip.check(fn(_hip.ptr(x), _hip.ptr(pk), _hip.ptr(bias), n, cin, cout, h, w, _hip.ptr(y),
                   _hip.stream_of(x)), f"sp_{algo}_conv3x3_fwd")
     return y if res is None else y.add_(res)
 

@@ -71,15 +71,17 @@ class TimestepEmbedding(nn.Module):
 
 
 def _shortcut_forward(conv: nn.Conv2d, x1: Tensor, x2: Tensor | None) -> Tensor:
-    """1x1 conv_shortcut over cat(x1, x2): W[:, :c1] x1 + W[:, c1:] x2 + b, the second
-    part accumulated in place by a batched GEMM (no concatenated input)."""
-    c1 = x1.shape[1]
-    y = F.conv2d(x1, conv.weight[:, :c1], conv.bias)
+    """1x1 conv_shortcut over cat(x1, x2) without its bias (the caller folds it into conv2's):
+    W[:, :c1] x1 + W[:, c1:] x2 as broadcast-batched GEMMs, the second part accumulated in
+    place (no concatenated input; 25-35 % faster than MIOpen's 1x1 path on these shapes,
+    tools/bench_shortcut.py)."""
+    n, c1 = x1.shape[:2]
+    w = conv.weight[:, :, 0, 0]
+    y = torch.matmul(w[:, :c1], x1.reshape(n, c1, -1))
     if x2 is not None:
-        n, cout = y.shape[:2]
-        w2 = conv.weight[:, c1:, 0, 0]
-        y.view(n, cout, -1).baddbmm_(w2.expand(n, *w2.shape), x2.reshape(n, x2.shape[1], -1))
-    return y
+        w2 = w[:, c1:]
+        y.baddbmm_(w2.expand(n, *w2.shape), x2.reshape(n, x2.shape[1], -1))
+    return y.reshape((n, w.shape[0]) + tuple(x1.shape[2:]))
 
 
 def _shortcut_input_vjp(conv: nn.Conv2d, dy: Tensor, c1: int, c2: int) -> tuple[Tensor, Tensor | None]:
@@ -111,11 +113,14 @@ class _ResnetBlockFn(torch.autograd.Function):
         h1 = conv3x3_forward(block.conv1, z1)
         del z1
         z2, st2 = gn_forward(block.norm2, h1, None, tb)
+        bias = block.conv2.bias
         if block.conv_shortcut is None:
             short = x1
         else:
             short = _shortcut_forward(block.conv_shortcut, x1, x2)
-        out = conv3x3_forward(block.conv2, z2, res=short)
+            if block.conv_shortcut.bias is not None:
+                bias = block.conv_shortcut.bias if bias is None else bias + block.conv_shortcut.bias
+        out = conv3x3_forward(block.conv2, z2, res=short, bias=bias)
         ctx.block = block
         ctx.save_for_backward(x1, x2, h1, tb, st1, st2)
         return out
