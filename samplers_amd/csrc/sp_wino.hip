@@ -90,9 +90,13 @@ constexpr int WR_NS = 4;    // unroll of the k-step ring (cin % (2 WR_NS) == 0)
 // TCW = 16 (images with W % 32 == 0): 2 x 16 tiles = 4 x 32 outputs; TCW = 8 (W = 16, the
 // UNet's 16x16 level): 4 x 8 tiles = 8 x 16 outputs.  A workgroup stacks two waves' rows
 // (and two 32-channel halves): 64 co x (4 TRW) x (2 TCW) outputs.
-template <int TCW_>
+template <int TCW_, bool MOSAIC_ = false>
 struct WGeo {
     static constexpr int TCW = TCW_;
+    // MOSAIC (8x8 images, the UNet's 8x8 level): the W = 16 geometry over two images side by
+    // side; in LDS image 1's columns start one position later, so one zero column (never
+    // written) is image 0's right and image 1's left padding.
+    static constexpr bool MOSAIC = MOSAIC_;
     static constexpr int TRW = 32 / TCW;
     static constexpr int ROWS = 2 * TRW + 2;     // input block rows per channel
     static constexpr int PPR = TCW / 2;          // 16-byte pieces per block row
@@ -122,6 +126,7 @@ struct WrSrc {                        // a tile's load sources
     const float* ub;                  // this lane's packed U rows at k-step 0
 };
 struct WrGeom {
+    int64_t batch;
     const float* x;
     const float* up;
     float* out;
@@ -134,6 +139,18 @@ struct WrGeom {
     int nsteps;
 };
 
+// First image of a wave's data and how many of its images exist (MOSAIC: 2 per wave).
+template <class GE>
+__device__ __forceinline__ int64_t wr_img0(const WrGeom& g, const WrTile& ti, int wv) {
+    return GE::MOSAIC ? ti.n + 2 * (wv >> 1) : ti.n;
+}
+template <class GE>
+__device__ __forceinline__ int wr_nimg(const WrGeom& g, const WrTile& ti, int wv) {
+    if constexpr (!GE::MOSAIC) return 1;
+    const int64_t left = g.batch - wr_img0<GE>(g, ti, wv);
+    return left <= 0 ? 0 : (left >= 2 ? 2 : 1);
+}
+
 template <class GE>
 __device__ __forceinline__ WrTile wr_tile(const WrGeom& g, int t, int wv) {
     // XCD-aware order: tiles t and t + 8 run on one XCD (persistent workgroups b and b + 8
@@ -141,6 +158,8 @@ __device__ __forceinline__ WrTile wr_tile(const WrGeom& g, int t, int wv) {
     // its neighbours) share an L2
     const int lb = (g.ntiles & 7) ? t : (t & 7) * (g.ntiles >> 3) + (t >> 3);
     const int co_blk = lb % g.cob, rest = lb / g.cob;
+    if constexpr (GE::MOSAIC)  // four images per workgroup, two per wave
+        return WrTile{4 * rest, 0, 0, co_blk * WR_CO + 32 * (wv & 1)};
     const int n = rest / g.per_img, r = rest - n * g.per_img;
     const int ty = r / g.tiles_w;
     return WrTile{n, ty * GE::WG_ROWS, (r - ty * g.tiles_w) * GE::WG_COLS, co_blk * WR_CO + 32 * (wv & 1)};
@@ -149,21 +168,26 @@ __device__ __forceinline__ WrTile wr_tile(const WrGeom& g, int t, int wv) {
 template <class GE>
 __device__ __forceinline__ WrSrc wr_src(const WrGeom& g, const WrTile& ti, int wv, int lane) {
     constexpr int OOB = 0x7FFFFFF0;  // outside the image: the buffer returns 0
-    const int row0 = ti.oh0 + 2 * GE::TRW * (wv >> 1) - 1;  // the wave's first input row
+    const int row0 = GE::MOSAIC ? -1 : ti.oh0 + 2 * GE::TRW * (wv >> 1) - 1;  // first input row
     const int ka = lane % GE::PPR, rca = lane / GE::PPR, rcb = 64 / GE::PPR + ((lane / GE::PPR) & 3);
     const int rch = (lane % (2 * GE::RC)) >> 1, side = lane & 1;
     auto goff = [&](int rc, int col) {
         const int ci = rc / GE::ROWS, gr = row0 + rc % GE::ROWS;
+        if constexpr (GE::MOSAIC) {  // virtual column -> (image, column); rows 0..7
+            return (unsigned)gr < (unsigned)g.H && col >= 0 && col < 2 * g.W
+                       ? ((col >> 3) * g.cin * g.plane + ci * g.plane + gr * g.W + (col & 7)) * 4
+                       : OOB;
+        }
         return ((unsigned)gr < (unsigned)g.H && (unsigned)col < (unsigned)g.W)
                    ? (ci * g.plane + gr * g.W + col) * 4 : OOB;
     };
     WrSrc s;
     s.rs = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<float*>(g.x + (int64_t)ti.n * g.cin * g.plane), (short)0, g.cin * g.plane * 4,
-        0x00020000);
+        const_cast<float*>(g.x + wr_img0<GE>(g, ti, wv) * g.cin * g.plane), (short)0,
+        wr_nimg<GE>(g, ti, wv) * g.cin * g.plane * 4, 0x00020000);
     s.oa = goff(rca, ti.ow0 + 4 * ka);
     s.ob = goff(rcb, ti.ow0 + 4 * ka);
-    s.oh = goff(rch, side ? ti.ow0 + 2 * GE::TCW : ti.ow0 - 1);
+    s.oh = GE::MOSAIC ? OOB : goff(rch, side ? ti.ow0 + 2 * GE::TCW : ti.ow0 - 1);
     s.ub = g.up + ((int64_t)(ti.co0 >> 5) * 64 + lane) * 16;
     return s;
 }
@@ -318,6 +342,11 @@ typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
 template <class GE>
 __device__ __forceinline__ int wr_out_voff(const WrGeom& g, const WrTile& ti, int wv, int lane) {
     const int hh = lane >> 5, l = lane & 31;
+    if constexpr (GE::MOSAIC) {
+        const int tr = l / GE::TCW, tc = l % GE::TCW;
+        return ((tc >> 2) * g.cout * g.plane + (ti.co0 + 4 * hh) * g.plane + 2 * tr * g.W +
+                2 * (tc & 3)) * 4;
+    }
     const int tr = GE::TRW * (wv >> 1) + l / GE::TCW, tc = l % GE::TCW;
     return ((ti.co0 + 4 * hh) * g.plane + (ti.oh0 + 2 * tr) * g.W + ti.ow0 + 2 * tc) * 4;
 }
@@ -330,8 +359,8 @@ template <class GE>
 __device__ __forceinline__ void wr_load_res(const WrGeom& g, const WrTile& ti, int wv, int lane,
                                             WrRes& rv) {
     const auto rrs = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<float*>(g.res) + (int64_t)ti.n * g.cout * g.plane, (short)0,
-        g.cout * g.plane * 4, 0x00020000);
+        const_cast<float*>(g.res) + wr_img0<GE>(g, ti, wv) * g.cout * g.plane, (short)0,
+        wr_nimg<GE>(g, ti, wv) * g.cout * g.plane * 4, 0x00020000);
     const int vo = wr_out_voff<GE>(g, ti, wv, lane);
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
@@ -346,7 +375,8 @@ __device__ __forceinline__ void wr_epilogue(const WrGeom& g, const WrTile& ti, i
                                             const f32x16 (&acc)[16], const WrRes& rv) {
     const int hh = lane >> 5, l = lane & 31;
     const auto ors = __builtin_amdgcn_make_buffer_rsrc(
-        g.out + (int64_t)ti.n * g.cout * g.plane, (short)0, g.cout * g.plane * 4, 0x00020000);
+        g.out + wr_img0<GE>(g, ti, wv) * g.cout * g.plane, (short)0,
+        wr_nimg<GE>(g, ti, wv) * g.cout * g.plane * 4, 0x00020000);
     const int vo = wr_out_voff<GE>(g, ti, wv, lane);
     // bias[co0 + (lane & 31)] in one register, each row's two values (channels c and c + 4)
     // read out with v_readlane; no bias: a zero-length buffer, whose loads return 0.
@@ -388,9 +418,9 @@ __device__ __forceinline__ void wr_epilogue(const WrGeom& g, const WrTile& ti, i
 // ring runs on across tile boundaries, so a tile's prologue latency and its predecessor's
 // store drain overlap MFMA work instead of leaving the CU idle (at one wave per SIMD no
 // other workgroup can fill those gaps).
-template <bool RES, int TCW>
+template <bool RES, int TCW, bool MOSAIC = false>
 __global__ __launch_bounds__(kBlock, 1) void k_wino3x3_r(WrGeom g) {
-    using GE = WGeo<TCW>;
+    using GE = WGeo<TCW, MOSAIC>;
     __shared__ __attribute__((aligned(16))) float xlds[4 * GE::WAVE];
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     float* const xw = xlds + wv * GE::WAVE;
@@ -399,11 +429,22 @@ __global__ __launch_bounds__(kBlock, 1) void k_wino3x3_r(WrGeom g) {
         auto loff = [](int rc) { return (rc / GE::ROWS) * GE::CI + GE::row(rc % GE::ROWS); };
         const int ka = lane % GE::PPR, rca = lane / GE::PPR, rcb = 64 / GE::PPR + ((lane / GE::PPR) & 3);
         const int rch = (lane % (2 * GE::RC)) >> 1, side = lane & 1;
-        xl.wa = loff(rca) + 4 + 4 * ka;
-        xl.wb = loff(rcb) + 4 + 4 * ka;
-        xl.wh = loff(rch) + (side ? 4 + 2 * GE::TCW : 3);
         const int l = lane & 31;
-        xl.rd = (lane >> 5) * GE::CI + GE::row(2 * (l / GE::TCW)) + 3 + 2 * (l % GE::TCW);
+        if constexpr (GE::MOSAIC) {
+            // image 1's columns one position later: cols 0..7 at 4..11 / 13..20; positions
+            // 3, 12, 21 hold the zero padding (12 is rewritten with the halo loads' zeros)
+            xl.wa = loff(rca) + 4 + 4 * ka + (ka >= 2);
+            xl.wb = loff(rcb) + 4 + 4 * ka + (ka >= 2);
+            xl.wh = loff(rch) + 12;
+            const int tc = l % GE::TCW;
+            xl.rd = (lane >> 5) * GE::CI + GE::row(2 * (l / GE::TCW)) + 3 + 2 * tc + (tc >= 4);
+            for (int i = lane; i < GE::WAVE; i += 64) xw[i] = 0.f;
+        } else {
+            xl.wa = loff(rca) + 4 + 4 * ka;
+            xl.wb = loff(rcb) + 4 + 4 * ka;
+            xl.wh = loff(rch) + (side ? 4 + 2 * GE::TCW : 3);
+            xl.rd = (lane >> 5) * GE::CI + GE::row(2 * (l / GE::TCW)) + 3 + 2 * (l % GE::TCW);
+        }
     }
     int t = blockIdx.x;
     const int stride = gridDim.x;
@@ -494,7 +535,8 @@ extern "C" {
 int sp_wino3x3_supported(int32_t cin, int32_t cout, int32_t height, int32_t width) {
     // W % 32: 32-column workgroup tiles of 8 rows; W = 16 (UNet 16x16 level): 16 x 16
     const bool geo = (width % WGeo<16>::WG_COLS == 0 && height % WGeo<16>::WG_ROWS == 0) ||
-                     (width == WGeo<8>::WG_COLS && height % WGeo<8>::WG_ROWS == 0);
+                     (width == WGeo<8>::WG_COLS && height % WGeo<8>::WG_ROWS == 0) ||
+                     (width == 8 && height == 8);  // MOSAIC
     return cin >= 16 && cout > 0 && cin % (2 * WR_NS) == 0 && cout % WR_CO == 0 && geo &&
            height > 0 && width > 0;
 }
@@ -532,10 +574,12 @@ static int wino3x3(int kind, const float* x, const float* up, const float* bias,
     if (!sp_wino3x3_supported(cin, cout, height, width) || n < 0) return SP_EINVAL;
     if (n == 0) return SP_OK;
     if (!x || !up || !y) return SP_EINVAL;
-    const bool narrow = width % WGeo<16>::WG_COLS != 0;  // the W = 16 geometry
+    const bool mosaic = width == 8;                     // 8x8 images, 4 per workgroup
+    const bool narrow = !mosaic && width % WGeo<16>::WG_COLS != 0;  // the W = 16 geometry
     const int wg_rows = narrow ? WGeo<8>::WG_ROWS : WGeo<16>::WG_ROWS;
     const int wg_cols = narrow ? WGeo<8>::WG_COLS : WGeo<16>::WG_COLS;
-    const int64_t tiles = n * (height / wg_rows) * (width / wg_cols) * (cout / WR_CO);
+    const int64_t tiles = mosaic ? (n + 3) / 4 * (cout / WR_CO)
+                                 : n * (height / wg_rows) * (width / wg_cols) * (cout / WR_CO);
     // per-sample planes are addressed by 32-bit buffer offsets (bytes < 2^31)
     if (tiles >= (int64_t(1) << 31) || (int64_t)cin * height * width * 4 >= (int64_t(1) << 31) ||
         (int64_t)cout * height * width * 4 >= (int64_t(1) << 31))
@@ -553,8 +597,9 @@ static int wino3x3(int kind, const float* x, const float* up, const float* bias,
     g.plane = height * width;
     g.ntiles = static_cast<int>(tiles);
     g.cob = cout / WR_CO;
-    g.tiles_w = width / wg_cols;
-    g.per_img = g.tiles_w * (height / wg_rows);
+    g.tiles_w = mosaic ? 1 : width / wg_cols;
+    g.per_img = mosaic ? 1 : g.tiles_w * (height / wg_rows);
+    g.batch = n;
     g.u_step = (int64_t)cout * 32;
     g.so_step = 2 * height * width * 4;
     g.nsteps = cin / 2;
@@ -565,7 +610,10 @@ static int wino3x3(int kind, const float* x, const float* up, const float* bias,
     const double flops = 8.0 * n * cin * cout * height * width;
     const dim3 gd(static_cast<unsigned>(grid)), bd(kBlock);
     hipStream_t st = static_cast<hipStream_t>(stream);
-    if (narrow) {
+    if (mosaic) {
+        if (res) launch_w(kind, flops, k_wino3x3_r<true, 8, true>, gd, bd, st, g);
+        else launch_w(kind, flops, k_wino3x3_r<false, 8, true>, gd, bd, st, g);
+    } else if (narrow) {
         if (res) launch_w(kind, flops, k_wino3x3_r<true, 8>, gd, bd, st, g);
         else launch_w(kind, flops, k_wino3x3_r<false, 8>, gd, bd, st, g);
     } else {

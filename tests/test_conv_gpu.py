@@ -79,7 +79,7 @@ def test_conv3x3_rejects_unsupported(cuda):
     assert not lib.sp_conv3x3_supported(128, 64, 32, 32)
     assert not lib.sp_conv3x3_supported(128, 128, 16, 16)
     assert not lib.sp_conv3x3_supported(128, 128, 4, 32)
-    conv = Conv3x3(128, 128).to(cuda)  # falls back to MIOpen at 16x16
+    conv = Conv3x3(128, 128).to(cuda)  # no direct tile at 16x16: the Winograd tile serves it
     x = torch.randn(1, 128, 16, 16, device=cuda)
     torch.testing.assert_close(conv(x), F.conv2d(x, conv.weight, conv.bias, padding=1))
 
@@ -115,11 +115,13 @@ def test_conv3x3_timing_records_flops(cuda, monkeypatch):
 
 @pytest.mark.parametrize("shape", [(2, 128, 128, 32, 64), (1, 256, 64, 16, 32), (2, 64, 128, 8, 96),
                                    (3, 64, 192, 24, 64), (3, 128, 64, 16, 16), (2, 64, 128, 32, 16),
-                                   (1, 512, 512, 16, 16)])
+                                   (1, 512, 512, 16, 16), (3, 64, 128, 8, 8), (5, 512, 512, 8, 8),
+                                   (8, 128, 64, 8, 8)])
 def test_winograd_forward_and_input_vjp(cuda, shape):
     """Winograd F(2x2,3x3) tile: fp32 transforms + exact fp32 MFMA accumulation; the
     transforms add F(2,3) rounding, so the bound is 1e-5 relative L2 (vs 2e-6 direct).
-    W = 16 shapes run the 4 x 8-tile wave geometry (the UNet's 16x16 level)."""
+    W = 16 shapes run the 4 x 8-tile wave geometry (the UNet's 16x16 level); 8x8 shapes the
+    same geometry over two images side by side (batches not a multiple of 4 included)."""
     n, cin, cout, h, w = shape
     lib = _hip.load_library()
     assert lib.sp_wino3x3_supported(cin, cout, h, w)
@@ -164,3 +166,6 @@ def test_winograd_residual_epilogue(cuda):
     x16 = torch.randn(2, 64, 16, 16, device=cuda)  # the W = 16 geometry
     r16 = torch.randn(2, 128, 16, 16, device=cuda)
     assert torch.equal(conv3x3_forward(conv, x16, res=r16), conv3x3_forward(conv, x16) + r16)
+    x8 = torch.randn(3, 64, 8, 8, device=cuda)  # the two-image mosaic geometry
+    r8 = torch.randn(3, 128, 8, 8, device=cuda)
+    assert torch.equal(conv3x3_forward(conv, x8, res=r8), conv3x3_forward(conv, x8) + r8)
