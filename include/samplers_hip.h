@@ -296,6 +296,17 @@ int sp_conv3x3_bwd_input(const float* dy, const float* wp_vjp, int64_t n, int32_
                          int32_t cout, int32_t height, int32_t width, float* dx,
                          sp_stream_t stream);
 
+/* 3x3 / stride 1 / pad 1 convolutions with few channels on one side (cout <= 8 or cin <= 8:
+ * the priors' conv_in / conv_out) as VALU direct convolutions on the raw weights
+ * [cout][cin][3][3]; the input VJP reads the same weights transposed and flipped. */
+int sp_conv3x3_thin_supported(int32_t cin, int32_t cout, int32_t height, int32_t width);
+int sp_conv3x3_thin_fwd(const float* x, const float* w, const float* bias, int64_t n,
+                        int32_t cin, int32_t cout, int32_t height, int32_t width, float* y,
+                        sp_stream_t stream);
+int sp_conv3x3_thin_bwd_input(const float* dy, const float* w, int64_t n, int32_t cin,
+                              int32_t cout, int32_t height, int32_t width, float* dx,
+                              sp_stream_t stream);
+
 /* The same layers by Winograd F(2x2,3x3) on fp32 MFMA (2.25x fewer multiplies; the
  * transforms add F(2,3) rounding, as MIOpen's Winograd solver does).  up = U = G g G^T
  * packed by sp_wino3x3_pack (input_vjp=1: of the transposed, flipped weights). */

@@ -172,6 +172,8 @@ def _conv_algo(lib, cin: int, cout: int, h: int, w: int, backend: str) -> str | 
         return "wino"
     if lib.sp_conv3x3_supported(cin, cout, h, w):
         return "direct"
+    if lib.sp_conv3x3_thin_supported(cin, cout, h, w):
+        return "thin"  # few channels on one side (conv_in / conv_out): VALU direct conv
     return None
 
 
@@ -190,6 +192,11 @@ def conv3x3_forward(module: "Conv3x3", x: Tensor, res: Tensor | None = None,
         return y if res is None else y.add_(res)
     x = x.contiguous()
     y = torch.empty(n, cout, h, w, device=x.device, dtype=torch.float32)
+    if algo == "thin":
+        _hip.check(lib.sp_conv3x3_thin_fwd(_hip.ptr(x), _hip.ptr(module.weight.detach().contiguous()),
+                                           _hip.ptr(bias), n, cin, cout, h, w, _hip.ptr(y),
+                                           _hip.stream_of(x)), "sp_conv3x3_thin_fwd")
+        return y if res is None else y.add_(res)
     pk = module._pack(algo, False)
     if algo == "wino" and res is not None:
         _hip.check(lib.sp_wino3x3_fwd_res(_hip.ptr(x), _hip.ptr(pk), _hip.ptr(bias),
@@ -212,6 +219,11 @@ def conv3x3_input_vjp(module: "Conv3x3", dy: Tensor, x_shape) -> Tensor:
     if algo is None:
         return torch.nn.grad.conv2d_input(tuple(x_shape), module.weight, dy, padding=1)
     dx = torch.empty(tuple(x_shape), device=dy.device, dtype=torch.float32)
+    if algo == "thin":
+        _hip.check(lib.sp_conv3x3_thin_bwd_input(_hip.ptr(dy), _hip.ptr(module.weight.detach().contiguous()),
+                                                 n, cin, cout, h, w, _hip.ptr(dx),
+                                                 _hip.stream_of(dy)), "sp_conv3x3_thin_bwd_input")
+        return dx
     fn = lib.sp_wino3x3_bwd_input if algo == "wino" else lib.sp_conv3x3_bwd_input
     _hip.check(fn(_hip.ptr(dy), _hip.ptr(module._pack(algo, True)), n, cin, cout, h, w,
                   _hip.ptr(dx), _hip.stream_of(dy)), f"sp_{algo}_conv3x3_bwd_input")
@@ -220,50 +232,33 @@ def conv3x3_input_vjp(module: "Conv3x3", dy: Tensor, x_shape) -> Tensor:
 
 class _Conv3x3Fn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, module, algo_fwd, algo_bwd):
-        lib = _hip.load_library()
-        n, cin, h, w = x.shape
-        cout = weight.shape[0]
-        x = x.contiguous()
-        y = torch.empty(n, cout, h, w, device=x.device, dtype=torch.float32)
-        pk = module._pack(algo_fwd, False)
-        fn = lib.sp_wino3x3_fwd if algo_fwd == "wino" else lib.sp_conv3x3_fwd
-        _hip.check(fn(_hip.ptr(x), _hip.ptr(pk), _hip.ptr(bias), n, cin, cout, h, w, _hip.ptr(y),
-                      _hip.stream_of(x)), f"sp_{algo_fwd}_conv3x3_fwd")
-        pv = module._pack(algo_bwd, True) if algo_bwd else None
-        ctx.save_for_backward(x, weight, pv)
+    def forward(ctx, x, weight, bias, module):
+        ctx.module = module
         ctx.has_bias = bias is not None
-        ctx.algo_bwd = algo_bwd
-        return y
+        ctx.save_for_backward(x if weight.requires_grad else None, weight)
+        ctx.x_shape = x.shape
+        return conv3x3_forward(module, x)
 
     @staticmethod
     def backward(ctx, dy):
-        x, weight, pv = ctx.saved_tensors
-        n, cin, h, w = x.shape
-        cout = weight.shape[0]
-        dy = dy.contiguous()
+        x, weight = ctx.saved_tensors
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
-            if ctx.algo_bwd:
-                lib = _hip.load_library()
-                dx = torch.empty_like(x)
-                fn = lib.sp_wino3x3_bwd_input if ctx.algo_bwd == "wino" else lib.sp_conv3x3_bwd_input
-                _hip.check(fn(_hip.ptr(dy), _hip.ptr(pv), n, cin, cout, h, w, _hip.ptr(dx),
-                              _hip.stream_of(dy)), f"sp_{ctx.algo_bwd}_conv3x3_bwd_input")
-            else:  # input VJP shape outside the tiles' rules (e.g. cin = 3 or 4): MIOpen
-                dx = torch.nn.grad.conv2d_input(x.shape, weight, dy, padding=1)
+            dx = conv3x3_input_vjp(ctx.module, dy, ctx.x_shape)
         if ctx.needs_input_grad[1]:
-            dw = torch.nn.grad.conv2d_weight(x, weight.shape, dy, padding=1)
+            dw = torch.nn.grad.conv2d_weight(x, weight.shape, dy.contiguous(), padding=1)
         if ctx.has_bias and ctx.needs_input_grad[2]:
             db = dy.sum(dim=(0, 2, 3))
-        return dx, dw, db, None, None, None
+        return dx, dw, db, None
 
 
 class Conv3x3(nn.Conv2d):
     """``nn.Conv2d(cin, cout, 3, padding=1)`` whose device forward / input VJP run this
-    project's fp32-MFMA tiles: Winograd F(2x2,3x3) (``csrc/sp_wino.hip``; cin % 8,
-    cout % 64, H % 8, W % 32) or the direct implicit GEMM (``csrc/sp_conv.hip``; cin % 4,
-    cout % 128, H % 8, W % 32), MIOpen elsewhere.  Transformed / packed weights are cached
+    project's kernels: the fp32-MFMA tiles — Winograd F(2x2,3x3) (``csrc/sp_wino.hip``;
+    cin % 8, cout % 64, W % 32 and H % 8, or 16x16, or 8x8) or the direct implicit GEMM
+    (``csrc/sp_conv.hip``; cin % 4, cout % 128, H % 8, W % 32) — or, with few channels on
+    one side (conv_in / conv_out), the thin VALU kernel (``csrc/sp_conv_thin.hip``);
+    MIOpen elsewhere.  Transformed / packed weights are cached
     per algorithm and rebuilt when the parameter changes."""
 
     def __init__(self, cin: int, cout: int) -> None:
@@ -291,10 +286,7 @@ class Conv3x3(nn.Conv2d):
     def forward(self, x: Tensor) -> Tensor:
         if x.is_cuda and x.dtype == torch.float32 and x.dim() == 4:
             lib = _hip.load_library()
-            be = conv_backend()
             n, cin, h, w = x.shape
-            algo = _conv_algo(lib, cin, self.out_channels, h, w, be)
-            if algo is not None:
-                algo_bwd = _conv_algo(lib, self.out_channels, cin, h, w, be)
-                return _Conv3x3Fn.apply(x, self.weight, self.bias, self, algo, algo_bwd)
+            if _conv_algo(lib, cin, self.out_channels, h, w, conv_backend()) is not None:
+                return _Conv3x3Fn.apply(x, self.weight, self.bias, self)
         return super().forward(x)

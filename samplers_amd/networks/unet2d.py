@@ -270,7 +270,7 @@ class UNet2DModel(nn.Module):
         g, eps = config.norm_num_groups, config.norm_eps
         temb = ch[0] * 4
         self.time_embedding = TimestepEmbedding(ch[0], temb)
-        self.conv_in = nn.Conv2d(config.in_channels, ch[0], 3, padding=1)
+        self.conv_in = Conv3x3(config.in_channels, ch[0])
 
         self.down_blocks = nn.ModuleList()
         cout = ch[0]
@@ -308,7 +308,7 @@ class UNet2DModel(nn.Module):
             prev = c
 
         self.conv_norm_out = GroupNormAct(g, ch[0], eps=eps, act=True)
-        self.conv_out = nn.Conv2d(ch[0], config.out_channels, 3, padding=1)
+        self.conv_out = Conv3x3(ch[0], config.out_channels)
 
     def forward(self, sample: Tensor, timestep: Tensor | int) -> Tensor:
         cfg = self.config

@@ -19,7 +19,7 @@ import torch
 import torch.nn.functional as F
 from torch import Tensor, nn
 
-from .layers import GroupNormAct
+from .layers import Conv3x3, GroupNormAct
 from .unet2d import Downsample2D, ResnetBlock2D, SpatialSelfAttention, Upsample2D
 
 
@@ -58,7 +58,7 @@ class Encoder(nn.Module):
     def __init__(self, c: VAEConfig) -> None:
         super().__init__()
         ch, g, eps = c.block_out_channels, c.norm_num_groups, c.norm_eps
-        self.conv_in = nn.Conv2d(c.in_channels, ch[0], 3, padding=1)
+        self.conv_in = Conv3x3(c.in_channels, ch[0])
         self.down_blocks = nn.ModuleList()
         cout = ch[0]
         for i, co in enumerate(ch):
@@ -70,7 +70,7 @@ class Encoder(nn.Module):
             self.down_blocks.append(blk)
         self.mid_block = _Mid(ch[-1], g, eps)
         self.conv_norm_out = GroupNormAct(g, ch[-1], eps=eps, act=True)
-        self.conv_out = nn.Conv2d(ch[-1], 2 * c.latent_channels, 3, padding=1)
+        self.conv_out = Conv3x3(ch[-1], 2 * c.latent_channels)
 
     def forward(self, x: Tensor) -> Tensor:
         h = self.conv_in(x)
@@ -88,7 +88,7 @@ class Decoder(nn.Module):
         super().__init__()
         ch, g, eps = c.block_out_channels, c.norm_num_groups, c.norm_eps
         rev = list(reversed(ch))
-        self.conv_in = nn.Conv2d(c.latent_channels, rev[0], 3, padding=1)
+        self.conv_in = Conv3x3(c.latent_channels, rev[0])
         self.mid_block = _Mid(rev[0], g, eps)
         self.up_blocks = nn.ModuleList()
         prev = rev[0]
@@ -100,7 +100,7 @@ class Decoder(nn.Module):
             self.up_blocks.append(blk)
             prev = co
         self.conv_norm_out = GroupNormAct(g, ch[0], eps=eps, act=True)
-        self.conv_out = nn.Conv2d(ch[0], c.out_channels, 3, padding=1)
+        self.conv_out = Conv3x3(ch[0], c.out_channels)
 
     def forward(self, z: Tensor) -> Tensor:
         h = self.mid_block(self.conv_in(z))

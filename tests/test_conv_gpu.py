@@ -169,3 +169,35 @@ def test_winograd_residual_epilogue(cuda):
     x8 = torch.randn(3, 64, 8, 8, device=cuda)  # the two-image mosaic geometry
     r8 = torch.randn(3, 128, 8, 8, device=cuda)
     assert torch.equal(conv3x3_forward(conv, x8, res=r8), conv3x3_forward(conv, x8) + r8)
+
+
+@pytest.mark.parametrize("shape", [(2, 3, 128, 32, 64), (3, 128, 3, 40, 66), (1, 4, 512, 16, 16),
+                                   (2, 512, 8, 16, 16), (2, 256, 4, 8, 10)])
+def test_thin_conv_forward_and_input_vjp(cuda, shape):
+    """The few-channel 3x3 kernel (conv_in / conv_out of the priors): forward with bias and
+    input VJP (transposed, flipped weights read in place) against fp64, ragged tiles
+    (H % 8, W % 64 != 0) included; fp32 accumulation, 2e-6 relative L2."""
+    n, cin, cout, h, w = shape
+    lib = _hip.load_library()
+    assert lib.sp_conv3x3_thin_supported(cin, cout, h, w)
+    assert lib.sp_conv3x3_thin_supported(cout, cin, h, w)
+    g = torch.Generator().manual_seed(5 + sum(shape))
+    x = torch.randn(n, cin, h, w, generator=g)
+    wt = torch.randn(cout, cin, 3, 3, generator=g) * (cin * 9) ** -0.5
+    b = torch.randn(cout, generator=g)
+    dy = torch.randn(n, cout, h, w, generator=g)
+    xd = x.double().requires_grad_()
+    ref = F.conv2d(xd, wt.double(), b.double(), padding=1)
+    (gref,) = torch.autograd.grad(ref, xd, dy.double())
+    st = torch.cuda.current_stream().cuda_stream
+    xg, wg, bg, dyg = x.to(cuda), wt.to(cuda), b.to(cuda), dy.to(cuda)
+    y = torch.full((n, cout, h, w), float("nan"), device=cuda)
+    dx = torch.full_like(xg, float("nan"))
+    _hip.check(lib.sp_conv3x3_thin_fwd(xg.data_ptr(), wg.data_ptr(), bg.data_ptr(), n, cin, cout, h, w,
+                                       y.data_ptr(), st), "thin fwd")
+    _hip.check(lib.sp_conv3x3_thin_bwd_input(dyg.data_ptr(), wg.data_ptr(), n, cin, cout, h, w,
+                                             dx.data_ptr(), st), "thin bwd")
+    rel = ((y.double().cpu() - ref.detach()).norm() / ref.detach().norm()).item()
+    assert rel < 2e-6, rel
+    rel = ((dx.double().cpu() - gref).norm() / gref.norm()).item()
+    assert rel < 2e-6, rel
