@@ -211,7 +211,8 @@ def test_adamw_step_matches_torch(cuda):
         g = torch.randn(1003)
         ref.grad = g.clone()
         opt.step()
-        _hip.check(lib.sp_adamw_step(p.data_ptr(), g.to(cuda).data_ptr(), mm.data_ptr(),
+        gd = g.to(cuda)  # held while the kernel runs
+        _hip.check(lib.sp_adamw_step(p.data_ptr(), gd.data_ptr(), mm.data_ptr(),
                                      vv.data_ptr(), p.numel(), adamw_coefficients(step, 5e-3),
                                      torch.cuda.current_stream().cuda_stream), "adamw")
     torch.testing.assert_close(p.cpu(), ref.detach(), rtol=1e-6, atol=1e-6)
