@@ -254,6 +254,14 @@ int sp_groupnorm_silu_bwd2(const float* dz, const float* x1, const float* x2, in
                            const float* add1, const float* add2, float* work,
                            sp_stream_t stream);
 
+/* Single-pass GroupNorm (default on): a team of workgroups per group keeps the group in
+ * registers across its reduction (forward reads x once, backward x and dz once).  enable:
+ * 1 on, 0 off (the two-pass kernels), < 0 query; returns the previous setting.  Process-wide;
+ * results are bit-identical either way.  team_timeouts: polls that gave up waiting for a
+ * team member (0 unless the GPU is shared with a kernel that holds CUs indefinitely). */
+int sp_groupnorm_single_pass(int32_t enable);
+int64_t sp_groupnorm_team_timeouts(void);
+
 /* ---- device-resident step schedule (hipGraph capture of a step) ----
  * One record per guided step, precomputed on the host in the same fp64->fp32 arithmetic
  * as the by-value calls; a device cursor selects the current record, so a captured step

@@ -143,6 +143,8 @@ SIGNATURES = {
     "sp_groupnorm_silu_bwd2": (ctypes.c_int, [_P, _P, _P, ctypes.c_int32, _P, _P, _P, _P, _P,
                                               _I64, ctypes.c_int32, _I64, ctypes.c_int32,
                                               ctypes.c_int32, _P, _P, _P, _P, _P, _P]),
+    "sp_groupnorm_single_pass": (ctypes.c_int, [ctypes.c_int32]),
+    "sp_groupnorm_team_timeouts": (_I64, []),
     "sp_wino3x3_fwd_res": (ctypes.c_int, [_P, _P, _P, _P, _I64, ctypes.c_int32, ctypes.c_int32,
                                           ctypes.c_int32, ctypes.c_int32, _P, _P]),
 }
@@ -169,6 +171,8 @@ def load_library() -> ctypes.CDLL:
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
+    if os.environ.get("SAMPLERS_AMD_GN_SINGLE_PASS", "1") == "0":  # two-pass GroupNorm kernels
+        lib.sp_groupnorm_single_pass(0)
     _lib = lib
     return lib
 

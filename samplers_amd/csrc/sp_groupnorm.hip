@@ -11,16 +11,30 @@
 //   bwd: stats  — A = sum(dy*gamma), B = sum(dy*gamma*xhat) per chunk (y recomputed)
 //        apply  — dx = rstd*(dy*gamma - A/n - xhat*B/n)
 // x is NCHW, so one group (sample n, channels g*Cg .. g*Cg+Cg-1) is one contiguous
-// run of Cg*HW floats; it is cut into chunks of 16384 floats, one workgroup each, so
-// the launch fills the chip even at batch 1.  The shift K is the group's first
+// run of Cg*HW floats; it is cut into chunks (16384 floats forward, 8192 backward), one
+// workgroup each, so the launch fills the chip even at batch 1.  Where the input is
+// float4-aligned, single-pass variants of both directions (below) replace the pairs.  The shift K is the group's first
 // element (removes the cancellation of plain sum/sum-of-squares); chunk partials are
 // combined in a fixed order (deterministic).  All four passes are HBM-bound.
 
 #include "sp_common.h"
 
+// No implicit mul+add contraction: which products the backend fuses depends on the code
+// around them, and the single-pass and two-pass kernels must round identically.
+#pragma clang fp contract(off)
+
 namespace sp {
 
-constexpr int GN_CHUNK = 16384;  // elements per workgroup
+// Elements per workgroup (chunk): forward 16384, backward 8192 (the single-pass backward
+// holds two tensors' chunks in registers; measured best on the UNet's shapes).
+#ifndef SP_GN_CHUNK_FWD
+#define SP_GN_CHUNK_FWD 16384
+#endif
+#ifndef SP_GN_CHUNK_BWD
+#define SP_GN_CHUNK_BWD 8192
+#endif
+constexpr int GN_CHUNK_FWD = SP_GN_CHUNK_FWD, GN_CHUNK_BWD = SP_GN_CHUNK_BWD;
+constexpr int GN_CHUNK_MIN = GN_CHUNK_FWD < GN_CHUNK_BWD ? GN_CHUNK_FWD : GN_CHUNK_BWD;
 
 // n / d for 0 <= n < 2^31 by multiply-high (d >= 1).
 struct FastDiv {
@@ -44,6 +58,7 @@ struct GnGeom {
     const float* beta;   // [C] or NULL (0)
     int C, G, Cg;
     uint32_t gs;         // elements per group
+    uint32_t chunk;      // elements per workgroup (GN_CHUNK_FWD / _BWD)
     int chunks;          // workgroups per group
     FastDiv hw_div;      // element (or float4) index in group -> channel in group
     float eps;
@@ -65,8 +80,7 @@ struct Parts {
 };
 
 template <typename T>
-__device__ __forceinline__ Parts<T> parts_of(T* x1, T* x2, const GnGeom& G) {
-    const int64_t gi = blockIdx.y;
+__device__ __forceinline__ Parts<T> parts_at(T* x1, T* x2, const GnGeom& G, int64_t gi) {
     const int64_t n = gi / G.G;
     const int64_t g0 = (gi - n * G.G) * (int64_t)G.gs;  // group start within the sample
     Parts<T> p;
@@ -80,6 +94,11 @@ __device__ __forceinline__ Parts<T> parts_of(T* x1, T* x2, const GnGeom& G) {
     const int64_t sp = (int64_t)G.c1hw - g0;
     p.split = static_cast<uint32_t>(sp < 0 ? 0 : (sp > (int64_t)G.gs ? G.gs : sp));
     return p;
+}
+
+template <typename T>
+__device__ __forceinline__ Parts<T> parts_of(T* x1, T* x2, const GnGeom& G) {
+    return parts_at<T>(x1, x2, G, blockIdx.y);
 }
 
 __device__ __forceinline__ float silu_f(float y) { return y / (1.f + __expf(-y)); }
@@ -100,17 +119,22 @@ struct GroupCtx {
 };
 
 template <int V>
-__device__ __forceinline__ GroupCtx group_ctx(const float* base, const GnGeom& G) {
+__device__ __forceinline__ GroupCtx group_ctx_at(const float* base, const GnGeom& G, int64_t gi,
+                                                 uint32_t chunk) {
     GroupCtx c;
-    const int64_t gi = blockIdx.y;
     c.n = gi / G.G;
     c.g = static_cast<int>(gi - c.n * G.G);
-    c.x = parts_of<const float>(base, G.x2, G);
+    c.x = parts_at<const float>(base, G.x2, G, gi);
     c.zoff = gi * (int64_t)G.gs;
-    const uint32_t nv = G.gs / V, per = GN_CHUNK / V;
-    c.lo = blockIdx.x * per;
+    const uint32_t nv = G.gs / V, per = G.chunk / V;
+    c.lo = chunk * per;
     c.hi = min(nv, c.lo + per);
     return c;
+}
+
+template <int V>
+__device__ __forceinline__ GroupCtx group_ctx(const float* base, const GnGeom& G) {
+    return group_ctx_at<V>(base, G, blockIdx.y, blockIdx.x);
 }
 
 template <int V>
@@ -331,10 +355,223 @@ __global__ __launch_bounds__(kBlock) void k_gn_bwd_apply(const float* __restrict
     }
 }
 
+
+// ---- single-pass kernels: one team of workgroups per group -------------------------------
+// The two-pass kernels read their inputs twice (forward: x for the moments, then x again to
+// normalise; backward: x and dz for the two sums, then again for dx).  Here the workgroups of
+// a team (one per chunk of the group) keep their chunk in registers across the group
+// reduction: each publishes its chunk partials as two 64-bit words {value, 1} with
+// agent-scope atomic stores (coherent across the XCDs' L2s, no cache flush), then polls the
+// team's words until all are present (the words are zeroed before the launch).  The grid is
+// persistent and no larger than the chip's resident capacity, so a team's members are
+// resident together; each team walks groups gi = team, team + nteams, ...  Chunking, the
+// per-thread element order and the summation order are those of the two-pass kernels, so
+// the results are bit-identical.  HBM traffic: forward 2 passes (was 3), backward 3 + the
+// addend (was 5 + the addend).
+constexpr int GNT_MAX_SPINS = 1 << 22;          // poll bound (~0.3 s): a stuck team exits
+
+__device__ unsigned int g_gnt_timeouts;  // polls that hit GNT_MAX_SPINS (sp_groupnorm_team_timeouts)
+
+__device__ __forceinline__ void gnt_publish(uint64_t* slot, float a, float b) {
+    __hip_atomic_store(slot, (uint64_t(1) << 32) | __float_as_uint(a), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(slot + 1, (uint64_t(1) << 32) | __float_as_uint(b), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// The team's sums, as group_sums forms them (lane i of every wave takes chunk i, i + 64, ...,
+// then a wave sum).  The words are polled by the first `chunks` threads only and passed
+// through LDS (sv: 2 x GNT_MAX_CHUNKS floats); a barrier separates the two.
+constexpr int GNT_MAX_CHUNKS = 256;
+
+__device__ __forceinline__ void gnt_sums(uint64_t* slots, int chunks, float* sv, float& a, float& b) {
+    const int t = threadIdx.x;
+    if (t < chunks) {
+        uint64_t wa = 0, wb = 0;
+#pragma nounroll
+        for (int spins = 0; spins <= GNT_MAX_SPINS; ++spins) {
+            wa = __hip_atomic_load(slots + 2 * t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            wb = __hip_atomic_load(slots + 2 * t + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if ((wa >> 32) && (wb >> 32)) break;
+            __builtin_amdgcn_s_sleep(2);
+        }
+        if (!((wa >> 32) && (wb >> 32))) atomicAdd(&g_gnt_timeouts, 1u);
+        sv[t] = __uint_as_float(static_cast<uint32_t>(wa));
+        sv[GNT_MAX_CHUNKS + t] = __uint_as_float(static_cast<uint32_t>(wb));
+    }
+    __syncthreads();
+    a = 0.f, b = 0.f;
+    for (int i = t & 63; i < chunks; i += 64) a += sv[i], b += sv[GNT_MAX_CHUNKS + i];
+    a = wave_sum(a);
+    b = wave_sum(b);
+}
+
+// Block-reduce (a, b) as the two-pass kernels do and publish them as chunk m's words.
+__device__ __forceinline__ void gnt_reduce_publish(float a, float b, float* red, uint64_t* slot) {
+    a = wave_sum(a);
+    b = wave_sum(b);
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    if (lane == 0) red[wid] = a, red[4 + wid] = b;
+    __syncthreads();
+    if (threadIdx.x == 0) gnt_publish(slot, (red[0] + red[1]) + (red[2] + red[3]),
+                                      (red[4] + red[5]) + (red[6] + red[7]));
+}
+
+// A group's elements in one tensor part (the team kernels require that no group straddles
+// the two parts of a concatenated input): buffer resource over the chunk's first `lim`
+// float4 of the group, so accesses past the chunk end read 0 / are dropped.  The range
+// check covers the VGPR offset only (not soffset), so a thread's float4 i is addressed as
+// voffset (lo + tid + i * kBlock) * 16.
+template <typename T>
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t gnt_rsrc(const Parts<T>& p, uint32_t lim) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p.split ? p.p1 : p.p2), (short)0,
+                                             lim * 16, 0x00020000);
+}
+
+typedef float gnt_f4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ void gnt_load(__amdgpu_buffer_rsrc_t r, uint32_t vo, int i, float (&d)[4]) {
+    const gnt_f4 t = __builtin_bit_cast(gnt_f4, __builtin_amdgcn_raw_buffer_load_b128(r, vo + i * kBlock * 16, 0, 0));
+    d[0] = t[0], d[1] = t[1], d[2] = t[2], d[3] = t[3];
+}
+
+__device__ __forceinline__ void gnt_store(__amdgpu_buffer_rsrc_t r, uint32_t vo, int i, const float (&d)[4]) {
+    typedef unsigned u4 __attribute__((ext_vector_type(4)));
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, gnt_f4{d[0], d[1], d[2], d[3]}), r,
+                                           vo + i * kBlock * 16, 0, 0);
+}
+
+template <bool ACT, int GNT_PER>  // GNT_PER: float4 per thread (chunk / 4 / kBlock)
+__global__ __launch_bounds__(kBlock, 2) void k_gn_fwd_team(const float* __restrict__ x, GnGeom G,
+                                                           uint64_t* __restrict__ slots, int nteams,
+                                                           int64_t ngroups, float* __restrict__ z,
+                                                           float* __restrict__ mean_out,
+                                                           float* __restrict__ rstd_out) {
+    __shared__ float red[8];
+    __shared__ float sv[2 * GNT_MAX_CHUNKS];
+    const uint32_t m = blockIdx.x % G.chunks;
+    for (int64_t gi = blockIdx.x / G.chunks; gi < ngroups; gi += nteams) {
+        const GroupCtx c = group_ctx_at<4>(x, G, gi, m);
+        const auto rx = gnt_rsrc(c.x, c.hi);
+        const uint32_t vo = (c.lo + threadIdx.x) * 16;
+        float v[GNT_PER][4];
+#pragma unroll
+        for (int i = 0; i < GNT_PER; ++i) gnt_load(rx, vo, i, v[i]);
+        const float K = *c.x.at(0) + (G.bias ? G.bias[c.n * G.C + c.g * G.Cg] : 0.f);
+        float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+        for (int i = 0; i < GNT_PER; ++i) {
+            const uint32_t j = c.lo + threadIdx.x + i * kBlock;
+            const bool in = j < c.hi;  // past the chunk end: adds exact zeros
+            const float b = G.bias ? G.bias[c.n * G.C + chan_of<4>(in ? j : c.lo, c, G)] : 0.f;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const float d = in ? v[i][e] + b - K : 0.f;
+                s1 += d;
+                s2 = fmaf(d, d, s2);
+            }
+        }
+        uint64_t* gslots = slots + gi * G.chunks * 2;
+        gnt_reduce_publish(s1, s2, red, gslots + 2 * m);
+        float S1, S2;
+        gnt_sums(gslots, G.chunks, sv, S1, S2);
+        const float inv_n = 1.f / static_cast<float>(G.gs);
+        const float m1 = S1 * inv_n;
+        const float mean = K + m1;
+        const float var = fmaxf(S2 * inv_n - m1 * m1, 0.f);
+        const float rstd = rsqrtf(var + G.eps);
+        if (m == 0 && threadIdx.x == 0) mean_out[gi] = mean, rstd_out[gi] = rstd;
+        const Parts<float> zp{z + c.zoff, z + c.zoff, G.gs};
+        const auto rz = gnt_rsrc(zp, c.hi);
+#pragma unroll
+        for (int i = 0; i < GNT_PER; ++i) {
+            const uint32_t j = c.lo + threadIdx.x + i * kBlock;
+            const int ch = chan_of<4>(j < c.hi ? j : c.lo, c, G);
+            const float b = G.bias ? G.bias[c.n * G.C + ch] : 0.f;
+            const float sc = rstd * (G.gamma ? G.gamma[ch] : 1.f);
+            const float sh = (G.beta ? G.beta[ch] : 0.f) - mean * sc;
+            float o[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const float y = fmaf(v[i][e] + b, sc, sh);
+                o[e] = ACT ? silu_f(y) : y;
+            }
+            gnt_store(rz, vo, i, o);  // past the chunk end: dropped
+        }
+        __syncthreads();  // red[] is reused by the next group
+    }
+}
+
+template <bool ACT, int GNT_PER>
+__global__ __launch_bounds__(kBlock, 2) void k_gn_bwd_team(
+    const float* __restrict__ dz, const float* __restrict__ x, GnGeom G,
+    const float* __restrict__ mean_in, const float* __restrict__ rstd_in,
+    uint64_t* __restrict__ slots, int nteams, int64_t ngroups, float* __restrict__ dx,
+    float* __restrict__ dx2, const float* __restrict__ add1, const float* __restrict__ add2) {
+    __shared__ float red[8];
+    __shared__ float sv[2 * GNT_MAX_CHUNKS];
+    const uint32_t m = blockIdx.x % G.chunks;
+    for (int64_t gi = blockIdx.x / G.chunks; gi < ngroups; gi += nteams) {
+        const GroupCtx c = group_ctx_at<4>(x, G, gi, m);
+        const float mean = mean_in[gi], rstd = rstd_in[gi];
+        const auto rx = gnt_rsrc(c.x, c.hi);
+        const Parts<const float> dzp{dz + c.zoff, dz + c.zoff, G.gs};
+        const auto rg = gnt_rsrc(dzp, c.hi);
+        const uint32_t vo = (c.lo + threadIdx.x) * 16;
+        float v[GNT_PER][4], g[GNT_PER][4];
+#pragma unroll
+        for (int i = 0; i < GNT_PER; ++i) {
+            gnt_load(rx, vo, i, v[i]);
+            gnt_load(rg, vo, i, g[i]);
+        }
+        // v, g are replaced by dy*gamma and xhat: the dx pass needs nothing else
+        float sa = 0.f, sb = 0.f;
+#pragma unroll
+        for (int i = 0; i < GNT_PER; ++i) {
+            const uint32_t j = c.lo + threadIdx.x + i * kBlock;
+            const bool in = j < c.hi;  // past the chunk end: adds exact zeros
+            const int ch = chan_of<4>(in ? j : c.lo, c, G);
+            float gdy[4], xh[4];
+            gn_grad_terms<4, ACT>(v[i], g[i], G.bias ? G.bias[c.n * G.C + ch] : 0.f, mean, rstd,
+                                  G.gamma ? G.gamma[ch] : 1.f, G.beta ? G.beta[ch] : 0.f, gdy, xh);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                sa += in ? gdy[e] : 0.f;
+                sb = fmaf(in ? gdy[e] : 0.f, xh[e], sb);
+                g[i][e] = gdy[e];
+                v[i][e] = xh[e];
+            }
+        }
+        uint64_t* gslots = slots + gi * G.chunks * 2;
+        gnt_reduce_publish(sa, sb, red, gslots + 2 * m);
+        float A, B;
+        gnt_sums(gslots, G.chunks, sv, A, B);
+        const float inv_n = 1.f / static_cast<float>(G.gs);
+        const float mA = A * inv_n, mB = B * inv_n;
+        const auto rd = gnt_rsrc(parts_at<float>(dx, G.x2 ? dx2 : nullptr, G, gi), c.hi);
+        const auto ra = gnt_rsrc(parts_at<const float>(add1, G.x2 ? add2 : nullptr, G, gi),
+                                 add1 ? c.hi : 0);
+#pragma unroll
+        for (int i = 0; i < GNT_PER; ++i) {
+            float o[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) o[e] = rstd * (g[i][e] - mA - v[i][e] * mB);
+            if (add1) {  // as k_gn_bwd_apply (same rounding)
+                float ad[4];
+                gnt_load(ra, vo, i, ad);
+#pragma unroll
+                for (int e = 0; e < 4; ++e) o[e] += ad[e];
+            }
+            gnt_store(rd, vo, i, o);
+        }
+        __syncthreads();
+    }
+}
+
 // ---- host side --------------------------------------------------------------------------
 static int gn_geom(int64_t n, int32_t c, int64_t hw, int32_t groups, const float* bias,
-                   const float* gamma, const float* beta, float eps, GnGeom* G, int* V,
-                   dim3* grid) {
+                   const float* gamma, const float* beta, float eps, int chunk, GnGeom* G,
+                   int* V, dim3* grid) {
     if (n < 0 || c <= 0 || hw <= 0 || groups <= 0 || c % groups) return SP_EINVAL;
     const int64_t gs = (int64_t)(c / groups) * hw;
     if (gs >= (int64_t(1) << 31) || n * groups >= 65536) return SP_EINVAL;
@@ -342,7 +579,8 @@ static int gn_geom(int64_t n, int32_t c, int64_t hw, int32_t groups, const float
     G->bias = bias, G->gamma = gamma, G->beta = beta;
     G->C = c, G->G = groups, G->Cg = c / groups;
     G->gs = static_cast<uint32_t>(gs);
-    G->chunks = static_cast<int>((gs + GN_CHUNK - 1) / GN_CHUNK);
+    G->chunk = static_cast<uint32_t>(chunk);
+    G->chunks = static_cast<int>((gs + chunk - 1) / chunk);
     G->hw_div = make_fastdiv(static_cast<uint32_t>(hw / *V));
     G->eps = eps;
     G->x2 = nullptr;
@@ -350,6 +588,19 @@ static int gn_geom(int64_t n, int32_t c, int64_t hw, int32_t groups, const float
     G->s2 = 0;
     *grid = dim3(G->chunks, static_cast<unsigned>(n * groups));
     return SP_OK;
+}
+
+static int g_single_pass = 1;  // sp_groupnorm_single_pass
+
+// Teams that fit the chip at once for a team kernel (0: the kernel cannot run).
+static int64_t gnt_teams(const void* kernel, int64_t ngroups, int chunks) {
+    int dev = 0, cus = 0, per_cu = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, kBlock, 0) != hipSuccess)
+        return 0;
+    const int64_t teams = (int64_t)cus * per_cu / chunks;
+    return teams < ngroups ? teams : ngroups;
 }
 
 }  // namespace sp
@@ -361,7 +612,20 @@ extern "C" {
 int64_t sp_groupnorm_workspace(int64_t n, int32_t channels, int64_t hw, int32_t groups) {
     if (n < 0 || channels <= 0 || hw <= 0 || groups <= 0 || channels % groups) return -1;
     const int64_t gs = (int64_t)(channels / groups) * hw;
-    return n * groups * ((gs + GN_CHUNK - 1) / GN_CHUNK) * 2;
+    // two-pass: 2 floats per chunk; single pass: 2 64-bit words per chunk
+    return n * groups * ((gs + GN_CHUNK_MIN - 1) / GN_CHUNK_MIN) * 4;
+}
+
+int sp_groupnorm_single_pass(int32_t enable) {
+    const int prev = g_single_pass;
+    if (enable >= 0) g_single_pass = enable ? 1 : 0;
+    return prev;
+}
+
+int64_t sp_groupnorm_team_timeouts(void) {
+    unsigned int v = 0;
+    if (hipMemcpyFromSymbol(&v, HIP_SYMBOL(g_gnt_timeouts), sizeof(v)) != hipSuccess) return -1;
+    return v;
 }
 
 // second part of a channel-concatenated input: x2 != NULL holds channels c1 .. channels-1
@@ -389,13 +653,29 @@ int sp_groupnorm_silu_fwd2(const float* x, const float* x2, int32_t c1, const fl
     GnGeom G;
     int V;
     dim3 grid;
-    int rc = gn_geom(n, channels, hw, groups, chan_bias, gamma, beta, eps, &G, &V, &grid);
+    int rc = gn_geom(n, channels, hw, groups, chan_bias, gamma, beta, eps, GN_CHUNK_FWD, &G, &V,
+                     &grid);
     if (rc == SP_OK) rc = gn_split(&G, x2, c1, channels, hw);
     if (rc != SP_OK) return rc;
     if (n == 0) return SP_OK;  // empty batch: nothing to read or write
     if (!x || !z || !mean || !rstd || !work) return SP_EINVAL;
     hipStream_t s = static_cast<hipStream_t>(stream);
     const dim3 blk(kBlock);
+    if (V == 4 && g_single_pass && (!x2 || c1 % G.Cg == 0)) {
+        const int64_t ngroups = n * groups;
+        constexpr int PER = GN_CHUNK_FWD / 4 / kBlock;
+        auto kern = act ? k_gn_fwd_team<true, PER> : k_gn_fwd_team<false, PER>;
+        const int64_t teams = G.chunks <= GNT_MAX_CHUNKS
+            ? gnt_teams(reinterpret_cast<const void*>(kern), ngroups, G.chunks) : 0;
+        if (teams > 0) {
+            uint64_t* slots = reinterpret_cast<uint64_t*>(work);
+            if (hipMemsetAsync(slots, 0, ngroups * G.chunks * 16, s) != hipSuccess)
+                return check_launch("sp_groupnorm_silu_fwd (slots)");
+            launch(0, kern, dim3(static_cast<unsigned>(teams * G.chunks)), blk, s, x, G, slots,
+                   static_cast<int>(teams), ngroups, z, mean, rstd);
+            return check_launch("sp_groupnorm_silu_fwd");
+        }
+    }
     if (V == 4) {
         launch(0, k_gn_stats<4>, grid, blk, s, x, G, work);
         if (act) launch(0, k_gn_apply<4, true>, grid, blk, s, x, G, (const float*)work, z, mean, rstd);
@@ -427,7 +707,8 @@ int sp_groupnorm_silu_bwd2(const float* dz, const float* x, const float* x2, int
     GnGeom G;
     int V;
     dim3 grid;
-    int rc = gn_geom(n, channels, hw, groups, chan_bias, gamma, beta, 0.f, &G, &V, &grid);
+    int rc = gn_geom(n, channels, hw, groups, chan_bias, gamma, beta, 0.f, GN_CHUNK_BWD, &G, &V,
+                     &grid);
     if (rc == SP_OK) rc = gn_split(&G, x2, c1, channels, hw);
     if (rc != SP_OK) return rc;
     if (n == 0) return SP_OK;
@@ -435,6 +716,21 @@ int sp_groupnorm_silu_bwd2(const float* dz, const float* x, const float* x2, int
         return SP_EINVAL;
     hipStream_t s = static_cast<hipStream_t>(stream);
     const dim3 blk(kBlock);
+    if (V == 4 && g_single_pass && (!x2 || c1 % G.Cg == 0)) {
+        const int64_t ngroups = n * groups;
+        constexpr int PER = GN_CHUNK_BWD / 4 / kBlock;
+        auto kern = act ? k_gn_bwd_team<true, PER> : k_gn_bwd_team<false, PER>;
+        const int64_t teams = G.chunks <= GNT_MAX_CHUNKS
+            ? gnt_teams(reinterpret_cast<const void*>(kern), ngroups, G.chunks) : 0;
+        if (teams > 0) {
+            uint64_t* slots = reinterpret_cast<uint64_t*>(work);
+            if (hipMemsetAsync(slots, 0, ngroups * G.chunks * 16, s) != hipSuccess)
+                return check_launch("sp_groupnorm_silu_bwd (slots)");
+            launch(0, kern, dim3(static_cast<unsigned>(teams * G.chunks)), blk, s, dz, x, G, mean,
+                   rstd, slots, static_cast<int>(teams), ngroups, dx, dx2, add1, add2);
+            return check_launch("sp_groupnorm_silu_bwd");
+        }
+    }
 #define SP_GN_BWD(VV, AA)                                                                      \
     launch(0, k_gn_bwd_stats<VV, AA>, grid, blk, s, dz, x, G, mean, rstd, work);              \
     launch(0, k_gn_bwd_apply<VV, AA>, grid, blk, s, dz, x, G, mean, rstd, (const float*)work, dx, \

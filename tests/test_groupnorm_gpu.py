@@ -153,3 +153,52 @@ def test_fused_resnet_blocks_match_cpu(cuda):
     (gx,) = torch.autograd.grad(out, xg, v.to(cuda))
     assert _rel(out.detach().cpu(), ref.detach()) < 1e-4
     assert _rel(gx.cpu(), gref) < 1e-4
+
+
+@pytest.mark.parametrize("shape", [  # (n, c1, c2, h, w, groups)
+    (2, 128, 128, 64, 64, 32),    # 8 channels per group, 4 chunks per group
+    (3, 64, 0, 48, 48, 32),       # 2 channels x 2304: one partial chunk
+    (2, 128, 0, 256, 256, 32),    # 16 chunks per group
+    (5, 256, 256, 8, 8, 32),      # many small groups: several groups per team
+    (2, 96, 32, 16, 16, 32),      # c1 % (channels per group) == 0 with a 2-part split
+])
+@pytest.mark.parametrize("act", [True, False])
+def test_single_pass_matches_two_pass_bitwise(cuda, shape, act):
+    """The single-pass team kernels (one workgroup per chunk, chunk partials exchanged through
+    agent-scope atomics) against the two-pass kernels: same chunking, same summation order,
+    so the forward output, statistics and the input VJP agree bit for bit."""
+    from samplers_amd import _hip
+    from samplers_amd.networks.layers import gn_backward, gn_forward
+
+    lib = _hip.load_library()
+    n, c1, c2, h, w, g = shape
+    gen = torch.Generator().manual_seed(sum(shape) + act)
+    c = c1 + c2
+    layer = GroupNormAct(g, c, eps=1e-6, act=act)
+    with torch.no_grad():
+        layer.weight.copy_(1 + 0.3 * torch.randn(c, generator=gen))
+        layer.bias.copy_(0.2 * torch.randn(c, generator=gen))
+    layer = layer.to(cuda)
+    x1 = (torch.randn(n, c1, h, w, generator=gen) * 2 + 0.5).to(cuda)
+    x2 = (torch.randn(n, c2, h, w, generator=gen) - 0.3).to(cuda) if c2 else None
+    cb = torch.randn(n, c, generator=gen).to(cuda)
+    dz = torch.randn(n, c, h, w, generator=gen).to(cuda)
+    a1 = torch.randn(n, c1, h, w, generator=gen).to(cuda)
+    a2 = torch.randn(n, c2, h, w, generator=gen).to(cuda) if c2 else None
+    outs = []
+    prev = lib.sp_groupnorm_single_pass(-1)
+    try:
+        for mode in (0, 1):
+            lib.sp_groupnorm_single_pass(mode)
+            z, st = gn_forward(layer, x1, x2, cb)
+            d1, d2 = gn_backward(layer, dz, x1, x2, cb, st, add1=a1, add2=a2)
+            torch.cuda.synchronize()
+            outs.append((z, st, d1, d2))
+    finally:
+        lib.sp_groupnorm_single_pass(prev)
+    assert lib.sp_groupnorm_team_timeouts() == 0
+    for a, b in zip(outs[0], outs[1]):
+        if a is None:
+            assert b is None
+            continue
+        assert torch.equal(a, b)
