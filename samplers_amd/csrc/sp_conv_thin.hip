@@ -8,7 +8,8 @@
 // The work is ~14 k FMA per output pixel at most and the memory traffic is the wide side's
 // tensor, so this is a VALU direct convolution: one workgroup = an 8 x 64 pixel tile of one
 // image x CO output channels; input channels are walked in chunks of CI, each chunk's
-// 10 x 66 patch (zero outside the image = the padding) staged in LDS; every thread owns two
+// 10 x 66 patch (zero outside the image = the padding) staged in LDS with float4 row
+// pieces (W % 4 == 0); every thread owns two
 // horizontally adjacent pixels x CO outputs, reads its 3 x 4 window per channel from LDS
 // and takes the weights as wave-uniform scalar loads.  The input VJP is the same kernel on
 // the transposed, flipped weights (strides + flip flag, no repacking).
@@ -18,8 +19,12 @@
 namespace sp {
 
 constexpr int TN_TH = 8, TN_TW = 64;        // output tile
-constexpr int TN_PH = TN_TH + 2, TN_PW = TN_TW + 2;
-constexpr int TN_PATCH = TN_PH * TN_PW;     // 660
+constexpr int TN_PH = TN_TH + 2;
+// patch row in LDS: [3] left padding column, [4, 68) the tile's 64 columns (16-byte
+// aligned, so the row is staged with float4 loads and stores), [68] right padding column
+constexpr int TN_PW = TN_TW + 8;
+constexpr int TN_PATCH = TN_PH * TN_PW;     // 720
+constexpr int TN_Q = TN_TW / 4;             // float4 pieces per patch row
 
 struct ThinArgs {
     const float* x;      // [n, cin, H, W]
@@ -34,7 +39,7 @@ struct ThinArgs {
 
 template <int CI, int CO>
 __global__ __launch_bounds__(kBlock) void k_conv3x3_thin(ThinArgs a) {
-    __shared__ float patch[CI * TN_PATCH];
+    __shared__ __attribute__((aligned(16))) float patch[CI * TN_PATCH];
     const int tile = blockIdx.x;
     const int co0 = blockIdx.y * CO;
     const int64_t n = blockIdx.z;
@@ -51,12 +56,22 @@ __global__ __launch_bounds__(kBlock) void k_conv3x3_thin(ThinArgs a) {
     }
     for (int c0 = 0; c0 < a.cin; c0 += CI) {
         __syncthreads();  // previous chunk's patch reads are done
-        for (int i = threadIdx.x; i < CI * TN_PATCH; i += kBlock) {
-            const int c = i / TN_PATCH, rem = i - c * TN_PATCH;
-            const int r = rem / TN_PW, col = rem - r * TN_PW;
-            const int gr = h0 - 1 + r, gc = w0 - 1 + col;
+        for (int i = threadIdx.x; i < CI * TN_PH * TN_Q; i += kBlock) {  // interior columns
+            const int cr = i / TN_Q, q = i - cr * TN_Q;                  // (channel, row), piece
+            const int c = cr / TN_PH, r = cr - c * TN_PH;
+            const int gr = h0 - 1 + r, gc = w0 + 4 * q;
+            float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (c0 + c < a.cin && (unsigned)gr < (unsigned)a.H && gc < a.W)
+                v = *reinterpret_cast<const float4*>(xn + (int64_t)(c0 + c) * plane + (int64_t)gr * a.W + gc);
+            *reinterpret_cast<float4*>(&patch[c * TN_PATCH + r * TN_PW + 4 + 4 * q]) = v;
+        }
+        for (int i = threadIdx.x; i < CI * TN_PH * 2; i += kBlock) {  // padding columns
+            const int cr = i >> 1, side = i & 1;
+            const int c = cr / TN_PH, r = cr - c * TN_PH;
+            const int gr = h0 - 1 + r, gc = side ? w0 + TN_TW : w0 - 1;
             const bool ok = c0 + c < a.cin && (unsigned)gr < (unsigned)a.H && (unsigned)gc < (unsigned)a.W;
-            patch[i] = ok ? xn[(int64_t)(c0 + c) * plane + (int64_t)gr * a.W + gc] : 0.f;
+            patch[c * TN_PATCH + r * TN_PW + (side ? 4 + TN_TW : 3)] =
+                ok ? xn[(int64_t)(c0 + c) * plane + (int64_t)gr * a.W + gc] : 0.f;
         }
         __syncthreads();
 #pragma unroll
@@ -66,7 +81,7 @@ __global__ __launch_bounds__(kBlock) void k_conv3x3_thin(ThinArgs a) {
 #pragma unroll
             for (int r = 0; r < 3; ++r)
 #pragma unroll
-                for (int s = 0; s < 4; ++s) win[r][s] = patch[c * TN_PATCH + (pr + r) * TN_PW + pc + s];
+                for (int s = 0; s < 4; ++s) win[r][s] = patch[c * TN_PATCH + (pr + r) * TN_PW + 3 + pc + s];
 #pragma unroll
             for (int o = 0; o < CO; ++o) {
                 if (co0 + o >= a.cout) break;
@@ -101,7 +116,7 @@ static int thin_launch(const ThinArgs& a0, int64_t n, hipStream_t s, int kind) {
     a.tiles_w = (a.W + TN_TW - 1) / TN_TW;
     a.tiles = a.tiles_w * ((a.H + TN_TH - 1) / TN_TH);
     if (n > 65535 || (int64_t)a.cin * a.H * a.W >= (int64_t(1) << 31) ||
-        (int64_t)a.cout * a.H * a.W >= (int64_t(1) << 31) || (a.W & 1))
+        (int64_t)a.cout * a.H * a.W >= (int64_t(1) << 31) || (a.W & 3))
         return SP_EINVAL;
     const double flops = 18.0 * n * a.cin * a.cout * a.H * a.W;
 #define SP_THIN(CI_, CO_)                                                                    \
@@ -126,7 +141,7 @@ using namespace sp;
 extern "C" {
 
 int sp_conv3x3_thin_supported(int32_t cin, int32_t cout, int32_t height, int32_t width) {
-    return cin > 0 && cout > 0 && height > 0 && width > 0 && width % 2 == 0 &&
+    return cin > 0 && cout > 0 && height > 0 && width > 0 && width % 4 == 0 &&
            (cout <= 8 || cin <= 8);
 }
 

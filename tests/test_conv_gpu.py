@@ -171,16 +171,18 @@ def test_winograd_residual_epilogue(cuda):
     assert torch.equal(conv3x3_forward(conv, x8, res=r8), conv3x3_forward(conv, x8) + r8)
 
 
-@pytest.mark.parametrize("shape", [(2, 3, 128, 32, 64), (3, 128, 3, 40, 66), (1, 4, 512, 16, 16),
-                                   (2, 512, 8, 16, 16), (2, 256, 4, 8, 10)])
+@pytest.mark.parametrize("shape", [(2, 3, 128, 32, 64), (3, 128, 3, 40, 68), (1, 4, 512, 16, 16),
+                                   (2, 512, 8, 16, 16), (2, 256, 4, 8, 12)])
 def test_thin_conv_forward_and_input_vjp(cuda, shape):
     """The few-channel 3x3 kernel (conv_in / conv_out of the priors): forward with bias and
     input VJP (transposed, flipped weights read in place) against fp64, ragged tiles
-    (H % 8, W % 64 != 0) included; fp32 accumulation, 2e-6 relative L2."""
+    (H % 8, W % 64 != 0) included; fp32 accumulation, 2e-6 relative L2.  Rows are staged as
+    float4 pieces, so W % 4 == 0 is required."""
     n, cin, cout, h, w = shape
     lib = _hip.load_library()
     assert lib.sp_conv3x3_thin_supported(cin, cout, h, w)
     assert lib.sp_conv3x3_thin_supported(cout, cin, h, w)
+    assert not lib.sp_conv3x3_thin_supported(cin, cout, h, w + 2)
     g = torch.Generator().manual_seed(5 + sum(shape))
     x = torch.randn(n, cin, h, w, generator=g)
     wt = torch.randn(cout, cin, 3, 3, generator=g) * (cin * 9) ** -0.5
