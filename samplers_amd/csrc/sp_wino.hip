@@ -25,6 +25,7 @@ namespace sp {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 // V = B^T d B for a 4x4 window d (row-major), B^T = [[1,0,-1,0],[0,1,1,0],[0,-1,1,0],[0,1,0,-1]]
 __device__ __forceinline__ void wino_in(const float (&d)[16], float (&v)[16]) {
@@ -43,6 +44,55 @@ __device__ __forceinline__ void wino_in(const float (&d)[16], float (&v)[16]) {
         v[r * 4 + 2] = t[r * 4 + 2] - t[r * 4 + 1];
         v[r * 4 + 3] = t[r * 4 + 1] - t[r * 4 + 3];
     }
+}
+
+// The same V on packed fp32 (v_pk_add_f32, two lanes per instruction).  Window row r is
+// held as two register pairs, e = (d[r][0], d[r][3]) and m = (d[r][1], d[r][2]) (one
+// ds_read2 each), so every step below is one packed add with operand swizzles:
+//   t = B^T d on pairs:  t0 = d0 - d2, t1 = d1 + d2, t2 = d2 - d1, t3 = d1 - d3
+//   v = t B per row:     (v0, -v3) = e - (m.y, m.x),  (v1, v2) = m + (m.y, -m.x)
+// 16 instructions for the 4x4 window instead of 32 scalar ones.  Column 3 of V comes out
+// negated (exactly: IEEE subtraction is antisymmetric); the packed U carries the
+// compensating sign (k_wino3x3_pack), so U * V and the result are unchanged bit for bit.
+// (The compiler does not form the swizzled packed adds from vector code, so they are
+// written out.)
+struct WinRow { f32x2 e, m; };
+
+__device__ __forceinline__ f32x2 pk_add(f32x2 a, f32x2 b) {  // a + b
+    f32x2 r;
+    asm("v_pk_add_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+__device__ __forceinline__ f32x2 pk_sub(f32x2 a, f32x2 b) {  // a - b
+    f32x2 r;
+    asm("v_pk_add_f32 %0, %1, %2 neg_lo:[0,1] neg_hi:[0,1]" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+__device__ __forceinline__ f32x2 pk_sub_swap(f32x2 a, f32x2 b) {  // (a.x - b.y, a.y - b.x)
+    f32x2 r;
+    asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0] neg_lo:[0,1] neg_hi:[0,1]"
+        : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+__device__ __forceinline__ f32x2 pk_sum_diff(f32x2 m) {  // (m.x + m.y, m.y - m.x)
+    f32x2 r;
+    asm("v_pk_add_f32 %0, %1, %1 op_sel:[0,1] op_sel_hi:[1,0] neg_hi:[0,1]" : "=v"(r) : "v"(m));
+    return r;
+}
+
+__device__ __forceinline__ WinRow wpk_t(int k, const WinRow (&d)[4]) {  // row k of B^T d
+    switch (k) {
+        case 0: return WinRow{pk_sub(d[0].e, d[2].e), pk_sub(d[0].m, d[2].m)};
+        case 1: return WinRow{pk_add(d[1].e, d[2].e), pk_add(d[1].m, d[2].m)};
+        case 2: return WinRow{pk_sub(d[2].e, d[1].e), pk_sub(d[2].m, d[1].m)};
+        default: return WinRow{pk_sub(d[1].e, d[3].e), pk_sub(d[1].m, d[3].m)};
+    }
+}
+
+__device__ __forceinline__ void wpk_v(const WinRow& t, float* v) {  // row of t B (v3 negated)
+    const f32x2 a = pk_sub_swap(t.e, t.m);  // (t0 - t2, t3 - t1)
+    const f32x2 b = pk_sum_diff(t.m);       // (t1 + t2, t2 - t1)
+    v[0] = a.x, v[3] = a.y, v[1] = b.x, v[2] = b.y;
 }
 
 // U = G g G^T (4x4, row-major) for a 3x3 filter g, G = [[1,0,0],[.5,.5,.5],[.5,-.5,.5],[0,0,1]]
@@ -212,15 +262,12 @@ __device__ __forceinline__ void wr_stage_x(float* xw, const WxLane& xl, const Wr
     xw[xl.wh] = x.h;
 }
 
-// This lane's 4x4 window: columns 2tc-1 .. 2tc+2 of the wave's rows 2tr .. 2tr+3.
+// Row r of this lane's 4x4 window (columns 2tc-1 .. 2tc+2 of the wave's rows 2tr .. 2tr+3)
+// as the pairs of the packed transform.
 template <class GE>
-__device__ __forceinline__ void wr_window(const float* xw, const WxLane& xl, float (&d)[16]) {
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-        const float* row = xw + xl.rd + GE::row(r);
-#pragma unroll
-        for (int c = 0; c < 4; ++c) d[r * 4 + c] = row[c];
-    }
+__device__ __forceinline__ WinRow wr_window_row(const float* xw, const WxLane& xl, int r) {
+    const float* row = xw + xl.rd + GE::row(r);
+    return WinRow{f32x2{row[0], row[3]}, f32x2{row[1], row[2]}};
 }
 
 struct WrRing {          // k-steps in flight
@@ -237,7 +284,7 @@ struct WrRing {          // k-steps in flight
 //   gap 1, 2  U loads for step q + 2
 //   gap 3, 4  stage the block of step q + 1 in LDS
 //   gap 5, 6  read this lane's window of it
-//   gap 8-15  V = B^T d B of step q + 1, four operations per gap
+//   gap 8-15  V = B^T d B of step q + 1, two packed operations per gap
 // (Four bursts after every fourth MFMA ran 12-14 % slower: the MFMA pipe idled while the
 // burst issued.)  Loads run 3 steps ahead for the input block, 2 for U; near the end of
 // a tile they fetch the next tile's first steps (XN / UN), so its operands arrive during
@@ -249,7 +296,7 @@ __device__ __forceinline__ void wr_step(const WrGeom& g, const WrSrc& cur, const
     const WrU& u = r.us[K];
     const float(&vc)[16] = r.v[K & 1];
     float(&vn)[16] = r.v[(K + 1) & 1];
-    float d[16], t[16];
+    WinRow d[4], t[4];
     const WrX& xb = r.xs[(K + 1) % 4];  // block of step q + 1
 #define WR_MFMA(xi)                                                                          \
     acc[xi] = __builtin_amdgcn_mfma_f32_32x32x2f32(u.u[(xi) >> 2][(xi) & 3], vc[xi],         \
@@ -287,46 +334,34 @@ __device__ __forceinline__ void wr_step(const WrGeom& g, const WrSrc& cur, const
     xw[xl.wh] = xb.h;
     WR_WALL;
     WR_MFMA(5);
-#pragma unroll
-    for (int rr = 0; rr < 2; ++rr)
-#pragma unroll
-        for (int c = 0; c < 4; ++c) d[rr * 4 + c] = xw[xl.rd + GE::row(rr) + c];
+    d[0] = wr_window_row<GE>(xw, xl, 0);
+    d[1] = wr_window_row<GE>(xw, xl, 1);
     WR_WALL;
     WR_MFMA(6);
-#pragma unroll
-    for (int rr = 2; rr < 4; ++rr)
-#pragma unroll
-        for (int c = 0; c < 4; ++c) d[rr * 4 + c] = xw[xl.rd + GE::row(rr) + c];
+    d[2] = wr_window_row<GE>(xw, xl, 2);
+    d[3] = wr_window_row<GE>(xw, xl, 3);
     WR_WALL;
     WR_MFMA(7);
     WR_MFMA(8);
-    // t = B^T d, B^T = [[1,0,-1,0],[0,1,1,0],[0,-1,1,0],[0,1,0,-1]], one column per gap
+    // t = B^T d, one row (two packed adds) per gap
 #pragma unroll
-    for (int c = 0; c < 4; ++c) {
-        t[0 * 4 + c] = d[0 * 4 + c] - d[2 * 4 + c];
-        t[1 * 4 + c] = d[1 * 4 + c] + d[2 * 4 + c];
-        t[2 * 4 + c] = d[2 * 4 + c] - d[1 * 4 + c];
-        t[3 * 4 + c] = d[1 * 4 + c] - d[3 * 4 + c];
+    for (int k = 0; k < 4; ++k) {
+        t[k] = wpk_t(k, d);
         WR_WALL;
-        WR_MFMA(9 + c);
+        WR_MFMA(9 + k);
     }
     // v = t B, one row per gap
 #pragma unroll
     for (int rr = 0; rr < 3; ++rr) {
-        vn[rr * 4 + 0] = t[rr * 4 + 0] - t[rr * 4 + 2];
-        vn[rr * 4 + 1] = t[rr * 4 + 1] + t[rr * 4 + 2];
-        vn[rr * 4 + 2] = t[rr * 4 + 2] - t[rr * 4 + 1];
-        vn[rr * 4 + 3] = t[rr * 4 + 1] - t[rr * 4 + 3];
+        wpk_v(t[rr], vn + 4 * rr);
         WR_WALL;
         WR_MFMA(13 + rr);
     }
-    vn[12] = t[12] - t[14];
-    vn[13] = t[13] + t[14];
-    vn[14] = t[14] - t[13];
-    vn[15] = t[13] - t[15];
+    wpk_v(t[3], vn + 12);
 #if SP_WINO_EXP == 3
 #pragma unroll
-    for (int i = 0; i < 16; ++i) vn[i] = d[i];  // diagnostics: no input transform
+    for (int i = 0; i < 4; ++i)  // diagnostics: no input transform
+        vn[4 * i] = d[i].e.x, vn[4 * i + 1] = d[i].m.x, vn[4 * i + 2] = d[i].m.y, vn[4 * i + 3] = d[i].e.y;
 #endif
     WR_WALL;
 #undef WR_MFMA
@@ -336,7 +371,6 @@ __device__ __forceinline__ void wr_step(const WrGeom& g, const WrSrc& cur, const
 // Y = A^T M A, A^T = [[1,1,1,0],[0,1,-1,-1]], per (channel, tile) in registers: register r
 // of every accumulator is channel co0 + (r&3) + 8(r>>2) + 4hh, tile l.  Buffer stores:
 // one per-lane offset, the register row's channel offset as a scalar.
-typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
 
 template <class GE>
@@ -467,10 +501,12 @@ __global__ __launch_bounds__(kBlock, 1) void k_wino3x3_r(WrGeom g) {
     wr_load_u(cur.ub + g.u_step, r.us[1]);
     __builtin_amdgcn_sched_barrier(0);
     {
-        float d[16];
         wr_stage_x(xw, xl, r.xs[0]);
-        wr_window<GE>(xw, xl, d);
-        wino_in(d, r.v[0]);
+        WinRow d[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) d[k] = wr_window_row<GE>(xw, xl, k);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) wpk_v(wpk_t(k, d), r.v[0] + 4 * k);
     }
     f32x16 acc[16];
     const int last = g.nsteps - 4;  // >= 4 (cin >= 16)
@@ -519,6 +555,8 @@ __global__ void k_wino3x3_pack(const float* __restrict__ w, int cout, int cin, i
     const int orow = flip ? ci : co, kin = flip ? co : ci, cout_p = flip ? cin : cout;
     float u[16];
     wino_filter(g, u);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) u[q * 4 + 3] = -u[q * 4 + 3];  // the packed transform's V column 3 is negated
     float* dst = up + (((int64_t)(kin >> 1) * (cout_p >> 5) + (orow >> 5)) * 64 +
                        32 * (kin & 1) + (orow & 31)) * 16;
 #pragma unroll
