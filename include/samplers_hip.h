@@ -315,6 +315,25 @@ int sp_conv3x3_thin_bwd_input(const float* dy, const float* w, int64_t n, int32_
                               int32_t cout, int32_t height, int32_t width, float* dx,
                               sp_stream_t stream);
 
+/* 3x3 / stride 2 convolution with one zero row / column on the bottom / right (diffusers'
+ * Downsample2D, downsample_padding=0: the UNet's and the VAE encoder's downsampling layers;
+ * reached from ddpm.py:40-43 and stable_diffusion.py:338-345), on fp32 MFMA, NCHW.
+ * height / width are the INPUT's (even); the output is height/2 x width/2.  Forward: cin % 4,
+ * cout % 128, (height/2) % 8, (width/2) % 32; input VJP (input_vjp=1): cout % 4, cin % 128,
+ * (height/2) % 2, (width/2) % 32 — each output phase (row & 1, column & 1) of dx is its own
+ * sum over the taps that reach it.  Weights packed once per layer by sp_conv3x3_s2_pack
+ * (cin * cout * 9 floats; layouts differ for the two directions).  FLOPs recorded for
+ * kinds 3-4 (18*N*Cin*Cout*(H/2)*(W/2)). */
+int sp_conv3x3_s2_supported(int32_t cin, int32_t cout, int32_t height, int32_t width,
+                            int32_t input_vjp);
+int sp_conv3x3_s2_pack(const float* w, int32_t cout, int32_t cin, int32_t input_vjp, float* wp,
+                       sp_stream_t stream);
+int sp_conv3x3_s2_fwd(const float* x, const float* wp, const float* bias, int64_t n, int32_t cin,
+                      int32_t cout, int32_t height, int32_t width, float* y, sp_stream_t stream);
+int sp_conv3x3_s2_bwd_input(const float* dy, const float* wp_vjp, int64_t n, int32_t cin,
+                            int32_t cout, int32_t height, int32_t width, float* dx,
+                            sp_stream_t stream);
+
 /* The same layers by Winograd F(2x2,3x3) on fp32 MFMA (2.25x fewer multiplies; the
  * transforms add F(2,3) rounding, as MIOpen's Winograd solver does).  up = U = G g G^T
  * packed by sp_wino3x3_pack (input_vjp=1: of the transposed, flipped weights). */

@@ -119,6 +119,12 @@ SIGNATURES = {
                                            ctypes.c_int32, ctypes.c_int32, _P, _P]),
     "sp_conv3x3_thin_bwd_input": (ctypes.c_int, [_P, _P, _I64, ctypes.c_int32, ctypes.c_int32,
                                                  ctypes.c_int32, ctypes.c_int32, _P, _P]),
+    "sp_conv3x3_s2_supported": (ctypes.c_int, [ctypes.c_int32] * 5),
+    "sp_conv3x3_s2_pack": (ctypes.c_int, [_P, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, _P, _P]),
+    "sp_conv3x3_s2_fwd": (ctypes.c_int, [_P, _P, _P, _I64, ctypes.c_int32, ctypes.c_int32,
+                                         ctypes.c_int32, ctypes.c_int32, _P, _P]),
+    "sp_conv3x3_s2_bwd_input": (ctypes.c_int, [_P, _P, _I64, ctypes.c_int32, ctypes.c_int32,
+                                               ctypes.c_int32, ctypes.c_int32, _P, _P]),
     "sp_wino3x3_supported": (ctypes.c_int, [ctypes.c_int32] * 4),
     "sp_wino3x3_packed_size": (_I64, [ctypes.c_int32, ctypes.c_int32]),
     "sp_wino3x3_pack": (ctypes.c_int, [_P, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, _P, _P]),

@@ -290,3 +290,83 @@ class Conv3x3(nn.Conv2d):
             if _conv_algo(lib, cin, self.out_channels, h, w, conv_backend()) is not None:
                 return _Conv3x3Fn.apply(x, self.weight, self.bias, self)
         return super().forward(x)
+
+
+# ---------------------------------------------------------------------------------------
+# 3x3 / stride 2 convolution of Downsample2D (zero row / column bottom / right) on fp32 MFMA
+# ---------------------------------------------------------------------------------------
+
+def _s2_packed(module: nn.Conv2d, input_vjp: bool) -> Tensor:
+    w = module.weight
+    key = (w.data_ptr(), w._version, w.device)
+    cache = module.__dict__.setdefault("_s2_packs", {})
+    if cache.get("key") != key:
+        cache.clear()
+        cache["key"] = key
+    if input_vjp not in cache:
+        lib = _hip.load_library()
+        cout, cin = w.shape[0], w.shape[1]
+        wc = w.detach().contiguous()
+        out = torch.empty(cin * cout * 9, device=w.device)
+        _hip.check(lib.sp_conv3x3_s2_pack(_hip.ptr(wc), cout, cin, int(input_vjp), _hip.ptr(out),
+                                          _hip.stream_of(wc)), "sp_conv3x3_s2_pack")
+        cache[input_vjp] = out
+    return cache[input_vjp]
+
+
+def downsample_s2_supported(module: nn.Conv2d, x: Tensor) -> bool:
+    """The stride-2 tile serves this call (forward and input VJP shape rules)."""
+    if not (x.is_cuda and x.dtype == torch.float32 and x.dim() == 4) or conv_backend() == "miopen":
+        return False
+    lib = _hip.load_library()
+    _, cin, h, w = x.shape
+    cout = module.out_channels
+    return bool(lib.sp_conv3x3_s2_supported(cin, cout, h, w, 0) and
+                lib.sp_conv3x3_s2_supported(cin, cout, h, w, 1))
+
+
+class _ConvS2Fn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias, module):
+        lib = _hip.load_library()
+        x = x.contiguous()
+        n, cin, h, w = x.shape
+        cout = module.out_channels
+        y = torch.empty(n, cout, h // 2, w // 2, device=x.device, dtype=torch.float32)
+        _hip.check(lib.sp_conv3x3_s2_fwd(_hip.ptr(x), _hip.ptr(_s2_packed(module, False)),
+                                         _hip.ptr(bias.contiguous()) if bias is not None else None,
+                                         n, cin, cout, h, w, _hip.ptr(y), _hip.stream_of(x)),
+                   "sp_conv3x3_s2_fwd")
+        ctx.module = module
+        ctx.has_bias = bias is not None
+        ctx.save_for_backward(x if weight.requires_grad else None, weight)
+        ctx.x_shape = x.shape
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, weight = ctx.saved_tensors
+        dx = dw = db = None
+        dy = dy.contiguous()
+        if ctx.needs_input_grad[0]:
+            lib = _hip.load_library()
+            n, cin, h, w = ctx.x_shape
+            dx = torch.empty(tuple(ctx.x_shape), device=dy.device, dtype=torch.float32)
+            _hip.check(lib.sp_conv3x3_s2_bwd_input(_hip.ptr(dy), _hip.ptr(_s2_packed(ctx.module, True)),
+                                                   n, cin, ctx.module.out_channels, h, w,
+                                                   _hip.ptr(dx), _hip.stream_of(dy)),
+                       "sp_conv3x3_s2_bwd_input")
+        if ctx.needs_input_grad[1]:
+            dw = torch.nn.grad.conv2d_weight(F.pad(x, (0, 1, 0, 1)), weight.shape, dy, stride=2)
+        if ctx.has_bias and ctx.needs_input_grad[2]:
+            db = dy.sum(dim=(0, 2, 3))
+        return dx, dw, db, None
+
+
+def downsample_conv(module: nn.Conv2d, x: Tensor) -> Tensor:
+    """``module(F.pad(x, (0, 1, 0, 1)))`` for a 3x3 / stride-2 / padding-0 ``nn.Conv2d``
+    (diffusers' Downsample2D with downsample_padding=0): the stride-2 MFMA tile
+    (``csrc/sp_conv_s2.hip``) where its shape rules hold, else MIOpen on the padded input."""
+    if downsample_s2_supported(module, x):
+        return _ConvS2Fn.apply(x, module.weight, module.bias, module)
+    return module(F.pad(x, (0, 1, 0, 1)))

@@ -26,7 +26,8 @@ import torch
 import torch.nn.functional as F
 from torch import Tensor, nn
 
-from .layers import Conv3x3, GroupNormAct, conv3x3_forward, conv3x3_input_vjp, gn_backward, gn_forward
+from .layers import (Conv3x3, GroupNormAct, conv3x3_forward, conv3x3_input_vjp, downsample_conv,
+                     gn_backward, gn_forward)
 
 
 @dataclass(frozen=True)
@@ -241,7 +242,7 @@ class Downsample2D(nn.Module):
         self.conv = nn.Conv2d(channels, channels, 3, stride=2, padding=0)
 
     def forward(self, x: Tensor) -> Tensor:
-        return self.conv(F.pad(x, (0, 1, 0, 1)))
+        return downsample_conv(self.conv, x)
 
 
 class Upsample2D(nn.Module):

@@ -203,3 +203,75 @@ def test_thin_conv_forward_and_input_vjp(cuda, shape):
     assert rel < 2e-6, rel
     rel = ((dx.double().cpu() - gref).norm() / gref.norm()).item()
     assert rel < 2e-6, rel
+
+
+S2_SHAPES = [  # n, cin, cout, h, w (input size; output h/2 x w/2)
+    (2, 128, 128, 32, 64),    # UNet level shape, both directions on the tile
+    (1, 256, 256, 128, 64),   # VAE encoder-like, several tiles per image
+    (2, 132, 256, 16, 128),   # cin % 128 != 0: forward on the tile, VJP on MIOpen
+    (1, 512, 512, 16, 16),    # 8x8 output: MIOpen both ways (fallback)
+]
+
+
+@pytest.mark.parametrize("shape", S2_SHAPES)
+def test_downsample_stride2_forward_and_input_vjp(cuda, shape):
+    """Downsample2D's 3x3 / stride-2 conv (zero row / column bottom / right) on the
+    csrc/sp_conv_s2.hip tiles (exact fp32 fmaf chains: the direct tile's tolerance) against
+    fp64 torch on the padded input; the output-phase sums of the input VJP cover every tap
+    exactly once (no tap is dropped or doubled at the image edges)."""
+    from samplers_amd.networks.layers import downsample_conv, downsample_s2_supported
+
+    n, cin, cout, h, w = shape
+    g = torch.Generator().manual_seed(sum(shape) + 7)
+    x = torch.randn(n, cin, h, w, generator=g)
+    conv = torch.nn.Conv2d(cin, cout, 3, stride=2, padding=0)
+    with torch.no_grad():
+        conv.weight.normal_(0, (cin * 9) ** -0.5, generator=g)
+        conv.bias.normal_(0, 0.1, generator=g)
+    dy = torch.randn(n, cout, h // 2, w // 2, generator=g)
+    xd = x.double().requires_grad_()
+    ref = F.conv2d(F.pad(xd, (0, 1, 0, 1)), conv.weight.double(), conv.bias.double(), stride=2)
+    (gref,) = torch.autograd.grad(ref, xd, dy.double())
+
+    lib = _hip.load_library()
+    fwd_tile = bool(lib.sp_conv3x3_s2_supported(cin, cout, h, w, 0))
+    vjp_tile = bool(lib.sp_conv3x3_s2_supported(cin, cout, h, w, 1))
+    assert (fwd_tile, vjp_tile) == {0: (True, True), 1: (True, True), 2: (True, False),
+                                    3: (False, False)}[S2_SHAPES.index(shape)]
+    cg = conv.to(cuda)
+    xg = x.to(cuda).requires_grad_()
+    assert downsample_s2_supported(cg, xg) == (fwd_tile and vjp_tile)
+    out = downsample_conv(cg, xg)
+    (gx,) = torch.autograd.grad(out, xg, dy.to(cuda))
+    _check(out.detach(), ref.detach())
+    _check(gx, gref)
+    # the raw entry points on the shapes each direction serves
+    if fwd_tile:
+        wp = torch.empty(cin * cout * 9, device=cuda)
+        _hip.check(lib.sp_conv3x3_s2_pack(_hip.ptr(cg.weight.detach().contiguous()), cout, cin, 0,
+                                          _hip.ptr(wp), None), "pack")
+        y = torch.empty(n, cout, h // 2, w // 2, device=cuda)
+        xc = x.to(cuda)
+        _hip.check(lib.sp_conv3x3_s2_fwd(_hip.ptr(xc), _hip.ptr(wp), None, n, cin, cout, h, w,
+                                         _hip.ptr(y), None), "fwd")
+        torch.cuda.synchronize()
+        _check(y, ref.detach() - cg.bias.detach().double().cpu().view(1, -1, 1, 1))
+    if vjp_tile:
+        wv = torch.empty(cin * cout * 9, device=cuda)
+        _hip.check(lib.sp_conv3x3_s2_pack(_hip.ptr(cg.weight.detach().contiguous()), cout, cin, 1,
+                                          _hip.ptr(wv), None), "pack vjp")
+        dx = torch.full((n, cin, h, w), float("nan"), device=cuda)
+        dyc = dy.to(cuda)
+        _hip.check(lib.sp_conv3x3_s2_bwd_input(_hip.ptr(dyc), _hip.ptr(wv), n, cin, cout, h, w,
+                                               _hip.ptr(dx), None), "bwd")
+        torch.cuda.synchronize()
+        assert torch.isfinite(dx).all()  # every dx element written
+        _check(dx, gref)
+
+
+def test_downsample_stride2_rejects_bad_shapes():
+    lib = _hip.load_library()
+    assert not lib.sp_conv3x3_s2_supported(128, 128, 33, 64, 0)   # odd height
+    assert not lib.sp_conv3x3_s2_supported(128, 100, 32, 64, 0)   # cout % 128
+    assert not lib.sp_conv3x3_s2_supported(100, 128, 32, 64, 1)   # cin % 128 (VJP)
+    assert lib.sp_conv3x3_s2_fwd(None, None, None, 1, 128, 100, 32, 64, None, None) != 0
