@@ -326,6 +326,14 @@ int sp_conv3x3_thin_bwd_input(const float* dy, const float* w, int64_t n, int32_
  * kinds 3-4 (18*N*Cin*Cout*(H/2)*(W/2)). */
 int sp_conv3x3_s2_supported(int32_t cin, int32_t cout, int32_t height, int32_t width,
                             int32_t input_vjp);
+/* 2x nearest-neighbour upsampling (Upsample2D of the UNet and the VAE decoder, before its
+ * 3x3 conv) over `planes` = N*C planes of height x width (width % 4, 16-B aligned buffers),
+ * and its VJP, the 2x2 block sum of dy (2*height x 2*width) into dx (height x width). */
+int sp_upsample2x_supported(int32_t height, int32_t width);
+int sp_upsample2x(const float* x, int64_t planes, int32_t height, int32_t width, float* y,
+                  sp_stream_t stream);
+int sp_upsample2x_vjp(const float* dy, int64_t planes, int32_t height, int32_t width, float* dx,
+                      sp_stream_t stream);
 int sp_conv3x3_s2_pack(const float* w, int32_t cout, int32_t cin, int32_t input_vjp, float* wp,
                        sp_stream_t stream);
 int sp_conv3x3_s2_fwd(const float* x, const float* wp, const float* bias, int64_t n, int32_t cin,

@@ -293,6 +293,42 @@ class Conv3x3(nn.Conv2d):
 
 
 # ---------------------------------------------------------------------------------------
+# 2x nearest upsampling of Upsample2D
+# ---------------------------------------------------------------------------------------
+
+def _upsample2x_call(fn_name: str, src: Tensor, out_shape) -> Tensor:
+    lib = _hip.load_library()
+    n, c, h, w = (src.shape if fn_name == "sp_upsample2x" else out_shape)
+    src = src.contiguous()
+    out = torch.empty(tuple(out_shape), device=src.device, dtype=torch.float32)
+    _hip.check(getattr(lib, fn_name)(_hip.ptr(src), n * c, h, w, _hip.ptr(out),
+                                     _hip.stream_of(src)), fn_name)
+    return out
+
+
+class _Upsample2xFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        n, c, h, w = x.shape
+        ctx.x_shape = x.shape
+        return _upsample2x_call("sp_upsample2x", x, (n, c, 2 * h, 2 * w))
+
+    @staticmethod
+    def backward(ctx, dy):
+        return _upsample2x_call("sp_upsample2x_vjp", dy, ctx.x_shape)
+
+
+def upsample_nearest2x(x: Tensor) -> Tensor:
+    """``F.interpolate(x, scale_factor=2.0, mode="nearest")``: the streaming kernels of
+    ``csrc/sp_upsample.hip`` (forward and the 2x2-block-sum VJP) on fp32 CUDA tensors whose
+    width is a multiple of 4, torch elsewhere."""
+    if (x.is_cuda and x.dtype == torch.float32 and x.dim() == 4 and x.numel() > 0 and
+            _hip.load_library().sp_upsample2x_supported(x.shape[2], x.shape[3])):
+        return _Upsample2xFn.apply(x)
+    return F.interpolate(x, scale_factor=2.0, mode="nearest")
+
+
+# ---------------------------------------------------------------------------------------
 # 3x3 / stride 2 convolution of Downsample2D (zero row / column bottom / right) on fp32 MFMA
 # ---------------------------------------------------------------------------------------
 

@@ -27,7 +27,7 @@ import torch.nn.functional as F
 from torch import Tensor, nn
 
 from .layers import (Conv3x3, GroupNormAct, conv3x3_forward, conv3x3_input_vjp, downsample_conv,
-                     gn_backward, gn_forward)
+                     gn_backward, gn_forward, upsample_nearest2x)
 
 
 @dataclass(frozen=True)
@@ -251,7 +251,7 @@ class Upsample2D(nn.Module):
         self.conv = Conv3x3(channels, channels)
 
     def forward(self, x: Tensor) -> Tensor:
-        return self.conv(F.interpolate(x, scale_factor=2.0, mode="nearest"))
+        return self.conv(upsample_nearest2x(x))
 
 
 class _Level(nn.Module):

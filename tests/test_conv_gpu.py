@@ -275,3 +275,24 @@ def test_downsample_stride2_rejects_bad_shapes():
     assert not lib.sp_conv3x3_s2_supported(128, 100, 32, 64, 0)   # cout % 128
     assert not lib.sp_conv3x3_s2_supported(100, 128, 32, 64, 1)   # cin % 128 (VJP)
     assert lib.sp_conv3x3_s2_fwd(None, None, None, 1, 128, 100, 32, 64, None, None) != 0
+
+
+@pytest.mark.parametrize("shape", [(2, 128, 8, 8), (1, 64, 32, 64), (3, 5, 16, 12), (2, 4, 6, 6)])
+def test_upsample_nearest2x_and_vjp(cuda, shape):
+    """csrc/sp_upsample.hip: forward is a copy (bit-exact vs F.interpolate); the VJP sums each
+    2x2 block of dy in torch's loop order (bit-exact vs torch's backward on the same device).
+    Width 6 is not a multiple of 4: the torch fallback serves it."""
+    from samplers_amd.networks.layers import upsample_nearest2x
+
+    g = torch.Generator().manual_seed(sum(shape))
+    x = torch.randn(*shape, generator=g).to(cuda).requires_grad_()
+    dy = torch.randn(shape[0], shape[1], 2 * shape[2], 2 * shape[3], generator=g).to(cuda)
+    out = upsample_nearest2x(x)
+    (gx,) = torch.autograd.grad(out, x, dy)
+    ref = F.interpolate(x, scale_factor=2.0, mode="nearest")
+    (gref,) = torch.autograd.grad(ref, x, dy)
+    assert torch.equal(out, ref)
+    torch.testing.assert_close(gx, gref, rtol=1e-6, atol=1e-6)
+    # fp64 block sums on the CPU
+    want = dy.double().cpu().reshape(shape[0], shape[1], shape[2], 2, shape[3], 2).sum((3, 5))
+    assert ((gx.double().cpu() - want).abs().max() <= 4e-7 * want.abs().max().clamp_min(1)).item()
