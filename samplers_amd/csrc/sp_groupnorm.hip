@@ -417,14 +417,16 @@ __device__ __forceinline__ void gnt_reduce_publish(float a, float b, float* red,
                                       (red[4] + red[5]) + (red[6] + red[7]));
 }
 
-// A group's elements in one tensor part (the team kernels require that no group straddles
+// A chunk's elements in one tensor part (the team kernels require that no chunk straddles
 // the two parts of a concatenated input): buffer resource over the chunk's first `lim`
 // float4 of the group, so accesses past the chunk end read 0 / are dropped.  The range
 // check covers the VGPR offset only (not soffset), so a thread's float4 i is addressed as
 // voffset (lo + tid + i * kBlock) * 16.
 template <typename T>
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t gnt_rsrc(const Parts<T>& p, uint32_t lim) {
-    return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p.split ? p.p1 : p.p2), (short)0,
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t gnt_rsrc(const Parts<T>& p, uint32_t lo, uint32_t lim) {
+    // a group straddling the two parts is served when the split falls on a chunk boundary
+    // (the host checks): the chunk [lo, lim) then lies in one part
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(lo * 4u < p.split ? p.p1 : p.p2), (short)0,
                                              lim * 16, 0x00020000);
 }
 
@@ -452,7 +454,7 @@ __global__ __launch_bounds__(kBlock, 2) void k_gn_fwd_team(const float* __restri
     const uint32_t m = blockIdx.x % G.chunks;
     for (int64_t gi = blockIdx.x / G.chunks; gi < ngroups; gi += nteams) {
         const GroupCtx c = group_ctx_at<4>(x, G, gi, m);
-        const auto rx = gnt_rsrc(c.x, c.hi);
+        const auto rx = gnt_rsrc(c.x, c.lo, c.hi);
         const uint32_t vo = (c.lo + threadIdx.x) * 16;
         float v[GNT_PER][4];
 #pragma unroll
@@ -482,7 +484,7 @@ __global__ __launch_bounds__(kBlock, 2) void k_gn_fwd_team(const float* __restri
         const float rstd = rsqrtf(var + G.eps);
         if (m == 0 && threadIdx.x == 0) mean_out[gi] = mean, rstd_out[gi] = rstd;
         const Parts<float> zp{z + c.zoff, z + c.zoff, G.gs};
-        const auto rz = gnt_rsrc(zp, c.hi);
+        const auto rz = gnt_rsrc(zp, c.lo, c.hi);
 #pragma unroll
         for (int i = 0; i < GNT_PER; ++i) {
             const uint32_t j = c.lo + threadIdx.x + i * kBlock;
@@ -514,9 +516,9 @@ __global__ __launch_bounds__(kBlock, 2) void k_gn_bwd_team(
     for (int64_t gi = blockIdx.x / G.chunks; gi < ngroups; gi += nteams) {
         const GroupCtx c = group_ctx_at<4>(x, G, gi, m);
         const float mean = mean_in[gi], rstd = rstd_in[gi];
-        const auto rx = gnt_rsrc(c.x, c.hi);
+        const auto rx = gnt_rsrc(c.x, c.lo, c.hi);
         const Parts<const float> dzp{dz + c.zoff, dz + c.zoff, G.gs};
-        const auto rg = gnt_rsrc(dzp, c.hi);
+        const auto rg = gnt_rsrc(dzp, c.lo, c.hi);
         const uint32_t vo = (c.lo + threadIdx.x) * 16;
         float v[GNT_PER][4], g[GNT_PER][4];
 #pragma unroll
@@ -548,9 +550,9 @@ __global__ __launch_bounds__(kBlock, 2) void k_gn_bwd_team(
         gnt_sums(gslots, G.chunks, sv, A, B);
         const float inv_n = 1.f / static_cast<float>(G.gs);
         const float mA = A * inv_n, mB = B * inv_n;
-        const auto rd = gnt_rsrc(parts_at<float>(dx, G.x2 ? dx2 : nullptr, G, gi), c.hi);
+        const auto rd = gnt_rsrc(parts_at<float>(dx, G.x2 ? dx2 : nullptr, G, gi), c.lo, c.hi);
         const auto ra = gnt_rsrc(parts_at<const float>(add1, G.x2 ? add2 : nullptr, G, gi),
-                                 add1 ? c.hi : 0);
+                                 c.lo, add1 ? c.hi : 0);
 #pragma unroll
         for (int i = 0; i < GNT_PER; ++i) {
             float o[4];
@@ -661,7 +663,7 @@ int sp_groupnorm_silu_fwd2(const float* x, const float* x2, int32_t c1, const fl
     if (!x || !z || !mean || !rstd || !work) return SP_EINVAL;
     hipStream_t s = static_cast<hipStream_t>(stream);
     const dim3 blk(kBlock);
-    if (V == 4 && g_single_pass && (!x2 || c1 % G.Cg == 0)) {
+    if (V == 4 && g_single_pass && (!x2 || (int64_t)(c1 % G.Cg) * hw % GN_CHUNK_FWD == 0)) {
         const int64_t ngroups = n * groups;
         constexpr int PER = GN_CHUNK_FWD / 4 / kBlock;
         auto kern = act ? k_gn_fwd_team<true, PER> : k_gn_fwd_team<false, PER>;
@@ -716,7 +718,7 @@ int sp_groupnorm_silu_bwd2(const float* dz, const float* x, const float* x2, int
         return SP_EINVAL;
     hipStream_t s = static_cast<hipStream_t>(stream);
     const dim3 blk(kBlock);
-    if (V == 4 && g_single_pass && (!x2 || c1 % G.Cg == 0)) {
+    if (V == 4 && g_single_pass && (!x2 || (int64_t)(c1 % G.Cg) * hw % GN_CHUNK_BWD == 0)) {
         const int64_t ngroups = n * groups;
         constexpr int PER = GN_CHUNK_BWD / 4 / kBlock;
         auto kern = act ? k_gn_bwd_team<true, PER> : k_gn_bwd_team<false, PER>;

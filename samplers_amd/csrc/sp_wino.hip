@@ -135,14 +135,21 @@ constexpr int WR_CO = 64;   // output channels per workgroup (2 waves x 32)
 #define SP_WINO_EXP 0  // diagnostics only: 1 = no loads in the k loop, 2 = no output stores,
                        // 3 = no input transform (wrong results, timing only)
 #endif
+#ifndef SP_WINO_SPLITK
+#define SP_WINO_SPLITK 1  // split K over two workgroups where the 8x8 mosaic leaves CUs idle
+#endif
 constexpr int WR_NS = 4;    // unroll of the k-step ring (cin % (2 WR_NS) == 0)
 // Tile geometry of a wave: 32 tiles (the MFMA's N) as TRW tile rows x TCW tile columns.
 // TCW = 16 (images with W % 32 == 0): 2 x 16 tiles = 4 x 32 outputs; TCW = 8 (W = 16, the
 // UNet's 16x16 level): 4 x 8 tiles = 8 x 16 outputs.  A workgroup stacks two waves' rows
 // (and two 32-channel halves): 64 co x (4 TRW) x (2 TCW) outputs.
-template <int TCW_, bool MOSAIC_ = false>
+template <int TCW_, bool MOSAIC_ = false, bool SPLIT_ = false>
 struct WGeo {
     static constexpr int TCW = TCW_;
+    // SPLIT (8x8 mosaic at small tile counts): K halved over two workgroups, partial outputs
+    // added atomically into the zeroed output (a compile-time variant: the other kernels keep
+    // their register allocation)
+    static constexpr bool SPLIT = SPLIT_;
     // MOSAIC (8x8 images, the UNet's 8x8 level): the W = 16 geometry over two images side by
     // side; in LDS image 1's columns start one position later, so one zero column (never
     // written) is image 0's right and image 1's left padding.
@@ -169,6 +176,7 @@ struct WxLane {                       // per-lane LDS indices (the same for ever
 };
 struct WrTile {                       // one tile: 64 channels x 8 x 32 outputs of one image
     int n, oh0, ow0, co0;             // co0: this wave's first channel
+    int kh;                           // split-K part (input channels kh * cin / ksplit ..)
 };
 struct WrSrc {                        // a tile's load sources
     __amdgpu_buffer_rsrc_t rs;        // the image's input planes
@@ -186,7 +194,8 @@ struct WrGeom {
     int ntiles, cob, tiles_w, per_img;
     int64_t u_step;                   // floats of packed U per k-step
     int so_step;                      // bytes of input per k-step (two channels)
-    int nsteps;
+    int nsteps;                       // k-steps per tile (of one split-K part)
+    int ksplit;                       // 2 for the SPLIT kernels, else 1
 };
 
 // First image of a wave's data and how many of its images exist (MOSAIC: 2 per wave).
@@ -206,13 +215,16 @@ __device__ __forceinline__ WrTile wr_tile(const WrGeom& g, int t, int wv) {
     // XCD-aware order: tiles t and t + 8 run on one XCD (persistent workgroups b and b + 8
     // share one), so consecutive logical tiles (the channel blocks of one tile group, then
     // its neighbours) share an L2
-    const int lb = (g.ntiles & 7) ? t : (t & 7) * (g.ntiles >> 3) + (t >> 3);
+    int lb = (g.ntiles & 7) ? t : (t & 7) * (g.ntiles >> 3) + (t >> 3);
+    int kh = 0;
+    if constexpr (GE::SPLIT) kh = lb & 1, lb >>= 1;
     const int co_blk = lb % g.cob, rest = lb / g.cob;
     if constexpr (GE::MOSAIC)  // four images per workgroup, two per wave
-        return WrTile{4 * rest, 0, 0, co_blk * WR_CO + 32 * (wv & 1)};
+        return WrTile{4 * rest, 0, 0, co_blk * WR_CO + 32 * (wv & 1), kh};
     const int n = rest / g.per_img, r = rest - n * g.per_img;
     const int ty = r / g.tiles_w;
-    return WrTile{n, ty * GE::WG_ROWS, (r - ty * g.tiles_w) * GE::WG_COLS, co_blk * WR_CO + 32 * (wv & 1)};
+    return WrTile{n, ty * GE::WG_ROWS, (r - ty * g.tiles_w) * GE::WG_COLS, co_blk * WR_CO + 32 * (wv & 1),
+                  kh};
 }
 
 template <class GE>
@@ -232,13 +244,16 @@ __device__ __forceinline__ WrSrc wr_src(const WrGeom& g, const WrTile& ti, int w
                    ? (ci * g.plane + gr * g.W + col) * 4 : OOB;
     };
     WrSrc s;
+    // split-K part kh reads input channels kofs .. kofs + 2 nsteps - 1 (and the matching U)
+    const int kofs = GE::SPLIT ? ti.kh * 2 * g.nsteps : 0, nimg = wr_nimg<GE>(g, ti, wv);
     s.rs = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<float*>(g.x + wr_img0<GE>(g, ti, wv) * g.cin * g.plane), (short)0,
-        wr_nimg<GE>(g, ti, wv) * g.cin * g.plane * 4, 0x00020000);
+        const_cast<float*>(g.x + wr_img0<GE>(g, ti, wv) * g.cin * g.plane + (int64_t)kofs * g.plane),
+        (short)0, nimg ? (nimg * g.cin - kofs) * g.plane * 4 : 0, 0x00020000);
     s.oa = goff(rca, ti.ow0 + 4 * ka);
     s.ob = goff(rcb, ti.ow0 + 4 * ka);
     s.oh = GE::MOSAIC ? OOB : goff(rch, side ? ti.ow0 + 2 * GE::TCW : ti.ow0 - 1);
-    s.ub = g.up + ((int64_t)(ti.co0 >> 5) * 64 + lane) * 16;
+    s.ub = g.up + (GE::SPLIT ? (int64_t)ti.kh * g.nsteps * g.u_step : 0) +
+           ((int64_t)(ti.co0 >> 5) * 64 + lane) * 16;
     return s;
 }
 
@@ -394,7 +409,7 @@ __device__ __forceinline__ void wr_load_res(const WrGeom& g, const WrTile& ti, i
                                             WrRes& rv) {
     const auto rrs = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<float*>(g.res) + wr_img0<GE>(g, ti, wv) * g.cout * g.plane, (short)0,
-        wr_nimg<GE>(g, ti, wv) * g.cout * g.plane * 4, 0x00020000);
+        GE::SPLIT && ti.kh ? 0 : wr_nimg<GE>(g, ti, wv) * g.cout * g.plane * 4, 0x00020000);  // part 0 only
     const int vo = wr_out_voff<GE>(g, ti, wv, lane);
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
@@ -417,7 +432,8 @@ __device__ __forceinline__ void wr_epilogue(const WrGeom& g, const WrTile& ti, i
     // (Sixteen vector bias registers here get hoisted and spilled while the next tile's
     // operands are live.)
     const auto brs = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<float*>(g.bias ? g.bias : g.up), (short)0, g.bias ? g.cout * 4 : 0, 0x00020000);
+        const_cast<float*>(g.bias ? g.bias : g.up), (short)0,
+        g.bias && !(GE::SPLIT && ti.kh) ? g.cout * 4 : 0, 0x00020000);  // SPLIT: part 0 only
     const float bl = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(brs, (ti.co0 + l) * 4, 0, 0));
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
@@ -440,8 +456,24 @@ __device__ __forceinline__ void wr_epilogue(const WrGeom& g, const WrTile& ti, i
         f32x2 y0 = {s0[0] + s0[1] + s0[2] + bv, s1[0] + s1[1] + s1[2] + bv};
         f32x2 y1 = {s0[1] - s0[2] - s0[3] + bv, s1[1] - s1[2] - s1[3] + bv};
         if constexpr (RES) y0 += rv.v[r][0], y1 += rv.v[r][1];
-        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, y0), ors, vo, so, 0);
-        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, y1), ors, vo, so + g.W * 4, 0);
+        if constexpr (!GE::SPLIT) {
+            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, y0), ors, vo, so, 0);
+            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, y1), ors, vo, so + g.W * 4, 0);
+        } else {  // this part's share into the zeroed output: two addends, order-independent
+            // global_atomic_add_f32 (device-coherent RMW, no return) on a wave-uniform base +
+            // a 32-bit lane offset: no per-lane 64-bit addresses (register pressure)
+            const int base = __builtin_amdgcn_readfirstlane(
+                static_cast<int>(wr_img0<GE>(g, ti, wv) * g.cout * g.plane));
+            const int lim = __builtin_amdgcn_readfirstlane(wr_nimg<GE>(g, ti, wv) * g.cout * g.plane);
+            const int e = (vo + so) >> 2;
+            if (e < lim) {
+                float* const o = g.out + base;
+                unsafeAtomicAdd(o + e, y0[0]);
+                unsafeAtomicAdd(o + e + 1, y0[1]);
+                unsafeAtomicAdd(o + e + g.W, y1[0]);
+                unsafeAtomicAdd(o + e + g.W + 1, y1[1]);
+            }
+        }
         // one register row at a time: the next tile's operands are live across the
         // epilogue, so its accumulator reads must not all be hoisted
         __builtin_amdgcn_sched_barrier(0);
@@ -452,9 +484,9 @@ __device__ __forceinline__ void wr_epilogue(const WrGeom& g, const WrTile& ti, i
 // ring runs on across tile boundaries, so a tile's prologue latency and its predecessor's
 // store drain overlap MFMA work instead of leaving the CU idle (at one wave per SIMD no
 // other workgroup can fill those gaps).
-template <bool RES, int TCW, bool MOSAIC = false>
+template <bool RES, int TCW, bool MOSAIC = false, bool SPLIT = false>
 __global__ __launch_bounds__(kBlock, 1) void k_wino3x3_r(WrGeom g) {
-    using GE = WGeo<TCW, MOSAIC>;
+    using GE = WGeo<TCW, MOSAIC, SPLIT>;
     __shared__ __attribute__((aligned(16))) float xlds[4 * GE::WAVE];
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     float* const xw = xlds + wv * GE::WAVE;
@@ -622,6 +654,9 @@ static int wino3x3(int kind, const float* x, const float* up, const float* bias,
     if (tiles >= (int64_t(1) << 31) || (int64_t)cin * height * width * 4 >= (int64_t(1) << 31) ||
         (int64_t)cout * height * width * 4 >= (int64_t(1) << 31))
         return SP_EINVAL;
+    // the UNet's 8x8 level is 128 mosaic tiles at B = 64, half the CUs: split K in two there
+    const int ksplit = SP_WINO_SPLITK && mosaic && 2 * tiles <= cu_count() && cin % 16 == 0 && cin >= 32
+                           ? 2 : 1;
     WrGeom g;
     g.x = x;
     g.up = up;
@@ -633,22 +668,28 @@ static int wino3x3(int kind, const float* x, const float* up, const float* bias,
     g.H = height;
     g.W = width;
     g.plane = height * width;
-    g.ntiles = static_cast<int>(tiles);
+    g.ntiles = static_cast<int>(tiles * ksplit);
+    g.ksplit = ksplit;
     g.cob = cout / WR_CO;
     g.tiles_w = mosaic ? 1 : width / wg_cols;
     g.per_img = mosaic ? 1 : g.tiles_w * (height / wg_rows);
     g.batch = n;
     g.u_step = (int64_t)cout * 32;
     g.so_step = 2 * height * width * 4;
-    g.nsteps = cin / 2;
+    g.nsteps = cin / 2 / ksplit;
     // one persistent workgroup per CU (a 512-register wave per SIMD: one workgroup fits)
-    const int grid = static_cast<int>(std::min<int64_t>(tiles, cu_count()));
+    const int grid = static_cast<int>(std::min<int64_t>(tiles * ksplit, cu_count()));
     // executed MFMA work: 16 GEMMs of 2*cin*cout per 2x2 tile = 8*cin*cout per pixel
     // (the direct-conv equivalent is 18*cin*cout per pixel, 2.25x more)
     const double flops = 8.0 * n * cin * cout * height * width;
     const dim3 gd(static_cast<unsigned>(grid)), bd(kBlock);
     hipStream_t st = static_cast<hipStream_t>(stream);
-    if (mosaic) {
+    if (ksplit > 1 && hipMemsetAsync(y, 0, (size_t)n * cout * height * width * sizeof(float), st) != hipSuccess)
+        return check_launch(what);
+    if (ksplit > 1) {
+        if (res) launch_w(kind, flops, k_wino3x3_r<true, 8, true, true>, gd, bd, st, g);
+        else launch_w(kind, flops, k_wino3x3_r<false, 8, true, true>, gd, bd, st, g);
+    } else if (mosaic) {
         if (res) launch_w(kind, flops, k_wino3x3_r<true, 8, true>, gd, bd, st, g);
         else launch_w(kind, flops, k_wino3x3_r<false, 8, true>, gd, bd, st, g);
     } else if (narrow) {

@@ -161,6 +161,7 @@ def test_fused_resnet_blocks_match_cpu(cuda):
     (2, 128, 0, 256, 256, 32),    # 16 chunks per group
     (5, 256, 256, 8, 8, 32),      # many small groups: several groups per team
     (2, 96, 32, 16, 16, 32),      # c1 % (channels per group) == 0 with a 2-part split
+    (1, 256, 128, 128, 128, 32),  # a group straddles the parts at a chunk boundary (UNet 128^2)
 ])
 @pytest.mark.parametrize("act", [True, False])
 def test_single_pass_matches_two_pass_bitwise(cuda, shape, act):
