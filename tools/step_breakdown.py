@@ -9,6 +9,12 @@ import sys
 def kind(n: str) -> str:
     if "k_wino" in n:
         return "HIP Winograd conv tile"
+    if "k_conv3x3_s2" in n:
+        return "HIP stride-2 conv tile (downsampling, fwd + VJP)"
+    if "k_conv3x3_thin" in n:
+        return "HIP thin conv (conv_in / conv_out)"
+    if "k_upsample2x" in n:
+        return "HIP nearest upsampling (fwd + VJP)"
     if "k_conv3x3" in n:
         return "HIP direct conv tile"
     if "k_gn" in n:
@@ -16,7 +22,7 @@ def kind(n: str) -> str:
     if "k_dps" in n or "k_blur" in n:
         return "HIP guidance passes"
     if "miopen" in n or "igemm" in n or "naive_conv" in n or "transpose" in n:
-        return "MIOpen convs (8x8 level, stride-2, conv_in/out) + layout transposes"
+        return "MIOpen convs (16x16 / 8x8 stride-2) + layout transposes"
     if "Cijk" in n:
         return "hipBLASLt GEMMs (1x1 shortcuts, attention, time embedding)"
     if "CUDAFunctor_add" in n:
@@ -24,7 +30,7 @@ def kind(n: str) -> str:
     if "softmax" in n.lower():
         return "softmax"
     if "upsample" in n:
-        return "nearest upsampling"
+        return "torch nearest upsampling"
     return "other torch elementwise / copies"
 
 
