@@ -419,6 +419,12 @@ __device__ __forceinline__ void wr_load_res(const WrGeom& g, const WrTile& ti, i
     }
 }
 
+// SPLIT epilogue: buffer_atomic_add_f32 (device-coherent RMW, no return) on a scalar
+// resource, one 32-bit lane offset, no branch
+__device__ __forceinline__ void wr_atomic_add(float v, __amdgpu_buffer_rsrc_t r, int voff) {
+    asm volatile("buffer_atomic_add_f32 %0, %1, %2, 0 offen" : : "v"(v), "v"(voff), "s"(r) : "memory");
+}
+
 template <class GE, bool RES>
 __device__ __forceinline__ void wr_epilogue(const WrGeom& g, const WrTile& ti, int wv, int lane,
                                             const f32x16 (&acc)[16], const WrRes& rv) {
@@ -434,6 +440,15 @@ __device__ __forceinline__ void wr_epilogue(const WrGeom& g, const WrTile& ti, i
     const auto brs = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<float*>(g.bias ? g.bias : g.up), (short)0,
         g.bias && !(GE::SPLIT && ti.kh) ? g.cout * 4 : 0, 0x00020000);  // SPLIT: part 0 only
+    // SPLIT: the same output range as `ors`, from wave-uniform (scalar) values, for the
+    // inline-asm atomics (out-of-range lanes dropped by the range check, like the stores)
+    __amdgpu_buffer_rsrc_t ars;
+    if constexpr (GE::SPLIT)
+        ars = __builtin_amdgcn_make_buffer_rsrc(
+            g.out + (int64_t)__builtin_amdgcn_readfirstlane(static_cast<int>(wr_img0<GE>(g, ti, wv))) *
+                        g.cout * g.plane,
+            (short)0, __builtin_amdgcn_readfirstlane(wr_nimg<GE>(g, ti, wv)) * g.cout * g.plane * 4,
+            0x00020000);
     const float bl = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(brs, (ti.co0 + l) * 4, 0, 0));
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
@@ -460,19 +475,10 @@ __device__ __forceinline__ void wr_epilogue(const WrGeom& g, const WrTile& ti, i
             __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, y0), ors, vo, so, 0);
             __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, y1), ors, vo, so + g.W * 4, 0);
         } else {  // this part's share into the zeroed output: two addends, order-independent
-            // global_atomic_add_f32 (device-coherent RMW, no return) on a wave-uniform base +
-            // a 32-bit lane offset: no per-lane 64-bit addresses (register pressure)
-            const int base = __builtin_amdgcn_readfirstlane(
-                static_cast<int>(wr_img0<GE>(g, ti, wv) * g.cout * g.plane));
-            const int lim = __builtin_amdgcn_readfirstlane(wr_nimg<GE>(g, ti, wv) * g.cout * g.plane);
-            const int e = (vo + so) >> 2;
-            if (e < lim) {
-                float* const o = g.out + base;
-                unsafeAtomicAdd(o + e, y0[0]);
-                unsafeAtomicAdd(o + e + 1, y0[1]);
-                unsafeAtomicAdd(o + e + g.W, y1[0]);
-                unsafeAtomicAdd(o + e + g.W + 1, y1[1]);
-            }
+            wr_atomic_add(y0[0], ars, vo + so);
+            wr_atomic_add(y0[1], ars, vo + so + 4);
+            wr_atomic_add(y1[0], ars, vo + so + g.W * 4);
+            wr_atomic_add(y1[1], ars, vo + so + g.W * 4 + 4);
         }
         // one register row at a time: the next tile's operands are live across the
         // epilogue, so its accumulator reads must not all be hoisted
