@@ -251,8 +251,8 @@ int sp_groupnorm_silu_bwd2(const float* dz, const float* x1, const float* x2, in
                            const float* chan_bias, const float* gamma, const float* beta,
                            const float* mean, const float* rstd, int64_t n, int32_t channels,
                            int64_t hw, int32_t groups, int32_t act, float* dx1, float* dx2,
-                           const float* add1, const float* add2, float* work,
-                           sp_stream_t stream);
+                           const float* add1, const float* add2, const float* add1b,
+                           float* work, sp_stream_t stream);
 
 /* Single-pass GroupNorm (default on): a team of workgroups per group keeps the group in
  * registers across its reduction (forward reads x once, backward x and dz once).  enable:
@@ -339,8 +339,8 @@ int sp_conv3x3_s2_pack(const float* w, int32_t cout, int32_t cin, int32_t input_
 int sp_conv3x3_s2_fwd(const float* x, const float* wp, const float* bias, int64_t n, int32_t cin,
                       int32_t cout, int32_t height, int32_t width, float* y, sp_stream_t stream);
 int sp_conv3x3_s2_bwd_input(const float* dy, const float* wp_vjp, int64_t n, int32_t cin,
-                            int32_t cout, int32_t height, int32_t width, float* dx,
-                            sp_stream_t stream);
+                            int32_t cout, int32_t height, int32_t width, int32_t accumulate,
+                            float* dx, sp_stream_t stream);
 
 /* The same layers by Winograd F(2x2,3x3) on fp32 MFMA (2.25x fewer multiplies; the
  * transforms add F(2,3) rounding, as MIOpen's Winograd solver does).  up = U = G g G^T

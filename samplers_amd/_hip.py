@@ -127,7 +127,7 @@ SIGNATURES = {
     "sp_conv3x3_s2_fwd": (ctypes.c_int, [_P, _P, _P, _I64, ctypes.c_int32, ctypes.c_int32,
                                          ctypes.c_int32, ctypes.c_int32, _P, _P]),
     "sp_conv3x3_s2_bwd_input": (ctypes.c_int, [_P, _P, _I64, ctypes.c_int32, ctypes.c_int32,
-                                               ctypes.c_int32, ctypes.c_int32, _P, _P]),
+                                               ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, _P, _P]),
     "sp_wino3x3_supported": (ctypes.c_int, [ctypes.c_int32] * 4),
     "sp_wino3x3_packed_size": (_I64, [ctypes.c_int32, ctypes.c_int32]),
     "sp_wino3x3_pack": (ctypes.c_int, [_P, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, _P, _P]),
@@ -151,7 +151,7 @@ SIGNATURES = {
                                               ctypes.c_int32, _P, _P, _P, _P, _P]),
     "sp_groupnorm_silu_bwd2": (ctypes.c_int, [_P, _P, _P, ctypes.c_int32, _P, _P, _P, _P, _P,
                                               _I64, ctypes.c_int32, _I64, ctypes.c_int32,
-                                              ctypes.c_int32, _P, _P, _P, _P, _P, _P]),
+                                              ctypes.c_int32, _P, _P, _P, _P, _P, _P, _P]),
     "sp_groupnorm_single_pass": (ctypes.c_int, [ctypes.c_int32]),
     "sp_groupnorm_team_timeouts": (_I64, []),
     "sp_wino3x3_fwd_res": (ctypes.c_int, [_P, _P, _P, _P, _I64, ctypes.c_int32, ctypes.c_int32,

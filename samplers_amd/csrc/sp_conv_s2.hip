@@ -12,7 +12,8 @@
 // stride-2 B reads of a wave are unit-stride LDS addresses: patch column 2c + s lives at
 // [parity s & 1][c + (s >> 1)].
 //
-// Input VJP, per output phase (p, q) = (row & 1, column & 1) of dx:
+// Input VJP (optionally accumulated into dx: dx += ..., for a UNet skip tensor whose other
+// consumer's gradient is already there), per output phase (p, q) = (row & 1, column & 1) of dx:
 //   dx[2i' + p, 2j' + q] = sum_co sum_{a = p, p + 2 <= 2} sum_{b = q, q + 2 <= 2}
 //                          W[co, ci, a, b] * dy[co, i' - a/2, j' - b/2]
 // i.e. 4, 2, 2 and 1 taps for the phases (0,0), (0,1), (1,0), (1,1) (9 in all: no padded
@@ -226,7 +227,7 @@ __device__ __forceinline__ void s2b_store(float* As, float* Ps, int tid, const S
 __global__ __launch_bounds__(kBlock, 2) void k_conv3x3_s2_bwd(const float* __restrict__ dy,
                                                               const float* __restrict__ wp,
                                                               float* __restrict__ dx, int cin,
-                                                              int cout, int H, int W) {
+                                                              int cout, int H, int W, int acc_in) {
     __shared__ __attribute__((aligned(16))) float As[2][S2B_K * S2B_M];
     __shared__ float Ps[2][S2B_CO * S2B_PATCH];
 
@@ -288,10 +289,13 @@ __global__ __launch_bounds__(kBlock, 2) void k_conv3x3_s2_bwd(const float* __res
         for (int r = 0; r < 16; ++r) {
             const int ci = ci0 + m_w + mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
 #pragma unroll
-            for (int p = 0; p < 2; ++p)
-                *reinterpret_cast<s2_f32x2*>(dn + (int64_t)ci * plane + (int64_t)(2 * ip + p) * W +
-                                             2 * (j0 + l)) =
-                    s2_f32x2{acc[p * 2][mt][r], acc[p * 2 + 1][mt][r]};
+            for (int p = 0; p < 2; ++p) {
+                s2_f32x2* d = reinterpret_cast<s2_f32x2*>(dn + (int64_t)ci * plane +
+                                                          (int64_t)(2 * ip + p) * W + 2 * (j0 + l));
+                s2_f32x2 v{acc[p * 2][mt][r], acc[p * 2 + 1][mt][r]};
+                if (acc_in) v = *d + v;  // accumulate: dx already holds another consumer's gradient
+                *d = v;
+            }
         }
     }
 }
@@ -353,8 +357,8 @@ int sp_conv3x3_s2_fwd(const float* x, const float* wp, const float* bias, int64_
 }
 
 int sp_conv3x3_s2_bwd_input(const float* dy, const float* wp_vjp, int64_t n, int32_t cin,
-                            int32_t cout, int32_t height, int32_t width, float* dx,
-                            sp_stream_t stream) {
+                            int32_t cout, int32_t height, int32_t width, int32_t accumulate,
+                            float* dx, sp_stream_t stream) {
     if (!sp_conv3x3_s2_supported(cin, cout, height, width, 1) || n < 0) return SP_EINVAL;
     if (n == 0) return SP_OK;
     if (!dy || !wp_vjp || !dx) return SP_EINVAL;
@@ -364,7 +368,8 @@ int sp_conv3x3_s2_bwd_input(const float* dy, const float* wp_vjp, int64_t n, int
     const double flops = 18.0 * n * cin * cout * (height / 2) * (width / 2);
     launch_w(TK_CONV3X3_BWD_INPUT, flops, k_conv3x3_s2_bwd,
              dim3(static_cast<unsigned>(tiles), cin / S2B_M), dim3(kBlock),
-             static_cast<hipStream_t>(stream), dy, wp_vjp, dx, cin, cout, height, width);
+             static_cast<hipStream_t>(stream), dy, wp_vjp, dx, cin, cout, height, width,
+             accumulate ? 1 : 0);
     return check_launch("sp_conv3x3_s2_bwd_input");
 }
 

@@ -67,6 +67,9 @@ struct GnGeom {
     // tensor.  The same split applies to the input gradient (dx1, dx2) and its addends.
     const float* x2;
     uint32_t c1hw, s2;   // elements per sample of x1 and of x2
+    // input VJP only: a second addend (one-part inputs), added after add1 — a UNet skip
+    // tensor's gradient from its up-block consumer, instead of an autograd accumulation add
+    const float* add1b;
 };
 
 // Element e of group blockIdx.y of a (possibly two-part) NCHW tensor: p1 + e before the
@@ -350,6 +353,12 @@ __global__ __launch_bounds__(kBlock) void k_gn_bwd_apply(const float* __restrict
 #pragma unroll
                 for (int e = 0; e < V; ++e) o[e] += ad[e];
             }
+            if (G.add1b) {  // + the skip gradient (one-part inputs)
+                float ad[V];
+                load_v<V>(G.add1b + c.zoff + (size_t)j * V, ad);
+#pragma unroll
+                for (int e = 0; e < V; ++e) o[e] += ad[e];
+            }
             store_v<V>(dxg.at(j * V), o);
         }
     }
@@ -556,6 +565,8 @@ __global__ __launch_bounds__(kBlock, 2) void k_gn_bwd_team(
         const auto rd = gnt_rsrc(parts_at<float>(dx, G.x2 ? dx2 : nullptr, G, gi), c.lo, c.hi);
         const auto ra = gnt_rsrc(parts_at<const float>(add1, G.x2 ? add2 : nullptr, G, gi),
                                  c.lo, add1 ? c.hi : 0);
+        const Parts<const float> abp{G.add1b + c.zoff, G.add1b + c.zoff, G.gs};
+        const auto rb = gnt_rsrc(abp, c.lo, G.add1b ? c.hi : 0);
 #pragma unroll
         for (int i = 0; i < GNT_PER; ++i) {
             float o[4];
@@ -564,6 +575,12 @@ __global__ __launch_bounds__(kBlock, 2) void k_gn_bwd_team(
             if (add1) {  // as k_gn_bwd_apply (same rounding)
                 float ad[4];
                 gnt_load(ra, vo, i, ad);
+#pragma unroll
+                for (int e = 0; e < 4; ++e) o[e] += ad[e];
+            }
+            if (G.add1b) {  // + the skip gradient, as k_gn_bwd_apply
+                float ad[4];
+                gnt_load(rb, vo, i, ad);
 #pragma unroll
                 for (int e = 0; e < 4; ++e) o[e] += ad[e];
             }
@@ -589,6 +606,7 @@ static int gn_geom(int64_t n, int32_t c, int64_t hw, int32_t groups, const float
     G->hw_div = make_fastdiv(static_cast<uint32_t>(hw / *V));
     G->eps = eps;
     G->x2 = nullptr;
+    G->add1b = nullptr;
     G->c1hw = static_cast<uint32_t>(c * hw);
     G->s2 = 0;
     *grid = dim3(G->chunks, static_cast<unsigned>(n * groups));
@@ -700,15 +718,15 @@ int sp_groupnorm_silu_bwd(const float* dz, const float* x, const float* chan_bia
                           sp_stream_t stream) {
     return sp_groupnorm_silu_bwd2(dz, x, nullptr, channels, chan_bias, gamma, beta, mean, rstd,
                                   n, channels, hw, groups, act, dx, nullptr, nullptr, nullptr,
-                                  work, stream);
+                                  nullptr, work, stream);
 }
 
 int sp_groupnorm_silu_bwd2(const float* dz, const float* x, const float* x2, int32_t c1,
                            const float* chan_bias, const float* gamma, const float* beta,
                            const float* mean, const float* rstd, int64_t n, int32_t channels,
                            int64_t hw, int32_t groups, int32_t act, float* dx, float* dx2,
-                           const float* add1, const float* add2, float* work,
-                           sp_stream_t stream) {
+                           const float* add1, const float* add2, const float* add1b,
+                           float* work, sp_stream_t stream) {
     GnGeom G;
     int V;
     dim3 grid;
@@ -717,8 +735,10 @@ int sp_groupnorm_silu_bwd2(const float* dz, const float* x, const float* x2, int
     if (rc == SP_OK) rc = gn_split(&G, x2, c1, channels, hw);
     if (rc != SP_OK) return rc;
     if (n == 0) return SP_OK;
-    if (!dz || !x || !mean || !rstd || !dx || !work || (x2 && !dx2) || (x2 && add1 && !add2))
+    if (!dz || !x || !mean || !rstd || !dx || !work || (x2 && !dx2) || (x2 && add1 && !add2) ||
+        (x2 && add1b))
         return SP_EINVAL;
+    G.add1b = add1b;
     hipStream_t s = static_cast<hipStream_t>(stream);
     const dim3 blk(kBlock);
     if (V == 4 && g_single_pass && (!x2 || (int64_t)(c1 % G.Cg) * hw % GN_CHUNK_BWD == 0)) {

@@ -52,9 +52,10 @@ def gn_forward(norm: "GroupNormAct", x1: Tensor, x2: Tensor | None = None,
 def gn_backward(norm: "GroupNormAct", dz: Tensor, x1: Tensor, x2: Tensor | None,
                 chan_bias: Tensor | None, stats: Tensor, add1: Tensor | None = None,
                 add2: Tensor | None = None, out1: Tensor | None = None,
-                out2: Tensor | None = None) -> tuple[Tensor, Tensor | None]:
+                out2: Tensor | None = None, add1b: Tensor | None = None) -> tuple[Tensor, Tensor | None]:
     """Input VJP of ``gn_forward`` into the parts' shapes, plus the optional addends
-    (out1 / out2 may be the addends themselves: accumulate in place)."""
+    (out1 / out2 may be the addends themselves: accumulate in place); ``add1b`` is a second
+    addend of a one-part input, added after ``add1``."""
     lib = _hip.load_library()
     n, c1 = x1.shape[0], x1.shape[1]
     c = dz.shape[1]
@@ -67,7 +68,7 @@ def gn_backward(norm: "GroupNormAct", dz: Tensor, x1: Tensor, x2: Tensor | None,
         _hip.ptr(dz.contiguous()), _hip.ptr(x1), _hip.ptr(x2), c1, _hip.ptr(chan_bias),
         _hip.ptr(norm.weight), _hip.ptr(norm.bias), _hip.ptr(stats[0]), _hip.ptr(stats[1]), n, c,
         hw, norm.num_groups, int(norm.act), _hip.ptr(dx1), _hip.ptr(dx2), _hip.ptr(add1),
-        _hip.ptr(add2), _hip.ptr(work), _hip.stream_of(x1)), "sp_groupnorm_silu_bwd2")
+        _hip.ptr(add2), _hip.ptr(add1b), _hip.ptr(work), _hip.stream_of(x1)), "sp_groupnorm_silu_bwd2")
     return dx1, dx2
 
 
@@ -361,9 +362,29 @@ def downsample_s2_supported(module: nn.Conv2d, x: Tensor) -> bool:
                 lib.sp_conv3x3_s2_supported(cin, cout, h, w, 1))
 
 
+class SkipGrad:
+    """Hand-off of a UNet skip tensor's gradient from its up-block consumer (which runs
+    first in the backward pass) to its down-path consumer, which adds it inside its own
+    input-VJP kernel (GroupNorm's second addend, or the stride-2 conv's accumulate mode)
+    instead of autograd's separate accumulation add.  ``enabled`` is cleared in the forward
+    pass when the down-path consumer cannot take it (the autograd add then happens)."""
+
+    __slots__ = ("grad", "enabled")
+
+    def __init__(self) -> None:
+        self.grad: Tensor | None = None
+        self.enabled = True
+
+    def take(self) -> Tensor:
+        g, self.grad = self.grad, None
+        if g is None:
+            raise RuntimeError("skip gradient missing: the up-block consumer's backward did not run first")
+        return g
+
+
 class _ConvS2Fn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, module):
+    def forward(ctx, x, weight, bias, module, box=None):
         lib = _hip.load_library()
         x = x.contiguous()
         n, cin, h, w = x.shape
@@ -374,6 +395,7 @@ class _ConvS2Fn(torch.autograd.Function):
                                          n, cin, cout, h, w, _hip.ptr(y), _hip.stream_of(x)),
                    "sp_conv3x3_s2_fwd")
         ctx.module = module
+        ctx.box = box
         ctx.has_bias = bias is not None
         ctx.save_for_backward(x if weight.requires_grad else None, weight)
         ctx.x_shape = x.shape
@@ -387,22 +409,28 @@ class _ConvS2Fn(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             lib = _hip.load_library()
             n, cin, h, w = ctx.x_shape
-            dx = torch.empty(tuple(ctx.x_shape), device=dy.device, dtype=torch.float32)
+            acc = ctx.box is not None
+            # with a skip gradient pending, accumulate into its buffer (dx = skip grad + VJP)
+            dx = ctx.box.take() if acc else torch.empty(tuple(ctx.x_shape), device=dy.device,
+                                                        dtype=torch.float32)
             _hip.check(lib.sp_conv3x3_s2_bwd_input(_hip.ptr(dy), _hip.ptr(_s2_packed(ctx.module, True)),
-                                                   n, cin, ctx.module.out_channels, h, w,
+                                                   n, cin, ctx.module.out_channels, h, w, int(acc),
                                                    _hip.ptr(dx), _hip.stream_of(dy)),
                        "sp_conv3x3_s2_bwd_input")
         if ctx.needs_input_grad[1]:
             dw = torch.nn.grad.conv2d_weight(F.pad(x, (0, 1, 0, 1)), weight.shape, dy, stride=2)
         if ctx.has_bias and ctx.needs_input_grad[2]:
             db = dy.sum(dim=(0, 2, 3))
-        return dx, dw, db, None
+        return dx, dw, db, None, None
 
 
-def downsample_conv(module: nn.Conv2d, x: Tensor) -> Tensor:
+def downsample_conv(module: nn.Conv2d, x: Tensor, box: SkipGrad | None = None) -> Tensor:
     """``module(F.pad(x, (0, 1, 0, 1)))`` for a 3x3 / stride-2 / padding-0 ``nn.Conv2d``
     (diffusers' Downsample2D with downsample_padding=0): the stride-2 MFMA tile
     (``csrc/sp_conv_s2.hip``) where its shape rules hold, else MIOpen on the padded input."""
-    if downsample_s2_supported(module, x):
-        return _ConvS2Fn.apply(x, module.weight, module.bias, module)
+    if downsample_s2_supported(module, x) and not module.weight.requires_grad:
+        return _ConvS2Fn.apply(x, module.weight, module.bias, module,
+                               box if box is not None and box.enabled else None)
+    if box is not None:
+        box.enabled = False
     return module(F.pad(x, (0, 1, 0, 1)))

@@ -26,8 +26,8 @@ import torch
 import torch.nn.functional as F
 from torch import Tensor, nn
 
-from .layers import (Conv3x3, GroupNormAct, conv3x3_forward, conv3x3_input_vjp, downsample_conv,
-                     gn_backward, gn_forward, upsample_nearest2x)
+from .layers import (Conv3x3, GroupNormAct, SkipGrad, conv3x3_forward, conv3x3_input_vjp,
+                     downsample_conv, gn_backward, gn_forward, upsample_nearest2x)
 
 
 @dataclass(frozen=True)
@@ -109,7 +109,7 @@ class _ResnetBlockFn(torch.autograd.Function):
     for weight gradients, which the samplers never take: weights are frozen)."""
 
     @staticmethod
-    def forward(ctx, block, tb, x1, x2):
+    def forward(ctx, block, tb, x1, x2, box_in=None, box_out=None):
         z1, st1 = gn_forward(block.norm1, x1, x2)
         h1 = conv3x3_forward(block.conv1, z1)
         del z1
@@ -123,6 +123,7 @@ class _ResnetBlockFn(torch.autograd.Function):
                 bias = block.conv_shortcut.bias if bias is None else bias + block.conv_shortcut.bias
         out = conv3x3_forward(block.conv2, z2, res=short, bias=bias)
         ctx.block = block
+        ctx.box_in, ctx.box_out = box_in, box_out
         ctx.save_for_backward(x1, x2, h1, tb, st1, st2)
         return out
 
@@ -137,14 +138,18 @@ class _ResnetBlockFn(torch.autograd.Function):
         zshape = (x1.shape[0], blk.conv1.in_channels) + tuple(x1.shape[2:])
         dz1 = conv3x3_input_vjp(blk.conv1, dh1, zshape)
         del dh1
-        if blk.conv_shortcut is None:  # identity shortcut: dx1 = GN1^T dz1 + dout
-            dx1, dx2 = gn_backward(blk.norm1, dz1, x1, x2, None, st1, add1=dout)
+        # x1 is a skip tensor whose up-block consumer left its gradient: added in the kernel
+        extra = ctx.box_in.take() if ctx.box_in is not None else None
+        if blk.conv_shortcut is None:  # identity shortcut: dx1 = GN1^T dz1 + dout (+ skip grad)
+            dx1, dx2 = gn_backward(blk.norm1, dz1, x1, x2, None, st1, add1=dout, add1b=extra)
         else:  # dx = shortcut^T dout, then += GN1^T dz1 in place
             s1, s2 = _shortcut_input_vjp(blk.conv_shortcut, dout, x1.shape[1],
                                          0 if x2 is None else x2.shape[1])
             dx1, dx2 = gn_backward(blk.norm1, dz1, x1, x2, None, st1, add1=s1, add2=s2,
-                                   out1=s1, out2=s2)
-        return None, None, dx1, dx2
+                                   out1=s1, out2=s2, add1b=extra)
+        if ctx.box_out is not None:  # x2 (a skip): its down-path consumer adds this gradient
+            ctx.box_out.grad, dx2 = dx2, None
+        return None, None, dx1, dx2, None, None
 
 
 class ResnetBlock2D(nn.Module):
@@ -169,12 +174,23 @@ class ResnetBlock2D(nn.Module):
                 and not any(p.requires_grad for p in self.parameters())
                 and x[0, 0].numel() % 4 == 0)
 
-    def forward(self, x: Tensor, temb: Tensor | None = None, skip: Tensor | None = None) -> Tensor:
+    def forward(self, x: Tensor, temb: Tensor | None = None, skip: Tensor | None = None,
+                box_in: SkipGrad | None = None, box_out: SkipGrad | None = None) -> Tensor:
+        """``box_in``: ``x`` is a UNet skip tensor (the mailbox of its up-block gradient);
+        ``box_out``: the mailbox of ``skip`` (see ``SkipGrad``)."""
         tb = self.time_emb_proj(F.silu(temb)) if self.time_emb_proj is not None else None
-        if self._fusable(x) and (skip is None or skip.dtype == x.dtype):
+        if (self._fusable(x) and (skip is None or skip.dtype == x.dtype)
+                and (box_in is None or box_in.enabled)):
             x1 = x.contiguous()
             x2 = None if skip is None else skip.contiguous()
-            return _ResnetBlockFn.apply(self, None if tb is None else tb.contiguous(), x1, x2)
+            if x1 is not x or (x2 is not None and x2 is not skip):
+                box_in = box_out = None  # copies: gradients flow through autograd as usual
+            box_in = box_in if box_in is not None and box_in.enabled else None
+            box_out = box_out if box_out is not None and box_out.enabled and x2 is not None else None
+            return _ResnetBlockFn.apply(self, None if tb is None else tb.contiguous(), x1, x2,
+                                        box_in, box_out)
+        if box_in is not None:
+            box_in.enabled = False
         if skip is not None:
             x = torch.cat([x, skip], dim=1)
         h = self.conv1(self.norm1(x))  # silu(norm1(x)), fused
@@ -241,8 +257,8 @@ class Downsample2D(nn.Module):
         super().__init__()
         self.conv = nn.Conv2d(channels, channels, 3, stride=2, padding=0)
 
-    def forward(self, x: Tensor) -> Tensor:
-        return downsample_conv(self.conv, x)
+    def forward(self, x: Tensor, box: SkipGrad | None = None) -> Tensor:
+        return downsample_conv(self.conv, x, box)
 
 
 class Upsample2D(nn.Module):
@@ -323,25 +339,32 @@ class UNet2DModel(nn.Module):
         ).to(sample.dtype)
         emb = self.time_embedding(t_emb)
 
+        # every skip tensor has two consumers (the next down-path layer and an up-block
+        # resnet); with grad on the device their gradients meet inside the down-path
+        # consumer's VJP kernel (SkipGrad) instead of an autograd accumulation add
+        mail = torch.is_grad_enabled() and sample.is_cuda
+        new_box = (lambda: SkipGrad()) if mail else (lambda: None)  # noqa: E731
         h = self.conv_in(sample)
-        skips = [h]
+        skips, boxes = [h], [new_box()]
         for lvl in self.down_blocks:
             for j, res in enumerate(lvl.resnets):
-                h = res(h, emb)
+                h = res(h, emb, box_in=boxes[-1] if skips[-1] is h else None)
                 if len(lvl.attentions):
                     h = lvl.attentions[j](h)
                 skips.append(h)
+                boxes.append(new_box())
             if lvl.downsamplers is not None:
-                h = lvl.downsamplers[0](h)
+                h = lvl.downsamplers[0](h, box=boxes[-1])
                 skips.append(h)
+                boxes.append(new_box())
 
-        h = self.mid_block.resnets[0](h, emb)
+        h = self.mid_block.resnets[0](h, emb, box_in=boxes[-1])
         h = self.mid_block.attentions[0](h)
         h = self.mid_block.resnets[1](h, emb)
 
         for lvl in self.up_blocks:
             for j, res in enumerate(lvl.resnets):
-                h = res(h, emb, skip=skips.pop())
+                h = res(h, emb, skip=skips.pop(), box_out=boxes.pop())
                 if len(lvl.attentions):
                     h = lvl.attentions[j](h)
             if lvl.upsamplers is not None:

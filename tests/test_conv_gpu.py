@@ -279,11 +279,17 @@ def test_downsample_stride2_forward_and_input_vjp(cuda, shape):
                                           _hip.ptr(wv), None), "pack vjp")
         dx = torch.full((n, cin, h, w), float("nan"), device=cuda)
         dyc = dy.to(cuda)
-        _hip.check(lib.sp_conv3x3_s2_bwd_input(_hip.ptr(dyc), _hip.ptr(wv), n, cin, cout, h, w,
+        _hip.check(lib.sp_conv3x3_s2_bwd_input(_hip.ptr(dyc), _hip.ptr(wv), n, cin, cout, h, w, 0,
                                                _hip.ptr(dx), None), "bwd")
         torch.cuda.synchronize()
         assert torch.isfinite(dx).all()  # every dx element written
         _check(dx, gref)
+        base = torch.randn(n, cin, h, w, generator=g)  # accumulate: dx += conv^T dy
+        dxa = base.to(cuda)
+        _hip.check(lib.sp_conv3x3_s2_bwd_input(_hip.ptr(dyc), _hip.ptr(wv), n, cin, cout, h, w, 1,
+                                               _hip.ptr(dxa), None), "bwd acc")
+        torch.cuda.synchronize()
+        assert torch.equal(dxa, base.to(cuda) + dx)
 
 
 def test_downsample_stride2_rejects_bad_shapes():
