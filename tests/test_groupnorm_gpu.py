@@ -203,3 +203,28 @@ def test_single_pass_matches_two_pass_bitwise(cuda, shape, act):
             assert b is None
             continue
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("single", [0, 1])
+def test_second_addend_matches_separate_add(cuda, single):
+    """add1b (a UNet skip tensor's gradient, added inside the VJP kernel after add1) equals
+    the separate add autograd would do, bit for bit, on both kernel paths."""
+    from samplers_amd import _hip
+    from samplers_amd.networks.layers import gn_backward, gn_forward
+
+    lib = _hip.load_library()
+    gen = torch.Generator().manual_seed(21)
+    n, c, h, w = 2, 128, 64, 64
+    layer = GroupNormAct(32, c, eps=1e-6, act=True).to(cuda)
+    x = torch.randn(n, c, h, w, generator=gen).to(cuda)
+    dz, a1, a1b = (torch.randn(n, c, h, w, generator=gen).to(cuda) for _ in range(3))
+    prev = lib.sp_groupnorm_single_pass(single)
+    try:
+        _, st = gn_forward(layer, x)
+        d_sep, _ = gn_backward(layer, dz, x, None, None, st, add1=a1)
+        d_sep = d_sep + a1b
+        d_in, _ = gn_backward(layer, dz, x, None, None, st, add1=a1, add1b=a1b)
+        torch.cuda.synchronize()
+    finally:
+        lib.sp_groupnorm_single_pass(prev)
+    assert torch.equal(d_in, d_sep)
