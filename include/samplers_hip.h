@@ -218,6 +218,12 @@ int sp_pixel_opt_step(const sp_op* op, float* x, float* exp_avg, float* exp_avg_
  *   *stop = 1 if loss < threshold (compared in double).  Skipped once *stop != 0. */
 int sp_opt_check(const float* partials, int64_t count, float total, double threshold,
                  int32_t* stop, float* loss_out, sp_stream_t stream);
+/* The latent-space loop's rule (resample_kernels.py:75-91): as sp_opt_check, and from
+ * iteration plateau_from (200 in the reference) on also *stop = 1 when the loss exceeds the
+ * previous iteration's (*prev_loss, updated here).  itr is the 0-based iteration. */
+int sp_opt_check_plateau(const float* partials, int64_t count, float total, double threshold,
+                         int64_t itr, int64_t plateau_from, float* prev_loss, int32_t* stop,
+                         float* loss_out, sp_stream_t stream);
 
 /* ---- prior building blocks (SURVEY.md §8b "groupnorm_silu_fwd/bwd") -------------------
  * GroupNorm over NCHW x (n, channels, hw = H*W) with `groups` groups, eps, optional

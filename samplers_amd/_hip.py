@@ -107,6 +107,8 @@ SIGNATURES = {
     "sp_pixel_opt_step": (ctypes.c_int, [_OPP, _P, _P, _P, _P, _I64, _I64, _F,
                                          ctypes.POINTER(SpAdamWCoefs), _P, _P, _P]),
     "sp_opt_check": (ctypes.c_int, [_P, _I64, _F, ctypes.c_double, _P, _P, _P]),
+    "sp_opt_check_plateau": (ctypes.c_int, [_P, _I64, _F, ctypes.c_double, _I64, _I64, _P, _P, _P,
+                                            _P]),
     "sp_conv3x3_supported": (ctypes.c_int, [ctypes.c_int32] * 4),
     "sp_conv3x3_packed_size": (_I64, [ctypes.c_int32, ctypes.c_int32]),
     "sp_conv3x3_pack": (ctypes.c_int, [_P, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, _P, _P]),
@@ -190,6 +192,28 @@ def check(status: int, what: str) -> None:
     if status != 0:
         detail = load_library().sp_last_error().decode(errors="replace")
         raise HipLibraryError(f"{what} failed: {_ERRORS.get(status, status)} {detail}".strip())
+
+
+class solve_guard:
+    """Checks, once per sampler call, that no single-pass GroupNorm team gave up waiting for
+    a member (``sp_groupnorm_team_timeouts``; a give-up leaves that group's statistics
+    built from missing partials).  The counter read waits for the device, so it runs at the
+    end of a solve, never inside the step loop."""
+
+    def __enter__(self):
+        self.lib = load_library()
+        self.before = int(self.lib.sp_groupnorm_team_timeouts())
+        return self
+
+    def __exit__(self, exc_type, exc, tb):
+        if exc_type is None:
+            after = int(self.lib.sp_groupnorm_team_timeouts())
+            if after != self.before:
+                raise HipLibraryError(
+                    f"GroupNorm team kernels timed out {after - self.before} time(s) during this "
+                    "solve: the result is invalid (a co-resident kernel held CUs); rerun, or set "
+                    "SAMPLERS_AMD_GN_SINGLE_PASS=0")
+        return False
 
 
 def ptr(t: torch.Tensor | None) -> int | None:

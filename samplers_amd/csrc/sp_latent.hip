@@ -289,6 +289,29 @@ __global__ __launch_bounds__(kBlock) void k_opt_check(const float* __restrict__ 
     }
 }
 
+// ReSample's latent-space stopping rule (resample_kernels.py:75-91) on the device: from
+// iteration `plateau_from` on, stop when the loss rose above the previous iteration's; stop
+// below the threshold.  prev[0] holds the previous loss (written from plateau_from on).
+__global__ void k_opt_check_plateau(const float* __restrict__ p, int64_t count, float total,
+                                    double threshold, int64_t itr, int64_t plateau_from,
+                                    float* __restrict__ prev, int32_t* __restrict__ stop,
+                                    float* __restrict__ loss_out) {
+    __shared__ float red[4];
+    if (*stop) return;
+    float s = 0.f;
+    for (int64_t i = threadIdx.x; i < count; i += kBlock) s += p[i];
+    const float t = block_sum(s, red);
+    if (threadIdx.x == 0) {
+        const float loss = t / total;
+        if (loss_out) *loss_out = loss;
+        if (itr >= plateau_from) {
+            if (itr > plateau_from && prev[0] < loss) *stop = 1;
+            prev[0] = loss;
+        }
+        if ((double)loss < threshold) *stop = 1;
+    }
+}
+
 static inline unsigned grid_for(int64_t work, int V, int64_t batch) {
     int64_t blocks = (work + (int64_t)kBlock * V - 1) / ((int64_t)kBlock * V);
     const int64_t cap = std::max<int64_t>(1, 4096 / std::max<int64_t>(batch, 1));
@@ -448,6 +471,16 @@ int sp_opt_check(const float* partials, int64_t count, float total, double thres
     launch(0, k_opt_check, dim3(1), dim3(kBlock), static_cast<hipStream_t>(stream), partials,
            count, total, threshold, stop, loss_out);
     return check_launch("sp_opt_check");
+}
+
+int sp_opt_check_plateau(const float* partials, int64_t count, float total, double threshold,
+                         int64_t itr, int64_t plateau_from, float* prev_loss, int32_t* stop,
+                         float* loss_out, sp_stream_t stream) {
+    if (!partials || !stop || !prev_loss || count <= 0 || !(total > 0.f) || itr < 0)
+        return SP_EINVAL;
+    launch(0, k_opt_check_plateau, dim3(1), dim3(kBlock), static_cast<hipStream_t>(stream),
+           partials, count, total, threshold, itr, plateau_from, prev_loss, stop, loss_out);
+    return check_launch("sp_opt_check_plateau");
 }
 
 }  // extern "C"

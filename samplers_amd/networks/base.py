@@ -40,7 +40,8 @@ class EpsilonNetwork(torch.nn.Module, ABC, Generic[C]):
         self._batch_size = None
         self._num_sampling_steps = None
         self._num_reconstructions = None
-        self.timesteps_host: list[int] | None = None
+        self._ts_host: list[int] | None = None
+        self._ts_src = None
 
     @abstractmethod
     def forward(self, x: Tensor, t: Tensor | int): ...
@@ -59,14 +60,33 @@ class EpsilonNetwork(torch.nn.Module, ABC, Generic[C]):
     @property
     def alphas_cumprod_host(self) -> np.ndarray:
         """fp32 host copy of ``alphas_cumprod`` (same values the device buffer holds)."""
-        if self._acp_host is None or self._acp_host.shape[0] != self.alphas_cumprod.shape[0]:
-            self._acp_host = self.alphas_cumprod.detach().float().cpu().numpy().copy()
+        buf = self.alphas_cumprod
+        if self._acp_host is None or getattr(self, "_acp_src", None) is not buf:
+            self._acp_host = buf.detach().float().cpu().numpy().copy()
+            self._acp_src = buf
         return self._acp_host
 
     def _set_timesteps_buffer(self, timesteps: Tensor) -> None:
         timesteps = timesteps.to(self.alphas_cumprod.device)
         self.register_buffer(name="timesteps", tensor=timesteps, persistent=True)
-        self.timesteps_host = [int(t) for t in timesteps.cpu().tolist()]
+        self._ts_host = [int(t) for t in timesteps.cpu().tolist()]
+        self._ts_src = timesteps
+
+    @property
+    def timesteps_host(self) -> list[int] | None:
+        """Host copy of the ``timesteps`` buffer (``None`` before it exists).
+
+        Subclasses written against the reference ABC register ``timesteps`` themselves in
+        ``set_sampling_parameters`` (``/root/reference/samplers/networks/diffusers/ddpm.py:58``);
+        the copy is then taken here, once per registered buffer (one device read per
+        sampler call, none per step)."""
+        buf = self._buffers.get("timesteps")
+        if buf is None:
+            return None
+        if self._ts_src is not buf or self._ts_host is None:
+            self._ts_host = [int(t) for t in buf.detach().cpu().tolist()]
+            self._ts_src = buf
+        return self._ts_host
 
     @property
     def device(self) -> torch.device:
@@ -127,6 +147,27 @@ class LatentEpsilonNetwork(EpsilonNetwork[C], ABC, Generic[C]):
 
     @abstractmethod
     def _encode(self, x: Tensor, *, differentiable: bool = False): ...
+
+
+def host_timesteps(net) -> list[int]:
+    """Ascending timestep indices of ``net`` on the host: ``timesteps_host`` when the network
+    derives from this package's ABC, else read once from its ``timesteps`` buffer (a network
+    written against the reference ABC, ``networks/base.py:13-85``, duck-typed)."""
+    ts = getattr(net, "timesteps_host", None)
+    if ts is None:
+        buf = getattr(net, "timesteps", None)
+        if buf is None:
+            raise RuntimeError("Call `set_sampling_parameters()` before sampling.")
+        ts = [int(t) for t in torch.as_tensor(buf).detach().cpu().tolist()]
+    return list(ts)
+
+
+def host_alphas_cumprod(net) -> np.ndarray:
+    """fp32 host copy of ``net.alphas_cumprod`` (see ``host_timesteps``)."""
+    acp = getattr(net, "alphas_cumprod_host", None)
+    if acp is None:
+        acp = net.alphas_cumprod.detach().float().cpu().numpy().copy()
+    return acp
 
 
 @dataclasses.dataclass(slots=True)

@@ -375,10 +375,10 @@ class SkipGrad:
         self.grad: Tensor | None = None
         self.enabled = True
 
-    def take(self) -> Tensor:
+    def take(self) -> Tensor | None:
+        """The delivered gradient, or ``None`` when the up-block consumer did not deliver one
+        (it fell back to the autograd path, which then accumulates its gradient itself)."""
         g, self.grad = self.grad, None
-        if g is None:
-            raise RuntimeError("skip gradient missing: the up-block consumer's backward did not run first")
         return g
 
 
@@ -396,32 +396,27 @@ class _ConvS2Fn(torch.autograd.Function):
                    "sp_conv3x3_s2_fwd")
         ctx.module = module
         ctx.box = box
-        ctx.has_bias = bias is not None
-        ctx.save_for_backward(x if weight.requires_grad else None, weight)
         ctx.x_shape = x.shape
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        x, weight = ctx.saved_tensors
-        dx = dw = db = None
-        dy = dy.contiguous()
+        """Input VJP only: the tile serves frozen weights (``downsample_conv``)."""
+        dx = None
         if ctx.needs_input_grad[0]:
             lib = _hip.load_library()
             n, cin, h, w = ctx.x_shape
-            acc = ctx.box is not None
             # with a skip gradient pending, accumulate into its buffer (dx = skip grad + VJP)
-            dx = ctx.box.take() if acc else torch.empty(tuple(ctx.x_shape), device=dy.device,
-                                                        dtype=torch.float32)
-            _hip.check(lib.sp_conv3x3_s2_bwd_input(_hip.ptr(dy), _hip.ptr(_s2_packed(ctx.module, True)),
+            dx = ctx.box.take() if ctx.box is not None else None
+            acc = dx is not None
+            if dx is None:
+                dx = torch.empty(tuple(ctx.x_shape), device=dy.device, dtype=torch.float32)
+            _hip.check(lib.sp_conv3x3_s2_bwd_input(_hip.ptr(dy.contiguous()),
+                                                   _hip.ptr(_s2_packed(ctx.module, True)),
                                                    n, cin, ctx.module.out_channels, h, w, int(acc),
                                                    _hip.ptr(dx), _hip.stream_of(dy)),
                        "sp_conv3x3_s2_bwd_input")
-        if ctx.needs_input_grad[1]:
-            dw = torch.nn.grad.conv2d_weight(F.pad(x, (0, 1, 0, 1)), weight.shape, dy, stride=2)
-        if ctx.has_bias and ctx.needs_input_grad[2]:
-            db = dy.sum(dim=(0, 2, 3))
-        return dx, dw, db, None, None
+        return dx, None, None, None, None
 
 
 def downsample_conv(module: nn.Conv2d, x: Tensor, box: SkipGrad | None = None) -> Tensor:

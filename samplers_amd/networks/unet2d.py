@@ -178,13 +178,20 @@ class ResnetBlock2D(nn.Module):
                 box_in: SkipGrad | None = None, box_out: SkipGrad | None = None) -> Tensor:
         """``box_in``: ``x`` is a UNet skip tensor (the mailbox of its up-block gradient);
         ``box_out``: the mailbox of ``skip`` (see ``SkipGrad``)."""
+        if box_in is not None and skip is not None:
+            raise ValueError("box_in (x is a skip tensor) and skip (an up-block input) are exclusive")
         tb = self.time_emb_proj(F.silu(temb)) if self.time_emb_proj is not None else None
         if (self._fusable(x) and (skip is None or skip.dtype == x.dtype)
                 and (box_in is None or box_in.enabled)):
             x1 = x.contiguous()
             x2 = None if skip is None else skip.contiguous()
             if x1 is not x or (x2 is not None and x2 is not skip):
-                box_in = box_out = None  # copies: gradients flow through autograd as usual
+                # copies: gradients flow through autograd as usual; both sides of the
+                # hand-off see the boxes disabled
+                for box in (box_in, box_out):
+                    if box is not None:
+                        box.enabled = False
+                box_in = box_out = None
             box_in = box_in if box_in is not None and box_in.enabled else None
             box_out = box_out if box_out is not None and box_out.enabled and x2 is not None else None
             return _ResnetBlockFn.apply(self, None if tb is None else tb.contiguous(), x1, x2,

@@ -40,9 +40,16 @@ class NoiseModel(nn.Module, ABC):
     def sample(self, shape: Shape, *, device: Device | None = None, dtype: DType = None,
                generator: RNG = None) -> Tensor: ...
 
-    @abstractmethod
-    def grad_scale(self) -> float:
-        """fp32 ``c`` such that ``∂ log p / ∂(Ax) = c · (y − Ax)`` per element."""
+    def grad_scale(self) -> float | None:
+        """fp32 ``c`` such that ``∂ log p / ∂(Ax) = c · (y − Ax)`` per element, or ``None``.
+
+        Not part of the reference ABC (``noise.py:13-45``), so a subclass written against
+        it need not define it.  This default probes ``score`` (autograd of ``log_prob``) on
+        a fixed residual: if the score is ``−c·r`` for one scalar c at every element (an
+        isotropic quadratic log-density, e.g. a Gaussian), c is returned and the fused HIP
+        passes apply it; otherwise ``None`` and the samplers differentiate ``log_prob``
+        by autograd for the residual cotangent (the generic plugin path)."""
+        return probe_grad_scale(self)
 
     @property
     def device(self) -> torch.device:
@@ -51,6 +58,41 @@ class NoiseModel(nn.Module, ABC):
     @property
     def dtype(self) -> torch.dtype:
         return next(self.buffers()).dtype
+
+
+def _draw_device(device, generator):
+    """Where to draw: the generator's device when one is given (a CPU generator with a device
+    observation draws on the host and the values move; the reference requires them to match),
+    else ``device``."""
+    if generator is None:
+        return device
+    return generator.device
+
+
+def probe_grad_scale(noise) -> float | None:
+    """``c`` with ``score(r) == −c·r`` on a probe residual, or ``None`` (see
+    ``NoiseModel.grad_scale``).  Works on any object with the reference's
+    ``score`` / ``log_prob`` methods (duck-typed third-party models)."""
+    gen = torch.Generator().manual_seed(0)
+    r = torch.randn(2, 64, generator=gen, dtype=torch.float32)
+    r[:, 0] = 1.0
+    try:
+        buffers = list(noise.buffers()) if isinstance(noise, nn.Module) else []
+        dev = buffers[0].device if buffers else torch.device("cpu")
+        score = getattr(noise, "score", None)
+        if score is None:
+            return None
+        g = score(r.to(dev)).detach().float().cpu()
+    except Exception:  # noqa: BLE001 - a model that cannot be probed takes the generic path
+        return None
+    if g.shape != r.shape or not torch.isfinite(g).all():
+        return None
+    c = -float(g[0, 0])
+    if not np.isfinite(c) or c == 0.0:
+        return None
+    if not torch.allclose(g, -c * r, rtol=1e-5, atol=1e-6 * abs(c)):
+        return None
+    return float(np.float32(c))
 
 
 class GaussianNoise(NoiseModel):
@@ -77,7 +119,8 @@ class GaussianNoise(NoiseModel):
                generator: RNG = None) -> Tensor:
         device = self.sigma.device if device is None else device
         dtype = self.sigma.dtype if dtype is None else dtype
-        eps = torch.randn(shape, dtype=dtype, device=device, generator=generator)
+        eps = torch.randn(shape, dtype=dtype, device=_draw_device(device, generator),
+                          generator=generator).to(device)
         return eps * self.sigma.to(dtype)
 
     def grad_scale(self) -> float:
@@ -109,9 +152,10 @@ class PoissonNoise(NoiseModel):
                generator: RNG = None) -> Tensor:
         device = self.rate.device if device is None else device
         dtype = self.rate.dtype if dtype is None else dtype
-        lam = torch.full(shape, self.rate.item(), device=device, dtype=dtype)
+        lam = torch.full(shape, self.rate.item(), device=_draw_device(device, generator),
+                         dtype=dtype)
         k = torch.poisson(lam, generator=generator)
-        return k - lam
+        return (k - lam).to(device)
 
     def grad_scale(self) -> float:
         denom = np.float32(self.rate.detach().cpu().item()) + np.float32(1e-3)

@@ -2,15 +2,34 @@
 
 from __future__ import annotations
 
+import functools
 from abc import ABC
 
+from samplers_amd import _hip
 from samplers_amd.dtypes import Shape, Tensor
 from samplers_amd.networks.base import EpsilonNetwork
 
 
+def _guarded(call):
+    @functools.wraps(call)
+    def run(self, *args, **kwargs):
+        with _hip.solve_guard():
+            return call(self, *args, **kwargs)
+
+    return run
+
+
 class PosteriorSampler(ABC):
+    """Every subclass's ``__call__`` runs under ``_hip.solve_guard`` (one check per solve
+    that the single-pass GroupNorm kernels completed every team)."""
+
     def __init__(self, network: EpsilonNetwork):
         self._epsilon_network = network
+
+    def __init_subclass__(cls, **kwargs):
+        super().__init_subclass__(**kwargs)
+        if "__call__" in cls.__dict__:
+            cls.__call__ = _guarded(cls.__dict__["__call__"])
 
     @staticmethod
     def _flatten_leading(x: Tensor, *, x_shape: Shape) -> tuple[Tensor, Shape]:

@@ -36,7 +36,7 @@ from torch import Tensor
 from samplers_amd import _hip
 from samplers_amd.dtypes import Shape
 from samplers_amd.inverse_problem import InverseProblem
-from samplers_amd.networks.base import EpsilonNetwork
+from samplers_amd.networks.base import EpsilonNetwork, host_alphas_cumprod, host_timesteps
 from samplers_amd.samplers.base import PosteriorSampler
 from samplers_amd.samplers.utils.batch_view import BatchView
 from samplers_amd.samplers.utils.bridge_kernels import bridge_coefficients, x0_coefficients
@@ -125,7 +125,7 @@ class FusedDPSStep:
                  micro_batch: int | None = None, timer: KernelTimer | None = None,
                  reuse_v: bool = True, mode: str = "dps", guidance_weight: float = 1.0) -> None:
         op = inverse_problem.operator
-        desc = op.hip_descriptor()
+        desc = getattr(op, "hip_descriptor", lambda: None)()
         if desc is None:
             raise NotImplementedError(
                 f"{type(op).__name__} has no native (HIP) implementation; the fused DPS path "
@@ -151,7 +151,18 @@ class FusedDPSStep:
         self.mode = mode
         # DPS: d log p/d(Ax) = c r.  PGDM: d/dx0 of ||A^+ y - A^+ A x0||^2 = -2 A^T r for the
         # partial isometries with a native kernel (A^+ = A^T: identity, inpainting, mask).
-        self.grad_scale = (float(inverse_problem.noise.grad_scale()) if mode == "dps" else -2.0)
+        self.grad_scale = -2.0
+        if mode == "dps":
+            gs = getattr(inverse_problem.noise, "grad_scale", None)
+            if gs is None:
+                from samplers_amd.noise import probe_grad_scale
+
+                gs = lambda: probe_grad_scale(inverse_problem.noise)  # noqa: E731
+            c = gs()
+            if c is None:
+                raise NotImplementedError(f"{type(inverse_problem.noise).__name__} has no constant "
+                                          "likelihood-gradient factor; use GenericDPSStep")
+            self.grad_scale = float(c)
         self.guidance_weight = float(guidance_weight)
         self.gamma, self.eta = float(gamma), float(eta)
         # pass 2 re-reads pass 1's v (default: one coalesced float4 stream; measured 4 % faster
@@ -162,7 +173,7 @@ class FusedDPSStep:
         self.timer = timer
 
     def coefficients(self, t: int, t_prev: int, s: int) -> _hip.SpDpsCoefs:
-        acp = self.network.alphas_cumprod_host
+        acp = host_alphas_cumprod(self.network)
         a, k = x0_coefficients(acp, t)
         br = bridge_coefficients(acp, ell=t, t=t_prev, s=s, eta=self.eta)
         # PGDM: sample = ddim - guidance_weight * sqrt(1 - acp_t) * grad   (pgdm.py:131-135)
@@ -223,7 +234,7 @@ class FusedDPSStep:
 
     def predict_x0(self, x: Tensor, t: int) -> Tensor:
         """Final ``predict_x0`` (``dps.py:125-126``): prior forward + HIP epilogue."""
-        a, k = x0_coefficients(self.network.alphas_cumprod_host, t)
+        a, k = x0_coefficients(host_alphas_cumprod(self.network), t)
         out = torch.empty_like(x)
         for b0, b1 in self._chunks(x.shape[0]):
             with torch.no_grad():
@@ -232,6 +243,124 @@ class FusedDPSStep:
                                               _hip.ptr(out[b0:b1]), _hip.stream_of(x)),
                        "sp_predict_x0")
         return out
+
+
+class GenericDPSStep(FusedDPSStep):
+    """One DPS / PGDM iteration for plugins the HIP library does not know.
+
+    The reference differentiates through *any* ``Operator`` and ``NoiseModel``
+    (``dps.py:99-103``, ``pgdm.py:104-119``).  Here the residual cotangent
+    ``v = ∂(objective)/∂x̂₀`` comes from torch autograd through the plugin's own
+    ``apply`` (and ``log_prob`` / ``apply_pseudo_inverse``) on the device, and everything
+    else stays on the HIP path: x̂₀ by ``sp_predict_x0``, the prior's input-VJP with
+    ``grad_outputs = v``, and pass 2 (``sp_dps_update`` over an identity descriptor of
+    the sample, v given) for the bridge mean, noise and guidance.  The per-sample
+    ``‖r_b‖²`` enters pass 2 through its partial-sum slot (column 0, the rest zero, so
+    the fixed-order sum is exact).
+    """
+
+    def __init__(self, network: EpsilonNetwork, inverse_problem: InverseProblem,
+                 observation_rows: Tensor, y_div: int, *, gamma: float = 1.0, eta: float = 1.0,
+                 micro_batch: int | None = None, timer: KernelTimer | None = None,
+                 mode: str = "dps", guidance_weight: float = 1.0, **_unused) -> None:
+        from samplers_amd.operators import IdentityOperator
+
+        if mode not in ("dps", "pgdm"):
+            raise ValueError(mode)
+        _hip.require_cuda(observation_rows, "DPSSampler")
+        self.lib = _hip.load_library()
+        self.network = network
+        self.problem = inverse_problem
+        self.operator = inverse_problem.operator
+        self.x_shape = tuple(self.operator.x_shape)
+        self.desc = IdentityOperator(self.x_shape).hip_descriptor()
+        self.n = self.m = int(self.desc.n)
+        self.partials = int(self.lib.sp_rsq_partials(self.desc))
+        self.y = observation_rows
+        self.y_div = int(y_div)
+        self.mode = mode
+        self.grad_scale = 0.0  # unused: v comes from autograd
+        self.guidance_weight = float(guidance_weight)
+        self.gamma, self.eta = float(gamma), float(eta)
+        self.needs_v = True
+        self.micro_batch = micro_batch
+        self.timer = timer
+        self._pinv_y = None
+
+    def _rows(self, b0: int, b1: int) -> Tensor:
+        idx = torch.arange(b0, b1, device=self.y.device) // self.y_div
+        return self.y.index_select(0, idx)
+
+    def _cotangent(self, x0: Tensor, b0: int, b1: int) -> tuple[Tensor, Tensor | None]:
+        """(v = ∂ objective / ∂x̂₀, ‖r_b‖² per sample or None) by autograd through the plugin."""
+        op = self.operator
+        y = self._rows(b0, b1)
+        with torch.enable_grad():
+            x0r = x0.detach().requires_grad_(True)
+            if self.mode == "dps":  # inverse_problem.log_likelihood (inverse_problem.py:17-21)
+                r = y - op.apply(x0r)
+                obj = self.problem.noise.log_prob(r).sum()
+            else:  # PGDM consistency loss (pgdm.py:110-115)
+                y_inv = op.apply_pseudo_inverse(y)
+                obj = (y_inv - op.apply_pseudo_inverse(op.forward(x0r))).pow(2).sum()
+                r = None
+            (v,) = torch.autograd.grad(obj, x0r)
+        rsq = None
+        if r is not None:
+            rsq = r.detach().reshape(r.shape[0], -1).float().square().sum(dim=1)
+        return v.to(torch.float32).contiguous(), rsq
+
+    def __call__(self, x: Tensor, step: int, t: int, t_prev: int, s: int, *,
+                 xi: Tensor | None = None, seed: int = 0, sample_offset: int = 0) -> Tensor:
+        lib, desc = self.lib, self.desc
+        coefs = self.coefficients(t, t_prev, s)
+        stream = _hip.stream_of(x)
+        for b0, b1 in self._chunks(x.shape[0]):
+            xc = x[b0:b1]
+            bc = b1 - b0
+            with torch.enable_grad():
+                xr = xc.detach().requires_grad_(True)
+                eps = self.network.forward(xr, t)
+            eps_c = eps.detach().contiguous()
+            x0 = torch.empty_like(xc)
+            _hip.check(lib.sp_predict_x0(_hip.ptr(xc), _hip.ptr(eps_c), xc.numel(), coefs.a,
+                                         coefs.k, _hip.ptr(x0), stream), "sp_predict_x0")
+            v, rsq = self._cotangent(x0, b0, b1)
+            part = None
+            if rsq is not None:
+                part = torch.zeros((bc, self.partials), device=x.device, dtype=torch.float32)
+                part[:, 0] = rsq
+            (w,) = torch.autograd.grad(eps, xr, grad_outputs=v.view_as(eps))
+            del eps, xr
+            xic = None if xi is None else xi[b0:b1].contiguous()
+            _hip.check(lib.sp_dps_update(desc, _hip.ptr(xc), _hip.ptr(eps_c), None, _hip.ptr(v),
+                                         _hip.ptr(w.contiguous()), _hip.ptr(part), _hip.ptr(xic),
+                                         seed, step, sample_offset + b0, bc, 1, coefs,
+                                         _hip.ptr(xc), stream), "sp_dps_update")
+        return x
+
+
+def native_plugins(inverse_problem) -> bool:
+    """True when the operator has a HIP descriptor and the noise a constant ∂log p/∂(Ax)
+    factor, i.e. the fused passes can replace autograd entirely."""
+    desc_fn = getattr(inverse_problem.operator, "hip_descriptor", None)
+    if desc_fn is None or desc_fn() is None:
+        return False
+    gs = getattr(inverse_problem.noise, "grad_scale", None)
+    if gs is None:
+        from samplers_amd.noise import probe_grad_scale
+
+        return probe_grad_scale(inverse_problem.noise) is not None
+    return gs() is not None
+
+
+def make_dps_step(network, inverse_problem, observation_rows, y_div, **kw):
+    """The fused HIP step for native plugins, the generic-plugin step otherwise."""
+    mode = kw.get("mode", "dps")
+    native_op = getattr(inverse_problem.operator, "hip_descriptor", lambda: None)() is not None
+    if (mode == "dps" and native_plugins(inverse_problem)) or (mode == "pgdm" and native_op):
+        return FusedDPSStep(network, inverse_problem, observation_rows, y_div, **kw)
+    return GenericDPSStep(network, inverse_problem, observation_rows, y_div, **kw)
 
 
 def initial_sample(shape: tuple, device: torch.device, *, rng: str, seed: int, sample_offset: int,
@@ -300,16 +429,18 @@ class DPSSampler(PosteriorSampler, Generic[Condition_co]):
             obs = inverse_problem.observation
             _hip.require_cuda(obs, "DPSSampler")
             y_rows = obs.reshape(max(view.batch_size, 1), *inverse_problem.operator.y_shape)
-            step = FusedDPSStep(net, inverse_problem, y_rows.to(torch.float32), num_reconstructions,
-                                gamma=gamma, eta=eta, micro_batch=micro_batch, timer=timer)
+            step = make_dps_step(net, inverse_problem, y_rows.to(torch.float32), num_reconstructions,
+                                 gamma=gamma, eta=eta, micro_batch=micro_batch, timer=timer)
             if seed is None and noise_fn is None and rng == "philox":
                 seed = draw_seed()
             seed = int(seed or 0)
 
             x = initial_sample(view.flat_shape, net.device, rng=rng, seed=seed,
                                sample_offset=sample_offset, noise_fn=noise_fn)
-            ts = net.timesteps_host
+            ts = host_timesteps(net)
             if graph:
+                if not isinstance(step, FusedDPSStep) or isinstance(step, GenericDPSStep):
+                    raise ValueError("graph=True needs natively implemented plugins")
                 if noise_fn is not None or rng != "philox":
                     raise ValueError("graph=True needs the in-kernel Philox noise (rng='philox')")
                 from .graph import GraphedStepLoop, schedule_for

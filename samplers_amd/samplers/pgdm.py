@@ -19,8 +19,9 @@ from torch import Tensor
 from samplers_amd import _hip
 from samplers_amd.dtypes import Shape
 from samplers_amd.inverse_problem import InverseProblem
+from samplers_amd.networks.base import host_timesteps
 from samplers_amd.samplers.base import PosteriorSampler
-from samplers_amd.samplers.dps import FusedDPSStep, KernelTimer, NoiseFn, draw_seed, initial_sample
+from samplers_amd.samplers.dps import KernelTimer, NoiseFn, draw_seed, initial_sample, make_dps_step
 from samplers_amd.samplers.utils.batch_view import BatchView
 
 Condition_co = TypeVar("Condition_co", covariant=True)
@@ -71,15 +72,15 @@ class PGDMSampler(PosteriorSampler, Generic[Condition_co]):
             obs = inverse_problem.observation
             _hip.require_cuda(obs, "PGDMSampler")
             y_rows = obs.reshape(max(view.batch_size, 1), *operator.y_shape).to(torch.float32)
-            step = FusedDPSStep(net, inverse_problem, y_rows, num_reconstructions, eta=eta,
-                                micro_batch=micro_batch, timer=timer, mode="pgdm",
-                                guidance_weight=guidance_weight)
+            step = make_dps_step(net, inverse_problem, y_rows, num_reconstructions, eta=eta,
+                                 micro_batch=micro_batch, timer=timer, mode="pgdm",
+                                 guidance_weight=guidance_weight)
             if seed is None and noise_fn is None and rng == "philox":
                 seed = draw_seed()
             seed = int(seed or 0)
             x = initial_sample(view.flat_shape, net.device, rng=rng, seed=seed,
                                sample_offset=sample_offset, noise_fn=noise_fn)
-            ts = net.timesteps_host
+            ts = host_timesteps(net)
             for i in range(len(ts) - 1, 1, -1):
                 xi = None
                 if noise_fn is not None:

@@ -27,13 +27,13 @@ import math
 from typing import Generic, TypeVar
 
 import torch
-import torch.distributed as dist
 from torch import Tensor
 
 from samplers_amd import _hip
+from samplers_amd.distributed import all_reduce_sum_
 from samplers_amd.dtypes import Shape
 from samplers_amd.inverse_problem import InverseProblem
-from samplers_amd.networks.base import LatentEpsilonNetwork
+from samplers_amd.networks.base import LatentEpsilonNetwork, host_alphas_cumprod, host_timesteps
 from samplers_amd.operators import IdentityOperator
 from samplers_amd.samplers.base import PosteriorSampler
 from samplers_amd.samplers.dps import NoiseFn, draw_seed, initial_sample
@@ -43,6 +43,25 @@ from samplers_amd.samplers.utils.bridge_kernels import bridge_coefficients, x0_c
 Condition_co = TypeVar("Condition_co", covariant=True)
 
 
+def generic_pixel_terms(op, y_rows: Tensor, hty_rows: Tensor, y_div: int, x0: Tensor):
+    """PSLD's pixel-space terms for an operator without a HIP descriptor, by its own ``apply``
+    / ``apply_transpose`` under autograd (``psld.py:129-136``): returns
+    (x_eff = Aᵀy + x̂₀ − AᵀA x̂₀ as a flat fp32 tensor, this shard's ‖y − A x̂₀‖² as a 1-element
+    tensor, the autograd graph (x̂₀ leaf, r, x_eff) for the cotangent).  Sample b uses
+    observation row b // y_div."""
+    b = x0.shape[0]
+    idx = torch.arange(b, device=x0.device) // y_div
+    y = y_rows.index_select(0, idx).reshape(b, *op.y_shape)
+    hty = hty_rows.index_select(0, idx).reshape(b, *op.x_shape)
+    with torch.enable_grad():
+        x0r = x0.detach().reshape(b, *op.x_shape).requires_grad_(True)
+        hx = op.apply(x0r)
+        r = y - hx
+        x_eff = hty + x0r - op.apply_transpose(hx)
+    ss = r.detach().float().square().sum().reshape(1)
+    return x_eff.detach().reshape(b, -1).to(torch.float32).contiguous(), ss, (x0r, r, x_eff)
+
+
 class FusedPSLDStep:
     """One PSLD iteration over a flat latent batch on the HIP path."""
 
@@ -50,30 +69,50 @@ class FusedPSLDStep:
                  observation_rows: Tensor, y_div: int, latent_shape: Shape, *, gamma: float = 1.0,
                  omega: float = 0.1, eta: float = 1.0, group=None) -> None:
         op = inverse_problem.operator
-        desc = op.hip_descriptor()
-        if desc is None:
-            raise NotImplementedError(f"{type(op).__name__} has no native (HIP) implementation")
+        desc = getattr(op, "hip_descriptor", lambda: None)()
         _hip.require_cuda(observation_rows, "PSLDSampler")
         self.lib = _hip.load_library()
         self.net, self.op, self.desc = network, op, desc
         self.y = observation_rows.to(torch.float32).contiguous()
         self.y_div = int(y_div)
-        self.blur = desc.kind == _hip.SP_OP_BLUR
-        self.n, self.m = int(desc.n), int(desc.m)
+        # operators without a HIP descriptor: A, A^T and their VJPs by torch autograd
+        self.generic = desc is None
+        self.blur = not self.generic and desc.kind == _hip.SP_OP_BLUR
+        if self.generic:
+            self.n, self.m = int(math.prod(op.x_shape)), int(math.prod(op.y_shape))
+        else:
+            self.n, self.m = int(desc.n), int(desc.m)
         self.latent_shape = tuple(latent_shape)
         self.nz = int(math.prod(self.latent_shape))
         self.zdesc = IdentityOperator(self.latent_shape).hip_descriptor()
         self.gamma, self.omega, self.eta = float(gamma), float(omega), float(eta)
         self.group = group
         self.hty = None
-        if self.blur:  # A^T y once per run (psld.py:113-115)
-            self.hty = op.apply_transpose(self.y.reshape(-1, *op.y_shape)).reshape(-1, self.n)
+        self._graph = None
+        if self.blur or self.generic:  # A^T y once per run (psld.py:113-115)
+            with torch.no_grad():
+                self.hty = op.apply_transpose(self.y.reshape(-1, *op.y_shape)).reshape(-1, self.n)
 
-    def _distributed(self) -> bool:
-        return dist.is_initialized() and dist.get_world_size(self.group) > 1
+    def _pixel_pass_generic(self, x0: Tensor, norms: Tensor) -> Tensor:
+        x_eff, ss, self._graph = generic_pixel_terms(self.op, self.y, self.hty, self.y_div, x0)
+        norms.copy_(ss)
+        return x_eff
+
+    def _cotangent_generic(self, u: Tensor, norms: Tensor) -> Tensor:
+        """c_x0 = ω J_rᵀ r/‖r‖ + J_{x_eff}ᵀ u through the saved graph (the gradient of
+        ω‖y − A x̂₀‖ + γ‖ẑ₀ − E(x_eff)‖ w.r.t. x̂₀, given u = its cotangent at x_eff)."""
+        x0r, r, x_eff = self._graph
+        self._graph = None
+        L = norms.sqrt()
+        scale = torch.where(L > 0, self.omega / L, torch.zeros_like(L))
+        (c,) = torch.autograd.grad((r, x_eff), x0r,
+                                   grad_outputs=(r.detach() * scale, u.reshape(x_eff.shape)))
+        return c.reshape(u.shape[0], self.n).to(torch.float32).contiguous()
 
     def _pixel_pass(self, x0: Tensor, norms: Tensor, stream: int) -> tuple[Tensor, Tensor]:
         lib, b = self.lib, x0.shape[0]
+        if self.generic:
+            return self._pixel_pass_generic(x0, norms), None
         x_eff, atr = torch.empty_like(x0), torch.empty_like(x0)
         if not self.blur:
             P = int(lib.sp_rsq_partials(self.desc))
@@ -106,7 +145,7 @@ class FusedPSLDStep:
         lib, net = self.lib, self.net
         b = z.shape[0]
         stream = _hip.stream_of(z)
-        acp = net.alphas_cumprod_host
+        acp = host_alphas_cumprod(net)
         a, k = x0_coefficients(acp, t)
         br = bridge_coefficients(acp, ell=t, t=t_prev, s=s, eta=self.eta)
         norms = torch.zeros(2, device=z.device, dtype=torch.float32)  # [|y - A x0|^2, |z0 - z_eff|^2]
@@ -135,8 +174,7 @@ class FusedPSLDStep:
                    "sp_residual_grad")
         _hip.check(lib.sp_sum_partials(_hip.ptr(partz), partz.numel(), norms[1:2].data_ptr(),
                                        stream), "sp_sum_partials")
-        if self._distributed():  # batch-global norms (psld.py:130,138): 8 bytes per step
-            dist.all_reduce(norms, group=self.group)
+        all_reduce_sum_(norms, self.group)  # batch-global norms (psld.py:130,138): 8 bytes
 
         go = torch.empty_like(d)  # d(gamma*G)/d z_eff = -gamma d / G
         _hip.check(lib.sp_scaled_combine(None, 0.0, _hip.ptr(d), -self.gamma, norms[1:2].data_ptr(),
@@ -144,15 +182,18 @@ class FusedPSLDStep:
         (u,) = torch.autograd.grad(z_eff, xer, grad_outputs=go)
         u = u.reshape(b, self.n).contiguous()
         ata_u = None
-        if self.blur:
+        if self.generic:
+            c_x0 = self._cotangent_generic(u, norms[0:1])
+        elif self.blur:
             au = torch.empty(b, self.m, device=z.device)
             _hip.check(lib.sp_op_apply(self.desc, _hip.ptr(u), _hip.ptr(au), b, stream), "apply")
             ata_u = torch.empty_like(u)
             _hip.check(lib.sp_op_adjoint(self.desc, _hip.ptr(au), _hip.ptr(ata_u), b, stream), "adj")
-        c_x0 = torch.empty_like(u)
-        _hip.check(lib.sp_psld_cotangent(self.desc, _hip.ptr(atr), _hip.ptr(u), _hip.ptr(ata_u),
-                                         norms[0:1].data_ptr(), self.omega, b, _hip.ptr(c_x0),
-                                         stream), "sp_psld_cotangent")
+        if not self.generic:
+            c_x0 = torch.empty_like(u)
+            _hip.check(lib.sp_psld_cotangent(self.desc, _hip.ptr(atr), _hip.ptr(u), _hip.ptr(ata_u),
+                                             norms[0:1].data_ptr(), self.omega, b, _hip.ptr(c_x0),
+                                             stream), "sp_psld_cotangent")
         (c_dec,) = torch.autograd.grad(x0, z0r, grad_outputs=c_x0.reshape(x0.shape))
         c = torch.empty_like(z0)
         _hip.check(lib.sp_scaled_combine(_hip.ptr(c_dec.contiguous()), 1.0, _hip.ptr(d), self.gamma,
@@ -169,7 +210,7 @@ class FusedPSLDStep:
         return z
 
     def predict_x0(self, z: Tensor, t: int) -> Tensor:
-        a, k = x0_coefficients(self.net.alphas_cumprod_host, t)
+        a, k = x0_coefficients(host_alphas_cumprod(self.net), t)
         with torch.no_grad():
             eps = self.net.forward(z, t).contiguous()
         out = torch.empty_like(z)
@@ -228,7 +269,7 @@ class PSLDSampler(PosteriorSampler, Generic[Condition_co]):
             seed = int(seed or 0)
             z = initial_sample(z_view.flat_shape, net.device, rng=rng, seed=seed,
                                sample_offset=sample_offset, noise_fn=noise_fn)
-            ts = net.timesteps_host
+            ts = host_timesteps(net)
             for i in range(len(ts) - 1, 1, -1):
                 xi = None
                 if noise_fn is not None:

@@ -18,10 +18,11 @@ between the priors is HIP:
 
 Losses and norms are batch-global (MSE mean / Frobenius norm over the whole
 flat batch, as in the reference); with a process group they are
-all-reduced (8 bytes) before use.  The pixel-space optimiser tests its stopping
-rule on the device; the latent-space one reads the loss on the host once per
-iteration where the reference calls ``.item()`` (``resample_kernels.py:81``) —
-each of its iterations is a decoder forward + VJP, so that sync costs < 0.1 %.
+all-reduced (8 bytes) before use.  Both optimisers test their stopping rules on
+the device (``sp_opt_check`` / ``sp_opt_check_plateau``) and the flag gates the
+AdamW update, where the reference calls ``.item()`` per iteration
+(``resample_kernels.py:50,81``).  Operators without a HIP descriptor take the
+same loops with ``A`` and its VJP from torch autograd (``_GenericConsistency``).
 """
 
 from __future__ import annotations
@@ -35,9 +36,10 @@ import torch.distributed as dist
 from torch import Tensor
 
 from samplers_amd import _hip
+from samplers_amd.distributed import all_reduce_sum_
 from samplers_amd.dtypes import Shape
 from samplers_amd.inverse_problem import InverseProblem
-from samplers_amd.networks.base import LatentEpsilonNetwork
+from samplers_amd.networks.base import LatentEpsilonNetwork, host_alphas_cumprod, host_timesteps
 from samplers_amd.noise import GaussianNoise
 from samplers_amd.samplers.base import PosteriorSampler
 from samplers_amd.samplers.dps import NoiseFn, draw_seed, initial_sample
@@ -78,8 +80,7 @@ class _Consistency:
     def _reduce(self, part: Tensor, out: Tensor, stream: int) -> None:
         _hip.check(self.lib.sp_sum_partials(_hip.ptr(part), part.numel(), out.data_ptr(), stream),
                    "sp_sum_partials")
-        if dist.is_initialized() and dist.get_world_size(self.group) > 1:
-            dist.all_reduce(out, group=self.group)
+        all_reduce_sum_(out, self.group)
 
     def residual(self, x: Tensor, scale: float) -> tuple[Tensor, Tensor]:
         """(g_y = scale * (y - A x), sum of squares (device scalar, global))."""
@@ -105,8 +106,13 @@ class _Consistency:
 
     def mse_grad(self, x: Tensor, total: int) -> tuple[Tensor, Tensor]:
         """(∂ MSE/∂x, MSE) with MSE = mean over all `total` observation elements."""
+        g, ss = self.mse_grad_ss(x, total)
+        return g, ss / total
+
+    def mse_grad_ss(self, x: Tensor, total: int) -> tuple[Tensor, Tensor]:
+        """(∂ MSE/∂x, global Σ r²)."""
         g, ss = self.residual(x, float(np.float32(-2.0 / total)))  # mse_loss backward: 2(y-Ax)/M
-        return self.adjoint(g, x), ss / total
+        return self.adjoint(g, x), ss
 
     def norm_grad(self, x: Tensor) -> Tensor:
         """∂ ||y - A x||_F / ∂x = -A^T r / ||r|| (0 at r = 0)."""
@@ -115,6 +121,59 @@ class _Consistency:
         _hip.check(self.lib.sp_scaled_combine(None, 0.0, _hip.ptr(g), -1.0, ss.data_ptr(), g.numel(),
                                               _hip.ptr(gs), _hip.stream_of(g)), "combine")
         return self.adjoint(gs, x)
+
+
+class _GenericConsistency(_Consistency):
+    """``_Consistency`` for operators without a HIP descriptor: ``A`` is the plugin's own
+    ``apply`` and its Jacobian-transpose products come from torch autograd on the device
+    (the reference's ``operator.apply`` inside ``MSELoss`` / ``linalg.norm``,
+    ``resample_kernels.py:15-93``); sums, norms and their all-reduce are the same device
+    scalars as on the HIP path."""
+
+    def __init__(self, operator, y_rows: Tensor, y_div: int, group=None) -> None:
+        self.lib = _hip.load_library()
+        self.op = operator
+        self.desc = None
+        self.y_div = int(y_div)
+        self.y = y_rows.to(torch.float32).reshape(-1, *operator.y_shape)
+        self.m, self.n = int(math.prod(operator.y_shape)), int(math.prod(operator.x_shape))
+        self.group = group
+
+    def residual_vjp(self, x: Tensor, scale: float) -> tuple[Tensor, Tensor]:
+        """(J_A(x)ᵀ(scale · r), Σ r² as a global device scalar) with r = y − A x."""
+        b = x.shape[0]
+        idx = torch.arange(b, device=x.device) // self.y_div
+        y = self.y.index_select(0, idx)
+        with torch.enable_grad():
+            xr = x.detach().reshape(b, *self.op.x_shape).requires_grad_(True)
+            r = y - self.op.apply(xr)
+            (g,) = torch.autograd.grad(r, xr, grad_outputs=r.detach() * (-scale))
+        ss = all_reduce_sum_(r.detach().float().square().sum().reshape(1), self.group)
+        return g.reshape(x.shape).to(torch.float32).contiguous(), ss
+
+    def mse_grad_ss(self, x: Tensor, total: int) -> tuple[Tensor, Tensor]:
+        return self.residual_vjp(x, float(np.float32(-2.0 / total)))
+
+    def norm_grad(self, x: Tensor) -> Tensor:
+        """−J_Aᵀ r / ‖r‖ (0 at r = 0)."""
+        g, ss = self.residual_vjp(x, 1.0)
+        out = torch.empty_like(g)
+        _hip.check(self.lib.sp_scaled_combine(None, 0.0, _hip.ptr(g), -1.0, ss.data_ptr(), g.numel(),
+                                              _hip.ptr(out), _hip.stream_of(g)), "combine")
+        return out
+
+
+def _is_gaussian(noise) -> bool:
+    """``isinstance(noise, GaussianNoise)`` (``resample.py:123``), also for a model derived
+    from the reference's own ``GaussianNoise`` (duck-typed plugins)."""
+    return isinstance(noise, GaussianNoise) or any(
+        c.__name__ == "GaussianNoise" for c in type(noise).__mro__)
+
+
+def make_consistency(operator, y_rows: Tensor, y_div: int, group=None) -> _Consistency:
+    if getattr(operator, "hip_descriptor", lambda: None)() is None:
+        return _GenericConsistency(operator, y_rows, y_div, group)
+    return _Consistency(operator, y_rows, y_div, group)
 
 
 class ReSampleSampler(PosteriorSampler, Generic[Condition_co]):
@@ -133,7 +192,7 @@ class ReSampleSampler(PosteriorSampler, Generic[Condition_co]):
                   seed: int, key: int, offset: int, *, want_x0: bool = False):
         """ε-form DDIM step (``bridge_kernels.py:82-115``) -> (z_prev, pseudo_x0[, x0])."""
         net, lib = self._epsilon_network, _hip.load_library()
-        c = eps_step_coefficients(net.alphas_cumprod_host, t, t_prev, eta)
+        c = eps_step_coefficients(host_alphas_cumprod(net), t, t_prev, eta)
         with torch.no_grad():
             e = net.predict_noise(z, t).contiguous()
         zp, pseudo = torch.empty_like(z), torch.empty_like(z)
@@ -164,13 +223,6 @@ class ReSampleSampler(PosteriorSampler, Generic[Condition_co]):
                                               _hip.stream_of(out)), "combine")
         return out
 
-    def _adamw(self, param: Tensor, grad: Tensor, state: dict, lr: float) -> None:
-        state["step"] += 1
-        c = adamw_coefficients(state["step"], lr)
-        _hip.check(_hip.load_library().sp_adamw_step(
-            _hip.ptr(param), _hip.ptr(grad.contiguous()), _hip.ptr(state["m"]), _hip.ptr(state["v"]),
-            param.numel(), c, _hip.stream_of(param)), "sp_adamw_step")
-
     def _pixel_optimization(self, x0: Tensor, cons: _Consistency, total: int, eps: float,
                             max_iters: int, check_every: int = 16) -> Tensor:
         """``resample_kernels.py:32-54``: AdamW(lr=1e-2) on x, MSE, stop below eps^2.
@@ -189,7 +241,8 @@ class ReSampleSampler(PosteriorSampler, Generic[Condition_co]):
         stream = _hip.stream_of(x)
         gs = float(np.float32(-2.0 / total))  # mse_loss backward w.r.t. A x: 2 (Ax - y) / M
         tot, thr = float(np.float32(total)), float(eps) ** 2
-        fused = int(cons.desc.kind) != _hip.SP_OP_BLUR
+        generic = cons.desc is None
+        fused = not generic and int(cons.desc.kind) != _hip.SP_OP_BLUR
         shared = dist.is_initialized() and dist.get_world_size(cons.group) > 1
         part = torch.empty(b, int(lib.sp_rsq_partials(cons.desc)), device=x.device) if fused else None
         ss = torch.empty(1, device=x.device)
@@ -203,9 +256,12 @@ class ReSampleSampler(PosteriorSampler, Generic[Condition_co]):
                 if shared:
                     cons._reduce(part, ss, stream)
                 parts, count = (ss, 1) if shared else (part, part.numel())
-            else:  # BLUR: A, residual, A^T composed; the update skips once stopped
-                g, ss = cons.residual(x, gs)
-                grad = cons.adjoint(g, x)
+            else:  # BLUR / generic: A, residual, A^T composed; the update skips once stopped
+                if generic:
+                    grad, ss = cons.residual_vjp(x, gs)
+                else:
+                    g, ss = cons.residual(x, gs)
+                    grad = cons.adjoint(g, x)
                 _hip.check(lib.sp_adamw_step_until(_hip.ptr(x), _hip.ptr(grad), _hip.ptr(m_),
                                                    _hip.ptr(v_), x.numel(), c, _hip.ptr(stop),
                                                    stream), "sp_adamw_step_until")
@@ -217,28 +273,46 @@ class ReSampleSampler(PosteriorSampler, Generic[Condition_co]):
         return x
 
     def _latent_optimization(self, z0: Tensor, cons: _Consistency, total: int, eps: float,
-                             max_iters: int) -> Tensor:
-        """``resample_kernels.py:57-93``: AdamW(lr=5e-3) on z through the decoder."""
-        net = self._epsilon_network
+                             max_iters: int, plateau_from: int = 200) -> Tensor:
+        """``resample_kernels.py:57-93``: AdamW(lr=5e-3) on z through the decoder.
+
+        The stopping rule (loss below eps², or, from iteration 200 on, a loss above the
+        previous iteration's) is evaluated on the device (``sp_opt_check_plateau``) and gates
+        the AdamW update (``sp_adamw_step_until``), so the iterate is the reference's
+        whatever the host does.  The host reads the flag one iteration late through pinned
+        memory: iteration i + 1 is already queued when it waits for iteration i's flag, so
+        the GPU queue never drains (the reference's ``.item()`` per iteration stalls it), at
+        the price of one decoder forward + VJP past the stop whose update is a no-op."""
+        net, lib = self._epsilon_network, cons.lib
         z = z0.detach().clone().contiguous()
-        st = {"step": 0, "m": torch.zeros_like(z), "v": torch.zeros_like(z)}
-        losses: list[float] = []
+        m_, v_ = torch.zeros_like(z), torch.zeros_like(z)
+        stop = torch.zeros(1, dtype=torch.int32, device=z.device)
+        prev = torch.zeros(1, dtype=torch.float32, device=z.device)
+        flags = torch.zeros(2, dtype=torch.int32, pin_memory=True)
+        events = [torch.cuda.Event(), torch.cuda.Event()]
+        stream = _hip.stream_of(z)
+        tot, thr = float(np.float32(total)), float(eps) ** 2
         for itr in range(max_iters):
             with torch.enable_grad():
                 zr = z.detach().requires_grad_(True)
                 x = net.decode(zr, differentiable=True)
-            gx, loss = cons.mse_grad(x.detach(), total)
+            gx, ss = cons.mse_grad_ss(x.detach(), total)
             (gz,) = torch.autograd.grad(x, zr, grad_outputs=gx.reshape(x.shape))
-            self._adamw(z, gz, st, 5e-3)
-            cur = loss.item()
-            if itr >= 200:
-                losses.append(cur)
-                if len(losses) > 1 and losses[0] < cur:
+            del x, zr
+            c = adamw_coefficients(itr + 1, 5e-3)
+            _hip.check(lib.sp_adamw_step_until(_hip.ptr(z), _hip.ptr(gz.contiguous()), _hip.ptr(m_),
+                                               _hip.ptr(v_), z.numel(), c, _hip.ptr(stop), stream),
+                       "sp_adamw_step_until")
+            _hip.check(lib.sp_opt_check_plateau(_hip.ptr(ss), 1, tot, thr, itr, plateau_from,
+                                                _hip.ptr(prev), _hip.ptr(stop), None, stream),
+                       "sp_opt_check_plateau")
+            slot = itr & 1
+            flags[slot:slot + 1].copy_(stop, non_blocking=True)
+            events[slot].record()
+            if itr >= 1:
+                events[slot ^ 1].synchronize()
+                if int(flags[slot ^ 1]):
                     break
-                if len(losses) > 1:
-                    losses.pop(0)
-            if cur < eps**2:
-                break
         return z
 
     def _resample(self, z_opt: Tensor, snapshot: Tensor, a_prev: float, sigma: float,
@@ -288,7 +362,7 @@ class ReSampleSampler(PosteriorSampler, Generic[Condition_co]):
             obs = inverse_problem.observation
             _hip.require_cuda(obs, "ReSampleSampler")
             y_rows = obs.reshape(max(x_view.batch_size, 1), -1)
-            cons = _Consistency(inverse_problem.operator, y_rows, num_reconstructions, group)
+            cons = make_consistency(inverse_problem.operator, y_rows, num_reconstructions, group)
             total = z_view.leading_size * cons.m  # MSELoss mean over the tiled observation
             if dist.is_initialized() and dist.get_world_size(group) > 1:
                 t = torch.tensor([float(total)], device=obs.device, dtype=torch.float64)
@@ -309,10 +383,10 @@ class ReSampleSampler(PosteriorSampler, Generic[Condition_co]):
 
             z = initial_sample(z_view.flat_shape, net.device, rng=rng, seed=seed,
                                sample_offset=off, noise_fn=noise_fn)
-            eps = float(inverse_problem.noise.sigma.item()) \
-                if isinstance(inverse_problem.noise, GaussianNoise) else 1e-3
-            ts = net.timesteps_host
-            acp = net.alphas_cumprod_host
+            eps = float(inverse_problem.noise.sigma.item()) if _is_gaussian(inverse_problem.noise) \
+                else 1e-3
+            ts = host_timesteps(net)
+            acp = host_alphas_cumprod(net)
             total_steps = len(ts) - 1
             index_split = total_steps // stage_splits
             for idx in range(len(ts) - 1, 1, -1):

@@ -19,7 +19,7 @@ import numpy as np
 import torch
 from torch import Tensor
 
-from samplers_amd.networks.base import EpsilonNetwork
+from samplers_amd.networks.base import EpsilonNetwork, host_alphas_cumprod, host_timesteps
 
 
 @dataclass(frozen=True)
@@ -60,7 +60,7 @@ def x0_coefficients(acp: np.ndarray, t: int) -> tuple[float, float]:
 
 def compute_bridge_kernel_statistics(x_ell: Tensor, x_s: Tensor, epsilon_net: EpsilonNetwork,
                                      ell: int, t: int, s: int, eta: float = 1.0) -> BridgeStatistics:
-    c = bridge_coefficients(epsilon_net.alphas_cumprod_host, ell, t, s, eta)
+    c = bridge_coefficients(host_alphas_cumprod(epsilon_net), ell, t, s, eta)
     mean = c.c_ell * x_ell + c.c_s * x_s
     return BridgeStatistics(mean=mean, std=torch.tensor(c.std, dtype=x_ell.dtype, device=x_ell.device))
 
@@ -74,7 +74,7 @@ def sample_bridge_kernel(x_ell: Tensor, x_s: Tensor, epsilon_net: EpsilonNetwork
 def ddim_step(x: Tensor, epsilon_net: EpsilonNetwork, t: int, t_prev: int, eta: float,
               e_t: Tensor | None = None) -> Tensor:
     """DDIM step in the x0 ("bridge") parameterisation (``bridge_kernels.py:62-75``)."""
-    t_0 = epsilon_net.timesteps_host[0]
+    t_0 = host_timesteps(epsilon_net)[0]
     if e_t is None:
         e_t = epsilon_net.predict_x0(x, t)
     return sample_bridge_kernel(x_ell=x, x_s=e_t, epsilon_net=epsilon_net, ell=t, t=t_prev, s=t_0,
@@ -102,7 +102,7 @@ def eps_step_coefficients(acp: np.ndarray, t: int, t_prev: int, eta: float) -> d
 def ddim_step_eps(x: Tensor, *, epsilon_net: EpsilonNetwork, t: int, t_prev: int,
                   eta: float) -> tuple[Tensor, Tensor, Tensor]:
     """ε-form DDIM step returning (x_prev, x0, pseudo-x0) (``bridge_kernels.py:82-115``)."""
-    c = eps_step_coefficients(epsilon_net.alphas_cumprod_host, t, t_prev, eta)
+    c = eps_step_coefficients(host_alphas_cumprod(epsilon_net), t, t_prev, eta)
     with torch.no_grad():
         e_t = epsilon_net.predict_noise(x, t)
     pred_x0 = (x - c["sqrt_oma"] * e_t) / c["sqrt_a"]

@@ -189,3 +189,122 @@ def relative_error(a: torch.Tensor, b: torch.Tensor) -> float:
 
 def count(shape) -> int:
     return int(math.prod(shape))
+
+
+# --- plugins written against the reference ABCs (no HIP descriptor, no grad_scale) -------
+
+def make_reference_style_net(kind: str, channels: int, coef: float = 0.1, device=None,
+                             latent: bool = False):
+    """A network subclass written the way the reference's own adapters are
+    (``/root/reference/samplers/networks/diffusers/ddpm.py:45-58``): it registers the
+    ``timesteps`` buffer itself and knows nothing of ``timesteps_host``."""
+    from samplers_amd.networks.base import EpsilonNetwork, LatentEpsilonNetwork
+
+    base = LatentEpsilonNetwork if latent else EpsilonNetwork
+
+    class RefStyle(base):
+        def __init__(self):
+            acp = ddpm_alphas_cumprod()
+            super().__init__(alphas_cumprod=torch.cat([acp.new_tensor([1.0]), acp]))
+            self.core = EpsCore(kind, 4 if latent else channels, coef)
+            if latent:
+                self.vae = LatentCore()
+
+        def forward(self, x, t):
+            return self.core(x, t)
+
+        @classmethod
+        def from_pretrained(cls, *a, **k):
+            raise NotImplementedError
+
+        def set_sampling_parameters(self, num_sampling_steps, batch_size=1, num_reconstructions=1):
+            self._batch_size = batch_size
+            self._num_sampling_steps = num_sampling_steps
+            self.register_buffer("timesteps",
+                                 leading_timesteps_ascending(num_sampling_steps).to(self.device))
+
+        def get_latent_shape(self, x_shape):
+            return self.vae.latent_shape(x_shape)
+
+        def _decode(self, z, *, differentiable=False):
+            return self.vae.decode(z)
+
+        def _encode(self, x, *, differentiable=False):
+            return self.vae.encode(x)
+
+        @property
+        def is_condition_initialized(self):
+            return True
+
+    net = RefStyle()
+    return net.to(device) if device is not None else net
+
+
+def torch_operator(shape, kept=None, device=None):
+    """An ``Operator`` subclass in plain torch (no ``hip_descriptor``): identity, or the
+    reference's flattened inpainting gather (``inpainting.py:49-53,132-187``)."""
+    from samplers_amd.operators.base import Operator
+
+    class TorchGather(Operator):
+        def __init__(self):
+            idx = None if kept is None else torch.as_tensor(kept).long()
+            self.kept = idx  # plain attribute while Operator.__init__ infers y_shape
+            Operator.__init__(self, shape)
+            del self.__dict__["kept"]
+            self.register_buffer("kept", idx)  # a buffer afterwards: moves with .to()
+
+        def apply(self, x):
+            lead = x.shape[: x.ndim - len(shape)]
+            flat = x.reshape(*lead, -1)
+            return x.clone() if self.kept is None else flat[..., self.kept]
+
+        def apply_transpose(self, y):
+            if self.kept is None:
+                return y.clone()
+            lead = y.shape[:-1]
+            out = y.new_zeros(*lead, count(shape))
+            out[..., self.kept] = y
+            return out.reshape(*lead, *shape)
+
+        def apply_pseudo_inverse(self, y):
+            return self.apply_transpose(y)
+
+    op = TorchGather()
+    return op.to(device) if device is not None else op
+
+
+def reference_style_gaussian(sigma: float):
+    """A noise model defining only the reference ABC's abstract methods (``noise.py:13-79``)."""
+    from samplers_amd.noise import NoiseModel
+
+    class RefGauss(NoiseModel):
+        def __init__(self):
+            super().__init__()
+            self.register_buffer("sigma", torch.tensor(float(sigma)))
+
+        def log_prob(self, r):
+            return -(r.square().sum(dim=tuple(range(1, r.ndim)))) / (2 * self.sigma.pow(2))
+
+        def sample(self, shape, *, device=None, dtype=None, generator=None):
+            return torch.randn(shape, generator=generator) * self.sigma
+
+    return RefGauss()
+
+
+def laplace_noise(scale: float):
+    """A non-quadratic log-likelihood (smooth L1 / pseudo-Huber): no constant gradient
+    factor, so the samplers must differentiate it by autograd."""
+    from samplers_amd.noise import NoiseModel
+
+    class PseudoHuber(NoiseModel):
+        def __init__(self):
+            super().__init__()
+            self.register_buffer("scale", torch.tensor(float(scale)))
+
+        def log_prob(self, r):
+            return -(torch.sqrt(1 + (r / self.scale).square()) - 1).sum(dim=tuple(range(1, r.ndim)))
+
+        def sample(self, shape, *, device=None, dtype=None, generator=None):
+            return torch.zeros(shape)
+
+    return PseudoHuber()

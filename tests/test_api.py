@@ -209,3 +209,91 @@ def test_hip_path_refuses_host_tensors():
     with pytest.raises(HipLibraryError):
         DPSSampler(net)(ip, num_sampling_steps=4)
     assert not net.are_sampling_parameters_initialized  # state cleared on error
+
+
+# --- the drop-in boundary for reference-style plugins (no GPU needed) ---------------------
+
+def test_grad_scale_probe_for_reference_style_noise():
+    import stand_ins as si
+
+    from samplers_amd.noise import GaussianNoise, PoissonNoise, probe_grad_scale
+
+    assert si.reference_style_gaussian(0.05).grad_scale() == GaussianNoise(0.05).grad_scale()
+    assert probe_grad_scale(PoissonNoise(1.0)) == pytest.approx(PoissonNoise(1.0).grad_scale(),
+                                                                rel=1e-6)
+    assert si.laplace_noise(0.1).grad_scale() is None  # not c * r: generic path
+
+
+def test_reference_style_noise_is_instantiable():
+    """grad_scale is not abstract: a subclass of the reference ABC's shape instantiates."""
+    import stand_ins as si
+
+    noise = si.reference_style_gaussian(0.1)
+    assert noise.log_prob(torch.ones(2, 3)).shape == (2,)
+
+
+def test_timesteps_host_follows_a_directly_registered_buffer():
+    import stand_ins as si
+
+    net = si.make_reference_style_net("linear", 3)
+    assert net.timesteps_host is None
+    net.set_sampling_parameters(5)
+    assert net.timesteps_host == [0, 200, 400, 600, 800]
+    net.set_sampling_parameters(4)  # a new buffer: a new host copy
+    assert net.timesteps_host == [0, 250, 500, 750]
+
+
+def test_skip_grad_take_without_delivery_returns_none():
+    from samplers_amd.networks.layers import SkipGrad
+
+    box = SkipGrad()
+    assert box.take() is None
+    box.grad = torch.ones(2)
+    assert torch.equal(box.take(), torch.ones(2)) and box.grad is None
+
+
+def test_resnet_block_rejects_box_in_with_skip():
+    from samplers_amd.networks.layers import SkipGrad
+    from samplers_amd.networks.unet2d import ResnetBlock2D
+
+    blk = ResnetBlock2D(64, 32, None, 32, 1e-6)
+    with pytest.raises(ValueError, match="exclusive"):
+        blk(torch.zeros(1, 32, 8, 8), skip=torch.zeros(1, 32, 8, 8), box_in=SkipGrad())
+
+
+def test_torch_operator_stand_in_matches_native_inpainting_on_cpu():
+    import stand_ins as si
+
+    from samplers_amd.operators import InpaintingOperator
+
+    shape = (3, 8, 8)
+    mask = si.fixture_mask(shape, "random")
+    native = InpaintingOperator(shape, mask)
+    plain = si.torch_operator(shape, native._kept_indices)
+    x = torch.randn(2, *shape)
+    assert plain.y_shape == native.y_shape
+    assert torch.equal(plain.apply(x), native.apply(x))
+    assert torch.equal(plain.apply_transpose(plain.apply(x)), native.apply_transpose(native.apply(x)))
+
+
+@pytest.mark.parametrize("name", sorted(p.stem for p in __import__("pathlib").Path(
+    __file__).resolve().parent.joinpath("golden").glob("*.npz")))
+def test_from_clean_data_reproduces_golden_observation(name):
+    """A15: ``InverseProblem.from_clean_data`` (``inverse_problem.py:34-67``) with the golden
+    generator's inputs (x_true seed 0, noise generator seed 7) gives the reference's y
+    bit for bit (tests/golden/make_golden.py: build_problem)."""
+    import stand_ins as si
+    from golden_cases import load_dps_case
+
+    case = load_dps_case(name)
+    m = case.meta
+    bs = m["batch_shape"]
+    x_true = si.fixture_x_true(int(np.prod(bs)) if bs else 1, case.shape, 0)
+    x_true = x_true.reshape(*bs, *case.shape)
+    op = (IdentityOperator(case.shape) if case.kept is None
+          else InpaintingOperator(case.shape, case.mask))
+    noise = PoissonNoise(1.0) if m["noise"] == "poisson" else GaussianNoise(0.05)
+    prob = InverseProblem.from_clean_data(x_true, operator=op, noise=noise,
+                                          rng=torch.Generator().manual_seed(7))
+    assert prob.observation.dtype == case.y.dtype
+    assert torch.equal(prob.observation, case.y)

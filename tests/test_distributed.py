@@ -84,3 +84,66 @@ def test_shard_bounds_cover_exactly():
 def test_gather_single_rank_is_identity():
     t = torch.randn(3, 2)
     assert gather_shards(t, [3]) is t
+
+
+# --- batch-coupled samplers: PSLD / ReSample global norms over ranks -------
+
+def _norm_worker(rank, world, port, result_path):
+    """Each rank holds a contiguous shard of a batch of 5 and computes the samplers' global
+    quantities with the production code (the generic-operator terms, which are plain torch
+    and so run on CPU): PSLD's ‖y − A x̂₀‖² (``generic_pixel_terms`` + ``all_reduce_sum_``),
+    ReSample's MSE sum of squares and its gradient (``_GenericConsistency``)."""
+    import stand_ins as si
+
+    from samplers_amd.distributed import all_reduce_sum_
+    from samplers_amd.samplers.psld import generic_pixel_terms
+    from samplers_amd.samplers.resample import _GenericConsistency
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        out = _norm_terms(si, generic_pixel_terms, _GenericConsistency, all_reduce_sum_,
+                          rank, world)
+        if rank == 0:
+            torch.save(out, result_path)
+    finally:
+        dist.destroy_process_group()
+
+
+def _norm_terms(si, generic_pixel_terms, consistency, reduce, rank, world):
+    shape, batch, R = (3, 8, 8), 5, 2
+    op = si.torch_operator(shape, torch.arange(0, 192, 3))
+    gen = torch.Generator().manual_seed(4)
+    y = torch.randn(batch, *op.y_shape, generator=gen)
+    x0 = torch.randn(batch * R, *shape, generator=gen)
+    hty = op.apply_transpose(y).reshape(batch, -1)
+    start, stop = shard_bounds(batch, rank, world)
+    ys, hs, xs = y[start:stop], hty[start:stop], x0[start * R:stop * R]
+    x_eff, ss, _ = generic_pixel_terms(op, ys.reshape(stop - start, -1), hs, R, xs)
+    ss = reduce(ss)
+    total = batch * R * op.y_shape[0]
+    cons = consistency(op, ys.reshape(stop - start, -1), R)
+    g, ss2 = cons.mse_grad_ss(xs, total)
+    full_g = torch.zeros(batch * R, *shape)
+    full_g[start * R:stop * R] = g
+    reduce(full_g)  # disjoint rows: the sum assembles the full gradient
+    return {"psld_ss": ss, "rs_ss": ss2, "rs_grad": full_g, "x_eff_rows": (start * R, x_eff)}
+
+
+def test_batch_global_norms_match_single_process(tmp_path):
+    import stand_ins as si
+
+    from samplers_amd.distributed import all_reduce_sum_
+    from samplers_amd.samplers.psld import generic_pixel_terms
+    from samplers_amd.samplers.resample import _GenericConsistency
+
+    path = tmp_path / "norms.pt"
+    mp.spawn(_norm_worker, args=(2, _free_port(), str(path)), nprocs=2, join=True)
+    sharded = torch.load(path, weights_only=True)
+    single = _norm_terms(si, generic_pixel_terms, _GenericConsistency, all_reduce_sum_, 0, 1)
+    # sums of squares: the same terms in a different association order
+    assert torch.allclose(sharded["psld_ss"], single["psld_ss"], rtol=1e-6)
+    assert torch.allclose(sharded["rs_ss"], single["rs_ss"], rtol=1e-6)
+    assert torch.equal(sharded["rs_grad"], single["rs_grad"])  # per-sample: bit-identical
+    r0, xe = sharded["x_eff_rows"]
+    assert torch.equal(xe, single["x_eff_rows"][1][r0:r0 + xe.shape[0]])

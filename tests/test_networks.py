@@ -46,3 +46,52 @@ def test_tiny_unet_shapes_and_determinism():
     ya = a(x, 10)
     assert ya.shape == x.shape
     torch.testing.assert_close(ya, b(x, torch.tensor([10])))
+
+
+def test_from_pretrained_loads_a_local_diffusers_layout_checkpoint(tmp_path):
+    """f4: ``DDPMNetwork.from_pretrained(local_dir)`` (the reference loads by hub name,
+    ``ddpm.py:22-38``): a safetensors state dict with diffusers key names — including the
+    legacy attention names query/key/value/proj_attn — plus unet/config.json and
+    scheduler/scheduler_config.json round-trip to the same module and outputs."""
+    import json
+
+    from safetensors.torch import save_file
+
+    from samplers_amd.networks.ddpm import DDPMNetwork
+    from samplers_amd.networks.unet2d import UNet2DConfig, build_unet
+
+    cfg = UNet2DConfig(sample_size=16, block_out_channels=(32, 64), attention_levels=(1,),
+                       layers_per_block=1)
+    src = build_unet(cfg, seed=3)
+    state = {}
+    for k, v in src.state_dict().items():
+        k = (k.replace(".to_q.", ".query.").replace(".to_k.", ".key.")
+             .replace(".to_v.", ".value.").replace(".to_out.0.", ".proj_attn."))
+        state[k] = v.contiguous()
+    (tmp_path / "unet").mkdir()
+    (tmp_path / "scheduler").mkdir()
+    save_file(state, str(tmp_path / "unet" / "diffusion_pytorch_model.safetensors"))
+    (tmp_path / "unet" / "config.json").write_text(json.dumps({
+        "sample_size": 16, "in_channels": 3, "out_channels": 3, "block_out_channels": [32, 64],
+        "down_block_types": ["DownBlock2D", "AttnDownBlock2D"], "layers_per_block": 1,
+        "norm_num_groups": 32, "norm_eps": 1e-6, "freq_shift": 1, "flip_sin_to_cos": False}))
+    (tmp_path / "scheduler" / "scheduler_config.json").write_text(json.dumps({
+        "num_train_timesteps": 1000, "beta_start": 1e-4, "beta_end": 0.02,
+        "beta_schedule": "linear"}))
+    net = DDPMNetwork.from_pretrained(str(tmp_path))
+    for (ka, a), (kb, b) in zip(src.state_dict().items(), net.unet.state_dict().items()):
+        assert ka == kb and torch.equal(a, b)
+    net.set_sampling_parameters(10)
+    x = torch.randn(2, 3, 16, 16, generator=torch.Generator().manual_seed(0))
+    with torch.no_grad():
+        assert torch.equal(net(x, 500), src(x, 500))
+    assert torch.allclose(net.alphas_cumprod[1:], torch.cumprod(1 - torch.linspace(1e-4, 0.02, 1000), 0).clip(1e-6, 1))
+
+
+def test_from_pretrained_never_fetches(tmp_path):
+    import pytest
+
+    from samplers_amd.networks.ddpm import DDPMNetwork
+
+    with pytest.raises(FileNotFoundError, match="never fetches"):
+        DDPMNetwork.from_pretrained("google/ddpm-celebahq-256", cache_dir=str(tmp_path))

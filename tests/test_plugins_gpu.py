@@ -1,0 +1,186 @@
+"""Reference-style plugins on the GPU: the drop-in boundary.
+
+A user of the reference writes plugins against its ABCs
+(``/root/reference/samplers/operators/base.py``, ``noise.py:13-45``,
+``networks/base.py:13-111``): operators with only ``apply`` (and optionally
+``apply_transpose`` / ``apply_pseudo_inverse``) in plain torch, noise models with
+only ``log_prob`` / ``sample``, networks that register ``timesteps`` themselves.
+Such plugins run here too: native plugins take the fused HIP passes, the others the
+generic path (the residual cotangent by autograd through the plugin, the bridge +
+guidance update still in HIP pass 2).  Every case is checked against the reference's
+golden vectors (the same tolerance as tests/test_dps_gpu.py and test_latent_gpu.py) or,
+where the reference has no such case, against the oracle loop.
+"""
+
+import pytest
+import torch
+
+import stand_ins as si
+from golden_cases import dps_case_names, load_dps_case
+from oracle import dps_loop
+from samplers_amd.inverse_problem import InverseProblem
+from samplers_amd.noise import GaussianNoise, PoissonNoise
+from samplers_amd.operators import IdentityOperator, InpaintingOperator
+from samplers_amd.samplers import DPSSampler
+from samplers_amd.samplers.dps import FusedDPSStep, GenericDPSStep, make_dps_step
+from samplers_amd.samplers.pgdm import PGDMSampler
+from samplers_amd.samplers.psld import PSLDSampler
+from samplers_amd.samplers.resample import ReSampleSampler
+from test_latent_gpu import _tol
+from test_oracle_latent import oracle_pgdm, oracle_psld, oracle_resample
+
+pytestmark = pytest.mark.gpu
+
+TOL = 1e-5
+
+
+def _noise_fn(case, device):
+    init, steps = case.noise()
+    return lambda kind, i, s: (init if kind == "init" else steps[i]).to(device)
+
+
+def _torch_op(case, device):
+    return si.torch_operator(case.shape, None if case.kept is None else case.kept, device=device)
+
+
+def _native_op(case, device):
+    return (IdentityOperator(case.shape) if case.kept is None
+            else InpaintingOperator(case.shape, case.mask).to(device))
+
+
+def _ref_noise(case, device):
+    if case.meta["noise"] == "gauss":
+        return si.reference_style_gaussian(0.05).to(device)
+    return PoissonNoise(1.0).to(device)
+
+
+@pytest.mark.parametrize("name", dps_case_names())
+def test_dps_reference_style_network_fused_path(cuda, name):
+    """A network that registers ``timesteps`` itself (``ddpm.py:58``) drives the fused path."""
+    case = load_dps_case(name)
+    m = case.meta
+    net = si.make_reference_style_net(m["prior"], case.shape[0], m["coef"], device=cuda)
+    noise = GaussianNoise(0.05) if m["noise"] == "gauss" else PoissonNoise(1.0)
+    prob = InverseProblem(_native_op(case, cuda), case.y.to(cuda), noise.to(cuda))
+    out = DPSSampler(net)(prob, num_sampling_steps=m["N"], num_reconstructions=m["R"],
+                          gamma=m["gamma"], eta=m["eta"], noise_fn=_noise_fn(case, cuda))
+    assert si.relative_error(out.cpu(), case.out) < TOL
+
+
+@pytest.mark.parametrize("name", dps_case_names())
+def test_dps_generic_plugins_match_golden(cuda, name):
+    """Plain-torch operator + reference-style noise model: the generic DPS step."""
+    case = load_dps_case(name)
+    m = case.meta
+    net = si.make_reference_style_net(m["prior"], case.shape[0], m["coef"], device=cuda)
+    prob = InverseProblem(_torch_op(case, cuda), case.y.to(cuda), _ref_noise(case, cuda))
+    step = make_dps_step(net, prob, case.y.to(cuda).reshape(-1, *prob.operator.y_shape), m["R"])
+    assert isinstance(step, GenericDPSStep)
+    out = DPSSampler(net)(prob, num_sampling_steps=m["N"], num_reconstructions=m["R"],
+                          gamma=m["gamma"], eta=m["eta"], noise_fn=_noise_fn(case, cuda))
+    assert tuple(out.shape) == tuple(m["out_shape"])
+    assert si.relative_error(out.cpu(), case.out) < TOL
+
+
+def test_dps_non_quadratic_noise_takes_autograd_cotangent(cuda):
+    """A native operator with a noise model whose gradient is not c·r (pseudo-Huber): the
+    cotangent comes from autograd of ``log_prob`` through the HIP operator; pinned by the
+    oracle loop (``dps.py:91-122`` restated) with the same log-likelihood."""
+    case = load_dps_case("dps_rnd_gauss_conv_b4")
+    m = case.meta
+    noise = si.laplace_noise(0.1)
+    net = si.make_samplers_amd_net(m["prior"], case.shape[0], m["coef"], device=cuda)
+    prob = InverseProblem(_native_op(case, cuda), case.y.to(cuda), noise.to(cuda))
+    rows = case.y.to(cuda).reshape(-1, *prob.operator.y_shape)
+    assert isinstance(make_dps_step(net, prob, rows, 1), GenericDPSStep)
+    init, steps = case.noise()
+    out = DPSSampler(net)(prob, num_sampling_steps=m["N"], gamma=m["gamma"], eta=m["eta"],
+                          noise_fn=_noise_fn(case, cuda))
+    core = si.EpsCore(m["prior"], case.shape[0], m["coef"])
+    acp = torch.cat([torch.ones(1), si.ddpm_alphas_cumprod()]).clip(1e-6, 1)
+    kept = torch.as_tensor(case.kept).long()
+    ref = dps_loop.dps_reference(lambda x, t: core(x, t), acp,
+                                 si.leading_timesteps_ascending(m["N"]).tolist(),
+                                 lambda x: x.reshape(x.shape[0], -1)[:, kept],
+                                 si.laplace_noise(0.1).log_prob,
+                                 case.y, init, lambda i: steps[i], gamma=m["gamma"], eta=m["eta"])
+    assert si.relative_error(out.cpu(), ref) < 1e-4
+
+
+def test_fused_path_selected_for_native_plugins(cuda):
+    case = load_dps_case("dps_rnd_gauss_lin_b4")
+    net = si.make_samplers_amd_net("linear", 3, 0.3, device=cuda)
+    prob = InverseProblem(_native_op(case, cuda), case.y.to(cuda), GaussianNoise(0.05).to(cuda))
+    step = make_dps_step(net, prob, case.y.to(cuda), 1)
+    assert type(step) is FusedDPSStep
+    # a reference-style Gaussian (no grad_scale override) is probed: fused as well
+    prob2 = InverseProblem(prob.operator, prob.observation, si.reference_style_gaussian(0.05).to(cuda))
+    assert type(make_dps_step(net, prob2, case.y.to(cuda), 1)) is FusedDPSStep
+
+
+def test_graph_mode_refuses_generic_plugins(cuda):
+    case = load_dps_case("dps_id_gauss_lin_b1")
+    net = si.make_samplers_amd_net("linear", 3, 0.1, device=cuda)
+    prob = InverseProblem(_torch_op(case, cuda), case.y.to(cuda), GaussianNoise(0.05).to(cuda))
+    with pytest.raises(ValueError, match="natively implemented"):
+        DPSSampler(net)(prob, num_sampling_steps=5, graph=True, seed=1)
+
+
+@pytest.mark.parametrize("name", dps_case_names("pgdm"))
+def test_pgdm_generic_operator_matches_golden(cuda, name):
+    case = load_dps_case(name)
+    m = case.meta
+    net = si.make_reference_style_net(m["prior"], case.shape[0], m["coef"], device=cuda)
+    prob = InverseProblem(_torch_op(case, cuda), case.y.to(cuda), GaussianNoise(0.05).to(cuda))
+    out = PGDMSampler(net)(prob, num_sampling_steps=m["N"], num_reconstructions=m["R"],
+                           guidance_weight=m["guidance_weight"], eta=m["eta"],
+                           noise_fn=_noise_fn(case, cuda))
+    assert si.relative_error(out.cpu(), case.out) < _tol(case, oracle_pgdm)
+
+
+@pytest.mark.parametrize("name", dps_case_names("psld"))
+def test_psld_generic_operator_matches_golden(cuda, name):
+    case = load_dps_case(name)
+    m = case.meta
+    net = si.make_reference_style_net(m["prior"], 3, m["coef"], device=cuda, latent=True)
+    prob = InverseProblem(_torch_op(case, cuda), case.y.to(cuda), GaussianNoise(0.05).to(cuda))
+    out = PSLDSampler(net)(prob, num_sampling_steps=m["N"], num_reconstructions=m["R"],
+                           gamma=m["gamma"], omega=m["omega"], eta=m["eta"],
+                           noise_fn=_noise_fn(case, cuda))
+    assert tuple(out.shape) == tuple(m["out_shape"])
+    assert si.relative_error(out.cpu(), case.out) < _tol(case, oracle_psld)
+
+
+@pytest.mark.parametrize("name", dps_case_names("rs"))
+def test_resample_generic_operator_matches_golden(cuda, name):
+    case = load_dps_case(name)
+    m = case.meta
+    noise = PoissonNoise(1.0) if m["noise"] == "poisson" else si.reference_style_gaussian(1e-3)
+    prob = InverseProblem(_torch_op(case, cuda), case.y.to(cuda), noise.to(cuda))
+    gen = torch.Generator().manual_seed(m["seed"])
+    net = si.make_reference_style_net("conv", 3, 0.1, device=cuda, latent=True)
+    out = ReSampleSampler(net)(prob, num_sampling_steps=m["N"], num_reconstructions=m["R"],
+                               max_optimization_iters=m["max_iters"], eta=m["eta"],
+                               inter_timesteps=m["inter_timesteps"],
+                               time_travel_interval=m["time_travel_interval"],
+                               stage_splits=m["stage_splits"],
+                               noise_fn=lambda k, key, s: torch.randn(s, generator=gen).to(cuda))
+    assert si.relative_error(out.cpu(), case.out) < _tol(case, oracle_resample)
+
+
+@pytest.mark.parametrize("name", dps_case_names("dps"))
+def test_from_clean_data_on_device_reproduces_golden_observation(cuda, name):
+    """A15 on the device: HIP operator (gather / identity) + the noise drawn from the same CPU
+    generator as the reference's run give its y bit for bit."""
+    import numpy as np
+
+    case = load_dps_case(name)
+    m = case.meta
+    bs = m["batch_shape"]
+    x_true = si.fixture_x_true(int(np.prod(bs)) if bs else 1, case.shape, 0)
+    x_true = x_true.reshape(*bs, *case.shape).to(cuda)
+    noise = PoissonNoise(1.0) if m["noise"] == "poisson" else GaussianNoise(0.05)
+    prob = InverseProblem.from_clean_data(x_true, operator=_native_op(case, cuda),
+                                          noise=noise.to(cuda), rng=torch.Generator().manual_seed(7))
+    assert prob.observation.is_cuda
+    assert torch.equal(prob.observation.cpu(), case.y)
