@@ -1,23 +1,38 @@
 """Latent diffusion prior (the reference's ``StableDiffusionNetwork`` role).
 
-Mirrors the parts of ``/root/reference/samplers/networks/diffusers/stable_diffusion.py``
-that the latent samplers use: ``get_latent_shape`` (``:135-144``), ``_decode``
-(``:330-336``: ``vae.decode(z / scaling_factor)``), ``_encode`` (``:338-345``:
-posterior mean × ``scaling_factor``), the padded ``alphas_cumprod`` and an
-ascending timestep buffer.
+Mirrors ``/root/reference/samplers/networks/diffusers/stable_diffusion.py``:
+``get_latent_shape`` (``:135-144``), ``set_condition`` (``:146-293``: input checks, the
+batch-size check, per-reconstruction repetition of the embeddings, classifier-free
+guidance), ``forward`` (``:295-328``: CFG batch doubling, ``u + s·(c − u)``, optional
+guidance rescale), ``_decode`` (``:330-336``: ``vae.decode(z / scaling_factor)``),
+``_encode`` (``:338-345``: posterior mean × ``scaling_factor``), the padded
+``alphas_cumprod`` and an ascending timestep buffer.
 
-What differs, and why: the text encoder, classifier-free guidance and
-IP-adapter paths (``set_condition``, ``forward`` CFG, ``:146-328``) need the
-CLIP weights and tokenizer, which are not available offline; they are out of
-the hot-path scope.  The ε-network is therefore an unconditional
-latent UNet (``UNet2DModel`` over 4-channel latents).  The schedule is SD 1.5's
-(scaled-linear betas 0.00085–0.012, ``steps_offset=1``) with PNDM's
-``skip_prk_steps`` timestep list (the second-to-last timestep repeated); that
-list is restated from diffusers' published algorithm and is not pinned by any
-reference fixture (diffusers is absent) — "parity unpinned" for the schedule.
+The ε-network is the SD 1.5 ``UNet2DConditionModel`` structure
+(``unet2d_condition.py``, 859.5 M parameters) over 4x64x64 latents, cross-attending to a
+77 x 768 context.  What differs, and why:
+
+* no text encoder (CLIP weights are not available offline; SURVEY.md §2 keeps it out of
+  scope): conditions are given as ``prompt_embeds`` / ``negative_prompt_embeds``; the
+  empty prompt ``""`` maps to a fixed synthetic null context (``null_context``), any other
+  prompt string raises ``NotImplementedError``; IP-adapter inputs likewise;
+* CFG with identical conditional and unconditional contexts (the reference's default
+  ``StableDiffusionCondition()``: prompt ``""``, no negative prompt, guidance 7.5) is
+  evaluated as a single pass: ``u + s·(c − u)`` with ``c = u`` is exactly ``u``, and the
+  guidance rescale of identical tensors is the identity, so the result is the same and
+  the doubled batch is skipped;
+* the schedule is SD 1.5's (scaled-linear betas 0.00085–0.012, ``steps_offset=1``) with
+  PNDM's ``skip_prk_steps`` timestep list, restated from diffusers' published algorithm
+  and not pinned by any reference fixture (diffusers is absent) — "parity unpinned".
+
+An unconditional ``UNet2DModel`` prior (``UNet2DConfig``) is still accepted (small test
+priors); it ignores the context.
 """
 
 from __future__ import annotations
+
+import dataclasses
+from typing import Any
 
 import numpy as np
 import torch
@@ -25,11 +40,14 @@ from torch import Tensor
 
 from samplers_amd.dtypes import Device, DType, Shape
 
-from .base import LatentEpsilonNetwork, NoCondition
+from .base import LatentEpsilonNetwork
 from .ddpm import DDPMSchedule
 from .unet2d import UNet2DConfig, UNet2DModel, build_unet
+from .unet2d_condition import (SD15_UNET, UNet2DConditionConfig, UNet2DConditionModel,
+                               build_unet_condition, null_context)
 from .vae import SD15_VAE, AutoencoderKL, VAEConfig, build_vae
 
+# the round-1 unconditional latent prior (kept for small CPU/GPU tests)
 LATENT_UNET_64 = UNet2DConfig(sample_size=64, in_channels=4, out_channels=4,
                               block_out_channels=(128, 256, 512, 512), attention_levels=(1, 2),
                               layers_per_block=2, attention_head_dim=64)
@@ -44,10 +62,47 @@ def pndm_timesteps(num_inference_steps: int, num_train_timesteps: int = 1000,
     return plms
 
 
-class LatentDiffusionNetwork(LatentEpsilonNetwork[NoCondition]):
-    """ε-UNet over VAE latents."""
+@dataclasses.dataclass(slots=True)
+class StableDiffusionCondition:
+    """Same fields as the reference's (``stable_diffusion.py:14-33``)."""
 
-    def __init__(self, unet: UNet2DModel, vae: AutoencoderKL, *,
+    prompt: str | list[str] | None = ""
+    negative_prompt: str | list[str] | None = None
+    guidance_scale: float = 7.5
+    guidance_rescale: float = 0.0
+    prompt_embeds: Tensor | None = None
+    negative_prompt_embeds: Tensor | None = None
+    clip_skip: int | None = None
+    cross_attention_kwargs: dict[str, Any] | None = None
+    ip_adapter_image: Any = None
+    ip_adapter_image_embeds: list[Tensor] | None = None
+
+
+@dataclasses.dataclass(slots=True)
+class ConditioningState:
+    """Per-run tensors (``stable_diffusion.py:36-47``).  ``prompt_embeds`` holds the
+    unconditional rows first when CFG runs (``cat([negative, positive])``), and may have one
+    row shared by the whole batch."""
+
+    prompt_embeds: Tensor
+    do_classifier_free_guidance: bool
+    guidance_scale: float
+    guidance_rescale: float
+
+
+def rescale_noise_cfg(noise_cfg: Tensor, noise_pred_text: Tensor, guidance_rescale: float) -> Tensor:
+    """Guidance rescale of arXiv:2305.08891 §3.4 (diffusers' ``rescale_noise_cfg``)."""
+    dims = list(range(1, noise_pred_text.ndim))
+    std_text = noise_pred_text.std(dim=dims, keepdim=True)
+    std_cfg = noise_cfg.std(dim=dims, keepdim=True)
+    rescaled = noise_cfg * (std_text / std_cfg)
+    return guidance_rescale * rescaled + (1 - guidance_rescale) * noise_cfg
+
+
+class LatentDiffusionNetwork(LatentEpsilonNetwork[StableDiffusionCondition]):
+    """ε-UNet over VAE latents (SD 1.5 structure)."""
+
+    def __init__(self, unet: UNet2DConditionModel | UNet2DModel, vae: AutoencoderKL, *,
                  schedule: DDPMSchedule | None = None, pndm: bool = True) -> None:
         schedule = schedule or DDPMSchedule(beta_start=0.00085, beta_end=0.012,
                                             beta_schedule="scaled_linear", steps_offset=1)
@@ -59,24 +114,124 @@ class LatentDiffusionNetwork(LatentEpsilonNetwork[NoCondition]):
         self.scaling_factor = vae.config.scaling_factor
         self.latent_num_channels = vae.config.latent_channels
         self.latent_resolution_ratio = vae.downscale
-        self.to(device=next(unet.parameters()).device)
+        self.conditional = isinstance(unet, UNet2DConditionModel)
+        dev = next(unet.parameters()).device
+        if self.conditional:
+            self.register_buffer("null_prompt_embeds", null_context(unet.config, device=dev))
+        self._conditioning: ConditioningState | None = None
+        self.to(device=dev)
 
     @classmethod
-    def from_config(cls, unet_config: UNet2DConfig = LATENT_UNET_64,
+    def from_config(cls, unet_config: UNet2DConditionConfig | UNet2DConfig = SD15_UNET,
                     vae_config: VAEConfig = SD15_VAE, *, seed: int = 0, device: Device = None,
                     torch_dtype: DType = None) -> "LatentDiffusionNetwork":
         dt = torch_dtype or torch.float32
-        return cls(build_unet(unet_config, seed=seed, device=device, dtype=dt),
-                   build_vae(vae_config, seed=seed + 1, device=device, dtype=dt))
+        if isinstance(unet_config, UNet2DConditionConfig):
+            unet = build_unet_condition(unet_config, seed=seed, device=device, dtype=dt)
+        else:
+            unet = build_unet(unet_config, seed=seed, device=device, dtype=dt)
+        return cls(unet, build_vae(vae_config, seed=seed + 1, device=device, dtype=dt))
 
     @classmethod
     def from_pretrained(cls, *args, **kwargs):
         raise NotImplementedError("no offline Stable Diffusion checkpoint; use from_config")
 
+    # -- conditioning --------------------------------------------------------------------
+
+    def _embed(self, prompt, what: str) -> Tensor:
+        """Embeddings of a prompt: only the empty prompt has one offline (the null context)."""
+        prompts = [prompt] if isinstance(prompt, str) else list(prompt)
+        if any(p != "" for p in prompts):
+            raise NotImplementedError(
+                f"no text encoder offline: pass {what}_embeds instead of a non-empty {what}")
+        return self.null_prompt_embeds.expand(len(prompts), -1, -1)
+
+    def set_condition(self, condition: StableDiffusionCondition | None) -> None:
+        """``stable_diffusion.py:146-293`` without the text encoder (see the module doc)."""
+        if not self.are_sampling_parameters_initialized:
+            raise RuntimeError("Call `set_sampling_parameters()` before conditioning.")
+        condition = condition if condition is not None else StableDiffusionCondition()
+        if condition.prompt is not None and condition.prompt_embeds is not None:
+            raise ValueError("Cannot forward both `prompt` and `prompt_embeds`.")
+        if condition.prompt is None and condition.prompt_embeds is None:
+            raise ValueError("Provide either `prompt` or `prompt_embeds`.")
+        if condition.negative_prompt is not None and condition.negative_prompt_embeds is not None:
+            raise ValueError("Cannot forward both `negative_prompt` and `negative_prompt_embeds`.")
+        if condition.ip_adapter_image is not None or condition.ip_adapter_image_embeds is not None:
+            raise NotImplementedError("IP-adapter conditioning is out of scope (SURVEY.md §2)")
+
+        if isinstance(condition.prompt, str):
+            batch_size = 1
+        elif isinstance(condition.prompt, list):
+            batch_size = len(condition.prompt)
+        else:
+            batch_size = condition.prompt_embeds.shape[0]
+        if batch_size != self._batch_size:
+            raise ValueError(
+                f"Batch size mismatch: received {batch_size} prompt(s) but the sampler was "
+                f"initialised with batch_size={self._batch_size}. Supply exactly this number "
+                "of prompts/embeddings, or call 'set_sampling_parameters' again.")
+        if not self.conditional:
+            self._conditioning = ConditioningState(self.alphas_cumprod.new_zeros(0), False, 1.0, 0.0)
+            return
+
+        dev, dt = self.device, self.alphas_cumprod.dtype
+        if condition.prompt_embeds is not None:
+            pos = condition.prompt_embeds.to(device=dev, dtype=dt)
+        else:
+            pos = self._embed(condition.prompt, "prompt")
+        do_cfg = condition.guidance_scale > 1.0
+        neg = None
+        if do_cfg:
+            if condition.negative_prompt_embeds is not None:
+                neg = condition.negative_prompt_embeds.to(device=dev, dtype=dt)
+            else:
+                negp = condition.negative_prompt if condition.negative_prompt is not None else ""
+                if isinstance(negp, str):
+                    negp = [negp] * batch_size
+                neg = self._embed(negp, "negative_prompt")
+            if neg.shape != pos.shape:
+                raise ValueError(f"negative_prompt_embeds {tuple(neg.shape)} and prompt_embeds "
+                                 f"{tuple(pos.shape)} must have the same shape")
+        # identical rows everywhere: keep one row and let the attention broadcast it
+        shared = bool((pos == pos[:1]).all())
+        if do_cfg and torch.equal(neg, pos):
+            do_cfg, neg = False, None  # u + s (c - u) with c == u is u (module doc)
+        if shared and neg is None:
+            embeds = pos[:1].contiguous()
+        else:
+            r = self._num_reconstructions or 1
+            pos = pos.repeat_interleave(r, dim=0)  # num_images_per_prompt (diffusers layout)
+            embeds = pos if neg is None else torch.cat([neg.repeat_interleave(r, dim=0), pos])
+        self._conditioning = ConditioningState(embeds.contiguous(), do_cfg,
+                                               float(condition.guidance_scale),
+                                               float(condition.guidance_rescale))
+
+    @property
+    def is_condition_initialized(self) -> bool:
+        return self._conditioning is not None
+
+    def clear_condition(self):
+        self._conditioning = None
+
+    # -- ε and the VAE ---------------------------------------------------------------------
+
     def forward(self, latents: Tensor, t: Tensor | int) -> Tensor:
         if self._num_sampling_steps is None:
             raise RuntimeError("Call `set_sampling_parameters()` before sampling.")
-        return self.unet(latents, t)
+        if not self.conditional:
+            return self.unet(latents, t)
+        if not self.is_condition_initialized:
+            raise RuntimeError("Call `set_condition()` before sampling.")
+        state = self._conditioning
+        if not state.do_classifier_free_guidance:
+            return self.unet(latents, t, state.prompt_embeds)
+        noise = self.unet(torch.cat([latents, latents]), t, state.prompt_embeds)
+        uncond, text = noise.chunk(2)
+        out = uncond + state.guidance_scale * (text - uncond)
+        if state.guidance_rescale > 0.0:
+            out = rescale_noise_cfg(out, text, state.guidance_rescale)
+        return out
 
     def set_sampling_parameters(self, num_sampling_steps: int, batch_size: int = 1,
                                 num_reconstructions: int = 1):
@@ -103,10 +258,6 @@ class LatentDiffusionNetwork(LatentEpsilonNetwork[NoCondition]):
 
     def _encode(self, x: Tensor, *, differentiable: bool = False) -> Tensor:
         return self.vae.encode_mean(x) * self.scaling_factor
-
-    @property
-    def is_condition_initialized(self) -> bool:
-        return True
 
     def to(self, *args, **kwargs):
         super().to(*args, **kwargs)

@@ -86,7 +86,7 @@ def test_dps_non_quadratic_noise_takes_autograd_cotangent(cuda):
     """A native operator with a noise model whose gradient is not c·r (pseudo-Huber): the
     cotangent comes from autograd of ``log_prob`` through the HIP operator; pinned by the
     oracle loop (``dps.py:91-122`` restated) with the same log-likelihood."""
-    case = load_dps_case("dps_rnd_gauss_conv_b4")
+    case = load_dps_case("dps_rnd_poiss_conv_b4")
     m = case.meta
     noise = si.laplace_noise(0.1)
     net = si.make_samplers_amd_net(m["prior"], case.shape[0], m["coef"], device=cuda)

@@ -3,8 +3,8 @@
     python tools/bench_psld.py [--batch 32 --steps 3 --warmup 1]
 
 Workload: PSLD (psld.py:118-153) with a centre-inpainting mask on 3x512x512 images,
-GaussianNoise(0.05), SD 1.5 VAE architecture (83.65 M parameters) + 4x64x64 latent
-UNet, random weights with fixed seeds, fp32, 100-step schedule (psld.py:50).  One
+GaussianNoise(0.05), SD 1.5 VAE architecture (83.65 M parameters) + SD 1.5
+UNet2DConditionModel (859.5 M, null 77x768 context), random weights with fixed seeds, fp32, 100-step schedule (psld.py:50).  One
 step = one PSLD iteration over the batch: latent UNet forward, VAE decode forward,
 HIP pixel pass, VAE encode forward, encode/decode/UNet VJPs, HIP glue and update
 (samplers_amd.samplers.psld.FusedPSLDStep).  Prints one JSON line; "vae_tflops" is
@@ -28,6 +28,8 @@ import samplers_amd  # noqa: E402,F401
 import torch  # noqa: E402
 
 VAE_FLOP_PER_SAMPLE = 7.13e12
+# SD 1.5 UNet at 64x64 latents: 0.80 TFLOP forward + 0.92 input VJP (torch FlopCounterMode)
+UNET_FLOP_PER_SAMPLE = 1.73e12
 
 
 def heartbeat(path: Path, every: float = 30.0) -> None:
@@ -55,7 +57,7 @@ def main():
 
     from samplers_amd import _hip
     from samplers_amd.inverse_problem import InverseProblem
-    from samplers_amd.networks.latent import LatentDiffusionNetwork
+    from samplers_amd.networks.latent import LatentDiffusionNetwork, StableDiffusionCondition
     from samplers_amd.noise import GaussianNoise
     from samplers_amd.operators import CenterInpaintingOperator
     from samplers_amd.samplers.dps import initial_sample
@@ -70,6 +72,7 @@ def main():
     y = y + (0.05 * torch.randn(tuple(y.shape), generator=gen)).to(dev)
     net = LatentDiffusionNetwork.from_config(seed=0, device=dev)
     net.set_sampling_parameters(100, batch_size=args.batch)
+    net.set_condition(StableDiffusionCondition(prompt=[""] * args.batch))  # reference default prompt, CFG collapses
     problem = InverseProblem(op, y, GaussianNoise(0.05).to(dev))
     lat = tuple(net.get_latent_shape(shape))
     step = FusedPSLDStep(net, problem, y.reshape(args.batch, -1), 1, lat)
@@ -107,10 +110,12 @@ def main():
         "n_gpus": 1, "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 2),
         "higher_is_better": True, "dtype": "f32",
         "data": "synthetic (seeded U(-1,1) images, centre mask, sigma=0.05); random-init SD1.5 "
-                "VAE architecture + 4x64x64 latent UNet",
+                "VAE + SD1.5 UNet2DConditionModel architecture (859.5 M, null 77x768 context)",
         "config": {"workload": f"PSLD + CenterInpainting(0.5) + GaussianNoise(0.05), 3x{args.image}²",
                    "batch": args.batch, "schedule": "100-step PNDM (psld.py:50)"},
         "vae_tflops": round(VAE_FLOP_PER_SAMPLE * args.batch / (ms / 1e3) / 1e12, 2),
+        "model_tflops": round((VAE_FLOP_PER_SAMPLE + UNET_FLOP_PER_SAMPLE) * args.batch
+                              / (ms / 1e3) / 1e12, 2),
         "peak_gib": round(torch.cuda.max_memory_allocated() / 2**30, 1),
     }), flush=True)
 

@@ -6,7 +6,7 @@ Config 5 is 256 samples sharded over 8 GPUs: 32 per GPU, which is what one proce
 runs (the batch shards with no data-path collective; the batch-global losses are 8-byte
 all-reduces).  Workload: ReSample (resample.py:131-228) with IdentityOperator on 3x512x512,
 PoissonNoise(rate=1.0) (config 5 fixes no rate), the SD 1.5 VAE architecture
-(83.65 M parameters) + 4x64x64 latent UNet, random weights with fixed seeds, fp32.
+(83.65 M parameters) + SD1.5 UNet2DConditionModel (859.5 M), random weights with fixed seeds, fp32.
 
 A full ReSample run (100 steps, default max_optimization_iters=2000) is 98 main-loop
 iterations plus time-travel blocks, three pixel-space and four latent-space hard
@@ -71,7 +71,7 @@ def main():
     dev = torch.device("cuda:0")
 
     from samplers_amd import _hip
-    from samplers_amd.networks.latent import LatentDiffusionNetwork
+    from samplers_amd.networks.latent import LatentDiffusionNetwork, StableDiffusionCondition
     from samplers_amd.noise import PoissonNoise
     from samplers_amd.operators import IdentityOperator
     from samplers_amd.samplers.dps import initial_sample
@@ -88,6 +88,7 @@ def main():
     y = y.to(dev)
     net = LatentDiffusionNetwork.from_config(seed=0, device=dev)
     net.set_sampling_parameters(100, batch_size=b)
+    net.set_condition(StableDiffusionCondition(prompt=[""] * b))  # reference default prompt, CFG collapses
     lat = tuple(net.get_latent_shape(shape))
     sampler = ReSampleSampler(net)
     cons = _Consistency(op, y.reshape(b, -1), 1)
@@ -131,7 +132,7 @@ def main():
         "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(step_s * 1e3, 2), "higher_is_better": True, "dtype": "f32",
         "data": "synthetic (seeded U(-1,1) images, Poisson(rate=1) noise); random-init SD1.5 VAE "
-                "architecture + 4x64x64 latent UNet",
+                "+ SD1.5 UNet2DConditionModel architectures (null 77x768 context)",
         "config": {"workload": f"ReSample + Identity + PoissonNoise(1.0), 3x{args.image}²",
                    "batch": b, "schedule": "100-step PNDM (resample.py:52)"},
         "decode_vjp_tflops": round(DECODE_FLOP_PER_SAMPLE * b / step_s / 1e12, 2),
