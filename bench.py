@@ -159,46 +159,135 @@ def conv_summary(kern: dict) -> dict | None:
     return out
 
 
+def host_cpu() -> dict:
+    """The host's CPU model, the cores this process may run on, and the cgroup CPU quota
+    (a container's share of the machine, which can be far below the visible core count)."""
+    model = "unknown"
+    try:
+        for line in Path("/proc/cpuinfo").read_text().splitlines():
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    affinity = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
+    quota = None
+    for path, parse_q in (("/sys/fs/cgroup/cpu.max", lambda s: s.split()),
+                          ("/sys/fs/cgroup/cpu/cpu.cfs_quota_us", None)):
+        try:
+            if parse_q is not None:
+                q, p = parse_q(Path(path).read_text())
+                if q != "max":
+                    quota = float(q) / float(p)
+            else:
+                q = float(Path(path).read_text())
+                p = float(Path("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read_text())
+                if q > 0:
+                    quota = q / p
+            break
+        except (OSError, ValueError):
+            continue
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    share = int(omp) if omp.isdigit() and int(omp) > 0 else None
+    if share is None and quota:
+        share = max(1, int(quota + 0.5))
+    return {"model": model, "affinity_cores": affinity, "cgroup_cpus": quota,
+            "cpu_share": min(share or affinity, affinity)}
+
+
+class _Heartbeat:
+    """A line on stderr every `every` s while a long CPU leg runs (a silent run is taken to be
+    hung by the GPU pool's watchdog)."""
+
+    def __init__(self, what: str, every: float = 30.0):
+        import threading
+
+        self.what, self.every, self.stop = what, every, threading.Event()
+        self.t0 = time.perf_counter()
+        self.th = threading.Thread(target=self._run, daemon=True)
+
+    def _run(self):
+        while not self.stop.wait(self.every):
+            log(f"{self.what}: still running at {time.perf_counter() - self.t0:.0f}s")
+
+    def __enter__(self):
+        self.th.start()
+        return self
+
+    def __exit__(self, *exc):
+        self.stop.set()
+        return False
+
+
 def cpu_baseline(image: int, seconds: float) -> dict:
-    """oracle/dps_loop.py on the host cores, B=1, same workload per sample."""
+    """oracle/dps_loop.py (dps.py:91-122 semantics) on the host cores with the same UNet and
+    workload per sample.  The thread count is probed first at batch 1 (the CPU share this
+    process is given — OMP_NUM_THREADS / the cgroup quota — and multiples of it up to every
+    core the process may run on), then batch 1 and batch 8 are timed on the best count for
+    about `seconds` / 2 each; the best per-sample rate is reported."""
+    with _Heartbeat("cpu baseline"):
+        return _cpu_baseline(image, seconds)
+
+
+def _cpu_baseline(image: int, seconds: float) -> dict:
     from oracle import dps_loop
     from samplers_amd.networks.unet2d import build_unet
     from samplers_amd.operators import get_mask_random
 
-    cores = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
-    cores = max(1, min(cores, 16))
-    torch.set_num_threads(cores)
+    host = host_cpu()
+    share, cores = host["cpu_share"], host["affinity_cores"]
+    candidates = sorted({min(cores, share * k) for k in (1, 2, 4)})
     shape = (3, image, image)
     unet = build_unet(seed=0)
     mask = get_mask_random(shape, 0.5, seed=1)
     kept = torch.nonzero(~mask.flatten()).squeeze(1)
-    gen = torch.Generator().manual_seed(1000)
-    x_true = torch.rand((1, *shape), generator=gen) * 2 - 1
-    y = x_true.reshape(1, -1)[:, kept] + 0.05 * torch.randn(1, kept.numel(), generator=gen)
     betas = torch.linspace(1e-4, 0.02, 1000, dtype=torch.float32)
     acp = torch.cat([torch.ones(1), torch.cumprod(1 - betas, 0)]).clip(1e-6, 1)
     ts = list(range(1000))
-    x = torch.randn((1, *shape), generator=gen)
     apply_op = lambda v: v.reshape(v.shape[0], -1)[:, kept]  # noqa: E731
     lp = dps_loop.gaussian_log_prob(0.05)
-    noise = lambda i: torch.randn((1, *shape), generator=gen)  # noqa: E731
-    # one warm-up iteration, then as many as fit in `seconds` (at least 2)
-    x = dps_loop.dps_reference(lambda v, t: unet(v, t), acp, ts, apply_op, lp, y, x, noise,
-                               gamma=1.0, eta=1.0, steps_limit=1, return_sample=True)
-    done, t0 = 0, time.perf_counter()
-    while done < 2 or time.perf_counter() - t0 < seconds:
+    def point(batch: int, nthreads: int, budget: float) -> dict:
+        torch.set_num_threads(nthreads)
+        gen = torch.Generator().manual_seed(1000)
+        x_true = torch.rand((batch, *shape), generator=gen) * 2 - 1
+        y = apply_op(x_true) + 0.05 * torch.randn(batch, kept.numel(), generator=gen)
+        x = torch.randn((batch, *shape), generator=gen)
+        noise = lambda i: torch.randn((batch, *shape), generator=gen)  # noqa: E731
+        # one warm-up iteration, then as many as fit in the budget (at least 1)
         x = dps_loop.dps_reference(lambda v, t: unet(v, t), acp, ts, apply_op, lp, y, x, noise,
                                    gamma=1.0, eta=1.0, steps_limit=1, return_sample=True)
-        done += 1
-    dt = time.perf_counter() - t0
+        done, t0 = 0, time.perf_counter()
+        while done < 1 or time.perf_counter() - t0 < budget:
+            x = dps_loop.dps_reference(lambda v, t: unet(v, t), acp, ts, apply_op, lp, y, x,
+                                       noise, gamma=1.0, eta=1.0, steps_limit=1,
+                                       return_sample=True)
+            done += 1
+        dt = time.perf_counter() - t0
+        rec = {"batch": batch, "threads": nthreads, "iterations": done,
+               "samples_per_s": round(batch * done / dt, 4)}
+        log(f"cpu baseline: batch {batch}, {nthreads} threads: {rec['samples_per_s']} samples/s")
+        return rec
+
+    probe = [point(1, t, 0.0) for t in candidates]  # thread-count probe: one timed iteration
+    nthreads = max(probe, key=lambda p: p["samples_per_s"])["threads"]
+    sweep = [point(b, nthreads, seconds / 2) for b in (1, 8)]
+    best = max(sweep, key=lambda p: p["samples_per_s"])
     return {
-        "value": round(done / dt, 4),
+        "value": best["samples_per_s"],
         "unit": "samples/sec (batch×steps/s)",
-        "cores": cores,
+        "cores": best["threads"],
         "kind": "port",
-        "sample": f"batch=1, {done} guided DPS iterations (t=999) of "
-                  f"oracle/dps_loop.py at 3x{image}x{image}, 50% random mask, same random-init "
-                  f"UNet, fp32, torch-CPU {torch.__version__}",
+        "cpu_model": host["model"],
+        "host_cores": cores,
+        "cpu_share": share,
+        "cgroup_cpus": host["cgroup_cpus"],
+        "thread_probe": probe,
+        "sweep": sweep,
+        "sample": f"batch 1 and 8 on the best of {candidates} threads (probed at batch 1): "
+                  f"guided DPS iterations (t=999) of oracle/dps_loop.py at 3x{image}x{image}, "
+                  f"50% random mask, same random-init UNet, fp32, torch-CPU {torch.__version__}; "
+                  f"best = batch {best['batch']} on {best['threads']} threads, "
+                  f"{best['iterations']} iterations",
     }
 
 
@@ -293,6 +382,15 @@ def main():
         "algorithmic_bytes_per_launch": rl[g_dom]["bytes"],
         "avg_launch_ms": round(rl[g_dom]["avg_ms"], 5),
     }
+    if g_dom == "dps_update" and step.needs_v:
+        # SURVEY §8d's minimal K2 bytes (read x, eps, w, y; write x'): pass 2 re-reads v
+        # instead (one more coalesced stream, measured faster than the gather), which the
+        # figure above counts; this one prices the launch at the minimum
+        d = kern["dps_update"]
+        min_bytes = nbytes["dps_update"] * d["samples"] / d["count"] + nbytes["index_per_launch"]
+        guidance_roofline["minimal_bytes_per_launch"] = min_bytes
+        guidance_roofline["frac_minimal"] = round(min_bytes / rl[g_dom]["avg_ms"] / 1e6
+                                                  / HBM_PEAK_GBS, 4)
     conv = conv_summary(kern)
     if conv and conv["ms"] > sum(rl[k]["avg_ms"] * kern[k]["count"] for k in rl):
         # the prior's fp32-MFMA convolution tile dominates the step

@@ -49,14 +49,21 @@ def main():
     if a.json:
         out = json.loads(Path(a.json).read_text()) if Path(a.json).exists() else {}
         for kv in a.key:
-            key, sub = kv.split("=", 1)
-            hits = [v for k, v in rows.items() if sub in k]
+            # NAME=SUB1|SUB2: every dispatch of every kernel whose name holds one of the
+            # substrings, so the per-launch figure covers the same launch set as the bench's
+            # per-launch FLOPs / bytes (all variants, not the first match)
+            key, subs = kv.split("=", 1)
+            hits = [(k, v) for k, v in rows.items() if any(s in k for s in subs.split("|"))]
             if hits:
-                n, fb, wb = hits[0]
+                n = sum(v[0] for _, v in hits)
+                fb = sum(v[0] * v[1] for _, v in hits) / n
+                wb = sum(v[0] * v[2] for _, v in hits) / n
                 out[key] = {"hbm_bytes_per_launch": round(fb + wb), "fetch_bytes": round(fb),
                             "write_bytes": round(wb), "dispatches": n,
+                            "kernels": sorted(short(k) for k, _ in hits),
                             "method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes), "
-                                      "KiB*1024, FETCH doubled (gfx950 wide-stream correction)"}
+                                      "KiB*1024, FETCH doubled (gfx950 wide-stream correction); "
+                                      "mean over all dispatches of the listed kernels"}
         Path(a.json).write_text(json.dumps(out, indent=1, sort_keys=True) + "\n")
 
 
