@@ -11,7 +11,7 @@
 //   bwd: stats  — A = sum(dy*gamma), B = sum(dy*gamma*xhat) per chunk (y recomputed)
 //        apply  — dx = rstd*(dy*gamma - A/n - xhat*B/n)
 // x is NCHW, so one group (sample n, channels g*Cg .. g*Cg+Cg-1) is one contiguous
-// run of Cg*HW floats; it is cut into chunks (16384 floats forward, 8192 backward), one
+// run of Cg*HW floats; it is cut into chunks (8192-16384 floats, see GN_CHUNK_*), one
 // workgroup each, so the launch fills the chip even at batch 1.  Where the input is
 // float4-aligned, single-pass variants of both directions (below) replace the pairs.  The shift K is the group's first
 // element (removes the cancellation of plain sum/sum-of-squares); chunk partials are
@@ -25,16 +25,15 @@
 
 namespace sp {
 
-// Elements per workgroup (chunk): forward 16384, backward 8192 (the single-pass backward
-// holds two tensors' chunks in registers; measured best on the UNet's shapes).
-#ifndef SP_GN_CHUNK_FWD
-#define SP_GN_CHUNK_FWD 16384
-#endif
-#ifndef SP_GN_CHUNK_BWD
-#define SP_GN_CHUNK_BWD 8192
-#endif
-constexpr int GN_CHUNK_FWD = SP_GN_CHUNK_FWD, GN_CHUNK_BWD = SP_GN_CHUNK_BWD;
-constexpr int GN_CHUNK_MIN = GN_CHUNK_FWD < GN_CHUNK_BWD ? GN_CHUNK_FWD : GN_CHUNK_BWD;
+// Elements per workgroup (chunk).  Forward: 16384 for groups of >= 2^17 elements, 8192 below
+// (fewer, larger chunks stream better on big groups; small groups need the chunks to fill the
+// chip); backward: 8192.  Measured on the UNet's shapes (tools/bench_gn.py, MI355X).  The
+// chunk is a function of the shape only, so every path over one call sums in the same order.
+constexpr int GN_CHUNK_FWD_BIG = 16384, GN_CHUNK_FWD = 8192, GN_CHUNK_BWD = 8192;
+constexpr int GN_FWD_BIG_GROUP = 1 << 17;
+constexpr int GN_CHUNK_MIN = 8192;
+
+static int gn_fwd_chunk(int64_t gs) { return gs >= GN_FWD_BIG_GROUP ? GN_CHUNK_FWD_BIG : GN_CHUNK_FWD; }
 
 // n / d for 0 <= n < 2^31 by multiply-high (d >= 1).
 struct FastDiv {
@@ -373,10 +372,14 @@ __global__ __launch_bounds__(kBlock) void k_gn_bwd_apply(const float* __restrict
 // agent-scope atomic stores (coherent across the XCDs' L2s, no cache flush), then polls the
 // team's words until all are present (the words are zeroed before the launch).  The grid is
 // persistent and no larger than the chip's resident capacity, so a team's members are
-// resident together; each team walks groups gi = team, team + nteams, ...  Chunking, the
-// per-thread element order and the summation order are those of the two-pass kernels, so
-// the results are bit-identical.  HBM traffic: forward 2 passes (was 3), backward 3 + the
-// addend (was 5 + the addend).
+// resident together; each team walks groups gi = team, team + nteams, ...  A workgroup keeps
+// two groups in flight: once a group's partials are published, the poll of the team's words
+// is ISSUED FIRST and the next group's chunk is loaded right behind it, so the wait for the
+// team (a cross-XCD hand-off: 1.5-3 us under load, against ~8 us of streaming per group)
+// overlaps the next chunk's HBM traffic — the poll's result is older than the prefetch, so
+// the wait for it leaves the prefetch in flight.  Chunking, the per-thread element order and
+// the summation order are those of the two-pass kernels, so the results are bit-identical.
+// HBM traffic: forward 2 passes (was 3), backward 3 + the addends (was 5 + the addends).
 constexpr int GNT_MAX_SPINS = 1 << 22;          // poll bound (~0.3 s): a stuck team exits
 
 __device__ unsigned int g_gnt_timeouts;  // polls that hit GNT_MAX_SPINS (sp_groupnorm_team_timeouts)
@@ -388,32 +391,7 @@ __device__ __forceinline__ void gnt_publish(uint64_t* slot, float a, float b) {
                        __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// The team's sums, as group_sums forms them (lane i of every wave takes chunk i, i + 64, ...,
-// then a wave sum).  The words are polled by the first `chunks` threads only and passed
-// through LDS (sv: 2 x GNT_MAX_CHUNKS floats); a barrier separates the two.
-constexpr int GNT_MAX_CHUNKS = 256;
-
-__device__ __forceinline__ void gnt_sums(uint64_t* slots, int chunks, float* sv, float& a, float& b) {
-    const int t = threadIdx.x;
-    if (t < chunks) {
-        uint64_t wa = 0, wb = 0;
-#pragma nounroll
-        for (int spins = 0; spins <= GNT_MAX_SPINS; ++spins) {
-            wa = __hip_atomic_load(slots + 2 * t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            wb = __hip_atomic_load(slots + 2 * t + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if ((wa >> 32) && (wb >> 32)) break;
-            __builtin_amdgcn_s_sleep(2);
-        }
-        if (!((wa >> 32) && (wb >> 32))) atomicAdd(&g_gnt_timeouts, 1u);
-        sv[t] = __uint_as_float(static_cast<uint32_t>(wa));
-        sv[GNT_MAX_CHUNKS + t] = __uint_as_float(static_cast<uint32_t>(wb));
-    }
-    __syncthreads();
-    a = 0.f, b = 0.f;
-    for (int i = t & 63; i < chunks; i += 64) a += sv[i], b += sv[GNT_MAX_CHUNKS + i];
-    a = wave_sum(a);
-    b = wave_sum(b);
-}
+constexpr int GNT_MAX_CHUNKS = 256;  // chunks per group (words polled per team)
 
 // Block-reduce (a, b) as the two-pass kernels do and publish them as chunk m's words.
 __device__ __forceinline__ void gnt_reduce_publish(float a, float b, float* red, uint64_t* slot) {
@@ -426,7 +404,7 @@ __device__ __forceinline__ void gnt_reduce_publish(float a, float b, float* red,
                                       (red[4] + red[5]) + (red[6] + red[7]));
 }
 
-// A chunk's elements in one tensor part (the team kernels require that no chunk straddles
+// A chunk's elements in one tensor part (the single-pass kernels require that no chunk straddles
 // the two parts of a concatenated input): buffer resource over the chunk's first `lim`
 // float4 of the group, so accesses past the chunk end read 0 / are dropped.  The range
 // check covers the VGPR offset only (not soffset), so a thread's float4 i is addressed as
@@ -455,138 +433,287 @@ __device__ __forceinline__ void gnt_store(__amdgpu_buffer_rsrc_t r, uint32_t vo,
                                            vo + i * kBlock * 16, 0, SP_GN_NT);
 }
 
-template <bool ACT, int GNT_PER>  // GNT_PER: float4 per thread (chunk / 4 / kBlock)
-__global__ __launch_bounds__(kBlock, 2) void k_gn_fwd_team(const float* __restrict__ x, GnGeom G,
+// The group's per-channel gamma / beta / bias come along with its chunk (one value per thread
+// t < Cg) and are read from a double-buffered LDS table.
+constexpr int GNP_MAX_CG = 128;  // channels per group the LDS table holds
+
+struct GnpBuf {  // one group's per-thread prefetch state besides the chunk itself
+    float ga, be, bi;  // thread t < Cg: gamma / beta / bias of the group's channel t
+    float kx, kb;      // the group's first element and that channel's bias: the shift K is
+                       // their sum, formed where it is used (forming it here would wait for
+                       // the whole prefetch)
+};
+
+// Issue the loads of group gi's chunk m and its per-channel state.  live == false: the chunk
+// loads get an empty range (no memory access, zeros) — the caller issues them anyway so that
+// the code after the prefetch has one path (see gnp_poll_finish).
+template <int PER>
+__device__ __forceinline__ void gnp_issue(const float* __restrict__ base, const GnGeom& G,
+                                          int64_t gi, uint32_t m, float (&v)[PER][4], GnpBuf& b,
+                                          bool live = true) {
+    const GroupCtx c = group_ctx_at<4>(base, G, gi, m);
+    const auto r = gnt_rsrc(c.x, c.lo, live ? c.hi : 0u);
+    const uint32_t vo = (c.lo + threadIdx.x) * 16;
+#pragma unroll
+    for (int i = 0; i < PER; ++i) gnt_load(r, vo, i, v[i]);
+    // every thread loads, from the input itself where a table is absent (threads t >= Cg
+    // re-read the last channel): no branch around a load, see above
+    const int ch = c.g * G.Cg + min(static_cast<int>(threadIdx.x), G.Cg - 1);
+    const float ga = (G.gamma ? G.gamma : base)[ch];
+    const float be = (G.beta ? G.beta : base)[ch];
+    const float bi = (G.bias ? G.bias : base)[c.n * G.C + ch];
+    b.ga = G.gamma ? ga : 1.f;
+    b.be = G.beta ? be : 0.f;
+    b.bi = G.bias ? bi : 0.f;
+    b.kx = *c.x.at(0);
+    const float kb = (G.bias ? G.bias : base)[c.n * G.C + c.g * G.Cg];
+    b.kb = G.bias ? kb : 0.f;
+}
+
+// Poll words of a team: every thread issues its loads (threads past the team re-read word 0),
+// so the loads precede anything issued after this call.
+__device__ __forceinline__ void gnp_poll_issue(const uint64_t* slots, int chunks, uint64_t& wa,
+                                               uint64_t& wb) {
+    const int t = threadIdx.x < chunks ? threadIdx.x : 0;
+    wa = __hip_atomic_load(slots + 2 * t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    wb = __hip_atomic_load(slots + 2 * t + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Finish the poll (threads t < chunks spin on their words) and form the team's sums as
+// gnt_sums does.  Every thread tests its issued words first, outside any branch and loop: the
+// wait for them then leaves the younger prefetch loads in flight (at a loop header or a join
+// the compiler merges paths and waits for everything).
+__device__ __forceinline__ void gnp_poll_finish(const uint64_t* slots, int chunks, uint64_t wa,
+                                                uint64_t wb, float* sv, float& a, float& b) {
+    const int t = threadIdx.x;
+    bool ready = (wa >> 32) && (wb >> 32);
+    if ((t < chunks) & !ready) {
+#pragma nounroll
+        for (int spins = 0; spins < GNT_MAX_SPINS; ++spins) {
+            __builtin_amdgcn_s_sleep(2);
+            wa = __hip_atomic_load(slots + 2 * t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            wb = __hip_atomic_load(slots + 2 * t + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            ready = (wa >> 32) && (wb >> 32);
+            if (ready) break;
+        }
+        if (!ready) atomicAdd(&g_gnt_timeouts, 1u);
+    }
+    if (t < chunks) {
+        sv[t] = __uint_as_float(static_cast<uint32_t>(wa));
+        sv[GNT_MAX_CHUNKS + t] = __uint_as_float(static_cast<uint32_t>(wb));
+    }
+    __syncthreads();
+    a = 0.f, b = 0.f;
+    for (int i = t & 63; i < chunks; i += 64) a += sv[i], b += sv[GNT_MAX_CHUNKS + i];
+    a = wave_sum(a);
+    b = wave_sum(b);
+}
+
+// One forward group: chunk v (loaded), state bf; prefetches group gn (< 0: none) into vn / bn.
+template <bool ACT, int PER>
+__device__ __forceinline__ void gnp_fwd_group(const float* __restrict__ x, const GnGeom& G,
+                                              uint64_t* __restrict__ slots, int64_t gi, int64_t gn,
+                                              uint32_t m, float (&v)[PER][4], const GnpBuf& bf,
+                                              float (&vn)[PER][4], GnpBuf& bn, float (*tab)[GNP_MAX_CG],
+                                              float* red, float* sv, float* __restrict__ z,
+                                              float* __restrict__ mean_out,
+                                              float* __restrict__ rstd_out) {
+    const int t = threadIdx.x;
+    const GroupCtx c = group_ctx_at<4>(x, G, gi, m);
+    if (t < G.Cg) tab[0][t] = bf.ga, tab[1][t] = bf.be, tab[2][t] = bf.bi;
+    __syncthreads();
+    const float K = bf.kx + bf.kb;
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+        const uint32_t j = c.lo + t + i * kBlock;
+        const bool in = j < c.hi;  // past the chunk end: adds exact zeros
+        const float b = G.bias ? tab[2][fdiv(in ? j : c.lo, G.hw_div)] : 0.f;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const float d = in ? v[i][e] + b - K : 0.f;
+            s1 += d;
+            s2 = fmaf(d, d, s2);
+        }
+    }
+    uint64_t* gslots = slots + gi * G.chunks * 2;
+    gnt_reduce_publish(s1, s2, red, gslots + 2 * m);
+    uint64_t wa, wb;
+    gnp_poll_issue(gslots, G.chunks, wa, wb);
+    gnp_issue<PER>(x, G, gn >= 0 ? gn : gi, m, vn, bn, gn >= 0);
+    float S1, S2;
+    gnp_poll_finish(gslots, G.chunks, wa, wb, sv, S1, S2);
+    const float inv_n = 1.f / static_cast<float>(G.gs);
+    const float m1 = S1 * inv_n;
+    const float mean = K + m1;
+    const float var = fmaxf(S2 * inv_n - m1 * m1, 0.f);
+    const float rstd = rsqrtf(var + G.eps);
+    if (m == 0 && t == 0) mean_out[gi] = mean, rstd_out[gi] = rstd;
+    const Parts<float> zp{z + c.zoff, z + c.zoff, G.gs};
+    const auto rz = gnt_rsrc(zp, c.lo, c.hi);
+    const uint32_t vo = (c.lo + t) * 16;
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+        const uint32_t j = c.lo + t + i * kBlock;
+        const uint32_t cl = fdiv(j < c.hi ? j : c.lo, G.hw_div);
+        const float b = G.bias ? tab[2][cl] : 0.f;
+        const float sc = rstd * tab[0][cl];
+        const float sh = tab[1][cl] - mean * sc;
+        float o[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const float y = fmaf(v[i][e] + b, sc, sh);
+            o[e] = ACT ? silu_f(y) : y;
+        }
+        gnt_store(rz, vo, i, o);  // past the chunk end: dropped
+    }
+}
+
+template <bool ACT, int PER>
+__global__ __launch_bounds__(kBlock, 2) void k_gn_fwd_pipe(const float* __restrict__ x, GnGeom G,
                                                            uint64_t* __restrict__ slots, int nteams,
                                                            int64_t ngroups, float* __restrict__ z,
                                                            float* __restrict__ mean_out,
                                                            float* __restrict__ rstd_out) {
     __shared__ float red[8];
     __shared__ float sv[2 * GNT_MAX_CHUNKS];
+    __shared__ float tab[2][3][GNP_MAX_CG];
     const uint32_t m = blockIdx.x % G.chunks;
-    for (int64_t gi = blockIdx.x / G.chunks; gi < ngroups; gi += nteams) {
-        const GroupCtx c = group_ctx_at<4>(x, G, gi, m);
-        const auto rx = gnt_rsrc(c.x, c.lo, c.hi);
-        const uint32_t vo = (c.lo + threadIdx.x) * 16;
-        float v[GNT_PER][4];
-#pragma unroll
-        for (int i = 0; i < GNT_PER; ++i) gnt_load(rx, vo, i, v[i]);
-        const float K = *c.x.at(0) + (G.bias ? G.bias[c.n * G.C + c.g * G.Cg] : 0.f);
-        float s1 = 0.f, s2 = 0.f;
-#pragma unroll
-        for (int i = 0; i < GNT_PER; ++i) {
-            const uint32_t j = c.lo + threadIdx.x + i * kBlock;
-            const bool in = j < c.hi;  // past the chunk end: adds exact zeros
-            const float b = G.bias ? G.bias[c.n * G.C + chan_of<4>(in ? j : c.lo, c, G)] : 0.f;
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                const float d = in ? v[i][e] + b - K : 0.f;
-                s1 += d;
-                s2 = fmaf(d, d, s2);
-            }
-        }
-        uint64_t* gslots = slots + gi * G.chunks * 2;
-        gnt_reduce_publish(s1, s2, red, gslots + 2 * m);
-        float S1, S2;
-        gnt_sums(gslots, G.chunks, sv, S1, S2);
-        const float inv_n = 1.f / static_cast<float>(G.gs);
-        const float m1 = S1 * inv_n;
-        const float mean = K + m1;
-        const float var = fmaxf(S2 * inv_n - m1 * m1, 0.f);
-        const float rstd = rsqrtf(var + G.eps);
-        if (m == 0 && threadIdx.x == 0) mean_out[gi] = mean, rstd_out[gi] = rstd;
-        const Parts<float> zp{z + c.zoff, z + c.zoff, G.gs};
-        const auto rz = gnt_rsrc(zp, c.lo, c.hi);
-#pragma unroll
-        for (int i = 0; i < GNT_PER; ++i) {
-            const uint32_t j = c.lo + threadIdx.x + i * kBlock;
-            const int ch = chan_of<4>(j < c.hi ? j : c.lo, c, G);
-            const float b = G.bias ? G.bias[c.n * G.C + ch] : 0.f;
-            const float sc = rstd * (G.gamma ? G.gamma[ch] : 1.f);
-            const float sh = (G.beta ? G.beta[ch] : 0.f) - mean * sc;
-            float o[4];
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                const float y = fmaf(v[i][e] + b, sc, sh);
-                o[e] = ACT ? silu_f(y) : y;
-            }
-            gnt_store(rz, vo, i, o);  // past the chunk end: dropped
-        }
-        __syncthreads();  // red[] is reused by the next group
+    int64_t gi = blockIdx.x / G.chunks;
+    if (gi >= ngroups) return;
+    float va[PER][4], vb[PER][4];
+    GnpBuf ba, bb;
+    gnp_issue<PER>(x, G, gi, m, va, ba);
+    for (;;) {  // two groups per trip: the register buffers are named, not indexed
+        int64_t gn = gi + nteams < ngroups ? gi + nteams : -1;
+        gnp_fwd_group<ACT, PER>(x, G, slots, gi, gn, m, va, ba, vb, bb, tab[0], red, sv, z,
+                                mean_out, rstd_out);
+        if (gn < 0) break;
+        gi = gn;
+        gn = gi + nteams < ngroups ? gi + nteams : -1;
+        gnp_fwd_group<ACT, PER>(x, G, slots, gi, gn, m, vb, bb, va, ba, tab[1], red, sv, z,
+                                mean_out, rstd_out);
+        if (gn < 0) break;
+        gi = gn;
     }
 }
 
-template <bool ACT, int GNT_PER>
-__global__ __launch_bounds__(kBlock, 2) void k_gn_bwd_team(
+// One backward group: x chunk v and dz chunk g (loaded); prefetches group gn into vn / gq.
+template <bool ACT, int PER>
+__device__ __forceinline__ void gnp_bwd_group(
+    const float* __restrict__ dz, const float* __restrict__ x, const GnGeom& G,
+    const float* __restrict__ mean_in, const float* __restrict__ rstd_in,
+    uint64_t* __restrict__ slots, int64_t gi, int64_t gn, uint32_t m, float (&v)[PER][4],
+    float (&g)[PER][4], const GnpBuf& bf, float (&vn)[PER][4], float (&gq)[PER][4], GnpBuf& bn,
+    float (*tab)[GNP_MAX_CG], float* red, float* sv, float* __restrict__ dx,
+    float* __restrict__ dx2, const float* __restrict__ add1, const float* __restrict__ add2) {
+    const int t = threadIdx.x;
+    const GroupCtx c = group_ctx_at<4>(x, G, gi, m);
+    if (t < G.Cg) tab[0][t] = bf.ga, tab[1][t] = bf.be, tab[2][t] = bf.bi;
+    __syncthreads();
+    const float mean = mean_in[gi], rstd = rstd_in[gi];
+    // v, g are replaced by xhat and dy*gamma: the dx pass needs nothing else
+    float sa = 0.f, sb = 0.f;
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+        const uint32_t j = c.lo + t + i * kBlock;
+        const bool in = j < c.hi;  // past the chunk end: adds exact zeros
+        const uint32_t cl = fdiv(in ? j : c.lo, G.hw_div);
+        float gdy[4], xh[4];
+        gn_grad_terms<4, ACT>(v[i], g[i], G.bias ? tab[2][cl] : 0.f, mean, rstd, tab[0][cl],
+                              tab[1][cl], gdy, xh);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            sa += in ? gdy[e] : 0.f;
+            sb = fmaf(in ? gdy[e] : 0.f, xh[e], sb);
+            g[i][e] = gdy[e];
+            v[i][e] = xh[e];
+        }
+    }
+    uint64_t* gslots = slots + gi * G.chunks * 2;
+    gnt_reduce_publish(sa, sb, red, gslots + 2 * m);
+    // the addends of this group, issued before the poll and the prefetch (an absent addend
+    // gets an empty range: zeros, no memory access, no branch around the loads)
+    const uint32_t vo = (c.lo + t) * 16;
+    float a1[PER][4], a1b[PER][4];
+    {
+        const auto ra = gnt_rsrc(parts_at<const float>(add1 ? add1 : x, G.x2 ? (add1 ? add2 : x) : nullptr,
+                                                       G, gi), c.lo, add1 ? c.hi : 0u);
+        const Parts<const float> abp{(G.add1b ? G.add1b : x) + c.zoff, (G.add1b ? G.add1b : x) + c.zoff,
+                                     G.gs};
+        const auto rb = gnt_rsrc(abp, c.lo, G.add1b ? c.hi : 0u);
+#pragma unroll
+        for (int i = 0; i < PER; ++i) {
+            gnt_load(ra, vo, i, a1[i]);
+            gnt_load(rb, vo, i, a1b[i]);
+        }
+    }
+    uint64_t wa, wb;
+    gnp_poll_issue(gslots, G.chunks, wa, wb);
+    {
+        const int64_t gq_i = gn >= 0 ? gn : gi;
+        gnp_issue<PER>(x, G, gq_i, m, vn, bn, gn >= 0);
+        const auto rg = gnt_rsrc(Parts<const float>{dz + gq_i * (int64_t)G.gs,
+                                                    dz + gq_i * (int64_t)G.gs, G.gs},
+                                 c.lo, gn >= 0 ? c.hi : 0u);
+#pragma unroll
+        for (int i = 0; i < PER; ++i) gnt_load(rg, vo, i, gq[i]);
+    }
+    float A, B;
+    gnp_poll_finish(gslots, G.chunks, wa, wb, sv, A, B);
+    const float inv_n = 1.f / static_cast<float>(G.gs);
+    const float mA = A * inv_n, mB = B * inv_n;
+    const auto rd = gnt_rsrc(parts_at<float>(dx, G.x2 ? dx2 : nullptr, G, gi), c.lo, c.hi);
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+        float o[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) o[e] = rstd * (g[i][e] - mA - v[i][e] * mB);
+        if (add1) {  // as k_gn_bwd_apply (same rounding)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) o[e] += a1[i][e];
+        }
+        if (G.add1b) {  // + the skip gradient, as k_gn_bwd_apply
+#pragma unroll
+            for (int e = 0; e < 4; ++e) o[e] += a1b[i][e];
+        }
+        gnt_store(rd, vo, i, o);
+    }
+}
+
+template <bool ACT, int PER>
+__global__ __launch_bounds__(kBlock, 2) void k_gn_bwd_pipe(
     const float* __restrict__ dz, const float* __restrict__ x, GnGeom G,
     const float* __restrict__ mean_in, const float* __restrict__ rstd_in,
     uint64_t* __restrict__ slots, int nteams, int64_t ngroups, float* __restrict__ dx,
     float* __restrict__ dx2, const float* __restrict__ add1, const float* __restrict__ add2) {
     __shared__ float red[8];
     __shared__ float sv[2 * GNT_MAX_CHUNKS];
+    __shared__ float tab[2][3][GNP_MAX_CG];
     const uint32_t m = blockIdx.x % G.chunks;
-    for (int64_t gi = blockIdx.x / G.chunks; gi < ngroups; gi += nteams) {
+    int64_t gi = blockIdx.x / G.chunks;
+    if (gi >= ngroups) return;
+    float va[PER][4], ga[PER][4], vb[PER][4], gb[PER][4];
+    GnpBuf ba, bb;
+    gnp_issue<PER>(x, G, gi, m, va, ba);
+    {
         const GroupCtx c = group_ctx_at<4>(x, G, gi, m);
-        const float mean = mean_in[gi], rstd = rstd_in[gi];
-        const auto rx = gnt_rsrc(c.x, c.lo, c.hi);
-        const Parts<const float> dzp{dz + c.zoff, dz + c.zoff, G.gs};
-        const auto rg = gnt_rsrc(dzp, c.lo, c.hi);
+        const auto rg = gnt_rsrc(Parts<const float>{dz + c.zoff, dz + c.zoff, G.gs}, c.lo, c.hi);
         const uint32_t vo = (c.lo + threadIdx.x) * 16;
-        float v[GNT_PER][4], g[GNT_PER][4];
 #pragma unroll
-        for (int i = 0; i < GNT_PER; ++i) {
-            gnt_load(rx, vo, i, v[i]);
-            gnt_load(rg, vo, i, g[i]);
-        }
-        // v, g are replaced by dy*gamma and xhat: the dx pass needs nothing else
-        float sa = 0.f, sb = 0.f;
-#pragma unroll
-        for (int i = 0; i < GNT_PER; ++i) {
-            const uint32_t j = c.lo + threadIdx.x + i * kBlock;
-            const bool in = j < c.hi;  // past the chunk end: adds exact zeros
-            const int ch = chan_of<4>(in ? j : c.lo, c, G);
-            float gdy[4], xh[4];
-            gn_grad_terms<4, ACT>(v[i], g[i], G.bias ? G.bias[c.n * G.C + ch] : 0.f, mean, rstd,
-                                  G.gamma ? G.gamma[ch] : 1.f, G.beta ? G.beta[ch] : 0.f, gdy, xh);
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                sa += in ? gdy[e] : 0.f;
-                sb = fmaf(in ? gdy[e] : 0.f, xh[e], sb);
-                g[i][e] = gdy[e];
-                v[i][e] = xh[e];
-            }
-        }
-        uint64_t* gslots = slots + gi * G.chunks * 2;
-        gnt_reduce_publish(sa, sb, red, gslots + 2 * m);
-        float A, B;
-        gnt_sums(gslots, G.chunks, sv, A, B);
-        const float inv_n = 1.f / static_cast<float>(G.gs);
-        const float mA = A * inv_n, mB = B * inv_n;
-        const auto rd = gnt_rsrc(parts_at<float>(dx, G.x2 ? dx2 : nullptr, G, gi), c.lo, c.hi);
-        const auto ra = gnt_rsrc(parts_at<const float>(add1, G.x2 ? add2 : nullptr, G, gi),
-                                 c.lo, add1 ? c.hi : 0);
-        const Parts<const float> abp{G.add1b + c.zoff, G.add1b + c.zoff, G.gs};
-        const auto rb = gnt_rsrc(abp, c.lo, G.add1b ? c.hi : 0);
-#pragma unroll
-        for (int i = 0; i < GNT_PER; ++i) {
-            float o[4];
-#pragma unroll
-            for (int e = 0; e < 4; ++e) o[e] = rstd * (g[i][e] - mA - v[i][e] * mB);
-            if (add1) {  // as k_gn_bwd_apply (same rounding)
-                float ad[4];
-                gnt_load(ra, vo, i, ad);
-#pragma unroll
-                for (int e = 0; e < 4; ++e) o[e] += ad[e];
-            }
-            if (G.add1b) {  // + the skip gradient, as k_gn_bwd_apply
-                float ad[4];
-                gnt_load(rb, vo, i, ad);
-#pragma unroll
-                for (int e = 0; e < 4; ++e) o[e] += ad[e];
-            }
-            gnt_store(rd, vo, i, o);
-        }
-        __syncthreads();
+        for (int i = 0; i < PER; ++i) gnt_load(rg, vo, i, ga[i]);
+    }
+    for (;;) {
+        int64_t gn = gi + nteams < ngroups ? gi + nteams : -1;
+        gnp_bwd_group<ACT, PER>(dz, x, G, mean_in, rstd_in, slots, gi, gn, m, va, ga, ba, vb, gb,
+                                bb, tab[0], red, sv, dx, dx2, add1, add2);
+        if (gn < 0) break;
+        gi = gn;
+        gn = gi + nteams < ngroups ? gi + nteams : -1;
+        gnp_bwd_group<ACT, PER>(dz, x, G, mean_in, rstd_in, slots, gi, gn, m, vb, gb, bb, va, ga,
+                                ba, tab[1], red, sv, dx, dx2, add1, add2);
+        if (gn < 0) break;
+        gi = gn;
     }
 }
 
@@ -615,7 +742,7 @@ static int gn_geom(int64_t n, int32_t c, int64_t hw, int32_t groups, const float
 
 static int g_single_pass = 1;  // sp_groupnorm_single_pass
 
-// Teams that fit the chip at once for a team kernel (0: the kernel cannot run).
+// Teams that fit the chip at once for a single-pass kernel (0: the kernel cannot run).
 static int64_t gnt_teams(const void* kernel, int64_t ngroups, int chunks) {
     int dev = 0, cus = 0, per_cu = 0;
     if (hipGetDevice(&dev) != hipSuccess ||
@@ -676,26 +803,41 @@ int sp_groupnorm_silu_fwd2(const float* x, const float* x2, int32_t c1, const fl
     GnGeom G;
     int V;
     dim3 grid;
-    int rc = gn_geom(n, channels, hw, groups, chan_bias, gamma, beta, eps, GN_CHUNK_FWD, &G, &V,
-                     &grid);
+    const int chunk = gn_fwd_chunk((int64_t)(channels / (groups > 0 ? groups : 1)) * hw);
+    int rc = gn_geom(n, channels, hw, groups, chan_bias, gamma, beta, eps, chunk, &G, &V, &grid);
     if (rc == SP_OK) rc = gn_split(&G, x2, c1, channels, hw);
     if (rc != SP_OK) return rc;
     if (n == 0) return SP_OK;  // empty batch: nothing to read or write
     if (!x || !z || !mean || !rstd || !work) return SP_EINVAL;
     hipStream_t s = static_cast<hipStream_t>(stream);
     const dim3 blk(kBlock);
-    if (V == 4 && g_single_pass && (!x2 || (int64_t)(c1 % G.Cg) * hw % GN_CHUNK_FWD == 0)) {
+    if (V == 4 && g_single_pass && G.Cg <= GNP_MAX_CG && G.chunks <= GNT_MAX_CHUNKS &&
+        (!x2 || (int64_t)(c1 % G.Cg) * hw % chunk == 0)) {
         const int64_t ngroups = n * groups;
-        constexpr int PER = GN_CHUNK_FWD / 4 / kBlock;
-        auto kern = act ? k_gn_fwd_team<true, PER> : k_gn_fwd_team<false, PER>;
-        const int64_t teams = G.chunks <= GNT_MAX_CHUNKS
-            ? gnt_teams(reinterpret_cast<const void*>(kern), ngroups, G.chunks) : 0;
+        const void* kern;
+        if (chunk == GN_CHUNK_FWD_BIG)
+            kern = act ? (const void*)k_gn_fwd_pipe<true, GN_CHUNK_FWD_BIG / 4 / kBlock>
+                       : (const void*)k_gn_fwd_pipe<false, GN_CHUNK_FWD_BIG / 4 / kBlock>;
+        else
+            kern = act ? (const void*)k_gn_fwd_pipe<true, GN_CHUNK_FWD / 4 / kBlock>
+                       : (const void*)k_gn_fwd_pipe<false, GN_CHUNK_FWD / 4 / kBlock>;
+        const int64_t teams = gnt_teams(kern, ngroups, G.chunks);
         if (teams > 0) {
             uint64_t* slots = reinterpret_cast<uint64_t*>(work);
             if (hipMemsetAsync(slots, 0, ngroups * G.chunks * 16, s) != hipSuccess)
                 return check_launch("sp_groupnorm_silu_fwd (slots)");
-            launch(0, kern, dim3(static_cast<unsigned>(teams * G.chunks)), blk, s, x, G, slots,
-                   static_cast<int>(teams), ngroups, z, mean, rstd);
+            const dim3 grid1(static_cast<unsigned>(teams * G.chunks));
+            const int nt = static_cast<int>(teams);
+#define SP_GN_FWD_PIPE(AA, PP) \
+    launch(0, k_gn_fwd_pipe<AA, PP>, grid1, blk, s, x, G, slots, nt, ngroups, z, mean, rstd)
+            if (chunk == GN_CHUNK_FWD_BIG) {
+                if (act) { SP_GN_FWD_PIPE(true, GN_CHUNK_FWD_BIG / 4 / kBlock); }
+                else { SP_GN_FWD_PIPE(false, GN_CHUNK_FWD_BIG / 4 / kBlock); }
+            } else {
+                if (act) { SP_GN_FWD_PIPE(true, GN_CHUNK_FWD / 4 / kBlock); }
+                else { SP_GN_FWD_PIPE(false, GN_CHUNK_FWD / 4 / kBlock); }
+            }
+#undef SP_GN_FWD_PIPE
             return check_launch("sp_groupnorm_silu_fwd");
         }
     }
@@ -741,12 +883,12 @@ int sp_groupnorm_silu_bwd2(const float* dz, const float* x, const float* x2, int
     G.add1b = add1b;
     hipStream_t s = static_cast<hipStream_t>(stream);
     const dim3 blk(kBlock);
-    if (V == 4 && g_single_pass && (!x2 || (int64_t)(c1 % G.Cg) * hw % GN_CHUNK_BWD == 0)) {
+    if (V == 4 && g_single_pass && G.Cg <= GNP_MAX_CG && G.chunks <= GNT_MAX_CHUNKS &&
+        (!x2 || (int64_t)(c1 % G.Cg) * hw % GN_CHUNK_BWD == 0)) {
         const int64_t ngroups = n * groups;
         constexpr int PER = GN_CHUNK_BWD / 4 / kBlock;
-        auto kern = act ? k_gn_bwd_team<true, PER> : k_gn_bwd_team<false, PER>;
-        const int64_t teams = G.chunks <= GNT_MAX_CHUNKS
-            ? gnt_teams(reinterpret_cast<const void*>(kern), ngroups, G.chunks) : 0;
+        auto kern = act ? k_gn_bwd_pipe<true, PER> : k_gn_bwd_pipe<false, PER>;
+        const int64_t teams = gnt_teams(reinterpret_cast<const void*>(kern), ngroups, G.chunks);
         if (teams > 0) {
             uint64_t* slots = reinterpret_cast<uint64_t*>(work);
             if (hipMemsetAsync(slots, 0, ngroups * G.chunks * 16, s) != hipSuccess)

@@ -28,6 +28,13 @@ def timed(fn, reps=10):
 def main():
     lib = _hip.load_library()
     dev = torch.device("cuda:0")
+    # the chip's read + write streaming rate on the largest shape: a device-to-device copy
+    a = torch.randn(SHAPES[0], device=dev)
+    b = torch.empty_like(a)
+    tc = timed(lambda: b.copy_(a))
+    print(json.dumps({"copy_GBps": round(2 * a.numel() * 4 / tc / 1e9), "bytes": 2 * a.numel() * 4}),
+          flush=True)
+    del a, b
     for shape in SHAPES:
         n, c, h, w = shape
         layer = GroupNormAct(32, c, eps=1e-6, act=True).to(dev)
