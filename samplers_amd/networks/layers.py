@@ -198,7 +198,7 @@ def conv3x3_forward(module: "Conv3x3", x: Tensor, res: Tensor | None = None,
                                            _hip.ptr(bias), n, cin, cout, h, w, _hip.ptr(y),
                                            _hip.stream_of(x)), "sp_conv3x3_thin_fwd")
         return y if res is None else y.add_(res)
-    pk = module._pack(algo, False)
+    pk = tile_pack(module, algo, False)
     if algo == "wino" and res is not None:
         _hip.check(lib.sp_wino3x3_fwd_res(_hip.ptr(x), _hip.ptr(pk), _hip.ptr(bias),
                                           _hip.ptr(res.contiguous()), n, cin, cout, h, w,
@@ -226,7 +226,7 @@ def conv3x3_input_vjp(module: "Conv3x3", dy: Tensor, x_shape) -> Tensor:
                                                  _hip.stream_of(dy)), "sp_conv3x3_thin_bwd_input")
         return dx
     fn = lib.sp_wino3x3_bwd_input if algo == "wino" else lib.sp_conv3x3_bwd_input
-    _hip.check(fn(_hip.ptr(dy), _hip.ptr(module._pack(algo, True)), n, cin, cout, h, w,
+    _hip.check(fn(_hip.ptr(dy), _hip.ptr(tile_pack(module, algo, True)), n, cin, cout, h, w,
                   _hip.ptr(dx), _hip.stream_of(dy)), f"sp_{algo}_conv3x3_bwd_input")
     return dx
 
@@ -253,6 +253,28 @@ class _Conv3x3Fn(torch.autograd.Function):
         return dx, dw, db, None
 
 
+def tile_pack(module: nn.Conv2d, algo: str, input_vjp: bool) -> Tensor:
+    """``module``'s 3x3 weights transformed / packed for a stride-1 tile (``algo`` "wino" or
+    "direct", forward or input VJP), cached on the module and rebuilt when the weight changes."""
+    w = module.weight
+    key = (w.data_ptr(), w._version, w.device)
+    cache = module.__dict__.setdefault("_tile_packs", {})
+    if cache.get("key") != key:
+        cache.clear()
+        cache["key"] = key
+    if (algo, input_vjp) not in cache:
+        lib = _hip.load_library()
+        cout, cin = w.shape[0], w.shape[1]
+        wc = w.detach().contiguous()
+        size = (lib.sp_wino3x3_packed_size if algo == "wino" else lib.sp_conv3x3_packed_size)(cin, cout)
+        out = torch.empty(int(size), device=w.device)
+        fn = lib.sp_wino3x3_pack if algo == "wino" else lib.sp_conv3x3_pack
+        _hip.check(fn(_hip.ptr(wc), cout, cin, int(input_vjp), _hip.ptr(out), _hip.stream_of(wc)),
+                   f"sp_{algo}3x3_pack")
+        cache[(algo, input_vjp)] = out
+    return cache[(algo, input_vjp)]
+
+
 class Conv3x3(nn.Conv2d):
     """``nn.Conv2d(cin, cout, 3, padding=1)`` whose device forward / input VJP run this
     project's kernels: the fp32-MFMA tiles — Winograd F(2x2,3x3) (``csrc/sp_wino.hip``;
@@ -264,25 +286,9 @@ class Conv3x3(nn.Conv2d):
 
     def __init__(self, cin: int, cout: int) -> None:
         super().__init__(cin, cout, 3, padding=1)
-        self._packs: dict = {}
-        self._pack_key = None
 
     def _pack(self, algo: str, input_vjp: bool) -> Tensor:
-        w = self.weight
-        key = (w.data_ptr(), w._version, w.device)
-        if self._pack_key != key:
-            self._packs, self._pack_key = {}, key
-        if (algo, input_vjp) not in self._packs:
-            lib = _hip.load_library()
-            cout, cin = w.shape[0], w.shape[1]
-            wc = w.detach().contiguous()
-            size = (lib.sp_wino3x3_packed_size if algo == "wino" else lib.sp_conv3x3_packed_size)(cin, cout)
-            out = torch.empty(int(size), device=w.device)
-            fn = lib.sp_wino3x3_pack if algo == "wino" else lib.sp_conv3x3_pack
-            _hip.check(fn(_hip.ptr(wc), cout, cin, int(input_vjp), _hip.ptr(out), _hip.stream_of(wc)),
-                       f"sp_{algo}3x3_pack")
-            self._packs[(algo, input_vjp)] = out
-        return self._packs[(algo, input_vjp)]
+        return tile_pack(self, algo, input_vjp)
 
     def forward(self, x: Tensor) -> Tensor:
         if x.is_cuda and x.dtype == torch.float32 and x.dim() == 4:
@@ -419,13 +425,65 @@ class _ConvS2Fn(torch.autograd.Function):
         return dx, None, None, None, None
 
 
+# A 3x3 / stride-2 convolution is the stride-1 / padding-1 convolution read at every other
+# position: with padding 1 on all sides (diffusers' downsample_padding=1) at the even rows and
+# columns, with one zero row / column bottom / right (downsample_padding=0) at the odd ones.
+# Where no stride-2 tile serves a shape (channels or widths outside its rules), the stride-1
+# MFMA tiles compute it at full resolution (4x the MACs, on tiles ~50x faster than MIOpen's
+# naive kernel that these shapes otherwise reach); the input VJP is the stride-1 VJP of dy
+# scattered to those positions (zeros elsewhere).
+
+def strided_full_supported(module: nn.Conv2d, x: Tensor) -> bool:
+    """The stride-1 tiles serve ``module`` (3x3, frozen weights) at ``x``'s full resolution,
+    forward and input VJP."""
+    if not (x.is_cuda and x.dtype == torch.float32 and x.dim() == 4) or module.weight.requires_grad:
+        return False
+    backend = conv_backend()
+    if backend == "miopen":
+        return False
+    lib = _hip.load_library()
+    _, cin, h, w = x.shape
+    cout = module.out_channels
+    fwd = _conv_algo(lib, cin, cout, h, w, backend)
+    vjp = _conv_algo(lib, cout, cin, h, w, backend)
+    return h % 2 == 0 and w % 2 == 0 and fwd in ("wino", "direct") and vjp in ("wino", "direct")
+
+
+class _ConvS2FullFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias, module, phase):
+        y = conv3x3_forward(module, x.contiguous())
+        ctx.module, ctx.phase, ctx.x_shape = module, phase, x.shape
+        return y[:, :, phase::2, phase::2].contiguous()
+
+    @staticmethod
+    def backward(ctx, dy):
+        dx = None
+        if ctx.needs_input_grad[0]:
+            n, _, h, w = ctx.x_shape
+            dyf = dy.new_zeros((n, ctx.module.out_channels, h, w))
+            dyf[:, :, ctx.phase::2, ctx.phase::2] = dy
+            dx = conv3x3_input_vjp(ctx.module, dyf, ctx.x_shape)
+        return dx, None, None, None, None
+
+
+def conv3x3_stride2(module: nn.Conv2d, x: Tensor, padding: int) -> Tensor:
+    """``module(x)`` for a 3x3 / stride-2 ``nn.Conv2d`` with ``padding=1`` (``padding=1``), or
+    ``module(F.pad(x, (0, 1, 0, 1)))`` with ``padding=0``, through the stride-1 tiles at full
+    resolution where they serve the shape, else torch / MIOpen."""
+    if strided_full_supported(module, x):
+        return _ConvS2FullFn.apply(x, module.weight, module.bias, module, 0 if padding else 1)
+    return module(x) if padding else module(F.pad(x, (0, 1, 0, 1)))
+
+
 def downsample_conv(module: nn.Conv2d, x: Tensor, box: SkipGrad | None = None) -> Tensor:
     """``module(F.pad(x, (0, 1, 0, 1)))`` for a 3x3 / stride-2 / padding-0 ``nn.Conv2d``
     (diffusers' Downsample2D with downsample_padding=0): the stride-2 MFMA tile
-    (``csrc/sp_conv_s2.hip``) where its shape rules hold, else MIOpen on the padded input."""
+    (``csrc/sp_conv_s2.hip``) where its shape rules hold, else the stride-1 tiles at full
+    resolution (``conv3x3_stride2``), else MIOpen on the padded input."""
     if downsample_s2_supported(module, x) and not module.weight.requires_grad:
         return _ConvS2Fn.apply(x, module.weight, module.bias, module,
                                box if box is not None and box.enabled else None)
     if box is not None:
         box.enabled = False
-    return module(F.pad(x, (0, 1, 0, 1)))
+    return conv3x3_stride2(module, x, padding=0)

@@ -31,7 +31,7 @@ import torch.nn.functional as F
 from torch import Tensor, nn
 
 from .attention import attention
-from .layers import Conv3x3, GroupNormAct, SkipGrad
+from .layers import Conv3x3, GroupNormAct, SkipGrad, conv3x3_stride2
 from .unet2d import ResnetBlock2D, TimestepEmbedding, Upsample2D, timestep_embedding
 
 
@@ -153,9 +153,9 @@ class Downsample2D(nn.Module):
         self.conv = nn.Conv2d(channels, channels, 3, stride=2, padding=1)
 
     def forward(self, x: Tensor, box: SkipGrad | None = None) -> Tensor:
-        if box is not None:  # MIOpen conv: autograd accumulates the skip gradient
+        if box is not None:  # no accumulate mode on this path: autograd adds the skip gradient
             box.enabled = False
-        return self.conv(x)
+        return conv3x3_stride2(self.conv, x, padding=1)
 
 
 class _Level(nn.Module):

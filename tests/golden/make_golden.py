@@ -171,6 +171,12 @@ DPS_CASES = [
     ("dps_id_poiss_lin_b1_64", "identity", "poisson", "linear", 0.3, (1,), 1, (3, 64, 64), 6, 1e-3, 0.0),
     ("dps_rnd_gauss_conv_r3", "random", "gauss", "conv", 0.1, (), 3, (3, 32, 32), 10, 1e-2, 1.0),
     ("dps_rnd_gauss_conv_b3_odd", "random", "gauss", "conv", 0.1, (3,), 1, (1, 5, 7), 10, 1e-2, 1.0),
+    # bounded-magnitude trajectories (|out| of order 1-10, the linear stand-in near the
+    # data's own scale): small-valued pixels are pinned too, not only the diverging ones
+    ("dps_rnd_gauss_lin_bounded", "random", "gauss", "linear", 0.9, (4,), 1, (3, 32, 32), 50, 1e-3, 1.0),
+    ("dps_ctr_gauss_lin_bounded", "center", "gauss", "linear", 0.5, (2,), 1, (3, 32, 32), 50, 1e-2, 0.0),
+    ("dps_id_poiss_lin_bounded", "identity", "poisson", "linear", 0.9, (2,), 1, (3, 16, 16), 30, 1e-3, 1.0),
+    ("dps_rnd_gauss_conv_bounded", "random", "gauss", "conv", 0.9, (2,), 1, (3, 16, 16), 50, 1e-3, 1.0),
 ]
 
 

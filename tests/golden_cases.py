@@ -44,7 +44,9 @@ class DpsCase:
 
 
 def dps_case_names(prefix: str = "dps") -> list[str]:
-    return sorted(p.stem for p in GOLDEN.glob(f"{prefix}_*.npz"))
+    """Fixture names ``{prefix}_*`` (a prefix may itself hold a glob, e.g. ``dps_*_bounded``)."""
+    pattern = f"{prefix}.npz" if "*" in prefix else f"{prefix}_*.npz"
+    return sorted(p.stem for p in GOLDEN.glob(pattern))
 
 
 def load_dps_case(name: str) -> DpsCase:

@@ -319,3 +319,49 @@ def test_upsample_nearest2x_and_vjp(cuda, shape):
     # fp64 block sums on the CPU
     want = dy.double().cpu().reshape(shape[0], shape[1], shape[2], 2, shape[3], 2).sum((3, 5))
     assert ((gx.double().cpu() - want).abs().max() <= 4e-7 * want.abs().max().clamp_min(1)).item()
+
+
+STRIDE2_FULL_SHAPES = [  # n, c, h, w: the SD 1.5 UNet's downsamplers and the UNet's 16x16 one
+    (2, 320, 64, 64),
+    (2, 640, 32, 32),
+    (1, 1280, 16, 16),
+    (3, 256, 16, 16),
+]
+
+
+@pytest.mark.parametrize("padding", [1, 0])
+@pytest.mark.parametrize("shape", STRIDE2_FULL_SHAPES)
+def test_stride2_conv_via_full_resolution_tiles(cuda, shape, padding):
+    """3x3 / stride-2 convolutions outside the stride-2 tile's rules run as the stride-1
+    tile at full resolution read at the even (padding 1) or odd (one zero row / column
+    bottom / right) positions; the input VJP scatters dy to those positions.  Against fp64
+    torch, with the Winograd tolerance; the path must not reach MIOpen."""
+    from samplers_amd.networks.layers import conv3x3_stride2, strided_full_supported
+
+    n, c, h, w = shape
+    g = torch.Generator().manual_seed(sum(shape) + padding)
+    x = torch.randn(n, c, h, w, generator=g)
+    conv = torch.nn.Conv2d(c, c, 3, stride=2, padding=padding).requires_grad_(False)
+    with torch.no_grad():
+        conv.weight.normal_(0, (c * 9) ** -0.5, generator=g)
+        conv.bias.normal_(0, 0.1, generator=g)
+    dy = torch.randn(n, c, h // 2, w // 2, generator=g)
+    xd = x.double().requires_grad_()
+    xin = xd if padding else F.pad(xd, (0, 1, 0, 1))
+    ref = F.conv2d(xin, conv.weight.double(), conv.bias.double(), stride=2, padding=padding)
+    (gref,) = torch.autograd.grad(ref, xd, dy.double())
+
+    cg = conv.to(cuda)
+    xg = x.to(cuda).requires_grad_()
+    assert strided_full_supported(cg, xg)
+    from torch.profiler import ProfilerActivity, profile
+
+    with profile(activities=[ProfilerActivity.CUDA]) as prof:
+        out = conv3x3_stride2(cg, xg, padding)
+        (gx,) = torch.autograd.grad(out, xg, dy.to(cuda))
+        torch.cuda.synchronize()
+    names = {e.name for e in prof.events() if e.device_type.name == "CUDA"}
+    assert not any("naive_conv" in k or "igemm" in k or "Conv" in k for k in names), names
+    assert out.shape == ref.shape
+    _check(out.detach(), ref.detach(), slack=5)
+    _check(gx, gref, slack=5)

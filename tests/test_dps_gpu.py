@@ -120,3 +120,16 @@ def test_dps_blur_matches_oracle(cuda, noise_kind):
                                  lambda x: oblur.blur(x, k).float(), lp, y, init,
                                  lambda i: steps[i], gamma=1e-2, eta=1.0)
     assert si.relative_error(out.cpu(), ref) < 1e-4
+
+
+@pytest.mark.parametrize("name", dps_case_names("dps_*_bounded"))
+def test_dps_bounded_golden_elementwise(cuda, name):
+    """The bounded-magnitude golden trajectories (|x-hat| of order 1): every element, not only
+    the relative L2 that the large pixels of the diverging cases dominate."""
+    case = load_dps_case(name)
+    m = case.meta
+    net = si.make_samplers_amd_net(m["prior"], case.shape[0], m["coef"], device=cuda)
+    out = DPSSampler(net)(_problem(case, cuda), num_sampling_steps=m["N"], num_reconstructions=m["R"],
+                          gamma=m["gamma"], eta=m["eta"], noise_fn=_noise_fn(case, cuda))
+    ref = case.out.numpy()
+    np.testing.assert_allclose(out.cpu().numpy(), ref, rtol=1e-4, atol=1e-5 * np.abs(ref).max())

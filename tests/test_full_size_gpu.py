@@ -6,8 +6,8 @@ step's HIP passes, through what the domain makes checkable at that size:
 * the two fused DPS passes (residual + update, injected noise): every element against the
   float64 closed form (oracle/closed_form.py) at 2e-5 x max|ref|, and every per-sample
   ||y - A x0||^2 at 2e-5 relative;
-* the blur residual pass (config 3, streaming kernel) against the float64 closed form on
-  8 of the samples (the reflect-padded 9x9 oracle is torch-CPU);
+* the blur residual pass (config 3, streaming kernel) and the update pass against the
+  float64 closed form on 8 of the samples (the reflect-padded 9x9 oracle is torch-CPU);
 * Philox noise: the 64-sample draw equals two 32-sample draws with sample offsets, bit for
   bit (the multi-GPU sharding invariant), and has standard-normal moments."""
 
@@ -75,25 +75,35 @@ def test_dps_passes_full_size(cuda):
                                atol=2e-5 * np.abs(out_ref).max())
 
 
-def test_blur_residual_full_size(cuda):
+def test_blur_passes_full_size(cuda):
+    """configs[2]'s two passes at 3 x 256 x 256, 8 samples: the streaming residual pass and
+    the update pass (bridge + injected noise + guidance through the re-read v)."""
     b = 8
     op = GaussianBlurOperator(SHAPE, 9, 3.0).to(cuda)
     desc = op.hip_descriptor()
     lib = _hip.load_library()
     g = torch.Generator().manual_seed(9)
-    x, eps, y = (torch.randn(b, N, generator=g) for _ in range(3))
+    x, eps, y, w, xi = (torch.randn(b, N, generator=g) for _ in range(5))
     a, k, gs = 0.5, math.sqrt(0.75), 400.0
     c = _hip.SpDpsCoefs(a, k, gs, 0.9, 0.2, 0.1, 1.0, 1e-9)
     part = torch.empty(b, int(lib.sp_rsq_partials(desc)), device=cuda)
     v = torch.empty(b, N, device=cuda)
-    xd, ed, yd = (t.to(cuda) for t in (x, eps, y))  # held: the kernel reads them asynchronously
+    xd, ed, yd, wd, xid = (t.to(cuda) for t in (x, eps, y, w, xi))  # held: read asynchronously
     _hip.check(lib.sp_dps_residual(desc, xd.data_ptr(), ed.data_ptr(), yd.data_ptr(), b, 1, c,
                                    v.data_ptr(), part.data_ptr(), _stream()), "residual")
+    out = torch.empty_like(xd)
+    _hip.check(lib.sp_dps_update(desc, xd.data_ptr(), ed.data_ptr(), yd.data_ptr(), v.data_ptr(),
+                                 wd.data_ptr(), part.data_ptr(), xid.data_ptr(), 0, 0, 0, b, 1, c,
+                                 out.data_ptr(), _stream()), "update")
     apply_np, adjoint_np = oblur.blur_ops(SHAPE, oblur.taps(9, 3.0))
     v_ref, rsq_ref = closed_form.residual_pass(x.numpy(), eps.numpy(), y.numpy(), 1, a, k, gs,
                                                apply_np, adjoint_np)
     np.testing.assert_allclose(v.cpu().numpy(), v_ref, rtol=0, atol=2e-5 * np.abs(v_ref).max())
     np.testing.assert_allclose(part.sum(1).cpu().numpy(), rsq_ref, rtol=2e-5)
+    out_ref = closed_form.update_pass(x.numpy(), eps.numpy(), v_ref, w.numpy(), rsq_ref,
+                                      xi.numpy(), a, k, 0.9, 0.2, 0.1, 1.0)
+    np.testing.assert_allclose(out.cpu().numpy(), out_ref, rtol=0,
+                               atol=2e-5 * np.abs(out_ref).max())
 
 
 def test_philox_full_size_shard_invariant(cuda):

@@ -125,3 +125,12 @@ def test_closed_form_matches_autograd_loop():
                                   br.c_ell, br.c_s, br.std, 0.3)
     ref = after["x"].reshape(b, n).numpy()
     assert np.abs(out - ref).max() / np.abs(ref).max() < 1e-6
+
+
+@pytest.mark.parametrize("name", dps_case_names("dps_*_bounded"))
+def test_oracle_bounded_golden_elementwise(name):
+    """The oracle on the bounded-magnitude cases, element by element."""
+    case = load_dps_case(name)
+    ref = case.out.numpy()
+    np.testing.assert_allclose(_oracle_dps(case).numpy(), ref, rtol=1e-5,
+                               atol=1e-6 * np.abs(ref).max())
