@@ -37,12 +37,27 @@ struct ThinArgs {
     int tiles_w, tiles;  // tiles per image row / per image
 };
 
+// Workgroups are dealt round-robin over the 8 XCDs in linear block order, so tiles that are
+// neighbours in the image would land on different XCDs and each fetch their shared halo lines
+// into its own L2 (the patch's single-column halo loads touch a whole line each: PMC fetch
+// 2.2x the input).  The linear id is remapped so that runs of consecutive logical tiles —
+// horizontal, then vertical neighbours — execute on one XCD and share its L2.
+__device__ __forceinline__ void thin_block(int& tile, int& cob, int64_t& n) {
+    const unsigned X = gridDim.x, Y = gridDim.y, T = X * Y * gridDim.z;
+    unsigned l = blockIdx.x + X * (blockIdx.y + Y * blockIdx.z);
+    if (T % 8 == 0) l = (l % 8) * (T / 8) + l / 8;  // placement only: any order is correct
+    tile = static_cast<int>(l % X);
+    cob = static_cast<int>((l / X) % Y);
+    n = l / (X * Y);
+}
+
 template <int CI, int CO>
 __global__ __launch_bounds__(kBlock) void k_conv3x3_thin(ThinArgs a) {
     __shared__ __attribute__((aligned(16))) float patch[CI * TN_PATCH];
-    const int tile = blockIdx.x;
-    const int co0 = blockIdx.y * CO;
-    const int64_t n = blockIdx.z;
+    int tile, cob;
+    int64_t n;
+    thin_block(tile, cob, n);
+    const int co0 = cob * CO;
     const int ty = tile / a.tiles_w, tx = tile - ty * a.tiles_w;
     const int h0 = ty * TN_TH, w0 = tx * TN_TW;
     const int64_t plane = (int64_t)a.H * a.W;
