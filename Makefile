@@ -6,7 +6,8 @@ CXXFLAGS ?= -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -Wall -Wno-unused-result
 SRC := samplers_amd/csrc/sp_dps.hip samplers_amd/csrc/sp_blur.hip samplers_amd/csrc/sp_latent.hip \
        samplers_amd/csrc/sp_groupnorm.hip samplers_amd/csrc/sp_conv.hip \
        samplers_amd/csrc/sp_wino.hip samplers_amd/csrc/sp_conv_thin.hip \
-       samplers_amd/csrc/sp_conv_s2.hip samplers_amd/csrc/sp_upsample.hip
+       samplers_amd/csrc/sp_conv_s2.hip samplers_amd/csrc/sp_upsample.hip \
+       samplers_amd/csrc/sp_attention.hip
 OBJ := $(patsubst samplers_amd/csrc/%.hip,build/%.o,$(SRC))
 LIB := samplers_amd/lib/libsamplers_hip.so
 

@@ -366,6 +366,22 @@ int sp_wino3x3_bwd_input(const float* dy, const float* up_vjp, int64_t n, int32_
                          int32_t cout, int32_t height, int32_t width, float* dx,
                          sp_stream_t stream);
 
+/* Fused self-attention softmax(q k^T * scale) v of the SD 1.5 eps-UNet's transformer blocks
+ * (attn1 over the latent tokens; diffusers UNet2DConditionModel, stable_diffusion.py:306-313;
+ * replaces the scores / softmax / weighted-sum chain and its autograd VJP) on fp32 MFMA,
+ * without materialising the score matrix.  q, k, v, out, dout, dq, dk, dv: [bh][n][d];
+ * lse, delta: [bh][n] (lse = row log-sum-exp, natural log, written by the forward; delta =
+ * rowsum(dout * out), written by the backward).  Self-attention only (m == n); head dims 40,
+ * 80, 160; n a multiple of the kernels' row blocks (see _supported).  The backward writes dq
+ * when dq != NULL and dk, dv when both are given. */
+int sp_attention_supported(int64_t bh, int64_t n, int64_t m, int32_t d);
+int sp_attention_fwd(const float* q, const float* k, const float* v, int64_t bh, int64_t n,
+                     int32_t d, float scale, float* out, float* lse, sp_stream_t stream);
+int sp_attention_bwd(const float* q, const float* k, const float* v, const float* out,
+                     const float* dout, const float* lse, int64_t bh, int64_t n, int32_t d,
+                     float scale, float* delta, float* dq, float* dk, float* dv,
+                     sp_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

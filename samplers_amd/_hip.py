@@ -125,6 +125,10 @@ SIGNATURES = {
     "sp_upsample2x_supported": (ctypes.c_int, [ctypes.c_int32] * 2),
     "sp_upsample2x": (ctypes.c_int, [_P, _I64, ctypes.c_int32, ctypes.c_int32, _P, _P]),
     "sp_upsample2x_vjp": (ctypes.c_int, [_P, _I64, ctypes.c_int32, ctypes.c_int32, _P, _P]),
+    "sp_attention_supported": (ctypes.c_int, [_I64, _I64, _I64, ctypes.c_int32]),
+    "sp_attention_fwd": (ctypes.c_int, [_P, _P, _P, _I64, _I64, ctypes.c_int32, _F, _P, _P, _P]),
+    "sp_attention_bwd": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _I64, _I64, ctypes.c_int32, _F,
+                                        _P, _P, _P, _P, _P]),
     "sp_conv3x3_s2_pack": (ctypes.c_int, [_P, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, _P, _P]),
     "sp_conv3x3_s2_fwd": (ctypes.c_int, [_P, _P, _P, _I64, ctypes.c_int32, ctypes.c_int32,
                                          ctypes.c_int32, ctypes.c_int32, _P, _P]),

@@ -45,7 +45,9 @@ struct ThinArgs {
 __device__ __forceinline__ void thin_block(int& tile, int& cob, int64_t& n) {
     const unsigned X = gridDim.x, Y = gridDim.y, T = X * Y * gridDim.z;
     unsigned l = blockIdx.x + X * (blockIdx.y + Y * blockIdx.z);
-    if (T % 8 == 0) l = (l % 8) * (T / 8) + l / 8;  // placement only: any order is correct
+    // (with several output-channel blocks the natural order already keeps a tile's blocks,
+    // X apart, on one XCD: remap single-block grids only)
+    if (Y == 1 && T % 8 == 0) l = (l % 8) * (T / 8) + l / 8;  // placement only: any order is correct
     tile = static_cast<int>(l % X);
     cob = static_cast<int>((l / X) % Y);
     n = l / (X * Y);

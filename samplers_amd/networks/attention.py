@@ -1,5 +1,10 @@
 """Multi-head attention for the latent prior with an O(N·d) memory footprint under autograd.
 
+Self-attention over the latent tokens runs on the fused fp32-MFMA kernels of
+``csrc/sp_attention.hip`` (the score matrix never reaches HBM; ``_FusedAttention``); the
+chunked GEMM path below serves the other calls (cross-attention to the 77-token context,
+other head dims) and ``SAMPLERS_AMD_LATENT_ATTN=gemm``.
+
 The SD 1.5 ε-UNet (``unet2d_condition.py``) runs self-attention over 64x64 = 4096 latent
 tokens with 8 heads per sample.  At the config-4 batch (32 latents) one layer's score
 matrix is 32·8·4096²·4 B = 17 GiB; autograd would keep the softmax of every such layer
@@ -57,37 +62,108 @@ class _RecomputeAttention(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dout: Tensor):
         q, k, v, out, lse = ctx.saved_tensors
-        scale = ctx.scale
+        return _gemm_backward(q, k, v, out, lse, dout.contiguous(), ctx.scale,
+                              ctx.needs_input_grad[:3])
+
+
+def _gemm_backward(q: Tensor, k: Tensor, v: Tensor, out: Tensor, lse: Tensor, dout: Tensor,
+                   scale: float, needs) -> tuple:
+    """The recompute-attention VJP on batched GEMMs, score blocks chunk by chunk."""
+    bh, n, _ = q.shape
+    m = k.shape[1]
+    need_q, need_k, need_v = needs
+    dq = torch.empty_like(q) if need_q else None
+    dk = torch.empty_like(k) if need_k else None
+    dv = torch.empty_like(v) if need_v else None
+    delta = (dout * out).sum(dim=-1)  # rowsum(do ∘ o) = rowsum(P ∘ dP)
+    step = _chunk_rows(bh, n, m)
+    for a in range(0, bh, step):
+        b = min(bh, a + step)
+        p = _scores(q[a:b], k[a:b], scale)
+        p.sub_(lse[a:b, :, None]).exp_()
+        if need_v:
+            torch.bmm(p.transpose(1, 2), dout[a:b], out=dv[a:b])
+        if not (need_q or need_k):
+            continue
+        dp = torch.bmm(dout[a:b], v[a:b].transpose(1, 2))
+        dp.sub_(delta[a:b, :, None]).mul_(p)  # dS
+        del p
+        if need_q:
+            torch.bmm(dp, k[a:b], out=dq[a:b]).mul_(scale)
+        if need_k:
+            torch.bmm(dp.transpose(1, 2), q[a:b], out=dk[a:b]).mul_(scale)
+    return dq, dk, dv
+
+
+# Under ~512 tokens the fused VJP kernels' grid is too small for them (one workgroup per 64
+# keys at d 160, one wave per SIMD) and the GEMM VJP wins: 256 tokens, d 160, 256 heads: 0.70
+# vs 0.45 ms per layer; 1024 tokens, d 80: 3.45 vs 3.85 (tools/bench_attention.py, MI355X).
+FUSED_BWD_MIN_TOKENS = 512
+
+
+class _FusedAttention(torch.autograd.Function):
+    """Self-attention on the fused fp32-MFMA kernels (``csrc/sp_attention.hip``): no score
+    matrix in HBM, forward or VJP; saves q, k, v, the output and the row log-sum-exp."""
+
+    @staticmethod
+    def forward(ctx, q: Tensor, k: Tensor, v: Tensor) -> Tensor:
+        from .. import _hip
+
+        lib = _hip.load_library()
+        bh, n, d = q.shape
+        scale = 1.0 / math.sqrt(d)
+        out = torch.empty_like(q)
+        lse = torch.empty(bh, n, device=q.device, dtype=q.dtype)
+        _hip.check(lib.sp_attention_fwd(_hip.ptr(q), _hip.ptr(k), _hip.ptr(v), bh, n, d, scale,
+                                        _hip.ptr(out), _hip.ptr(lse), _hip.stream_of(q)),
+                   "sp_attention_fwd")
+        ctx.save_for_backward(q, k, v, out, lse)
+        ctx.scale = scale
+        return out
+
+    @staticmethod
+    def backward(ctx, dout: Tensor):
+        from .. import _hip
+
+        q, k, v, out, lse = ctx.saved_tensors
+        lib = _hip.load_library()
+        bh, n, d = q.shape
         dout = dout.contiguous()
-        bh, n, _ = q.shape
-        m = k.shape[1]
         need_q, need_k, need_v = ctx.needs_input_grad[:3]
+        if n < FUSED_BWD_MIN_TOKENS:  # few tokens: the GEMM VJP is faster (tools/bench_attention.py)
+            return _gemm_backward(q, k, v, out, lse, dout, ctx.scale, (need_q, need_k, need_v))
         dq = torch.empty_like(q) if need_q else None
-        dk = torch.empty_like(k) if need_k else None
-        dv = torch.empty_like(v) if need_v else None
-        delta = (dout * out).sum(dim=-1)  # rowsum(do ∘ o) = rowsum(P ∘ dP)
-        step = _chunk_rows(bh, n, m)
-        for a in range(0, bh, step):
-            b = min(bh, a + step)
-            p = _scores(q[a:b], k[a:b], scale)
-            p.sub_(lse[a:b, :, None]).exp_()
-            if need_v:
-                torch.bmm(p.transpose(1, 2), dout[a:b], out=dv[a:b])
-            if not (need_q or need_k):
-                continue
-            dp = torch.bmm(dout[a:b], v[a:b].transpose(1, 2))
-            dp.sub_(delta[a:b, :, None]).mul_(p)  # dS
-            del p
-            if need_q:
-                torch.bmm(dp, k[a:b], out=dq[a:b]).mul_(scale)
-            if need_k:
-                torch.bmm(dp.transpose(1, 2), q[a:b], out=dk[a:b]).mul_(scale)
-        return dq, dk, dv
+        dk = torch.empty_like(k) if (need_k or need_v) else None
+        dv = torch.empty_like(v) if (need_k or need_v) else None
+        delta = torch.empty(bh, n, device=q.device, dtype=q.dtype)
+        _hip.check(lib.sp_attention_bwd(_hip.ptr(q), _hip.ptr(k), _hip.ptr(v), _hip.ptr(out),
+                                        _hip.ptr(dout), _hip.ptr(lse), bh, n, d, ctx.scale,
+                                        _hip.ptr(delta), _hip.ptr(dq), _hip.ptr(dk), _hip.ptr(dv),
+                                        _hip.stream_of(q)), "sp_attention_bwd")
+        return dq, (dk if need_k else None), (dv if need_v else None)
+
+
+def fused_supported(q: Tensor, k: Tensor) -> bool:
+    """The fused kernels serve this call (fp32 device self-attention at their head dims and
+    token counts; ``SAMPLERS_AMD_LATENT_ATTN=gemm`` forces the GEMM path)."""
+    if not (q.is_cuda and q.dtype == torch.float32 and k.dtype == torch.float32 and q.dim() == 3):
+        return False
+    if os.environ.get("SAMPLERS_AMD_LATENT_ATTN", "fused").lower() == "gemm":
+        return False
+    from .. import _hip
+
+    bh, n, d = q.shape
+    return k.shape == q.shape and bool(_hip.load_library().sp_attention_supported(bh, n, k.shape[1], d))
 
 
 def attention(q: Tensor, k: Tensor, v: Tensor) -> Tensor:
-    """softmax(q kᵀ/√d) v over (batch·heads, tokens, d) fp32 tensors; on the device the
-    score blocks are recomputed in the VJP instead of being kept (see the module doc)."""
+    """softmax(q kᵀ/√d) v over (batch·heads, tokens, d) fp32 tensors.  On the device:
+    self-attention at the fused kernels' shapes runs on them (``_FusedAttention``); other
+    calls (cross-attention to the 77-token context) recompute the score blocks in the VJP
+    instead of keeping them (see the module doc)."""
     if not q.is_cuda:
         return torch.softmax(_scores(q, k, 1.0 / math.sqrt(q.shape[-1])), dim=-1) @ v
-    return _RecomputeAttention.apply(q.contiguous(), k.contiguous(), v.contiguous())
+    q, k, v = q.contiguous(), k.contiguous(), v.contiguous()
+    if v.shape == q.shape and fused_supported(q, k):
+        return _FusedAttention.apply(q, k, v)
+    return _RecomputeAttention.apply(q, k, v)
