@@ -47,16 +47,16 @@ __device__ __forceinline__ void wino_in(const float (&d)[16], float (&v)[16]) {
 }
 
 // The same V on packed fp32 (v_pk_add_f32, two lanes per instruction).  Window row r is
-// held as two register pairs, e = (d[r][0], d[r][3]) and m = (d[r][1], d[r][2]) (one
-// ds_read2 each), so every step below is one packed add with operand swizzles:
+// held as its two natural register pairs, p = (d[r][0], d[r][1]) and q = (d[r][2], d[r][3])
+// (ds_read2 results, used in place: no register moves), so every step below is one packed
+// add with operand swizzles:
 //   t = B^T d on pairs:  t0 = d0 - d2, t1 = d1 + d2, t2 = d2 - d1, t3 = d1 - d3
-//   v = t B per row:     (v0, -v3) = e - (m.y, m.x),  (v1, v2) = m + (m.y, -m.x)
-// 16 instructions for the 4x4 window instead of 32 scalar ones.  Column 3 of V comes out
-// negated (exactly: IEEE subtraction is antisymmetric); the packed U carries the
-// compensating sign (k_wino3x3_pack), so U * V and the result are unchanged bit for bit.
+//   v = t B per row:     (v0, v1) = (p.x - q.x, p.y + q.x),  (v2, v3) = (q.x - p.y, p.y - q.y)
+// 16 instructions for the 4x4 window instead of 32 scalar ones; every element is the same
+// single IEEE add or subtract as the scalar transform (bit-identical).
 // (The compiler does not form the swizzled packed adds from vector code, so they are
 // written out.)
-struct WinRow { f32x2 e, m; };
+struct WinRow { f32x2 p, q; };
 
 __device__ __forceinline__ f32x2 pk_add(f32x2 a, f32x2 b) {  // a + b
     f32x2 r;
@@ -68,31 +68,31 @@ __device__ __forceinline__ f32x2 pk_sub(f32x2 a, f32x2 b) {  // a - b
     asm("v_pk_add_f32 %0, %1, %2 neg_lo:[0,1] neg_hi:[0,1]" : "=v"(r) : "v"(a), "v"(b));
     return r;
 }
-__device__ __forceinline__ f32x2 pk_sub_swap(f32x2 a, f32x2 b) {  // (a.x - b.y, a.y - b.x)
+__device__ __forceinline__ f32x2 pk_row01(f32x2 p, f32x2 q) {  // (p.x - q.x, p.y + q.x)
     f32x2 r;
-    asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0] neg_lo:[0,1] neg_hi:[0,1]"
-        : "=v"(r) : "v"(a), "v"(b));
+    asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,0] op_sel_hi:[1,0] neg_lo:[0,1]" : "=v"(r) : "v"(p), "v"(q));
     return r;
 }
-__device__ __forceinline__ f32x2 pk_sum_diff(f32x2 m) {  // (m.x + m.y, m.y - m.x)
+__device__ __forceinline__ f32x2 pk_row23(f32x2 p, f32x2 q) {  // (q.x - p.y, p.y - q.y)
     f32x2 r;
-    asm("v_pk_add_f32 %0, %1, %1 op_sel:[0,1] op_sel_hi:[1,0] neg_hi:[0,1]" : "=v"(r) : "v"(m));
+    asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,1] neg_lo:[0,1] neg_hi:[1,0]"
+        : "=v"(r) : "v"(q), "v"(p));
     return r;
 }
 
 __device__ __forceinline__ WinRow wpk_t(int k, const WinRow (&d)[4]) {  // row k of B^T d
     switch (k) {
-        case 0: return WinRow{pk_sub(d[0].e, d[2].e), pk_sub(d[0].m, d[2].m)};
-        case 1: return WinRow{pk_add(d[1].e, d[2].e), pk_add(d[1].m, d[2].m)};
-        case 2: return WinRow{pk_sub(d[2].e, d[1].e), pk_sub(d[2].m, d[1].m)};
-        default: return WinRow{pk_sub(d[1].e, d[3].e), pk_sub(d[1].m, d[3].m)};
+        case 0: return WinRow{pk_sub(d[0].p, d[2].p), pk_sub(d[0].q, d[2].q)};
+        case 1: return WinRow{pk_add(d[1].p, d[2].p), pk_add(d[1].q, d[2].q)};
+        case 2: return WinRow{pk_sub(d[2].p, d[1].p), pk_sub(d[2].q, d[1].q)};
+        default: return WinRow{pk_sub(d[1].p, d[3].p), pk_sub(d[1].q, d[3].q)};
     }
 }
 
-__device__ __forceinline__ void wpk_v(const WinRow& t, float* v) {  // row of t B (v3 negated)
-    const f32x2 a = pk_sub_swap(t.e, t.m);  // (t0 - t2, t3 - t1)
-    const f32x2 b = pk_sum_diff(t.m);       // (t1 + t2, t2 - t1)
-    v[0] = a.x, v[3] = a.y, v[1] = b.x, v[2] = b.y;
+__device__ __forceinline__ void wpk_v(const WinRow& t, float* v) {  // row of t B
+    const f32x2 a = pk_row01(t.p, t.q);  // (t0 - t2, t1 + t2)
+    const f32x2 b = pk_row23(t.p, t.q);  // (t2 - t1, t1 - t3)
+    v[0] = a.x, v[1] = a.y, v[2] = b.x, v[3] = b.y;
 }
 
 // U = G g G^T (4x4, row-major) for a 3x3 filter g, G = [[1,0,0],[.5,.5,.5],[.5,-.5,.5],[0,0,1]]
@@ -134,6 +134,10 @@ constexpr int WR_CO = 64;   // output channels per workgroup (2 waves x 32)
 #ifndef SP_WINO_EXP
 #define SP_WINO_EXP 0  // diagnostics only: 1 = no loads in the k loop, 2 = no output stores,
                        // 3 = no input transform (wrong results, timing only)
+#endif
+#ifndef SP_WINO_BURST
+#define SP_WINO_BURST 1  // the transform's placement in the k-step: 0 one row per MFMA gap, 1 one
+                         // burst, 2 two bursts (see wr_step)
 #endif
 #ifndef SP_WINO_SPLITK
 #define SP_WINO_SPLITK 1  // split K over two workgroups where the 8x8 mosaic leaves CUs idle
@@ -282,7 +286,7 @@ __device__ __forceinline__ void wr_stage_x(float* xw, const WxLane& xl, const Wr
 template <class GE>
 __device__ __forceinline__ WinRow wr_window_row(const float* xw, const WxLane& xl, int r) {
     const float* row = xw + xl.rd + GE::row(r);
-    return WinRow{f32x2{row[0], row[3]}, f32x2{row[1], row[2]}};
+    return WinRow{f32x2{row[0], row[1]}, f32x2{row[2], row[3]}};
 }
 
 struct WrRing {          // k-steps in flight
@@ -356,6 +360,7 @@ __device__ __forceinline__ void wr_step(const WrGeom& g, const WrSrc& cur, const
     d[2] = wr_window_row<GE>(xw, xl, 2);
     d[3] = wr_window_row<GE>(xw, xl, 3);
     WR_WALL;
+#if SP_WINO_BURST == 0
     WR_MFMA(7);
     WR_MFMA(8);
     // t = B^T d, one row (two packed adds) per gap
@@ -373,10 +378,46 @@ __device__ __forceinline__ void wr_step(const WrGeom& g, const WrSrc& cur, const
         WR_MFMA(13 + rr);
     }
     wpk_v(t[3], vn + 12);
+#elif SP_WINO_BURST == 1
+    // the whole transform as one burst: beside fp32 MFMAs the first VALU instruction of a gap
+    // costs ~14 cycles and each further one ~4-5 (tools/mfma_gap.hip), so one burst of 16
+    // packed adds costs about a third of 16 gaps with one each
+    WR_MFMA(7);
+    WR_MFMA(8);
+    WR_MFMA(9);
+    WR_MFMA(10);
+    WR_MFMA(11);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) t[k] = wpk_t(k, d);
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) wpk_v(t[rr], vn + 4 * rr);
+    WR_WALL;
+    WR_MFMA(12);
+    WR_MFMA(13);
+    WR_MFMA(14);
+    WR_MFMA(15);
+#else
+    // two bursts: t = B^T d after MFMA 9, v = t B after MFMA 13
+    WR_MFMA(7);
+    WR_MFMA(8);
+    WR_MFMA(9);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) t[k] = wpk_t(k, d);
+    WR_WALL;
+    WR_MFMA(10);
+    WR_MFMA(11);
+    WR_MFMA(12);
+    WR_MFMA(13);
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) wpk_v(t[rr], vn + 4 * rr);
+    WR_WALL;
+    WR_MFMA(14);
+    WR_MFMA(15);
+#endif
 #if SP_WINO_EXP == 3
 #pragma unroll
     for (int i = 0; i < 4; ++i)  // diagnostics: no input transform
-        vn[4 * i] = d[i].e.x, vn[4 * i + 1] = d[i].m.x, vn[4 * i + 2] = d[i].m.y, vn[4 * i + 3] = d[i].e.y;
+        vn[4 * i] = d[i].p.x, vn[4 * i + 1] = d[i].p.y, vn[4 * i + 2] = d[i].q.x, vn[4 * i + 3] = d[i].q.y;
 #endif
     WR_WALL;
 #undef WR_MFMA
@@ -593,8 +634,6 @@ __global__ void k_wino3x3_pack(const float* __restrict__ w, int cout, int cin, i
     const int orow = flip ? ci : co, kin = flip ? co : ci, cout_p = flip ? cin : cout;
     float u[16];
     wino_filter(g, u);
-#pragma unroll
-    for (int q = 0; q < 4; ++q) u[q * 4 + 3] = -u[q * 4 + 3];  // the packed transform's V column 3 is negated
     float* dst = up + (((int64_t)(kin >> 1) * (cout_p >> 5) + (orow >> 5)) * 64 +
                        32 * (kin & 1) + (orow & 31)) * 16;
 #pragma unroll

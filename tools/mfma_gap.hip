@@ -10,10 +10,36 @@
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
-template <int GAP>
+// filler kinds: 0 v_fma_f32, 1 v_pk_add_f32, 2 v_mov_b32, 3 v_add_u32, 4 ds_read_b128,
+// 5 ds_write_b64, 6 v_exp_f32
+template <int GAP, int KIND = 0>
 __device__ __forceinline__ void fillers(float (&f)[8], float b) {
+    typedef float f2 __attribute__((ext_vector_type(2)));
+    typedef float f4 __attribute__((ext_vector_type(4)));
+    __shared__ float lds[4096];
 #pragma unroll
-    for (int i = 0; i < GAP; ++i) asm volatile("v_fma_f32 %0, %1, %1, %0" : "+v"(f[i & 7]) : "v"(b));
+    for (int i = 0; i < GAP; ++i) {
+        if constexpr (KIND == 0) asm volatile("v_fma_f32 %0, %1, %1, %0" : "+v"(f[i & 7]) : "v"(b));
+        if constexpr (KIND == 1) {
+            f2 x{f[i & 7], f[(i + 1) & 7]};
+            asm volatile("v_pk_add_f32 %0, %0, %0" : "+v"(x));
+            f[i & 7] = x[0];
+        }
+        if constexpr (KIND == 2) asm volatile("v_mov_b32 %0, %1" : "=v"(f[i & 7]) : "v"(b));
+        if constexpr (KIND == 3) asm volatile("v_add_u32 %0, %0, %1" : "+v"(f[i & 7]) : "v"(b));
+        if constexpr (KIND == 4) {
+            f4 x;
+            asm volatile("ds_read_b128 %0, %1" : "=v"(x) : "v"((threadIdx.x & 63) * 16 + (i & 7) * 1024));
+            asm volatile("s_waitcnt lgkmcnt(8)" ::: "memory");
+            f[i & 7] += 0.f * x[0];
+        }
+        if constexpr (KIND == 5) {
+            f2 x{f[i & 7], b};
+            asm volatile("ds_write_b64 %0, %1" : : "v"((threadIdx.x & 63) * 8 + (i & 7) * 512), "v"(x) : "memory");
+        }
+        if constexpr (KIND == 6) asm volatile("v_exp_f32 %0, %1" : "=v"(f[i & 7]) : "v"(b));
+    }
+    if (b < -1e30f) lds[threadIdx.x] = f[0];
 }
 
 // 16x16x4: NM = 36 MFMAs per round (the F(4x4,3x3) k-step)
@@ -44,7 +70,7 @@ __global__ __launch_bounds__(256, 1) void k16(int iters, float* out) {
 }
 
 // 32x32x2: NM = 16 MFMAs per round (the F(2x2,3x3) k-step)
-template <int GAP>
+template <int GAP, int KIND = 0>
 __global__ __launch_bounds__(256, 1) void k32(int iters, float* out) {
     f32x16 acc[16];
 #pragma unroll
@@ -58,7 +84,34 @@ __global__ __launch_bounds__(256, 1) void k32(int iters, float* out) {
         for (int i = 0; i < 16; ++i) {
             acc[i] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc[i], 0, 0, 0);
             __builtin_amdgcn_sched_barrier(0);
-            fillers<GAP>(f, b);
+            fillers<GAP, KIND>(f, b);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    }
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) s += acc[i][0] + acc[i][15];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) s += f[i];
+    out[blockIdx.x * 256 + threadIdx.x] = s;
+}
+
+// bursts: GAP fillers after every EVERY-th MFMA (the same total as GAP / EVERY per gap)
+template <int GAP, int EVERY, int KIND = 0>
+__global__ __launch_bounds__(256, 1) void k32b(int iters, float* out) {
+    f32x16 acc[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[i] = f32x16{};
+    float a = threadIdx.x * 1e-3f, b = 1.0001f;
+    float f[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) f[i] = a + i;
+    for (int it = 0; it < iters; ++it) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            acc[i] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc[i], 0, 0, 0);
+            __builtin_amdgcn_sched_barrier(0);
+            if (i % EVERY == EVERY - 1) fillers<GAP, KIND>(f, b);
             __builtin_amdgcn_sched_barrier(0);
         }
     }
@@ -71,7 +124,8 @@ __global__ __launch_bounds__(256, 1) void k32(int iters, float* out) {
 }
 
 template <class K>
-static void run(const char* name, K kern, int nm, int gap, double flops_per_mfma, float* out, int cus) {
+static void run(const char* name, K kern, int nm, int gap, double flops_per_mfma, float* out, int cus,
+                const char* kind = "v_fma_f32") {
     const int iters = 2000;
     hipEvent_t e0, e1;
     hipEventCreate(&e0);
@@ -87,8 +141,8 @@ static void run(const char* name, K kern, int nm, int gap, double flops_per_mfma
     const double tf = mfmas * flops_per_mfma / (ms * 1e-3) / 1e12;
     // cycles per MFMA at 2.4 GHz nominal (the chip may run slower under load)
     const double cyc = (ms * 1e-3) * 2.4e9 / ((double)iters * nm);
-    printf("{\"shape\": \"%s\", \"gap_fma\": %d, \"tflops\": %.1f, \"cycles_per_mfma_at_2.4GHz\": %.1f}\n",
-           name, gap, tf, cyc);
+    printf("{\"shape\": \"%s\", \"filler\": \"%s\", \"per_gap\": %d, \"tflops\": %.1f, "
+           "\"cycles_per_mfma_at_2.4GHz\": %.1f}\n", name, kind, gap, tf, cyc);
 }
 
 int main() {
@@ -109,6 +163,26 @@ int main() {
     run("32x32x2", k32<12>, 16, 12, 4096, out, cus);
     run("32x32x2", k32<16>, 16, 16, 4096, out, cus);
     run("32x32x2", k32<24>, 16, 24, 4096, out, cus);
+    const char* kinds[] = {"v_fma_f32", "v_pk_add_f32", "v_mov_b32", "v_add_u32", "ds_read_b128",
+                           "ds_write_b64", "v_exp_f32"};
+    run("32x32x2", k32<4, 1>, 16, 4, 4096, out, cus, kinds[1]);
+    run("32x32x2", k32<4, 2>, 16, 4, 4096, out, cus, kinds[2]);
+    run("32x32x2", k32<4, 3>, 16, 4, 4096, out, cus, kinds[3]);
+    run("32x32x2", k32<2, 4>, 16, 2, 4096, out, cus, kinds[4]);
+    run("32x32x2", k32<4, 4>, 16, 4, 4096, out, cus, kinds[4]);
+    run("32x32x2", k32<2, 5>, 16, 2, 4096, out, cus, kinds[5]);
+    run("32x32x2", k32<4, 5>, 16, 4, 4096, out, cus, kinds[5]);
+    run("32x32x2", k32<4, 6>, 16, 4, 4096, out, cus, kinds[6]);
+    run("32x32x2", k32<1, 0>, 16, 1, 4096, out, cus, kinds[0]);
+    run("32x32x2", k32<2, 0>, 16, 2, 4096, out, cus, kinds[0]);
+    run("32x32x2", k32<1, 1>, 16, 1, 4096, out, cus, kinds[1]);
+    run("32x32x2", k32<2, 1>, 16, 2, 4096, out, cus, kinds[1]);
+    run("32x32x2 burst/2", k32b<4, 2>, 16, 4, 4096, out, cus, kinds[0]);
+    run("32x32x2 burst/4", k32b<8, 4>, 16, 8, 4096, out, cus, kinds[0]);
+    run("32x32x2 burst/8", k32b<16, 8>, 16, 16, 4096, out, cus, kinds[0]);
+    run("32x32x2 burst/16", k32b<32, 16>, 16, 32, 4096, out, cus, kinds[0]);
+    run("32x32x2 burst/4", k32b<4, 4>, 16, 4, 4096, out, cus, kinds[1]);
+    run("32x32x2 burst/8", k32b<8, 8>, 16, 8, 4096, out, cus, kinds[1]);
     hipFree(out);
     return 0;
 }
