@@ -185,7 +185,8 @@ struct WrTile {                       // one tile: 64 channels x 8 x 32 outputs 
 struct WrSrc {                        // a tile's load sources
     __amdgpu_buffer_rsrc_t rs;        // the image's input planes
     int oa, ob, oh;                   // byte offsets of this lane's pieces (or OOB)
-    const float* ub;                  // this lane's packed U rows at k-step 0
+    int uso;                          // byte offset of the wave's packed U rows at k-step 0
+                                      // (wave-uniform; a lane adds lane * 64)
 };
 struct WrGeom {
     int64_t batch;
@@ -256,8 +257,9 @@ __device__ __forceinline__ WrSrc wr_src(const WrGeom& g, const WrTile& ti, int w
     s.oa = goff(rca, ti.ow0 + 4 * ka);
     s.ob = goff(rcb, ti.ow0 + 4 * ka);
     s.oh = GE::MOSAIC ? OOB : goff(rch, side ? ti.ow0 + 2 * GE::TCW : ti.ow0 - 1);
-    s.ub = g.up + (GE::SPLIT ? (int64_t)ti.kh * g.nsteps * g.u_step : 0) +
-           ((int64_t)(ti.co0 >> 5) * 64 + lane) * 16;
+    s.uso = __builtin_amdgcn_readfirstlane(
+        static_cast<int>(((GE::SPLIT ? (int64_t)ti.kh * g.nsteps * g.u_step : 0) +
+                          (int64_t)(ti.co0 >> 5) * 64 * 16) * 4));
     return s;
 }
 
@@ -267,9 +269,15 @@ __device__ __forceinline__ void wr_load_x(const WrSrc& s, int so, WrX& x) {
     x.h = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(s.rs, s.oh, so, 0));
 }
 
-__device__ __forceinline__ void wr_load_u(const float* __restrict__ src, WrU& u) {
+// U rows of k-step `step` by buffer loads: the lane's offset is a fixed VGPR (lane * 64), the
+// step's a scalar — no per-step vector address arithmetic beside the MFMAs.
+__device__ __forceinline__ f32x4 wr_u4(__amdgpu_buffer_rsrc_t urs, int lane, int soff, int i) {
+    return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(urs, lane * 64 + 16 * i, soff, 0));
+}
+
+__device__ __forceinline__ void wr_load_u(__amdgpu_buffer_rsrc_t urs, int lane, int soff, WrU& u) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) u.u[i] = reinterpret_cast<const f32x4*>(src)[i];
+    for (int i = 0; i < 4; ++i) u.u[i] = wr_u4(urs, lane, soff, i);
 }
 
 // Block piece -> LDS (columns in natural order; dword pairs, so no register shuffles).
@@ -310,8 +318,8 @@ struct WrRing {          // k-steps in flight
 // this tile's epilogue.
 template <class GE, int K, bool FIRST, bool XN, bool UN>
 __device__ __forceinline__ void wr_step(const WrGeom& g, const WrSrc& cur, const WrSrc& nxt,
-                                        float* xw, const WxLane& xl, int q, WrRing& r,
-                                        f32x16 (&acc)[16]) {
+                                        __amdgpu_buffer_rsrc_t urs, int lane, float* xw,
+                                        const WxLane& xl, int q, WrRing& r, f32x16 (&acc)[16]) {
     const WrU& u = r.us[K];
     const float(&vc)[16] = r.v[K & 1];
     float(&vn)[16] = r.v[(K + 1) & 1];
@@ -330,17 +338,17 @@ __device__ __forceinline__ void wr_step(const WrGeom& g, const WrSrc& cur, const
 #endif
     WR_WALL;
     WR_MFMA(1);
-    const float* usrc = (UN ? nxt.ub : cur.ub) + (UN ? q + 2 - g.nsteps : q + 2) * g.u_step;
+    const int uso = (UN ? nxt.uso : cur.uso) + (UN ? q + 2 - g.nsteps : q + 2) * g.u_step * 4;
     WrU& un = r.us[(K + 2) % 4];
 #if SP_WINO_EXP != 1
-    un.u[0] = reinterpret_cast<const f32x4*>(usrc)[0];
-    un.u[1] = reinterpret_cast<const f32x4*>(usrc)[1];
+    un.u[0] = wr_u4(urs, lane, uso, 0);
+    un.u[1] = wr_u4(urs, lane, uso, 1);
 #endif
     WR_WALL;
     WR_MFMA(2);
 #if SP_WINO_EXP != 1
-    un.u[2] = reinterpret_cast<const f32x4*>(usrc)[2];
-    un.u[3] = reinterpret_cast<const f32x4*>(usrc)[3];
+    un.u[2] = wr_u4(urs, lane, uso, 2);
+    un.u[3] = wr_u4(urs, lane, uso, 3);
 #endif
     WR_WALL;
     WR_MFMA(3);
@@ -559,6 +567,10 @@ __global__ __launch_bounds__(kBlock, 1) void k_wino3x3_r(WrGeom g) {
             xl.rd = (lane >> 5) * GE::CI + GE::row(2 * (l / GE::TCW)) + 3 + 2 * (l % GE::TCW);
         }
     }
+    // all of packed U: (cin / 2) k-steps of u_step floats
+    const auto urs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(g.up), (short)0,
+                                                       g.nsteps * g.ksplit * static_cast<int>(g.u_step) * 4,
+                                                       0x00020000);
     int t = blockIdx.x;
     const int stride = gridDim.x;
     WrTile ti = wr_tile<GE>(g, t, wv);
@@ -573,11 +585,11 @@ __global__ __launch_bounds__(kBlock, 1) void k_wino3x3_r(WrGeom g) {
     __builtin_amdgcn_sched_barrier(0);
     wr_load_x(cur, g.so_step, r.xs[1]);
     __builtin_amdgcn_sched_barrier(0);
-    wr_load_u(cur.ub, r.us[0]);
+    wr_load_u(urs, lane, cur.uso, r.us[0]);
     __builtin_amdgcn_sched_barrier(0);
     wr_load_x(cur, 2 * g.so_step, r.xs[2]);
     __builtin_amdgcn_sched_barrier(0);
-    wr_load_u(cur.ub + g.u_step, r.us[1]);
+    wr_load_u(urs, lane, cur.uso + g.u_step * 4, r.us[1]);
     __builtin_amdgcn_sched_barrier(0);
     {
         wr_stage_x(xw, xl, r.xs[0]);
@@ -590,15 +602,15 @@ __global__ __launch_bounds__(kBlock, 1) void k_wino3x3_r(WrGeom g) {
     f32x16 acc[16];
     const int last = g.nsteps - 4;  // >= 4 (cin >= 16)
     for (;;) {
-        wr_step<GE, 0, true, false, false>(g, cur, nxt, xw, xl, 0, r, acc);
-        wr_step<GE, 1, false, false, false>(g, cur, nxt, xw, xl, 1, r, acc);
-        wr_step<GE, 2, false, false, false>(g, cur, nxt, xw, xl, 2, r, acc);
-        wr_step<GE, 3, false, false, false>(g, cur, nxt, xw, xl, 3, r, acc);
+        wr_step<GE, 0, true, false, false>(g, cur, nxt, urs, lane, xw, xl, 0, r, acc);
+        wr_step<GE, 1, false, false, false>(g, cur, nxt, urs, lane, xw, xl, 1, r, acc);
+        wr_step<GE, 2, false, false, false>(g, cur, nxt, urs, lane, xw, xl, 2, r, acc);
+        wr_step<GE, 3, false, false, false>(g, cur, nxt, urs, lane, xw, xl, 3, r, acc);
         for (int p = 4; p < last; p += 4) {
-            wr_step<GE, 0, false, false, false>(g, cur, nxt, xw, xl, p + 0, r, acc);
-            wr_step<GE, 1, false, false, false>(g, cur, nxt, xw, xl, p + 1, r, acc);
-            wr_step<GE, 2, false, false, false>(g, cur, nxt, xw, xl, p + 2, r, acc);
-            wr_step<GE, 3, false, false, false>(g, cur, nxt, xw, xl, p + 3, r, acc);
+            wr_step<GE, 0, false, false, false>(g, cur, nxt, urs, lane, xw, xl, p + 0, r, acc);
+            wr_step<GE, 1, false, false, false>(g, cur, nxt, urs, lane, xw, xl, p + 1, r, acc);
+            wr_step<GE, 2, false, false, false>(g, cur, nxt, urs, lane, xw, xl, p + 2, r, acc);
+            wr_step<GE, 3, false, false, false>(g, cur, nxt, urs, lane, xw, xl, p + 3, r, acc);
         }
         WrRes rv;
         if constexpr (RES) {
@@ -606,10 +618,10 @@ __global__ __launch_bounds__(kBlock, 1) void k_wino3x3_r(WrGeom g) {
             __builtin_amdgcn_sched_barrier(0);
         }
         // last four steps: the ring starts fetching the next tile's steps 0..2 / 0..1
-        wr_step<GE, 0, false, false, false>(g, cur, nxt, xw, xl, last + 0, r, acc);
-        wr_step<GE, 1, false, true, false>(g, cur, nxt, xw, xl, last + 1, r, acc);
-        wr_step<GE, 2, false, true, true>(g, cur, nxt, xw, xl, last + 2, r, acc);
-        wr_step<GE, 3, false, true, true>(g, cur, nxt, xw, xl, last + 3, r, acc);
+        wr_step<GE, 0, false, false, false>(g, cur, nxt, urs, lane, xw, xl, last + 0, r, acc);
+        wr_step<GE, 1, false, true, false>(g, cur, nxt, urs, lane, xw, xl, last + 1, r, acc);
+        wr_step<GE, 2, false, true, true>(g, cur, nxt, urs, lane, xw, xl, last + 2, r, acc);
+        wr_step<GE, 3, false, true, true>(g, cur, nxt, urs, lane, xw, xl, last + 3, r, acc);
         wr_epilogue<GE, RES>(g, ti, wv, lane, acc, rv);
         t = tn;
         if (t >= g.ntiles) break;
