@@ -47,7 +47,7 @@ def main():
     p.add_argument("--batch", type=int, default=32)
     p.add_argument("--image", type=int, default=512)
     p.add_argument("--steps", type=int, default=3)
-    p.add_argument("--warmup", type=int, default=1)
+    p.add_argument("--warmup", type=int, default=2)
     p.add_argument("--heartbeat", default="gpurun_out/psld_heartbeat.log")
     args = p.parse_args()
     Path(args.heartbeat).parent.mkdir(parents=True, exist_ok=True)
