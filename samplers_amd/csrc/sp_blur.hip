@@ -443,7 +443,10 @@ __device__ __forceinline__ void wave_lds_sync() {
 // register moves shift them.
 // ---------------------------------------------------------------------------
 constexpr int DCH = 2;            // rows per chunk
-constexpr int DSLOT = 4;          // ring slots: DSLOT - 1 chunks in flight
+#ifndef SP_BLUR_SLOTS
+#define SP_BLUR_SLOTS 4
+#endif
+constexpr int DSLOT = SP_BLUR_SLOTS;  // ring slots: DSLOT - 1 chunks in flight
 constexpr int DROWS = 3 * DCH;    // x, eps, y rows per slot
 constexpr int DRING = DSLOT * DROWS * SWID;
 
@@ -460,13 +463,15 @@ __device__ __forceinline__ void dma_row(__amdgpu_buffer_rsrc_t rsrc, uint32_t vo
         : "memory");
 }
 
-// s_waitcnt vmcnt(n) for the even n a chunk can leave younger (<= 24)
+// s_waitcnt vmcnt(n) for the even n a chunk can leave younger (<= 62, the counter's range)
 __device__ __forceinline__ void wait_vm(int n) {
     switch (n) {
 #define SP_VM(N) \
     case N: asm volatile("s_waitcnt vmcnt(" #N ")" ::: "memory"); break;
         SP_VM(0) SP_VM(2) SP_VM(4) SP_VM(6) SP_VM(8) SP_VM(10) SP_VM(12) SP_VM(14)
-        SP_VM(16) SP_VM(18) SP_VM(20) SP_VM(22) SP_VM(24)
+        SP_VM(16) SP_VM(18) SP_VM(20) SP_VM(22) SP_VM(24) SP_VM(26) SP_VM(28) SP_VM(30)
+        SP_VM(32) SP_VM(34) SP_VM(36) SP_VM(38) SP_VM(40) SP_VM(42) SP_VM(44) SP_VM(46)
+        SP_VM(48) SP_VM(50) SP_VM(52) SP_VM(54) SP_VM(56) SP_VM(58) SP_VM(60) SP_VM(62)
 #undef SP_VM
         default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
@@ -492,7 +497,7 @@ __global__ __launch_bounds__(64) void k_blur_dps_dma(
     constexpr int K = 2 * R + 1, CH = DCH, WIN = CH + 2 * R, NCH = (SSEG + 4 * R) / CH;
     constexpr int C2 = (2 * R) / CH, C3 = (4 * R) / CH, PER = WIN / gcd_c(WIN, CH);
     static_assert(SSEG % CH == 0 && (4 * R) % CH == 0 && R >= 1 && R <= SPAD, "dma geometry");
-    static_assert(DROWS * (DSLOT - 1) + CH * (DSLOT - 1) <= 24 && DROWS % 2 == 0 && CH % 2 == 0, "vmcnt cases");
+    static_assert(DROWS * (DSLOT - 1) + CH * (DSLOT - 1) <= 62 && DROWS % 2 == 0 && CH % 2 == 0, "vmcnt cases");
     if (sched) {
         const sp_dps_coefs& cf = sched[*cursor].c;
         a = cf.a, k = cf.k, gs = cf.grad_scale;
