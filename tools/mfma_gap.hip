@@ -123,6 +123,34 @@ __global__ __launch_bounds__(256, 1) void k32b(int iters, float* out) {
     out[blockIdx.x * 256 + threadIdx.x] = s;
 }
 
+// k-step models: F(4x4,3x3) = 36 x 16x16x4 MFMAs + NPK packed adds in NB bursts;
+// F(2x2,3x3) = 16 x 32x32x2 MFMAs + 16 packed adds in one burst (the current tile)
+template <int NPK, int NB>
+__global__ __launch_bounds__(256, 1) void kf43(int iters, float* out) {
+    f32x4 acc[36];
+#pragma unroll
+    for (int i = 0; i < 36; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    float a = threadIdx.x * 1e-3f, b = 1.0001f;
+    float f[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) f[i] = a + i;
+    for (int it = 0; it < iters; ++it) {
+#pragma unroll
+        for (int i = 0; i < 36; ++i) {
+            acc[i] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc[i], 0, 0, 0);
+            __builtin_amdgcn_sched_barrier(0);
+            if ((i + 1) % (36 / NB) == 0) fillers<NPK / NB, 1>(f, b);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    }
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < 36; ++i) s += acc[i][0] + acc[i][3];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) s += f[i];
+    out[blockIdx.x * 256 + threadIdx.x] = s;
+}
+
 template <class K>
 static void run(const char* name, K kern, int nm, int gap, double flops_per_mfma, float* out, int cus,
                 const char* kind = "v_fma_f32") {
@@ -183,6 +211,11 @@ int main() {
     run("32x32x2 burst/16", k32b<32, 16>, 16, 32, 4096, out, cus, kinds[0]);
     run("32x32x2 burst/4", k32b<4, 4>, 16, 4, 4096, out, cus, kinds[1]);
     run("32x32x2 burst/8", k32b<8, 8>, 16, 8, 4096, out, cus, kinds[1]);
+    run("32x32x2 burst/16 (F23 k-step: 16 pk)", k32b<16, 16>, 16, 16, 4096, out, cus, kinds[1]);
+    run("16x16x4 F43 k-step: 96 pk in 4 bursts", kf43<96, 4>, 36, 96, 2048, out, cus, kinds[1]);
+    run("16x16x4 F43 k-step: 96 pk in 2 bursts", kf43<96, 2>, 36, 96, 2048, out, cus, kinds[1]);
+    run("16x16x4 F43 k-step: 72 pk in 4 bursts", kf43<72, 4>, 36, 72, 2048, out, cus, kinds[1]);
+    run("16x16x4 F43 k-step: 0 pk", kf43<0, 4>, 36, 0, 2048, out, cus, kinds[1]);
     hipFree(out);
     return 0;
 }
