@@ -442,7 +442,10 @@ __device__ __forceinline__ void wave_lds_sync() {
 // period WIN / gcd(WIN, DCH) (the chunk body is instantiated per phase), so no
 // register moves shift them.
 // ---------------------------------------------------------------------------
-constexpr int DCH = 2;            // rows per chunk
+#ifndef SP_BLUR_CHUNK
+#define SP_BLUR_CHUNK 2
+#endif
+constexpr int DCH = SP_BLUR_CHUNK;  // rows per chunk
 #ifndef SP_BLUR_SLOTS
 #define SP_BLUR_SLOTS 4
 #endif
