@@ -87,16 +87,22 @@ def log(msg: str) -> None:
 
 
 def setup_dist(gpus: int):
+    """One rank per GPU over RCCL (backend "nccl").  SAMPLERS_AMD_DIST_BACKEND=gloo is a
+    rehearsal mode for a box with fewer GPUs than ranks: ranks share devices round-robin
+    and the collectives go through host memory (not a measurement configuration)."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != gpus:
         raise SystemExit(f"--gpus {gpus} but WORLD_SIZE={world}")
+    backend = os.environ.get("SAMPLERS_AMD_DIST_BACKEND", "nccl")
+    if backend == "gloo":
+        local %= torch.cuda.device_count()
     torch.cuda.set_device(local)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", rank=rank, world_size=world,
-                                device_id=torch.device("cuda", local))
+        extra = {"device_id": torch.device("cuda", local)} if backend == "nccl" else {}
+        dist.init_process_group(backend, rank=rank, world_size=world, **extra)
     return rank, world, torch.device("cuda", local)
 
 

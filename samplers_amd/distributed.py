@@ -7,10 +7,16 @@ index (``sample_offset``), which makes the result bit-identical to the
 single-GPU run whatever the world size.  The only collective is one RCCL
 ``all_gather`` of the x-hat shards at the end (over xGMI; ``backend="nccl"`` is
 RCCL on ROCm), plus a 8-byte broadcast of the seed at the start.
+
+PSLD and ReSample couple the batch through their norms (``psld.py:130,138``,
+``resample_kernels.py:26,67``: one scalar over the whole flat batch); their samplers take
+a ``group`` and sum those scalars over it (``all_reduce_sum_``, a few bytes per step), so
+the sharded run equals the single-process one up to the summation order of the norms.
 """
 
 from __future__ import annotations
 
+import inspect
 from typing import Callable
 
 import torch
@@ -62,15 +68,31 @@ def all_reduce_sum_(t: Tensor, group=None) -> Tensor:
     return t
 
 
+def _parameters(fn) -> dict:
+    try:
+        return dict(inspect.signature(fn).parameters)
+    except (TypeError, ValueError):
+        return {}
+
+
 def sharded_call(sampler: Callable[..., Tensor], inverse_problem: InverseProblem, *,
                  num_reconstructions: int = 1, seed: int | None = None, group=None,
                  **kwargs) -> Tensor:
     """Run ``sampler`` on this rank's block of observations and all-gather x-hat.
 
-    ``sampler`` is a posterior sampler accepting ``seed``/``sample_offset``/
-    ``keep_reconstruction_dim`` (``DPSSampler``).  Returns the same tensor the
-    single-process call would, on every rank.
+    ``sampler`` is a posterior sampler accepting ``seed``/``sample_offset``.  One that also
+    names a ``group`` parameter (``PSLDSampler``, ``ReSampleSampler``: batch-coupled norms)
+    receives ``group`` (narrowed to the ranks that hold observations when there are more
+    ranks than observations, so an idle rank is never waited for in the per-step norm
+    reductions); one with ``keep_reconstruction_dim`` (``DPSSampler``, ``PGDMSampler``)
+    squeezes an R = 1 axis exactly as its single-process call would.  Returns the same
+    tensor the single-process call would, on every rank.
     """
+    params = _parameters(sampler)
+    coupled = "group" in params
+    keep = bool(kwargs.pop("keep_reconstruction_dim", False))
+    squeezes = "keep_reconstruction_dim" in params or any(
+        v.kind is inspect.Parameter.VAR_KEYWORD for v in params.values())
     world = dist.get_world_size(group) if dist.is_initialized() else 1
     rank = dist.get_rank(group) if dist.is_initialized() else 0
     obs = inverse_problem.observation
@@ -83,17 +105,24 @@ def sharded_call(sampler: Callable[..., Tensor], inverse_problem: InverseProblem
     start, stop = shard_bounds(total, rank, world)
     seed = broadcast_seed(seed, obs.device, group)
     local = InverseProblem(inverse_problem.operator, obs[start:stop], inverse_problem.noise)
+    counts = [b - a for a, b in (shard_bounds(total, r, world) for r in range(world))]
     if stop > start:
+        if coupled:
+            kwargs["group"] = group
+            active = [r for r, c in enumerate(counts) if c > 0]
+            if len(active) < world:  # only the active ranks create (and use) the subgroup
+                ranks = [r if group is None else dist.get_global_rank(group, r) for r in active]
+                kwargs["group"] = dist.new_group(ranks, use_local_synchronization=True)
+        if squeezes:
+            kwargs["keep_reconstruction_dim"] = True
         out = sampler(local, num_reconstructions=num_reconstructions, seed=seed,
-                      sample_offset=start * num_reconstructions, keep_reconstruction_dim=True,
-                      **kwargs)
+                      sample_offset=start * num_reconstructions, **kwargs)
     else:  # more ranks than observations: this rank only joins the gather
         out = torch.empty((0, num_reconstructions, *inverse_problem.operator.x_shape),
                           device=obs.device, dtype=torch.float32)
-    counts = [b - a for a, b in (shard_bounds(total, r, world) for r in range(world))]
     full = gather_shards(out.contiguous(), counts, group)
     if not batch_shape:
         full = full.squeeze(0)
-    if num_reconstructions == 1:
+    if squeezes and num_reconstructions == 1 and not keep:
         full = full.squeeze(len(batch_shape))
     return full

@@ -147,3 +147,47 @@ def test_batch_global_norms_match_single_process(tmp_path):
     assert torch.equal(sharded["rs_grad"], single["rs_grad"])  # per-sample: bit-identical
     r0, xe = sharded["x_eff_rows"]
     assert torch.equal(xe, single["x_eff_rows"][1][r0:r0 + xe.shape[0]])
+
+
+# --- sharded_call with a batch-coupled sampler (group-taking, never squeezes R) -----------
+
+def coupled_sampler(problem, *, num_reconstructions, seed, sample_offset, group=None):
+    """A PSLD-like sampler: every sample is scaled by a batch-global sum of squares,
+    reduced over ``group`` three times (one per 'step'); the R axis is always kept."""
+    from samplers_amd.distributed import all_reduce_sum_
+
+    obs = problem.observation
+    x = obs.repeat_interleave(num_reconstructions, 0)
+    for _ in range(3):
+        ss = all_reduce_sum_(x.square().sum().reshape(1), group)
+        x = x / ss.sqrt()
+    return x.reshape(obs.shape[0], num_reconstructions, *SHAPE)
+
+
+def _coupled_worker(rank, world, port, batch, R, result_path):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        obs = torch.arange(1, batch * N + 1, dtype=torch.float32).reshape(batch, *SHAPE)
+        prob = InverseProblem(IdentityOperator(SHAPE), obs, GaussianNoise(0.1))
+        out = sharded_call(coupled_sampler, prob, num_reconstructions=R, seed=3)
+        if rank == 0:
+            torch.save(out, result_path)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,batch,R", [(2, 5, 1), (3, 2, 2)])
+def test_sharded_coupled_sampler_equals_single_process(tmp_path, world, batch, R):
+    """(3, 2, 2): one rank holds no observation and must not be waited for by the others'
+    per-step reductions (they reduce over the subgroup of active ranks)."""
+    path = tmp_path / "out.pt"
+    mp.spawn(_coupled_worker, args=(world, _free_port(), batch, R, str(path)), nprocs=world,
+             join=True)
+    sharded = torch.load(path, weights_only=True)
+    obs = torch.arange(1, batch * N + 1, dtype=torch.float32).reshape(batch, *SHAPE)
+    prob = InverseProblem(IdentityOperator(SHAPE), obs, GaussianNoise(0.1))
+    single = sharded_call(coupled_sampler, prob, num_reconstructions=R, seed=3)
+    assert single.shape == (batch, R, *SHAPE)  # R kept, as the coupled samplers do
+    assert sharded.shape == single.shape
+    assert torch.allclose(sharded, single, rtol=1e-6, atol=0)

@@ -1,15 +1,22 @@
 """PSLD benchmark (BASELINE.json configs[3], "config 4"): latent-space inpainting at 512².
 
-    python tools/bench_psld.py [--batch 32 --steps 3 --warmup 1]
+    python tools/bench_psld.py [--batch 32 --steps 3 --warmup 2]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 \
+        tools/bench_psld.py --gpus N            (batch per rank; RCCL all-reduce of the norms)
 
 Workload: PSLD (psld.py:118-153) with a centre-inpainting mask on 3x512x512 images,
 GaussianNoise(0.05), SD 1.5 VAE architecture (83.65 M parameters) + SD 1.5
 UNet2DConditionModel (859.5 M, null 77x768 context), random weights with fixed seeds, fp32, 100-step schedule (psld.py:50).  One
 step = one PSLD iteration over the batch: latent UNet forward, VAE decode forward,
 HIP pixel pass, VAE encode forward, encode/decode/UNet VJPs, HIP glue and update
-(samplers_amd.samplers.psld.FusedPSLDStep).  Prints one JSON line; "vae_tflops" is
+(samplers_amd.samplers.psld.FusedPSLDStep).  Prints one JSON line; "vae_tflops" (per GPU) is
 the algorithmic VAE work (7.13 TFLOP per sample-step) over the step
 time, an upper bound on what the VAE convolutions achieve.
+
+With N ranks each holds ``--batch`` samples of a global batch of N x batch (sample
+offset rank x batch for the Philox noise) and the step's two batch-global norms
+(psld.py:130,138) are summed over ranks by one 8-byte all-reduce; value = N x batch x K /
+the max-over-ranks wall time of the K timed steps (weak scaling, as bench.py).
 """
 
 from __future__ import annotations
@@ -26,6 +33,9 @@ sys.path.insert(0, str(ROOT))
 import samplers_amd  # noqa: E402,F401
 
 import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+from bench import setup_dist  # noqa: E402
 
 VAE_FLOP_PER_SAMPLE = 7.13e12
 # SD 1.5 UNet at 64x64 latents: 0.80 TFLOP forward + 0.92 input VJP (torch FlopCounterMode)
@@ -44,7 +54,8 @@ def heartbeat(path: Path, every: float = 30.0) -> None:
 
 def main():
     p = argparse.ArgumentParser()
-    p.add_argument("--batch", type=int, default=32)
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--batch", type=int, default=32, help="samples per rank")
     p.add_argument("--image", type=int, default=512)
     p.add_argument("--steps", type=int, default=3)
     p.add_argument("--warmup", type=int, default=2)
@@ -53,7 +64,8 @@ def main():
     Path(args.heartbeat).parent.mkdir(parents=True, exist_ok=True)
     heartbeat(Path(args.heartbeat))
     torch.backends.cudnn.benchmark = False
-    dev = torch.device("cuda:0")
+    rank, world, dev = setup_dist(args.gpus)
+    group = dist.group.WORLD if world > 1 else None
 
     from samplers_amd import _hip
     from samplers_amd.inverse_problem import InverseProblem
@@ -66,7 +78,7 @@ def main():
     _hip.load_library()
     shape = (3, args.image, args.image)
     op = CenterInpaintingOperator(shape, 0.5).to(dev)
-    gen = torch.Generator().manual_seed(1000)
+    gen = torch.Generator().manual_seed(1000 + rank)
     x_true = (torch.rand((args.batch, *shape), generator=gen) * 2 - 1).to(dev)
     y = op.apply(x_true)
     y = y + (0.05 * torch.randn(tuple(y.shape), generator=gen)).to(dev)
@@ -75,44 +87,61 @@ def main():
     net.set_condition(StableDiffusionCondition(prompt=[""] * args.batch))  # reference default prompt, CFG collapses
     problem = InverseProblem(op, y, GaussianNoise(0.05).to(dev))
     lat = tuple(net.get_latent_shape(shape))
-    step = FusedPSLDStep(net, problem, y.reshape(args.batch, -1), 1, lat)
-    seed = 20260101
-    z = initial_sample((args.batch, *lat), dev, rng="philox", seed=seed, sample_offset=0,
+    step = FusedPSLDStep(net, problem, y.reshape(args.batch, -1), 1, lat, group=group)
+    seed, off = 20260101, rank * args.batch
+    z = initial_sample((args.batch, *lat), dev, rng="philox", seed=seed, sample_offset=off,
                        noise_fn=None)
     ts = net.timesteps_host
     it = iter(range(len(ts) - 1, 1, -1))
 
     def one():
         i = next(it)
-        step(z, i, ts[i], ts[i - 1], ts[0], seed=seed)
+        step(z, i, ts[i], ts[i - 1], ts[0], seed=seed, sample_offset=off)
 
     t0 = time.perf_counter()
     for k in range(args.warmup):
         one()
         torch.cuda.synchronize()
-        print(f"[psld] warmup {k + 1} done at {time.perf_counter() - t0:.1f}s", file=sys.stderr,
-              flush=True)
+        if rank == 0:
+            print(f"[psld] warmup {k + 1} done at {time.perf_counter() - t0:.1f}s",
+                  file=sys.stderr, flush=True)
     torch.cuda.reset_peak_memory_stats()
+    if world > 1:
+        dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for k in range(args.steps):
         one()
         torch.cuda.synchronize()
-        print(f"[psld] step {k + 1} at {time.perf_counter() - t0:.1f}s", file=sys.stderr, flush=True)
+        if rank == 0:
+            print(f"[psld] step {k + 1} at {time.perf_counter() - t0:.1f}s", file=sys.stderr,
+                  flush=True)
+    if world > 1:
+        dist.barrier()
     dt = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([dt], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
     if not torch.isfinite(z).all():
         raise SystemExit("non-finite latents")
     ms = dt / args.steps * 1e3
+    if world > 1:
+        dist.destroy_process_group()
+    if rank != 0:
+        return
     print(json.dumps({
         "metric": "posterior samples/sec (batch×steps/s), PSLD SD1.5 512² (BASELINE configs[3])",
-        "value": round(args.batch * args.steps / dt, 4),
+        "value": round(args.batch * world * args.steps / dt, 4),
         "unit": "samples/sec (batch×steps/s)",
-        "n_gpus": 1, "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 2),
+        "n_gpus": world, "scaling": "weak", "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(ms, 2),
         "higher_is_better": True, "dtype": "f32",
         "data": "synthetic (seeded U(-1,1) images, centre mask, sigma=0.05); random-init SD1.5 "
                 "VAE + SD1.5 UNet2DConditionModel architecture (859.5 M, null 77x768 context)",
         "config": {"workload": f"PSLD + CenterInpainting(0.5) + GaussianNoise(0.05), 3x{args.image}²",
-                   "batch": args.batch, "schedule": "100-step PNDM (psld.py:50)"},
+                   "batch_per_gpu": args.batch, "global_batch": args.batch * world,
+                   "parallelism": f"dp{world}", "schedule": "100-step PNDM (psld.py:50)"},
         "vae_tflops": round(VAE_FLOP_PER_SAMPLE * args.batch / (ms / 1e3) / 1e12, 2),
         "model_tflops": round((VAE_FLOP_PER_SAMPLE + UNET_FLOP_PER_SAMPLE) * args.batch
                               / (ms / 1e3) / 1e12, 2),

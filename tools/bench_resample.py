@@ -1,6 +1,8 @@
 """ReSample benchmark (BASELINE.json configs[4], "config 5"): SD1.5 latent, 512², Poisson noise.
 
     python tools/bench_resample.py [--batch 32 --steps 3 --warmup 2]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 \
+        tools/bench_resample.py --gpus N        (batch per rank)
 
 Config 5 is 256 samples sharded over 8 GPUs: 32 per GPU, which is what one process here
 runs (the batch shards with no data-path collective; the batch-global losses are 8-byte
@@ -22,7 +24,12 @@ on the same tensors and reports each:
   latent_iter   one latent-space AdamW iteration (VAE decode forward + VJP, HIP MSE
                 gradient and AdamW)
 
-Prints one JSON line.
+With N ranks each holds ``--batch`` samples (Philox sample offset rank x batch); the
+consistency losses and MSE totals are batch-global through 8-byte RCCL all-reduces
+(resample.py's norms), and every figure is the max over ranks of the wall
+time; "value" = N x batch x K / that time (weak scaling, as bench.py).
+
+Prints one JSON line (rank 0).
 """
 
 from __future__ import annotations
@@ -38,6 +45,9 @@ sys.path.insert(0, str(ROOT))
 import samplers_amd  # noqa: E402,F401
 
 import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+from bench import setup_dist  # noqa: E402
 
 sys.path.insert(0, str(ROOT / "tools"))
 from bench_psld import VAE_FLOP_PER_SAMPLE, heartbeat  # noqa: E402
@@ -45,20 +55,33 @@ from bench_psld import VAE_FLOP_PER_SAMPLE, heartbeat  # noqa: E402
 DECODE_FLOP_PER_SAMPLE = 4.96e12  # decode forward + VJP at 512²
 
 
-def timed(fn, reps: int, label: str) -> float:
+def timed(fn, reps: int, label: str, world: int = 1, rank: int = 0) -> float:
+    """Mean wall time of ``reps`` calls, bracketed by barriers, max over ranks."""
+    if world > 1:
+        dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for k in range(reps):
         fn()
         torch.cuda.synchronize()
-        print(f"[resample] {label} {k + 1}/{reps} at {time.perf_counter() - t0:.1f}s",
-              file=sys.stderr, flush=True)
-    return (time.perf_counter() - t0) / reps
+        if rank == 0:
+            print(f"[resample] {label} {k + 1}/{reps} at {time.perf_counter() - t0:.1f}s",
+                  file=sys.stderr, flush=True)
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([dt], device=torch.device("cuda", torch.cuda.current_device()),
+                         dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    return dt / reps
 
 
 def main():
     p = argparse.ArgumentParser()
-    p.add_argument("--batch", type=int, default=32)
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--batch", type=int, default=32, help="samples per rank")
     p.add_argument("--image", type=int, default=512)
     p.add_argument("--steps", type=int, default=3)
     p.add_argument("--warmup", type=int, default=2)
@@ -68,7 +91,8 @@ def main():
     args = p.parse_args()
     Path(args.heartbeat).parent.mkdir(parents=True, exist_ok=True)
     heartbeat(Path(args.heartbeat))
-    dev = torch.device("cuda:0")
+    rank, world, dev = setup_dist(args.gpus)
+    group = dist.group.WORLD if world > 1 else None
 
     from samplers_amd import _hip
     from samplers_amd.networks.latent import LatentDiffusionNetwork, StableDiffusionCondition
@@ -81,7 +105,7 @@ def main():
     shape = (3, args.image, args.image)
     b = args.batch
     op = IdentityOperator(shape)
-    gen = torch.Generator().manual_seed(1000)
+    gen = torch.Generator().manual_seed(1000 + rank)
     x_true = torch.rand((b, *shape), generator=gen) * 2 - 1
     noise = PoissonNoise(1.0)
     y = noise.sample(tuple(x_true.shape), generator=gen) + x_true  # y = A x + Poisson noise
@@ -91,56 +115,63 @@ def main():
     net.set_condition(StableDiffusionCondition(prompt=[""] * b))  # reference default prompt, CFG collapses
     lat = tuple(net.get_latent_shape(shape))
     sampler = ReSampleSampler(net)
-    cons = _Consistency(op, y.reshape(b, -1), 1)
-    total = b * cons.m
-    seed = 20260101
-    z = initial_sample((b, *lat), dev, rng="philox", seed=seed, sample_offset=0, noise_fn=None)
+    cons = _Consistency(op, y.reshape(b, -1), 1, group)
+    total = b * world * cons.m  # MSE mean over the global batch
+    seed, off = 20260101, rank * b
+    z = initial_sample((b, *lat), dev, rng="philox", seed=seed, sample_offset=off, noise_fn=None)
     ts, acp = net.timesteps_host, net.alphas_cumprod_host
     it = iter(range(len(ts) - 1, 1, -1))
 
     def one():
         nonlocal z
         i = next(it)
-        z_next, pseudo, sqrt_a = sampler._ddim_eps(z, ts[i], ts[i - 1], 1.0, None, seed, i, 0)
+        z_next, pseudo, sqrt_a = sampler._ddim_eps(z, ts[i], ts[i - 1], 1.0, None, seed, i, off)
         z = sampler._dps_conditioning(z_next, pseudo, sqrt_a, float(acp[ts[i]]), cons)
 
     t0 = time.perf_counter()
     for k in range(args.warmup):
         one()
         torch.cuda.synchronize()
-        print(f"[resample] warmup {k + 1} done at {time.perf_counter() - t0:.1f}s",
-              file=sys.stderr, flush=True)
+        if rank == 0:
+            print(f"[resample] warmup {k + 1} done at {time.perf_counter() - t0:.1f}s",
+                  file=sys.stderr, flush=True)
     torch.cuda.reset_peak_memory_stats()
-    step_s = timed(one, args.steps, "step")
+    step_s = timed(one, args.steps, "step", world, rank)
     if not torch.isfinite(z).all():
         raise SystemExit("non-finite latents")
 
     x_pix = net.decode(z, differentiable=False).reshape(b, *shape).contiguous()
     sampler._pixel_optimization(x_pix, cons, total, 1e-3, 16)  # warm
     pix_s = timed(lambda: sampler._pixel_optimization(x_pix, cons, total, 0.0, args.pixel_iters),
-                  1, "pixel") / args.pixel_iters
+                  1, "pixel", world, rank) / args.pixel_iters
     sampler._latent_optimization(z, cons, total, 1e-3, 1)  # warm
     lat_s = timed(lambda: sampler._latent_optimization(z, cons, total, 0.0, args.latent_iters),
-                  1, "latent") / args.latent_iters
+                  1, "latent", world, rank) / args.latent_iters
 
     n = b * shape[0] * args.image * args.image
+    peak_gib = round(torch.cuda.max_memory_allocated() / 2**30, 1)
+    if world > 1:
+        dist.destroy_process_group()
+    if rank != 0:
+        return
     print(json.dumps({
         "metric": "posterior samples/sec (batch×steps/s), ReSample SD1.5 512² Poisson "
                   "(BASELINE configs[4], 32 per GPU of 256 over 8)",
-        "value": round(b * args.steps / (step_s * args.steps), 4),
+        "value": round(b * world / step_s, 4),
         "unit": "samples/sec (batch×steps/s)",
-        "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
+        "n_gpus": world, "scaling": "weak", "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(step_s * 1e3, 2), "higher_is_better": True, "dtype": "f32",
         "data": "synthetic (seeded U(-1,1) images, Poisson(rate=1) noise); random-init SD1.5 VAE "
                 "+ SD1.5 UNet2DConditionModel architectures (null 77x768 context)",
         "config": {"workload": f"ReSample + Identity + PoissonNoise(1.0), 3x{args.image}²",
-                   "batch": b, "schedule": "100-step PNDM (resample.py:52)"},
+                   "batch_per_gpu": b, "global_batch": b * world,
+                   "parallelism": f"dp{world}", "schedule": "100-step PNDM (resample.py:52)"},
         "decode_vjp_tflops": round(DECODE_FLOP_PER_SAMPLE * b / step_s / 1e12, 2),
         "pixel_iter_ms": round(pix_s * 1e3, 4),
         "pixel_iter_GBps": round(4 * 7 * n / pix_s / 1e9, 1),  # x,m,v,y read; x,m,v written
         "latent_iter_ms": round(lat_s * 1e3, 2),
         "latent_iter_tflops": round(DECODE_FLOP_PER_SAMPLE * b / lat_s / 1e12, 2),
-        "peak_gib": round(torch.cuda.max_memory_allocated() / 2**30, 1),
+        "peak_gib": peak_gib,
         "vae_flop_per_sample_step": VAE_FLOP_PER_SAMPLE,
     }), flush=True)
 
