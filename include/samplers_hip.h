@@ -366,6 +366,24 @@ int sp_wino3x3_bwd_input(const float* dy, const float* up_vjp, int64_t n, int32_
                          int32_t cout, int32_t height, int32_t width, float* dx,
                          sp_stream_t stream);
 
+/* Winograd F(2x2,3x3) with the 16 GEMMs on bf16 MFMAs over exact three-term bf16 splits of
+ * the fp32 operands (six partial products per product, fp32 accumulation: fp32-class error,
+ * tests/test_conv_gpu.py).  Replaces the same layers as sp_wino3x3_* (diffusers' UNet / VAE
+ * 3x3 convolutions: unet_2d_blocks ResnetBlock2D conv1/conv2) where
+ * cin % 16 == 0, cout % 32 == 0, H % 16 == 0, W % 32 == 0.  Packed U (sp_wino3x3_x6_pack,
+ * input_vjp=1: transposed, flipped weights) takes sp_wino3x3_x6_packed_size floats of
+ * storage; res (nullable) is added in the epilogue (must not alias y). */
+int sp_wino3x3_x6_supported(int32_t cin, int32_t cout, int32_t height, int32_t width);
+int64_t sp_wino3x3_x6_packed_size(int32_t cin, int32_t cout);
+int sp_wino3x3_x6_pack(const float* w, int32_t cout, int32_t cin, int32_t input_vjp, float* up,
+                       sp_stream_t stream);
+int sp_wino3x3_x6_fwd(const float* x, const float* up, const float* bias, const float* res, int64_t n,
+                      int32_t cin, int32_t cout, int32_t height, int32_t width, float* y,
+                      sp_stream_t stream);
+int sp_wino3x3_x6_bwd_input(const float* dy, const float* up_vjp, int64_t n, int32_t cin,
+                            int32_t cout, int32_t height, int32_t width, float* dx,
+                            sp_stream_t stream);
+
 /* Fused self-attention softmax(q k^T * scale) v of the SD 1.5 eps-UNet's transformer blocks
  * (attn1 over the latent tokens; diffusers UNet2DConditionModel, stable_diffusion.py:306-313;
  * replaces the scores / softmax / weighted-sum chain and its autograd VJP) on fp32 MFMA,

@@ -159,8 +159,10 @@ class GroupNormAct(nn.GroupNorm):
 
 def conv_backend() -> str:
     """``SAMPLERS_AMD_CONV``: ``auto`` (default: Winograd F(2x2,3x3) tile where its shape
-    rules hold, else the direct tile, else MIOpen), ``direct`` (direct tile or MIOpen),
-    ``miopen`` (always torch/MIOpen)."""
+    rules hold, else the direct tile, else MIOpen), ``x6`` (as auto, with the Winograd GEMMs
+    on bf16 MFMAs over exact three-term splits of the fp32 operands where its shape rules
+    hold: ``csrc/sp_wino_x6.hip``), ``direct`` (direct tile or MIOpen), ``miopen`` (always
+    torch/MIOpen)."""
     import os
 
     return os.environ.get("SAMPLERS_AMD_CONV", "auto").lower()
@@ -169,7 +171,9 @@ def conv_backend() -> str:
 def _conv_algo(lib, cin: int, cout: int, h: int, w: int, backend: str) -> str | None:
     if backend == "miopen":
         return None
-    if backend == "auto" and lib.sp_wino3x3_supported(cin, cout, h, w):
+    if backend == "x6" and lib.sp_wino3x3_x6_supported(cin, cout, h, w):
+        return "x6"
+    if backend in ("auto", "x6") and lib.sp_wino3x3_supported(cin, cout, h, w):
         return "wino"
     if lib.sp_conv3x3_supported(cin, cout, h, w):
         return "direct"
@@ -199,6 +203,12 @@ def conv3x3_forward(module: "Conv3x3", x: Tensor, res: Tensor | None = None,
                                            _hip.stream_of(x)), "sp_conv3x3_thin_fwd")
         return y if res is None else y.add_(res)
     pk = tile_pack(module, algo, False)
+    if algo == "x6":
+        _hip.check(lib.sp_wino3x3_x6_fwd(_hip.ptr(x), _hip.ptr(pk), _hip.ptr(bias),
+                                         _hip.ptr(None if res is None else res.contiguous()), n, cin,
+                                         cout, h, w, _hip.ptr(y), _hip.stream_of(x)),
+                   "sp_wino3x3_x6_fwd")
+        return y
     if algo == "wino" and res is not None:
         _hip.check(lib.sp_wino3x3_fwd_res(_hip.ptr(x), _hip.ptr(pk), _hip.ptr(bias),
                                           _hip.ptr(res.contiguous()), n, cin, cout, h, w,
@@ -225,7 +235,8 @@ def conv3x3_input_vjp(module: "Conv3x3", dy: Tensor, x_shape) -> Tensor:
                                                  n, cin, cout, h, w, _hip.ptr(dx),
                                                  _hip.stream_of(dy)), "sp_conv3x3_thin_bwd_input")
         return dx
-    fn = lib.sp_wino3x3_bwd_input if algo == "wino" else lib.sp_conv3x3_bwd_input
+    fn = {"wino": lib.sp_wino3x3_bwd_input, "x6": lib.sp_wino3x3_x6_bwd_input}.get(
+        algo, lib.sp_conv3x3_bwd_input)
     _hip.check(fn(_hip.ptr(dy), _hip.ptr(tile_pack(module, algo, True)), n, cin, cout, h, w,
                   _hip.ptr(dx), _hip.stream_of(dy)), f"sp_{algo}_conv3x3_bwd_input")
     return dx
@@ -266,9 +277,10 @@ def tile_pack(module: nn.Conv2d, algo: str, input_vjp: bool) -> Tensor:
         lib = _hip.load_library()
         cout, cin = w.shape[0], w.shape[1]
         wc = w.detach().contiguous()
-        size = (lib.sp_wino3x3_packed_size if algo == "wino" else lib.sp_conv3x3_packed_size)(cin, cout)
-        out = torch.empty(int(size), device=w.device)
-        fn = lib.sp_wino3x3_pack if algo == "wino" else lib.sp_conv3x3_pack
+        size_fn, fn = {"wino": (lib.sp_wino3x3_packed_size, lib.sp_wino3x3_pack),
+                       "x6": (lib.sp_wino3x3_x6_packed_size, lib.sp_wino3x3_x6_pack)}.get(
+            algo, (lib.sp_conv3x3_packed_size, lib.sp_conv3x3_pack))
+        out = torch.empty(int(size_fn(cin, cout)), device=w.device)
         _hip.check(fn(_hip.ptr(wc), cout, cin, int(input_vjp), _hip.ptr(out), _hip.stream_of(wc)),
                    f"sp_{algo}3x3_pack")
         cache[(algo, input_vjp)] = out
@@ -446,7 +458,7 @@ def strided_full_supported(module: nn.Conv2d, x: Tensor) -> bool:
     cout = module.out_channels
     fwd = _conv_algo(lib, cin, cout, h, w, backend)
     vjp = _conv_algo(lib, cout, cin, h, w, backend)
-    return h % 2 == 0 and w % 2 == 0 and fwd in ("wino", "direct") and vjp in ("wino", "direct")
+    return h % 2 == 0 and w % 2 == 0 and fwd in ("wino", "x6", "direct") and vjp in ("wino", "x6", "direct")
 
 
 class _ConvS2FullFn(torch.autograd.Function):

@@ -11,7 +11,7 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 // filler kinds: 0 v_fma_f32, 1 v_pk_add_f32, 2 v_mov_b32, 3 v_add_u32, 4 ds_read_b128,
-// 5 ds_write_b64, 6 v_exp_f32
+// 5 ds_write_b64, 6 v_exp_f32, 7 v_cvt_pk_bf16_f32
 template <int GAP, int KIND = 0>
 __device__ __forceinline__ void fillers(float (&f)[8], float b) {
     typedef float f2 __attribute__((ext_vector_type(2)));
@@ -38,6 +38,8 @@ __device__ __forceinline__ void fillers(float (&f)[8], float b) {
             asm volatile("ds_write_b64 %0, %1" : : "v"((threadIdx.x & 63) * 8 + (i & 7) * 512), "v"(x) : "memory");
         }
         if constexpr (KIND == 6) asm volatile("v_exp_f32 %0, %1" : "=v"(f[i & 7]) : "v"(b));
+        if constexpr (KIND == 7)
+            asm volatile("v_cvt_pk_bf16_f32 %0, %0, %1" : "+v"(f[i & 7]) : "v"(b));
     }
     if (b < -1e30f) lds[threadIdx.x] = f[0];
 }
@@ -151,6 +153,38 @@ __global__ __launch_bounds__(256, 1) void kf43(int iters, float* out) {
     out[blockIdx.x * 256 + threadIdx.x] = s;
 }
 
+// bf16 MFMA (v_mfma_f32_32x32x16_bf16, 16x the fp32 MFMA's MACs per cycle): 16 per round,
+// GAP fillers after every EVERY-th — is VALU work beside bf16 MFMAs hidden, unlike fp32?
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+template <int GAP, int EVERY, int KIND>
+__global__ __launch_bounds__(256, 1) void kbf(int iters, float* out) {
+    f32x16 acc[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[i] = f32x16{};
+    float a = threadIdx.x * 1e-3f, b = 1.0001f;
+    bf16x8 av, bv;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) av[i] = (__bf16)(a + i), bv[i] = (__bf16)(b - i);
+    float f[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) f[i] = a + i;
+    for (int it = 0; it < iters; ++it) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, bv, acc[i], 0, 0, 0);
+            __builtin_amdgcn_sched_barrier(0);
+            if (i % EVERY == EVERY - 1) fillers<GAP, KIND>(f, b);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    }
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) s += acc[i][0] + acc[i][15];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) s += f[i];
+    out[blockIdx.x * 256 + threadIdx.x] = s;
+}
+
 template <class K>
 static void run(const char* name, K kern, int nm, int gap, double flops_per_mfma, float* out, int cus,
                 const char* kind = "v_fma_f32") {
@@ -192,7 +226,7 @@ int main() {
     run("32x32x2", k32<16>, 16, 16, 4096, out, cus);
     run("32x32x2", k32<24>, 16, 24, 4096, out, cus);
     const char* kinds[] = {"v_fma_f32", "v_pk_add_f32", "v_mov_b32", "v_add_u32", "ds_read_b128",
-                           "ds_write_b64", "v_exp_f32"};
+                           "ds_write_b64", "v_exp_f32", "v_cvt_pk_bf16_f32"};
     run("32x32x2", k32<4, 1>, 16, 4, 4096, out, cus, kinds[1]);
     run("32x32x2", k32<4, 2>, 16, 4, 4096, out, cus, kinds[2]);
     run("32x32x2", k32<4, 3>, 16, 4, 4096, out, cus, kinds[3]);
@@ -216,6 +250,20 @@ int main() {
     run("16x16x4 F43 k-step: 96 pk in 2 bursts", kf43<96, 2>, 36, 96, 2048, out, cus, kinds[1]);
     run("16x16x4 F43 k-step: 72 pk in 4 bursts", kf43<72, 4>, 36, 72, 2048, out, cus, kinds[1]);
     run("16x16x4 F43 k-step: 0 pk", kf43<0, 4>, 36, 0, 2048, out, cus, kinds[1]);
+    run("bf16 32x32x16", kbf<0, 1, 0>, 16, 0, 32768, out, cus, kinds[0]);
+    run("bf16 32x32x16", kbf<1, 1, 0>, 16, 1, 32768, out, cus, kinds[0]);
+    run("bf16 32x32x16", kbf<2, 1, 0>, 16, 2, 32768, out, cus, kinds[0]);
+    run("bf16 32x32x16", kbf<4, 1, 0>, 16, 4, 32768, out, cus, kinds[0]);
+    run("bf16 32x32x16", kbf<8, 1, 0>, 16, 8, 32768, out, cus, kinds[0]);
+    run("bf16 32x32x16", kbf<2, 1, 1>, 16, 2, 32768, out, cus, kinds[1]);
+    run("bf16 32x32x16", kbf<4, 1, 1>, 16, 4, 32768, out, cus, kinds[1]);
+    run("bf16 32x32x16", kbf<8, 1, 1>, 16, 8, 32768, out, cus, kinds[1]);
+    run("bf16 32x32x16", kbf<2, 1, 7>, 16, 2, 32768, out, cus, kinds[7]);
+    run("bf16 32x32x16", kbf<4, 1, 7>, 16, 4, 32768, out, cus, kinds[7]);
+    run("bf16 32x32x16", kbf<8, 1, 7>, 16, 8, 32768, out, cus, kinds[7]);
+    run("bf16 32x32x16", kbf<2, 1, 4>, 16, 2, 32768, out, cus, kinds[4]);
+    run("bf16 32x32x16 burst/4", kbf<16, 4, 1>, 16, 16, 32768, out, cus, kinds[1]);
+    run("bf16 32x32x16 burst/16", kbf<64, 16, 1>, 16, 64, 32768, out, cus, kinds[1]);
     hipFree(out);
     return 0;
 }
