@@ -384,6 +384,21 @@ int sp_wino3x3_x6_bwd_input(const float* dy, const float* up_vjp, int64_t n, int
                             int32_t cout, int32_t height, int32_t width, float* dx,
                             sp_stream_t stream);
 
+/* 1x1 convolution as a per-pixel GEMM on bf16 MFMAs over exact three-term splits of the fp32
+ * operands (fp32-class error): Y[n][co][p] = sum_k W[co][k] X[n][k][p] (+ bias[co]) (+ res),
+ * X = cat(x1 [n][c1][hw], x2 [n][c2][hw]) read in place, Y split into y1 [n][o1][hw] and
+ * y2 [n][o2][hw] (o2 may be 0).  Replaces diffusers ResnetBlock2D.conv_shortcut over the
+ * up path's concatenation (forward) and its input VJP (W^T dy into both parts), SURVEY.md §8f
+ * f1.  M = o1 + o2 % 128, K = c1 + c2 % 16, c1 % 8, c2 % 8, o1 % 32, o2 % 32, hw % 256;
+ * res only with o2 == 0.  W packed by sp_gemm_x6_pack from a row-major [M][K] matrix, or
+ * (trans = 1) from one stored [K][M]. */
+int sp_gemm_x6_supported(int32_t m, int32_t k, int64_t hw);
+int64_t sp_gemm_x6_packed_size(int32_t m, int32_t k);
+int sp_gemm_x6_pack(const float* w, int32_t m, int32_t k, int32_t trans, float* wp, sp_stream_t stream);
+int sp_gemm_x6(const float* x1, int32_t c1, const float* x2, int32_t c2, const float* wp,
+               const float* bias, const float* res, int64_t n, int64_t hw, float* y1, int32_t o1,
+               float* y2, int32_t o2, sp_stream_t stream);
+
 /* Fused self-attention softmax(q k^T * scale) v of the SD 1.5 eps-UNet's transformer blocks
  * (attn1 over the latent tokens; diffusers UNet2DConditionModel, stable_diffusion.py:306-313;
  * replaces the scores / softmax / weighted-sum chain and its autograd VJP) on fp32 MFMA,

@@ -1,0 +1,400 @@
+// 1x1 convolution (per-pixel GEMM) Y[n][co][p] = sum_k W[co][k] X[n][k][p] on bf16 MFMAs over
+// exact three-term bf16 splits of the fp32 operands (the scheme of sp_wino_x6.hip: six partial
+// products, fp32 accumulation; error at or below an fp32 GEMM's, tests/test_gemm_x6_gpu.py).
+//
+// The UNet's ResnetBlock conv_shortcut (diffusers ResnetBlock2D) over
+// cat(x1, x2) in the up path: forward W [x1; x2] (+ its bias folded elsewhere), input VJP
+// [W1^T; W2^T] dy into two outputs.  Both sides of the concatenation are addressed in place:
+// K blocks of 16 channels come from X1 or X2, output blocks of 32 channels go to Y1 or Y2.
+//
+// Why bf16 here: with K = 128-256 the fp32-MFMA GEMM is compute-bound (43 FLOP/B against a
+// 20 FLOP/B ridge); at the bf16 rate / 6 it is HBM-bound, so one pass over x and y is the
+// cost (W, 100-200 KB of split terms, stays in L2).
+//
+// Tile: workgroup = 128 output channels x 256 pixels of one image; its 8 waves (two per SIMD)
+// each own channels 64 (w & 1) .. +63 and pixels 64 (w >> 1) .. +63 (2 x 2 tiles of 32 x 32).
+// k-step = 16 input channels: X (16 ch x 256 px, fp32) and W's packed fragments (12 KB) come
+// by direct global->LDS loads two k-steps ahead; the workgroup splits X one k-step ahead
+// into the three bf16 terms as [term][pixel][16 ch] (a lane's B fragment = 16 contiguous
+// bytes).
+
+#include "sp_common.h"
+
+#include <algorithm>
+
+namespace sp {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef unsigned uvec4 __attribute__((ext_vector_type(4)));
+typedef unsigned uvec2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __attribute__((address_space(3))) void lds_void_g;
+
+#ifndef G6_SCHED
+#define G6_SCHED 1  // hand-ordered issue within the k-step (see k_gemm_x6)
+#endif
+#ifndef G6_EXP
+#define G6_EXP 0  // diagnostics only (wrong results, timing): 1 no MFMAs, 2 no split, 3 no loads
+#endif
+constexpr int G6_CO = 128;     // output channels per workgroup
+constexpr int G6_PX = 256;     // pixels per workgroup
+constexpr int G6_KC = 16;      // input channels per k-step
+constexpr int G6_XB = 3 * G6_PX * G6_KC * 2;  // bytes of split X per k-step (24 KB)
+constexpr int G6_WB = 4 * 3 * 64 * 16;        // bytes of W fragments per k-step (12 KB)
+
+struct G6Geom {
+    const float* x1;
+    const float* x2;      // nullable: channels c1 .. c1 + c2 - 1
+    const unsigned short* wp;
+    float* y1;
+    float* y2;            // nullable: output channels o1 .. o1 + o2 - 1
+    const float* bias;    // nullable, per output channel (o1 + o2)
+    const float* res;     // nullable, shaped like y1 (o2 == 0 only)
+    int c1, c2, o1, o2, hw;
+    int ntiles, cob, ptiles, nsteps;
+};
+
+__device__ __forceinline__ void g6_split(float v, unsigned& h, unsigned& m, unsigned& l) {
+    const unsigned vb = __float_as_uint(v);
+    h = vb & 0xffff0000u;
+    const float r = v - __uint_as_float(h);
+    m = __float_as_uint(r) & 0xffff0000u;
+    l = __float_as_uint(r - __uint_as_float(m));
+}
+__device__ __forceinline__ unsigned g6_pack(unsigned a, unsigned b) {
+    return __builtin_amdgcn_perm(b, a, 0x07060302u);
+}
+__device__ __forceinline__ f32x16 g6_mfma(uvec4 a, uvec4 b, f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a),
+                                                   __builtin_bit_cast(bf16x8, b), c, 0, 0, 0);
+}
+
+// direct global->LDS load (64 lanes x 16 B to lds .. lds + 1 KB) written as inline asm: the
+// compiler's wait insertion does not see it, so it does not drain it with vmcnt(0) before every
+// later LDS read it cannot prove disjoint; the kernel waits for these loads itself (counted vmcnt)
+__device__ __forceinline__ void g6_lds_dma(__amdgpu_buffer_rsrc_t rs, const void* lds, int voff, int soff) {
+    const unsigned la = static_cast<unsigned>(reinterpret_cast<size_t>((lds_void_g*)lds));
+    asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds"
+                 :
+                 : "s"(__builtin_amdgcn_readfirstlane(la)), "v"(voff), "s"(rs), "s"(soff)
+                 : "memory", "m0");
+}
+
+// gfx9 s_waitcnt immediate: vmcnt <= n (6 bits), lgkmcnt / expcnt not waited for
+constexpr int g6_vmcnt(int n) { return (n & 0xF) | ((n >> 4) << 14) | (0x7 << 4) | (0xF << 8); }
+
+// raw X of one k-step -> LDS ring slot ([16 ch][256 px] fp32): 16 direct 1-KB loads, 2 per wave
+// (channel 2 wv + i, lane l: pixels 4l .. 4l + 3)
+__device__ __forceinline__ void g6_dma_x(const G6Geom& g, int n, int p0, int kstep, int wv, int lane,
+                                         unsigned char* slot) {
+    const int k0 = kstep * G6_KC;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const int c = k0 + 2 * wv + i;
+        const bool second = c >= g.c1;
+        const float* base = second ? g.x2 + ((int64_t)n * g.c2 + (c - g.c1)) * g.hw
+                                   : g.x1 + ((int64_t)n * g.c1 + c) * g.hw;
+        const auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), (short)0, g.hw * 4,
+                                                          0x00020000);
+        g6_lds_dma(rs, slot + (2 * wv + i) * 1024, lane * 16, p0 * 4);
+    }
+}
+
+// W fragments of one k-step (12 KB contiguous in the packed layout): 12 direct 1-KB loads, two
+// by each of waves 0-3 and one by each of waves 4-7
+__device__ __forceinline__ void g6_dma_w(__amdgpu_buffer_rsrc_t wrs, int stage, int wv, int lane,
+                                         unsigned char* wb) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const int chunk = i == 0 ? wv : 8 + wv;
+        if (chunk < 12)
+            g6_lds_dma(wrs, wb + chunk * 1024, lane * 16, stage * G6_WB + chunk * 1024);
+    }
+}
+// vm ops a wave issues per k-step (2 X + 2 or 1 W)
+__device__ __forceinline__ int g6_dma_per_wave(int wv) { return wv < 4 ? 4 : 3; }
+
+// raw slot -> split [term][pixel][16 ch] bf16: thread = 8 channels (tid >> 8) x pixel tid & 255
+__device__ __forceinline__ void g6_split_x(const unsigned char* raw, unsigned char* xb, int tid) {
+    const int grp = tid >> 8, px = tid & 255;
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = *reinterpret_cast<const float*>(raw + (8 * grp + j) * 1024 + px * 4);
+    uvec4 th, tm, tl;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        unsigned h0, m0, l0, h1, m1, l1;
+        g6_split(v[2 * q], h0, m0, l0);
+        g6_split(v[2 * q + 1], h1, m1, l1);
+        th[q] = g6_pack(h0, h1);
+        tm[q] = g6_pack(m0, m1);
+        tl[q] = g6_pack(l0, l1);
+    }
+    const int off = (px * G6_KC + 8 * grp) * 2;
+    *reinterpret_cast<uvec4*>(xb + 0 * G6_PX * G6_KC * 2 + off) = th;
+    *reinterpret_cast<uvec4*>(xb + 1 * G6_PX * G6_KC * 2 + off) = tm;
+    *reinterpret_cast<uvec4*>(xb + 2 * G6_PX * G6_KC * 2 + off) = tl;
+}
+
+struct G6Pos { int n, p0, cb; };
+__device__ __forceinline__ G6Pos g6_pos(const G6Geom& g, int t) {
+    // XCD-aware: the output-channel blocks of one pixel tile on one XCD (shared X lines)
+    const int lb = (g.ntiles & 7) ? t : (t & 7) * (g.ntiles >> 3) + (t >> 3);
+    const int cb = lb % g.cob, rest = lb / g.cob;
+    const int n = rest / g.ptiles;
+    return G6Pos{n, (rest - n * g.ptiles) * G6_PX, cb};
+}
+
+// epilogue: register q of tile (a, b) = channel 32 sub + (q&3) + 8(q>>2) + 4(lane>>5),
+// pixel 64 pq + 32 b + (lane & 31); bias and residual added, the 32-channel block to y1 or y2
+__device__ __forceinline__ void g6_epilogue(const G6Geom& g, const G6Pos& ps, int ch, int pq, int lane,
+                                            const f32x16 (&acc)[2][2]) {
+#pragma unroll
+    for (int a = 0; a < 2; ++a) {
+        const int co0 = ps.cb * G6_CO + 32 * (2 * ch + a);  // first channel of the 32-block
+        const bool second = co0 >= g.o1;
+        float* yb = second ? g.y2 + ((int64_t)ps.n * g.o2 + (co0 - g.o1)) * g.hw
+                           : g.y1 + ((int64_t)ps.n * g.o1 + co0) * g.hw;
+        const auto ors = __builtin_amdgcn_make_buffer_rsrc(yb, (short)0, 32 * g.hw * 4, 0x00020000);
+        const auto rrs = __builtin_amdgcn_make_buffer_rsrc(
+            const_cast<float*>(g.res ? g.res + ((int64_t)ps.n * g.o1 + co0) * g.hw : g.y1), (short)0,
+            g.res ? 32 * g.hw * 4 : 0, 0x00020000);
+        const auto brs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(g.bias ? g.bias + co0 : g.y1),
+                                                           (short)0, g.bias ? 32 * 4 : 0, 0x00020000);
+        const float bl = g.bias ? __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(brs, (lane & 31) * 4, 0, 0))
+                                : 0.f;
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+            const int vo = (ps.p0 + pq * 64 + b * 32 + (lane & 31)) * 4;
+            float rv[16];
+#pragma unroll
+            for (int q = 0; q < 16; ++q) rv[q] = 0.f;
+            if (g.res) {  // all 16 loads first (one wait), not a load-use pair per register
+#pragma unroll
+                for (int q = 0; q < 16; ++q) {
+                    const int cc = (q & 3) + 8 * (q >> 2) + 4 * (lane >> 5);
+                    rv[q] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rrs, vo + cc * g.hw * 4, 0, 0));
+                }
+            }
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
+                const int c = (q & 3) + 8 * (q >> 2);
+                const float b0 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, bl), c));
+                const float b1 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, bl), c + 4));
+                const int cc = c + 4 * (lane >> 5);
+                const float y = acc[a][b][q] + ((lane >> 5) ? b1 : b0) + rv[q];
+                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(y), ors, vo + cc * g.hw * 4, 0, 0);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    }
+}
+
+// The workgroup walks a flat stream of k-steps j = (its tile j / nsteps, step j % nsteps): the
+// loads of X(j + 3) and W(j + 2) and the split of X(j + 1) run during the MFMAs of step j, across
+// tile boundaries (raw X in a 4-slot and W in a 3-slot LDS ring filled by direct loads, split X
+// in 2 slots).
+// Eight waves, two per SIMD: one wave's MFMAs cover the other's LDS waits and split work.
+constexpr int G6_THREADS = 512;
+
+__global__ __launch_bounds__(G6_THREADS, 1) void k_gemm_x6(G6Geom g) {
+    __shared__ __attribute__((aligned(16))) unsigned char xraw[4][G6_KC * G6_PX * 4];
+    __shared__ __attribute__((aligned(16))) unsigned char xs[2][G6_XB];
+    __shared__ __attribute__((aligned(16))) unsigned char wl[3][G6_WB];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int ch = wv & 1, pq = wv >> 1;  // 64 output channels x 64 pixels
+    const auto wrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<unsigned short*>(g.wp), (short)0,
+                                                       g.cob * g.nsteps * G6_WB, 0x00020000);
+    const int G = gridDim.x, b0 = blockIdx.x;
+    const int ntile_wg = (g.ntiles - b0 + G - 1) / G;
+    const int J = ntile_wg * g.nsteps;
+    // two load streams, advanced one k-step at a time (divisions once per tile): raw X three
+    // steps ahead (4 slots), W two steps ahead (3 slots)
+    struct Cursor { int j, tw, s, slot; G6Pos ps; };
+    Cursor cx{0, 0, 0, 0, g6_pos(g, b0)}, cw = cx;
+    auto advance = [&](Cursor& c, int nslots) {
+        ++c.j;
+        c.slot = c.slot + 1 == nslots ? 0 : c.slot + 1;
+        if (++c.s == g.nsteps) {
+            c.s = 0;
+            if (++c.tw < ntile_wg) c.ps = g6_pos(g, b0 + c.tw * G);
+        }
+    };
+    auto dma_x = [&]() {
+        if (cx.j < J) g6_dma_x(g, cx.ps.n, cx.ps.p0, cx.s, wv, lane, xraw[cx.slot]);
+        advance(cx, 4);
+    };
+    auto dma_w = [&]() {
+        if (cw.j < J) g6_dma_w(wrs, cw.ps.cb * g.nsteps + cw.s, wv, lane, wl[cw.slot]);
+        advance(cw, 3);
+    };
+    // prologue: W 0, 1 and X 0, 1, 2 in flight; split of step 0
+    dma_w();
+    dma_x();
+    dma_w();
+    dma_x();
+    dma_x();
+    __builtin_amdgcn_s_waitcnt(g6_vmcnt(0));
+    __builtin_amdgcn_s_barrier();
+    g6_split_x(xraw[0], xs[0], tid);
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
+    __builtin_amdgcn_s_barrier();
+
+    const bool four = g6_dma_per_wave(wv) == 4;  // this wave's W loads per step: 2 (else 1)
+    f32x16 acc[2][2];
+    int j = 0, wslot = 0, xslot1 = 1;  // W slot of step j, X slot of step j + 1
+    for (int tw = 0; tw < ntile_wg; ++tw) {
+#pragma unroll
+        for (int a = 0; a < 2; ++a)
+#pragma unroll
+            for (int b = 0; b < 2; ++b) acc[a][b] = f32x16{};
+        for (int s = 0; s < g.nsteps; ++s, ++j) {
+#if G6_EXP != 3
+            dma_w();  // step j + 2
+            dma_x();  // step j + 3
+#endif
+            // step j's fragments (split X(j) and W(j), both in since the last barrier)
+            const uvec4* wq = reinterpret_cast<const uvec4*>(wl[wslot]) + lane;
+            const unsigned char* xb = xs[j & 1];
+            uvec4 fu[2][3], fv[2][3];
+#pragma unroll
+            for (int a = 0; a < 2; ++a)
+#pragma unroll
+                for (int e = 0; e < 3; ++e) fu[a][e] = wq[((2 * ch + a) * 3 + e) * 64];
+#pragma unroll
+            for (int b = 0; b < 2; ++b) {
+                const int off = ((pq * 64 + b * 32 + (lane & 31)) * G6_KC + 8 * (lane >> 5)) * 2;
+#pragma unroll
+                for (int e = 0; e < 3; ++e)
+                    fv[b][e] = *reinterpret_cast<const uvec4*>(xb + e * G6_PX * G6_KC * 2 + off);
+            }
+#if G6_EXP != 2
+            // X(j + 1)'s split (unconditional: past the stream's end it rewrites an unused slot)
+            g6_split_x(xraw[xslot1], xs[(j + 1) & 1], tid);
+#endif
+#if G6_EXP != 1
+            // the six partial products (small terms first) over the 4 independent accumulators
+            constexpr int TU[6] = {2, 0, 1, 1, 0, 0}, TV[6] = {0, 2, 1, 0, 1, 0};
+#pragma unroll
+            for (int e = 0; e < 6; ++e)
+#pragma unroll
+                for (int b = 0; b < 2; ++b)
+#pragma unroll
+                    for (int a = 0; a < 2; ++a) acc[a][b] = g6_mfma(fu[a][TU[e]], fv[b][TV[e]], acc[a][b]);
+#endif
+#if G6_SCHED
+            // issue order: the fragment reads, the split's reads, then the MFMAs with the split's
+            // VALU work between them, the split's writes last
+            __builtin_amdgcn_sched_group_barrier(0x100, 12, 0);
+            __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);
+#pragma unroll
+            for (int k = 0; k < 24; ++k) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
+            }
+            __builtin_amdgcn_sched_group_barrier(0x200, 3, 0);
+#endif
+            // one barrier per k-step: the split's writes are done (lgkmcnt) and X(j + 2), W(j + 1)
+            // are in — what may still be in flight was issued after X(j + 2): W(j + 2), X(j + 3)
+            if (j + 3 >= J) __builtin_amdgcn_s_waitcnt(0x0070);  // vmcnt(0) lgkmcnt(0)
+            else if (four) __builtin_amdgcn_s_waitcnt(g6_vmcnt(4) & ~0x0F00);
+            else __builtin_amdgcn_s_waitcnt(g6_vmcnt(3) & ~0x0F00);
+            __builtin_amdgcn_s_barrier();
+            wslot = wslot == 2 ? 0 : wslot + 1;
+            xslot1 = xslot1 == 3 ? 0 : xslot1 + 1;
+        }
+        const G6Pos ps = g6_pos(g, b0 + tw * G);
+        g6_epilogue(g, ps, ch, pq, lane, acc);
+    }
+}
+
+// W [M = o rows][K = c columns] (row-major fp32, or its transpose for trans = 1: W stored [K][M])
+// -> packed A fragments: u16 index (((cb * nsteps + s) * 4 + sub) * 3 + term) * 64 + lane) * 8 + j
+// for row 128 cb + 32 sub + (lane & 31), column 16 s + 8 (lane >> 5) + j.
+__global__ void k_gemm_x6_pack(const float* __restrict__ w, int m, int k, int trans,
+                               unsigned short* __restrict__ wp) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (int64_t)m * k) return;
+    const int row = static_cast<int>(i / k), col = static_cast<int>(i - (int64_t)row * k);
+    const float v = trans ? w[(int64_t)col * m + row] : w[i];
+    unsigned h, mm, l;
+    g6_split(v, h, mm, l);
+    const int nsteps = k / G6_KC, cb = row / G6_CO, sub = (row % G6_CO) / 32, s = col / G6_KC;
+    const int lane = (row & 31) + 32 * ((col & 15) >> 3), j = col & 7;
+    const int64_t base = (((int64_t)cb * nsteps + s) * 4 + sub) * 3;
+    wp[((base + 0) * 64 + lane) * 8 + j] = static_cast<unsigned short>(h >> 16);
+    wp[((base + 1) * 64 + lane) * 8 + j] = static_cast<unsigned short>(mm >> 16);
+    wp[((base + 2) * 64 + lane) * 8 + j] = static_cast<unsigned short>(l >> 16);
+}
+
+}  // namespace sp
+
+using namespace sp;
+
+extern "C" {
+
+int sp_gemm_x6_supported(int32_t m, int32_t k, int64_t hw) {
+    return m >= G6_CO && m % G6_CO == 0 && k >= G6_KC && k % G6_KC == 0 && hw >= G6_PX &&
+           hw % G6_PX == 0 && hw * 32 * 4 < (int64_t(1) << 31);
+}
+
+int64_t sp_gemm_x6_packed_size(int32_t m, int32_t k) { return (int64_t)m * k * 6 / 4; }
+
+int sp_gemm_x6_pack(const float* w, int32_t m, int32_t k, int32_t trans, float* wp, sp_stream_t stream) {
+    if (!w || !wp || m % G6_CO || k % G6_KC || m <= 0 || k <= 0) return SP_EINVAL;
+    const int64_t total = (int64_t)m * k;
+    launch(0, k_gemm_x6_pack, dim3(static_cast<unsigned>((total + 255) / 256)), dim3(256),
+           static_cast<hipStream_t>(stream), w, m, k, trans, reinterpret_cast<unsigned short*>(wp));
+    return check_launch("sp_gemm_x6_pack");
+}
+
+static int g6_cu_count() {
+    static int cached[64] = {};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+    if (!cached[dev]) {
+        int v = 0;
+        if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0)
+            v = 256;
+        cached[dev] = v;
+    }
+    return cached[dev];
+}
+
+int sp_gemm_x6(const float* x1, int32_t c1, const float* x2, int32_t c2, const float* wp,
+               const float* bias, const float* res, int64_t n, int64_t hw, float* y1, int32_t o1,
+               float* y2, int32_t o2, sp_stream_t stream) {
+    const int k = c1 + c2, m = o1 + o2;
+    if (!sp_gemm_x6_supported(m, k, hw) || n < 0 || c1 <= 0 || o1 <= 0 || c2 < 0 || o2 < 0)
+        return SP_EINVAL;
+    if (c1 % 8 || c2 % 8 || o1 % 32 || o2 % 32 || (c2 && !x2) || (o2 && !y2) || (res && o2))
+        return SP_EINVAL;
+    if (n == 0) return SP_OK;
+    if (!x1 || !wp || !y1) return SP_EINVAL;
+    const int64_t tiles = n * (hw / G6_PX) * (m / G6_CO);
+    if (tiles >= (int64_t(1) << 31)) return SP_EINVAL;
+    G6Geom g;
+    g.x1 = x1;
+    g.x2 = x2;
+    g.wp = reinterpret_cast<const unsigned short*>(wp);
+    g.y1 = y1;
+    g.y2 = y2;
+    g.bias = bias;
+    g.res = res;
+    g.c1 = c1;
+    g.c2 = c2;
+    g.o1 = o1;
+    g.o2 = o2;
+    g.hw = static_cast<int>(hw);
+    g.ntiles = static_cast<int>(tiles);
+    g.cob = m / G6_CO;
+    g.ptiles = static_cast<int>(hw / G6_PX);
+    g.nsteps = k / G6_KC;
+    const int grid = static_cast<int>(std::min<int64_t>(tiles, g6_cu_count()));
+    launch(0, k_gemm_x6, dim3(grid), dim3(G6_THREADS), static_cast<hipStream_t>(stream), g);
+    return check_launch("sp_gemm_x6");
+}
+
+}  // extern "C"

@@ -26,6 +26,7 @@ import torch
 import torch.nn.functional as F
 from torch import Tensor, nn
 
+from .. import _hip
 from .layers import (Conv3x3, GroupNormAct, SkipGrad, conv3x3_forward, conv3x3_input_vjp,
                      downsample_conv, gn_backward, gn_forward, upsample_nearest2x)
 
@@ -71,12 +72,61 @@ class TimestepEmbedding(nn.Module):
         return self.linear_2(F.silu(self.linear_1(x)))
 
 
+def _shortcut_backend() -> str:
+    """``SAMPLERS_AMD_SHORTCUT``: ``x6`` (default: the 1x1 GEMM on bf16 MFMAs over exact
+    three-term splits of the fp32 operands, ``csrc/sp_gemm_x6.hip``, where its shape rules
+    hold) or ``torch`` (hipBLASLt fp32 GEMMs)."""
+    import os
+
+    return os.environ.get("SAMPLERS_AMD_SHORTCUT", "x6").lower()
+
+
+def _pointwise_pack(conv: nn.Conv2d, trans: bool) -> Tensor:
+    """conv's 1x1 weights [cout, cin] (trans: as [cin, cout] for the input VJP) packed for
+    sp_gemm_x6, cached on the module and rebuilt when the weight changes."""
+    w = conv.weight
+    key = (w.data_ptr(), w._version, w.device)
+    cache = conv.__dict__.setdefault("_x6_packs", {})
+    if cache.get("key") != key:
+        cache.clear()
+        cache["key"] = key
+    if trans not in cache:
+        lib = _hip.load_library()
+        cout, cin = w.shape[0], w.shape[1]
+        m, k = (cin, cout) if trans else (cout, cin)
+        wc = w.detach().reshape(cout, cin).contiguous()
+        out = torch.empty(int(lib.sp_gemm_x6_packed_size(m, k)), device=w.device)
+        _hip.check(lib.sp_gemm_x6_pack(_hip.ptr(wc), m, k, int(trans), _hip.ptr(out), _hip.stream_of(wc)),
+                   "sp_gemm_x6_pack")
+        cache[trans] = out
+    return cache[trans]
+
+
+def _x6_ok(m: int, c1: int, c2: int, o1: int, o2: int, hw: int) -> bool:
+    lib = _hip.load_library()
+    return (_shortcut_backend() == "x6" and bool(lib.sp_gemm_x6_supported(m, c1 + c2, hw))
+            and c1 % 8 == 0 and c2 % 8 == 0 and o1 % 32 == 0 and o2 % 32 == 0)
+
+
 def _shortcut_forward(conv: nn.Conv2d, x1: Tensor, x2: Tensor | None) -> Tensor:
     """1x1 conv_shortcut over cat(x1, x2) without its bias (the caller folds it into conv2's):
-    W[:, :c1] x1 + W[:, c1:] x2 as broadcast-batched GEMMs, the second part accumulated in
-    place (no concatenated input; 25-35 % faster than MIOpen's 1x1 path on these shapes,
-    tools/bench_shortcut.py)."""
+    one pass of the bf16x6 1x1 GEMM over both parts read in place (``csrc/sp_gemm_x6.hip``),
+    or W[:, :c1] x1 + W[:, c1:] x2 as broadcast-batched fp32 GEMMs, the second part
+    accumulated in place (no concatenated input; 25-35 % faster than MIOpen's 1x1 path on
+    these shapes, tools/bench_shortcut.py)."""
     n, c1 = x1.shape[:2]
+    c2 = 0 if x2 is None else x2.shape[1]
+    cout = conv.out_channels
+    hw = x1[0, 0].numel()
+    if _x6_ok(cout, c1, c2, cout, 0, hw):
+        lib = _hip.load_library()
+        x1 = x1.contiguous()
+        x2 = None if x2 is None else x2.contiguous()
+        y = torch.empty((n, cout) + tuple(x1.shape[2:]), device=x1.device, dtype=torch.float32)
+        _hip.check(lib.sp_gemm_x6(_hip.ptr(x1), c1, _hip.ptr(x2), c2, _hip.ptr(_pointwise_pack(conv, False)),
+                                  None, None, n, hw, _hip.ptr(y), cout, None, 0, _hip.stream_of(x1)),
+                   "sp_gemm_x6")
+        return y
     w = conv.weight[:, :, 0, 0]
     y = torch.matmul(w[:, :c1], x1.reshape(n, c1, -1))
     if x2 is not None:
@@ -86,8 +136,18 @@ def _shortcut_forward(conv: nn.Conv2d, x1: Tensor, x2: Tensor | None) -> Tensor:
 
 
 def _shortcut_input_vjp(conv: nn.Conv2d, dy: Tensor, c1: int, c2: int) -> tuple[Tensor, Tensor | None]:
-    """(W[:, :c1]^T dy, W[:, c1:]^T dy) as batched GEMMs."""
+    """(W[:, :c1]^T dy, W[:, c1:]^T dy): one pass of the bf16x6 1x1 GEMM writing both parts,
+    or two fp32 batched GEMMs."""
     n, cout = dy.shape[:2]
+    hw = dy[0, 0].numel()
+    if _x6_ok(c1 + c2, cout, 0, c1, c2, hw):
+        lib = _hip.load_library()
+        dy = dy.contiguous()
+        d1 = torch.empty((n, c1) + tuple(dy.shape[2:]), device=dy.device, dtype=torch.float32)
+        d2 = torch.empty((n, c2) + tuple(dy.shape[2:]), device=dy.device, dtype=torch.float32) if c2 else None
+        _hip.check(lib.sp_gemm_x6(_hip.ptr(dy), cout, None, 0, _hip.ptr(_pointwise_pack(conv, True)), None, None,
+                                  n, hw, _hip.ptr(d1), c1, _hip.ptr(d2), c2, _hip.stream_of(dy)), "sp_gemm_x6")
+        return d1, d2
     dyv = dy.reshape(n, cout, -1)
     w = conv.weight[:, :, 0, 0]
     d1 = torch.matmul(w[:, :c1].t(), dyv).reshape((n, c1) + tuple(dy.shape[2:]))

@@ -1,0 +1,101 @@
+"""The bf16x6 1x1-conv GEMM (csrc/sp_gemm_x6.hip) against fp64: Y = W cat(x1, x2) (+ bias)
+(+ residual), and the two-output transposed form of the UNet shortcut's input VJP.
+
+Tolerance: relative L2 <= 1.5x the error of torch's fp32 GEMM on the same data, and < 1e-6
+(three exact bf16 terms per operand, six partial products, fp32 accumulation)."""
+
+import pytest
+import torch
+
+from samplers_amd import _hip
+
+pytestmark = pytest.mark.gpu
+
+CASES = [  # n, c1, c2, o1, o2, h, w
+    (2, 64, 64, 128, 0, 16, 16),
+    (1, 128, 0, 128, 0, 32, 32),
+    (2, 128, 0, 64, 64, 16, 32),
+    (3, 96, 32, 256, 0, 16, 16),
+    (2, 128, 0, 96, 32, 32, 16),
+]
+
+
+def _rel(a, b):
+    return float((a.double().cpu() - b).norm() / b.norm())
+
+
+@pytest.mark.parametrize("case", CASES)
+@pytest.mark.parametrize("extras", [False, True])
+def test_gemm_x6_matches_fp64(cuda, case, extras):
+    n, c1, c2, o1, o2, h, w = case
+    lib = _hip.load_library()
+    k, m, hw = c1 + c2, o1 + o2, h * w
+    assert lib.sp_gemm_x6_supported(m, k, hw)
+    g = torch.Generator().manual_seed(sum(case))
+    x1 = torch.randn(n, c1, h, w, generator=g)
+    x2 = torch.randn(n, c2, h, w, generator=g) if c2 else None
+    W = torch.randn(m, k, generator=g) * k ** -0.5
+    bias = torch.randn(m, generator=g) if extras else None
+    res = torch.randn(n, o1, h, w, generator=g) if extras and not o2 else None
+    x = x1 if x2 is None else torch.cat([x1, x2], 1)
+    ref = torch.einsum("ok,nkp->nop", W.double(), x.reshape(n, k, hw).double())
+    if bias is not None:
+        ref = ref + bias.double()[None, :, None]
+    if res is not None:
+        ref = ref + res.reshape(n, o1, hw).double()
+    t32 = torch.einsum("ok,nkp->nop", W.to(cuda), x.reshape(n, k, hw).to(cuda))
+    if bias is not None:
+        t32 = t32 + bias.to(cuda)[None, :, None]
+    if res is not None:
+        t32 = t32 + res.reshape(n, o1, hw).to(cuda)
+
+    st = torch.cuda.current_stream().cuda_stream
+    wg = W.to(cuda)
+    wp = torch.empty(int(lib.sp_gemm_x6_packed_size(m, k)), device=cuda)
+    _hip.check(lib.sp_gemm_x6_pack(wg.data_ptr(), m, k, 0, wp.data_ptr(), st), "pack")
+    x1g = x1.to(cuda)
+    x2g = None if x2 is None else x2.to(cuda)
+    y1 = torch.full((n, o1, h, w), float("nan"), device=cuda)
+    y2 = torch.full((n, o2, h, w), float("nan"), device=cuda) if o2 else None
+    _hip.check(lib.sp_gemm_x6(x1g.data_ptr(), c1, None if x2g is None else x2g.data_ptr(), c2,
+                              wp.data_ptr(), None if bias is None else bias.to(cuda).data_ptr(),
+                              None if res is None else res.to(cuda).data_ptr(), n, hw, y1.data_ptr(),
+                              o1, None if y2 is None else y2.data_ptr(), o2, st), "sp_gemm_x6")
+    torch.cuda.synchronize()
+    y = y1.reshape(n, o1, hw) if y2 is None else torch.cat([y1, y2], 1).reshape(n, m, hw)
+    assert torch.isfinite(y).all()
+    e6, e32 = _rel(y, ref), _rel(t32, ref)
+    assert e6 <= 1.5 * e32 + 1e-9 and e6 < 1e-6, (e6, e32)
+
+
+def test_gemm_x6_transposed_pack_is_the_vjp(cuda):
+    """trans = 1 packs W stored [K][M]: the shortcut's input VJP W^T dy into two outputs."""
+    lib = _hip.load_library()
+    n, co, c1, c2, h, w = 2, 128, 64, 64, 16, 16
+    g = torch.Generator().manual_seed(3)
+    W = torch.randn(co, c1 + c2, generator=g) * 0.1
+    dy = torch.randn(n, co, h, w, generator=g)
+    ref = torch.einsum("ok,nop->nkp", W.double(), dy.reshape(n, co, h * w).double())
+    st = torch.cuda.current_stream().cuda_stream
+    wg = W.to(cuda)
+    wp = torch.empty(int(lib.sp_gemm_x6_packed_size(c1 + c2, co)), device=cuda)
+    _hip.check(lib.sp_gemm_x6_pack(wg.data_ptr(), c1 + c2, co, 1, wp.data_ptr(), st), "pack")
+    d1 = torch.empty(n, c1, h, w, device=cuda)
+    d2 = torch.empty(n, c2, h, w, device=cuda)
+    dyg = dy.to(cuda)
+    _hip.check(lib.sp_gemm_x6(dyg.data_ptr(), co, None, 0, wp.data_ptr(), None, None, n, h * w,
+                              d1.data_ptr(), c1, d2.data_ptr(), c2, st), "sp_gemm_x6")
+    torch.cuda.synchronize()
+    got = torch.cat([d1, d2], 1).reshape(n, c1 + c2, h * w)
+    assert _rel(got, ref) < 1e-6
+
+
+def test_gemm_x6_rejects_bad_shapes(cuda):
+    lib = _hip.load_library()
+    assert not lib.sp_gemm_x6_supported(96, 64, 256)     # M % 128
+    assert not lib.sp_gemm_x6_supported(128, 24, 256)    # K % 16
+    assert not lib.sp_gemm_x6_supported(128, 64, 200)    # HW % 256
+    x = torch.empty(1, device=cuda)
+    # residual with a split output is refused
+    assert lib.sp_gemm_x6(x.data_ptr(), 64, None, 0, x.data_ptr(), None, x.data_ptr(), 1, 256,
+                          x.data_ptr(), 64, x.data_ptr(), 64, 0) != 0
