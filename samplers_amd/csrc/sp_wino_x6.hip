@@ -150,14 +150,22 @@ __device__ __forceinline__ void x6_stage(float* xw, const X6Lane& L, int lane, c
 }
 
 // U terms of one k-step (48 KB, contiguous in the packed layout) -> LDS buffer, 12 direct
-// buffer loads of 1 KB per wave (lane offset lane * 16 in one VGPR, the chunk as a scalar)
+// buffer loads of 1 KB per wave (lane offset lane * 16 in one VGPR, the chunk as a scalar).
+// Written as inline asm: the compiler's wait insertion does not see these loads, so it does not
+// drain them (vmcnt(0)) before every LDS read of the k-step; the kernel waits for them itself.
+__device__ __forceinline__ void x6_lds_dma(__amdgpu_buffer_rsrc_t rs, const void* lds, int voff, int soff) {
+    const unsigned la = static_cast<unsigned>(reinterpret_cast<size_t>((lds_void*)lds));
+    asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds"
+                 :
+                 : "s"(__builtin_amdgcn_readfirstlane(la)), "v"(voff), "s"(rs), "s"(soff)
+                 : "memory", "m0");
+}
 __device__ __forceinline__ void x6_load_u(__amdgpu_buffer_rsrc_t urs, int stage, int wv, int lane,
                                           unsigned char* ubuf) {
 #pragma unroll
     for (int i = 0; i < 12; ++i) {
         const int chunk = 12 * wv + i;
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(urs, (lds_void*)(ubuf + chunk * 1024), 16, lane * 16,
-                                                 stage * X6_USTAGE + chunk * 1024, 0, 0);
+        x6_lds_dma(urs, ubuf + chunk * 1024, lane * 16, stage * X6_USTAGE + chunk * 1024);
     }
 }
 
