@@ -23,8 +23,10 @@ def kind(n: str) -> str:
         return "HIP guidance passes"
     if "miopen" in n or "igemm" in n or "naive_conv" in n or "transpose" in n:
         return "MIOpen convs (16x16 / 8x8 stride-2) + layout transposes"
+    if "k_gemm_x6" in n:
+        return "HIP 1x1 shortcut GEMM (bf16x6, fwd + VJP)"
     if "Cijk" in n:
-        return "hipBLASLt GEMMs (1x1 shortcuts, attention, time embedding)"
+        return "hipBLASLt GEMMs (attention, time embedding)"
     if "CUDAFunctor_add" in n:
         return "torch adds"
     if "softmax" in n.lower():
