@@ -207,6 +207,56 @@ static void run(const char* name, K kern, int nm, int gap, double flops_per_mfma
            "\"cycles_per_mfma_at_2.4GHz\": %.1f}\n", name, kind, gap, tf, cyc);
 }
 
+
+// Two waves per SIMD (512 threads) vs one (256): 16x16x4 f32 MFMAs on 32 independent
+// accumulators (128 registers) with GAP fillers after every EVERY-th MFMA.  If one wave's
+// VALU work co-executes with the other wave's MFMAs, the fillers' cost disappears at 2 waves.
+template <int GAP, int EVERY, int KIND>
+__global__ __launch_bounds__(512, 1) void k16w(int iters, float* out) {
+    f32x4 acc[32];
+#pragma unroll
+    for (int i = 0; i < 32; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    float a = threadIdx.x * 1e-3f, b = 1.0001f;
+    float f[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) f[i] = a + i;
+    for (int it = 0; it < iters; ++it) {
+#pragma unroll
+        for (int i = 0; i < 32; ++i) {
+            acc[i] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc[i], 0, 0, 0);
+            __builtin_amdgcn_sched_barrier(0);
+            if (i % EVERY == EVERY - 1) fillers<GAP, KIND>(f, b);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    }
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < 32; ++i) s += acc[i][0] + acc[i][3];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) s += f[i];
+    out[blockIdx.x * 512 + threadIdx.x] = s;
+}
+
+template <class K>
+static void run_w(const char* name, K kern, int threads, int nm, int gap, double flops_per_mfma, float* out,
+                  int cus, const char* kind) {
+    const int iters = 1000;
+    hipEvent_t e0, e1;
+    hipEventCreate(&e0);
+    hipEventCreate(&e1);
+    kern<<<cus, threads>>>(10, out);
+    hipEventRecord(e0);
+    kern<<<cus, threads>>>(iters, out);
+    hipEventRecord(e1);
+    hipEventSynchronize(e1);
+    float ms = 0.f;
+    hipEventElapsedTime(&ms, e0, e1);
+    const double mfmas = (double)cus * (threads / 64) * iters * nm;
+    const double tf = mfmas * flops_per_mfma / (ms * 1e-3) / 1e12;
+    printf("{\"shape\": \"%s\", \"waves_per_simd\": %d, \"filler\": \"%s\", \"per_burst\": %d, \"tflops\": %.1f}\n",
+           name, threads / 256, kind, gap, tf);
+}
+
 int main() {
     int cus = 0;
     hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0);
@@ -264,6 +314,13 @@ int main() {
     run("bf16 32x32x16", kbf<2, 1, 4>, 16, 2, 32768, out, cus, kinds[4]);
     run("bf16 32x32x16 burst/4", kbf<16, 4, 1>, 16, 16, 32768, out, cus, kinds[1]);
     run("bf16 32x32x16 burst/16", kbf<64, 16, 1>, 16, 64, 32768, out, cus, kinds[1]);
+    for (int thr : {256, 512}) {
+        run_w("16x16x4 f32", k16w<0, 1, 0>, thr, 32, 0, 2048, out, cus, kinds[0]);
+        run_w("16x16x4 f32", k16w<16, 4, 1>, thr, 32, 16, 2048, out, cus, kinds[1]);
+        run_w("16x16x4 f32", k16w<16, 16, 1>, thr, 32, 16, 2048, out, cus, kinds[1]);
+        run_w("16x16x4 f32", k16w<8, 4, 0>, thr, 32, 8, 2048, out, cus, kinds[0]);
+        run_w("16x16x4 f32", k16w<32, 16, 0>, thr, 32, 32, 2048, out, cus, kinds[0]);
+    }
     hipFree(out);
     return 0;
 }
