@@ -75,10 +75,12 @@ __device__ __forceinline__ f32x16 g6_mfma(uvec4 a, uvec4 b, f32x16 c) {
 // later LDS read it cannot prove disjoint; the kernel waits for these loads itself (counted vmcnt)
 __device__ __forceinline__ void g6_lds_dma(__amdgpu_buffer_rsrc_t rs, const void* lds, int voff, int soff) {
     const unsigned la = static_cast<unsigned>(reinterpret_cast<size_t>((lds_void_g*)lds));
-    asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds"
-                 :
+    unsigned keep;  // m0 is reserved to the compiler: saved and restored around the load
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\tbuffer_load_dwordx4 %2, %3, %4 offen lds\n\t"
+                 "s_mov_b32 m0, %0"
+                 : "=&s"(keep)
                  : "s"(__builtin_amdgcn_readfirstlane(la)), "v"(voff), "s"(rs), "s"(soff)
-                 : "memory", "m0");
+                 : "memory");
 }
 
 // gfx9 s_waitcnt immediate: vmcnt <= n (6 bits), lgkmcnt / expcnt not waited for

@@ -155,10 +155,12 @@ __device__ __forceinline__ void x6_stage(float* xw, const X6Lane& L, int lane, c
 // drain them (vmcnt(0)) before every LDS read of the k-step; the kernel waits for them itself.
 __device__ __forceinline__ void x6_lds_dma(__amdgpu_buffer_rsrc_t rs, const void* lds, int voff, int soff) {
     const unsigned la = static_cast<unsigned>(reinterpret_cast<size_t>((lds_void*)lds));
-    asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds"
-                 :
+    unsigned keep;  // m0 is reserved to the compiler: saved and restored around the load
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\tbuffer_load_dwordx4 %2, %3, %4 offen lds\n\t"
+                 "s_mov_b32 m0, %0"
+                 : "=&s"(keep)
                  : "s"(__builtin_amdgcn_readfirstlane(la)), "v"(voff), "s"(rs), "s"(soff)
-                 : "memory", "m0");
+                 : "memory");
 }
 __device__ __forceinline__ void x6_load_u(__amdgpu_buffer_rsrc_t urs, int stage, int wv, int lane,
                                           unsigned char* ubuf) {
