@@ -399,6 +399,15 @@ int sp_gemm_x6(const float* x1, int32_t c1, const float* x2, int32_t c2, const f
                const float* bias, const float* res, int64_t n, int64_t hw, float* y1, int32_t o1,
                float* y2, int32_t o2, sp_stream_t stream);
 
+/* nn.Linear on token-major activations with the same bf16x6 arithmetic:
+ * y[t][o] = sum_k x[t][k] W[o][k] (+ bias[o]) (+ res[t][o]), tokens % 256, k % 16, m % 32
+ * (W's rows padded to 128 with zeros by sp_gemm_x6_pack; pack W^T with trans = 1 for the
+ * input VJP).  Replaces torch.nn.functional.linear in the ε-UNets' attention / transformer
+ * blocks (diffusers Attention to_q/k/v/out, FeedForward), SURVEY.md §8f f1. */
+int sp_linear_x6_supported(int64_t tokens, int32_t k, int32_t m);
+int sp_linear_x6(const float* x, const float* wp, const float* bias, const float* res, int64_t tokens,
+                 int32_t k, int32_t m, float* y, sp_stream_t stream);
+
 /* Fused self-attention softmax(q k^T * scale) v of the SD 1.5 eps-UNet's transformer blocks
  * (attn1 over the latent tokens; diffusers UNet2DConditionModel, stable_diffusion.py:306-313;
  * replaces the scores / softmax / weighted-sum chain and its autograd VJP) on fp32 MFMA,

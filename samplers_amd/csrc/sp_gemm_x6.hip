@@ -53,6 +53,8 @@ struct G6Geom {
     const float* res;     // nullable, shaped like y1 (o2 == 0 only)
     int c1, c2, o1, o2, hw;
     int ntiles, cob, ptiles, nsteps;
+    // token-major mode (k_gemm_x6<true>, nn.Linear on [tokens][features]): x1 is [hw][c1],
+    // y1 is [hw][o1] with o1 % 32 (W's rows padded to 128 with zeros), one input and output
 };
 
 __device__ __forceinline__ void g6_split(float v, unsigned& h, unsigned& m, unsigned& l) {
@@ -103,6 +105,20 @@ __device__ __forceinline__ void g6_dma_x(const G6Geom& g, int n, int p0, int kst
     }
 }
 
+// token-major X (nn.Linear input [tokens][c1]) -> LDS slot [256 tokens][16 ch] fp32: load i of
+// wave wv covers tokens 16 (2 wv + i) .. +15, lane l: token + (l >> 2), channels 4 (l & 3) .. +3
+__device__ __forceinline__ void g6_dma_x_tm(const G6Geom& g, int p0, int kstep, int wv, int lane,
+                                            unsigned char* slot) {
+    const auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(g.x1), (short)0, g.hw * g.c1 * 4,
+                                                      0x00020000);
+    const int vo = ((lane >> 2) * g.c1 + 4 * (lane & 3)) * 4;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const int t0 = p0 + 16 * (2 * wv + i);
+        g6_lds_dma(rs, slot + (2 * wv + i) * 1024, vo, (t0 * g.c1 + kstep * G6_KC) * 4);
+    }
+}
+
 // W fragments of one k-step (12 KB contiguous in the packed layout): 12 direct 1-KB loads, two
 // by each of waves 0-3 and one by each of waves 4-7
 __device__ __forceinline__ void g6_dma_w(__amdgpu_buffer_rsrc_t wrs, int stage, int wv, int lane,
@@ -139,6 +155,29 @@ __device__ __forceinline__ void g6_split_x(const unsigned char* raw, unsigned ch
     *reinterpret_cast<uvec4*>(xb + 2 * G6_PX * G6_KC * 2 + off) = tl;
 }
 
+// token-major raw slot -> the same split layout: thread = channels 8 (tid >> 8) .. +7 of token tid & 255
+__device__ __forceinline__ void g6_split_x_tm(const unsigned char* raw, unsigned char* xb, int tid) {
+    const int grp = tid >> 8, px = tid & 255;
+    const uvec4 a = *reinterpret_cast<const uvec4*>(raw + px * 64 + grp * 32);
+    const uvec4 b = *reinterpret_cast<const uvec4*>(raw + px * 64 + grp * 32 + 16);
+    const float v[8] = {__uint_as_float(a[0]), __uint_as_float(a[1]), __uint_as_float(a[2]), __uint_as_float(a[3]),
+                        __uint_as_float(b[0]), __uint_as_float(b[1]), __uint_as_float(b[2]), __uint_as_float(b[3])};
+    uvec4 th, tm, tl;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        unsigned h0, m0, l0, h1, m1, l1;
+        g6_split(v[2 * q], h0, m0, l0);
+        g6_split(v[2 * q + 1], h1, m1, l1);
+        th[q] = g6_pack(h0, h1);
+        tm[q] = g6_pack(m0, m1);
+        tl[q] = g6_pack(l0, l1);
+    }
+    const int off = (px * G6_KC + 8 * grp) * 2;
+    *reinterpret_cast<uvec4*>(xb + 0 * G6_PX * G6_KC * 2 + off) = th;
+    *reinterpret_cast<uvec4*>(xb + 1 * G6_PX * G6_KC * 2 + off) = tm;
+    *reinterpret_cast<uvec4*>(xb + 2 * G6_PX * G6_KC * 2 + off) = tl;
+}
+
 struct G6Pos { int n, p0, cb; };
 __device__ __forceinline__ G6Pos g6_pos(const G6Geom& g, int t) {
     // XCD-aware: the output-channel blocks of one pixel tile on one XCD (shared X lines)
@@ -151,7 +190,7 @@ __device__ __forceinline__ G6Pos g6_pos(const G6Geom& g, int t) {
 // epilogue: register q of tile (a, b) = channel 32 sub + (q&3) + 8(q>>2) + 4(lane>>5),
 // pixel 64 pq + 32 b + (lane & 31); bias and residual added, the 32-channel block to y1 or y2
 __device__ __forceinline__ void g6_epilogue(const G6Geom& g, const G6Pos& ps, int ch, int pq, int lane,
-                                            const f32x16 (&acc)[2][2]) {
+                                            const f32x16 (&acc)[2][2], const f32x16 (&acs)[2][2]) {
 #pragma unroll
     for (int a = 0; a < 2; ++a) {
         const int co0 = ps.cb * G6_CO + 32 * (2 * ch + a);  // first channel of the 32-block
@@ -185,8 +224,44 @@ __device__ __forceinline__ void g6_epilogue(const G6Geom& g, const G6Pos& ps, in
                 const float b0 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, bl), c));
                 const float b1 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, bl), c + 4));
                 const int cc = c + 4 * (lane >> 5);
-                const float y = acc[a][b][q] + ((lane >> 5) ? b1 : b0) + rv[q];
+                const float y = (acc[a][b][q] + acs[a][b][q]) + ((lane >> 5) ? b1 : b0) + rv[q];
                 __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(y), ors, vo + cc * g.hw * 4, 0, 0);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    }
+}
+
+// token-major epilogue: the MFMA ran with X as A and W as B, so register q of tile (a, b) is token
+// 128 ph... = p0 + 64 pq + 32 b + (q&3) + 8(q>>2) + 4(lane>>5) and output feature o0 + (lane & 31):
+// each register row is 32 consecutive features of one token (128 contiguous bytes)
+__device__ __forceinline__ void g6_epilogue_tm(const G6Geom& g, const G6Pos& ps, int ch, int pq, int lane,
+                                               const f32x16 (&acc)[2][2], const f32x16 (&acs)[2][2]) {
+    const auto ors = __builtin_amdgcn_make_buffer_rsrc(g.y1, (short)0, g.hw * g.o1 * 4, 0x00020000);
+    const auto rrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(g.res ? g.res : g.y1), (short)0,
+                                                       g.res ? g.hw * g.o1 * 4 : 0, 0x00020000);
+#pragma unroll
+    for (int a = 0; a < 2; ++a) {
+        const int o = ps.cb * G6_CO + 32 * (2 * ch + a) + (lane & 31);
+        if (ps.cb * G6_CO + 32 * (2 * ch + a) >= g.o1) continue;  // padded rows of W (uniform)
+        const float bv = g.bias ? g.bias[o] : 0.f;
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+            const int t0 = ps.p0 + pq * 64 + b * 32 + 4 * (lane >> 5);
+            float rv[16];
+#pragma unroll
+            for (int q = 0; q < 16; ++q) rv[q] = 0.f;
+            if (g.res) {
+#pragma unroll
+                for (int q = 0; q < 16; ++q)
+                    rv[q] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
+                        rrs, ((t0 + (q & 3) + 8 * (q >> 2)) * g.o1 + o) * 4, 0, 0));
+            }
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
+                const float y = (acc[a][b][q] + acs[a][b][q]) + bv + rv[q];
+                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(y), ors,
+                                                      ((t0 + (q & 3) + 8 * (q >> 2)) * g.o1 + o) * 4, 0, 0);
             }
             __builtin_amdgcn_sched_barrier(0);
         }
@@ -200,6 +275,7 @@ __device__ __forceinline__ void g6_epilogue(const G6Geom& g, const G6Pos& ps, in
 // Eight waves, two per SIMD: one wave's MFMAs cover the other's LDS waits and split work.
 constexpr int G6_THREADS = 512;
 
+template <bool TM>
 __global__ __launch_bounds__(G6_THREADS, 1) void k_gemm_x6(G6Geom g) {
     __shared__ __attribute__((aligned(16))) unsigned char xraw[4][G6_KC * G6_PX * 4];
     __shared__ __attribute__((aligned(16))) unsigned char xs[2][G6_XB];
@@ -225,7 +301,10 @@ __global__ __launch_bounds__(G6_THREADS, 1) void k_gemm_x6(G6Geom g) {
         }
     };
     auto dma_x = [&]() {
-        if (cx.j < J) g6_dma_x(g, cx.ps.n, cx.ps.p0, cx.s, wv, lane, xraw[cx.slot]);
+        if (cx.j < J) {
+            if constexpr (TM) g6_dma_x_tm(g, cx.ps.p0, cx.s, wv, lane, xraw[cx.slot]);
+            else g6_dma_x(g, cx.ps.n, cx.ps.p0, cx.s, wv, lane, xraw[cx.slot]);
+        }
         advance(cx, 4);
     };
     auto dma_w = [&]() {
@@ -240,18 +319,22 @@ __global__ __launch_bounds__(G6_THREADS, 1) void k_gemm_x6(G6Geom g) {
     dma_x();
     __builtin_amdgcn_s_waitcnt(g6_vmcnt(0));
     __builtin_amdgcn_s_barrier();
-    g6_split_x(xraw[0], xs[0], tid);
+    if constexpr (TM) g6_split_x_tm(xraw[0], xs[0], tid);
+    else g6_split_x(xraw[0], xs[0], tid);
     __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
     __builtin_amdgcn_s_barrier();
 
     const bool four = g6_dma_per_wave(wv) == 4;  // this wave's W loads per step: 2 (else 1)
-    f32x16 acc[2][2];
+    // two accumulators per tile: the leading product (hi x hi) and the five small terms, so the
+    // small terms' fp32 roundings happen at 2^-8 of the result's magnitude (with one
+    // accumulator the error grew past an fp32 GEMM's at K = 768)
+    f32x16 acc[2][2], acs[2][2];
     int j = 0, wslot = 0, xslot1 = 1;  // W slot of step j, X slot of step j + 1
     for (int tw = 0; tw < ntile_wg; ++tw) {
 #pragma unroll
         for (int a = 0; a < 2; ++a)
 #pragma unroll
-            for (int b = 0; b < 2; ++b) acc[a][b] = f32x16{};
+            for (int b = 0; b < 2; ++b) acc[a][b] = f32x16{}, acs[a][b] = f32x16{};
         for (int s = 0; s < g.nsteps; ++s, ++j) {
 #if G6_EXP != 3
             dma_w();  // step j + 2
@@ -274,7 +357,8 @@ __global__ __launch_bounds__(G6_THREADS, 1) void k_gemm_x6(G6Geom g) {
             }
 #if G6_EXP != 2
             // X(j + 1)'s split (unconditional: past the stream's end it rewrites an unused slot)
-            g6_split_x(xraw[xslot1], xs[(j + 1) & 1], tid);
+            if constexpr (TM) g6_split_x_tm(xraw[xslot1], xs[(j + 1) & 1], tid);
+            else g6_split_x(xraw[xslot1], xs[(j + 1) & 1], tid);
 #endif
 #if G6_EXP != 1
             // the six partial products (small terms first) over the 4 independent accumulators
@@ -284,7 +368,12 @@ __global__ __launch_bounds__(G6_THREADS, 1) void k_gemm_x6(G6Geom g) {
 #pragma unroll
                 for (int b = 0; b < 2; ++b)
 #pragma unroll
-                    for (int a = 0; a < 2; ++a) acc[a][b] = g6_mfma(fu[a][TU[e]], fv[b][TV[e]], acc[a][b]);
+                    for (int a = 0; a < 2; ++a) {
+                        if constexpr (TM)  // tokens as the MFMA's rows: features contiguous in C
+                            (e == 5 ? acc : acs)[a][b] = g6_mfma(fv[b][TV[e]], fu[a][TU[e]], (e == 5 ? acc : acs)[a][b]);
+                        else
+                            (e == 5 ? acc : acs)[a][b] = g6_mfma(fu[a][TU[e]], fv[b][TV[e]], (e == 5 ? acc : acs)[a][b]);
+                    }
 #endif
 #if G6_SCHED
             // issue order: the fragment reads, the split's reads, then the MFMAs with the split's
@@ -308,7 +397,8 @@ __global__ __launch_bounds__(G6_THREADS, 1) void k_gemm_x6(G6Geom g) {
             xslot1 = xslot1 == 3 ? 0 : xslot1 + 1;
         }
         const G6Pos ps = g6_pos(g, b0 + tw * G);
-        g6_epilogue(g, ps, ch, pq, lane, acc);
+        if constexpr (TM) g6_epilogue_tm(g, ps, ch, pq, lane, acc, acs);
+        else g6_epilogue(g, ps, ch, pq, lane, acc, acs);
     }
 }
 
@@ -317,10 +407,11 @@ __global__ __launch_bounds__(G6_THREADS, 1) void k_gemm_x6(G6Geom g) {
 // for row 128 cb + 32 sub + (lane & 31), column 16 s + 8 (lane >> 5) + j.
 __global__ void k_gemm_x6_pack(const float* __restrict__ w, int m, int k, int trans,
                                unsigned short* __restrict__ wp) {
+    const int mpad = (m + G6_CO - 1) / G6_CO * G6_CO;  // rows past m packed as zeros
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= (int64_t)m * k) return;
+    if (i >= (int64_t)mpad * k) return;
     const int row = static_cast<int>(i / k), col = static_cast<int>(i - (int64_t)row * k);
-    const float v = trans ? w[(int64_t)col * m + row] : w[i];
+    const float v = row >= m ? 0.f : trans ? w[(int64_t)col * m + row] : w[(int64_t)row * k + col];
     unsigned h, mm, l;
     g6_split(v, h, mm, l);
     const int nsteps = k / G6_KC, cb = row / G6_CO, sub = (row % G6_CO) / 32, s = col / G6_KC;
@@ -342,11 +433,13 @@ int sp_gemm_x6_supported(int32_t m, int32_t k, int64_t hw) {
            hw % G6_PX == 0 && hw * 32 * 4 < (int64_t(1) << 31);
 }
 
-int64_t sp_gemm_x6_packed_size(int32_t m, int32_t k) { return (int64_t)m * k * 6 / 4; }
+int64_t sp_gemm_x6_packed_size(int32_t m, int32_t k) {
+    return (int64_t)((m + G6_CO - 1) / G6_CO * G6_CO) * k * 6 / 4;
+}
 
 int sp_gemm_x6_pack(const float* w, int32_t m, int32_t k, int32_t trans, float* wp, sp_stream_t stream) {
-    if (!w || !wp || m % G6_CO || k % G6_KC || m <= 0 || k <= 0) return SP_EINVAL;
-    const int64_t total = (int64_t)m * k;
+    if (!w || !wp || m % 32 || k % G6_KC || m <= 0 || k <= 0) return SP_EINVAL;
+    const int64_t total = (int64_t)((m + G6_CO - 1) / G6_CO * G6_CO) * k;
     launch(0, k_gemm_x6_pack, dim3(static_cast<unsigned>((total + 255) / 256)), dim3(256),
            static_cast<hipStream_t>(stream), w, m, k, trans, reinterpret_cast<unsigned short*>(wp));
     return check_launch("sp_gemm_x6_pack");
@@ -395,8 +488,39 @@ int sp_gemm_x6(const float* x1, int32_t c1, const float* x2, int32_t c2, const f
     g.ptiles = static_cast<int>(hw / G6_PX);
     g.nsteps = k / G6_KC;
     const int grid = static_cast<int>(std::min<int64_t>(tiles, g6_cu_count()));
-    launch(0, k_gemm_x6, dim3(grid), dim3(G6_THREADS), static_cast<hipStream_t>(stream), g);
+    launch(0, k_gemm_x6<false>, dim3(grid), dim3(G6_THREADS), static_cast<hipStream_t>(stream), g);
     return check_launch("sp_gemm_x6");
+}
+
+int sp_linear_x6_supported(int64_t tokens, int32_t k, int32_t m) {
+    return tokens >= G6_PX && tokens % G6_PX == 0 && k >= G6_KC && k % G6_KC == 0 && m >= 32 && m % 32 == 0 &&
+           tokens * (int64_t)std::max(k, m) * 4 < (int64_t(1) << 31);
+}
+
+// nn.Linear on token-major activations: y[t][o] = sum_k x[t][k] W[o][k] (+ bias[o]) (+ res[t][o]);
+// W packed by sp_gemm_x6_pack(w, m, k, 0) (or trans = 1 from W^T for the input VJP).
+int sp_linear_x6(const float* x, const float* wp, const float* bias, const float* res, int64_t tokens,
+                 int32_t k, int32_t m, float* y, sp_stream_t stream) {
+    if (!sp_linear_x6_supported(tokens, k, m)) return SP_EINVAL;
+    if (!x || !wp || !y || (res && res == y)) return SP_EINVAL;
+    const int cob = (m + G6_CO - 1) / G6_CO;
+    const int64_t tiles = tokens / G6_PX * cob;
+    G6Geom g = {};
+    g.x1 = x;
+    g.wp = reinterpret_cast<const unsigned short*>(wp);
+    g.y1 = y;
+    g.bias = bias;
+    g.res = res;
+    g.c1 = k;
+    g.o1 = m;
+    g.hw = static_cast<int>(tokens);
+    g.ntiles = static_cast<int>(tiles);
+    g.cob = cob;
+    g.ptiles = static_cast<int>(tokens / G6_PX);  // one "image" of all tokens
+    g.nsteps = k / G6_KC;
+    const int grid = static_cast<int>(std::min<int64_t>(tiles, g6_cu_count()));
+    launch(0, k_gemm_x6<true>, dim3(grid), dim3(G6_THREADS), static_cast<hipStream_t>(stream), g);
+    return check_launch("sp_linear_x6");
 }
 
 }  // extern "C"

@@ -499,3 +499,87 @@ def downsample_conv(module: nn.Conv2d, x: Tensor, box: SkipGrad | None = None) -
     if box is not None:
         box.enabled = False
     return conv3x3_stride2(module, x, padding=0)
+
+
+# ---------------------------------------------------------------------------------------
+# nn.Linear on token-major activations: fp32 arithmetic on the bf16 MFMAs (csrc/sp_gemm_x6.hip)
+# ---------------------------------------------------------------------------------------
+
+def linear_backend() -> str:
+    """``SAMPLERS_AMD_LINEAR``: ``x6`` (default: ``sp_linear_x6`` where its shape rules hold —
+    exact three-term bf16 splits of the fp32 operands, six partial products, fp32
+    accumulation) or ``torch`` (hipBLASLt fp32)."""
+    import os
+
+    return os.environ.get("SAMPLERS_AMD_LINEAR", "x6").lower()
+
+
+def _linear_pack(module: nn.Module, w2d: Tensor, trans: bool) -> Tensor:
+    """``w2d`` ([out, in]) packed for sp_linear_x6 (trans: as Wᵀ for the input VJP), cached on
+    ``module`` and rebuilt when the weight changes."""
+    key = (w2d.data_ptr(), module.weight._version, w2d.device)
+    cache = module.__dict__.setdefault("_x6_linear_packs", {})
+    if cache.get("key") != key:
+        cache.clear()
+        cache["key"] = key
+    if trans not in cache:
+        lib = _hip.load_library()
+        m, k = w2d.shape
+        wc = w2d.detach().contiguous()
+        rows, cols = (k, m) if trans else (m, k)
+        out = torch.empty(int(lib.sp_gemm_x6_packed_size(rows, cols)), device=w2d.device)
+        _hip.check(lib.sp_gemm_x6_pack(_hip.ptr(wc), rows, cols, int(trans), _hip.ptr(out), _hip.stream_of(wc)),
+                   "sp_gemm_x6_pack")
+        cache[trans] = out
+    return cache[trans]
+
+
+class _LinearX6Fn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias, module, w2d):
+        lib = _hip.load_library()
+        m, k = w2d.shape
+        x2 = x.reshape(-1, k).contiguous()
+        t = x2.shape[0]
+        y = torch.empty(t, m, device=x.device, dtype=torch.float32)
+        _hip.check(lib.sp_linear_x6(_hip.ptr(x2), _hip.ptr(_linear_pack(module, w2d, False)),
+                                    _hip.ptr(None if bias is None else bias.detach().contiguous()), None,
+                                    t, k, m, _hip.ptr(y), _hip.stream_of(x2)), "sp_linear_x6")
+        ctx.module, ctx.w2d, ctx.shape = module, w2d, x.shape
+        return y.reshape(*x.shape[:-1], m)
+
+    @staticmethod
+    def backward(ctx, dy):
+        """Input VJP only (the priors' weights are frozen): dx = dy W."""
+        lib = _hip.load_library()
+        m, k = ctx.w2d.shape
+        d2 = dy.reshape(-1, m).contiguous()
+        t = d2.shape[0]
+        dx = torch.empty(t, k, device=dy.device, dtype=torch.float32)
+        _hip.check(lib.sp_linear_x6(_hip.ptr(d2), _hip.ptr(_linear_pack(ctx.module, ctx.w2d, True)), None, None,
+                                    t, m, k, _hip.ptr(dx), _hip.stream_of(d2)), "sp_linear_x6")
+        return dx.reshape(ctx.shape), None, None, None, None
+
+
+def linear(x: Tensor, module: nn.Module, w2d: Tensor | None = None, bias: Tensor | None = None) -> Tensor:
+    """``F.linear(x, w2d, bias)`` (``w2d`` defaults to ``module.weight``, ``bias`` to
+    ``module.bias``) on ``sp_linear_x6`` when x is a CUDA fp32 token-major batch whose token
+    count and widths fit its rules and the weights are frozen; hipBLASLt otherwise."""
+    w2d = module.weight if w2d is None else w2d
+    bias = getattr(module, "bias", None) if bias is None else bias
+    m, k = w2d.shape
+    t = x.numel() // k if x.dim() else 0
+    if (x.is_cuda and x.dtype == torch.float32 and not w2d.requires_grad
+            and (bias is None or not bias.requires_grad) and linear_backend() == "x6"):
+        lib = _hip.load_library()
+        if lib.sp_linear_x6_supported(t, k, m):
+            return _LinearX6Fn.apply(x, w2d, bias, module, w2d)
+    return F.linear(x, w2d, bias)
+
+
+class Linear(nn.Linear):
+    """``nn.Linear`` (same parameters and state-dict keys) whose device forward / input VJP run
+    ``sp_linear_x6`` where it applies (``linear``)."""
+
+    def forward(self, x: Tensor) -> Tensor:
+        return linear(x, self)

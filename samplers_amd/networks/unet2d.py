@@ -27,7 +27,7 @@ import torch.nn.functional as F
 from torch import Tensor, nn
 
 from .. import _hip
-from .layers import (Conv3x3, GroupNormAct, SkipGrad, conv3x3_forward, conv3x3_input_vjp,
+from .layers import (Conv3x3, GroupNormAct, Linear, SkipGrad, conv3x3_forward, conv3x3_input_vjp,
                      downsample_conv, gn_backward, gn_forward, upsample_nearest2x)
 
 
@@ -301,10 +301,10 @@ class SpatialSelfAttention(nn.Module):
         super().__init__()
         self.heads = 1 if head_dim is None else channels // head_dim
         self.group_norm = GroupNormAct(groups, channels, eps=eps)
-        self.to_q = nn.Linear(channels, channels)
-        self.to_k = nn.Linear(channels, channels)
-        self.to_v = nn.Linear(channels, channels)
-        self.to_out = nn.ModuleList([nn.Linear(channels, channels)])
+        self.to_q = Linear(channels, channels)
+        self.to_k = Linear(channels, channels)
+        self.to_v = Linear(channels, channels)
+        self.to_out = nn.ModuleList([Linear(channels, channels)])
 
     def forward(self, x: Tensor) -> Tensor:
         b, c, h, w = x.shape

@@ -31,7 +31,7 @@ import torch.nn.functional as F
 from torch import Tensor, nn
 
 from .attention import attention
-from .layers import Conv3x3, GroupNormAct, SkipGrad, conv3x3_stride2
+from .layers import Conv3x3, GroupNormAct, Linear, SkipGrad, conv3x3_stride2, linear
 from .unet2d import ResnetBlock2D, TimestepEmbedding, Upsample2D, timestep_embedding
 
 
@@ -65,10 +65,10 @@ class Attention(nn.Module):
         super().__init__()
         kv_dim = context_dim or dim
         self.heads = heads
-        self.to_q = nn.Linear(dim, dim, bias=False)
-        self.to_k = nn.Linear(kv_dim, dim, bias=False)
-        self.to_v = nn.Linear(kv_dim, dim, bias=False)
-        self.to_out = nn.ModuleList([nn.Linear(dim, dim)])
+        self.to_q = Linear(dim, dim, bias=False)
+        self.to_k = Linear(kv_dim, dim, bias=False)
+        self.to_v = Linear(kv_dim, dim, bias=False)
+        self.to_out = nn.ModuleList([Linear(dim, dim)])
 
     def _split(self, t: Tensor) -> Tensor:
         b, n, c = t.shape
@@ -92,7 +92,7 @@ class Attention(nn.Module):
 class GEGLU(nn.Module):
     def __init__(self, dim: int, inner: int) -> None:
         super().__init__()
-        self.proj = nn.Linear(dim, 2 * inner)
+        self.proj = Linear(dim, 2 * inner)
 
     def forward(self, x: Tensor) -> Tensor:
         a, gate = self.proj(x).chunk(2, dim=-1)
@@ -103,7 +103,7 @@ class FeedForward(nn.Module):
     def __init__(self, dim: int, mult: int = 4) -> None:
         super().__init__()
         # diffusers' ModuleList layout: [GEGLU, Dropout, Linear]
-        self.net = nn.ModuleList([GEGLU(dim, dim * mult), nn.Dropout(0.0), nn.Linear(dim * mult, dim)])
+        self.net = nn.ModuleList([GEGLU(dim, dim * mult), nn.Dropout(0.0), Linear(dim * mult, dim)])
 
     def forward(self, x: Tensor) -> Tensor:
         return self.net[2](self.net[0](x))
@@ -138,10 +138,10 @@ class Transformer2DModel(nn.Module):
     def forward(self, x: Tensor, context: Tensor) -> Tensor:
         b, c, h, w = x.shape
         tokens = self.norm(x).reshape(b, c, h * w).transpose(1, 2)
-        tokens = F.linear(tokens, self.proj_in.weight.view(c, c), self.proj_in.bias)
+        tokens = linear(tokens, self.proj_in, self.proj_in.weight.view(c, c), self.proj_in.bias)
         for blk in self.transformer_blocks:
             tokens = blk(tokens, context)
-        out = F.linear(tokens, self.proj_out.weight.view(c, c), self.proj_out.bias)
+        out = linear(tokens, self.proj_out, self.proj_out.weight.view(c, c), self.proj_out.bias)
         return out.transpose(1, 2).reshape(b, c, h, w) + x
 
 

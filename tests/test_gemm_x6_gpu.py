@@ -99,3 +99,67 @@ def test_gemm_x6_rejects_bad_shapes(cuda):
     # residual with a split output is refused
     assert lib.sp_gemm_x6(x.data_ptr(), 64, None, 0, x.data_ptr(), None, x.data_ptr(), 1, 256,
                           x.data_ptr(), 64, x.data_ptr(), 64, 0) != 0
+
+
+# --- token-major mode: nn.Linear on [tokens][features] (sp_linear_x6) ----------------------
+
+LINEAR_CASES = [  # tokens, k, m
+    (512, 320, 320),
+    (256, 768, 320),
+    (1024, 64, 96),
+    (768, 512, 1280),
+]
+
+
+@pytest.mark.parametrize("case", LINEAR_CASES)
+@pytest.mark.parametrize("extras", [False, True])
+def test_linear_x6_matches_fp64(cuda, case, extras):
+    t, k, m = case
+    lib = _hip.load_library()
+    assert lib.sp_linear_x6_supported(t, k, m)
+    g = torch.Generator().manual_seed(t + k + m)
+    x = torch.randn(t, k, generator=g)
+    W = torch.randn(m, k, generator=g) * k ** -0.5
+    bias = torch.randn(m, generator=g) if extras else None
+    res = torch.randn(t, m, generator=g) if extras else None
+    ref = x.double() @ W.double().t()
+    if bias is not None:
+        ref = ref + bias.double()
+    if res is not None:
+        ref = ref + res.double()
+    t32 = torch.nn.functional.linear(x.to(cuda), W.to(cuda), None if bias is None else bias.to(cuda))
+    if res is not None:
+        t32 = t32 + res.to(cuda)
+    st = torch.cuda.current_stream().cuda_stream
+    wg = W.to(cuda)
+    wp = torch.empty(int(lib.sp_gemm_x6_packed_size(m, k)), device=cuda)
+    _hip.check(lib.sp_gemm_x6_pack(wg.data_ptr(), m, k, 0, wp.data_ptr(), st), "pack")
+    xg = x.to(cuda)
+    y = torch.full((t, m), float("nan"), device=cuda)
+    _hip.check(lib.sp_linear_x6(xg.data_ptr(), wp.data_ptr(), None if bias is None else bias.to(cuda).data_ptr(),
+                                None if res is None else res.to(cuda).data_ptr(), t, k, m, y.data_ptr(), st),
+               "sp_linear_x6")
+    torch.cuda.synchronize()
+    assert torch.isfinite(y).all()
+    e6, e32 = _rel(y, ref), _rel(t32, ref)
+    assert e6 <= 1.5 * e32 + 1e-9 and e6 < 1e-6, (e6, e32)
+
+
+def test_linear_x6_input_vjp(cuda):
+    """dx = dy W through a W^T pack (trans = 1): the Linear's input VJP."""
+    lib = _hip.load_library()
+    t, k, m = 512, 320, 640
+    g = torch.Generator().manual_seed(11)
+    W = torch.randn(m, k, generator=g) * 0.05
+    dy = torch.randn(t, m, generator=g)
+    ref = dy.double() @ W.double()
+    st = torch.cuda.current_stream().cuda_stream
+    wg = W.to(cuda)
+    wt = torch.empty(int(lib.sp_gemm_x6_packed_size(k, m)), device=cuda)
+    _hip.check(lib.sp_gemm_x6_pack(wg.data_ptr(), k, m, 1, wt.data_ptr(), st), "pack")
+    dx = torch.empty(t, k, device=cuda)
+    dyg = dy.to(cuda)
+    _hip.check(lib.sp_linear_x6(dyg.data_ptr(), wt.data_ptr(), None, None, t, m, k, dx.data_ptr(), st),
+               "sp_linear_x6")
+    torch.cuda.synchronize()
+    assert _rel(dx, ref) < 1e-6
