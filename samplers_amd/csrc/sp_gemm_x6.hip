@@ -1,6 +1,7 @@
 // 1x1 convolution (per-pixel GEMM) Y[n][co][p] = sum_k W[co][k] X[n][k][p] on bf16 MFMAs over
 // exact three-term bf16 splits of the fp32 operands (the scheme of sp_wino_x6.hip: six partial
-// products, fp32 accumulation; error at or below an fp32 GEMM's, tests/test_gemm_x6_gpu.py).
+// products, fp32 accumulation in two accumulators: the leading product and the small ones;
+// error half of an fp32 GEMM's, tests/test_gemm_x6_gpu.py).
 //
 // The UNet's ResnetBlock conv_shortcut (diffusers ResnetBlock2D) over
 // cat(x1, x2) in the up path: forward W [x1; x2] (+ its bias folded elsewhere), input VJP
