@@ -68,6 +68,9 @@ def all_reduce_sum_(t: Tensor, group=None) -> Tensor:
     return t
 
 
+_ACTIVE_GROUPS: dict = {}  # rank tuple -> process group of the ranks holding observations
+
+
 def _parameters(fn) -> dict:
     try:
         return dict(inspect.signature(fn).parameters)
@@ -111,8 +114,10 @@ def sharded_call(sampler: Callable[..., Tensor], inverse_problem: InverseProblem
             kwargs["group"] = group
             active = [r for r, c in enumerate(counts) if c > 0]
             if len(active) < world:  # only the active ranks create (and use) the subgroup
-                ranks = [r if group is None else dist.get_global_rank(group, r) for r in active]
-                kwargs["group"] = dist.new_group(ranks, use_local_synchronization=True)
+                ranks = tuple(r if group is None else dist.get_global_rank(group, r) for r in active)
+                if ranks not in _ACTIVE_GROUPS:  # one process group per rank set, not per call
+                    _ACTIVE_GROUPS[ranks] = dist.new_group(list(ranks), use_local_synchronization=True)
+                kwargs["group"] = _ACTIVE_GROUPS[ranks]
         if squeezes:
             kwargs["keep_reconstruction_dim"] = True
         out = sampler(local, num_reconstructions=num_reconstructions, seed=seed,
