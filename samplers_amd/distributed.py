@@ -68,7 +68,7 @@ def all_reduce_sum_(t: Tensor, group=None) -> Tensor:
     return t
 
 
-_ACTIVE_GROUPS: dict = {}  # rank tuple -> process group of the ranks holding observations
+_ACTIVE_GROUPS: dict = {}  # (rank tuple, world) -> process group of the ranks holding observations
 
 
 def _parameters(fn) -> dict:
@@ -115,9 +115,12 @@ def sharded_call(sampler: Callable[..., Tensor], inverse_problem: InverseProblem
             active = [r for r, c in enumerate(counts) if c > 0]
             if len(active) < world:  # only the active ranks create (and use) the subgroup
                 ranks = tuple(r if group is None else dist.get_global_rank(group, r) for r in active)
-                if ranks not in _ACTIVE_GROUPS:  # one process group per rank set, not per call
-                    _ACTIVE_GROUPS[ranks] = dist.new_group(list(ranks), use_local_synchronization=True)
-                kwargs["group"] = _ACTIVE_GROUPS[ranks]
+                # one process group per rank set (and default group: a re-initialised world
+                # gets new ones), not one per call
+                key = (ranks, id(dist.group.WORLD))
+                if key not in _ACTIVE_GROUPS:
+                    _ACTIVE_GROUPS[key] = dist.new_group(list(ranks), use_local_synchronization=True)
+                kwargs["group"] = _ACTIVE_GROUPS[key]
         if squeezes:
             kwargs["keep_reconstruction_dim"] = True
         out = sampler(local, num_reconstructions=num_reconstructions, seed=seed,
