@@ -430,6 +430,12 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f32",
+        "arithmetic": {
+            "guidance, GroupNorm, 3x3 convs (Winograd / direct / stride-2), attention": "fp32 (fp32 MFMA, fp32 VALU)",
+            "1x1 shortcuts, attention / transformer linears":
+                "fp32 operands on bf16 MFMAs: exact three-term splits, six partial products, fp32 "
+                "accumulation (relative L2 error 1.1e-7 vs fp64, hipBLASLt fp32 2.0e-7; "
+                "SAMPLERS_AMD_SHORTCUT=torch / SAMPLERS_AMD_LINEAR=torch select hipBLASLt fp32)"},
         "data": "synthetic (seeded U(-1,1) images, sigma=0.05 Gaussian noise; "
                 "random-init ddpm-celebahq-256 UNet architecture)",
         "config": {"workload": f"{CONFIGS[args.config]}, 3x{args.image}x{args.image}, "
