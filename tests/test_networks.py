@@ -3,7 +3,7 @@ fused-norm layer's CPU semantics."""
 
 import torch
 
-from samplers_amd.networks.layers import GroupNormAct
+from samplers_amd.networks.layers import GroupNormAct, Linear, linear
 from samplers_amd.networks.unet2d import CELEBAHQ_256, UNet2DConfig, UNet2DModel, build_unet, count_parameters
 from samplers_amd.networks.vae import SD15_VAE, AutoencoderKL
 
@@ -18,6 +18,25 @@ def test_group_norm_act_cpu_is_torch():
     torch.testing.assert_close(layer(x, cb), torch.nn.functional.silu(ref(x + cb[:, :, None, None])))
     layer.act = False
     torch.testing.assert_close(layer(x), ref(x))
+
+
+def test_linear_cpu_is_nn_linear():
+    """``layers.Linear`` keeps nn.Linear's parameters / state-dict keys and, off the GPU,
+    its exact forward and input gradient; ``linear`` with an explicit 2-D view of a 1x1
+    conv weight (proj_in / proj_out) is F.linear on that view."""
+    torch.manual_seed(0)
+    lin, ref = Linear(12, 7), torch.nn.Linear(12, 7)
+    ref.load_state_dict(lin.state_dict())
+    assert list(lin.state_dict()) == ["weight", "bias"]
+    x = torch.randn(2, 5, 12, requires_grad=True)
+    xr = x.detach().clone().requires_grad_(True)
+    y, yr = lin(x), ref(xr)
+    assert torch.equal(y, yr)
+    y.square().sum().backward(), yr.square().sum().backward()
+    assert torch.equal(x.grad, xr.grad)
+    conv = torch.nn.Conv2d(12, 7, 1)
+    out = linear(x.detach(), conv, conv.weight.view(7, 12), conv.bias)
+    assert torch.equal(out, torch.nn.functional.linear(x.detach(), conv.weight.view(7, 12), conv.bias))
 
 
 def test_unet_size_and_names():
