@@ -408,6 +408,18 @@ int sp_linear_x6_supported(int64_t tokens, int32_t k, int32_t m);
 int sp_linear_x6(const float* x, const float* wp, const float* bias, const float* res, int64_t tokens,
                  int32_t k, int32_t m, float* y, sp_stream_t stream);
 
+/* Direct 3x3 convolution (stride 1, zero padding 1) with the same bf16x6 arithmetic:
+ * y = conv(x, W) (+ bias[cout]) (+ res), x [n][cin][h][w], y / res [n][cout][h][w];
+ * cout % 128, cin % 16, h % 8, w % 32.  W [cout][cin][3][3] packed by sp_conv3x3_x6_pack
+ * (trans = 1: pack the forward's W [cin'][cout'][3][3] transposed and flipped, so that
+ * sp_conv3x3_x6(dy, ..., cin = cout', cout = cin') is the input VJP).  Replaces the priors'
+ * nn.Conv2d(3x3) forward / input VJP (diffusers ResnetBlock2D.conv1/conv2), SURVEY.md §8f f1. */
+int sp_conv3x3_x6_supported(int32_t cout, int32_t cin, int32_t h, int32_t w);
+int64_t sp_conv3x3_x6_packed_size(int32_t cout, int32_t cin);
+int sp_conv3x3_x6_pack(const float* w, int32_t cout, int32_t cin, int32_t trans, float* wp, sp_stream_t stream);
+int sp_conv3x3_x6(const float* x, const float* wp, const float* bias, const float* res, int64_t n,
+                  int32_t cin, int32_t cout, int32_t h, int32_t w, float* y, sp_stream_t stream);
+
 /* Fused self-attention softmax(q k^T * scale) v of the SD 1.5 eps-UNet's transformer blocks
  * (attn1 over the latent tokens; diffusers UNet2DConditionModel, stable_diffusion.py:306-313;
  * replaces the scores / softmax / weighted-sum chain and its autograd VJP) on fp32 MFMA,

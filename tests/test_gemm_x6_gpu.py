@@ -55,11 +55,13 @@ def test_gemm_x6_matches_fp64(cuda, case, extras):
     _hip.check(lib.sp_gemm_x6_pack(wg.data_ptr(), m, k, 0, wp.data_ptr(), st), "pack")
     x1g = x1.to(cuda)
     x2g = None if x2 is None else x2.to(cuda)
+    bg = None if bias is None else bias.to(cuda)  # held by name for the call
+    rg = None if res is None else res.to(cuda)
     y1 = torch.full((n, o1, h, w), float("nan"), device=cuda)
     y2 = torch.full((n, o2, h, w), float("nan"), device=cuda) if o2 else None
     _hip.check(lib.sp_gemm_x6(x1g.data_ptr(), c1, None if x2g is None else x2g.data_ptr(), c2,
-                              wp.data_ptr(), None if bias is None else bias.to(cuda).data_ptr(),
-                              None if res is None else res.to(cuda).data_ptr(), n, hw, y1.data_ptr(),
+                              wp.data_ptr(), None if bg is None else bg.data_ptr(),
+                              None if rg is None else rg.data_ptr(), n, hw, y1.data_ptr(),
                               o1, None if y2 is None else y2.data_ptr(), o2, st), "sp_gemm_x6")
     torch.cuda.synchronize()
     y = y1.reshape(n, o1, hw) if y2 is None else torch.cat([y1, y2], 1).reshape(n, m, hw)
@@ -135,9 +137,11 @@ def test_linear_x6_matches_fp64(cuda, case, extras):
     wp = torch.empty(int(lib.sp_gemm_x6_packed_size(m, k)), device=cuda)
     _hip.check(lib.sp_gemm_x6_pack(wg.data_ptr(), m, k, 0, wp.data_ptr(), st), "pack")
     xg = x.to(cuda)
+    bg = None if bias is None else bias.to(cuda)  # held by name for the call
+    rg = None if res is None else res.to(cuda)
     y = torch.full((t, m), float("nan"), device=cuda)
-    _hip.check(lib.sp_linear_x6(xg.data_ptr(), wp.data_ptr(), None if bias is None else bias.to(cuda).data_ptr(),
-                                None if res is None else res.to(cuda).data_ptr(), t, k, m, y.data_ptr(), st),
+    _hip.check(lib.sp_linear_x6(xg.data_ptr(), wp.data_ptr(), None if bg is None else bg.data_ptr(),
+                                None if rg is None else rg.data_ptr(), t, k, m, y.data_ptr(), st),
                "sp_linear_x6")
     torch.cuda.synchronize()
     assert torch.isfinite(y).all()
