@@ -190,7 +190,8 @@ __device__ __forceinline__ G6Pos g6_pos(const G6Geom& g, int t) {
 
 // epilogue: register q of tile (a, b) = channel 32 sub + (q&3) + 8(q>>2) + 4(lane>>5),
 // pixel pxb[b] + (lane & 31) of image n (pxb[b]: the first of tile b's 32 pixels in the plane);
-// bias and residual added, the 32-channel block to y1 or y2
+// bias and residual added, the 32-channel block to y1 or y2 (TWO = false: acs already added into acc)
+template <bool TWO = true>
 __device__ __forceinline__ void g6_epilogue(const G6Geom& g, int n, int cb, const int (&pxb)[2], int ch, int lane,
                                             const f32x16 (&acc)[2][2], const f32x16 (&acs)[2][2]) {
 #pragma unroll
@@ -226,7 +227,7 @@ __device__ __forceinline__ void g6_epilogue(const G6Geom& g, int n, int cb, cons
                 const float b0 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, bl), c));
                 const float b1 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, bl), c + 4));
                 const int cc = c + 4 * (lane >> 5);
-                const float y = (acc[a][b][q] + acs[a][b][q]) + ((lane >> 5) ? b1 : b0) + rv[q];
+                const float y = (TWO ? acc[a][b][q] + acs[a][b][q] : acc[a][b][q]) + ((lane >> 5) ? b1 : b0) + rv[q];
                 __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(y), ors, vo + cc * g.hw * 4, 0, 0);
             }
             __builtin_amdgcn_sched_barrier(0);
@@ -455,6 +456,9 @@ constexpr int C6_NDMA = C6_RAWB / 1024;              // 25 direct loads per bloc
 constexpr int C6_PPX = C6_PR * C6_PC;                // 340 patch pixels
 constexpr int C6_XB = 3 * C6_PPX * G6_KC * 2;        // 32640 B of split terms per block
 static_assert(C6_RAWB % 1024 == 0 && C6_NDMA <= 32, "patch loads");
+#ifndef C6_PIPE
+#define C6_PIPE 1  // k_conv3x3_x6<true>: fragments of the next sub-step read during this one's products
+#endif
 #ifndef C6_LATE
 #define C6_LATE 0  // > 0: issue the sub-step's loads / split after products 0 .. C6_LATE - 1
 #endif
@@ -488,10 +492,13 @@ __device__ __forceinline__ C6Pos c6_pos(const C6Geom& g, int t) {
     return C6Pos{n, ri * C6_TR, (rem - ri * g.ct) * C6_TC, cb};
 }
 
+// PIPE: the next sub-step's fragments are read during this one's products (below); W ring of 4
+template <bool PIPE>
 __global__ __launch_bounds__(G6_THREADS, 1) void k_conv3x3_x6(C6Geom g) {
+    constexpr int WSLOTS = PIPE ? 4 : 3;
     __shared__ __attribute__((aligned(16))) unsigned char raw[C6_RAWB];
     __shared__ __attribute__((aligned(16))) unsigned char xs[2][C6_XB];
-    __shared__ __attribute__((aligned(16))) unsigned char wl[3][G6_WB];
+    __shared__ __attribute__((aligned(16))) unsigned char wl[WSLOTS][G6_WB];
     const int tid = threadIdx.x, lane = tid & 63;
     const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int ch = wv & 1, pq = wv >> 1;
@@ -527,6 +534,7 @@ __global__ __launch_bounds__(G6_THREADS, 1) void k_conv3x3_x6(C6Geom g) {
     auto split = [&](const C6Pos& p, unsigned char* xb) {
 #pragma unroll
         for (int rep = 0; rep < 2; ++rep) {
+            __builtin_amdgcn_sched_barrier(0);  // one task's registers at a time
             const int task = tid + rep * G6_THREADS;
             if (task < 2 * C6_PPX) {
                 const int grp = task >= C6_PPX ? 1 : 0, px = task - grp * C6_PPX;
@@ -561,7 +569,7 @@ __global__ __launch_bounds__(G6_THREADS, 1) void k_conv3x3_x6(C6Geom g) {
     auto dma_w = [&]() {
         if (cw.j < J) g6_dma_w(wrs, cw.cb * nst + cw.s, wv, lane, wl[cw.slot]);
         ++cw.j;
-        cw.slot = cw.slot == 2 ? 0 : cw.slot + 1;
+        cw.slot = cw.slot == WSLOTS - 1 ? 0 : cw.slot + 1;
         if (++cw.s == nst) {
             cw.s = 0;
             if (++cw.tw < ntile_wg) cw.cb = c6_pos(g, b0 + cw.tw * G).cb;
@@ -578,10 +586,11 @@ __global__ __launch_bounds__(G6_THREADS, 1) void k_conv3x3_x6(C6Geom g) {
         }
     };
 
-    // prologue: W 0, 1 and patch 0 in, patch 0 split
+    // prologue: W 0, 1 (and 2) and patch 0 in, patch 0 split
     dma_w();
     dma_raw(nb.ps, 0);
     dma_w();
+    if constexpr (PIPE) dma_w();
     __builtin_amdgcn_s_waitcnt(g6_vmcnt(0));
     __builtin_amdgcn_s_barrier();
     split(nb.ps, xs[0]);
@@ -591,6 +600,112 @@ __global__ __launch_bounds__(G6_THREADS, 1) void k_conv3x3_x6(C6Geom g) {
 
     // per wave: W loads per sub-step nw = 2 (waves 0-3) or 1, patch loads per block nx = 4 (wave 0) or 3
     static_assert(C6_NDMA == 25, "the wait counts below assume 25 patch loads");
+    if constexpr (PIPE) {
+        // Sub-step j: barrier (W(j + 1) in), loads of W(j + 3) / the next patch / its split, then
+        // the six products over fragments read during sub-step j - 1, each term's registers
+        // refilled with sub-step j + 1's term as soon as its last product has issued.
+        auto rdU = [&](int slot, int e, uvec4 (&t)[2]) {
+            const uvec4* wq = reinterpret_cast<const uvec4*>(wl[slot]) + lane;
+#pragma unroll
+            for (int a = 0; a < 2; ++a) t[a] = wq[((2 * ch + a) * 3 + e) * 64];
+        };
+        auto rdV = [&](const unsigned char* xb, int tap, int e, uvec4 (&t)[2]) {
+            const int ty = tap / 3, tx = tap % 3;
+#pragma unroll
+            for (int b = 0; b < 2; ++b) {
+                const int px = (2 * pq + b + ty) * C6_PC + (lane & 31) + tx;
+                const int off = (px * G6_KC + 8 * ((lane >> 5) ^ ((px >> 3) & 1))) * 2;
+                t[b] = *reinterpret_cast<const uvec4*>(xb + e * C6_PPX * G6_KC * 2 + off);
+            }
+        };
+        f32x16 acc[2][2], acs[2][2];
+        auto prod = [&](const uvec4 (&u)[2], const uvec4 (&v)[2], f32x16 (&c)[2][2]) {
+#pragma unroll
+            for (int b = 0; b < 2; ++b)
+#pragma unroll
+                for (int a = 0; a < 2; ++a) c[a][b] = g6_mfma(u[a], v[b], c[a][b]);
+        };
+        uvec4 uh[2], um[2], ul[2], vh[2], vm[2], vl[2];
+        rdU(0, 0, uh);
+        rdU(0, 1, um);
+        rdU(0, 2, ul);
+        rdV(xs[0], 0, 0, vh);
+        rdV(xs[0], 0, 1, vm);
+        rdV(xs[0], 0, 2, vl);
+        int j = 0, blk = 0, wslot = 0;
+        for (int tw = 0; tw < ntile_wg; ++tw) {
+#pragma unroll
+            for (int a = 0; a < 2; ++a)
+#pragma unroll
+                for (int b = 0; b < 2; ++b) acc[a][b] = f32x16{}, acs[a][b] = f32x16{};
+            for (int kc = 0; kc < g.nkc; ++kc, ++blk) {
+                const unsigned char* xb = xs[blk & 1];
+                const unsigned char* xn = xs[(blk + 1) & 1];
+#pragma unroll
+                for (int tap = 0; tap < 9; ++tap, ++j) {
+                    // W(j + 1) in (older loads retired); at taps 2 - 3 the patch issued at tap 1
+                    // may stay in flight; at tap 5 the split written at tap 4 is visible
+                    if (j > 0) {
+                        if (j + 12 >= J) __builtin_amdgcn_s_waitcnt(0x0070);
+                        else if (tap == 5) {
+                            if (wv < 4) __builtin_amdgcn_s_waitcnt(g6_vmcnt(2) & ~0x0F00);
+                            else __builtin_amdgcn_s_waitcnt(g6_vmcnt(1) & ~0x0F00);
+                        } else if (tap == 2 || tap == 3) {
+                            if (wv == 0) __builtin_amdgcn_s_waitcnt(g6_vmcnt(6));
+                            else if (wv < 4) __builtin_amdgcn_s_waitcnt(g6_vmcnt(5));
+                            else __builtin_amdgcn_s_waitcnt(g6_vmcnt(4));
+                        } else if (wv < 4) __builtin_amdgcn_s_waitcnt(g6_vmcnt(2));
+                        else __builtin_amdgcn_s_waitcnt(g6_vmcnt(1));
+                        __builtin_amdgcn_s_barrier();
+                    }
+                    dma_w();  // W(j + 3)
+                    if (tap == 1 && nb.b < NB) dma_raw(nb.ps, nb.kc);
+                    if (tap == 4) {
+                        if (nb.b < NB) split(nb.ps, xs[(blk + 1) & 1]);
+                        advance_b();
+                    }
+                    const int ns = wslot == WSLOTS - 1 ? 0 : wslot + 1;
+                    const unsigned char* nxb = tap == 8 ? xn : xb;
+                    const int NT = tap == 8 ? 0 : tap + 1;  // constant once unrolled
+                    // products (m,m) (m,h) (h,m) (l,h) (h,l) into acs, (h,h) into acc; each term
+                    // refilled after its last use: um, vm, ul, vl, then uh, vh (needed second and
+                    // third in the next sub-step)
+                    __builtin_amdgcn_sched_barrier(0);
+                    prod(um, vm, acs);
+                    prod(um, vh, acs);
+                    __builtin_amdgcn_sched_barrier(0);
+                    rdU(ns, 1, um);
+                    __builtin_amdgcn_sched_barrier(0);
+                    prod(uh, vm, acs);
+                    __builtin_amdgcn_sched_barrier(0);
+                    rdV(nxb, NT, 1, vm);
+                    __builtin_amdgcn_sched_barrier(0);
+                    prod(ul, vh, acs);
+                    __builtin_amdgcn_sched_barrier(0);
+                    rdU(ns, 2, ul);
+                    __builtin_amdgcn_sched_barrier(0);
+                    prod(uh, vl, acs);
+                    __builtin_amdgcn_sched_barrier(0);
+                    rdV(nxb, NT, 2, vl);
+                    __builtin_amdgcn_sched_barrier(0);
+                    prod(uh, vh, acc);
+                    __builtin_amdgcn_sched_barrier(0);
+                    rdV(nxb, NT, 0, vh);
+                    rdU(ns, 0, uh);
+                    wslot = ns;
+                }
+            }
+            // the next tile's first fragments are live here: fold acs in first (64 registers)
+#pragma unroll
+            for (int a = 0; a < 2; ++a)
+#pragma unroll
+                for (int b = 0; b < 2; ++b) acc[a][b] += acs[a][b];
+            const C6Pos ps = c6_pos(g, b0 + tw * G);
+            const int pxb[2] = {(ps.r0 + 2 * pq) * g.w + ps.c0, (ps.r0 + 2 * pq + 1) * g.w + ps.c0};
+            g6_epilogue<false>(g.out, ps.n, ps.cb, pxb, ch, lane, acc, acc);
+        }
+        return;
+    }
     f32x16 acc[2][2], acs[2][2];
     int j = 0, blk = 0, wslot = 0;
     for (int tw = 0; tw < ntile_wg; ++tw) {
@@ -851,7 +966,7 @@ int sp_conv3x3_x6(const float* x, const float* wp, const float* bias, const floa
     g.ct = w / C6_TC;
     g.nkc = cin / G6_KC;
     const int grid = static_cast<int>(std::min<int64_t>(tiles, g6_cu_count()));
-    launch(0, k_conv3x3_x6, dim3(grid), dim3(G6_THREADS), static_cast<hipStream_t>(stream), g);
+    launch(0, k_conv3x3_x6<C6_PIPE != 0>, dim3(grid), dim3(G6_THREADS), static_cast<hipStream_t>(stream), g);
     return check_launch("sp_conv3x3_x6");
 }
 
