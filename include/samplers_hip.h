@@ -263,10 +263,15 @@ int sp_groupnorm_silu_bwd2(const float* dz, const float* x1, const float* x2, in
 /* Single-pass GroupNorm (default on): a team of workgroups per group keeps the group in
  * registers across its reduction (forward reads x once, backward x and dz once).  enable:
  * 1 on, 0 off (the two-pass kernels), < 0 query; returns the previous setting.  Process-wide;
- * results are bit-identical either way.  team_timeouts: polls that gave up waiting for a
- * team member (0 unless the GPU is shared with a kernel that holds CUs indefinitely). */
+ * results are bit-identical either way.  A team member that has not published its chunk
+ * partials within the poll bound (not resident: another process or stream holds CUs) has
+ * them recomputed by the waiting workgroup from the chunk's inputs, in the member's own
+ * order, so the result stays bit-identical.  team_timeouts: how many chunk partials were
+ * recomputed that way (a cost, not an error).  set_spin_limit: the poll bound (< 0 default;
+ * 0 recomputes every partial not present at the first poll — a test of that path). */
 int sp_groupnorm_single_pass(int32_t enable);
 int64_t sp_groupnorm_team_timeouts(void);
+int sp_groupnorm_set_spin_limit(int32_t spins);
 
 /* ---- device-resident step schedule (hipGraph capture of a step) ----
  * One record per guided step, precomputed on the host in the same fp64->fp32 arithmetic

@@ -179,6 +179,7 @@ SIGNATURES = {
                                               ctypes.c_int32, _P, _P, _P, _P, _P, _P, _P]),
     "sp_groupnorm_single_pass": (ctypes.c_int, [ctypes.c_int32]),
     "sp_groupnorm_team_timeouts": (_I64, []),
+    "sp_groupnorm_set_spin_limit": (ctypes.c_int, [ctypes.c_int32]),
     "sp_wino3x3_fwd_res": (ctypes.c_int, [_P, _P, _P, _P, _I64, ctypes.c_int32, ctypes.c_int32,
                                           ctypes.c_int32, ctypes.c_int32, _P, _P]),
 }
@@ -218,24 +219,21 @@ def check(status: int, what: str) -> None:
 
 
 class solve_guard:
-    """Checks, once per sampler call, that no single-pass GroupNorm team gave up waiting for
-    a member (``sp_groupnorm_team_timeouts``; a give-up leaves that group's statistics
-    built from missing partials).  The counter read waits for the device, so it runs at the
-    end of a solve, never inside the step loop."""
+    """Counts, once per sampler call, the single-pass GroupNorm chunk partials that had to be
+    recomputed because a team member was not resident (``sp_groupnorm_team_timeouts``).  The
+    kernels recompute them exactly, so this is a diagnostic (``self.recomputed``), not an
+    error.  The counter read waits for the device, so it runs at the end of a solve, never
+    inside the step loop."""
 
     def __enter__(self):
         self.lib = load_library()
         self.before = int(self.lib.sp_groupnorm_team_timeouts())
+        self.recomputed = 0
         return self
 
     def __exit__(self, exc_type, exc, tb):
         if exc_type is None:
-            after = int(self.lib.sp_groupnorm_team_timeouts())
-            if after != self.before:
-                raise HipLibraryError(
-                    f"GroupNorm team kernels timed out {after - self.before} time(s) during this "
-                    "solve: the result is invalid (a co-resident kernel held CUs); rerun, or set "
-                    "SAMPLERS_AMD_GN_SINGLE_PASS=0")
+            self.recomputed = int(self.lib.sp_groupnorm_team_timeouts()) - self.before
         return False
 
 

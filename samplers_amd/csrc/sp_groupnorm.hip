@@ -380,9 +380,18 @@ __global__ __launch_bounds__(kBlock) void k_gn_bwd_apply(const float* __restrict
 // the wait for it leaves the prefetch in flight.  Chunking, the per-thread element order and
 // the summation order are those of the two-pass kernels, so the results are bit-identical.
 // HBM traffic: forward 2 passes (was 3), backward 3 + the addends (was 5 + the addends).
-constexpr int GNT_MAX_SPINS = 1 << 22;          // poll bound (~0.3 s): a stuck team exits
+// Poll bound: a member still absent after this many polls (~5-20 ms) is taken to be missing
+// (not resident: another process or stream holds CUs, so the grid's co-residency assumption
+// failed) and the waiting workgroup recomputes that member's chunk partials itself from the
+// chunk's inputs, in the member's own element order and block reduction — bit-identical to
+// what the member publishes.  The result is therefore exact whatever the residency; a missing
+// member costs one extra read of its chunk.  g_gnt_spin_limit overrides the bound
+// (sp_groupnorm_set_spin_limit; 0 = recompute every word not present at the first poll, which
+// tests use to exercise the recompute path).
+constexpr int GNT_MAX_SPINS = 1 << 16;
 
-__device__ unsigned int g_gnt_timeouts;  // polls that hit GNT_MAX_SPINS (sp_groupnorm_team_timeouts)
+__device__ unsigned int g_gnt_timeouts;  // chunk partials recomputed (sp_groupnorm_team_timeouts)
+__device__ int g_gnt_spin_limit = GNT_MAX_SPINS;
 
 __device__ __forceinline__ void gnt_publish(uint64_t* slot, float a, float b) {
     __hip_atomic_store(slot, (uint64_t(1) << 32) | __float_as_uint(a), __ATOMIC_RELAXED,
@@ -482,31 +491,90 @@ __device__ __forceinline__ void gnp_poll_issue(const uint64_t* slots, int chunks
 // Finish the poll (threads t < chunks spin on their words) and form the team's sums as
 // gnt_sums does.  Every thread tests its issued words first, outside any branch and loop: the
 // wait for them then leaves the younger prefetch loads in flight (at a loop header or a join
-// the compiler merges paths and waits for everything).
+// the compiler merges paths and waits for everything).  Words still absent after the poll
+// bound are recomputed by the whole workgroup with `recompute(mm, a, b)` (a block-wide call
+// that leaves chunk mm's two partials in thread 0's a, b).
+template <typename Recompute>
 __device__ __forceinline__ void gnp_poll_finish(const uint64_t* slots, int chunks, uint64_t wa,
-                                                uint64_t wb, float* sv, float& a, float& b) {
+                                                uint64_t wb, float* sv, int* miss, float& a,
+                                                float& b, Recompute recompute) {
     const int t = threadIdx.x;
     bool ready = (wa >> 32) && (wb >> 32);
+    if (t == 0) miss[GNT_MAX_CHUNKS] = 0;
     if ((t < chunks) & !ready) {
+        const int limit = g_gnt_spin_limit;
 #pragma nounroll
-        for (int spins = 0; spins < GNT_MAX_SPINS; ++spins) {
+        for (int spins = 0; spins < limit; ++spins) {
             __builtin_amdgcn_s_sleep(2);
             wa = __hip_atomic_load(slots + 2 * t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             wb = __hip_atomic_load(slots + 2 * t + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             ready = (wa >> 32) && (wb >> 32);
             if (ready) break;
         }
-        if (!ready) atomicAdd(&g_gnt_timeouts, 1u);
     }
+    __syncthreads();  // miss[] count cleared before any thread records a missing word
     if (t < chunks) {
         sv[t] = __uint_as_float(static_cast<uint32_t>(wa));
         sv[GNT_MAX_CHUNKS + t] = __uint_as_float(static_cast<uint32_t>(wb));
+        if (!ready) miss[atomicAdd(&miss[GNT_MAX_CHUNKS], 1)] = t;
     }
     __syncthreads();
+    const int nmiss = miss[GNT_MAX_CHUNKS];
+    if (nmiss) {  // rare (block-uniform): a team member did not publish in time
+        if (t == 0) atomicAdd(&g_gnt_timeouts, static_cast<unsigned>(nmiss));
+        for (int q = 0; q < nmiss; ++q) {
+            const int mm = miss[q];
+            float ra, rb;
+            recompute(mm, ra, rb);
+            if (t == 0) sv[mm] = ra, sv[GNT_MAX_CHUNKS + mm] = rb;
+            __syncthreads();
+        }
+    }
     a = 0.f, b = 0.f;
     for (int i = t & 63; i < chunks; i += 64) a += sv[i], b += sv[GNT_MAX_CHUNKS + i];
     a = wave_sum(a);
     b = wave_sum(b);
+}
+
+// Block-reduce (a, b) exactly as gnt_reduce_publish does; thread 0 gets the chunk's words.
+__device__ __forceinline__ void gnt_reduce_local(float& a, float& b, float* red) {
+    a = wave_sum(a);
+    b = wave_sum(b);
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    __syncthreads();  // red[] may still be read by a previous reduction
+    if (lane == 0) red[wid] = a, red[4 + wid] = b;
+    __syncthreads();
+    a = (red[0] + red[1]) + (red[2] + red[3]);
+    b = (red[4] + red[5]) + (red[6] + red[7]);
+}
+
+// Forward chunk mm's shifted moments, recomputed from x (the terms and order of gnp_fwd_group).
+template <int PER>
+__device__ __forceinline__ void gnp_fwd_recompute(const float* __restrict__ x, const GnGeom& G,
+                                               int64_t gi, uint32_t mm, float K,
+                                               const float (*tab)[GNP_MAX_CG], float* red,
+                                               float& a, float& b) {
+    const int t = threadIdx.x;
+    const GroupCtx c = group_ctx_at<4>(x, G, gi, mm);
+    const auto r = gnt_rsrc(c.x, c.lo, c.hi);
+    const uint32_t vo = (c.lo + t) * 16;
+    float s1 = 0.f, s2 = 0.f;
+#pragma nounroll
+    for (int i = 0; i < PER; ++i) {
+        float v[4];
+        gnt_load(r, vo, i, v);
+        const uint32_t j = c.lo + t + i * kBlock;
+        const bool in = j < c.hi;
+        const float bb = G.bias ? tab[2][fdiv(in ? j : c.lo, G.hw_div)] : 0.f;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const float d = in ? v[e] + bb - K : 0.f;
+            s1 += d;
+            s2 = fmaf(d, d, s2);
+        }
+    }
+    gnt_reduce_local(s1, s2, red);
+    a = s1, b = s2;
 }
 
 // One forward group: chunk v (loaded), state bf; prefetches group gn (< 0: none) into vn / bn.
@@ -515,7 +583,7 @@ __device__ __forceinline__ void gnp_fwd_group(const float* __restrict__ x, const
                                               uint64_t* __restrict__ slots, int64_t gi, int64_t gn,
                                               uint32_t m, float (&v)[PER][4], const GnpBuf& bf,
                                               float (&vn)[PER][4], GnpBuf& bn, float (*tab)[GNP_MAX_CG],
-                                              float* red, float* sv, float* __restrict__ z,
+                                              float* red, float* sv, int* miss, float* __restrict__ z,
                                               float* __restrict__ mean_out,
                                               float* __restrict__ rstd_out) {
     const int t = threadIdx.x;
@@ -542,7 +610,9 @@ __device__ __forceinline__ void gnp_fwd_group(const float* __restrict__ x, const
     gnp_poll_issue(gslots, G.chunks, wa, wb);
     gnp_issue<PER>(x, G, gn >= 0 ? gn : gi, m, vn, bn, gn >= 0);
     float S1, S2;
-    gnp_poll_finish(gslots, G.chunks, wa, wb, sv, S1, S2);
+    gnp_poll_finish(gslots, G.chunks, wa, wb, sv, miss, S1, S2, [&](int mm, float& ra, float& rb) {
+        gnp_fwd_recompute<PER>(x, G, gi, static_cast<uint32_t>(mm), K, tab, red, ra, rb);
+    });
     const float inv_n = 1.f / static_cast<float>(G.gs);
     const float m1 = S1 * inv_n;
     const float mean = K + m1;
@@ -577,6 +647,7 @@ __global__ __launch_bounds__(kBlock, 2) void k_gn_fwd_pipe(const float* __restri
                                                            float* __restrict__ rstd_out) {
     __shared__ float red[8];
     __shared__ float sv[2 * GNT_MAX_CHUNKS];
+    __shared__ int miss[GNT_MAX_CHUNKS + 1];
     __shared__ float tab[2][3][GNP_MAX_CG];
     const uint32_t m = blockIdx.x % G.chunks;
     int64_t gi = blockIdx.x / G.chunks;
@@ -586,16 +657,51 @@ __global__ __launch_bounds__(kBlock, 2) void k_gn_fwd_pipe(const float* __restri
     gnp_issue<PER>(x, G, gi, m, va, ba);
     for (;;) {  // two groups per trip: the register buffers are named, not indexed
         int64_t gn = gi + nteams < ngroups ? gi + nteams : -1;
-        gnp_fwd_group<ACT, PER>(x, G, slots, gi, gn, m, va, ba, vb, bb, tab[0], red, sv, z,
+        gnp_fwd_group<ACT, PER>(x, G, slots, gi, gn, m, va, ba, vb, bb, tab[0], red, sv, miss, z,
                                 mean_out, rstd_out);
         if (gn < 0) break;
         gi = gn;
         gn = gi + nteams < ngroups ? gi + nteams : -1;
-        gnp_fwd_group<ACT, PER>(x, G, slots, gi, gn, m, vb, bb, va, ba, tab[1], red, sv, z,
+        gnp_fwd_group<ACT, PER>(x, G, slots, gi, gn, m, vb, bb, va, ba, tab[1], red, sv, miss, z,
                                 mean_out, rstd_out);
         if (gn < 0) break;
         gi = gn;
     }
+}
+
+// Backward chunk mm's sums of dy*gamma and dy*gamma*xhat, recomputed from x and dz (the terms
+// and order of gnp_bwd_group).
+template <bool ACT, int PER>
+__device__ __forceinline__ void gnp_bwd_recompute(const float* __restrict__ dz,
+                                               const float* __restrict__ x, const GnGeom& G,
+                                               int64_t gi, uint32_t mm, float mean, float rstd,
+                                               const float (*tab)[GNP_MAX_CG], float* red,
+                                               float& a, float& b) {
+    const int t = threadIdx.x;
+    const GroupCtx c = group_ctx_at<4>(x, G, gi, mm);
+    const auto r = gnt_rsrc(c.x, c.lo, c.hi);
+    const auto rg = gnt_rsrc(Parts<const float>{dz + c.zoff, dz + c.zoff, G.gs}, c.lo, c.hi);
+    const uint32_t vo = (c.lo + t) * 16;
+    float sa = 0.f, sb = 0.f;
+#pragma nounroll
+    for (int i = 0; i < PER; ++i) {
+        float v[4], g[4];
+        gnt_load(r, vo, i, v);
+        gnt_load(rg, vo, i, g);
+        const uint32_t j = c.lo + t + i * kBlock;
+        const bool in = j < c.hi;
+        const uint32_t cl = fdiv(in ? j : c.lo, G.hw_div);
+        float gdy[4], xh[4];
+        gn_grad_terms<4, ACT>(v, g, G.bias ? tab[2][cl] : 0.f, mean, rstd, tab[0][cl], tab[1][cl],
+                              gdy, xh);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            sa += in ? gdy[e] : 0.f;
+            sb = fmaf(in ? gdy[e] : 0.f, xh[e], sb);
+        }
+    }
+    gnt_reduce_local(sa, sb, red);
+    a = sa, b = sb;
 }
 
 // One backward group: x chunk v and dz chunk g (loaded); prefetches group gn into vn / gq.
@@ -605,7 +711,7 @@ __device__ __forceinline__ void gnp_bwd_group(
     const float* __restrict__ mean_in, const float* __restrict__ rstd_in,
     uint64_t* __restrict__ slots, int64_t gi, int64_t gn, uint32_t m, float (&v)[PER][4],
     float (&g)[PER][4], const GnpBuf& bf, float (&vn)[PER][4], float (&gq)[PER][4], GnpBuf& bn,
-    float (*tab)[GNP_MAX_CG], float* red, float* sv, float* __restrict__ dx,
+    float (*tab)[GNP_MAX_CG], float* red, float* sv, int* miss, float* __restrict__ dx,
     float* __restrict__ dx2, const float* __restrict__ add1, const float* __restrict__ add2) {
     const int t = threadIdx.x;
     const GroupCtx c = group_ctx_at<4>(x, G, gi, m);
@@ -660,7 +766,10 @@ __device__ __forceinline__ void gnp_bwd_group(
         for (int i = 0; i < PER; ++i) gnt_load(rg, vo, i, gq[i]);
     }
     float A, B;
-    gnp_poll_finish(gslots, G.chunks, wa, wb, sv, A, B);
+    gnp_poll_finish(gslots, G.chunks, wa, wb, sv, miss, A, B, [&](int mm, float& ra, float& rb) {
+        gnp_bwd_recompute<ACT, PER>(dz, x, G, gi, static_cast<uint32_t>(mm), mean, rstd, tab, red,
+                                    ra, rb);
+    });
     const float inv_n = 1.f / static_cast<float>(G.gs);
     const float mA = A * inv_n, mB = B * inv_n;
     const auto rd = gnt_rsrc(parts_at<float>(dx, G.x2 ? dx2 : nullptr, G, gi), c.lo, c.hi);
@@ -689,6 +798,7 @@ __global__ __launch_bounds__(kBlock, 2) void k_gn_bwd_pipe(
     float* __restrict__ dx2, const float* __restrict__ add1, const float* __restrict__ add2) {
     __shared__ float red[8];
     __shared__ float sv[2 * GNT_MAX_CHUNKS];
+    __shared__ int miss[GNT_MAX_CHUNKS + 1];
     __shared__ float tab[2][3][GNP_MAX_CG];
     const uint32_t m = blockIdx.x % G.chunks;
     int64_t gi = blockIdx.x / G.chunks;
@@ -706,12 +816,12 @@ __global__ __launch_bounds__(kBlock, 2) void k_gn_bwd_pipe(
     for (;;) {
         int64_t gn = gi + nteams < ngroups ? gi + nteams : -1;
         gnp_bwd_group<ACT, PER>(dz, x, G, mean_in, rstd_in, slots, gi, gn, m, va, ga, ba, vb, gb,
-                                bb, tab[0], red, sv, dx, dx2, add1, add2);
+                                bb, tab[0], red, sv, miss, dx, dx2, add1, add2);
         if (gn < 0) break;
         gi = gn;
         gn = gi + nteams < ngroups ? gi + nteams : -1;
         gnp_bwd_group<ACT, PER>(dz, x, G, mean_in, rstd_in, slots, gi, gn, m, vb, gb, bb, va, ga,
-                                ba, tab[1], red, sv, dx, dx2, add1, add2);
+                                ba, tab[1], red, sv, miss, dx, dx2, add1, add2);
         if (gn < 0) break;
         gi = gn;
     }
@@ -770,6 +880,13 @@ int sp_groupnorm_single_pass(int32_t enable) {
     const int prev = g_single_pass;
     if (enable >= 0) g_single_pass = enable ? 1 : 0;
     return prev;
+}
+
+int sp_groupnorm_set_spin_limit(int32_t spins) {
+    const int32_t v = spins < 0 ? GNT_MAX_SPINS : spins;
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_gnt_spin_limit), &v, sizeof(v)) != hipSuccess)
+        return check_launch("sp_groupnorm_set_spin_limit");
+    return SP_OK;
 }
 
 int64_t sp_groupnorm_team_timeouts(void) {

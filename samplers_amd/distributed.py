@@ -46,11 +46,45 @@ def broadcast_seed(seed: int | None, device: torch.device, group=None) -> int:
     return seed
 
 
-def gather_shards(local: Tensor, counts: list[int], group=None) -> Tensor:
-    """All-gather variable-size leading-axis shards into the full tensor on every rank."""
+_MAX_RANK = 8  # trailing dims a gathered shard may have (shape exchange buffer)
+
+
+def _trailing_shape(local: Tensor | None, counts: list[int], rank: int, group=None,
+                    device: torch.device | None = None) -> tuple[int, ...]:
+    """The per-item shape of the gathered tensor, taken from the first rank that holds items.
+    An idle rank (count 0) cannot know it: what a sampler returns depends on its options
+    (PSLD / ReSample with ``decode_output=False`` return latents, not ``x_shape``), so the
+    active ranks' shape is exchanged first (a 72-byte all-gather)."""
+    buf = torch.full((_MAX_RANK + 1,), -1, dtype=torch.int64, device=device)
+    if local is not None and counts[rank] > 0:
+        tail = tuple(local.shape[1:])
+        if len(tail) > _MAX_RANK:
+            raise ValueError(f"shards with more than {_MAX_RANK} trailing dims")
+        buf[0] = len(tail)
+        if tail:
+            buf[1:1 + len(tail)] = torch.tensor(tail, dtype=torch.int64)
+    out = torch.empty((len(counts), _MAX_RANK + 1), dtype=torch.int64, device=device)
+    dist.all_gather_into_tensor(out.view(-1), buf, group=group)
+    first = next(r for r, c in enumerate(counts) if c > 0)
+    nd = int(out[first, 0])
+    return tuple(int(v) for v in out[first, 1:1 + nd].tolist())
+
+
+def gather_shards(local: Tensor | None, counts: list[int], group=None, *,
+                  device: torch.device | None = None, dtype: torch.dtype = torch.float32) -> Tensor:
+    """All-gather variable-size leading-axis shards into the full tensor on every rank.
+    ``local`` may be None on a rank that holds no items (its placeholder takes the trailing
+    shape the active ranks report)."""
     world = len(counts)
     if world == 1:
         return local
+    rank = dist.get_rank(group)
+    device = local.device if local is not None else device
+    if any(c == 0 for c in counts):
+        tail = _trailing_shape(local, counts, rank, group, device)
+        if local is None or counts[rank] == 0:
+            local = torch.empty((0, *tail), device=device, dtype=local.dtype if local is not None
+                                else dtype)
     width = max(counts)
     pad = torch.zeros((width, *local.shape[1:]), device=local.device, dtype=local.dtype)
     pad[: local.shape[0]] = local
@@ -68,7 +102,21 @@ def all_reduce_sum_(t: Tensor, group=None) -> Tensor:
     return t
 
 
-_ACTIVE_GROUPS: dict = {}  # (rank tuple, world) -> process group of the ranks holding observations
+_ACTIVE_GROUPS: dict = {}  # rank tuple -> process group of the ranks holding observations
+_ACTIVE_WORLD: list = [None]  # the default group _ACTIVE_GROUPS was built under
+
+
+def _active_group(ranks: tuple[int, ...]):
+    """One process group per rank set, not one per call.  The cache belongs to the default
+    group it was built under: a destroyed and re-initialised world (a new WORLD object, whose
+    id() CPython may reuse) starts a fresh cache instead of returning dead subgroups."""
+    world = dist.group.WORLD
+    if _ACTIVE_WORLD[0] is not world:
+        _ACTIVE_GROUPS.clear()
+        _ACTIVE_WORLD[0] = world
+    if ranks not in _ACTIVE_GROUPS:
+        _ACTIVE_GROUPS[ranks] = dist.new_group(list(ranks), use_local_synchronization=True)
+    return _ACTIVE_GROUPS[ranks]
 
 
 def _parameters(fn) -> dict:
@@ -115,20 +163,15 @@ def sharded_call(sampler: Callable[..., Tensor], inverse_problem: InverseProblem
             active = [r for r, c in enumerate(counts) if c > 0]
             if len(active) < world:  # only the active ranks create (and use) the subgroup
                 ranks = tuple(r if group is None else dist.get_global_rank(group, r) for r in active)
-                # one process group per rank set (and default group: a re-initialised world
-                # gets new ones), not one per call
-                key = (ranks, id(dist.group.WORLD))
-                if key not in _ACTIVE_GROUPS:
-                    _ACTIVE_GROUPS[key] = dist.new_group(list(ranks), use_local_synchronization=True)
-                kwargs["group"] = _ACTIVE_GROUPS[key]
+                kwargs["group"] = _active_group(ranks)
         if squeezes:
             kwargs["keep_reconstruction_dim"] = True
         out = sampler(local, num_reconstructions=num_reconstructions, seed=seed,
                       sample_offset=start * num_reconstructions, **kwargs)
-    else:  # more ranks than observations: this rank only joins the gather
-        out = torch.empty((0, num_reconstructions, *inverse_problem.operator.x_shape),
-                          device=obs.device, dtype=torch.float32)
-    full = gather_shards(out.contiguous(), counts, group)
+    else:  # more ranks than observations: this rank only joins the gather (the shard shape
+        out = None  # comes from the active ranks: latents when a sampler skips the decode)
+    full = gather_shards(None if out is None else out.contiguous(), counts, group,
+                         device=obs.device)
     if not batch_shape:
         full = full.squeeze(0)
     if squeezes and num_reconstructions == 1 and not keep:

@@ -69,29 +69,44 @@ def _draw_device(device, generator):
     return generator.device
 
 
+PROBE_SCALES = (1.0, 1e2, 1e-3)  # residual magnitudes the probe checks the score at
+
+
 def probe_grad_scale(noise) -> float | None:
-    """``c`` with ``score(r) == −c·r`` on a probe residual, or ``None`` (see
+    """``c`` with ``score(r) == −c·r`` on probe residuals, or ``None`` (see
     ``NoiseModel.grad_scale``).  Works on any object with the reference's
-    ``score`` / ``log_prob`` methods (duck-typed third-party models)."""
+    ``score`` / ``log_prob`` methods (duck-typed third-party models).
+
+    The residuals are standard normals scaled by each of ``PROBE_SCALES`` (|r| from ~1e-3
+    to a few hundred): a density that is quadratic only near zero (Huber, a clipped or
+    tempered Gaussian) gives a different ``c`` at some scale and takes the generic autograd
+    path, as does anything whose score is not exactly proportional to the residual."""
     gen = torch.Generator().manual_seed(0)
-    r = torch.randn(2, 64, generator=gen, dtype=torch.float32)
-    r[:, 0] = 1.0
-    try:
-        buffers = list(noise.buffers()) if isinstance(noise, nn.Module) else []
-        dev = buffers[0].device if buffers else torch.device("cpu")
-        score = getattr(noise, "score", None)
-        if score is None:
+    base = torch.randn(2, 64, generator=gen, dtype=torch.float32)
+    base[:, 0] = 1.0
+    c = None
+    for scale in PROBE_SCALES:
+        r = base * scale
+        try:
+            buffers = list(noise.buffers()) if isinstance(noise, nn.Module) else []
+            dev = buffers[0].device if buffers else torch.device("cpu")
+            score = getattr(noise, "score", None)
+            if score is None:
+                return None
+            g = score(r.to(dev)).detach().float().cpu()
+        except Exception:  # noqa: BLE001 - a model that cannot be probed takes the generic path
             return None
-        g = score(r.to(dev)).detach().float().cpu()
-    except Exception:  # noqa: BLE001 - a model that cannot be probed takes the generic path
-        return None
-    if g.shape != r.shape or not torch.isfinite(g).all():
-        return None
-    c = -float(g[0, 0])
-    if not np.isfinite(c) or c == 0.0:
-        return None
-    if not torch.allclose(g, -c * r, rtol=1e-5, atol=1e-6 * abs(c)):
-        return None
+        if g.shape != r.shape or not torch.isfinite(g).all():
+            return None
+        cs = -float(g[0, 0]) / scale
+        if not np.isfinite(cs) or cs == 0.0:
+            return None
+        if not torch.allclose(g, -cs * r, rtol=1e-5, atol=1e-6 * abs(cs) * scale):
+            return None
+        if c is None:
+            c = cs
+        elif abs(cs - c) > 1e-5 * abs(c):
+            return None
     return float(np.float32(c))
 
 

@@ -13,15 +13,18 @@ from samplers_amd.networks.base import EpsilonNetwork
 def _guarded(call):
     @functools.wraps(call)
     def run(self, *args, **kwargs):
-        with _hip.solve_guard():
-            return call(self, *args, **kwargs)
+        with _hip.solve_guard() as guard:
+            out = call(self, *args, **kwargs)
+        self.last_groupnorm_recomputed = guard.recomputed
+        return out
 
     return run
 
 
 class PosteriorSampler(ABC):
-    """Every subclass's ``__call__`` runs under ``_hip.solve_guard`` (one check per solve
-    that the single-pass GroupNorm kernels completed every team)."""
+    """Every subclass's ``__call__`` runs under ``_hip.solve_guard``: after a solve,
+    ``last_groupnorm_recomputed`` holds how many single-pass GroupNorm chunk partials were
+    recomputed because a team member was not resident (exact either way; a diagnostic)."""
 
     def __init__(self, network: EpsilonNetwork):
         self._epsilon_network = network

@@ -224,6 +224,32 @@ def test_grad_scale_probe_for_reference_style_noise():
     assert si.laplace_noise(0.1).grad_scale() is None  # not c * r: generic path
 
 
+@pytest.mark.parametrize("kind", ["huber", "clipped"])
+def test_grad_scale_probe_rejects_densities_quadratic_only_near_zero(kind):
+    """A Huber loss with delta = 10 or a Gaussian whose residual is clipped at 50 has score
+    -c r for |r| up to ~10 (the old single-scale probe accepted them); the multi-scale
+    probe sees the residuals at 1e2 x and sends them to the generic autograd path."""
+    from samplers_amd.noise import NoiseModel, probe_grad_scale
+
+    class Odd(NoiseModel):
+        def __init__(self):
+            super().__init__()
+            self.register_buffer("sigma", torch.tensor(0.5))
+
+        def log_prob(self, r):
+            if kind == "huber":
+                a = r.abs()
+                v = torch.where(a < 10.0, 0.5 * r.square(), 10.0 * (a - 5.0))
+            else:
+                v = 0.5 * r.clamp(-50.0, 50.0).square()
+            return -(v / self.sigma ** 2).sum(dim=tuple(range(1, r.ndim)))
+
+        def sample(self, shape, **kw):
+            return torch.zeros(shape)
+
+    assert probe_grad_scale(Odd()) is None
+
+
 def test_reference_style_noise_is_instantiable():
     """grad_scale is not abstract: a subclass of the reference ABC's shape instantiates."""
     import stand_ins as si

@@ -151,9 +151,14 @@ def test_batch_global_norms_match_single_process(tmp_path):
 
 # --- sharded_call with a batch-coupled sampler (group-taking, never squeezes R) -----------
 
-def coupled_sampler(problem, *, num_reconstructions, seed, sample_offset, group=None):
+LATENT = (2, 2, 3)  # a latent shape unlike SHAPE (PSLD / ReSample with decode_output=False)
+
+
+def coupled_sampler(problem, *, num_reconstructions, seed, sample_offset, group=None,
+                    decode_output=True):
     """A PSLD-like sampler: every sample is scaled by a batch-global sum of squares,
-    reduced over ``group`` three times (one per 'step'); the R axis is always kept."""
+    reduced over ``group`` three times (one per 'step'); the R axis is always kept.
+    ``decode_output=False`` returns a latent-shaped slice, as PSLD / ReSample do."""
     from samplers_amd.distributed import all_reduce_sum_
 
     obs = problem.observation
@@ -161,33 +166,46 @@ def coupled_sampler(problem, *, num_reconstructions, seed, sample_offset, group=
     for _ in range(3):
         ss = all_reduce_sum_(x.square().sum().reshape(1), group)
         x = x / ss.sqrt()
-    return x.reshape(obs.shape[0], num_reconstructions, *SHAPE)
+    out = x.reshape(obs.shape[0], num_reconstructions, *SHAPE)
+    if not decode_output:
+        out = out.reshape(obs.shape[0], num_reconstructions, -1)[..., :12].reshape(
+            obs.shape[0], num_reconstructions, *LATENT)
+    return out
 
 
-def _coupled_worker(rank, world, port, batch, R, result_path):
+def _coupled_worker(rank, world, port, batch, R, decode, result_path):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         obs = torch.arange(1, batch * N + 1, dtype=torch.float32).reshape(batch, *SHAPE)
         prob = InverseProblem(IdentityOperator(SHAPE), obs, GaussianNoise(0.1))
-        out = sharded_call(coupled_sampler, prob, num_reconstructions=R, seed=3)
+        out = sharded_call(coupled_sampler, prob, num_reconstructions=R, seed=3,
+                           decode_output=decode)
         if rank == 0:
             torch.save(out, result_path)
+        # a second call on the same world reuses the cached subgroup of active ranks
+        again = sharded_call(coupled_sampler, prob, num_reconstructions=R, seed=3,
+                             decode_output=decode)
+        assert torch.equal(again, out)
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,batch,R", [(2, 5, 1), (3, 2, 2)])
-def test_sharded_coupled_sampler_equals_single_process(tmp_path, world, batch, R):
+@pytest.mark.parametrize("world,batch,R,decode", [(2, 5, 1, True), (3, 2, 2, True),
+                                                  (4, 3, 1, False)])
+def test_sharded_coupled_sampler_equals_single_process(tmp_path, world, batch, R, decode):
     """(3, 2, 2): one rank holds no observation and must not be waited for by the others'
-    per-step reductions (they reduce over the subgroup of active ranks)."""
+    per-step reductions (they reduce over the subgroup of active ranks).  (4, 3, 1, False):
+    an idle rank while the sampler returns latents — its placeholder shard takes the shape
+    the active ranks report, not x_shape."""
     path = tmp_path / "out.pt"
-    mp.spawn(_coupled_worker, args=(world, _free_port(), batch, R, str(path)), nprocs=world,
-             join=True)
+    mp.spawn(_coupled_worker, args=(world, _free_port(), batch, R, decode, str(path)),
+             nprocs=world, join=True)
     sharded = torch.load(path, weights_only=True)
     obs = torch.arange(1, batch * N + 1, dtype=torch.float32).reshape(batch, *SHAPE)
     prob = InverseProblem(IdentityOperator(SHAPE), obs, GaussianNoise(0.1))
-    single = sharded_call(coupled_sampler, prob, num_reconstructions=R, seed=3)
-    assert single.shape == (batch, R, *SHAPE)  # R kept, as the coupled samplers do
+    single = sharded_call(coupled_sampler, prob, num_reconstructions=R, seed=3,
+                          decode_output=decode)
+    assert single.shape == (batch, R, *(SHAPE if decode else LATENT))  # R kept
     assert sharded.shape == single.shape
     assert torch.allclose(sharded, single, rtol=1e-6, atol=0)

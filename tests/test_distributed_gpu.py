@@ -30,6 +30,7 @@ def _free_port():
 
 
 def _run(kind: str, device):
+    """kind: psld | resample | resample_latent (decode_output=False: latent shards)."""
     from samplers_amd.distributed import sharded_call
     from samplers_amd.inverse_problem import InverseProblem
     from samplers_amd.noise import GaussianNoise, PoissonNoise
@@ -55,7 +56,8 @@ def _run(kind: str, device):
     # 12 steps, split 3 ways: time travel at 10 (pixel-space solve) and the final latent solve
     return sharded_call(ReSampleSampler(net), prob, num_reconstructions=R, seed=13,
                         num_sampling_steps=12, max_optimization_iters=24, inter_timesteps=3,
-                        time_travel_interval=5, stage_splits=3)
+                        time_travel_interval=5, stage_splits=3,
+                        decode_output=kind != "resample_latent")
 
 
 def _worker(rank, world, port, kind, path):
@@ -71,7 +73,8 @@ def _worker(rank, world, port, kind, path):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("kind,world", [("psld", 2), ("resample", 2), ("resample", 4)])
+@pytest.mark.parametrize("kind,world", [("psld", 2), ("resample", 2), ("resample", 4),
+                                        ("resample_latent", 4)])
 def test_batch_coupled_sampler_sharded_equals_single(cuda, tmp_path, kind, world):
     path = tmp_path / "out.pt"
     mp.spawn(_worker, args=(world, _free_port(), kind, str(path)), nprocs=world, join=True)
