@@ -170,6 +170,69 @@ def host_alphas_cumprod(net) -> np.ndarray:
     return acp
 
 
+class Fp32Boundary:
+    """A reduced-precision ε-network (bf16 / fp16) seen by the fp32 samplers.
+
+    The reference allocates its samples in ``epsilon_net.dtype`` and runs the whole loop in
+    it (``dps.py:83-87``, ``psld.py:102-106``; its scripts drive bf16 / fp16 priors,
+    ``scripts/run_psld.py:14``, ``scripts/sd15.py:10``).  Here the guidance passes, the bridge
+    update and the sample itself stay fp32: only the network's own calls run in its dtype —
+    inputs are cast to it on the way in and outputs back to fp32 on the way out, both inside
+    the autograd graph, so the input-VJP ``J^T v`` also flows through the network in its
+    dtype.  Every other attribute is the wrapped network's; the samplers return their result
+    in the network's dtype, as the reference's do.
+    """
+
+    def __init__(self, network) -> None:
+        object.__setattr__(self, "_net", network)
+        object.__setattr__(self, "_dt", network.dtype)
+
+    def __getattr__(self, name):
+        return getattr(self._net, name)
+
+    def __setattr__(self, name, value):
+        setattr(self._net, name, value)
+
+    @property
+    def dtype(self) -> torch.dtype:
+        return torch.float32
+
+    @property
+    def wrapped(self):
+        return self._net
+
+    def forward(self, x: Tensor, t) -> Tensor:
+        return self._net.forward(x.to(self._dt), t).to(torch.float32)
+
+    __call__ = forward
+
+    def predict_noise(self, x: Tensor, t) -> Tensor:
+        return self.forward(x, t)
+
+    def decode(self, z: Tensor, differentiable: bool = False) -> Tensor:
+        return self._net.decode(z.to(self._dt), differentiable=differentiable).to(torch.float32)
+
+    def encode(self, x: Tensor, differentiable: bool = False) -> Tensor:
+        return self._net.encode(x.to(self._dt), differentiable=differentiable).to(torch.float32)
+
+
+def fp32_view(network):
+    """``network`` itself when it computes in fp32, else an ``Fp32Boundary`` around it.  A
+    network in any other non-float dtype is refused at sampler entry (``TypeError``)."""
+    dt = getattr(network, "dtype", torch.float32)
+    if dt == torch.float32:
+        return network
+    if dt not in (torch.bfloat16, torch.float16, torch.float64):
+        raise TypeError(f"ε-network dtype {dt} is not a floating-point type the samplers accept "
+                        "(float32, bfloat16, float16, float64)")
+    return Fp32Boundary(network)
+
+
+def output_dtype(network) -> torch.dtype:
+    """The dtype the samplers return in: the network's (``dps.py:83-87``)."""
+    return getattr(network, "dtype", torch.float32)
+
+
 @dataclasses.dataclass(slots=True)
 class NoCondition:
     """Placeholder type meaning "this diffusion model does NOT use any conditioning"."""

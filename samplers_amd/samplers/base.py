@@ -7,7 +7,7 @@ from abc import ABC
 
 from samplers_amd import _hip
 from samplers_amd.dtypes import Shape, Tensor
-from samplers_amd.networks.base import EpsilonNetwork
+from samplers_amd.networks.base import EpsilonNetwork, fp32_view, output_dtype
 
 
 def _guarded(call):
@@ -28,6 +28,17 @@ class PosteriorSampler(ABC):
 
     def __init__(self, network: EpsilonNetwork):
         self._epsilon_network = network
+
+    @property
+    def _network(self):
+        """The ε-network as the fp32 hot path calls it (``networks.base.fp32_view``: a bf16 /
+        fp16 network runs in its dtype behind an fp32 boundary)."""
+        return fp32_view(self._epsilon_network)
+
+    def _as_output(self, x: Tensor) -> Tensor:
+        """Results are returned in the network's dtype, as the reference's are (its samples
+        live in ``epsilon_net.dtype``, ``dps.py:83-87``)."""
+        return x.to(output_dtype(self._epsilon_network))
 
     def __init_subclass__(cls, **kwargs):
         super().__init_subclass__(**kwargs)

@@ -63,7 +63,7 @@ class PGDMSampler(PosteriorSampler, Generic[Condition_co]):
         x_shape: Shape = operator.x_shape
         batch_shape: Shape = inverse_problem.batch_shape
         view = BatchView(batch_shape=batch_shape, num_samples=num_reconstructions, data_shape=x_shape)
-        net = self._epsilon_network
+        net = self._network
         net.set_sampling_parameters(num_sampling_steps=num_sampling_steps,
                                     num_reconstructions=num_reconstructions,
                                     batch_size=view.batch_size)
@@ -91,7 +91,7 @@ class PGDMSampler(PosteriorSampler, Generic[Condition_co]):
             x0_final = view.unflatten(step.predict_x0(x, ts[1]))
             if num_reconstructions == 1 and not keep_reconstruction_dim:
                 x0_final = x0_final.squeeze(len(batch_shape))
-            return x0_final
+            return self._as_output(x0_final)
         finally:
             net.clear_condition()
             net.clear_sampling_parameters()

@@ -250,7 +250,7 @@ class PSLDSampler(PosteriorSampler, Generic[Condition_co]):
         x_shape: Shape = inverse_problem.operator.x_shape
         batch_shape: Shape = inverse_problem.batch_shape
         x_view = BatchView(batch_shape, num_reconstructions, x_shape)
-        net: LatentEpsilonNetwork = self._epsilon_network
+        net: LatentEpsilonNetwork = self._network
         latent_shape: Shape = tuple(net.get_latent_shape(x_shape))
         z_view = BatchView(batch_shape, num_reconstructions, latent_shape)
 
@@ -261,7 +261,7 @@ class PSLDSampler(PosteriorSampler, Generic[Condition_co]):
         try:
             obs = inverse_problem.observation
             _hip.require_cuda(obs, "PSLDSampler")
-            y_rows = obs.reshape(max(x_view.batch_size, 1), -1)
+            y_rows = obs.reshape(max(x_view.batch_size, 1), -1).to(torch.float32)
             step = FusedPSLDStep(net, inverse_problem, y_rows, num_reconstructions, latent_shape,
                                  gamma=gamma, omega=omega, eta=eta, group=group)
             if seed is None and noise_fn is None and rng == "philox":
@@ -279,8 +279,8 @@ class PSLDSampler(PosteriorSampler, Generic[Condition_co]):
                 step(z, i, ts[i], ts[i - 1], ts[0], xi=xi, seed=seed, sample_offset=sample_offset)
             final_z0 = step.predict_x0(z, ts[1])
             if decode_output:
-                return x_view.unflatten(net.decode(final_z0, differentiable=False))
-            return z_view.unflatten(final_z0)
+                return self._as_output(x_view.unflatten(net.decode(final_z0, differentiable=False)))
+            return self._as_output(z_view.unflatten(final_z0))
         finally:
             net.clear_condition()
             net.clear_sampling_parameters()

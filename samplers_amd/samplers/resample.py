@@ -191,7 +191,7 @@ class ReSampleSampler(PosteriorSampler, Generic[Condition_co]):
     def _ddim_eps(self, z: Tensor, t: int, t_prev: int, eta: float, noise: Tensor | None,
                   seed: int, key: int, offset: int, *, want_x0: bool = False):
         """ε-form DDIM step (``bridge_kernels.py:82-115``) -> (z_prev, pseudo_x0[, x0])."""
-        net, lib = self._epsilon_network, _hip.load_library()
+        net, lib = self._network, _hip.load_library()
         c = eps_step_coefficients(host_alphas_cumprod(net), t, t_prev, eta)
         with torch.no_grad():
             e = net.predict_noise(z, t).contiguous()
@@ -209,7 +209,7 @@ class ReSampleSampler(PosteriorSampler, Generic[Condition_co]):
     def _dps_conditioning(self, z_next: Tensor, pseudo: Tensor, sqrt_a: float, a_t: float,
                           cons: _Consistency) -> Tensor:
         """``resample_kernels.py:15-29``: z_next - 0.5 a_t * ∇_z ||y - A D(pseudo)||."""
-        net = self._epsilon_network
+        net = self._network
         with torch.enable_grad():
             pr = pseudo.detach().requires_grad_(True)
             x = net.decode(pr, differentiable=True)
@@ -283,7 +283,7 @@ class ReSampleSampler(PosteriorSampler, Generic[Condition_co]):
         memory: iteration i + 1 is already queued when it waits for iteration i's flag, so
         the GPU queue never drains (the reference's ``.item()`` per iteration stalls it), at
         the price of one decoder forward + VJP past the stop whose update is a no-op."""
-        net, lib = self._epsilon_network, cons.lib
+        net, lib = self._network, cons.lib
         z = z0.detach().clone().contiguous()
         m_, v_ = torch.zeros_like(z), torch.zeros_like(z)
         stop = torch.zeros(1, dtype=torch.int32, device=z.device)
@@ -351,7 +351,7 @@ class ReSampleSampler(PosteriorSampler, Generic[Condition_co]):
         x_shape: Shape = inverse_problem.operator.x_shape
         batch_shape: Shape = inverse_problem.batch_shape
         x_view = BatchView(batch_shape, num_reconstructions, x_shape)
-        net: LatentEpsilonNetwork = self._epsilon_network
+        net: LatentEpsilonNetwork = self._network
         latent_shape: Shape = tuple(net.get_latent_shape(x_shape))
         z_view = BatchView(batch_shape, num_reconstructions, latent_shape)
         net.set_sampling_parameters(num_sampling_steps=num_sampling_steps,
@@ -361,7 +361,7 @@ class ReSampleSampler(PosteriorSampler, Generic[Condition_co]):
         try:
             obs = inverse_problem.observation
             _hip.require_cuda(obs, "ReSampleSampler")
-            y_rows = obs.reshape(max(x_view.batch_size, 1), -1)
+            y_rows = obs.reshape(max(x_view.batch_size, 1), -1).to(torch.float32)
             cons = make_consistency(inverse_problem.operator, y_rows, num_reconstructions, group)
             total = z_view.leading_size * cons.m  # MSELoss mean over the tiled observation
             if dist.is_initialized() and dist.get_world_size(group) > 1:
@@ -420,8 +420,8 @@ class ReSampleSampler(PosteriorSampler, Generic[Condition_co]):
                                        draw("resample", key, z_opt), seed, key, off)
             final_z0 = self._latent_optimization(z, cons, total, eps, max_optimization_iters)
             if decode_output:
-                return x_view.unflatten(net.decode(final_z0, differentiable=False))
-            return z_view.unflatten(final_z0)
+                return self._as_output(x_view.unflatten(net.decode(final_z0, differentiable=False)))
+            return self._as_output(z_view.unflatten(final_z0))
         finally:
             net.clear_condition()
             net.clear_sampling_parameters()

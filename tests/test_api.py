@@ -323,3 +323,35 @@ def test_from_clean_data_reproduces_golden_observation(name):
                                           rng=torch.Generator().manual_seed(7))
     assert prob.observation.dtype == case.y.dtype
     assert torch.equal(prob.observation, case.y)
+
+
+def test_fp32_view_of_networks():
+    """fp32 networks pass through; bf16 / fp16 get the fp32 boundary (inputs cast in, outputs
+    cast out, the rest delegated); non-float dtypes are refused at sampler entry."""
+    from samplers_amd.networks.base import Fp32Boundary, fp32_view
+
+    class Net:
+        def __init__(self, dt):
+            self.dtype, self.calls = dt, []
+
+        def forward(self, x, t):
+            self.calls.append(x.dtype)
+            return x * 2
+
+        def set_sampling_parameters(self, n):
+            self.n = n
+
+    f = Net(torch.float32)
+    assert fp32_view(f) is f
+    b = Net(torch.bfloat16)
+    v = fp32_view(b)
+    assert isinstance(v, Fp32Boundary) and v.dtype == torch.float32
+    x = torch.ones(2, 3, requires_grad=True)
+    out = v(x, 5)
+    assert b.calls == [torch.bfloat16] and out.dtype == torch.float32
+    (g,) = torch.autograd.grad(out.sum(), x)  # the VJP flows through both casts
+    assert torch.equal(g, torch.full((2, 3), 2.0))
+    v.set_sampling_parameters(7)
+    assert b.n == 7
+    with pytest.raises(TypeError, match="dtype"):
+        fp32_view(Net(torch.int32))

@@ -184,3 +184,48 @@ def test_from_clean_data_on_device_reproduces_golden_observation(cuda, name):
                                           noise=noise.to(cuda), rng=torch.Generator().manual_seed(7))
     assert prob.observation.is_cuda
     assert torch.equal(prob.observation.cpu(), case.y)
+
+
+# --- reduced-precision networks at the boundary (dps.py:83-87, scripts/run_psld.py:14) ------
+
+def test_dps_bf16_reference_style_network(cuda):
+    """A bf16 ε-network (the reference's scripts drive bf16 / fp16 priors): the network runs
+    in bf16 behind the fp32 boundary, the guidance and the sample stay fp32, the result comes
+    back in bf16.  Pinned by the oracle loop with the same bf16 network calls (the linear
+    stand-in's bf16 product is one correctly rounded multiply on either device), tolerance
+    = the bf16 rounding of the returned x̂."""
+    case = load_dps_case("dps_rnd_gauss_lin_b4")
+    m = case.meta
+    net = si.make_reference_style_net("linear", 3, m["coef"], device=cuda).to(torch.bfloat16)
+    assert net.dtype == torch.bfloat16
+    prob = InverseProblem(_native_op(case, cuda), case.y.to(cuda), GaussianNoise(0.05).to(cuda))
+    out = DPSSampler(net)(prob, num_sampling_steps=m["N"], gamma=m["gamma"], eta=m["eta"],
+                          noise_fn=_noise_fn(case, cuda))
+    assert out.dtype == torch.bfloat16 and tuple(out.shape) == tuple(m["out_shape"])
+    init, steps = case.noise()
+    acp = net.alphas_cumprod.float().cpu()
+    kept = torch.as_tensor(case.kept).long()
+    ref = dps_loop.dps_reference(lambda x, t: (m["coef"] * x.bfloat16()).float(), acp,
+                                 si.leading_timesteps_ascending(m["N"]).tolist(),
+                                 lambda x: x.reshape(x.shape[0], -1)[:, kept],
+                                 dps_loop.gaussian_log_prob(0.05), case.y, init,
+                                 lambda i: steps[i], gamma=m["gamma"], eta=m["eta"])
+    assert si.relative_error(out.float().cpu(), ref.reshape(out.shape)) < 4e-3
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+def test_psld_reduced_precision_latent_network(cuda, dtype):
+    """PSLD with a bf16 / fp16 latent network (decode / encode / ε in that dtype): runs, returns
+    the network's dtype, and stays within that dtype's rounding of the fp32 network's run."""
+    case = load_dps_case("psld_id_conv_b2")
+    m = case.meta
+    outs = {}
+    for dt in (torch.float32, dtype):
+        net = si.make_reference_style_net("linear", 3, m["coef"], device=cuda, latent=True).to(dt)
+        prob = InverseProblem(_torch_op(case, cuda), case.y.to(cuda), GaussianNoise(0.05).to(cuda))
+        outs[dt] = PSLDSampler(net)(prob, num_sampling_steps=m["N"], num_reconstructions=m["R"],
+                                    gamma=m["gamma"], omega=m["omega"], eta=m["eta"],
+                                    noise_fn=_noise_fn(case, cuda))
+    assert outs[dtype].dtype == dtype and outs[dtype].shape == outs[torch.float32].shape
+    assert torch.isfinite(outs[dtype].float()).all()
+    assert si.relative_error(outs[dtype].float().cpu(), outs[torch.float32].cpu()) < 5e-2
