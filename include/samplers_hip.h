@@ -371,24 +371,6 @@ int sp_wino3x3_bwd_input(const float* dy, const float* up_vjp, int64_t n, int32_
                          int32_t cout, int32_t height, int32_t width, float* dx,
                          sp_stream_t stream);
 
-/* Winograd F(2x2,3x3) with the 16 GEMMs on bf16 MFMAs over exact three-term bf16 splits of
- * the fp32 operands (six partial products per product, fp32 accumulation: fp32-class error,
- * tests/test_conv_gpu.py).  Replaces the same layers as sp_wino3x3_* (diffusers' UNet / VAE
- * 3x3 convolutions: unet_2d_blocks ResnetBlock2D conv1/conv2) where
- * cin % 16 == 0, cout % 32 == 0, H % 16 == 0, W % 32 == 0.  Packed U (sp_wino3x3_x6_pack,
- * input_vjp=1: transposed, flipped weights) takes sp_wino3x3_x6_packed_size floats of
- * storage; res (nullable) is added in the epilogue (must not alias y). */
-int sp_wino3x3_x6_supported(int32_t cin, int32_t cout, int32_t height, int32_t width);
-int64_t sp_wino3x3_x6_packed_size(int32_t cin, int32_t cout);
-int sp_wino3x3_x6_pack(const float* w, int32_t cout, int32_t cin, int32_t input_vjp, float* up,
-                       sp_stream_t stream);
-int sp_wino3x3_x6_fwd(const float* x, const float* up, const float* bias, const float* res, int64_t n,
-                      int32_t cin, int32_t cout, int32_t height, int32_t width, float* y,
-                      sp_stream_t stream);
-int sp_wino3x3_x6_bwd_input(const float* dy, const float* up_vjp, int64_t n, int32_t cin,
-                            int32_t cout, int32_t height, int32_t width, float* dx,
-                            sp_stream_t stream);
-
 /* 1x1 convolution as a per-pixel GEMM on bf16 MFMAs over exact three-term splits of the fp32
  * operands (fp32-class error): Y[n][co][p] = sum_k W[co][k] X[n][k][p] (+ bias[co]) (+ res),
  * X = cat(x1 [n][c1][hw], x2 [n][c2][hw]) read in place, Y split into y1 [n][o1][hw] and
@@ -412,18 +394,6 @@ int sp_gemm_x6(const float* x1, int32_t c1, const float* x2, int32_t c2, const f
 int sp_linear_x6_supported(int64_t tokens, int32_t k, int32_t m);
 int sp_linear_x6(const float* x, const float* wp, const float* bias, const float* res, int64_t tokens,
                  int32_t k, int32_t m, float* y, sp_stream_t stream);
-
-/* Direct 3x3 convolution (stride 1, zero padding 1) with the same bf16x6 arithmetic:
- * y = conv(x, W) (+ bias[cout]) (+ res), x [n][cin][h][w], y / res [n][cout][h][w];
- * cout % 128, cin % 16, h % 8, w % 32.  W [cout][cin][3][3] packed by sp_conv3x3_x6_pack
- * (trans = 1: pack the forward's W [cin'][cout'][3][3] transposed and flipped, so that
- * sp_conv3x3_x6(dy, ..., cin = cout', cout = cin') is the input VJP).  Replaces the priors'
- * nn.Conv2d(3x3) forward / input VJP (diffusers ResnetBlock2D.conv1/conv2), SURVEY.md §8f f1. */
-int sp_conv3x3_x6_supported(int32_t cout, int32_t cin, int32_t h, int32_t w);
-int64_t sp_conv3x3_x6_packed_size(int32_t cout, int32_t cin);
-int sp_conv3x3_x6_pack(const float* w, int32_t cout, int32_t cin, int32_t trans, float* wp, sp_stream_t stream);
-int sp_conv3x3_x6(const float* x, const float* wp, const float* bias, const float* res, int64_t n,
-                  int32_t cin, int32_t cout, int32_t h, int32_t w, float* y, sp_stream_t stream);
 
 /* Fused self-attention softmax(q k^T * scale) v of the SD 1.5 eps-UNet's transformer blocks
  * (attn1 over the latent tokens; diffusers UNet2DConditionModel, stable_diffusion.py:306-313;

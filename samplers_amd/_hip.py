@@ -142,18 +142,6 @@ SIGNATURES = {
                                   _P, ctypes.c_int32, _P, ctypes.c_int32, _P]),
     "sp_linear_x6_supported": (ctypes.c_int, [_I64, ctypes.c_int32, ctypes.c_int32]),
     "sp_linear_x6": (ctypes.c_int, [_P, _P, _P, _P, _I64, ctypes.c_int32, ctypes.c_int32, _P, _P]),
-    "sp_conv3x3_x6_supported": (ctypes.c_int, [ctypes.c_int32] * 4),
-    "sp_conv3x3_x6_packed_size": (_I64, [ctypes.c_int32, ctypes.c_int32]),
-    "sp_conv3x3_x6_pack": (ctypes.c_int, [_P, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, _P, _P]),
-    "sp_conv3x3_x6": (ctypes.c_int, [_P, _P, _P, _P, _I64, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
-                                     ctypes.c_int32, _P, _P]),
-    "sp_wino3x3_x6_supported": (ctypes.c_int, [ctypes.c_int32] * 4),
-    "sp_wino3x3_x6_packed_size": (_I64, [ctypes.c_int32, ctypes.c_int32]),
-    "sp_wino3x3_x6_pack": (ctypes.c_int, [_P, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, _P, _P]),
-    "sp_wino3x3_x6_fwd": (ctypes.c_int, [_P, _P, _P, _P, _I64, ctypes.c_int32, ctypes.c_int32,
-                                         ctypes.c_int32, ctypes.c_int32, _P, _P]),
-    "sp_wino3x3_x6_bwd_input": (ctypes.c_int, [_P, _P, _I64, ctypes.c_int32, ctypes.c_int32,
-                                               ctypes.c_int32, ctypes.c_int32, _P, _P]),
     "sp_wino3x3_packed_size": (_I64, [ctypes.c_int32, ctypes.c_int32]),
     "sp_wino3x3_pack": (ctypes.c_int, [_P, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, _P, _P]),
     "sp_wino3x3_fwd": (ctypes.c_int, [_P, _P, _P, _I64, ctypes.c_int32, ctypes.c_int32,

@@ -22,6 +22,8 @@
 // from the XCD's L2 (tiles are ordered so one XCD walks neighbouring tiles).
 // Taps live in SGPRs (uniform loads), not LDS.
 
+#include <utility>
+
 #include "sp_common.h"
 
 namespace sp {
@@ -704,6 +706,273 @@ __global__ __launch_bounds__(64) void k_blur_dps_dma(
     if (lane == 0) partial[(int64_t)b * P + c * nseg + sg] = racc;
 }
 
+// ---------------------------------------------------------------------------
+// Register-streamed DPS pass (the default for 256-column planes; k_blur_dps_dma above is the
+// LDS-DMA form it replaced, kept selectable with -DSP_BLUR_REG=0).  Same sweep, same
+// segment / flip geometry and the same arithmetic order per element; what changed is how
+// the wave spends its instruction issue, which (not HBM) bounded the DMA form: ~10.3 k
+// instructions per wave at 1.5 waves per SIMD, a third of them scalar bookkeeping (M0
+// juggling per DMA, run-time chunk-phase tests, a vmcnt switch) — PMC, round 2.
+//   * the whole sweep is unrolled at compile time (chunk index, stage presence, the |r|^2
+//     rows, the edge cases are constants; the vertical windows are arrays with constant
+//     indices, i.e. registers; the compiler derives every vmcnt wait);
+//   * x, eps and y rows go straight to VGPRs (buffer_load_dwordx4, row offset in soffset),
+//     PF chunks ahead; LDS holds only the two exchange rows of the horizontal passes;
+//   * the horizontal forward pass runs on row pairs: the chunk's two x0 rows are exchanged
+//     interleaved ({row0, row1} per column), so each window column is one aligned register
+//     pair and one v_pk_fma_f32 applies a tap to both rows (18 per row instead of 36 FMAs);
+//   * the horizontal adjoint (per-lane fold-corrected taps) runs on column pairs: the V row
+//     is exchanged twice, as is and shifted by one column, so that the column pair at every
+//     tap offset is an aligned register pair of one of the two windows; V's off-image
+//     columns are zero pads written once.
+// Requires an even number of segments per plane (H / SSEG), so that in sweep coordinates no
+// segment reaches the bottom edge (the flip maps the last segment to the top).
+// ---------------------------------------------------------------------------
+#ifndef SP_BLUR_REG
+#define SP_BLUR_REG 0
+#endif
+#ifndef SP_BLUR_PF
+#define SP_BLUR_PF 1
+#endif
+#ifndef SP_BLUR_LDSWAIT
+#define SP_BLUR_LDSWAIT 0
+#endif
+#ifndef SP_BLUR_HADJ
+#define SP_BLUR_HADJ 0
+#endif
+#ifndef SP_BLUR_DBG
+#define SP_BLUR_DBG 0  // 1: store the vertical adjoint V (before the horizontal pass) as v
+#endif
+
+template <int N>
+using ic_t = std::integral_constant<int, N>;
+
+template <class F, int... I>
+__device__ __forceinline__ void unroll_seq(F& f, std::integer_sequence<int, I...>) {
+    (f(ic_t<I>{}), ...);
+}
+
+typedef float f2v_t __attribute__((ext_vector_type(2)));
+typedef unsigned u4v_t __attribute__((ext_vector_type(4)));
+
+template <int R, int SEG>
+__global__ __launch_bounds__(64, 2) void k_blur_dps_reg(
+    sp_op op, const float* __restrict__ x, const float* __restrict__ eps,
+    const float* __restrict__ y, int y_div, float a, float k, float gs, float* __restrict__ out,
+    float* __restrict__ partial, int P, unsigned units, const sp_step_rec* __restrict__ sched,
+    const int32_t* __restrict__ cursor) {
+    constexpr int K = 2 * R + 1, CH = 2, NCH = (SEG + 4 * R) / CH, NR = NCH * CH;
+    constexpr int C2 = 2 * R / CH, C3 = 4 * R / CH, PF = SP_BLUR_PF;
+    static_assert((4 * R) % CH == 0 && SEG % CH == 0 && R >= 1 && R <= SPAD, "geometry");
+    if (sched) {
+        const sp_dps_coefs& cf = sched[*cursor].c;
+        a = cf.a, k = cf.k, gs = cf.grad_scale;
+    }
+    constexpr int XS = SWID + 2 * SPAD;  // exchange row stride (columns -SPAD .. SWID+SPAD-1)
+    __shared__ __attribute__((aligned(16))) float xb[2 * XS];      // x0 row pair, interleaved
+    __shared__ __attribute__((aligned(16))) float vb[2][2][XS];    // V rows: [row][as is / shifted]
+    __shared__ float tl[2][K];
+    const int lane = threadIdx.x;
+    if (lane < K) tl[0][lane] = tl[1][K - 1 - lane] = op.taps[lane];
+    // V = 0 off the image: the row writes never touch the pads (as-is copy: indices < SPAD and
+    // >= SWID + SPAD; shifted copy: < SPAD - 1 and >= SWID + SPAD - 1), so zero them once
+    for (int i = lane; i < 4 * XS; i += 64) (&vb[0][0][0])[i] = 0.f;
+    __syncthreads();
+
+    const int H = op.height, C = op.channels, nseg = H / SEG;
+    const unsigned nblk = gridDim.x;
+    const unsigned q8 = nblk / 8, r8 = nblk % 8, xcd = blockIdx.x % 8, loc = blockIdx.x / 8;
+    const unsigned u = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + loc;
+    if (u >= units) return;
+    const unsigned pl = u / nseg;
+    const int sg = static_cast<int>(u - pl * nseg);
+    const int c = static_cast<int>(pl % C);
+    const unsigned b = pl / C;
+    const bool flip = sg & 1;  // odd segments sweep bottom-up (see k_blur_dps_dma)
+    const int s0 = flip ? H - (sg + 1) * SEG : sg * SEG;
+    const bool top = s0 == 0;  // the only segments that meet an image edge in sweep coordinates
+    const int64_t plane = (int64_t)H * SWID;
+    const int pbytes = static_cast<int>(plane * 4);
+    const auto xr = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(x + pl * plane), (short)0, pbytes, 0x00020000);
+    const auto er = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(eps + pl * plane), (short)0, pbytes, 0x00020000);
+    const auto yr = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(y + ((int64_t)(b / (unsigned)y_div) * C + c) * plane), (short)0, pbytes, 0x00020000);
+    const auto vr = __builtin_amdgcn_make_buffer_rsrc(out + pl * plane, (short)0, pbytes, 0x00020000);
+    const int col = 4 * lane;
+    const uint32_t voff = 16u * lane;
+    // physical byte offset of sweep row g (0 <= g < H); rows above the top reflect
+    const int rbase = flip ? (H - 1) * SWID * 4 : 0, rstep = flip ? -SWID * 4 : SWID * 4;
+    auto row_off = [&](int g) { return rbase + rstep * g; };
+
+    float tk[K], tv[K];
+#pragma unroll
+    for (int d = 0; d < K; ++d) tk[d] = op.taps[d];
+#pragma unroll
+    for (int d = 0; d < K; ++d) tv[d] = flip ? tk[K - 1 - d] : tk[d];
+    f2v_t th01[K], th23[K];  // per-lane fold-corrected adjoint taps, column pairs (q0,q1), (q2,q3)
+#pragma unroll
+    for (int o = -R; o <= R; ++o) {
+        th01[o + R] = f2v_t{adj_tap(tl[0], R, SWID, col, o), adj_tap(tl[0], R, SWID, col + 1, o)};
+        th23[o + R] = f2v_t{adj_tap(tl[0], R, SWID, col + 2, o), adj_tap(tl[0], R, SWID, col + 3, o)};
+    }
+    const float inv_a = 1.f / a;
+
+    f4v px[NCH][CH], pe[NCH][CH], py[NCH][CH];  // constant indices only: registers
+    f4v hw[NR], sw[NR];
+    f4v racc = {0.f, 0.f, 0.f, 0.f};
+
+    auto issue = [&](auto icc) __attribute__((always_inline)) {
+        constexpr int cc = decltype(icc)::value;
+        if constexpr (cc < NCH) {
+#pragma unroll
+            for (int e = 0; e < CH; ++e) {
+                const int gi = s0 - 2 * R + CH * cc + e;  // sweep row
+                int gr = gi;
+                if (CH * cc + CH <= 2 * R) gr = gi < 0 ? -gi : gi;  // top reflection (s0 == 0)
+                const int so = row_off(gr);
+                px[cc][e] = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(xr, voff, so, 0));
+                pe[cc][e] = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(er, voff, so, 0));
+                if (cc >= C2) {  // y rows are first used by stage 2 (rows above the image: unused)
+                    const int gy = max(gi - R, 0);
+                    py[cc][e] = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(yr, voff, row_off(gy), 0));
+                }
+            }
+        }
+    };
+
+    auto body = [&](auto icc) __attribute__((always_inline)) {
+        constexpr int cc = decltype(icc)::value;
+        issue(ic_t<cc + PF>{});
+        // ---- 1: x0, horizontal A on the row pair ----
+        {
+            f4v x0[CH];
+#pragma unroll
+            for (int e = 0; e < CH; ++e) x0[e] = (px[cc][e] - k * pe[cc][e]) * inv_a;
+            wave_lds_sync();
+            float* dst = xb + 2 * (col + SPAD);
+            *reinterpret_cast<f4v*>(dst) = f4v{x0[0].x, x0[1].x, x0[0].y, x0[1].y};
+            *reinterpret_cast<f4v*>(dst + 4) = f4v{x0[0].z, x0[1].z, x0[0].w, x0[1].w};
+            wave_lds_sync();
+            f2v_t W[12];
+#pragma unroll
+            for (int q = 0; q < 6; ++q) {
+                const f4v t = *reinterpret_cast<const f4v*>(xb + 2 * col + 4 * q);
+                W[2 * q] = f2v_t{t.x, t.y};
+                W[2 * q + 1] = f2v_t{t.z, t.w};
+            }
+#pragma unroll
+            for (int i = 1; i <= R; ++i) {  // reflect padding at the side edges
+                W[SPAD - i] = lane == 0 ? W[SPAD + i] : W[SPAD - i];
+                W[SPAD + 3 + i] = lane == 63 ? W[SPAD + 3 - i] : W[SPAD + 3 + i];
+            }
+            f2v_t acc[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                f2v_t s = {0.f, 0.f};
+#pragma unroll
+                for (int d = 0; d < K; ++d) s = __builtin_elementwise_fma(f2v_t{tk[d], tk[d]}, W[SPAD - R + q + d], s);
+                acc[q] = s;
+            }
+            hw[CH * cc] = f4v{acc[0].x, acc[1].x, acc[2].x, acc[3].x};
+            hw[CH * cc + 1] = f4v{acc[0].y, acc[1].y, acc[2].y, acc[3].y};
+        }
+        // ---- 2: vertical A, residual, S, |r|^2 ----
+        if constexpr (cc >= C2) {
+#pragma unroll
+            for (int e = 0; e < CH; ++e) {
+                constexpr int g0 = CH * cc - R;  // z row (loaded-row index) of e = 0
+                const int g = g0 + e;
+                f4v z = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                for (int d = 0; d < K; ++d) z += tv[d] * hw[g - R + d];
+                const f4v rr = py[cc][e] - z;
+                // global sweep row s0 - 2R + g: above the image only in a top segment
+                const bool in = (g0 + e >= 2 * R) || !top;
+                sw[g] = in ? rr * gs : f4v{0.f, 0.f, 0.f, 0.f};
+                if (g >= 2 * R && g < 2 * R + SEG) racc += rr * rr;
+            }
+        }
+        // ---- 3: vertical A^T; 4: horizontal A^T, store v ----
+        if constexpr (cc >= C3) {
+#pragma unroll
+            for (int e = 0; e < CH; ++e) {
+                const int h = CH * cc - 2 * R + e;  // v row (loaded-row index); sweep row s0 + h - 2R
+                f4v vv = {0.f, 0.f, 0.f, 0.f};
+                if (CH * cc - 4 * R + e <= R && top) {  // near the top edge: folded taps
+#pragma unroll
+                    for (int o = -R; o <= R; ++o)
+                        vv += adj_tap(tl[flip ? 1 : 0], R, H, CH * cc - 4 * R + e, o) * sw[h + o];
+                } else {
+#pragma unroll
+                    for (int i = 0; i < K; ++i) vv += tv[i] * sw[h + R - i];
+                }
+                wave_lds_sync();
+                *reinterpret_cast<f4v*>(&vb[e][0][col + SPAD]) = vv;
+                float* s1 = &vb[e][1][col + SPAD - 1];  // shifted copy: column c at c + SPAD - 1
+                s1[0] = vv.x, s1[1] = vv.y, s1[2] = vv.z, s1[3] = vv.w;
+                if (SP_BLUR_LDSWAIT) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                wave_lds_sync();
+                f2v_t wn[6], ws[6];  // wn[i] = V(col-SPAD+2i, +1); ws[i] = V(col-SPAD+2i+1, +2)
+#pragma unroll
+                for (int q = 0; q < 3; ++q) {
+                    const f4v t0 = *reinterpret_cast<const f4v*>(&vb[e][0][col + 4 * q]);
+                    const f4v t1 = *reinterpret_cast<const f4v*>(&vb[e][1][col + 4 * q]);
+                    wn[2 * q] = f2v_t{t0.x, t0.y}, wn[2 * q + 1] = f2v_t{t0.z, t0.w};
+                    ws[2 * q] = f2v_t{t1.x, t1.y}, ws[2 * q + 1] = f2v_t{t1.z, t1.w};
+                }
+                // window index j = SPAD + q + o holds V(col + q + o); pair (j, j+1) lives in wn
+                // (j even) or ws (j odd)
+                auto pair = [&](int j) { return (j & 1) ? ws[j >> 1] : wn[j >> 1]; };
+                f2v_t o01 = {0.f, 0.f}, o23 = {0.f, 0.f};
+                if (SP_BLUR_HADJ == 0) {
+#pragma unroll
+                    for (int o = -R; o <= R; ++o) {
+                        o01 = __builtin_elementwise_fma(th01[o + R], pair(SPAD + o), o01);
+                        o23 = __builtin_elementwise_fma(th23[o + R], pair(SPAD + 2 + o), o23);
+                    }
+                } else if (SP_BLUR_HADJ == 1) {
+                    float w[12];
+#pragma unroll
+                    for (int i = 0; i < 6; ++i) w[2 * i] = wn[i].x, w[2 * i + 1] = wn[i].y;
+                    float oo[4];
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        float acc = 0.f;
+#pragma unroll
+                        for (int o = -R; o <= R; ++o)
+                            acc = fmaf(q < 2 ? (q == 0 ? th01[o + R].x : th01[o + R].y)
+                                             : (q == 2 ? th23[o + R].x : th23[o + R].y),
+                                       w[SPAD + q + o], acc);
+                        oo[q] = acc;
+                    }
+                    o01 = f2v_t{oo[0], oo[1]}, o23 = f2v_t{oo[2], oo[3]};
+                } else {
+#pragma unroll
+                    for (int o = -R; o <= R; ++o) {
+                        o01 = __builtin_elementwise_fma(f2v_t{tk[R - o], tk[R - o]}, pair(SPAD + o), o01);
+                        o23 = __builtin_elementwise_fma(f2v_t{tk[R - o], tk[R - o]}, pair(SPAD + 2 + o), o23);
+                    }
+                }
+                const int gv = s0 - 2 * R + h;
+                const f4v res = SP_BLUR_DBG == 1 ? vv : f4v{o01.x, o01.y, o23.x, o23.y};
+                __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4v_t, res), vr, voff,
+                                                       row_off(gv), 0);
+                // hipcc (ROCm 7.2) lets the next instruction overwrite a buffer_store_dwordx4's data
+                // VGPRs with no wait state; the store then reads some lanes' data after the write
+                // (seen as corrupt lanes of the stored row).  Keep the data live across two wait
+                // states (tools/store_hazard_scan.py checks the built code).
+                asm volatile("s_nop 1" ::"v"(res) : "memory");
+            }
+        }
+    };
+
+    unroll_seq(issue, std::make_integer_sequence<int, PF>{});
+    unroll_seq(body, std::make_integer_sequence<int, NCH>{});
+    float t = (racc.x + racc.y) + (racc.z + racc.w);
+    t = wave_sum(t);
+    if (lane == 0) partial[(int64_t)b * P + c * nseg + sg] = t;
+}
+
 int64_t blur_partials(const sp_op* op) {
     if (blur_streams(op)) return (int64_t)op->channels * (op->height / SSEG);
     const int64_t tiles = (int64_t)((op->height + TH - 1) / TH) * ((op->width + TW - 1) / TW);
@@ -725,6 +994,21 @@ static int launch_blur(const sp_op* op, const float* in, const float* eps, const
     const int P = static_cast<int>(blur_partials(op));
     if (MODE == MODE_DPS && blur_streams(op)) {
         const int64_t units = (int64_t)op->channels * (op->height / SSEG) * batch;
+        if (SP_BLUR_REG && (op->height / SSEG) % 2 == 0) {
+            switch (op->radius) {
+#define SP_REG_CASE(RR)                                                                         \
+    case RR:                                                                                    \
+        launch_w(TK_DPS_RESIDUAL, (double)batch, k_blur_dps_reg<RR, SSEG>,                      \
+                 dim3(static_cast<unsigned>(units)), dim3(64), s, *op, in, eps, y,              \
+                 static_cast<int>(y_div), a, k, gs, out, partial, P,                            \
+                 static_cast<unsigned>(units), sched, cursor);                                  \
+        break;
+                SP_REG_CASE(1) SP_REG_CASE(2) SP_REG_CASE(3) SP_REG_CASE(4)
+#undef SP_REG_CASE
+                default: return SP_EINVAL;
+            }
+            return check_launch("blur_stream_reg");
+        }
         switch (op->radius) {
 #define SP_STREAM_CASE(RR)                                                                      \
     case RR:                                                                                    \

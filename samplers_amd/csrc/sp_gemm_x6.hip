@@ -1,5 +1,5 @@
 // 1x1 convolution (per-pixel GEMM) Y[n][co][p] = sum_k W[co][k] X[n][k][p] on bf16 MFMAs over
-// exact three-term bf16 splits of the fp32 operands (the scheme of sp_wino_x6.hip: six partial
+// exact three-term bf16 splits of the fp32 operands (six partial
 // products, fp32 accumulation in two accumulators: the leading product and the small ones;
 // error half of an fp32 GEMM's, tests/test_gemm_x6_gpu.py).
 //
@@ -434,394 +434,6 @@ __global__ void k_gemm_x6_pack(const float* __restrict__ w, int m, int k, int tr
 }
 
 
-// ---------------------------------------------------------------------------------------------
-// Direct 3x3 convolution (stride 1, zero padding 1) with the same arithmetic: implicit GEMM with
-// K = 9 taps x Cin.  Tile = 128 output channels x 8 rows x 32 columns of one image; wave w owns
-// channels 64 (w & 1) .. +63 and rows 2 (w >> 1), +1 (2 x 2 MFMA tiles of 32 x 32).  Per block of
-// 16 input channels the workgroup loads the 10 x 40 patch (rows r0 - 1 .. r0 + 8, columns c0 - 4
-// .. c0 + 35: float4-aligned) by 25 direct 1-KB loads and splits it once into the three bf16
-// terms as [term][10 x 34 pixels][16 ch] (zero outside the image; the two 8-channel halves of
-// a pixel swapped when bit 3 of its index is set, so that the 16 lanes of a ds_read_b128 group,
-// 16 distinct pixels mod 16, hit 16 distinct bank quads); the 9 taps are 9 sub-steps
-// that read shifted windows of that patch, each with its own 12-KB W fragment block streamed
-// two sub-steps ahead (the GEMM's W ring).  The patch of the next block is loaded at tap 1 and
-// split at tap 4, so its load overlaps three sub-steps of MFMAs.  W is packed by
-// sp_conv3x3_x6_pack as an [M][9 Cin] GEMM operand (column (16 kc + tap) ... see k_conv3x3_x6_pack).
-// ---------------------------------------------------------------------------------------------
-constexpr int C6_TR = 8, C6_TC = 32;                 // output rows x columns per tile
-constexpr int C6_PR = C6_TR + 2, C6_PC = C6_TC + 2;  // split patch: 10 x 34
-constexpr int C6_RC = C6_TC + 8;                     // raw patch row: 40 floats from c0 - 4
-constexpr int C6_RAWB = G6_KC * C6_PR * C6_RC * 4;   // 25600 B
-constexpr int C6_NDMA = C6_RAWB / 1024;              // 25 direct loads per block
-constexpr int C6_PPX = C6_PR * C6_PC;                // 340 patch pixels
-constexpr int C6_XB = 3 * C6_PPX * G6_KC * 2;        // 32640 B of split terms per block
-static_assert(C6_RAWB % 1024 == 0 && C6_NDMA <= 32, "patch loads");
-#ifndef C6_PIPE
-#define C6_PIPE 1  // k_conv3x3_x6<true>: fragments of the next sub-step read during this one's products
-#endif
-#ifndef C6_LATE
-#define C6_LATE 0  // > 0: issue the sub-step's loads / split after products 0 .. C6_LATE - 1
-#endif
-#ifndef C6_EXP
-#define C6_EXP 0  // diagnostics only (wrong results, timing): 1 no MFMAs, 2 no split, 3 no loads,
-                  // 4 no fragment reads, 5 one barrier per block
-#endif
-
-struct C6Geom {
-    const float* x;
-    const unsigned short* wp;
-    G6Geom out;  // y1 / bias / res / o1 / hw for g6_epilogue (o2 = 0)
-    int cin, h, w;
-    int ntiles, cob, rt, ct, nkc;
-};
-struct C6Pos { int n, r0, c0, cb; };
-
-__device__ __forceinline__ C6Pos c6_pos(const C6Geom& g, int t) {
-    // XCD-aware: the W of one output-channel block stays in one XCD's L2 (cob | 8); neighbouring
-    // spatial tiles (shared halo rows) run together on it
-    int cb, s;
-    if ((g.ntiles & 7) == 0 && g.cob <= 8 && (8 % g.cob) == 0) {
-        const int x8 = t & 7;
-        cb = x8 % g.cob;
-        s = (t >> 3) * (8 / g.cob) + x8 / g.cob;
-    } else {
-        cb = t % g.cob;
-        s = t / g.cob;
-    }
-    const int per = g.rt * g.ct, n = s / per, rem = s - n * per, ri = rem / g.ct;
-    return C6Pos{n, ri * C6_TR, (rem - ri * g.ct) * C6_TC, cb};
-}
-
-// PIPE: the next sub-step's fragments are read during this one's products (below); W ring of 4
-template <bool PIPE>
-__global__ __launch_bounds__(G6_THREADS, 1) void k_conv3x3_x6(C6Geom g) {
-    constexpr int WSLOTS = PIPE ? 4 : 3;
-    __shared__ __attribute__((aligned(16))) unsigned char raw[C6_RAWB];
-    __shared__ __attribute__((aligned(16))) unsigned char xs[2][C6_XB];
-    __shared__ __attribute__((aligned(16))) unsigned char wl[WSLOTS][G6_WB];
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int ch = wv & 1, pq = wv >> 1;
-    const int nst = 9 * g.nkc;  // sub-steps per tile
-    const auto wrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<unsigned short*>(g.wp), (short)0,
-                                                       g.cob * nst * G6_WB, 0x00020000);
-    const int G = gridDim.x, b0 = blockIdx.x;
-    const int ntile_wg = (g.ntiles - b0 + G - 1) / G;
-    const int J = ntile_wg * nst, NB = ntile_wg * g.nkc;
-
-    // this wave's patch loads: load i = wv + 8 r (r < 4, i < 25); lane: float4 q of patch row
-    // (channel, row) = divmod(64 i + lane, 10) -> its offset inside the block, tile-independent
-    int loff[4];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-        const int f = (wv + 8 * r) * 64 + lane, seg = f / 10, q = f - 10 * seg, cc = seg / 10, row = seg - 10 * cc;
-        loff[r] = (cc * g.h * g.w + row * g.w) * 4 + q * 16;
-    }
-    const int plane_b = g.h * g.w * 4;
-    auto dma_raw = [&](const C6Pos& p, int kc) {
-        const auto rs = __builtin_amdgcn_make_buffer_rsrc(
-            const_cast<float*>(g.x + (int64_t)p.n * g.cin * g.h * g.w), (short)0, g.cin * plane_b, 0x00020000);
-        const int toff = kc * G6_KC * plane_b + ((p.r0 - 1) * g.w + p.c0 - 4) * 4;  // may be < 0
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            if (wv + 8 * r < C6_NDMA) {
-                const int o = loff[r] + toff;  // before the image: out of range (reads 0)
-                g6_lds_dma(rs, raw + (wv + 8 * r) * 1024, o < 0 ? int(0x80000000u) : o, 0);
-            }
-        }
-    };
-    // raw patch -> split terms: task = 8 channels (grp) x patch pixel, 680 tasks on 512 threads
-    auto split = [&](const C6Pos& p, unsigned char* xb) {
-#pragma unroll
-        for (int rep = 0; rep < 2; ++rep) {
-            __builtin_amdgcn_sched_barrier(0);  // one task's registers at a time
-            const int task = tid + rep * G6_THREADS;
-            if (task < 2 * C6_PPX) {
-                const int grp = task >= C6_PPX ? 1 : 0, px = task - grp * C6_PPX;
-                const int pr = px / C6_PC, pc = px - pr * C6_PC;
-                const int gr = p.r0 - 1 + pr, gc = p.c0 - 1 + pc;
-                const bool in = (unsigned)gr < (unsigned)g.h && (unsigned)gc < (unsigned)g.w;
-                const float* rp = reinterpret_cast<const float*>(raw) + (8 * grp * C6_PR + pr) * C6_RC + pc + 3;
-                float v[8];
-#pragma unroll
-                for (int j = 0; j < 8; ++j) v[j] = in ? rp[j * C6_PR * C6_RC] : 0.f;
-                uvec4 th, tm, tl;
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    unsigned h0, m0, l0, h1, m1, l1;
-                    g6_split(v[2 * q], h0, m0, l0);
-                    g6_split(v[2 * q + 1], h1, m1, l1);
-                    th[q] = g6_pack(h0, h1);
-                    tm[q] = g6_pack(m0, m1);
-                    tl[q] = g6_pack(l0, l1);
-                }
-                const int off = (px * G6_KC + 8 * (grp ^ ((px >> 3) & 1))) * 2;  // swizzled halves
-                *reinterpret_cast<uvec4*>(xb + 0 * C6_PPX * G6_KC * 2 + off) = th;
-                *reinterpret_cast<uvec4*>(xb + 1 * C6_PPX * G6_KC * 2 + off) = tm;
-                *reinterpret_cast<uvec4*>(xb + 2 * C6_PPX * G6_KC * 2 + off) = tl;
-            }
-        }
-    };
-
-    // W stream: one 12-KB block per sub-step, two ahead (stage = cb * nst + sub-step)
-    struct WCur { int j, tw, s, slot, cb; };
-    WCur cw{0, 0, 0, 0, c6_pos(g, b0).cb};
-    auto dma_w = [&]() {
-        if (cw.j < J) g6_dma_w(wrs, cw.cb * nst + cw.s, wv, lane, wl[cw.slot]);
-        ++cw.j;
-        cw.slot = cw.slot == WSLOTS - 1 ? 0 : cw.slot + 1;
-        if (++cw.s == nst) {
-            cw.s = 0;
-            if (++cw.tw < ntile_wg) cw.cb = c6_pos(g, b0 + cw.tw * G).cb;
-        }
-    };
-    // patch stream: block nb (tile nb / nkc, channel block nb % nkc)
-    struct BCur { int b, tw, kc; C6Pos ps; };
-    BCur nb{0, 0, 0, c6_pos(g, b0)};
-    auto advance_b = [&]() {
-        ++nb.b;
-        if (++nb.kc == g.nkc) {
-            nb.kc = 0;
-            if (++nb.tw < ntile_wg) nb.ps = c6_pos(g, b0 + nb.tw * G);
-        }
-    };
-
-    // prologue: W 0, 1 (and 2) and patch 0 in, patch 0 split
-    dma_w();
-    dma_raw(nb.ps, 0);
-    dma_w();
-    if constexpr (PIPE) dma_w();
-    __builtin_amdgcn_s_waitcnt(g6_vmcnt(0));
-    __builtin_amdgcn_s_barrier();
-    split(nb.ps, xs[0]);
-    advance_b();
-    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
-    __builtin_amdgcn_s_barrier();
-
-    // per wave: W loads per sub-step nw = 2 (waves 0-3) or 1, patch loads per block nx = 4 (wave 0) or 3
-    static_assert(C6_NDMA == 25, "the wait counts below assume 25 patch loads");
-    if constexpr (PIPE) {
-        // Sub-step j: barrier (W(j + 1) in), loads of W(j + 3) / the next patch / its split, then
-        // the six products over fragments read during sub-step j - 1, each term's registers
-        // refilled with sub-step j + 1's term as soon as its last product has issued.
-        auto rdU = [&](int slot, int e, uvec4 (&t)[2]) {
-            const uvec4* wq = reinterpret_cast<const uvec4*>(wl[slot]) + lane;
-#pragma unroll
-            for (int a = 0; a < 2; ++a) t[a] = wq[((2 * ch + a) * 3 + e) * 64];
-        };
-        auto rdV = [&](const unsigned char* xb, int tap, int e, uvec4 (&t)[2]) {
-            const int ty = tap / 3, tx = tap % 3;
-#pragma unroll
-            for (int b = 0; b < 2; ++b) {
-                const int px = (2 * pq + b + ty) * C6_PC + (lane & 31) + tx;
-                const int off = (px * G6_KC + 8 * ((lane >> 5) ^ ((px >> 3) & 1))) * 2;
-                t[b] = *reinterpret_cast<const uvec4*>(xb + e * C6_PPX * G6_KC * 2 + off);
-            }
-        };
-        f32x16 acc[2][2], acs[2][2];
-        auto prod = [&](const uvec4 (&u)[2], const uvec4 (&v)[2], f32x16 (&c)[2][2]) {
-#pragma unroll
-            for (int b = 0; b < 2; ++b)
-#pragma unroll
-                for (int a = 0; a < 2; ++a) c[a][b] = g6_mfma(u[a], v[b], c[a][b]);
-        };
-        uvec4 uh[2], um[2], ul[2], vh[2], vm[2], vl[2];
-        rdU(0, 0, uh);
-        rdU(0, 1, um);
-        rdU(0, 2, ul);
-        rdV(xs[0], 0, 0, vh);
-        rdV(xs[0], 0, 1, vm);
-        rdV(xs[0], 0, 2, vl);
-        int j = 0, blk = 0, wslot = 0;
-        for (int tw = 0; tw < ntile_wg; ++tw) {
-#pragma unroll
-            for (int a = 0; a < 2; ++a)
-#pragma unroll
-                for (int b = 0; b < 2; ++b) acc[a][b] = f32x16{}, acs[a][b] = f32x16{};
-            for (int kc = 0; kc < g.nkc; ++kc, ++blk) {
-                const unsigned char* xb = xs[blk & 1];
-                const unsigned char* xn = xs[(blk + 1) & 1];
-#pragma unroll
-                for (int tap = 0; tap < 9; ++tap, ++j) {
-                    // W(j + 1) in (older loads retired); at taps 2 - 3 the patch issued at tap 1
-                    // may stay in flight; at tap 5 the split written at tap 4 is visible
-                    if (j > 0) {
-                        if (j + 12 >= J) __builtin_amdgcn_s_waitcnt(0x0070);
-                        else if (tap == 5) {
-                            if (wv < 4) __builtin_amdgcn_s_waitcnt(g6_vmcnt(2) & ~0x0F00);
-                            else __builtin_amdgcn_s_waitcnt(g6_vmcnt(1) & ~0x0F00);
-                        } else if (tap == 2 || tap == 3) {
-                            if (wv == 0) __builtin_amdgcn_s_waitcnt(g6_vmcnt(6));
-                            else if (wv < 4) __builtin_amdgcn_s_waitcnt(g6_vmcnt(5));
-                            else __builtin_amdgcn_s_waitcnt(g6_vmcnt(4));
-                        } else if (wv < 4) __builtin_amdgcn_s_waitcnt(g6_vmcnt(2));
-                        else __builtin_amdgcn_s_waitcnt(g6_vmcnt(1));
-                        __builtin_amdgcn_s_barrier();
-                    }
-                    dma_w();  // W(j + 3)
-                    if (tap == 1 && nb.b < NB) dma_raw(nb.ps, nb.kc);
-                    if (tap == 4) {
-                        if (nb.b < NB) split(nb.ps, xs[(blk + 1) & 1]);
-                        advance_b();
-                    }
-                    const int ns = wslot == WSLOTS - 1 ? 0 : wslot + 1;
-                    const unsigned char* nxb = tap == 8 ? xn : xb;
-                    const int NT = tap == 8 ? 0 : tap + 1;  // constant once unrolled
-                    // products (m,m) (m,h) (h,m) (l,h) (h,l) into acs, (h,h) into acc; each term
-                    // refilled after its last use: um, vm, ul, vl, then uh, vh (needed second and
-                    // third in the next sub-step)
-                    __builtin_amdgcn_sched_barrier(0);
-                    prod(um, vm, acs);
-                    prod(um, vh, acs);
-                    __builtin_amdgcn_sched_barrier(0);
-                    rdU(ns, 1, um);
-                    __builtin_amdgcn_sched_barrier(0);
-                    prod(uh, vm, acs);
-                    __builtin_amdgcn_sched_barrier(0);
-                    rdV(nxb, NT, 1, vm);
-                    __builtin_amdgcn_sched_barrier(0);
-                    prod(ul, vh, acs);
-                    __builtin_amdgcn_sched_barrier(0);
-                    rdU(ns, 2, ul);
-                    __builtin_amdgcn_sched_barrier(0);
-                    prod(uh, vl, acs);
-                    __builtin_amdgcn_sched_barrier(0);
-                    rdV(nxb, NT, 2, vl);
-                    __builtin_amdgcn_sched_barrier(0);
-                    prod(uh, vh, acc);
-                    __builtin_amdgcn_sched_barrier(0);
-                    rdV(nxb, NT, 0, vh);
-                    rdU(ns, 0, uh);
-                    wslot = ns;
-                }
-            }
-            // the next tile's first fragments are live here: fold acs in first (64 registers)
-#pragma unroll
-            for (int a = 0; a < 2; ++a)
-#pragma unroll
-                for (int b = 0; b < 2; ++b) acc[a][b] += acs[a][b];
-            const C6Pos ps = c6_pos(g, b0 + tw * G);
-            const int pxb[2] = {(ps.r0 + 2 * pq) * g.w + ps.c0, (ps.r0 + 2 * pq + 1) * g.w + ps.c0};
-            g6_epilogue<false>(g.out, ps.n, ps.cb, pxb, ch, lane, acc, acc);
-        }
-        return;
-    }
-    f32x16 acc[2][2], acs[2][2];
-    int j = 0, blk = 0, wslot = 0;
-    for (int tw = 0; tw < ntile_wg; ++tw) {
-#pragma unroll
-        for (int a = 0; a < 2; ++a)
-#pragma unroll
-            for (int b = 0; b < 2; ++b) acc[a][b] = f32x16{}, acs[a][b] = f32x16{};
-        for (int kc = 0; kc < g.nkc; ++kc, ++blk) {
-            const unsigned char* xb = xs[blk & 1];
-#pragma unroll
-            for (int tap = 0; tap < 9; ++tap, ++j) {
-                auto side = [&]() {
-#if C6_EXP != 3
-                    dma_w();  // sub-step j + 2
-#else
-                    ++cw.j;
-#endif
-                    // next block's patch: loaded after this sub-step's W (so the W waited for at the
-                    // end of taps 1 and 2 is older than it), in by the end of tap 3, split at tap 4
-#if C6_EXP != 3
-                    if (tap == 1 && nb.b < NB) dma_raw(nb.ps, nb.kc);
-#endif
-                    if (tap == 4) {
-#if C6_EXP != 2
-                        if (nb.b < NB) split(nb.ps, xs[(blk + 1) & 1]);
-#endif
-                        advance_b();
-                    }
-                };
-#if !C6_LATE
-                side();
-#endif
-                const int ty = tap / 3, tx = tap % 3;
-                const uvec4* wq = reinterpret_cast<const uvec4*>(wl[wslot]) + lane;
-                uvec4 fu[2][3], fv[2][3];
-#if C6_EXP == 4
-#pragma unroll
-                for (int a = 0; a < 2; ++a)
-#pragma unroll
-                    for (int e = 0; e < 3; ++e) fu[a][e] = fv[a][e] = uvec4{unsigned(lane + tap), unsigned(e), unsigned(a), 1u};
-#else
-#pragma unroll
-                for (int a = 0; a < 2; ++a)
-#pragma unroll
-                    for (int e = 0; e < 3; ++e) fu[a][e] = wq[((2 * ch + a) * 3 + e) * 64];
-#pragma unroll
-                for (int b = 0; b < 2; ++b) {
-                    const int px = (2 * pq + b + ty) * C6_PC + (lane & 31) + tx;
-                    const int off = (px * G6_KC + 8 * ((lane >> 5) ^ ((px >> 3) & 1))) * 2;
-#pragma unroll
-                    for (int e = 0; e < 3; ++e)
-                        fv[b][e] = *reinterpret_cast<const uvec4*>(xb + e * C6_PPX * G6_KC * 2 + off);
-                }
-#endif
-#if C6_EXP != 1
-                constexpr int TU[6] = {2, 0, 1, 1, 0, 0}, TV[6] = {0, 2, 1, 0, 1, 0};
-#pragma unroll
-                for (int e = 0; e < 6; ++e) {
-#if C6_LATE
-                    if (e == C6_LATE) {  // the loads / split issued behind the first products
-                        __builtin_amdgcn_sched_barrier(0);
-                        side();
-                        __builtin_amdgcn_sched_barrier(0);
-                    }
-#endif
-#pragma unroll
-                    for (int b = 0; b < 2; ++b)
-#pragma unroll
-                        for (int a = 0; a < 2; ++a)
-                            (e == 5 ? acc : acs)[a][b] = g6_mfma(fu[a][TU[e]], fv[b][TV[e]], (e == 5 ? acc : acs)[a][b]);
-                }
-#else
-                if (C6_LATE) side();
-                acc[0][0][0] += __uint_as_float(fu[0][0][0] ^ fv[1][2][1]);
-#endif
-#if C6_EXP == 5
-                if (tap != 8 && j + 9 < J) {
-                    wslot = wslot == 2 ? 0 : wslot + 1;
-                    continue;
-                }
-#endif
-                // W(j + 1) in; younger loads may stay in flight: W(j + 2), and at taps 1 - 2 the
-                // patch (issued after W(j + 1) at tap 1, before W(j + 2) at tap 2)
-                if (j + 9 >= J) __builtin_amdgcn_s_waitcnt(0x0070);  // vmcnt(0) lgkmcnt(0)
-                else if (tap == 1 || tap == 2) {  // nw + nx: 2 + 4 (wave 0), 2 + 3, 1 + 3
-                    if (wv == 0) __builtin_amdgcn_s_waitcnt(g6_vmcnt(6) & ~0x0F00);
-                    else if (wv < 4) __builtin_amdgcn_s_waitcnt(g6_vmcnt(5) & ~0x0F00);
-                    else __builtin_amdgcn_s_waitcnt(g6_vmcnt(4) & ~0x0F00);
-                } else if (wv < 4) __builtin_amdgcn_s_waitcnt(g6_vmcnt(2) & ~0x0F00);
-                else __builtin_amdgcn_s_waitcnt(g6_vmcnt(1) & ~0x0F00);
-                __builtin_amdgcn_s_barrier();
-                wslot = wslot == 2 ? 0 : wslot + 1;
-            }
-        }
-        const C6Pos ps = c6_pos(g, b0 + tw * G);
-        const int pxb[2] = {(ps.r0 + 2 * pq) * g.w + ps.c0, (ps.r0 + 2 * pq + 1) * g.w + ps.c0};
-        g6_epilogue(g.out, ps.n, ps.cb, pxb, ch, lane, acc, acs);
-    }
-}
-
-// W [m][k][3][3] (trans = 0), or for the input VJP the forward's W [k][m][3][3] read transposed
-// and spatially flipped (trans = 1) -> the [m][9 k] GEMM operand with column (9 kc + tap) * 16 + c
-// for input channel 16 kc + c, packed like k_gemm_x6_pack.
-__global__ void k_conv3x3_x6_pack(const float* __restrict__ w, int m, int k, int trans,
-                                  unsigned short* __restrict__ wp) {
-    const int mpad = (m + G6_CO - 1) / G6_CO * G6_CO, kk = 9 * k;
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= (int64_t)mpad * kk) return;
-    const int row = static_cast<int>(i / kk), col = static_cast<int>(i - (int64_t)row * kk);
-    const int s = col / G6_KC, kc = s / 9, tap = s - 9 * kc, ci = kc * G6_KC + (col & (G6_KC - 1));
-    const float v = row >= m ? 0.f
-                    : trans  ? w[((int64_t)ci * m + row) * 9 + 8 - tap]
-                             : w[((int64_t)row * k + ci) * 9 + tap];
-    g6_pack_store(wp, v, row, col, kk);
-}
-
 }  // namespace sp
 
 using namespace sp;
@@ -921,53 +533,6 @@ int sp_linear_x6(const float* x, const float* wp, const float* bias, const float
     const int grid = static_cast<int>(std::min<int64_t>(tiles, g6_cu_count()));
     launch(0, k_gemm_x6<true>, dim3(grid), dim3(G6_THREADS), static_cast<hipStream_t>(stream), g);
     return check_launch("sp_linear_x6");
-}
-
-int sp_conv3x3_x6_supported(int32_t cout, int32_t cin, int32_t h, int32_t w) {
-    return cout >= G6_CO && cout % G6_CO == 0 && cin >= G6_KC && cin % G6_KC == 0 && h >= C6_TR &&
-           h % C6_TR == 0 && w >= C6_TC && w % C6_TC == 0 &&
-           (int64_t)std::max(cin, cout) * h * w * 4 < (int64_t(1) << 31);
-}
-
-int64_t sp_conv3x3_x6_packed_size(int32_t cout, int32_t cin) {
-    return (int64_t)((cout + G6_CO - 1) / G6_CO * G6_CO) * cin * 9 * 6 / 4;
-}
-
-int sp_conv3x3_x6_pack(const float* w, int32_t cout, int32_t cin, int32_t trans, float* wp, sp_stream_t stream) {
-    if (!w || !wp || cout <= 0 || cin <= 0 || cout % 32 || cin % G6_KC) return SP_EINVAL;
-    const int64_t total = (int64_t)((cout + G6_CO - 1) / G6_CO * G6_CO) * cin * 9;
-    launch(0, k_conv3x3_x6_pack, dim3(static_cast<unsigned>((total + 255) / 256)), dim3(256),
-           static_cast<hipStream_t>(stream), w, cout, cin, trans, reinterpret_cast<unsigned short*>(wp));
-    return check_launch("sp_conv3x3_x6_pack");
-}
-
-// y = conv3x3(x, W) (+ bias) (+ res): x [n][cin][h][w], y / res [n][cout][h][w]
-int sp_conv3x3_x6(const float* x, const float* wp, const float* bias, const float* res, int64_t n,
-                  int32_t cin, int32_t cout, int32_t h, int32_t w, float* y, sp_stream_t stream) {
-    if (!sp_conv3x3_x6_supported(cout, cin, h, w) || n < 0) return SP_EINVAL;
-    if (n == 0) return SP_OK;
-    if (!x || !wp || !y || x == y || (res && res == y)) return SP_EINVAL;
-    const int64_t tiles = n * (h / C6_TR) * (w / C6_TC) * (cout / G6_CO);
-    if (tiles >= (int64_t(1) << 31)) return SP_EINVAL;
-    C6Geom g = {};
-    g.x = x;
-    g.wp = reinterpret_cast<const unsigned short*>(wp);
-    g.out.y1 = y;
-    g.out.bias = bias;
-    g.out.res = res;
-    g.out.o1 = cout;
-    g.out.hw = h * w;
-    g.cin = cin;
-    g.h = h;
-    g.w = w;
-    g.ntiles = static_cast<int>(tiles);
-    g.cob = cout / G6_CO;
-    g.rt = h / C6_TR;
-    g.ct = w / C6_TC;
-    g.nkc = cin / G6_KC;
-    const int grid = static_cast<int>(std::min<int64_t>(tiles, g6_cu_count()));
-    launch(0, k_conv3x3_x6<C6_PIPE != 0>, dim3(grid), dim3(G6_THREADS), static_cast<hipStream_t>(stream), g);
-    return check_launch("sp_conv3x3_x6");
 }
 
 }  // extern "C"

@@ -159,11 +159,10 @@ class GroupNormAct(nn.GroupNorm):
 
 def conv_backend() -> str:
     """``SAMPLERS_AMD_CONV``: ``auto`` (default: Winograd F(2x2,3x3) tile where its shape
-    rules hold, else the direct tile, else MIOpen), ``x6`` (as auto, with the Winograd GEMMs
-    on bf16 MFMAs over exact three-term splits of the fp32 operands where its shape rules
-    hold: ``csrc/sp_wino_x6.hip``), ``x6d`` (as auto, with the direct 3x3 implicit GEMM on
-    the same bf16x6 arithmetic where its shape rules hold: ``csrc/sp_gemm_x6.hip``
-    ``k_conv3x3_x6``), ``direct`` (direct tile or MIOpen), ``miopen`` (always torch/MIOpen)."""
+    rules hold, else the direct tile, else MIOpen), ``direct`` (direct tile or MIOpen),
+    ``miopen`` (always torch/MIOpen).  (Two split-bf16 3x3 backends, a Winograd and a direct
+    one, were measured 1.2-1.6x and 1.1-1.3x slower than the fp32 Winograd tile on every
+    UNet shape and were removed from the library; DESIGN.md §3 keeps the measurements.)"""
     import os
 
     return os.environ.get("SAMPLERS_AMD_CONV", "auto").lower()
@@ -172,11 +171,7 @@ def conv_backend() -> str:
 def _conv_algo(lib, cin: int, cout: int, h: int, w: int, backend: str) -> str | None:
     if backend == "miopen":
         return None
-    if backend == "x6" and lib.sp_wino3x3_x6_supported(cin, cout, h, w):
-        return "x6"
-    if backend == "x6d" and lib.sp_conv3x3_x6_supported(cout, cin, h, w):
-        return "x6d"
-    if backend in ("auto", "x6", "x6d") and lib.sp_wino3x3_supported(cin, cout, h, w):
+    if backend == "auto" and lib.sp_wino3x3_supported(cin, cout, h, w):
         return "wino"
     if lib.sp_conv3x3_supported(cin, cout, h, w):
         return "direct"
@@ -206,17 +201,6 @@ def conv3x3_forward(module: "Conv3x3", x: Tensor, res: Tensor | None = None,
                                            _hip.stream_of(x)), "sp_conv3x3_thin_fwd")
         return y if res is None else y.add_(res)
     pk = tile_pack(module, algo, False)
-    if algo == "x6d":
-        _hip.check(lib.sp_conv3x3_x6(_hip.ptr(x), _hip.ptr(pk), _hip.ptr(bias),
-                                     _hip.ptr(None if res is None else res.contiguous()), n, cin, cout, h, w,
-                                     _hip.ptr(y), _hip.stream_of(x)), "sp_conv3x3_x6")
-        return y
-    if algo == "x6":
-        _hip.check(lib.sp_wino3x3_x6_fwd(_hip.ptr(x), _hip.ptr(pk), _hip.ptr(bias),
-                                         _hip.ptr(None if res is None else res.contiguous()), n, cin,
-                                         cout, h, w, _hip.ptr(y), _hip.stream_of(x)),
-                   "sp_wino3x3_x6_fwd")
-        return y
     if algo == "wino" and res is not None:
         _hip.check(lib.sp_wino3x3_fwd_res(_hip.ptr(x), _hip.ptr(pk), _hip.ptr(bias),
                                           _hip.ptr(res.contiguous()), n, cin, cout, h, w,
@@ -243,12 +227,7 @@ def conv3x3_input_vjp(module: "Conv3x3", dy: Tensor, x_shape) -> Tensor:
                                                  n, cin, cout, h, w, _hip.ptr(dx),
                                                  _hip.stream_of(dy)), "sp_conv3x3_thin_bwd_input")
         return dx
-    if algo == "x6d":  # the forward kernel on the transposed / flipped pack
-        _hip.check(lib.sp_conv3x3_x6(_hip.ptr(dy), _hip.ptr(tile_pack(module, algo, True)), None, None, n, cout,
-                                     cin, h, w, _hip.ptr(dx), _hip.stream_of(dy)), "sp_conv3x3_x6")
-        return dx
-    fn = {"wino": lib.sp_wino3x3_bwd_input, "x6": lib.sp_wino3x3_x6_bwd_input}.get(
-        algo, lib.sp_conv3x3_bwd_input)
+    fn = lib.sp_wino3x3_bwd_input if algo == "wino" else lib.sp_conv3x3_bwd_input
     _hip.check(fn(_hip.ptr(dy), _hip.ptr(tile_pack(module, algo, True)), n, cin, cout, h, w,
                   _hip.ptr(dx), _hip.stream_of(dy)), f"sp_{algo}_conv3x3_bwd_input")
     return dx
@@ -289,16 +268,8 @@ def tile_pack(module: nn.Conv2d, algo: str, input_vjp: bool) -> Tensor:
         lib = _hip.load_library()
         cout, cin = w.shape[0], w.shape[1]
         wc = w.detach().contiguous()
-        if algo == "x6d":  # [rows][9 channels] operand: rows = the conv's outputs (cin for the VJP)
-            m, k = (cin, cout) if input_vjp else (cout, cin)
-            out = torch.empty(int(lib.sp_conv3x3_x6_packed_size(m, k)), device=w.device)
-            _hip.check(lib.sp_conv3x3_x6_pack(_hip.ptr(wc), m, k, int(input_vjp), _hip.ptr(out),
-                                              _hip.stream_of(wc)), "sp_conv3x3_x6_pack")
-            cache[(algo, input_vjp)] = out
-            return out
-        size_fn, fn = {"wino": (lib.sp_wino3x3_packed_size, lib.sp_wino3x3_pack),
-                       "x6": (lib.sp_wino3x3_x6_packed_size, lib.sp_wino3x3_x6_pack)}.get(
-            algo, (lib.sp_conv3x3_packed_size, lib.sp_conv3x3_pack))
+        size_fn, fn = ((lib.sp_wino3x3_packed_size, lib.sp_wino3x3_pack) if algo == "wino"
+                       else (lib.sp_conv3x3_packed_size, lib.sp_conv3x3_pack))
         out = torch.empty(int(size_fn(cin, cout)), device=w.device)
         _hip.check(fn(_hip.ptr(wc), cout, cin, int(input_vjp), _hip.ptr(out), _hip.stream_of(wc)),
                    f"sp_{algo}3x3_pack")
@@ -477,7 +448,7 @@ def strided_full_supported(module: nn.Conv2d, x: Tensor) -> bool:
     cout = module.out_channels
     fwd = _conv_algo(lib, cin, cout, h, w, backend)
     vjp = _conv_algo(lib, cout, cin, h, w, backend)
-    ok = ("wino", "x6", "x6d", "direct")
+    ok = ("wino", "direct")
     return h % 2 == 0 and w % 2 == 0 and fwd in ok and vjp in ok
 
 

@@ -51,31 +51,24 @@ def test_library_loads_without_gpu():
     assert lib.sp_vec_partials(0) == -1
 
 
-def test_x6_shape_rules_and_pack_sizes_on_the_host():
-    """The bf16x6 kernels' shape rules and packed sizes are host-side C (no GPU needed): the
-    direct 3x3 conv takes cout % 128, cin % 16, h % 8, w % 32; its pack holds three bf16 terms
-    of the [cout (padded to 128)][9 cin] operand."""
+def test_x6_gemm_pack_sizes_on_the_host():
+    """The bf16x6 GEMM's shape rules and packed size are host-side C (no GPU needed): the pack
+    holds three bf16 terms of the [M (padded to 128)][K] operand."""
     lib = _hip.load_library()
-    assert lib.sp_conv3x3_x6_supported(128, 128, 256, 256)
-    assert lib.sp_conv3x3_x6_supported(512, 256, 64, 64)
-    assert not lib.sp_conv3x3_x6_supported(64, 128, 32, 32)   # cout % 128
-    assert not lib.sp_conv3x3_x6_supported(128, 8, 32, 32)    # cin % 16
-    assert not lib.sp_conv3x3_x6_supported(128, 128, 16, 16)  # w % 32
-    assert not lib.sp_conv3x3_x6_supported(128, 128, 4, 32)   # h % 8
-    assert lib.sp_conv3x3_x6_packed_size(128, 64) == 128 * 9 * 64 * 6 // 4
-    assert lib.sp_conv3x3_x6_packed_size(96, 64) == 128 * 9 * 64 * 6 // 4  # rows padded
     assert lib.sp_gemm_x6_packed_size(256, 128) == 256 * 128 * 6 // 4
+    assert lib.sp_gemm_x6_supported(128, 256, 256 * 256)
+    assert not lib.sp_gemm_x6_supported(128, 250, 256 * 256)  # K % 16
 
 
 def test_conv_backend_selection(monkeypatch):
-    """``SAMPLERS_AMD_CONV`` picks the tile per shape: x6d where the direct bf16x6 conv's rules
-    hold, the fp32 Winograd tile elsewhere (the UNet's 16² / 8² levels)."""
+    """``SAMPLERS_AMD_CONV`` picks the tile per shape: the fp32 Winograd tile where its rules
+    hold, the direct tile under ``direct``, MIOpen under ``miopen``."""
     from samplers_amd.networks.layers import _conv_algo, conv_backend
 
     lib = _hip.load_library()
-    monkeypatch.setenv("SAMPLERS_AMD_CONV", "x6d")
-    assert conv_backend() == "x6d"
-    assert _conv_algo(lib, 128, 128, 256, 256, "x6d") == "x6d"
-    assert _conv_algo(lib, 512, 512, 16, 16, "x6d") == "wino"
+    monkeypatch.setenv("SAMPLERS_AMD_CONV", "direct")
+    assert conv_backend() == "direct"
+    assert _conv_algo(lib, 128, 128, 256, 256, "direct") == "direct"
     assert _conv_algo(lib, 128, 128, 256, 256, "auto") == "wino"
+    assert _conv_algo(lib, 512, 512, 16, 16, "auto") == "wino"
     assert _conv_algo(lib, 128, 128, 256, 256, "miopen") is None
