@@ -75,8 +75,8 @@ def parse():
                    help="DPS workload: inpaint = BASELINE configs[1] (headline), blur = configs[2] "
                         "(64 per GPU of the 512 sharded over 8), identity = configs[0] on the GPU")
     p.add_argument("--micro-batch", type=int, default=0)
-    p.add_argument("--recompute-v", action="store_true",
-                   help="pass 2 re-derives v from y (gather) instead of re-reading pass 1's v")
+    p.add_argument("--reuse-v", action="store_true",
+                   help="pass 2 re-reads pass 1's v instead of re-deriving it from y (the default)")
     p.add_argument("--graph", action="store_true",
                    help="replay one hipGraph-captured step (samplers/graph.py); kernel times and "
                         "the roofline then come from the eager warmup steps")
@@ -355,7 +355,7 @@ def main():
     index_bytes = 12 * ((n + 63) // 64) if args.config == "inpaint" else 0
     timer = KernelTimer()
     step = FusedDPSStep(net, problem, problem.observation, 1, gamma=1.0, eta=1.0,
-                        micro_batch=args.micro_batch or None, timer=timer, reuse_v=not args.recompute_v)
+                        micro_batch=args.micro_batch or None, timer=timer, reuse_v=args.reuse_v)
     from samplers_amd.samplers.dps import initial_sample
 
     seed = 20260101

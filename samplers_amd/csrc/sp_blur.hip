@@ -729,7 +729,7 @@ __global__ __launch_bounds__(64) void k_blur_dps_dma(
 // segment reaches the bottom edge (the flip maps the last segment to the top).
 // ---------------------------------------------------------------------------
 #ifndef SP_BLUR_REG
-#define SP_BLUR_REG 0
+#define SP_BLUR_REG 1
 #endif
 #ifndef SP_BLUR_PF
 #define SP_BLUR_PF 1
@@ -739,6 +739,15 @@ __global__ __launch_bounds__(64) void k_blur_dps_dma(
 #endif
 #ifndef SP_BLUR_HADJ
 #define SP_BLUR_HADJ 0
+#endif
+#ifndef SP_BLUR_NT
+#define SP_BLUR_NT 2  // aux (cache policy) bits for the loads of rows only this segment reads
+#endif
+#ifndef SP_BLUR_NTST
+#define SP_BLUR_NTST 0  // aux bits of the v stores
+#endif
+#ifndef SP_BLUR_G
+#define SP_BLUR_G 1  // waves (segments) per workgroup of the register-streamed pass
 #endif
 #ifndef SP_BLUR_DBG
 #define SP_BLUR_DBG 0  // 1: store the vertical adjoint V (before the horizontal pass) as v
@@ -755,8 +764,12 @@ __device__ __forceinline__ void unroll_seq(F& f, std::integer_sequence<int, I...
 typedef float f2v_t __attribute__((ext_vector_type(2)));
 typedef unsigned u4v_t __attribute__((ext_vector_type(4)));
 
-template <int R, int SEG>
-__global__ __launch_bounds__(64, 2) void k_blur_dps_reg(
+// G waves per workgroup: G = 2 puts the two segments that END their sweeps at a shared boundary
+// (an even segment sweeping down, the odd one below it sweeping up) on one CU, so they reach
+// their shared halo rows together and the second read is served by the CU's L2 (separately
+// placed, their progress drifts apart over the sweep and part of those reads went to HBM)
+template <int R, int SEG, int G>
+__global__ __launch_bounds__(64 * G, 2) void k_blur_dps_reg(
     sp_op op, const float* __restrict__ x, const float* __restrict__ eps,
     const float* __restrict__ y, int y_div, float a, float k, float gs, float* __restrict__ out,
     float* __restrict__ partial, int P, unsigned units, const sp_step_rec* __restrict__ sched,
@@ -769,20 +782,23 @@ __global__ __launch_bounds__(64, 2) void k_blur_dps_reg(
         a = cf.a, k = cf.k, gs = cf.grad_scale;
     }
     constexpr int XS = SWID + 2 * SPAD;  // exchange row stride (columns -SPAD .. SWID+SPAD-1)
-    __shared__ __attribute__((aligned(16))) float xb[2 * XS];      // x0 row pair, interleaved
-    __shared__ __attribute__((aligned(16))) float vb[2][2][XS];    // V rows: [row][as is / shifted]
+    __shared__ __attribute__((aligned(16))) float xbs[G][2 * XS];    // x0 row pair, interleaved
+    __shared__ __attribute__((aligned(16))) float vbs[G][2][2][XS];  // V rows: [row][as is / shifted]
     __shared__ float tl[2][K];
-    const int lane = threadIdx.x;
-    if (lane < K) tl[0][lane] = tl[1][K - 1 - lane] = op.taps[lane];
+    const int lane = threadIdx.x & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x) >> 6);
+    float* xb = xbs[wv];
+    float (*vb)[2][XS] = vbs[wv];
+    if (threadIdx.x < K) tl[0][threadIdx.x] = tl[1][K - 1 - threadIdx.x] = op.taps[threadIdx.x];
     // V = 0 off the image: the row writes never touch the pads (as-is copy: indices < SPAD and
     // >= SWID + SPAD; shifted copy: < SPAD - 1 and >= SWID + SPAD - 1), so zero them once
-    for (int i = lane; i < 4 * XS; i += 64) (&vb[0][0][0])[i] = 0.f;
+    for (int i = threadIdx.x; i < G * 4 * XS; i += 64 * G) (&vbs[0][0][0][0])[i] = 0.f;
     __syncthreads();
 
     const int H = op.height, C = op.channels, nseg = H / SEG;
     const unsigned nblk = gridDim.x;
     const unsigned q8 = nblk / 8, r8 = nblk % 8, xcd = blockIdx.x % 8, loc = blockIdx.x / 8;
-    const unsigned u = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + loc;
+    const unsigned u = ((xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + loc) * G + wv;
     if (u >= units) return;
     const unsigned pl = u / nseg;
     const int sg = static_cast<int>(u - pl * nseg);
@@ -808,7 +824,9 @@ __global__ __launch_bounds__(64, 2) void k_blur_dps_reg(
 #pragma unroll
     for (int d = 0; d < K; ++d) tk[d] = op.taps[d];
 #pragma unroll
-    for (int d = 0; d < K; ++d) tv[d] = flip ? tk[K - 1 - d] : tk[d];
+    for (int d = 0; d < K; ++d)  // wave-uniform: keep them scalar (SGPR pairs for v_pk_fma_f32)
+        tv[d] = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(
+                                              __builtin_bit_cast(int, flip ? tk[K - 1 - d] : tk[d])));
     f2v_t th01[K], th23[K];  // per-lane fold-corrected adjoint taps, column pairs (q0,q1), (q2,q3)
 #pragma unroll
     for (int o = -R; o <= R; ++o) {
@@ -830,11 +848,16 @@ __global__ __launch_bounds__(64, 2) void k_blur_dps_reg(
                 int gr = gi;
                 if (CH * cc + CH <= 2 * R) gr = gi < 0 ? -gi : gi;  // top reflection (s0 == 0)
                 const int so = row_off(gr);
-                px[cc][e] = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(xr, voff, so, 0));
-                pe[cc][e] = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(er, voff, so, 0));
+                // rows no other segment reads (not within 4R rows of either end of the sweep)
+                // may stream past the L2; the shared halo rows keep the default policy
+                constexpr int ri0 = CH * cc;
+                constexpr int AUX = (SP_BLUR_NT && ri0 >= 4 * R && ri0 + CH <= NR - 4 * R) ? SP_BLUR_NT : 0;
+                constexpr int AUXY = (SP_BLUR_NT && ri0 >= 4 * R && ri0 + CH <= NR - 2 * R) ? SP_BLUR_NT : 0;
+                px[cc][e] = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(xr, voff, so, AUX));
+                pe[cc][e] = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(er, voff, so, AUX));
                 if (cc >= C2) {  // y rows are first used by stage 2 (rows above the image: unused)
                     const int gy = max(gi - R, 0);
-                    py[cc][e] = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(yr, voff, row_off(gy), 0));
+                    py[cc][e] = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(yr, voff, row_off(gy), AUXY));
                 }
             }
         }
@@ -956,7 +979,7 @@ __global__ __launch_bounds__(64, 2) void k_blur_dps_reg(
                 const int gv = s0 - 2 * R + h;
                 const f4v res = SP_BLUR_DBG == 1 ? vv : f4v{o01.x, o01.y, o23.x, o23.y};
                 __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4v_t, res), vr, voff,
-                                                       row_off(gv), 0);
+                                                       row_off(gv), SP_BLUR_NTST);
                 // hipcc (ROCm 7.2) lets the next instruction overwrite a buffer_store_dwordx4's data
                 // VGPRs with no wait state; the store then reads some lanes' data after the write
                 // (seen as corrupt lanes of the stored row).  Keep the data live across two wait
@@ -998,8 +1021,8 @@ static int launch_blur(const sp_op* op, const float* in, const float* eps, const
             switch (op->radius) {
 #define SP_REG_CASE(RR)                                                                         \
     case RR:                                                                                    \
-        launch_w(TK_DPS_RESIDUAL, (double)batch, k_blur_dps_reg<RR, SSEG>,                      \
-                 dim3(static_cast<unsigned>(units)), dim3(64), s, *op, in, eps, y,              \
+        launch_w(TK_DPS_RESIDUAL, (double)batch, k_blur_dps_reg<RR, SSEG, SP_BLUR_G>,           \
+                 dim3(static_cast<unsigned>(units / SP_BLUR_G)), dim3(64 * SP_BLUR_G), s, *op, in, eps, y, \
                  static_cast<int>(y_div), a, k, gs, out, partial, P,                            \
                  static_cast<unsigned>(units), sched, cursor);                                  \
         break;

@@ -11,7 +11,7 @@
 namespace sp {
 
 #ifndef SP_KITER
-#define SP_KITER 4
+#define SP_KITER 2
 #endif
 #ifndef SP_NT_STORE
 #define SP_NT_STORE 0
@@ -96,10 +96,16 @@ __device__ __forceinline__ float sum_partials(const float* __restrict__ p, int P
 // ---------------------------------------------------------------------------
 // Vector access
 // ---------------------------------------------------------------------------
-template <int V>
+// NT = non-temporal (streamed-once inputs)
+template <int V, bool NT = false>
 __device__ __forceinline__ void load_v(const float* __restrict__ p, float (&r)[V]) {
     if constexpr (V == 4) {
-        const float4 t = *reinterpret_cast<const float4*>(p);
+        typedef float f4v __attribute__((ext_vector_type(4)));
+        f4v t;
+        if constexpr (NT)
+            t = __builtin_nontemporal_load(reinterpret_cast<const f4v*>(p));
+        else
+            t = *reinterpret_cast<const f4v*>(p);
         r[0] = t.x; r[1] = t.y; r[2] = t.z; r[3] = t.w;
     } else {
 #pragma unroll

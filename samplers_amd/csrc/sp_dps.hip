@@ -67,6 +67,9 @@ void timing_events(int kind, double work, hipEvent_t* start, hipEvent_t* stop) {
 // ---------------------------------------------------------------------------
 // K1: x0 -> residual -> v = A^T(grad_scale * r), per-block sum r^2
 // ---------------------------------------------------------------------------
+#ifndef SP_UPD_NT
+#define SP_UPD_NT 1  // non-temporal loads of the DPS passes' once-read streams (measured +4-5 %)
+#endif
 template <int OPK, int V>
 __global__ __launch_bounds__(kBlock) void k_dps_residual(sp_op op, const float* __restrict__ x,
                                                          const float* __restrict__ eps,
@@ -96,8 +99,8 @@ __global__ __launch_bounds__(kBlock) void k_dps_residual(sp_op op, const float* 
     for (int it = 0; it < kIter; ++it) {
         const int64_t j = j0 + it * (kBlock * V);
         if (j < n) {
-            load_v<V>(xb + j, xv[it]);
-            load_v<V>(eb + j, ev[it]);
+            load_v<V, SP_UPD_NT>(xb + j, xv[it]);
+            load_v<V, SP_UPD_NT>(eb + j, ev[it]);
             if constexpr (OPK == SP_OP_INPAINT) {
                 inpaint_lookup(op, j, bits[it], rank[it]);
             } else {
@@ -115,7 +118,8 @@ __global__ __launch_bounds__(kBlock) void k_dps_residual(sp_op op, const float* 
 #pragma unroll
                 for (int e = 0; e < V; ++e) {
                     yv[it][e] = 0.f;
-                    if ((bits[it] >> e) & 1u) yv[it][e] = yb[r++];
+                    if ((bits[it] >> e) & 1u) yv[it][e] = yb[r];
+                    r += (bits[it] >> e) & 1u;
                 }
             }
         }
@@ -145,8 +149,16 @@ __global__ __launch_bounds__(kBlock) void k_dps_residual(sp_op op, const float* 
 // ---------------------------------------------------------------------------
 // K2: bridge mean + std*xi + gamma/(||r_b|| + eps) * (v - k*w)/a
 // ---------------------------------------------------------------------------
+#ifndef SP_UPD_RCP
+#define SP_UPD_RCP 1  // 1: multiply by 1/a instead of dividing (1 ulp from the reference's division)
+#endif
+#ifndef SP_UPD_WAVES
+#define SP_UPD_WAVES 5  // waves per SIMD the update pass is built for (<= 80 VGPRs, see below)
+#endif
+// 6 waves per SIMD = 6 blocks per CU = 1536 resident blocks: the 3072 blocks of the B = 64,
+// 256^2 step run in exactly two rounds (at 5, 83 VGPRs, they took 2.4 with a partial tail)
 template <int OPK, int V, bool V_IN, bool XI_IN>
-__global__ __launch_bounds__(kBlock) void k_dps_update(
+__global__ __launch_bounds__(kBlock, SP_UPD_WAVES) void k_dps_update(
     sp_op op, const float* __restrict__ x, const float* __restrict__ eps,
     const float* __restrict__ y, const float* __restrict__ v, const float* __restrict__ w,
     const float* __restrict__ partial, int P, const float* __restrict__ xi, uint64_t seed,
@@ -172,11 +184,11 @@ __global__ __launch_bounds__(kBlock) void k_dps_update(
     for (int it = 0; it < kIter; ++it) {
         const int64_t j = j0 + it * (kBlock * V);
         if (j < n) {
-            load_v<V>(xb + j, xv[it]);
-            load_v<V>(eb + j, ev[it]);
-            load_v<V>(wb + j, wv[it]);
+            load_v<V, SP_UPD_NT>(xb + j, xv[it]);
+            load_v<V, SP_UPD_NT>(eb + j, ev[it]);
+            load_v<V, SP_UPD_NT>(wb + j, wv[it]);
             if constexpr (V_IN) {
-                load_v<V>(v + b * n + j, yv[it]);  // yv holds v in this variant
+                load_v<V, SP_UPD_NT>(v + b * n + j, yv[it]);  // yv holds v in this variant
             } else if constexpr (OPK == SP_OP_INPAINT) {
                 inpaint_lookup(op, j, bits[it], rank[it]);
             } else {
@@ -194,11 +206,13 @@ __global__ __launch_bounds__(kBlock) void k_dps_update(
 #pragma unroll
                 for (int e = 0; e < V; ++e) {
                     yv[it][e] = 0.f;
-                    if ((bits[it] >> e) & 1u) yv[it][e] = yb[r++];
+                    if ((bits[it] >> e) & 1u) yv[it][e] = yb[r];
+                    r += (bits[it] >> e) & 1u;
                 }
             }
         }
     }
+    const float inv_a = 1.f / c.a;
     // DPS: gamma / (||r_b|| + eps); without partials a fixed factor (PGDM, PSLD)
     const float scale =
         partial ? c.gamma / (sqrtf(sum_partials(partial + b * P, P)) + c.norm_eps) : c.gamma;
@@ -215,7 +229,8 @@ __global__ __launch_bounds__(kBlock) void k_dps_update(
             float out[V];
 #pragma unroll
             for (int e = 0; e < V; ++e) {
-                const float x0 = (xv[it][e] - c.k * ev[it][e]) / c.a;
+                const float x0 = SP_UPD_RCP ? (xv[it][e] - c.k * ev[it][e]) * inv_a
+                                            : (xv[it][e] - c.k * ev[it][e]) / c.a;
                 float vv;
                 if constexpr (V_IN) {
                     vv = yv[it][e];
@@ -224,7 +239,7 @@ __global__ __launch_bounds__(kBlock) void k_dps_update(
                     vv = kept ? c.grad_scale * (yv[it][e] - x0) : 0.f;
                 }
                 const float mean = c.c_ell * xv[it][e] + c.c_s * x0;
-                const float g = (vv - c.k * wv[it][e]) / c.a;
+                const float g = SP_UPD_RCP ? (vv - c.k * wv[it][e]) * inv_a : (vv - c.k * wv[it][e]) / c.a;
                 out[e] = (mean + c.std * z[e]) + scale * g;
             }
             store_v<V, true>(ob + j, out);

@@ -123,7 +123,7 @@ class FusedDPSStep:
     def __init__(self, network: EpsilonNetwork, inverse_problem: InverseProblem,
                  observation_rows: Tensor, y_div: int, *, gamma: float = 1.0, eta: float = 1.0,
                  micro_batch: int | None = None, timer: KernelTimer | None = None,
-                 reuse_v: bool = True, mode: str = "dps", guidance_weight: float = 1.0) -> None:
+                 reuse_v: bool = False, mode: str = "dps", guidance_weight: float = 1.0) -> None:
         op = inverse_problem.operator
         desc = getattr(op, "hip_descriptor", lambda: None)()
         if desc is None:
@@ -165,9 +165,10 @@ class FusedDPSStep:
             self.grad_scale = float(c)
         self.guidance_weight = float(guidance_weight)
         self.gamma, self.eta = float(gamma), float(eta)
-        # pass 2 re-reads pass 1's v (default: one coalesced float4 stream; measured 4 % faster
-        # than re-deriving v from (x, eps, y) through the inpainting gather on MI355X) or
-        # re-derives it (fewer bytes).  Blur always re-reads it (its adjoint needs a halo).
+        # pass 2 re-derives v from (x, eps, y) (default: SURVEY §8d's minimal bytes, 4n + m per
+        # sample; with non-temporal loads and 2 float4 groups per thread it is 7 % faster than
+        # re-reading pass 1's v, 42.3 vs 45.2 us at B = 64, 256^2) or re-reads v (reuse_v).
+        # Blur always re-reads it (its adjoint needs a halo).
         self.needs_v = desc.kind == _hip.SP_OP_BLUR or bool(reuse_v)
         self.micro_batch = micro_batch
         self.timer = timer
