@@ -47,7 +47,8 @@ def test_struct_layouts_match_header():
 def test_library_loads_without_gpu():
     lib = _hip.load_library()
     assert lib.sp_version() >= 100
-    assert lib.sp_vec_partials(4096) == 1
+    assert lib.sp_vec_partials(2048) == 1  # one partial per 2 float4 groups x 256 threads
+    assert lib.sp_vec_partials(4096) == 2
     assert lib.sp_vec_partials(0) == -1
 
 
