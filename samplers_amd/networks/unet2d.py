@@ -8,9 +8,11 @@ this module rebuilds the architecture of ``google/ddpm-celebahq-256`` (six
 levels of 128/128/256/256/512/512 channels, two residual blocks per level,
 single-head self-attention at 16x16, GroupNorm(32, eps=1e-6) + SiLU,
 sinusoidal time embedding with ``freq_shift=1``) with random weights.  It is
-the prior of the hot path, and it stays in PyTorch-ROCm (MIOpen convolutions,
-hipBLASLt projections); the guidance arithmetic around it is HIP
-(``samplers_amd/csrc``).
+the prior of the hot path.  PyTorch-ROCm drives it (module graph, autograd of the input
+VJP), but its layers run this project's HIP kernels (``samplers_amd/csrc``): 3x3 convs on
+the fp32-MFMA Winograd / stride-2 / thin tiles, GroupNorm(+SiLU) single-pass kernels, the
+1x1 shortcuts and attention projections on the split-bf16 GEMM, nearest upsampling; the
+16x16 attention's scores / softmax stay batched hipBLASLt GEMMs (about 1 % of the step).
 
 Parameters can be loaded from a local safetensors file whose keys follow the
 diffusers naming (``load_state_dict`` accepts them unchanged), so a real

@@ -7,8 +7,10 @@ mean * scaling_factor``.  Architecture (SD 1.5): 128/256/512/512 channels, 2
 residual blocks per encoder level and 3 per decoder level, single-head
 self-attention in both mid blocks, GroupNorm(32, eps=1e-6) + SiLU, 4 latent
 channels, 8x spatial reduction; 83.65 M parameters with random weights (no
-checkpoint offline).  Convolutions run on PyTorch-ROCm (MIOpen); the
-hand-written MFMA conv tiles are SURVEY.md §8f row f1.
+checkpoint offline).  Its 3x3 convolutions run on this project's fp32-MFMA tiles (Winograd,
+stride-2, thin conv_in / conv_out), GroupNorm(+SiLU) and upsampling on HIP kernels, the
+channel-changing 1x1 shortcuts on the split-bf16 GEMM; the mid
+blocks' single-head attention and the 1x1 quant / post-quant convs are torch ops.
 """
 
 from __future__ import annotations

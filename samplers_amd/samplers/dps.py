@@ -5,9 +5,9 @@ Same call contract as ``DPSSampler.__call__`` of the reference
 (``dps.py:91-122``) is rebuilt around two fused HIP passes with the prior's
 input-VJP between them::
 
-    eps = unet(x, t)                               PyTorch-ROCm (MIOpen / hipBLASLt)
+    eps = unet(x, t)                               the prior (its layers on this project's kernels)
     v, |r|^2 partials = sp_dps_residual(x, eps, y) HIP pass 1: x0, A x0, residual, A^T grad
-    w = J_eps^T v                                  PyTorch-ROCm autograd (input-VJP only)
+    w = J_eps^T v                                  the prior's input VJP (PyTorch-ROCm autograd)
     x <- sp_dps_update(x, eps, y|v, w, noise)      HIP pass 2: bridge mean + std*xi + guidance
 
 which is algebraically the reference's ``autograd.grad(log_likelihood(predict_x0(x)).sum(), x)``

@@ -1,8 +1,9 @@
 """Posterior Sampling with Latent Diffusion (mirrors ``/root/reference/samplers/samplers/psld.py:17-166``).
 
 Loop body (``psld.py:118-153``) as an explicit reverse-mode chain: the priors
-(latent UNet, VAE decoder, VAE encoder) stay in PyTorch-ROCm and are
-differentiated with ``autograd.grad(out, in, grad_outputs=...)``; every
+(latent UNet, VAE decoder, VAE encoder: module graphs over this project's conv /
+GroupNorm / GEMM / attention kernels) are differentiated with
+``autograd.grad(out, in, grad_outputs=...)``; every
 pixel/latent-space step between them is a HIP kernel::
 
     eps  = UNet(z, t)                     z0 = (z - k eps)/a           sp_predict_x0

@@ -35,7 +35,7 @@ import samplers_amd  # noqa: E402,F401
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
-from bench import setup_dist  # noqa: E402
+from bench import MFMA_F32_PEAK_TFLOPS, conv_summary, host_cpu, setup_dist  # noqa: E402
 
 VAE_FLOP_PER_SAMPLE = 7.13e12
 # SD 1.5 UNet at 64x64 latents: 0.80 TFLOP forward + 0.92 input VJP (torch FlopCounterMode)
@@ -60,6 +60,12 @@ def main():
     p.add_argument("--steps", type=int, default=3)
     p.add_argument("--warmup", type=int, default=2)
     p.add_argument("--heartbeat", default="gpurun_out/psld_heartbeat.log")
+    p.add_argument("--cfg", action="store_true",
+                   help="classifier-free guidance on: distinct (seeded random) prompt embeddings, "
+                        "guidance 7.5, so the UNet batch doubles (stable_diffusion.py:300-320)")
+    p.add_argument("--cpu-baseline", action="store_true",
+                   help="also time one PSLD iteration of oracle/latent_loops.py on the host cores "
+                        "(batch 1, same networks)")
     args = p.parse_args()
     Path(args.heartbeat).parent.mkdir(parents=True, exist_ok=True)
     heartbeat(Path(args.heartbeat))
@@ -84,7 +90,12 @@ def main():
     y = y + (0.05 * torch.randn(tuple(y.shape), generator=gen)).to(dev)
     net = LatentDiffusionNetwork.from_config(seed=0, device=dev)
     net.set_sampling_parameters(100, batch_size=args.batch)
-    net.set_condition(StableDiffusionCondition(prompt=[""] * args.batch))  # reference default prompt, CFG collapses
+    if args.cfg:  # distinct conditional / unconditional contexts: the doubled-batch path
+        pe = torch.randn(args.batch, 77, 768, generator=torch.Generator().manual_seed(77))
+        cond = StableDiffusionCondition(prompt=None, prompt_embeds=pe, guidance_scale=7.5)
+    else:
+        cond = StableDiffusionCondition(prompt=[""] * args.batch)  # reference default: CFG collapses
+    net.set_condition(cond)
     problem = InverseProblem(op, y, GaussianNoise(0.05).to(dev))
     lat = tuple(net.get_latent_shape(shape))
     step = FusedPSLDStep(net, problem, y.reshape(args.batch, -1), 1, lat, group=group)
@@ -106,6 +117,10 @@ def main():
             print(f"[psld] warmup {k + 1} done at {time.perf_counter() - t0:.1f}s",
                   file=sys.stderr, flush=True)
     torch.cuda.reset_peak_memory_stats()
+    from samplers_amd.samplers.dps import KernelTimer
+
+    timer = KernelTimer()  # dispatch-packet events on the library's timed kernels (conv tiles)
+    timer.clear()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -126,6 +141,21 @@ def main():
     if not torch.isfinite(z).all():
         raise SystemExit("non-finite latents")
     ms = dt / args.steps * 1e3
+    conv = conv_summary(timer.summary())
+    timer.close()
+    roofline = None
+    if conv:
+        roofline = {"kernel": "3x3 conv tiles (" + " + ".join(conv["kernels"]) + ")",
+                    "bound": "mfma", "achieved": round(conv["tflops"], 2),
+                    "peak": MFMA_F32_PEAK_TFLOPS, "unit": "TFLOP/s",
+                    "frac": round(conv["tflops"] / MFMA_F32_PEAK_TFLOPS, 4), "traffic": None,
+                    "algorithmic_flops_per_launch": conv["flops"] / conv["count"],
+                    "flops_basis": "executed MFMA FLOPs (Winograd: 8*N*Cin*Cout*H*W, direct: 18*...)",
+                    "avg_launch_ms": round(conv["ms"] / conv["count"], 4),
+                    "share_of_step": round(conv["ms"] / args.steps / ms, 4)}
+    cpu = None
+    if args.cpu_baseline and rank == 0:
+        cpu = cpu_baseline_psld(args.image, cond if args.cfg else None)
     if world > 1:
         dist.destroy_process_group()
     if rank != 0:
@@ -146,7 +176,57 @@ def main():
         "model_tflops": round((VAE_FLOP_PER_SAMPLE + UNET_FLOP_PER_SAMPLE) * args.batch
                               / (ms / 1e3) / 1e12, 2),
         "peak_gib": round(torch.cuda.max_memory_allocated() / 2**30, 1),
+        "cfg": bool(args.cfg),
+        "roofline": roofline,
+        "cpu_baseline": cpu,
     }), flush=True)
+
+
+def cpu_baseline_psld(image: int, cond) -> dict:
+    """One PSLD iteration (oracle/latent_loops.py, psld.py:118-153 semantics) at batch 1 on
+    the host cores with the same random-init SD 1.5 networks (CPU copies), at the CPU share
+    the job is given (bench.host_cpu)."""
+    import numpy as np
+
+    from oracle.latent_loops import psld_reference
+    from samplers_amd.networks.latent import LatentDiffusionNetwork, StableDiffusionCondition
+    from samplers_amd.operators import CenterInpaintingOperator
+
+    host = host_cpu()
+    torch.set_num_threads(host["cpu_share"])
+    shape = (3, image, image)
+    net = LatentDiffusionNetwork.from_config(seed=0)
+    net.set_sampling_parameters(100, batch_size=1)
+    if cond is not None:
+        cond = StableDiffusionCondition(prompt=None, prompt_embeds=cond.prompt_embeds[:1],
+                                        guidance_scale=cond.guidance_scale)
+    net.set_condition(cond if cond is not None else StableDiffusionCondition(prompt=[""]))
+    kept = CenterInpaintingOperator(shape, 0.5)._kept_indices
+    n = int(np.prod(shape))
+
+    def apply(v):
+        return v.reshape(v.shape[0], -1)[:, kept]
+
+    def adjoint(v):
+        out = torch.zeros(v.shape[0], n, dtype=v.dtype)
+        out = out.index_put((torch.arange(v.shape[0])[:, None], kept[None, :]), v)
+        return out.reshape(v.shape[0], *shape)
+
+    gen = torch.Generator().manual_seed(5)
+    y = apply(torch.rand(1, *shape, generator=gen) * 2 - 1)
+    z = torch.randn(1, *net.get_latent_shape(shape), generator=gen)
+    ts = net.timesteps_host
+    t0 = time.perf_counter()
+    psld_reference(lambda v, t: net(v, t), net.alphas_cumprod, ts, apply, adjoint,
+                   lambda v: net.decode(v, differentiable=True),
+                   lambda v: net.encode(v, differentiable=True), y, z,
+                   lambda i: torch.randn(z.shape, generator=gen), steps_limit=1)
+    dt = time.perf_counter() - t0
+    return {"value": round(1 / dt, 5), "unit": "samples/sec (batch×steps/s)",
+            "cores": host["cpu_share"], "kind": "port", "cpu_model": host["model"],
+            "sample": f"one PSLD iteration of oracle/latent_loops.py at batch 1, 3x{image}², "
+                      f"same random-init SD 1.5 VAE + UNet{' with CFG' if cond is not None else ''}, "
+                      f"fp32, torch-CPU {torch.__version__}: {dt:.1f} s"}
 
 
 if __name__ == "__main__":

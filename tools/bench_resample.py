@@ -47,7 +47,7 @@ import samplers_amd  # noqa: E402,F401
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
-from bench import setup_dist  # noqa: E402
+from bench import MFMA_F32_PEAK_TFLOPS, conv_summary, host_cpu, setup_dist  # noqa: E402
 
 sys.path.insert(0, str(ROOT / "tools"))
 from bench_psld import VAE_FLOP_PER_SAMPLE, heartbeat  # noqa: E402
@@ -88,6 +88,15 @@ def main():
     p.add_argument("--pixel-iters", type=int, default=200)
     p.add_argument("--latent-iters", type=int, default=3)
     p.add_argument("--heartbeat", default="gpurun_out/resample_heartbeat.log")
+    p.add_argument("--full-call", type=int, default=0, metavar="N",
+                   help="also time one whole ReSampleSampler.__call__ with N sampling steps "
+                        "(time travel every 5 indices, the reference's stopping rules, "
+                        "--max-iters AdamW iterations at most)")
+    p.add_argument("--max-iters", type=int, default=220,
+                   help="max_optimization_iters of the whole call (the plateau rule needs > 200)")
+    p.add_argument("--cpu-baseline", action="store_true",
+                   help="also time one main-loop iteration and one latent AdamW iteration of "
+                        "oracle/resample_loop.py on the host cores (batch 1)")
     args = p.parse_args()
     Path(args.heartbeat).parent.mkdir(parents=True, exist_ok=True)
     heartbeat(Path(args.heartbeat))
@@ -145,8 +154,45 @@ def main():
     pix_s = timed(lambda: sampler._pixel_optimization(x_pix, cons, total, 0.0, args.pixel_iters),
                   1, "pixel", world, rank) / args.pixel_iters
     sampler._latent_optimization(z, cons, total, 1e-3, 1)  # warm
+    from samplers_amd.samplers.dps import KernelTimer
+
+    timer = KernelTimer()  # the decoder fwd + VJP's conv tiles during the latent AdamW iterations
+    timer.clear()
     lat_s = timed(lambda: sampler._latent_optimization(z, cons, total, 0.0, args.latent_iters),
                   1, "latent", world, rank) / args.latent_iters
+    conv = conv_summary(timer.summary())
+    timer.close()
+    roofline = None
+    if conv:
+        roofline = {"kernel": "3x3 conv tiles (" + " + ".join(conv["kernels"]) + "), latent AdamW "
+                              "iterations (VAE decode forward + VJP)",
+                    "bound": "mfma", "achieved": round(conv["tflops"], 2),
+                    "peak": MFMA_F32_PEAK_TFLOPS, "unit": "TFLOP/s",
+                    "frac": round(conv["tflops"] / MFMA_F32_PEAK_TFLOPS, 4), "traffic": None,
+                    "algorithmic_flops_per_launch": conv["flops"] / conv["count"],
+                    "flops_basis": "executed MFMA FLOPs (Winograd: 8*N*Cin*Cout*H*W, direct: 18*...)",
+                    "avg_launch_ms": round(conv["ms"] / conv["count"], 4),
+                    "share_of_iteration": round(conv["ms"] / (args.latent_iters * lat_s * 1e3), 4)}
+
+    full = None
+    if args.full_call:
+        # one whole ReSample solve: main loop, time travel (pixel-space hard consistency in
+        # the later stages), stochastic resampling and the final latent-space solve, with
+        # the reference's stopping rules (resample_kernels.py:32-93)
+        from samplers_amd.inverse_problem import InverseProblem
+
+        prob = InverseProblem(op, y, noise)
+        kw = dict(num_sampling_steps=args.full_call, max_optimization_iters=args.max_iters,
+                  time_travel_interval=5, seed=seed, sample_offset=off, group=group,
+                  condition=StableDiffusionCondition(prompt=[""] * b))
+        wall = timed(lambda: sampler(prob, **kw), 1, "full call", world, rank)
+        full = {"num_sampling_steps": args.full_call, "guided_iterations": args.full_call - 2,
+                "max_optimization_iters": args.max_iters, "time_travel_interval": 5,
+                "wall_s": round(wall, 2), "gpu_s_per_sample": round(wall / b, 3),
+                "samples_x_steps_per_s": round(b * world * (args.full_call - 2) / wall, 4)}
+    cpu = None
+    if args.cpu_baseline and rank == 0:
+        cpu = cpu_baseline_resample(args.image)
 
     n = b * shape[0] * args.image * args.image
     peak_gib = round(torch.cuda.max_memory_allocated() / 2**30, 1)
@@ -173,7 +219,53 @@ def main():
         "latent_iter_tflops": round(DECODE_FLOP_PER_SAMPLE * b / lat_s / 1e12, 2),
         "peak_gib": peak_gib,
         "vae_flop_per_sample_step": VAE_FLOP_PER_SAMPLE,
+        "roofline": roofline,
+        "full_call": full,
+        "cpu_baseline": cpu,
     }), flush=True)
+
+
+def cpu_baseline_resample(image: int) -> dict:
+    """One ReSample main-loop iteration (ε-form DDIM step + DPS conditioning through the
+    decoder VJP) and one latent-space AdamW iteration (decoder forward + VJP), restated by
+    oracle/resample_loop.py, at batch 1 on the host cores with the same random-init SD 1.5
+    networks (CPU copies)."""
+    from oracle.resample_loop import ddim_step_eps
+    from samplers_amd.networks.latent import LatentDiffusionNetwork, StableDiffusionCondition
+
+    host = host_cpu()
+    torch.set_num_threads(host["cpu_share"])
+    shape = (3, image, image)
+    net = LatentDiffusionNetwork.from_config(seed=0)
+    net.set_sampling_parameters(100, batch_size=1)
+    net.set_condition(StableDiffusionCondition(prompt=[""]))
+    gen = torch.Generator().manual_seed(5)
+    y = (torch.rand(1, *shape, generator=gen) * 2 - 1).reshape(1, -1)
+    z = torch.randn(1, *net.get_latent_shape(shape), generator=gen)
+    acp, ts = net.alphas_cumprod, net.timesteps_host
+    i = len(ts) - 1
+    t0 = time.perf_counter()
+    zr = z.clone().requires_grad_()
+    z_next, _x0, pseudo = ddim_step_eps(zr, lambda v, t: net(v, t), acp, ts[i], ts[i - 1], 1.0,
+                                        lambda s: torch.randn(s, generator=gen))
+    norm = torch.linalg.norm(y - net.decode(pseudo, differentiable=True).reshape(1, -1))
+    (g,) = torch.autograd.grad(norm, zr)
+    z = z_next.detach() - g * 0.5 * acp[ts[i]]
+    step_s = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    zo = z.clone().requires_grad_()
+    opt = torch.optim.AdamW([zo], lr=5e-3)
+    opt.zero_grad()
+    loss = torch.nn.MSELoss()(y, net.decode(zo, differentiable=True).reshape(1, -1))
+    loss.backward()
+    opt.step()
+    lat_s = time.perf_counter() - t0
+    return {"value": round(1 / step_s, 5), "unit": "samples/sec (batch×steps/s)",
+            "cores": host["cpu_share"], "kind": "port", "cpu_model": host["model"],
+            "latent_iter_s": round(lat_s, 2),
+            "sample": f"one main-loop iteration ({step_s:.1f} s) and one latent AdamW iteration "
+                      f"({lat_s:.1f} s) of oracle/resample_loop.py at batch 1, 3x{image}², same "
+                      f"random-init SD 1.5 VAE + UNet, fp32, torch-CPU {torch.__version__}"}
 
 
 if __name__ == "__main__":
