@@ -395,6 +395,15 @@ int sp_linear_x6_supported(int64_t tokens, int32_t k, int32_t m);
 int sp_linear_x6(const float* x, const float* wp, const float* bias, const float* res, int64_t tokens,
                  int32_t k, int32_t m, float* y, sp_stream_t stream);
 
+/* The same GEMM between the two activation layouts of the transformer blocks' 1x1 proj_in /
+ * proj_out (diffusers Transformer2DModel): x [n][k][hw] (in_tm = 0) or [n hw][k] (in_tm = 1),
+ * y and res [n][m][hw] (out_tm = 0) or [n hw][m] (out_tm = 1); the NCHW <-> token transposes
+ * happen in the tile's loads and stores.  hw % 256, k % 16, m % 32. */
+int sp_gemm_x6_layout_supported(int64_t n, int64_t hw, int32_t k, int32_t m);
+int sp_gemm_x6_layout(const float* x, const float* wp, const float* bias, const float* res, int64_t n,
+                      int64_t hw, int32_t k, int32_t m, int32_t in_tm, int32_t out_tm, float* y,
+                      sp_stream_t stream);
+
 /* Fused self-attention softmax(q k^T * scale) v of the SD 1.5 eps-UNet's transformer blocks
  * (attn1 over the latent tokens; diffusers UNet2DConditionModel, stable_diffusion.py:306-313;
  * replaces the scores / softmax / weighted-sum chain and its autograd VJP) on fp32 MFMA,
@@ -410,6 +419,52 @@ int sp_attention_bwd(const float* q, const float* k, const float* v, const float
                      const float* dout, const float* lse, int64_t bh, int64_t n, int32_t d,
                      float scale, float* delta, float* dq, float* dk, float* dv,
                      sp_stream_t stream);
+/* The same on the token-major activations of the projections, without head split / merge
+ * copies, and cross-attention: row i of head h of sample b of q (and dq) starts at
+ * (b n + i) rs + h d, of out (and dout) at (b n + i) ro + h d, of k, v (and dk, dv) at
+ * (b' m + j) rs_kv + h d with b' = b (kv_batch = batch) or 0 (kv_batch = 1: one context
+ * shared by the batch).  Self-attention: m = n, rs_kv = rs (rs = 3 heads d when q, k, v are
+ * the thirds of one fused qkv projection [b n][3 heads d]).  Cross-attention (m != n, any
+ * m >= 1, e.g. the 77-token text context of attn2): forward and dq only (dk = dv = NULL).
+ * lse, delta: [b heads][n]. */
+int sp_attention_mh_supported(int64_t batch, int32_t heads, int64_t n, int64_t m, int32_t d);
+int sp_attention_fwd_mh(const float* q, const float* k, const float* v, int64_t batch, int32_t heads,
+                        int64_t n, int64_t m, int32_t d, int32_t rs, int32_t rs_kv, int64_t kv_batch,
+                        int32_t ro, float scale, float* out, float* lse, sp_stream_t stream);
+int sp_attention_bwd_mh(const float* q, const float* k, const float* v, const float* out,
+                        const float* dout, const float* lse, int64_t batch, int32_t heads, int64_t n,
+                        int64_t m, int32_t d, int32_t rs, int32_t rs_kv, int64_t kv_batch, int32_t ro,
+                        float scale, float* delta, float* dq, float* dk, float* dv, sp_stream_t stream);
+
+/* Transformer-block glue of the SD 1.5 eps-UNet (diffusers BasicTransformerBlock,
+ * stable_diffusion.py:306-313): torch.nn.LayerNorm over the C channels of token-major rows
+ * [rows][C] (C % 4, C <= 2048; mean / rstd [rows] written for the VJP) and its input VJP
+ * (frozen weights; add != NULL is summed into dx: the residual branch's gradient of the same
+ * tensor), and the feed-forward's GEGLU gate y = a * gelu(gate) over h = [a | gate]
+ * ([rows][2F] -> [rows][F], exact erf GELU, F % 4) and its input VJP dh. */
+int sp_layernorm_supported(int64_t rows, int32_t c);
+int sp_layernorm_fwd(const float* x, const float* w, const float* b, int64_t rows, int32_t c, float eps,
+                     float* y, float* mean, float* rstd, sp_stream_t stream);
+int sp_layernorm_bwd(const float* dy, const float* x, const float* w, const float* mean, const float* rstd,
+                     const float* add, int64_t rows, int32_t c, float* dx, sp_stream_t stream);
+int sp_geglu_fwd(const float* h, int64_t rows, int32_t f, float* y, sp_stream_t stream);
+int sp_geglu_bwd(const float* h, const float* dy, int64_t rows, int32_t f, float* dh, sp_stream_t stream);
+
+/* Row softmax of materialised attention scores [rows][n] in place (n % 4, n <= 4096; lse
+ * [rows] = row log-sum-exp when non-NULL) and its VJP scaled by the score scale,
+ * dp <- scale * p * (dp - rowsum(p * dp)): the single-head d = 512 attention of the SD VAE
+ * mid blocks and the DDPM UNet (diffusers Attention, ddpm.py:40-43 / stable_diffusion.py:
+ * 330-345), whose score GEMMs are hipBLASLt's. */
+int sp_softmax_rows_supported(int64_t rows, int32_t n);
+int sp_softmax_rows(float* s, int64_t rows, int32_t n, float* lse, sp_stream_t stream);
+int sp_softmax_bwd_rows(const float* p, float* dp, int64_t rows, int32_t n, float scale, sp_stream_t stream);
+
+/* 1x1 convolution over 4 or 8 channels (the SD VAE's quant_conv / post_quant_conv):
+ * y[n][o][p] = sum_c w[o][c] x[n][c][p] (+ b[o]); trans = 1 applies W^T (input VJP, b NULL).
+ * hw % 4. */
+int sp_conv1x1_small_supported(int32_t cin, int32_t cout, int64_t hw);
+int sp_conv1x1_small(const float* x, const float* w, const float* b, int64_t n, int32_t cin, int32_t cout,
+                     int64_t hw, int32_t trans, float* y, sp_stream_t stream);
 
 #ifdef __cplusplus
 }

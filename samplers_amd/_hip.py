@@ -129,6 +129,13 @@ SIGNATURES = {
     "sp_attention_fwd": (ctypes.c_int, [_P, _P, _P, _I64, _I64, ctypes.c_int32, _F, _P, _P, _P]),
     "sp_attention_bwd": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _I64, _I64, ctypes.c_int32, _F,
                                         _P, _P, _P, _P, _P]),
+    "sp_attention_mh_supported": (ctypes.c_int, [_I64, ctypes.c_int32, _I64, _I64, ctypes.c_int32]),
+    "sp_attention_fwd_mh": (ctypes.c_int, [_P, _P, _P, _I64, ctypes.c_int32, _I64, _I64, ctypes.c_int32,
+                                           ctypes.c_int32, ctypes.c_int32, _I64, ctypes.c_int32, _F, _P, _P,
+                                           _P]),
+    "sp_attention_bwd_mh": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _I64, ctypes.c_int32, _I64, _I64,
+                                           ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, _I64,
+                                           ctypes.c_int32, _F, _P, _P, _P, _P, _P]),
     "sp_conv3x3_s2_pack": (ctypes.c_int, [_P, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, _P, _P]),
     "sp_conv3x3_s2_fwd": (ctypes.c_int, [_P, _P, _P, _I64, ctypes.c_int32, ctypes.c_int32,
                                          ctypes.c_int32, ctypes.c_int32, _P, _P]),
@@ -142,6 +149,20 @@ SIGNATURES = {
                                   _P, ctypes.c_int32, _P, ctypes.c_int32, _P]),
     "sp_linear_x6_supported": (ctypes.c_int, [_I64, ctypes.c_int32, ctypes.c_int32]),
     "sp_linear_x6": (ctypes.c_int, [_P, _P, _P, _P, _I64, ctypes.c_int32, ctypes.c_int32, _P, _P]),
+    "sp_gemm_x6_layout_supported": (ctypes.c_int, [_I64, _I64, ctypes.c_int32, ctypes.c_int32]),
+    "sp_gemm_x6_layout": (ctypes.c_int, [_P, _P, _P, _P, _I64, _I64, ctypes.c_int32, ctypes.c_int32,
+                                         ctypes.c_int32, ctypes.c_int32, _P, _P]),
+    "sp_layernorm_supported": (ctypes.c_int, [_I64, ctypes.c_int32]),
+    "sp_layernorm_fwd": (ctypes.c_int, [_P, _P, _P, _I64, ctypes.c_int32, _F, _P, _P, _P, _P]),
+    "sp_layernorm_bwd": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _I64, ctypes.c_int32, _P, _P]),
+    "sp_geglu_fwd": (ctypes.c_int, [_P, _I64, ctypes.c_int32, _P, _P]),
+    "sp_geglu_bwd": (ctypes.c_int, [_P, _P, _I64, ctypes.c_int32, _P, _P]),
+    "sp_softmax_rows_supported": (ctypes.c_int, [_I64, ctypes.c_int32]),
+    "sp_softmax_rows": (ctypes.c_int, [_P, _I64, ctypes.c_int32, _P, _P]),
+    "sp_softmax_bwd_rows": (ctypes.c_int, [_P, _P, _I64, ctypes.c_int32, _F, _P]),
+    "sp_conv1x1_small_supported": (ctypes.c_int, [ctypes.c_int32, ctypes.c_int32, _I64]),
+    "sp_conv1x1_small": (ctypes.c_int, [_P, _P, _P, _I64, ctypes.c_int32, ctypes.c_int32, _I64,
+                                        ctypes.c_int32, _P, _P]),
     "sp_wino3x3_packed_size": (_I64, [ctypes.c_int32, ctypes.c_int32]),
     "sp_wino3x3_pack": (ctypes.c_int, [_P, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, _P, _P]),
     "sp_wino3x3_fwd": (ctypes.c_int, [_P, _P, _P, _I64, ctypes.c_int32, ctypes.c_int32,

@@ -6,7 +6,11 @@
 // 17 GiB per layer at configs[3]'s batch) never reaches HBM: every kernel keeps a 16 x 16
 // score block in registers (the FlashAttention recurrence, exact fp32 MFMA accumulation).
 //
-// Layouts: q, k, v, out, dout, dq, dk, dv are [bh][n][d] row-major; lse, delta are [bh][n].
+// Layouts: row i of head h of batch b of q, k, v, dq, dk, dv starts at (b n + i) rs + h d, of
+// out and dout at (b n + i) ro + h d: the token-major [b][n][heads x d] activations the
+// projections read and write (rs = 3 heads d when q, k, v are the thirds of one fused
+// projection), so no head split / merge copies exist.  heads = 1, rs = ro = d is the plain
+// [bh][n][d] layout.  lse, delta are [bh][n].
 // MFMA operand maps (16x16x4 f32): A[m = l & 15][k = l >> 4], B[k = l >> 4][n = l & 15],
 // C[row = 4 (l >> 4) + i][col = l & 15], i = 0..3 (cdna_hip_programming.md §3).
 //
@@ -27,6 +31,7 @@
 
 #include "sp_common.h"
 
+#include <algorithm>
 #include <cmath>
 
 namespace sp {
@@ -61,15 +66,36 @@ struct AtStage {
     float4 r[AtGeo<D>::NF4];
 };
 
+// rows >= lim (past the last key of a cross-attention context) are staged as zeros
 template <int D>
-__device__ __forceinline__ void at_load(const float* __restrict__ src, AtStage<D>& st) {
+__device__ __forceinline__ void at_load(const float* __restrict__ src, int rs, AtStage<D>& st,
+                                        int lim = 1 << 30) {
     using G = AtGeo<D>;
 #pragma unroll
     for (int j = 0; j < G::NF4; ++j) {
         const int i = threadIdx.x + j * kBlock;
-        if (i < G::SB * D / 4) st.r[j] = reinterpret_cast<const float4*>(src)[i];
+        if (i < G::SB * D / 4) {
+            const int row = (4 * i) / D, col = 4 * i - row * D;
+            st.r[j] = row < lim ? *reinterpret_cast<const float4*>(src + (int64_t)row * rs + col)
+                                : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
     }
 }
+
+// first element of head h = bh % heads of batch bh / heads, in a layout of row stride rs
+__device__ __forceinline__ int64_t at_base(int bh, int heads, int n, int rs, int d) {
+    const int b = bh / heads;
+    return (int64_t)b * n * rs + (int64_t)(bh - b * heads) * d;
+}
+
+// The keys / values: m rows of stride rs per sample; shared = one sample for the whole batch
+// (cross-attention to one context row broadcast over the batch)
+struct AtKV {
+    int m, rs, shared;
+    __device__ __forceinline__ int64_t base(int bh, int heads, int d) const {
+        return at_base(shared ? bh % heads : bh, heads, m, rs, d);
+    }
+};
 
 template <int D>
 __device__ __forceinline__ void at_store(float* dst, const AtStage<D>& st) {
@@ -102,23 +128,26 @@ __device__ __forceinline__ float at_colsum(float v) {
 template <int D>
 __global__ __launch_bounds__(kBlock) void k_attn_fwd(const float* __restrict__ q,
                                                      const float* __restrict__ k,
-                                                     const float* __restrict__ v, int n, float sl2,
+                                                     const float* __restrict__ v, int n, int heads,
+                                                     int rs, int ro, AtKV kv, float sl2,
                                                      float* __restrict__ out,
                                                      float* __restrict__ lse) {
     using G = AtGeo<D>;
     __shared__ __attribute__((aligned(16))) float Ks[G::SB * G::DP + G::PAD];
     __shared__ __attribute__((aligned(16))) float Vs[G::SB * G::DP + G::PAD];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, li = lane & 15, kl = lane >> 4;
-    const int64_t base = (int64_t)blockIdx.y * n * D;
+    const int64_t base = at_base(blockIdx.y, heads, n, rs, D);
     const int q0 = blockIdx.x * G::WB + wv * G::QT * 16;
-    const float* __restrict__ kb = k + base;
-    const float* __restrict__ vb = v + base;
+    const int64_t kvb = kv.base(blockIdx.y, heads, D);
+    const float* __restrict__ kb = k + kvb;
+    const float* __restrict__ vb = v + kvb;
+    const int m_keys = kv.m;
 
     float qr[G::QT][G::DS];  // B operand of S^T = K Q^T: Q[q][4s + kl] * scale * log2 e
 #pragma unroll
     for (int t = 0; t < G::QT; ++t)
 #pragma unroll
-        for (int s = 0; s < G::DS; ++s) qr[t][s] = q[base + (int64_t)(q0 + 16 * t + li) * D + 4 * s + kl] * sl2;
+        for (int s = 0; s < G::DS; ++s) qr[t][s] = q[base + (int64_t)(q0 + 16 * t + li) * rs + 4 * s + kl] * sl2;
     at_f4 o[G::QT][G::DT];
     float m[G::QT], l[G::QT];
 #pragma unroll
@@ -129,20 +158,23 @@ __global__ __launch_bounds__(kBlock) void k_attn_fwd(const float* __restrict__ q
     }
 
     AtStage<D> sk, sv;
-    at_load<D>(kb, sk);
-    at_load<D>(vb, sv);
-    const int nst = n / G::SB;
+    const int rk = kv.rs;
+    at_load<D>(kb, rk, sk, m_keys);
+    at_load<D>(vb, rk, sv, m_keys);
+    const int nst = (m_keys + G::SB - 1) / G::SB;
     for (int st = 0; st < nst; ++st) {
         __syncthreads();  // the previous stage's reads are done
         at_store<D>(Ks, sk);
         at_store<D>(Vs, sv);
         __syncthreads();
         if (st + 1 < nst) {  // next stage's rows in flight during this stage's MFMAs
-            at_load<D>(kb + (int64_t)(st + 1) * G::SB * D, sk);
-            at_load<D>(vb + (int64_t)(st + 1) * G::SB * D, sv);
+            at_load<D>(kb + (int64_t)(st + 1) * G::SB * rk, rk, sk, m_keys - (st + 1) * G::SB);
+            at_load<D>(vb + (int64_t)(st + 1) * G::SB * rk, rk, sv, m_keys - (st + 1) * G::SB);
         }
 #pragma unroll
         for (int sb = 0; sb < G::SB / 16; ++sb) {
+            const int key0 = st * G::SB + sb * 16;
+            if (key0 >= m_keys) break;  // past the context's last key (uniform)
             const float* kr = Ks + (sb * 16 + li) * G::DP + kl;       // K[key li][4s + kl]
             at_f4 s[G::QT];
 #pragma unroll
@@ -152,6 +184,13 @@ __global__ __launch_bounds__(kBlock) void k_attn_fwd(const float* __restrict__ q
                 const float a = kr[4 * ss];
 #pragma unroll
                 for (int t = 0; t < G::QT; ++t) s[t] = at_mfma(a, qr[t][ss], s[t]);
+            }
+            if (key0 + 16 > m_keys) {  // keys past the last one score -inf (p = 0)
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+                    if (key0 + 4 * kl + i >= m_keys)
+#pragma unroll
+                        for (int t = 0; t < G::QT; ++t) s[t][i] = -INFINITY;
             }
             float p[G::QT][4];
 #pragma unroll
@@ -187,7 +226,7 @@ __global__ __launch_bounds__(kBlock) void k_attn_fwd(const float* __restrict__ q
         const float tot = at_colsum(l[t]);
         const float inv = 1.f / tot;
         const int qq = q0 + 16 * t + li;
-        float* orow = out + base + (int64_t)qq * D;
+        float* orow = out + at_base(blockIdx.y, heads, n, ro, D) + (int64_t)qq * ro;
 #pragma unroll
         for (int dt = 0; dt < G::DT; ++dt) {
             const int d0 = dt * 16 + 4 * kl;
@@ -202,11 +241,14 @@ __global__ __launch_bounds__(kBlock) void k_attn_fwd(const float* __restrict__ q
 template <int D>
 __global__ __launch_bounds__(kBlock) void k_attn_delta(const float* __restrict__ out,
                                                        const float* __restrict__ dout, int64_t rows,
+                                                       int n, int heads, int ro,
                                                        float* __restrict__ delta) {
-    const int64_t r = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    const int64_t r = (int64_t)blockIdx.x * kBlock + threadIdx.x;  // (bh, token) = (r / n, r % n)
     if (r >= rows) return;
-    const float4* a = reinterpret_cast<const float4*>(out + r * D);
-    const float4* b = reinterpret_cast<const float4*>(dout + r * D);
+    const int bh = static_cast<int>(r / n), tok = static_cast<int>(r - (int64_t)bh * n);
+    const int64_t off = at_base(bh, heads, n, ro, D) + (int64_t)tok * ro;
+    const float4* a = reinterpret_cast<const float4*>(out + off);
+    const float4* b = reinterpret_cast<const float4*>(dout + off);
     float s = 0.f;
 #pragma unroll
     for (int j = 0; j < D / 4; ++j) {
@@ -225,24 +267,29 @@ __global__ __launch_bounds__(kBlock) void k_attn_dq(const float* __restrict__ q,
                                                     const float* __restrict__ dout,
                                                     const float* __restrict__ lse,
                                                     const float* __restrict__ delta, int n,
-                                                    float sl2, float scale, float* __restrict__ dq) {
+                                                    int heads, int rs, int ro, AtKV kv, float sl2,
+                                                    float scale, float* __restrict__ dq) {
     using G = AtGeo<D>;
     __shared__ __attribute__((aligned(16))) float Ks[G::SB * G::DP + G::PAD];
     __shared__ __attribute__((aligned(16))) float Vs[G::SB * G::DP + G::PAD];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, li = lane & 15, kl = lane >> 4;
-    const int64_t base = (int64_t)blockIdx.y * n * D;
+    const int64_t base = at_base(blockIdx.y, heads, n, rs, D);
+    const int64_t obase = at_base(blockIdx.y, heads, n, ro, D);
     const int q0 = blockIdx.x * G::WB + wv * G::QT * 16;
-    const float* __restrict__ kb = k + base;
-    const float* __restrict__ vb = v + base;
+    const int64_t kvb = kv.base(blockIdx.y, heads, D);
+    const float* __restrict__ kb = k + kvb;
+    const float* __restrict__ vb = v + kvb;
+    const int m_keys = kv.m;
 
     float qr[G::QT][G::DS], dr[G::QT][G::DS], ls[G::QT], de[G::QT];
 #pragma unroll
     for (int t = 0; t < G::QT; ++t) {
-        const int64_t row = base + (int64_t)(q0 + 16 * t + li) * D;
+        const int64_t row = base + (int64_t)(q0 + 16 * t + li) * rs;
+        const int64_t orow = obase + (int64_t)(q0 + 16 * t + li) * ro;
 #pragma unroll
         for (int s = 0; s < G::DS; ++s) {
             qr[t][s] = q[row + 4 * s + kl] * sl2;
-            dr[t][s] = dout[row + 4 * s + kl];
+            dr[t][s] = dout[orow + 4 * s + kl];
         }
         const int64_t r = (int64_t)blockIdx.y * n + q0 + 16 * t + li;
         ls[t] = lse[r] * AT_LOG2E;
@@ -255,20 +302,23 @@ __global__ __launch_bounds__(kBlock) void k_attn_dq(const float* __restrict__ q,
         for (int dt = 0; dt < G::DT; ++dt) acc[t][dt] = at_f4{0.f, 0.f, 0.f, 0.f};
 
     AtStage<D> sk, sv;
-    at_load<D>(kb, sk);
-    at_load<D>(vb, sv);
-    const int nst = n / G::SB;
+    const int rk = kv.rs;
+    at_load<D>(kb, rk, sk, m_keys);
+    at_load<D>(vb, rk, sv, m_keys);
+    const int nst = (m_keys + G::SB - 1) / G::SB;
     for (int st = 0; st < nst; ++st) {
         __syncthreads();
         at_store<D>(Ks, sk);
         at_store<D>(Vs, sv);
         __syncthreads();
         if (st + 1 < nst) {
-            at_load<D>(kb + (int64_t)(st + 1) * G::SB * D, sk);
-            at_load<D>(vb + (int64_t)(st + 1) * G::SB * D, sv);
+            at_load<D>(kb + (int64_t)(st + 1) * G::SB * rk, rk, sk, m_keys - (st + 1) * G::SB);
+            at_load<D>(vb + (int64_t)(st + 1) * G::SB * rk, rk, sv, m_keys - (st + 1) * G::SB);
         }
 #pragma unroll
         for (int sb = 0; sb < G::SB / 16; ++sb) {
+            const int key0 = st * G::SB + sb * 16;
+            if (key0 >= m_keys) break;  // past the context's last key (uniform)
             const float* kr = Ks + (sb * 16 + li) * G::DP + kl;
             const float* vr = Vs + (sb * 16 + li) * G::DP + kl;
             at_f4 s[G::QT], dp[G::QT];
@@ -282,6 +332,13 @@ __global__ __launch_bounds__(kBlock) void k_attn_dq(const float* __restrict__ q,
                     s[t] = at_mfma(a, qr[t][ss], s[t]);
                     dp[t] = at_mfma(b, dr[t][ss], dp[t]);
                 }
+            }
+            if (key0 + 16 > m_keys) {  // keys past the last one: p = 0
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+                    if (key0 + 4 * kl + i >= m_keys)
+#pragma unroll
+                        for (int t = 0; t < G::QT; ++t) s[t][i] = -INFINITY;
             }
             float ds[G::QT][4];
 #pragma unroll
@@ -302,7 +359,7 @@ __global__ __launch_bounds__(kBlock) void k_attn_dq(const float* __restrict__ q,
     }
 #pragma unroll
     for (int t = 0; t < G::QT; ++t) {
-        float* drow = dq + base + (int64_t)(q0 + 16 * t + li) * D;
+        float* drow = dq + base + (int64_t)(q0 + 16 * t + li) * rs;
 #pragma unroll
         for (int dt = 0; dt < G::DT; ++dt) {
             const int d0 = dt * 16 + 4 * kl;
@@ -324,23 +381,23 @@ __global__ __launch_bounds__(kBlock) void k_attn_dkv(const float* __restrict__ q
                                                      const float* __restrict__ dout,
                                                      const float* __restrict__ lse,
                                                      const float* __restrict__ delta, int n,
-                                                     float sl2, float scale,
+                                                     int heads, int rs, int ro, float sl2, float scale,
                                                      float* __restrict__ dk, float* __restrict__ dv) {
     using G = AtGeo<D>;
     __shared__ __attribute__((aligned(16))) float Qs[G::SB * G::DP + G::PAD];
     __shared__ __attribute__((aligned(16))) float Os[G::SB * G::DP + G::PAD];  // dO rows
     __shared__ float Ls[G::SB], Es[G::SB];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, li = lane & 15, kl = lane >> 4;
-    const int64_t base = (int64_t)blockIdx.y * n * D;
+    const int64_t base = at_base(blockIdx.y, heads, n, rs, D);
     const int64_t rbase = (int64_t)blockIdx.y * n;
     const int k0 = blockIdx.x * G::WB + wv * G::QT * 16;
     const float* __restrict__ qb = q + base;
-    const float* __restrict__ ob = dout + base;
+    const float* __restrict__ ob = dout + at_base(blockIdx.y, heads, n, ro, D);
 
     float kr[G::QT][G::DS], vr[G::QT][G::DS];  // B operands: K[key li][4s + kl] * sl2, V[..]
 #pragma unroll
     for (int t = 0; t < G::QT; ++t) {
-        const int64_t row = base + (int64_t)(k0 + 16 * t + li) * D;
+        const int64_t row = base + (int64_t)(k0 + 16 * t + li) * rs;
 #pragma unroll
         for (int s = 0; s < G::DS; ++s) {
             kr[t][s] = k[row + 4 * s + kl] * sl2;
@@ -356,8 +413,8 @@ __global__ __launch_bounds__(kBlock) void k_attn_dkv(const float* __restrict__ q
     AtStage<D> sq, so;
     float sl = 0.f, se = 0.f;
     auto load_rows = [&](int st) {
-        at_load<D>(qb + (int64_t)st * G::SB * D, sq);
-        at_load<D>(ob + (int64_t)st * G::SB * D, so);
+        at_load<D>(qb + (int64_t)st * G::SB * rs, rs, sq);
+        at_load<D>(ob + (int64_t)st * G::SB * ro, ro, so);
         if (threadIdx.x < G::SB) {
             sl = lse[rbase + st * G::SB + threadIdx.x] * AT_LOG2E;
             se = delta[rbase + st * G::SB + threadIdx.x];
@@ -418,7 +475,7 @@ __global__ __launch_bounds__(kBlock) void k_attn_dkv(const float* __restrict__ q
     }
 #pragma unroll
     for (int t = 0; t < G::QT; ++t) {
-        const int64_t row = base + (int64_t)(k0 + 16 * t + li) * D;
+        const int64_t row = base + (int64_t)(k0 + 16 * t + li) * rs;
 #pragma unroll
         for (int dt = 0; dt < G::DT; ++dt) {
             const int d0 = dt * 16 + 4 * kl;
@@ -434,31 +491,31 @@ __global__ __launch_bounds__(kBlock) void k_attn_dkv(const float* __restrict__ q
 }
 
 template <int D>
-static int attn_fwd_d(const float* q, const float* k, const float* v, int64_t bh, int64_t n,
-                      float scale, float* out, float* lse, hipStream_t s) {
+static int attn_fwd_d(const float* q, const float* k, const float* v, int64_t bh, int heads, int64_t n,
+                      int rs, int ro, AtKV kv, float scale, float* out, float* lse, hipStream_t s) {
     using G = AtGeo<D>;
-    const double flops = 4.0 * bh * n * n * D;
+    const double flops = 4.0 * bh * n * kv.m * D;
     launch_w(0, flops, k_attn_fwd<D>, dim3(static_cast<unsigned>(n / G::WB), static_cast<unsigned>(bh)),
-             dim3(kBlock), s, q, k, v, static_cast<int>(n), scale * AT_LOG2E, out, lse);
+             dim3(kBlock), s, q, k, v, static_cast<int>(n), heads, rs, ro, kv, scale * AT_LOG2E, out, lse);
     return check_launch("sp_attention_fwd");
 }
 
 template <int D>
 static int attn_bwd_d(const float* q, const float* k, const float* v, const float* out,
-                      const float* dout, const float* lse, int64_t bh, int64_t n, float scale,
-                      float* delta, float* dq, float* dk, float* dv, hipStream_t s) {
+                      const float* dout, const float* lse, int64_t bh, int heads, int64_t n, int rs, int ro,
+                      AtKV kv, float scale, float* delta, float* dq, float* dk, float* dv, hipStream_t s) {
     using G = AtGeo<D>;
     const int64_t rows = bh * n;
     launch(0, k_attn_delta<D>, dim3(static_cast<unsigned>((rows + kBlock - 1) / kBlock)), dim3(kBlock), s,
-           out, dout, rows, delta);
+           out, dout, rows, static_cast<int>(n), heads, ro, delta);
     const dim3 grid(static_cast<unsigned>(n / G::WB), static_cast<unsigned>(bh));
     const float sl2 = scale * AT_LOG2E;
     if (dq) launch(0, k_attn_dq<D>, grid, dim3(kBlock), s, q, k, v, dout, lse, (const float*)delta,
-                   static_cast<int>(n), sl2, scale, dq);
+                   static_cast<int>(n), heads, rs, ro, kv, sl2, scale, dq);
     if (dk || dv) {
         if (!dk || !dv) return SP_EINVAL;
         launch(0, k_attn_dkv<D>, grid, dim3(kBlock), s, q, k, v, dout, lse, (const float*)delta,
-               static_cast<int>(n), sl2, scale, dk, dv);
+               static_cast<int>(n), heads, rs, ro, sl2, scale, dk, dv);
     }
     return check_launch("sp_attention_bwd");
 }
@@ -479,30 +536,73 @@ int sp_attention_supported(int64_t bh, int64_t n, int64_t m, int32_t d) {
     }
 }
 
+int sp_attention_mh_supported(int64_t batch, int32_t heads, int64_t n, int64_t m, int32_t d) {
+    if (batch <= 0 || heads <= 0 || batch * heads > 65535 || n <= 0 || m <= 0 || n > (int64_t(1) << 24) ||
+        m > (int64_t(1) << 24))
+        return 0;
+    switch (d) {
+        case 40: return n % AtGeo<40>::WB == 0 && (m != n || n % AtGeo<40>::SB == 0);
+        case 80: return n % AtGeo<80>::WB == 0 && (m != n || n % AtGeo<80>::SB == 0);
+        case 160: return n % AtGeo<160>::WB == 0 && (m != n || n % AtGeo<160>::SB == 0);
+        default: return 0;
+    }
+}
+
+static bool mh_ok(int64_t batch, int32_t heads, int64_t n, int64_t m, int32_t d, int32_t rs, int32_t ro,
+                  int32_t rs_kv, int64_t kv_batch) {
+    const int32_t c = heads * d;
+    return sp_attention_mh_supported(batch, heads, n, m, d) && rs >= c && ro >= c && rs_kv >= c &&
+           rs % 4 == 0 && ro % 4 == 0 && rs_kv % 4 == 0 && (kv_batch == 1 || kv_batch == batch) &&
+           batch * n * (int64_t)std::max(rs, ro) < (int64_t(1) << 40);
+}
+
+int sp_attention_fwd_mh(const float* q, const float* k, const float* v, int64_t batch, int32_t heads,
+                        int64_t n, int64_t m, int32_t d, int32_t rs, int32_t rs_kv, int64_t kv_batch,
+                        int32_t ro, float scale, float* out, float* lse, sp_stream_t stream) {
+    if (!mh_ok(batch, heads, n, m, d, rs, ro, rs_kv, kv_batch) || !q || !k || !v || !out || !lse)
+        return SP_EINVAL;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const int64_t bh = batch * heads;
+    const AtKV kv{static_cast<int>(m), rs_kv, kv_batch == 1 && batch > 1};
+    switch (d) {
+        case 40: return attn_fwd_d<40>(q, k, v, bh, heads, n, rs, ro, kv, scale, out, lse, s);
+        case 80: return attn_fwd_d<80>(q, k, v, bh, heads, n, rs, ro, kv, scale, out, lse, s);
+        default: return attn_fwd_d<160>(q, k, v, bh, heads, n, rs, ro, kv, scale, out, lse, s);
+    }
+}
+
+int sp_attention_bwd_mh(const float* q, const float* k, const float* v, const float* out,
+                        const float* dout, const float* lse, int64_t batch, int32_t heads, int64_t n,
+                        int64_t m, int32_t d, int32_t rs, int32_t rs_kv, int64_t kv_batch, int32_t ro,
+                        float scale, float* delta, float* dq, float* dk, float* dv, sp_stream_t stream) {
+    if (!mh_ok(batch, heads, n, m, d, rs, ro, rs_kv, kv_batch) || !q || !k || !v || !out || !dout || !lse ||
+        !delta)
+        return SP_EINVAL;
+    // dk / dv only for self-attention (the same rows, the same geometry)
+    if ((dk || dv) && (m != n || rs_kv != rs || kv_batch != batch)) return SP_EINVAL;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const int64_t bh = batch * heads;
+    const AtKV kv{static_cast<int>(m), rs_kv, kv_batch == 1 && batch > 1};
+    switch (d) {
+        case 40: return attn_bwd_d<40>(q, k, v, out, dout, lse, bh, heads, n, rs, ro, kv, scale, delta, dq, dk, dv, s);
+        case 80: return attn_bwd_d<80>(q, k, v, out, dout, lse, bh, heads, n, rs, ro, kv, scale, delta, dq, dk, dv, s);
+        default: return attn_bwd_d<160>(q, k, v, out, dout, lse, bh, heads, n, rs, ro, kv, scale, delta, dq, dk, dv, s);
+    }
+}
+
 int sp_attention_fwd(const float* q, const float* k, const float* v, int64_t bh, int64_t n,
                      int32_t d, float scale, float* out, float* lse, sp_stream_t stream) {
-    if (!sp_attention_supported(bh, n, n, d) || !q || !k || !v || !out || !lse) return SP_EINVAL;
-    hipStream_t s = static_cast<hipStream_t>(stream);
-    switch (d) {
-        case 40: return attn_fwd_d<40>(q, k, v, bh, n, scale, out, lse, s);
-        case 80: return attn_fwd_d<80>(q, k, v, bh, n, scale, out, lse, s);
-        default: return attn_fwd_d<160>(q, k, v, bh, n, scale, out, lse, s);
-    }
+    if (!sp_attention_supported(bh, n, n, d)) return SP_EINVAL;
+    return sp_attention_fwd_mh(q, k, v, bh, 1, n, n, d, d, d, bh, d, scale, out, lse, stream);
 }
 
 int sp_attention_bwd(const float* q, const float* k, const float* v, const float* out,
                      const float* dout, const float* lse, int64_t bh, int64_t n, int32_t d,
                      float scale, float* delta, float* dq, float* dk, float* dv,
                      sp_stream_t stream) {
-    if (!sp_attention_supported(bh, n, n, d) || !q || !k || !v || !out || !dout || !lse ||
-        !delta)
-        return SP_EINVAL;
-    hipStream_t s = static_cast<hipStream_t>(stream);
-    switch (d) {
-        case 40: return attn_bwd_d<40>(q, k, v, out, dout, lse, bh, n, scale, delta, dq, dk, dv, s);
-        case 80: return attn_bwd_d<80>(q, k, v, out, dout, lse, bh, n, scale, delta, dq, dk, dv, s);
-        default: return attn_bwd_d<160>(q, k, v, out, dout, lse, bh, n, scale, delta, dq, dk, dv, s);
-    }
+    if (!sp_attention_supported(bh, n, n, d)) return SP_EINVAL;
+    return sp_attention_bwd_mh(q, k, v, out, dout, lse, bh, 1, n, n, d, d, d, bh, d, scale, delta, dq, dk, dv,
+                               stream);
 }
 
 }  // extern "C"

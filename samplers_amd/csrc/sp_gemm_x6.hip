@@ -36,7 +36,8 @@ typedef __attribute__((address_space(3))) void lds_void_g;
 #define G6_SCHED 1  // hand-ordered issue within the k-step (see k_gemm_x6)
 #endif
 #ifndef G6_EXP
-#define G6_EXP 0  // diagnostics only (wrong results, timing): 1 no MFMAs, 2 no split, 3 no loads
+#define G6_EXP 0  // diagnostics only (wrong results, timing): 1 no MFMAs, 2 no split, 3 no loads,
+                  // 4 no output stores
 #endif
 constexpr int G6_CO = 128;     // output channels per workgroup
 constexpr int G6_PX = 256;     // pixels per workgroup
@@ -54,8 +55,10 @@ struct G6Geom {
     const float* res;     // nullable, shaped like y1 (o2 == 0 only)
     int c1, c2, o1, o2, hw;
     int ntiles, cob, ptiles, nsteps;
-    // token-major mode (k_gemm_x6<true>, nn.Linear on [tokens][features]): x1 is [hw][c1],
-    // y1 is [hw][o1] with o1 % 32 (W's rows padded to 128 with zeros), one input and output
+    int tokens;           // token-major operands: rows of x1 / y1 (images x hw)
+    // token-major operands (k_gemm_x6<LTM, STM>, nn.Linear on [tokens][features]): x1 is
+    // [tokens][c1] and / or y1 [tokens][o1] with o1 % 32 (W's rows padded to 128 with zeros),
+    // one input and output
 };
 
 __device__ __forceinline__ void g6_split(float v, unsigned& h, unsigned& m, unsigned& l) {
@@ -107,10 +110,10 @@ __device__ __forceinline__ void g6_dma_x(const G6Geom& g, int n, int p0, int kst
 }
 
 // token-major X (nn.Linear input [tokens][c1]) -> LDS slot [256 tokens][16 ch] fp32: load i of
-// wave wv covers tokens 16 (2 wv + i) .. +15, lane l: token + (l >> 2), channels 4 (l & 3) .. +3
+// wave wv covers tokens p0 + 16 (2 wv + i) .. +15, lane l: token + (l >> 2), channels 4 (l & 3) .. +3
 __device__ __forceinline__ void g6_dma_x_tm(const G6Geom& g, int p0, int kstep, int wv, int lane,
                                             unsigned char* slot) {
-    const auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(g.x1), (short)0, g.hw * g.c1 * 4,
+    const auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(g.x1), (short)0, g.tokens * g.c1 * 4,
                                                       0x00020000);
     const int vo = ((lane >> 2) * g.c1 + 4 * (lane & 3)) * 4;
 #pragma unroll
@@ -197,6 +200,7 @@ __device__ __forceinline__ void g6_epilogue(const G6Geom& g, int n, int cb, cons
 #pragma unroll
     for (int a = 0; a < 2; ++a) {
         const int co0 = cb * G6_CO + 32 * (2 * ch + a);  // first channel of the 32-block
+        if (co0 >= g.o1 + g.o2) continue;  // padded rows of W (uniform)
         const bool second = co0 >= g.o1;
         float* yb = second ? g.y2 + ((int64_t)n * g.o2 + (co0 - g.o1)) * g.hw
                            : g.y1 + ((int64_t)n * g.o1 + co0) * g.hw;
@@ -228,6 +232,9 @@ __device__ __forceinline__ void g6_epilogue(const G6Geom& g, int n, int cb, cons
                 const float b1 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, bl), c + 4));
                 const int cc = c + 4 * (lane >> 5);
                 const float y = (TWO ? acc[a][b][q] + acs[a][b][q] : acc[a][b][q]) + ((lane >> 5) ? b1 : b0) + rv[q];
+#if G6_EXP == 4
+                if (g.hw >= 0) continue;  // never true at run time: the stores are skipped, all math kept
+#endif
                 __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(y), ors, vo + cc * g.hw * 4, 0, 0);
             }
             __builtin_amdgcn_sched_barrier(0);
@@ -240,9 +247,10 @@ __device__ __forceinline__ void g6_epilogue(const G6Geom& g, int n, int cb, cons
 // each register row is 32 consecutive features of one token (128 contiguous bytes)
 __device__ __forceinline__ void g6_epilogue_tm(const G6Geom& g, const G6Pos& ps, int ch, int pq, int lane,
                                                const f32x16 (&acc)[2][2], const f32x16 (&acs)[2][2]) {
-    const auto ors = __builtin_amdgcn_make_buffer_rsrc(g.y1, (short)0, g.hw * g.o1 * 4, 0x00020000);
+    const auto ors = __builtin_amdgcn_make_buffer_rsrc(g.y1, (short)0, g.tokens * g.o1 * 4, 0x00020000);
     const auto rrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(g.res ? g.res : g.y1), (short)0,
-                                                       g.res ? g.hw * g.o1 * 4 : 0, 0x00020000);
+                                                       g.res ? g.tokens * g.o1 * 4 : 0, 0x00020000);
+    const int tok0 = ps.n * g.hw + ps.p0;  // first token row of the tile (image n's plane)
 #pragma unroll
     for (int a = 0; a < 2; ++a) {
         const int o = ps.cb * G6_CO + 32 * (2 * ch + a) + (lane & 31);
@@ -250,7 +258,7 @@ __device__ __forceinline__ void g6_epilogue_tm(const G6Geom& g, const G6Pos& ps,
         const float bv = g.bias ? g.bias[o] : 0.f;
 #pragma unroll
         for (int b = 0; b < 2; ++b) {
-            const int t0 = ps.p0 + pq * 64 + b * 32 + 4 * (lane >> 5);
+            const int t0 = tok0 + pq * 64 + b * 32 + 4 * (lane >> 5);
             float rv[16];
 #pragma unroll
             for (int q = 0; q < 16; ++q) rv[q] = 0.f;
@@ -278,7 +286,10 @@ __device__ __forceinline__ void g6_epilogue_tm(const G6Geom& g, const G6Pos& ps,
 // Eight waves, two per SIMD: one wave's MFMAs cover the other's LDS waits and split work.
 constexpr int G6_THREADS = 512;
 
-template <bool TM>
+// LTM / STM: X read token-major ([tokens][k]) / Y written token-major ([tokens][m]); else the
+// per-image channel-major planes ([n][k][hw] / [n][m][hw]).  Tokens of image n are rows
+// n hw .. n hw + hw - 1.
+template <bool LTM, bool STM>
 __global__ __launch_bounds__(G6_THREADS, 1) void k_gemm_x6(G6Geom g) {
     __shared__ __attribute__((aligned(16))) unsigned char xraw[4][G6_KC * G6_PX * 4];
     __shared__ __attribute__((aligned(16))) unsigned char xs[2][G6_XB];
@@ -305,7 +316,7 @@ __global__ __launch_bounds__(G6_THREADS, 1) void k_gemm_x6(G6Geom g) {
     };
     auto dma_x = [&]() {
         if (cx.j < J) {
-            if constexpr (TM) g6_dma_x_tm(g, cx.ps.p0, cx.s, wv, lane, xraw[cx.slot]);
+            if constexpr (LTM) g6_dma_x_tm(g, cx.ps.n * g.hw + cx.ps.p0, cx.s, wv, lane, xraw[cx.slot]);
             else g6_dma_x(g, cx.ps.n, cx.ps.p0, cx.s, wv, lane, xraw[cx.slot]);
         }
         advance(cx, 4);
@@ -322,7 +333,7 @@ __global__ __launch_bounds__(G6_THREADS, 1) void k_gemm_x6(G6Geom g) {
     dma_x();
     __builtin_amdgcn_s_waitcnt(g6_vmcnt(0));
     __builtin_amdgcn_s_barrier();
-    if constexpr (TM) g6_split_x_tm(xraw[0], xs[0], tid);
+    if constexpr (LTM) g6_split_x_tm(xraw[0], xs[0], tid);
     else g6_split_x(xraw[0], xs[0], tid);
     __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
     __builtin_amdgcn_s_barrier();
@@ -360,7 +371,7 @@ __global__ __launch_bounds__(G6_THREADS, 1) void k_gemm_x6(G6Geom g) {
             }
 #if G6_EXP != 2
             // X(j + 1)'s split (unconditional: past the stream's end it rewrites an unused slot)
-            if constexpr (TM) g6_split_x_tm(xraw[xslot1], xs[(j + 1) & 1], tid);
+            if constexpr (LTM) g6_split_x_tm(xraw[xslot1], xs[(j + 1) & 1], tid);
             else g6_split_x(xraw[xslot1], xs[(j + 1) & 1], tid);
 #endif
 #if G6_EXP != 1
@@ -372,7 +383,7 @@ __global__ __launch_bounds__(G6_THREADS, 1) void k_gemm_x6(G6Geom g) {
                 for (int b = 0; b < 2; ++b)
 #pragma unroll
                     for (int a = 0; a < 2; ++a) {
-                        if constexpr (TM)  // tokens as the MFMA's rows: features contiguous in C
+                        if constexpr (STM)  // tokens as the MFMA's rows: features contiguous in C
                             (e == 5 ? acc : acs)[a][b] = g6_mfma(fv[b][TV[e]], fu[a][TU[e]], (e == 5 ? acc : acs)[a][b]);
                         else
                             (e == 5 ? acc : acs)[a][b] = g6_mfma(fu[a][TU[e]], fv[b][TV[e]], (e == 5 ? acc : acs)[a][b]);
@@ -400,7 +411,7 @@ __global__ __launch_bounds__(G6_THREADS, 1) void k_gemm_x6(G6Geom g) {
             xslot1 = xslot1 == 3 ? 0 : xslot1 + 1;
         }
         const G6Pos ps = g6_pos(g, b0 + tw * G);
-        if constexpr (TM) g6_epilogue_tm(g, ps, ch, pq, lane, acc, acs);
+        if constexpr (STM) g6_epilogue_tm(g, ps, ch, pq, lane, acc, acs);
         else {
             const int pxb[2] = {ps.p0 + pq * 64, ps.p0 + pq * 64 + 32};
             g6_epilogue(g, ps.n, ps.cb, pxb, ch, lane, acc, acs);
@@ -500,7 +511,8 @@ int sp_gemm_x6(const float* x1, int32_t c1, const float* x2, int32_t c2, const f
     g.ptiles = static_cast<int>(hw / G6_PX);
     g.nsteps = k / G6_KC;
     const int grid = static_cast<int>(std::min<int64_t>(tiles, g6_cu_count()));
-    launch(0, k_gemm_x6<false>, dim3(grid), dim3(G6_THREADS), static_cast<hipStream_t>(stream), g);
+    g.tokens = 0;
+    launch(0, k_gemm_x6<false, false>, dim3(grid), dim3(G6_THREADS), static_cast<hipStream_t>(stream), g);
     return check_launch("sp_gemm_x6");
 }
 
@@ -530,9 +542,49 @@ int sp_linear_x6(const float* x, const float* wp, const float* bias, const float
     g.cob = cob;
     g.ptiles = static_cast<int>(tokens / G6_PX);  // one "image" of all tokens
     g.nsteps = k / G6_KC;
+    g.tokens = static_cast<int>(tokens);
     const int grid = static_cast<int>(std::min<int64_t>(tiles, g6_cu_count()));
-    launch(0, k_gemm_x6<true>, dim3(grid), dim3(G6_THREADS), static_cast<hipStream_t>(stream), g);
+    launch(0, k_gemm_x6<true, true>, dim3(grid), dim3(G6_THREADS), static_cast<hipStream_t>(stream), g);
     return check_launch("sp_linear_x6");
+}
+
+int sp_gemm_x6_layout_supported(int64_t n, int64_t hw, int32_t k, int32_t m) {
+    return n >= 0 && hw >= G6_PX && hw % G6_PX == 0 && k >= G6_KC && k % G6_KC == 0 && m >= 32 &&
+           m % 32 == 0 && n * hw * (int64_t)std::max(k, m) * 4 < (int64_t(1) << 31) &&
+           n * hw / G6_PX * ((m + G6_CO - 1) / G6_CO) < (int64_t(1) << 31);
+}
+
+// 1x1 conv / linear between the two activation layouts: x [n][k][hw] (in_tm = 0) or
+// [n hw][k] (in_tm = 1), y (and res) [n][m][hw] (out_tm = 0) or [n hw][m] (out_tm = 1)
+int sp_gemm_x6_layout(const float* x, const float* wp, const float* bias, const float* res, int64_t n,
+                      int64_t hw, int32_t k, int32_t m, int32_t in_tm, int32_t out_tm, float* y,
+                      sp_stream_t stream) {
+    if (!sp_gemm_x6_layout_supported(n, hw, k, m)) return SP_EINVAL;
+    if (n == 0) return SP_OK;
+    if (!x || !wp || !y || (res && res == y) || x == y) return SP_EINVAL;
+    const int cob = (m + G6_CO - 1) / G6_CO;
+    G6Geom g = {};
+    g.x1 = x;
+    g.wp = reinterpret_cast<const unsigned short*>(wp);
+    g.y1 = y;
+    g.bias = bias;
+    g.res = res;
+    g.c1 = k;
+    g.o1 = m;
+    g.hw = static_cast<int>(hw);
+    g.ptiles = static_cast<int>(hw / G6_PX);
+    g.ntiles = static_cast<int>(n * g.ptiles * cob);
+    g.cob = cob;
+    g.nsteps = k / G6_KC;
+    g.tokens = static_cast<int>(n * hw);
+    const int grid = static_cast<int>(std::min<int64_t>(g.ntiles, g6_cu_count()));
+    const dim3 gd(grid), bd(G6_THREADS);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    if (in_tm && out_tm) launch(0, k_gemm_x6<true, true>, gd, bd, s, g);
+    else if (in_tm) launch(0, k_gemm_x6<true, false>, gd, bd, s, g);
+    else if (out_tm) launch(0, k_gemm_x6<false, true>, gd, bd, s, g);
+    else launch(0, k_gemm_x6<false, false>, gd, bd, s, g);
+    return check_launch("sp_gemm_x6_layout");
 }
 
 }  // extern "C"

@@ -143,6 +143,137 @@ class _FusedAttention(torch.autograd.Function):
         return dq, (dk if need_k else None), (dv if need_v else None)
 
 
+class _FusedQKVAttention(torch.autograd.Function):
+    """Multi-head self-attention straight on the fused projection's output ``qkv``
+    ([b][n][3 heads d]: the q, k, v thirds) into ``out`` ([b][n][heads d]), on the fused
+    kernels' strided entry points: no head split / merge copies either way; the VJP writes
+    dq, dk, dv into one [b][n][3 heads d] buffer, the fused projection's cotangent."""
+
+    @staticmethod
+    def forward(ctx, qkv: Tensor, heads: int) -> Tensor:
+        from .. import _hip
+
+        lib = _hip.load_library()
+        b, n, c3 = qkv.shape
+        c = c3 // 3
+        d = c // heads
+        scale = 1.0 / math.sqrt(d)
+        qkv = qkv.contiguous()
+        out = torch.empty(b, n, c, device=qkv.device, dtype=torch.float32)
+        lse = torch.empty(b * heads, n, device=qkv.device, dtype=torch.float32)
+        base = qkv.data_ptr()
+        _hip.check(lib.sp_attention_fwd_mh(base, base + 4 * c, base + 8 * c, b, heads, n, n, d, c3, c3, b, c,
+                                           scale, _hip.ptr(out), _hip.ptr(lse), _hip.stream_of(qkv)),
+                   "sp_attention_fwd_mh")
+        ctx.save_for_backward(qkv, out, lse)
+        ctx.heads, ctx.scale = heads, scale
+        return out
+
+    @staticmethod
+    def backward(ctx, dout: Tensor):
+        from .. import _hip
+
+        qkv, out, lse = ctx.saved_tensors
+        lib = _hip.load_library()
+        b, n, c3 = qkv.shape
+        c = c3 // 3
+        heads = ctx.heads
+        d = c // heads
+        dout = dout.contiguous()
+        dqkv = torch.empty_like(qkv)
+        delta = torch.empty(b * heads, n, device=qkv.device, dtype=torch.float32)
+        base, dbase = qkv.data_ptr(), dqkv.data_ptr()
+        _hip.check(lib.sp_attention_bwd_mh(base, base + 4 * c, base + 8 * c, _hip.ptr(out), _hip.ptr(dout),
+                                           _hip.ptr(lse), b, heads, n, n, d, c3, c3, b, c, ctx.scale,
+                                           _hip.ptr(delta), dbase, dbase + 4 * c, dbase + 8 * c,
+                                           _hip.stream_of(dout)),
+                   "sp_attention_bwd_mh")
+        return dqkv, None
+
+
+class _FusedCrossAttention(torch.autograd.Function):
+    """Multi-head cross-attention of token rows q ([b][n][heads d]) to a context's keys and
+    values ([bc][m][heads d], bc = 1: one context for the whole batch, or bc = b) on the fused
+    kernels (keys past m masked; scores never in HBM), output in the token layout; the VJP
+    is dq only (the context is a constant of the prior's call)."""
+
+    @staticmethod
+    def forward(ctx, q: Tensor, k: Tensor, v: Tensor, heads: int) -> Tensor:
+        from .. import _hip
+
+        lib = _hip.load_library()
+        b, n, c = q.shape
+        bc, m, _ = k.shape
+        d = c // heads
+        scale = 1.0 / math.sqrt(d)
+        q, k, v = q.contiguous(), k.contiguous(), v.contiguous()
+        out = torch.empty(b, n, c, device=q.device, dtype=torch.float32)
+        lse = torch.empty(b * heads, n, device=q.device, dtype=torch.float32)
+        _hip.check(lib.sp_attention_fwd_mh(_hip.ptr(q), _hip.ptr(k), _hip.ptr(v), b, heads, n, m, d, c, c, bc, c,
+                                           scale, _hip.ptr(out), _hip.ptr(lse), _hip.stream_of(q)),
+                   "sp_attention_fwd_mh")
+        ctx.save_for_backward(q, k, v, out, lse)
+        ctx.heads, ctx.scale = heads, scale
+        return out
+
+    @staticmethod
+    def backward(ctx, dout: Tensor):
+        from .. import _hip
+
+        q, k, v, out, lse = ctx.saved_tensors
+        lib = _hip.load_library()
+        b, n, c = q.shape
+        bc, m, _ = k.shape
+        heads = ctx.heads
+        dout = dout.contiguous()
+        dq = torch.empty_like(q)
+        delta = torch.empty(b * heads, n, device=q.device, dtype=torch.float32)
+        _hip.check(lib.sp_attention_bwd_mh(_hip.ptr(q), _hip.ptr(k), _hip.ptr(v), _hip.ptr(out), _hip.ptr(dout),
+                                           _hip.ptr(lse), b, heads, n, m, c // heads, c, c, bc, c, ctx.scale,
+                                           _hip.ptr(delta), _hip.ptr(dq), None, None, _hip.stream_of(dout)),
+                   "sp_attention_bwd_mh")
+        return dq, None, None, None
+
+
+def fused_cross_supported(q: Tensor, k: Tensor, heads: int) -> bool:
+    """``_FusedCrossAttention`` serves this call: fp32 device tensors, a context that needs no
+    gradient, one context row or one per sample, the kernels' head dims and query counts."""
+    if not (q.is_cuda and q.dtype == torch.float32 and k.dtype == torch.float32 and q.dim() == 3
+            and k.dim() == 3 and not k.requires_grad):
+        return False
+    if os.environ.get("SAMPLERS_AMD_LATENT_ATTN", "fused").lower() == "gemm":
+        return False
+    from .. import _hip
+
+    b, n, c = q.shape
+    bc, m, ck = k.shape
+    return (ck == c and c % heads == 0 and bc in (1, b)
+            and bool(_hip.load_library().sp_attention_mh_supported(b, heads, n, m, c // heads)))
+
+
+def fused_cross_attention(q: Tensor, k: Tensor, v: Tensor, heads: int) -> Tensor:
+    return _FusedCrossAttention.apply(q, k, v, heads)
+
+
+def fused_qkv_supported(x: Tensor, heads: int) -> bool:
+    """``_FusedQKVAttention`` serves self-attention over ``x`` ((b, n, c) fp32 on the device)
+    with this head count: the fused kernels' head dims and token counts, and at least
+    ``FUSED_BWD_MIN_TOKENS`` tokens (below that the GEMM VJP wins, see above)."""
+    if not (x.is_cuda and x.dtype == torch.float32 and x.dim() == 3):
+        return False
+    if os.environ.get("SAMPLERS_AMD_LATENT_ATTN", "fused").lower() == "gemm":
+        return False
+    from .. import _hip
+
+    b, n, c = x.shape
+    return (c % heads == 0 and n >= FUSED_BWD_MIN_TOKENS
+            and bool(_hip.load_library().sp_attention_supported(b * heads, n, n, c // heads)))
+
+
+def fused_qkv_attention(qkv: Tensor, heads: int) -> Tensor:
+    return _FusedQKVAttention.apply(qkv, heads)
+
+
 def fused_supported(q: Tensor, k: Tensor) -> bool:
     """The fused kernels serve this call (fp32 device self-attention at their head dims and
     token counts; ``SAMPLERS_AMD_LATENT_ATTN=gemm`` forces the GEMM path)."""

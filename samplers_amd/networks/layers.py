@@ -527,21 +527,24 @@ def _linear_pack(module: nn.Module, w2d: Tensor, trans: bool) -> Tensor:
 
 class _LinearX6Fn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, module, w2d):
+    def forward(ctx, x, weight, bias, module, w2d, res=None, box=None):
         lib = _hip.load_library()
         m, k = w2d.shape
         x2 = x.reshape(-1, k).contiguous()
         t = x2.shape[0]
         y = torch.empty(t, m, device=x.device, dtype=torch.float32)
+        r2 = None if res is None else res.reshape(t, m).contiguous()
         _hip.check(lib.sp_linear_x6(_hip.ptr(x2), _hip.ptr(_linear_pack(module, w2d, False)),
-                                    _hip.ptr(None if bias is None else bias.detach().contiguous()), None,
-                                    t, k, m, _hip.ptr(y), _hip.stream_of(x2)), "sp_linear_x6")
+                                    _hip.ptr(None if bias is None else bias.detach().contiguous()),
+                                    _hip.ptr(r2), t, k, m, _hip.ptr(y), _hip.stream_of(x2)), "sp_linear_x6")
         ctx.module, ctx.w2d, ctx.shape = module, w2d, x.shape
+        ctx.box = box if res is not None else None
         return y.reshape(*x.shape[:-1], m)
 
     @staticmethod
     def backward(ctx, dy):
-        """Input VJP only (the priors' weights are frozen): dx = dy W."""
+        """Input VJP only (the priors' weights are frozen): dx = dy W; the residual's gradient
+        is dy itself — handed to ``box`` (the LayerNorm VJP that adds it) when one was given."""
         lib = _hip.load_library()
         m, k = ctx.w2d.shape
         d2 = dy.reshape(-1, m).contiguous()
@@ -549,28 +552,246 @@ class _LinearX6Fn(torch.autograd.Function):
         dx = torch.empty(t, k, device=dy.device, dtype=torch.float32)
         _hip.check(lib.sp_linear_x6(_hip.ptr(d2), _hip.ptr(_linear_pack(ctx.module, ctx.w2d, True)), None, None,
                                     t, m, k, _hip.ptr(dx), _hip.stream_of(d2)), "sp_linear_x6")
-        return dx.reshape(ctx.shape), None, None, None, None
+        dres = None
+        if ctx.needs_input_grad[5]:
+            if ctx.box is not None and ctx.box.enabled:
+                ctx.box.grad = d2
+            else:
+                dres = dy
+        return dx.reshape(ctx.shape), None, None, None, None, dres, None
 
 
-def linear(x: Tensor, module: nn.Module, w2d: Tensor | None = None, bias: Tensor | None = None) -> Tensor:
-    """``F.linear(x, w2d, bias)`` (``w2d`` defaults to ``module.weight``, ``bias`` to
+def linear(x: Tensor, module: nn.Module, w2d: Tensor | None = None, bias: Tensor | None = None,
+           res: Tensor | None = None, box: "SkipGrad | None" = None) -> Tensor:
+    """``F.linear(x, w2d, bias) (+ res)`` (``w2d`` defaults to ``module.weight``, ``bias`` to
     ``module.bias``) on ``sp_linear_x6`` when x is a CUDA fp32 token-major batch whose token
-    count and widths fit its rules and the weights are frozen; hipBLASLt otherwise."""
+    count and widths fit its rules and the weights are frozen; hipBLASLt otherwise.  ``res``
+    (shaped like the output) is added in the GEMM's epilogue; its gradient goes to ``box``
+    when the residual's other consumer (a ``LayerNorm`` given the same box) adds it in its VJP."""
     w2d = module.weight if w2d is None else w2d
     bias = getattr(module, "bias", None) if bias is None else bias
     m, k = w2d.shape
     t = x.numel() // k if x.dim() else 0
     if (x.is_cuda and x.dtype == torch.float32 and not w2d.requires_grad
-            and (bias is None or not bias.requires_grad) and linear_backend() == "x6"):
+            and (bias is None or not bias.requires_grad) and linear_backend() == "x6"
+            and (res is None or (res.dtype == torch.float32 and res.numel() == t * m))):
         lib = _hip.load_library()
         if lib.sp_linear_x6_supported(t, k, m):
-            return _LinearX6Fn.apply(x, w2d, bias, module, w2d)
-    return F.linear(x, w2d, bias)
+            return _LinearX6Fn.apply(x, w2d, bias, module, w2d, res, box)
+    if box is not None:
+        box.enabled = False
+    y = F.linear(x, w2d, bias)
+    return y if res is None else y + res
+
+
+class _ProjLayoutFn(torch.autograd.Function):
+    """1x1 projection between the NCHW planes and token-major rows (``sp_gemm_x6_layout``)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, module, w2d, n, hw, in_tm, out_tm, res=None):
+        lib = _hip.load_library()
+        m, k = w2d.shape
+        xc = x.contiguous()
+        y = torch.empty((n * hw, m) if out_tm else (n, m, hw), device=x.device, dtype=torch.float32)
+        rc = None if res is None else res.contiguous()
+        _hip.check(lib.sp_gemm_x6_layout(_hip.ptr(xc), _hip.ptr(_linear_pack(module, w2d, False)),
+                                         _hip.ptr(None if bias is None else bias.detach().contiguous()),
+                                         _hip.ptr(rc), n, hw, k, m, int(in_tm), int(out_tm), _hip.ptr(y),
+                                         _hip.stream_of(xc)), "sp_gemm_x6_layout")
+        ctx.module, ctx.w2d, ctx.geo, ctx.shape = module, w2d, (n, hw, in_tm, out_tm), x.shape
+        ctx.res_shape = None if res is None else res.shape
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        lib = _hip.load_library()
+        m, k = ctx.w2d.shape
+        n, hw, in_tm, out_tm = ctx.geo
+        dc = dy.contiguous()
+        dx = torch.empty((n * hw, k) if in_tm else (n, k, hw), device=dy.device, dtype=torch.float32)
+        _hip.check(lib.sp_gemm_x6_layout(_hip.ptr(dc), _hip.ptr(_linear_pack(ctx.module, ctx.w2d, True)),
+                                         None, None, n, hw, m, k, int(out_tm), int(in_tm), _hip.ptr(dx),
+                                         _hip.stream_of(dc)), "sp_gemm_x6_layout")
+        dres = dy.reshape(ctx.res_shape) if ctx.res_shape is not None and ctx.needs_input_grad[9] else None
+        return dx.reshape(ctx.shape), None, None, None, None, None, None, None, None, dres
+
+
+def _layout_ok(x: Tensor, w2d: Tensor, n: int, hw: int) -> bool:
+    m, k = w2d.shape
+    return (x.is_cuda and x.dtype == torch.float32 and not w2d.requires_grad and linear_backend() == "x6"
+            and bool(_hip.load_library().sp_gemm_x6_layout_supported(n, hw, k, m)))
+
+
+def proj_nchw_to_tokens(x: Tensor, module, w2d: Tensor | None = None, bias: Tensor | None = None) -> Tensor:
+    """A 1x1 projection (``module``: a 1x1 ``nn.Conv2d``, an ``nn.Linear`` or a weight holder;
+    ``w2d`` [c_out][c] defaults to its weight) of NCHW ``x``, returned as token rows
+    ``(b, h w, c_out)``: the transpose happens in the GEMM's stores (HIP, CUDA fp32, frozen
+    weights), else reshape + transpose + linear in torch."""
+    b, c, h, w = x.shape
+    w2d = module.weight.reshape(module.weight.shape[0], c) if w2d is None else w2d
+    bias = getattr(module, "bias", None) if bias is None else bias
+    co = w2d.shape[0]
+    if _layout_ok(x, w2d, b, h * w):
+        y = _ProjLayoutFn.apply(x, w2d, bias, module, w2d, b, h * w, False, True, None)
+        return y.reshape(b, h * w, co)
+    return linear(x.reshape(b, c, h * w).transpose(1, 2), module, w2d, bias)
+
+
+def proj_tokens_to_nchw(tokens: Tensor, module, res: Tensor, w2d: Tensor | None = None,
+                        bias: Tensor | None = None) -> Tensor:
+    """The reverse projection: token rows ``(b, h w, c)`` to NCHW, plus the residual ``res``
+    (b, c_out, h, w) in the epilogue (HIP), else torch."""
+    b, co, h, w = res.shape
+    c = tokens.shape[-1]
+    w2d = module.weight.reshape(co, c) if w2d is None else w2d
+    bias = getattr(module, "bias", None) if bias is None else bias
+    if _layout_ok(tokens, w2d, b, h * w) and res.dtype == torch.float32:
+        y = _ProjLayoutFn.apply(tokens, w2d, bias, module, w2d, b, h * w, True, False, res)
+        return y.reshape(b, co, h, w)
+    out = linear(tokens, module, w2d, bias)
+    return out.transpose(1, 2).reshape(b, co, h, w) + res
+
+
+class _Conv1x1SmallFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias):
+        lib = _hip.load_library()
+        n, c, h, w = x.shape
+        co = weight.shape[0]
+        xc = x.contiguous()
+        y = torch.empty(n, co, h, w, device=x.device, dtype=torch.float32)
+        _hip.check(lib.sp_conv1x1_small(_hip.ptr(xc), _hip.ptr(weight), _hip.ptr(bias), n, c, co, h * w, 0,
+                                        _hip.ptr(y), _hip.stream_of(xc)), "sp_conv1x1_small")
+        ctx.save_for_backward(weight)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (weight,) = ctx.saved_tensors
+        lib = _hip.load_library()
+        n, co, h, w = dy.shape
+        c = weight.shape[1]
+        dc = dy.contiguous()
+        dx = torch.empty(n, c, h, w, device=dy.device, dtype=torch.float32)
+        _hip.check(lib.sp_conv1x1_small(_hip.ptr(dc), _hip.ptr(weight), None, n, co, c, h * w, 1,
+                                        _hip.ptr(dx), _hip.stream_of(dc)), "sp_conv1x1_small")
+        return dx, None, None
+
+
+def conv1x1_small(conv: nn.Conv2d, x: Tensor) -> Tensor:
+    """``conv(x)`` for the VAE's 4- / 8-channel 1x1 quant convs on a HIP kernel (CUDA fp32,
+    frozen weights), else torch."""
+    co, c = conv.weight.shape[:2]
+    if (x.is_cuda and x.dtype == torch.float32 and not conv.weight.requires_grad
+            and (conv.bias is None or not conv.bias.requires_grad)
+            and _hip.load_library().sp_conv1x1_small_supported(c, co, x.shape[2] * x.shape[3])):
+        w2d = conv.weight.detach().reshape(co, c).contiguous()
+        b = None if conv.bias is None else conv.bias.detach().contiguous()
+        return _Conv1x1SmallFn.apply(x, w2d, b)
+    return conv(x)
 
 
 class Linear(nn.Linear):
     """``nn.Linear`` (same parameters and state-dict keys) whose device forward / input VJP run
     ``sp_linear_x6`` where it applies (``linear``)."""
 
-    def forward(self, x: Tensor) -> Tensor:
-        return linear(x, self)
+    def forward(self, x: Tensor, res: Tensor | None = None, box: "SkipGrad | None" = None) -> Tensor:
+        return linear(x, self, res=res, box=box)
+
+
+# ---- transformer-block glue: LayerNorm, GEGLU (csrc/sp_transformer.hip) -------------------
+def _hip_rows_ok(x: Tensor, *params: Tensor | None) -> bool:
+    return (x.is_cuda and x.dtype == torch.float32
+            and all(p is None or not p.requires_grad for p in params))
+
+
+class _LayerNormFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias, eps, box):
+        lib = _hip.load_library()
+        c = x.shape[-1]
+        x2 = x.reshape(-1, c).contiguous()
+        rows = x2.shape[0]
+        y = torch.empty_like(x2)
+        stats = torch.empty(2, rows, device=x.device, dtype=torch.float32)
+        _hip.check(lib.sp_layernorm_fwd(_hip.ptr(x2), _hip.ptr(weight), _hip.ptr(bias), rows, c, float(eps),
+                                        _hip.ptr(y), _hip.ptr(stats[0]), _hip.ptr(stats[1]),
+                                        _hip.stream_of(x2)), "sp_layernorm_fwd")
+        ctx.save_for_backward(x2, weight, stats)
+        ctx.box, ctx.shape = box, x.shape
+        return y.reshape(x.shape)
+
+    @staticmethod
+    def backward(ctx, dy):
+        """Input VJP (frozen weights), plus the residual branch's gradient of the same tensor
+        when its consumer handed it over (``box``)."""
+        x2, weight, stats = ctx.saved_tensors
+        lib = _hip.load_library()
+        rows, c = x2.shape
+        d2 = dy.reshape(rows, c).contiguous()
+        add = ctx.box.take() if ctx.box is not None else None
+        dx = torch.empty_like(x2)
+        _hip.check(lib.sp_layernorm_bwd(_hip.ptr(d2), _hip.ptr(x2), _hip.ptr(weight), _hip.ptr(stats[0]),
+                                        _hip.ptr(stats[1]), _hip.ptr(add), rows, c, _hip.ptr(dx),
+                                        _hip.stream_of(d2)), "sp_layernorm_bwd")
+        return dx.reshape(ctx.shape), None, None, None, None
+
+
+def layer_norm(x: Tensor, module: nn.LayerNorm, box: SkipGrad | None = None) -> Tensor:
+    """``module(x)`` (torch.nn.LayerNorm over the last dim, elementwise affine) on the HIP row
+    kernel for CUDA fp32 activations with frozen parameters, else torch.  ``box``: the residual
+    gradient of ``x`` that a ``linear(..., res=x, box=box)`` consumer hands over, added inside
+    the VJP kernel."""
+    c = x.shape[-1]
+    if (_hip_rows_ok(x, module.weight, module.bias) and module.weight is not None
+            and tuple(module.normalized_shape) == (c,)):
+        lib = _hip.load_library()
+        if lib.sp_layernorm_supported(x.numel() // c, c):
+            return _LayerNormFn.apply(x, module.weight.detach().contiguous(),
+                                      module.bias.detach().contiguous(), module.eps, box)
+    if box is not None:
+        box.enabled = False
+    return F.layer_norm(x, module.normalized_shape, module.weight, module.bias, module.eps)
+
+
+class LayerNorm(nn.LayerNorm):
+    """``nn.LayerNorm`` (same parameters and state-dict keys) on ``sp_layernorm_fwd/bwd``."""
+
+    def forward(self, x: Tensor, box: SkipGrad | None = None) -> Tensor:
+        return layer_norm(x, self, box)
+
+
+class _GegluFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, h):
+        lib = _hip.load_library()
+        f = h.shape[-1] // 2
+        h2 = h.reshape(-1, 2 * f).contiguous()
+        rows = h2.shape[0]
+        y = torch.empty(rows, f, device=h.device, dtype=torch.float32)
+        _hip.check(lib.sp_geglu_fwd(_hip.ptr(h2), rows, f, _hip.ptr(y), _hip.stream_of(h2)), "sp_geglu_fwd")
+        ctx.save_for_backward(h2)
+        ctx.shape = h.shape
+        return y.reshape(*h.shape[:-1], f)
+
+    @staticmethod
+    def backward(ctx, dy):
+        (h2,) = ctx.saved_tensors
+        lib = _hip.load_library()
+        rows, f2 = h2.shape
+        d2 = dy.reshape(rows, f2 // 2).contiguous()
+        dh = torch.empty_like(h2)
+        _hip.check(lib.sp_geglu_bwd(_hip.ptr(h2), _hip.ptr(d2), rows, f2 // 2, _hip.ptr(dh), _hip.stream_of(d2)),
+                   "sp_geglu_bwd")
+        return dh.reshape(ctx.shape)
+
+
+def geglu(h: Tensor) -> Tensor:
+    """``a * gelu(gate)`` with ``a, gate = h.chunk(2, -1)`` (diffusers GEGLU after its
+    projection): one HIP pass each way on CUDA fp32, torch otherwise."""
+    f = h.shape[-1] // 2
+    if (h.is_cuda and h.dtype == torch.float32 and h.shape[-1] % 8 == 0
+            and (h.numel() // 2) < 2**31):
+        return _GegluFn.apply(h)
+    a, gate = h.chunk(2, dim=-1)
+    return a * F.gelu(gate)

@@ -30,7 +30,8 @@ from torch import Tensor, nn
 
 from .. import _hip
 from .layers import (Conv3x3, GroupNormAct, Linear, SkipGrad, conv3x3_forward, conv3x3_input_vjp,
-                     downsample_conv, gn_backward, gn_forward, upsample_nearest2x)
+                     downsample_conv, gn_backward, gn_forward, proj_nchw_to_tokens, proj_tokens_to_nchw,
+                     upsample_nearest2x)
 
 
 @dataclass(frozen=True)
@@ -272,10 +273,51 @@ class ResnetBlock2D(nn.Module):
 
 def attention_backend() -> str:
     """``SAMPLERS_AMD_ATTN``: ``gemm`` (default: scores materialised, batched fp32 GEMMs +
-    softmax, autograd through them) or ``sdpa`` (``F.scaled_dot_product_attention``)."""
+    the HIP row softmax and its VJP) or ``sdpa`` (``F.scaled_dot_product_attention``)."""
     import os
 
     return os.environ.get("SAMPLERS_AMD_ATTN", "gemm").lower()
+
+
+class _ScoreAttention(torch.autograd.Function):
+    """softmax(q kᵀ · scale) v over (batch, n, d) with the scores materialised: the score /
+    value GEMMs on hipBLASLt (batched fp32; q, k, v may be strided views, e.g. the thirds of a
+    fused projection), the row softmax and its VJP on HIP (``sp_softmax_rows`` /
+    ``sp_softmax_bwd_rows``, one pass over the scores each).  Saves q, k, v and P."""
+
+    @staticmethod
+    def forward(ctx, q: Tensor, k: Tensor, v: Tensor) -> Tensor:
+        lib = _hip.load_library()
+        bh, n, d = q.shape
+        m = k.shape[1]
+        scale = 1.0 / math.sqrt(d)
+        p = torch.baddbmm(torch.empty(bh, n, m, device=q.device, dtype=q.dtype), q, k.transpose(1, 2),
+                          beta=0.0, alpha=scale)
+        _hip.check(lib.sp_softmax_rows(_hip.ptr(p), bh * n, m, None, _hip.stream_of(p)), "sp_softmax_rows")
+        ctx.save_for_backward(q, k, v, p)
+        ctx.scale = scale
+        return torch.bmm(p, v)
+
+    @staticmethod
+    def backward(ctx, dout: Tensor):
+        q, k, v, p = ctx.saved_tensors
+        lib = _hip.load_library()
+        bh, n, m = p.shape
+        need_q, need_k, need_v = ctx.needs_input_grad[:3]
+        dv = torch.bmm(p.transpose(1, 2), dout) if need_v else None
+        dq = dk = None
+        if need_q or need_k:
+            ds = torch.bmm(dout, v.transpose(1, 2))
+            _hip.check(lib.sp_softmax_bwd_rows(_hip.ptr(p), _hip.ptr(ds), bh * n, m, ctx.scale,
+                                               _hip.stream_of(ds)), "sp_softmax_bwd_rows")
+            dq = torch.bmm(ds, k) if need_q else None
+            dk = torch.bmm(ds.transpose(1, 2), q) if need_k else None
+        return dq, dk, dv
+
+
+def _score_attention_ok(q: Tensor, k: Tensor) -> bool:
+    return (q.is_cuda and q.dtype == torch.float32 and attention_backend() == "gemm"
+            and bool(_hip.load_library().sp_softmax_rows_supported(q.shape[0] * q.shape[1], k.shape[1])))
 
 
 def attention(q: Tensor, k: Tensor, v: Tensor) -> Tensor:
@@ -286,14 +328,25 @@ def attention(q: Tensor, k: Tensor, v: Tensor) -> Tensor:
     fused flash kernels of PyTorch-ROCm run fp32 at 54 TFLOP/s forward and 25 backward
     (their Q/K/V tiles do not fit on chip); materialising the scores (B x N x N fp32:
     2 GiB for 32 VAE samples, small beside 288 GB) turns both directions into large
-    batched GEMMs on hipBLASLt plus one softmax, forward and backward."""
-    if attention_backend() == "sdpa" or not q.is_cuda:
-        return F.scaled_dot_product_attention(q, k, v)
+    batched GEMMs on hipBLASLt (about 0.9 of the fp32 MFMA peak at these sizes) plus one
+    HIP softmax pass each way (``_ScoreAttention``)."""
     b, nh, n, d = q.shape
     qf, kf, vf = (t.reshape(b * nh, n, d) for t in (q, k, v))
+    if _score_attention_ok(qf, kf):
+        return _ScoreAttention.apply(qf, kf, vf).reshape(b, nh, n, d)
+    if attention_backend() == "sdpa" or not q.is_cuda:
+        return F.scaled_dot_product_attention(q, k, v)
     s = torch.baddbmm(torch.empty(b * nh, n, n, device=q.device, dtype=q.dtype), qf,
                       kf.transpose(1, 2), beta=0.0, alpha=1.0 / math.sqrt(d))
     return torch.bmm(torch.softmax(s, dim=-1), vf).reshape(b, nh, n, d)
+
+
+class _QKVHolder:
+    """[W_q; W_k; W_v] and [b_q; b_k; b_v] of one attention block, outside the module tree
+    (``layers.linear`` caches the packed weight on this object)."""
+
+    def __init__(self, weight: Tensor, bias: Tensor | None) -> None:
+        self.weight, self.bias = weight, bias
 
 
 class SpatialSelfAttention(nn.Module):
@@ -308,9 +361,31 @@ class SpatialSelfAttention(nn.Module):
         self.to_v = Linear(channels, channels)
         self.to_out = nn.ModuleList([Linear(channels, channels)])
 
+    def _qkv(self) -> _QKVHolder:
+        mods = (self.to_q, self.to_k, self.to_v)
+        key = tuple((m.weight.data_ptr(), m.weight._version, m.weight.device) for m in mods)
+        cache = self.__dict__.setdefault("_qkv_cache", {})
+        if cache.get("key") != key:
+            w = torch.cat([m.weight.detach() for m in mods], 0)
+            b = None if mods[0].bias is None else torch.cat([m.bias.detach() for m in mods], 0)
+            cache.clear()
+            cache.update(key=key, holder=_QKVHolder(w, b))
+        return cache["holder"]
+
     def forward(self, x: Tensor) -> Tensor:
         b, c, h, w = x.shape
-        tokens = self.group_norm(x).reshape(b, c, h * w).transpose(1, 2)
+        z = self.group_norm(x)
+        if (self.heads == 1 and z.is_cuda and not self.to_q.weight.requires_grad
+                and attention_backend() == "gemm"):
+            # one projection for q, k, v from the NCHW planes straight into token rows; the
+            # attention reads its thirds in place; to_out writes NCHW with the residual added
+            hold = self._qkv()
+            qkv = proj_nchw_to_tokens(z, hold, hold.weight, hold.bias)
+            q, k, v = qkv.split(c, dim=-1)
+            if _score_attention_ok(q, k):
+                o = _ScoreAttention.apply(q, k, v)
+                return proj_tokens_to_nchw(o, self.to_out[0], x, self.to_out[0].weight, self.to_out[0].bias)
+        tokens = z.reshape(b, c, h * w).transpose(1, 2)
         q, k, v = self.to_q(tokens), self.to_k(tokens), self.to_v(tokens)
         nh = self.heads
         q, k, v = (t.reshape(b, h * w, nh, c // nh).transpose(1, 2) for t in (q, k, v))

@@ -18,8 +18,11 @@ local SD 1.5 ``unet`` safetensors file loads unchanged (``load_state_dict``).
 On the device the residual blocks run this project's kernels exactly as in the pixel
 UNet (``unet2d.ResnetBlock2D``: HIP GroupNorm+SiLU, Winograd / direct fp32-MFMA 3x3
 convolutions, residual in the conv epilogue, skip gradients added inside the VJP
-kernels); the transformer blocks are fp32 GEMMs on hipBLASLt with the attention
-probabilities recomputed in the VJP (``attention.py``).
+kernels); in the transformer blocks every ``nn.Linear`` (to_q/k/v/out, GEGLU, FF out,
+proj_in/out) runs on the split-bf16 GEMM (``layers.Linear``: fp32 operands as exact
+three-term bf16 splits on the bf16 MFMAs), self-attention on the fused fp32-MFMA kernels
+(``attention.py``, scores never in HBM); cross-attention's scores / softmax over the 77
+context tokens and the LayerNorms are torch ops.
 """
 
 from __future__ import annotations
@@ -27,11 +30,12 @@ from __future__ import annotations
 from dataclasses import dataclass
 
 import torch
-import torch.nn.functional as F
 from torch import Tensor, nn
 
-from .attention import attention
-from .layers import Conv3x3, GroupNormAct, Linear, SkipGrad, conv3x3_stride2, linear
+from .attention import (attention, fused_cross_attention, fused_cross_supported, fused_qkv_attention,
+                        fused_qkv_supported)
+from .layers import (Conv3x3, GroupNormAct, LayerNorm, Linear, SkipGrad, conv3x3_stride2, geglu,
+                     linear, proj_nchw_to_tokens, proj_tokens_to_nchw)
 from .unet2d import ResnetBlock2D, TimestepEmbedding, Upsample2D, timestep_embedding
 
 
@@ -57,6 +61,14 @@ class UNet2DConditionConfig:
 SD15_UNET = UNet2DConditionConfig()
 
 
+class _Holder:
+    """A weight outside the module tree (the concatenated q/k/v projection): ``linear`` caches
+    its packed form on this object."""
+
+    def __init__(self, weight: Tensor) -> None:
+        self.weight = weight
+
+
 class Attention(nn.Module):
     """diffusers ``Attention`` without biases on q/k/v (``to_out.0`` has one): self-attention
     when ``context`` is None, else cross-attention to it."""
@@ -70,13 +82,47 @@ class Attention(nn.Module):
         self.to_v = Linear(kv_dim, dim, bias=False)
         self.to_out = nn.ModuleList([Linear(dim, dim)])
 
+    def _qkv_weight(self) -> Tensor:
+        """[W_q; W_k; W_v] ([3 dim][dim]), rebuilt when a weight changes (state-dict load)."""
+        ws = (self.to_q.weight, self.to_k.weight, self.to_v.weight)
+        key = tuple((w.data_ptr(), w._version, w.device) for w in ws)
+        cache = self.__dict__.setdefault("_qkv", {})
+        if cache.get("key") != key:
+            holder = _Holder(torch.cat([w.detach() for w in ws], 0))
+            cache.clear()
+            cache.update(key=key, holder=holder)
+        return cache["holder"]
+
     def _split(self, t: Tensor) -> Tensor:
         b, n, c = t.shape
         h = self.heads
         return t.reshape(b, n, h, c // h).transpose(1, 2).reshape(b * h, n, c // h)
 
-    def forward(self, x: Tensor, context: Tensor | None = None) -> Tensor:
+    def forward(self, x: Tensor, context: Tensor | None = None, res: Tensor | None = None,
+                box: SkipGrad | None = None) -> Tensor:
+        """``res`` is added in ``to_out``'s epilogue (the block's residual); ``box`` carries
+        its gradient to the LayerNorm VJP that adds it (``layers.linear``)."""
         b, n, c = x.shape
+        if context is None and not self.to_q.weight.requires_grad and fused_qkv_supported(x, self.heads):
+            # one projection for q, k, v; attention reads its thirds in place
+            h = self._qkv_weight()
+            qkv = linear(x, h, h.weight, None)
+            if qkv.dim() == 3 and qkv.is_cuda:
+                o = fused_qkv_attention(qkv, self.heads)
+                return self.to_out[0](o, res, box)
+        if context is not None and x.is_cuda and not self.to_q.weight.requires_grad:
+            # cross-attention straight on the projections' token rows (one context row may
+            # serve the whole batch); keys past the context's length masked in the kernel
+            q, k, v = self.to_q(x), self.to_k(context), self.to_v(context)
+            if fused_cross_supported(q, k, self.heads) and not v.requires_grad:
+                return self.to_out[0](fused_cross_attention(q, k, v, self.heads), res, box)
+            q = self._split(q)
+            k, v = self._split(k), self._split(v)
+            if k.shape[0] == self.heads and b > 1:
+                k, v = (t.unsqueeze(0).expand(b, *t.shape).reshape(b * self.heads, *t.shape[1:])
+                        for t in (k, v))
+            o = attention(q, k, v).reshape(b, self.heads, n, -1).transpose(1, 2).reshape(b, n, c)
+            return self.to_out[0](o, res, box)
         q = self._split(self.to_q(x))
         src = x if context is None else context
         k, v = self._split(self.to_k(src)), self._split(self.to_v(src))
@@ -86,7 +132,7 @@ class Attention(nn.Module):
                     for t in (k, v))
         o = attention(q, k, v)
         o = o.reshape(b, self.heads, n, -1).transpose(1, 2).reshape(b, n, c)
-        return self.to_out[0](o)
+        return self.to_out[0](o, res, box)
 
 
 class GEGLU(nn.Module):
@@ -95,8 +141,7 @@ class GEGLU(nn.Module):
         self.proj = Linear(dim, 2 * inner)
 
     def forward(self, x: Tensor) -> Tensor:
-        a, gate = self.proj(x).chunk(2, dim=-1)
-        return a * F.gelu(gate)
+        return geglu(self.proj(x))  # a * gelu(gate), a, gate = proj(x).chunk(2, -1)
 
 
 class FeedForward(nn.Module):
@@ -105,24 +150,31 @@ class FeedForward(nn.Module):
         # diffusers' ModuleList layout: [GEGLU, Dropout, Linear]
         self.net = nn.ModuleList([GEGLU(dim, dim * mult), nn.Dropout(0.0), Linear(dim * mult, dim)])
 
-    def forward(self, x: Tensor) -> Tensor:
-        return self.net[2](self.net[0](x))
+    def forward(self, x: Tensor, res: Tensor | None = None, box: SkipGrad | None = None) -> Tensor:
+        return self.net[2](self.net[0](x), res, box)
 
 
 class BasicTransformerBlock(nn.Module):
     def __init__(self, dim: int, heads: int, context_dim: int) -> None:
         super().__init__()
-        self.norm1 = nn.LayerNorm(dim)
+        self.norm1 = LayerNorm(dim)
         self.attn1 = Attention(dim, heads)
-        self.norm2 = nn.LayerNorm(dim)
+        self.norm2 = LayerNorm(dim)
         self.attn2 = Attention(dim, heads, context_dim)
-        self.norm3 = nn.LayerNorm(dim)
+        self.norm3 = LayerNorm(dim)
         self.ff = FeedForward(dim)
 
     def forward(self, x: Tensor, context: Tensor) -> Tensor:
-        x = x + self.attn1(self.norm1(x))
-        x = x + self.attn2(self.norm2(x), context)
-        return x + self.ff(self.norm3(x))
+        # x + f(norm(x)) three times: the residual is added in f's last linear, and its
+        # gradient rides into the norm's VJP kernel (one box per residual)
+        grad = torch.is_grad_enabled() and x.is_cuda
+        box = (lambda: SkipGrad()) if grad else (lambda: None)  # noqa: E731
+        b1 = box()
+        x = self.attn1(self.norm1(x, b1), res=x, box=b1)
+        b2 = box()
+        x = self.attn2(self.norm2(x, b2), context, res=x, box=b2)
+        b3 = box()
+        return self.ff(self.norm3(x, b3), res=x, box=b3)
 
 
 class Transformer2DModel(nn.Module):
@@ -136,13 +188,12 @@ class Transformer2DModel(nn.Module):
         self.proj_out = nn.Conv2d(channels, channels, 1)
 
     def forward(self, x: Tensor, context: Tensor) -> Tensor:
-        b, c, h, w = x.shape
-        tokens = self.norm(x).reshape(b, c, h * w).transpose(1, 2)
-        tokens = linear(tokens, self.proj_in, self.proj_in.weight.view(c, c), self.proj_in.bias)
+        # NCHW -> token rows and back inside the two 1x1 projections' loads / stores; the
+        # residual x added in proj_out's epilogue
+        tokens = proj_nchw_to_tokens(self.norm(x), self.proj_in)
         for blk in self.transformer_blocks:
             tokens = blk(tokens, context)
-        out = linear(tokens, self.proj_out, self.proj_out.weight.view(c, c), self.proj_out.bias)
-        return out.transpose(1, 2).reshape(b, c, h, w) + x
+        return proj_tokens_to_nchw(tokens, self.proj_out, x)
 
 
 class Downsample2D(nn.Module):

@@ -21,7 +21,7 @@ import torch
 import torch.nn.functional as F
 from torch import Tensor, nn
 
-from .layers import Conv3x3, GroupNormAct
+from .layers import Conv3x3, GroupNormAct, conv1x1_small
 from .unet2d import Downsample2D, ResnetBlock2D, SpatialSelfAttention, Upsample2D
 
 
@@ -130,11 +130,11 @@ class AutoencoderKL(nn.Module):
         return 2 ** (len(self.config.block_out_channels) - 1)
 
     def encode_mean(self, x: Tensor) -> Tensor:
-        moments = self.quant_conv(self.encoder(x))
+        moments = conv1x1_small(self.quant_conv, self.encoder(x))
         return moments[:, : self.config.latent_channels]
 
     def decode(self, z: Tensor) -> Tensor:
-        return self.decoder(self.post_quant_conv(z))
+        return self.decoder(conv1x1_small(self.post_quant_conv, z))
 
 
 def build_vae(config: VAEConfig = SD15_VAE, *, seed: int = 0, device=None,
