@@ -74,7 +74,7 @@ def gn_backward(norm: "GroupNormAct", dz: Tensor, x1: Tensor, x2: Tensor | None,
 
 class _GroupNormActFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, chan_bias, groups: int, eps: float, act: bool):
+    def forward(ctx, x, weight, bias, chan_bias, groups: int, eps: float, act: bool, box=None):
         lib = _hip.load_library()
         n, c = x.shape[0], x.shape[1]
         hw = x[0, 0].numel() if x.numel() else 1
@@ -90,6 +90,7 @@ class _GroupNormActFn(torch.autograd.Function):
             _hip.ptr(work), _hip.stream_of(x)), "sp_groupnorm_silu_fwd")
         ctx.save_for_backward(x, weight, bias, cb, stats)
         ctx.cfg = (groups, float(eps), bool(act))
+        ctx.box = box
         return z
 
     @staticmethod
@@ -103,10 +104,18 @@ class _GroupNormActFn(torch.autograd.Function):
         dx = torch.empty_like(x)
         work = torch.empty(max(int(lib.sp_groupnorm_workspace(n, c, hw, groups)), 1),
                            device=x.device, dtype=torch.float32)
-        _hip.check(lib.sp_groupnorm_silu_bwd(
-            _hip.ptr(dz), _hip.ptr(x), _hip.ptr(cb), _hip.ptr(weight), _hip.ptr(bias),
-            _hip.ptr(stats[0]), _hip.ptr(stats[1]), n, c, hw, groups, int(act), _hip.ptr(dx),
-            _hip.ptr(work), _hip.stream_of(x)), "sp_groupnorm_silu_bwd")
+        add = ctx.box.take() if ctx.box is not None else None
+        if add is not None:  # the residual branch's gradient of x, summed in the VJP kernel
+            _hip.check(lib.sp_groupnorm_silu_bwd2(
+                _hip.ptr(dz), _hip.ptr(x), None, c, _hip.ptr(cb), _hip.ptr(weight), _hip.ptr(bias),
+                _hip.ptr(stats[0]), _hip.ptr(stats[1]), n, c, hw, groups, int(act), _hip.ptr(dx), None,
+                _hip.ptr(add.contiguous()), None, None, _hip.ptr(work), _hip.stream_of(x)),
+                "sp_groupnorm_silu_bwd2")
+        else:
+            _hip.check(lib.sp_groupnorm_silu_bwd(
+                _hip.ptr(dz), _hip.ptr(x), _hip.ptr(cb), _hip.ptr(weight), _hip.ptr(bias),
+                _hip.ptr(stats[0]), _hip.ptr(stats[1]), n, c, hw, groups, int(act), _hip.ptr(dx),
+                _hip.ptr(work), _hip.stream_of(x)), "sp_groupnorm_silu_bwd")
         d_w = d_b = d_cb = None
         need_w, need_b, need_cb = ctx.needs_input_grad[1], ctx.needs_input_grad[2], ctx.needs_input_grad[3]
         if need_cb:
@@ -129,7 +138,7 @@ class _GroupNormActFn(torch.autograd.Function):
                 d_w = (dy * xh).sum(dim=red)
             if need_b:
                 d_b = dy.sum(dim=red)
-        return dx, d_w, d_b, d_cb, None, None, None
+        return dx, d_w, d_b, d_cb, None, None, None, None
 
 
 class GroupNormAct(nn.GroupNorm):
@@ -140,14 +149,18 @@ class GroupNormAct(nn.GroupNorm):
         super().__init__(num_groups, num_channels, eps=eps, affine=affine)
         self.act = act
 
-    def forward(self, x: Tensor, chan_bias: Tensor | None = None) -> Tensor:
+    def forward(self, x: Tensor, chan_bias: Tensor | None = None, box: SkipGrad | None = None) -> Tensor:
+        """``box``: a residual consumer of ``x`` hands its gradient over to be summed inside the
+        VJP kernel (``SkipGrad``)."""
         if not x.is_cuda:
+            if box is not None:
+                box.enabled = False
             return group_norm_act_torch(x, self.num_groups, self.weight, self.bias, self.eps,
                                         self.act, chan_bias)
         if x.dtype != torch.float32:
             raise _hip.HipLibraryError(f"GroupNormAct computes in fp32, got {x.dtype}")
         return _GroupNormActFn.apply(x, self.weight, self.bias, chan_bias, self.num_groups,
-                                     self.eps, self.act)
+                                     self.eps, self.act, box)
 
     def extra_repr(self) -> str:
         return super().extra_repr() + f", act={'silu' if self.act else 'none'}"
@@ -588,7 +601,7 @@ class _ProjLayoutFn(torch.autograd.Function):
     """1x1 projection between the NCHW planes and token-major rows (``sp_gemm_x6_layout``)."""
 
     @staticmethod
-    def forward(ctx, x, weight, bias, module, w2d, n, hw, in_tm, out_tm, res=None):
+    def forward(ctx, x, weight, bias, module, w2d, n, hw, in_tm, out_tm, res=None, box=None):
         lib = _hip.load_library()
         m, k = w2d.shape
         xc = x.contiguous()
@@ -600,6 +613,7 @@ class _ProjLayoutFn(torch.autograd.Function):
                                          _hip.stream_of(xc)), "sp_gemm_x6_layout")
         ctx.module, ctx.w2d, ctx.geo, ctx.shape = module, w2d, (n, hw, in_tm, out_tm), x.shape
         ctx.res_shape = None if res is None else res.shape
+        ctx.box = box if res is not None else None
         return y
 
     @staticmethod
@@ -612,8 +626,13 @@ class _ProjLayoutFn(torch.autograd.Function):
         _hip.check(lib.sp_gemm_x6_layout(_hip.ptr(dc), _hip.ptr(_linear_pack(ctx.module, ctx.w2d, True)),
                                          None, None, n, hw, m, k, int(out_tm), int(in_tm), _hip.ptr(dx),
                                          _hip.stream_of(dc)), "sp_gemm_x6_layout")
-        dres = dy.reshape(ctx.res_shape) if ctx.res_shape is not None and ctx.needs_input_grad[9] else None
-        return dx.reshape(ctx.shape), None, None, None, None, None, None, None, None, dres
+        dres = None
+        if ctx.res_shape is not None and ctx.needs_input_grad[9]:
+            if ctx.box is not None and ctx.box.enabled:
+                ctx.box.grad = dc.reshape(ctx.res_shape)  # summed by the norm's VJP kernel
+            else:
+                dres = dy.reshape(ctx.res_shape)
+        return dx.reshape(ctx.shape), None, None, None, None, None, None, None, None, dres, None
 
 
 def _layout_ok(x: Tensor, w2d: Tensor, n: int, hw: int) -> bool:
@@ -638,16 +657,19 @@ def proj_nchw_to_tokens(x: Tensor, module, w2d: Tensor | None = None, bias: Tens
 
 
 def proj_tokens_to_nchw(tokens: Tensor, module, res: Tensor, w2d: Tensor | None = None,
-                        bias: Tensor | None = None) -> Tensor:
+                        bias: Tensor | None = None, box: SkipGrad | None = None) -> Tensor:
     """The reverse projection: token rows ``(b, h w, c)`` to NCHW, plus the residual ``res``
-    (b, c_out, h, w) in the epilogue (HIP), else torch."""
+    (b, c_out, h, w) in the epilogue (HIP), else torch.  ``box``: the residual's gradient goes
+    to the norm that reads ``res`` (``GroupNormAct(..., box=box)``)."""
     b, co, h, w = res.shape
     c = tokens.shape[-1]
     w2d = module.weight.reshape(co, c) if w2d is None else w2d
     bias = getattr(module, "bias", None) if bias is None else bias
     if _layout_ok(tokens, w2d, b, h * w) and res.dtype == torch.float32:
-        y = _ProjLayoutFn.apply(tokens, w2d, bias, module, w2d, b, h * w, True, False, res)
+        y = _ProjLayoutFn.apply(tokens, w2d, bias, module, w2d, b, h * w, True, False, res, box)
         return y.reshape(b, co, h, w)
+    if box is not None:
+        box.enabled = False
     out = linear(tokens, module, w2d, bias)
     return out.transpose(1, 2).reshape(b, co, h, w) + res
 

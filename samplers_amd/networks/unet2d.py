@@ -279,6 +279,43 @@ def attention_backend() -> str:
     return os.environ.get("SAMPLERS_AMD_ATTN", "gemm").lower()
 
 
+class _ScoreAttentionQKV(torch.autograd.Function):
+    """``_ScoreAttention`` on the fused projection's output ``qkv`` ([b][n][3c], q, k, v its
+    thirds read in place); the VJP writes dq, dk, dv straight into one [b][n][3c] cotangent
+    (GEMM outputs with row stride 3c), so no concatenation follows."""
+
+    @staticmethod
+    def forward(ctx, qkv: Tensor) -> Tensor:
+        lib = _hip.load_library()
+        b, n, c3 = qkv.shape
+        c = c3 // 3
+        q, k, v = qkv.split(c, dim=-1)
+        scale = 1.0 / math.sqrt(c)
+        p = torch.baddbmm(torch.empty(b, n, n, device=qkv.device, dtype=qkv.dtype), q, k.transpose(1, 2),
+                          beta=0.0, alpha=scale)
+        _hip.check(lib.sp_softmax_rows(_hip.ptr(p), b * n, n, None, _hip.stream_of(p)), "sp_softmax_rows")
+        ctx.save_for_backward(qkv, p)
+        ctx.scale = scale
+        return torch.bmm(p, v)
+
+    @staticmethod
+    def backward(ctx, dout: Tensor):
+        qkv, p = ctx.saved_tensors
+        lib = _hip.load_library()
+        b, n, c3 = qkv.shape
+        c = c3 // 3
+        q, k, v = qkv.split(c, dim=-1)
+        dqkv = torch.empty_like(qkv)
+        dq, dk, dv = dqkv.split(c, dim=-1)
+        torch.bmm(p.transpose(1, 2), dout, out=dv)
+        ds = torch.bmm(dout, v.transpose(1, 2))
+        _hip.check(lib.sp_softmax_bwd_rows(_hip.ptr(p), _hip.ptr(ds), b * n, n, ctx.scale, _hip.stream_of(ds)),
+                   "sp_softmax_bwd_rows")
+        torch.bmm(ds, k, out=dq)
+        torch.bmm(ds.transpose(1, 2), q, out=dk)
+        return dqkv
+
+
 class _ScoreAttention(torch.autograd.Function):
     """softmax(q kᵀ · scale) v over (batch, n, d) with the scores materialised: the score /
     value GEMMs on hipBLASLt (batched fp32; q, k, v may be strided views, e.g. the thirds of a
@@ -374,17 +411,21 @@ class SpatialSelfAttention(nn.Module):
 
     def forward(self, x: Tensor) -> Tensor:
         b, c, h, w = x.shape
-        z = self.group_norm(x)
-        if (self.heads == 1 and z.is_cuda and not self.to_q.weight.requires_grad
-                and attention_backend() == "gemm"):
+        fast = (self.heads == 1 and x.is_cuda and not self.to_q.weight.requires_grad
+                and attention_backend() == "gemm"
+                and bool(_hip.load_library().sp_softmax_rows_supported(b * h * w, h * w)))
+        box = SkipGrad() if fast and torch.is_grad_enabled() else None  # x's residual gradient
+        z = self.group_norm(x, box=box)
+        if fast:
             # one projection for q, k, v from the NCHW planes straight into token rows; the
             # attention reads its thirds in place; to_out writes NCHW with the residual added
+            # (its gradient summed in the norm's VJP kernel)
             hold = self._qkv()
-            qkv = proj_nchw_to_tokens(z, hold, hold.weight, hold.bias)
-            q, k, v = qkv.split(c, dim=-1)
-            if _score_attention_ok(q, k):
-                o = _ScoreAttention.apply(q, k, v)
-                return proj_tokens_to_nchw(o, self.to_out[0], x, self.to_out[0].weight, self.to_out[0].bias)
+            qkv = proj_nchw_to_tokens(z, hold, hold.weight, hold.bias).reshape(b, h * w, 3 * c)
+            o = _ScoreAttentionQKV.apply(qkv)
+            return proj_tokens_to_nchw(o, self.to_out[0], x, self.to_out[0].weight, self.to_out[0].bias, box)
+        if box is not None:
+            box.enabled = False
         tokens = z.reshape(b, c, h * w).transpose(1, 2)
         q, k, v = self.to_q(tokens), self.to_k(tokens), self.to_v(tokens)
         nh = self.heads

@@ -190,10 +190,11 @@ class Transformer2DModel(nn.Module):
     def forward(self, x: Tensor, context: Tensor) -> Tensor:
         # NCHW -> token rows and back inside the two 1x1 projections' loads / stores; the
         # residual x added in proj_out's epilogue
-        tokens = proj_nchw_to_tokens(self.norm(x), self.proj_in)
+        box = SkipGrad() if torch.is_grad_enabled() and x.is_cuda else None  # x's residual gradient
+        tokens = proj_nchw_to_tokens(self.norm(x, box=box), self.proj_in)
         for blk in self.transformer_blocks:
             tokens = blk(tokens, context)
-        return proj_tokens_to_nchw(tokens, self.proj_out, x)
+        return proj_tokens_to_nchw(tokens, self.proj_out, x, box=box)
 
 
 class Downsample2D(nn.Module):

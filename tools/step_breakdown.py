@@ -29,6 +29,10 @@ def kind(n: str) -> str:
         return "hipBLASLt GEMMs (attention, time embedding)"
     if "CUDAFunctor_add" in n:
         return "torch adds"
+    if "k_softmax" in n or "k_layernorm" in n or "k_geglu" in n or "k_conv1x1_small" in n:
+        return "HIP softmax / LayerNorm / GEGLU / small 1x1"
+    if "k_attn" in n:
+        return "HIP fused attention"
     if "softmax" in n.lower():
         return "softmax"
     if "upsample" in n:
