@@ -428,13 +428,19 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t gnt_rsrc(const Parts<T>& p, ui
 
 typedef float gnt_f4 __attribute__((ext_vector_type(4)));
 
+#ifndef SP_GN_NTL
+#define SP_GN_NTL 2  // cache-policy bits of the chunk loads: non-temporal (once-read streams)
+#endif
 __device__ __forceinline__ void gnt_load(__amdgpu_buffer_rsrc_t r, uint32_t vo, int i, float (&d)[4]) {
-    const gnt_f4 t = __builtin_bit_cast(gnt_f4, __builtin_amdgcn_raw_buffer_load_b128(r, vo + i * kBlock * 16, 0, 0));
+    const gnt_f4 t = __builtin_bit_cast(
+        gnt_f4, __builtin_amdgcn_raw_buffer_load_b128(r, vo + i * kBlock * 16, 0, SP_GN_NTL));
     d[0] = t[0], d[1] = t[1], d[2] = t[2], d[3] = t[3];
 }
 
 #ifndef SP_GN_NT
-#define SP_GN_NT 0  // 2: non-temporal output stores (measured: GN -0.9 %, the consuming conv +0.4 %)
+#define SP_GN_NT 2  // non-temporal output stores.  With non-temporal loads as well: GroupNorm
+                    // -8 / -9 % (fwd / VJP) and the DPS step +1.4 % (profiles/round3/wino/
+                    // xi_ab.txt); non-temporal stores alone measured -0.9 % in round 2
 #endif
 __device__ __forceinline__ void gnt_store(__amdgpu_buffer_rsrc_t r, uint32_t vo, int i, const float (&d)[4]) {
     typedef unsigned u4 __attribute__((ext_vector_type(4)));

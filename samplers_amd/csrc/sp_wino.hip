@@ -633,6 +633,267 @@ __global__ __launch_bounds__(kBlock, 1) void k_wino3x3_r(WrGeom g) {
     }
 }
 
+// ---------------------------------------------------------------------------------------
+// ξ-split tile (SP_WINO_XI, the W % 32 geometry): the two waves of a tile-row pair split the
+// 16 transformed GEMMs by ξ instead of by output channel.  Wave H holds ξ 8H .. 8H + 7 for all
+// 64 channels of the workgroup (8 ξ x 2 channel blocks x 16 accumulator registers = the same
+// 256 AGPRs), so per k-step it transforms only its half of V (ξ rows 2H, 2H + 1: 8 packed adds
+// instead of 16, three window rows instead of four) and feeds each V value to two MFMAs.  No
+// barrier in the k-loop: each wave stages the whole input block in its own LDS region as
+// before.  The output transform needs all four ξ rows: once per tile the waves exchange the
+// row sums of the channel block the other one finishes (16 KB per wave through LDS, two
+// barriers), and each completes and stores one 32-channel block — in the same operation order
+// as wr_epilogue, so results are bit-identical to k_wino3x3_r.
+// ---------------------------------------------------------------------------------------
+#ifndef SP_WINO_XI
+#define SP_WINO_XI 1
+#endif
+
+struct XiRing {
+    WrX xs[4];
+    WrU us[4];       // u[2 cb + j]: channel block cb, ξ 8H + 4j .. + 3
+    float v[2][8];   // this wave's half of V (slot i = ξ 8H + i) for the current / next step
+};
+
+constexpr int XI_EX = 16 * 64 * 4;  // floats per wave of the epilogue exchange
+
+template <int H>
+__device__ __forceinline__ void xi_load_u(__amdgpu_buffer_rsrc_t urs, int lane, int soff, WrU& u) {
+#pragma unroll
+    for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+            u.u[2 * cb + j] = __builtin_bit_cast(
+                f32x4, __builtin_amdgcn_raw_buffer_load_b128(urs, lane * 64 + 32 * H + 16 * j,
+                                                             soff + cb * 64 * 64, 0));
+}
+
+// this wave's half of V from window rows e0, e1, e2 (= rows H .. H + 2 of the window)
+template <int H>
+__device__ __forceinline__ void xi_half(const WinRow& e0, const WinRow& e1, const WinRow& e2, float* vn) {
+    const WinRow f{pk_sub(e0.p, e2.p), pk_sub(e0.q, e2.q)};
+    if constexpr (H == 0) {  // ξ row 0 = t0 = d0 - d2, row 1 = t1 = d1 + d2
+        wpk_v(f, vn);
+        wpk_v(WinRow{pk_add(e1.p, e2.p), pk_add(e1.q, e2.q)}, vn + 4);
+    } else {                 // ξ row 2 = t2 = d2 - d1, row 3 = t3 = d1 - d3
+        wpk_v(WinRow{pk_sub(e1.p, e0.p), pk_sub(e1.q, e0.q)}, vn);
+        wpk_v(f, vn + 4);
+    }
+}
+
+template <int H, int K, bool FIRST, bool XN, bool UN>
+__device__ __forceinline__ void xi_step(const WrGeom& g, const WrSrc& cur, const WrSrc& nxt,
+                                        __amdgpu_buffer_rsrc_t urs, int lane, float* xw,
+                                        const WxLane& xl, int q, XiRing& r, f32x16 (&acc)[16]) {
+    using GE = WGeo<16>;
+    const WrU& u = r.us[K];
+    const float(&vc)[8] = r.v[K & 1];
+    float(&vn)[8] = r.v[(K + 1) & 1];
+    WinRow e[3];
+    const WrX& xb = r.xs[(K + 1) % 4];  // block of step q + 1
+#define XI_MFMA(sl)                                                                               \
+    acc[sl] = __builtin_amdgcn_mfma_f32_32x32x2f32(u.u[2 * ((sl) >> 3) + (((sl) & 7) >> 2)][(sl) & 3], \
+                                                   vc[(sl) & 7], FIRST ? f32x16{} : acc[sl], 0, 0, 0); \
+    __builtin_amdgcn_sched_barrier(0)
+#define XI_WALL                                \
+    asm volatile("" ::: "memory");             \
+    __builtin_amdgcn_sched_barrier(0)
+    XI_MFMA(0);
+    wr_load_x(XN ? nxt : cur, (XN ? q + 3 - g.nsteps : q + 3) * g.so_step, r.xs[(K + 3) % 4]);
+    XI_WALL;
+    XI_MFMA(1);
+    const int uso = (UN ? nxt.uso : cur.uso) + (UN ? q + 2 - g.nsteps : q + 2) * g.u_step * 4;
+    WrU& un = r.us[(K + 2) % 4];
+    un.u[0] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(urs, lane * 64 + 32 * H, uso, 0));
+    un.u[1] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(urs, lane * 64 + 32 * H + 16, uso, 0));
+    XI_WALL;
+    XI_MFMA(2);
+    un.u[2] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(urs, lane * 64 + 32 * H, uso + 64 * 64, 0));
+    un.u[3] = __builtin_bit_cast(f32x4,
+                                 __builtin_amdgcn_raw_buffer_load_b128(urs, lane * 64 + 32 * H + 16, uso + 64 * 64, 0));
+    XI_WALL;
+    XI_MFMA(3);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) xw[xl.wa + i] = xb.a[i];
+    XI_WALL;
+    XI_MFMA(4);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) xw[xl.wb + i] = xb.b[i];
+    xw[xl.wh] = xb.h;
+    XI_WALL;
+    XI_MFMA(5);
+    e[0] = wr_window_row<GE>(xw, xl, H + 0);
+    e[1] = wr_window_row<GE>(xw, xl, H + 1);
+    XI_WALL;
+    XI_MFMA(6);
+    e[2] = wr_window_row<GE>(xw, xl, H + 2);
+    XI_WALL;
+    XI_MFMA(7);
+    XI_MFMA(8);
+    XI_MFMA(9);
+    XI_MFMA(10);
+    XI_MFMA(11);
+    xi_half<H>(e[0], e[1], e[2], vn);
+    XI_WALL;
+    XI_MFMA(12);
+    XI_MFMA(13);
+    XI_MFMA(14);
+    XI_MFMA(15);
+    XI_WALL;
+#undef XI_MFMA
+#undef XI_WALL
+}
+
+// Epilogue: row sums of this wave's ξ rows for both channel blocks; the block the partner
+// completes goes through LDS, the partner's rows of this wave's block come back; then the
+// output transform, bias, residual and stores as wr_epilogue (same order of operations).
+template <int H, bool RES>
+__device__ __forceinline__ void xi_epilogue(const WrGeom& g, const WrTile& ti, int wv, int lane,
+                                            const f32x16 (&acc)[16], const WrRes& rv, float* ex) {
+    using GE = WGeo<16>;
+    float* mine = ex + H * XI_EX;          // written by this wave (the partner's block)
+    const float* theirs = ex + (1 - H) * XI_EX;
+#pragma unroll
+    for (int rr = 0; rr < 16; ++rr) {
+        float o[4];
+#pragma unroll
+        for (int a = 0; a < 2; ++a) {
+            const int b = (1 - H) * 8 + a * 4;  // the partner's channel block, ξ row 2H + a
+            o[a] = acc[b + 0][rr] + acc[b + 1][rr] + acc[b + 2][rr];
+            o[2 + a] = acc[b + 1][rr] - acc[b + 2][rr] - acc[b + 3][rr];
+        }
+        *reinterpret_cast<f32x4*>(mine + (rr * 64 + lane) * 4) = f32x4{o[0], o[1], o[2], o[3]};
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+    __builtin_amdgcn_s_barrier();
+    WrTile tf = ti;
+    tf.co0 = ti.co0 + 32 * H;  // this wave completes channel block H
+    const int hh = lane >> 5, l = lane & 31;
+    const auto ors = __builtin_amdgcn_make_buffer_rsrc(g.out + (int64_t)tf.n * g.cout * g.plane, (short)0,
+                                                       g.cout * g.plane * 4, 0x00020000);
+    const int vo = wr_out_voff<GE>(g, tf, wv, lane);
+    const auto brs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(g.bias ? g.bias : g.up), (short)0,
+                                                       g.bias ? g.cout * 4 : 0, 0x00020000);
+    const float bl = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(brs, (tf.co0 + l) * 4, 0, 0));
+#pragma unroll
+    for (int rr = 0; rr < 16; ++rr) {
+        const f32x4 p = *reinterpret_cast<const f32x4*>(theirs + (rr * 64 + lane) * 4);
+        float s0[4], s1[4];
+#pragma unroll
+        for (int a = 0; a < 2; ++a) {
+            const int b = H * 8 + a * 4;  // this wave's rows of its own block: ξ row 2H + a
+            s0[2 * H + a] = acc[b + 0][rr] + acc[b + 1][rr] + acc[b + 2][rr];
+            s1[2 * H + a] = acc[b + 1][rr] - acc[b + 2][rr] - acc[b + 3][rr];
+            s0[2 * (1 - H) + a] = p[a];
+            s1[2 * (1 - H) + a] = p[2 + a];
+        }
+        const int c = (rr & 3) + 8 * (rr >> 2);
+        const float b0 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, bl), c));
+        const float b1 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, bl), c + 4));
+        const float bv = hh ? b1 : b0;
+        const int so = c * g.plane * 4;
+        f32x2 y0 = {s0[0] + s0[1] + s0[2] + bv, s1[0] + s1[1] + s1[2] + bv};
+        f32x2 y1 = {s0[1] - s0[2] - s0[3] + bv, s1[1] - s1[2] - s1[3] + bv};
+        if constexpr (RES) y0 += rv.v[rr][0], y1 += rv.v[rr][1];
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, y0), ors, vo, so, 0);
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, y1), ors, vo, so + g.W * 4, 0);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // the partner's rows are read before it writes again
+    __builtin_amdgcn_s_barrier();
+}
+
+template <bool RES, int H>
+__device__ __forceinline__ void xi_body(const WrGeom& g, int wv, int lane, float* xw, float* ex) {
+    using GE = WGeo<16>;
+    const int wq = wv & ~1;  // tile geometry of channel half 0 (the pair covers all 64 channels)
+    WxLane xl;
+    {
+        auto loff = [](int rc) { return (rc / GE::ROWS) * GE::CI + GE::row(rc % GE::ROWS); };
+        const int ka = lane % GE::PPR, rca = lane / GE::PPR, rcb = 64 / GE::PPR + ((lane / GE::PPR) & 3);
+        const int rch = (lane % (2 * GE::RC)) >> 1, side = lane & 1;
+        const int l = lane & 31;
+        xl.wa = loff(rca) + 4 + 4 * ka;
+        xl.wb = loff(rcb) + 4 + 4 * ka;
+        xl.wh = loff(rch) + (side ? 4 + 2 * GE::TCW : 3);
+        xl.rd = (lane >> 5) * GE::CI + GE::row(2 * (l / GE::TCW)) + 3 + 2 * (l % GE::TCW);
+    }
+    const auto urs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(g.up), (short)0,
+                                                       g.nsteps * static_cast<int>(g.u_step) * 4, 0x00020000);
+    int t = blockIdx.x;
+    const int stride = gridDim.x;
+    WrTile ti = wr_tile<GE>(g, t, wq);
+    WrSrc cur = wr_src<GE>(g, ti, wq, lane);
+    int tn = t + stride;
+    WrTile tin = wr_tile<GE>(g, tn < g.ntiles ? tn : t, wq);
+    WrSrc nxt = wr_src<GE>(g, tin, wq, lane);
+
+    XiRing r;
+    wr_load_x(cur, 0, r.xs[0]);
+    __builtin_amdgcn_sched_barrier(0);
+    wr_load_x(cur, g.so_step, r.xs[1]);
+    __builtin_amdgcn_sched_barrier(0);
+    xi_load_u<H>(urs, lane, cur.uso, r.us[0]);
+    __builtin_amdgcn_sched_barrier(0);
+    wr_load_x(cur, 2 * g.so_step, r.xs[2]);
+    __builtin_amdgcn_sched_barrier(0);
+    xi_load_u<H>(urs, lane, cur.uso + g.u_step * 4, r.us[1]);
+    __builtin_amdgcn_sched_barrier(0);
+    {
+        wr_stage_x(xw, xl, r.xs[0]);
+        const WinRow e0 = wr_window_row<GE>(xw, xl, H + 0), e1 = wr_window_row<GE>(xw, xl, H + 1),
+                     e2 = wr_window_row<GE>(xw, xl, H + 2);
+        xi_half<H>(e0, e1, e2, r.v[0]);
+    }
+    f32x16 acc[16];
+    const int last = g.nsteps - 4;
+    for (;;) {
+        xi_step<H, 0, true, false, false>(g, cur, nxt, urs, lane, xw, xl, 0, r, acc);
+        xi_step<H, 1, false, false, false>(g, cur, nxt, urs, lane, xw, xl, 1, r, acc);
+        xi_step<H, 2, false, false, false>(g, cur, nxt, urs, lane, xw, xl, 2, r, acc);
+        xi_step<H, 3, false, false, false>(g, cur, nxt, urs, lane, xw, xl, 3, r, acc);
+        for (int p = 4; p < last; p += 4) {
+            xi_step<H, 0, false, false, false>(g, cur, nxt, urs, lane, xw, xl, p + 0, r, acc);
+            xi_step<H, 1, false, false, false>(g, cur, nxt, urs, lane, xw, xl, p + 1, r, acc);
+            xi_step<H, 2, false, false, false>(g, cur, nxt, urs, lane, xw, xl, p + 2, r, acc);
+            xi_step<H, 3, false, false, false>(g, cur, nxt, urs, lane, xw, xl, p + 3, r, acc);
+        }
+        WrRes rv;
+        if constexpr (RES) {
+            WrTile tf = ti;
+            tf.co0 = ti.co0 + 32 * H;
+            wr_load_res<GE>(g, tf, wv, lane, rv);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        xi_step<H, 0, false, false, false>(g, cur, nxt, urs, lane, xw, xl, last + 0, r, acc);
+        xi_step<H, 1, false, true, false>(g, cur, nxt, urs, lane, xw, xl, last + 1, r, acc);
+        xi_step<H, 2, false, true, true>(g, cur, nxt, urs, lane, xw, xl, last + 2, r, acc);
+        xi_step<H, 3, false, true, true>(g, cur, nxt, urs, lane, xw, xl, last + 3, r, acc);
+        xi_epilogue<H, RES>(g, ti, wv, lane, acc, rv, ex);
+        t = tn;
+        if (t >= g.ntiles) break;
+        ti = tin;
+        cur = nxt;
+        tn = t + stride;
+        tin = wr_tile<GE>(g, tn < g.ntiles ? tn : t, wq);
+        nxt = wr_src<GE>(g, tin, wq, lane);
+    }
+}
+
+template <bool RES>
+__global__ __launch_bounds__(kBlock, 1) void k_wino3x3_xi(WrGeom g) {
+    using GE = WGeo<16>;
+    __shared__ __attribute__((aligned(16))) float xlds[4 * GE::WAVE];
+    __shared__ __attribute__((aligned(16))) float exlds[2 * 2 * XI_EX];  // [pair][writer][...]
+    const int lane = threadIdx.x & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    float* const xw = xlds + wv * GE::WAVE;
+    float* const ex = exlds + (wv >> 1) * 2 * XI_EX;
+    if (wv & 1) xi_body<RES, 1>(g, wv, lane, xw, ex);
+    else xi_body<RES, 0>(g, wv, lane, xw, ex);
+}
+
 // Pack for k_wino3x3_r (U = G g G^T per (co, ci), G = [[1,0,0],[.5,.5,.5],[.5,-.5,.5],[0,0,1]]): up[((kin / 2 * (cout_p / 32) + orow / 32) * 64 + lane) * 16 + xi],
 // lane = 32 (kin & 1) + orow % 32.
 __global__ void k_wino3x3_pack(const float* __restrict__ w, int cout, int cin, int flip,
@@ -752,6 +1013,9 @@ static int wino3x3(int kind, const float* x, const float* up, const float* bias,
     } else if (narrow) {
         if (res) launch_w(kind, flops, k_wino3x3_r<true, 8>, gd, bd, st, g);
         else launch_w(kind, flops, k_wino3x3_r<false, 8>, gd, bd, st, g);
+    } else if (SP_WINO_XI) {
+        if (res) launch_w(kind, flops, k_wino3x3_xi<true>, gd, bd, st, g);
+        else launch_w(kind, flops, k_wino3x3_xi<false>, gd, bd, st, g);
     } else {
         if (res) launch_w(kind, flops, k_wino3x3_r<true, 16>, gd, bd, st, g);
         else launch_w(kind, flops, k_wino3x3_r<false, 16>, gd, bd, st, g);
