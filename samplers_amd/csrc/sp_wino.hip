@@ -8,10 +8,13 @@
 //   Y = A^T M A   (2x2 outputs per (co, tile))
 //
 // Kernel structure: see k_wino3x3_r below (register-resident, one persistent workgroup
-// per CU).  Earlier layouts, measured and replaced: an LDS-staged workgroup tile (U and V
-// through double-buffered LDS, one barrier per 4 input channels, 4 waves splitting the 16
-// GEMMs by rows of M and reducing the output transform through LDS): 167-203 effective
-// TFLOP/s, barrier- and wait-bound (42 % of wave time parked).
+// per CU) and its ξ-split form k_wino3x3_xi (the default for the W % 32 layers: the waves of
+// a pair split the 16 GEMMs by ξ, so each transforms half of V).  Earlier layouts, measured
+// and replaced: an LDS-staged workgroup tile (U and V through double-buffered LDS, one
+// barrier per 4 input channels, 4 waves splitting the 16 GEMMs by rows of M and reducing the
+// output transform through LDS): 167-203 effective TFLOP/s, barrier- and wait-bound (42 % of
+// wave time parked); round 3: V shared between the co-half waves through LDS (-0.6 %), a
+// four-way ξ-row split (-1.7 % against the two-way one).
 //
 // Numerics: exact fp32 MFMA accumulation of fp32 transforms; the transforms add the
 // usual F(2,3) rounding (|coefficients| <= 1, one 0.5 factor), comparable to MIOpen's
