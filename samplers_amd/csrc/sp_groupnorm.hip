@@ -29,9 +29,26 @@ namespace sp {
 // (fewer, larger chunks stream better on big groups; small groups need the chunks to fill the
 // chip); backward: 8192.  Measured on the UNet's shapes (tools/bench_gn.py, MI355X).  The
 // chunk is a function of the shape only, so every path over one call sums in the same order.
-constexpr int GN_CHUNK_FWD_BIG = 16384, GN_CHUNK_FWD = 8192, GN_CHUNK_BWD = 8192;
+#ifndef SP_GN_CHUNK_FWD_BIG
+#define SP_GN_CHUNK_FWD_BIG 16384
+#endif
+#ifndef SP_GN_CHUNK_FWD
+#define SP_GN_CHUNK_FWD 8192
+#endif
+#ifndef SP_GN_CHUNK_BWD
+#define SP_GN_CHUNK_BWD 8192
+#endif
+#ifndef SP_GN_FWD_WPC
+#define SP_GN_FWD_WPC 2  // workgroups per CU the single-pass forward is compiled for
+#endif
+#ifndef SP_GN_BWD_WPC
+#define SP_GN_BWD_WPC 2  // ... and the single-pass input VJP
+#endif
+constexpr int GN_CHUNK_FWD_BIG = SP_GN_CHUNK_FWD_BIG, GN_CHUNK_FWD = SP_GN_CHUNK_FWD,
+              GN_CHUNK_BWD = SP_GN_CHUNK_BWD;
 constexpr int GN_FWD_BIG_GROUP = 1 << 17;
-constexpr int GN_CHUNK_MIN = 8192;
+constexpr int GN_CHUNK_MIN = GN_CHUNK_FWD < GN_CHUNK_BWD ? GN_CHUNK_FWD : GN_CHUNK_BWD;
+static_assert(GN_CHUNK_FWD_BIG >= GN_CHUNK_MIN, "workspace sizing");
 
 static int gn_fwd_chunk(int64_t gs) { return gs >= GN_FWD_BIG_GROUP ? GN_CHUNK_FWD_BIG : GN_CHUNK_FWD; }
 
@@ -646,7 +663,7 @@ __device__ __forceinline__ void gnp_fwd_group(const float* __restrict__ x, const
 }
 
 template <bool ACT, int PER>
-__global__ __launch_bounds__(kBlock, 2) void k_gn_fwd_pipe(const float* __restrict__ x, GnGeom G,
+__global__ __launch_bounds__(kBlock, SP_GN_FWD_WPC) void k_gn_fwd_pipe(const float* __restrict__ x, GnGeom G,
                                                            uint64_t* __restrict__ slots, int nteams,
                                                            int64_t ngroups, float* __restrict__ z,
                                                            float* __restrict__ mean_out,
@@ -797,7 +814,7 @@ __device__ __forceinline__ void gnp_bwd_group(
 }
 
 template <bool ACT, int PER>
-__global__ __launch_bounds__(kBlock, 2) void k_gn_bwd_pipe(
+__global__ __launch_bounds__(kBlock, SP_GN_BWD_WPC) void k_gn_bwd_pipe(
     const float* __restrict__ dz, const float* __restrict__ x, GnGeom G,
     const float* __restrict__ mean_in, const float* __restrict__ rstd_in,
     uint64_t* __restrict__ slots, int nteams, int64_t ngroups, float* __restrict__ dx,
