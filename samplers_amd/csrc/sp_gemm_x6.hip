@@ -13,11 +13,12 @@
 // cost (W, 100-200 KB of split terms, stays in L2).
 //
 // Tile: workgroup = 128 output channels x 256 pixels of one image; its 8 waves (two per SIMD)
-// each own channels 64 (w & 1) .. +63 and pixels 64 (w >> 1) .. +63 (2 x 2 tiles of 32 x 32).
-// k-step = 16 input channels: X (16 ch x 256 px, fp32) and W's packed fragments (12 KB) come
-// by direct global->LDS loads two k-steps ahead; the workgroup splits X one k-step ahead
-// into the three bf16 terms as [term][pixel][16 ch] (a lane's B fragment = 16 contiguous
-// bytes).
+// each own channels 64 (w & 1) .. +63 and pixels 64 (w >> 1) .. +63 (2 x 2 tiles of 32 x 32;
+// pixel tile b holds the wave's pixels of parity b).  k-step = 16 input channels: raw fp32 X
+// (16 ch x 256 px) comes by direct global->LDS loads six k-steps ahead (a 7-slot ring, 112 KB),
+// W's packed fragments (12 KB) two ahead; each wave reads its fp32 X fragments (a ds_read_b64
+// = two adjacent pixels, one per pixel tile) and splits them into the three bf16 terms in
+// registers right before its MFMAs.
 
 #include "sp_common.h"
 
@@ -42,8 +43,9 @@ typedef __attribute__((address_space(3))) void lds_void_g;
 constexpr int G6_CO = 128;     // output channels per workgroup
 constexpr int G6_PX = 256;     // pixels per workgroup
 constexpr int G6_KC = 16;      // input channels per k-step
-constexpr int G6_XB = 3 * G6_PX * G6_KC * 2;  // bytes of split X per k-step (24 KB)
 constexpr int G6_WB = 4 * 3 * 64 * 16;        // bytes of W fragments per k-step (12 KB)
+constexpr int G6_NX = 6;       // raw X ring slots: X of k-step j + 5 loads during step j
+constexpr int G6_NW = 4;       // W ring slots: W of k-step j + 3 loads during step j
 
 struct G6Geom {
     const float* x1;
@@ -79,8 +81,9 @@ __device__ __forceinline__ f32x16 g6_mfma(uvec4 a, uvec4 b, f32x16 c) {
 // direct global->LDS load (64 lanes x 16 B to lds .. lds + 1 KB) written as inline asm: the
 // compiler's wait insertion does not see it, so it does not drain it with vmcnt(0) before every
 // later LDS read it cannot prove disjoint; the kernel waits for these loads itself (counted vmcnt)
-__device__ __forceinline__ void g6_lds_dma(__amdgpu_buffer_rsrc_t rs, const void* lds, int voff, int soff) {
-    const unsigned la = static_cast<unsigned>(reinterpret_cast<size_t>((lds_void_g*)lds));
+// (lds: the LDS byte address, formed once per kernel from the __shared__ array — a generic
+// pointer cast here costs a null check per load, and one form of it trips a backend bug)
+__device__ __forceinline__ void g6_lds_dma(__amdgpu_buffer_rsrc_t rs, unsigned la, int voff, int soff) {
     unsigned keep;  // m0 is reserved to the compiler: saved and restored around the load
     asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %1\n\ts_nop 0\n\tbuffer_load_dwordx4 %2, %3, %4 offen lds\n\t"
                  "s_mov_b32 m0, %0"
@@ -95,7 +98,7 @@ constexpr int g6_vmcnt(int n) { return (n & 0xF) | ((n >> 4) << 14) | (0x7 << 4)
 // raw X of one k-step -> LDS ring slot ([16 ch][256 px] fp32): 16 direct 1-KB loads, 2 per wave
 // (channel 2 wv + i, lane l: pixels 4l .. 4l + 3)
 __device__ __forceinline__ void g6_dma_x(const G6Geom& g, int n, int p0, int kstep, int wv, int lane,
-                                         unsigned char* slot) {
+                                         unsigned slot) {
     const int k0 = kstep * G6_KC;
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
@@ -112,7 +115,7 @@ __device__ __forceinline__ void g6_dma_x(const G6Geom& g, int n, int p0, int kst
 // token-major X (nn.Linear input [tokens][c1]) -> LDS slot [256 tokens][16 ch] fp32: load i of
 // wave wv covers tokens p0 + 16 (2 wv + i) .. +15, lane l: token + (l >> 2), channels 4 (l & 3) .. +3
 __device__ __forceinline__ void g6_dma_x_tm(const G6Geom& g, int p0, int kstep, int wv, int lane,
-                                            unsigned char* slot) {
+                                            unsigned slot) {
     const auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(g.x1), (short)0, g.tokens * g.c1 * 4,
                                                       0x00020000);
     const int vo = ((lane >> 2) * g.c1 + 4 * (lane & 3)) * 4;
@@ -126,7 +129,7 @@ __device__ __forceinline__ void g6_dma_x_tm(const G6Geom& g, int p0, int kstep, 
 // W fragments of one k-step (12 KB contiguous in the packed layout): 12 direct 1-KB loads, two
 // by each of waves 0-3 and one by each of waves 4-7
 __device__ __forceinline__ void g6_dma_w(__amdgpu_buffer_rsrc_t wrs, int stage, int wv, int lane,
-                                         unsigned char* wb) {
+                                         unsigned wb) {
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
         const int chunk = i == 0 ? wv : 8 + wv;
@@ -137,49 +140,45 @@ __device__ __forceinline__ void g6_dma_w(__amdgpu_buffer_rsrc_t wrs, int stage, 
 // vm ops a wave issues per k-step (2 X + 2 or 1 W)
 __device__ __forceinline__ int g6_dma_per_wave(int wv) { return wv < 4 ? 4 : 3; }
 
-// raw slot -> split [term][pixel][16 ch] bf16: thread = 8 channels (tid >> 8) x pixel tid & 255
-__device__ __forceinline__ void g6_split_x(const unsigned char* raw, unsigned char* xb, int tid) {
-    const int grp = tid >> 8, px = tid & 255;
-    float v[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = *reinterpret_cast<const float*>(raw + (8 * grp + j) * 1024 + px * 4);
-    uvec4 th, tm, tl;
+// eight fp32 values (channels c0 .. c0 + 7 of one pixel) -> the lane's three bf16 term fragments
+__device__ __forceinline__ void g6_split8(const float (&v)[8], uvec4 (&t)[3]) {
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
+#if G6_EXP == 2
+        const unsigned a = __float_as_uint(v[2 * q]), b = __float_as_uint(v[2 * q + 1]);
+        t[0][q] = t[1][q] = t[2][q] = g6_pack(a, b);
+#else
         unsigned h0, m0, l0, h1, m1, l1;
         g6_split(v[2 * q], h0, m0, l0);
         g6_split(v[2 * q + 1], h1, m1, l1);
-        th[q] = g6_pack(h0, h1);
-        tm[q] = g6_pack(m0, m1);
-        tl[q] = g6_pack(l0, l1);
+        t[0][q] = g6_pack(h0, h1);
+        t[1][q] = g6_pack(m0, m1);
+        t[2][q] = g6_pack(l0, l1);
+#endif
     }
-    const int off = (px * G6_KC + 8 * grp) * 2;
-    *reinterpret_cast<uvec4*>(xb + 0 * G6_PX * G6_KC * 2 + off) = th;
-    *reinterpret_cast<uvec4*>(xb + 1 * G6_PX * G6_KC * 2 + off) = tm;
-    *reinterpret_cast<uvec4*>(xb + 2 * G6_PX * G6_KC * 2 + off) = tl;
 }
 
-// token-major raw slot -> the same split layout: thread = channels 8 (tid >> 8) .. +7 of token tid & 255
-__device__ __forceinline__ void g6_split_x_tm(const unsigned char* raw, unsigned char* xb, int tid) {
-    const int grp = tid >> 8, px = tid & 255;
-    const uvec4 a = *reinterpret_cast<const uvec4*>(raw + px * 64 + grp * 32);
-    const uvec4 b = *reinterpret_cast<const uvec4*>(raw + px * 64 + grp * 32 + 16);
-    const float v[8] = {__uint_as_float(a[0]), __uint_as_float(a[1]), __uint_as_float(a[2]), __uint_as_float(a[3]),
-                        __uint_as_float(b[0]), __uint_as_float(b[1]), __uint_as_float(b[2]), __uint_as_float(b[3])};
-    uvec4 th, tm, tl;
+// The lane's raw X of one k-step from an NCHW slot ([16 ch][256 px] fp32): channels
+// 8 (lane >> 5) .. +7 of the wave's pixels 64 pq + 2 (lane & 31) + b, b = 0, 1 (pixel tile b)
+// — one ds_read_b64 per channel gives both tiles' pixel
+__device__ __forceinline__ void g6_raw_x(const unsigned char* raw, int pq, int lane, float (&v)[2][8]) {
+    const unsigned char* p = raw + 8 * (lane >> 5) * 1024 + (pq * 64 + 2 * (lane & 31)) * 4;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        unsigned h0, m0, l0, h1, m1, l1;
-        g6_split(v[2 * q], h0, m0, l0);
-        g6_split(v[2 * q + 1], h1, m1, l1);
-        th[q] = g6_pack(h0, h1);
-        tm[q] = g6_pack(m0, m1);
-        tl[q] = g6_pack(l0, l1);
+    for (int i = 0; i < 8; ++i) {
+        const f32x2 t = *reinterpret_cast<const f32x2*>(p + i * 1024);
+        v[0][i] = t.x, v[1][i] = t.y;
     }
-    const int off = (px * G6_KC + 8 * grp) * 2;
-    *reinterpret_cast<uvec4*>(xb + 0 * G6_PX * G6_KC * 2 + off) = th;
-    *reinterpret_cast<uvec4*>(xb + 1 * G6_PX * G6_KC * 2 + off) = tm;
-    *reinterpret_cast<uvec4*>(xb + 2 * G6_PX * G6_KC * 2 + off) = tl;
+}
+
+// the same from a token-major slot ([256 tokens][16 ch] fp32): 32 contiguous bytes per token
+__device__ __forceinline__ void g6_raw_x_tm(const unsigned char* raw, int pq, int lane, float (&v)[2][8]) {
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+        const unsigned char* p = raw + (pq * 64 + 2 * (lane & 31) + b) * 64 + (lane >> 5) * 32;
+        const uvec4 x = *reinterpret_cast<const uvec4*>(p), y = *reinterpret_cast<const uvec4*>(p + 16);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) v[b][i] = __uint_as_float(x[i]), v[b][4 + i] = __uint_as_float(y[i]);
+    }
 }
 
 struct G6Pos { int n, p0, cb; };
@@ -191,12 +190,14 @@ __device__ __forceinline__ G6Pos g6_pos(const G6Geom& g, int t) {
     return G6Pos{n, (rest - n * g.ptiles) * G6_PX, cb};
 }
 
-// epilogue: register q of tile (a, b) = channel 32 sub + (q&3) + 8(q>>2) + 4(lane>>5),
-// pixel pxb[b] + (lane & 31) of image n (pxb[b]: the first of tile b's 32 pixels in the plane);
-// bias and residual added, the 32-channel block to y1 or y2 (TWO = false: acs already added into acc)
-template <bool TWO = true>
-__device__ __forceinline__ void g6_epilogue(const G6Geom& g, int n, int cb, const int (&pxb)[2], int ch, int lane,
-                                            const f32x16 (&acc)[2][2], const f32x16 (&acs)[2][2]) {
+// epilogue: register q of tile (a, b) = channel 32 (2 ch + a) + (q&3) + 8(q>>2) + 4(lane>>5),
+// pixel px0 + 2 (lane & 31) + b of image n (px0: the wave's first pixel in the plane), so both
+// tiles' registers q form one 8-byte store; bias and residual added, the 32-channel block to y1
+// or y2.  Returns the stores issued (the caller's wait count for the next k-step).
+__device__ __forceinline__ int g6_epilogue(const G6Geom& g, int n, int cb, int px0, int ch, int lane,
+                                           const f32x16 (&acc)[2][2], const f32x16 (&acs)[2][2]) {
+    int nst = 0;
+    const int vo = (px0 + 2 * (lane & 31)) * 4;
 #pragma unroll
     for (int a = 0; a < 2; ++a) {
         const int co0 = cb * G6_CO + 32 * (2 * ch + a);  // first channel of the 32-block
@@ -212,45 +213,46 @@ __device__ __forceinline__ void g6_epilogue(const G6Geom& g, int n, int cb, cons
                                                            (short)0, g.bias ? 32 * 4 : 0, 0x00020000);
         const float bl = g.bias ? __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(brs, (lane & 31) * 4, 0, 0))
                                 : 0.f;
+        f32x2 rv[16];
 #pragma unroll
-        for (int b = 0; b < 2; ++b) {
-            const int vo = (pxb[b] + (lane & 31)) * 4;
-            float rv[16];
-#pragma unroll
-            for (int q = 0; q < 16; ++q) rv[q] = 0.f;
-            if (g.res) {  // all 16 loads first (one wait), not a load-use pair per register
-#pragma unroll
-                for (int q = 0; q < 16; ++q) {
-                    const int cc = (q & 3) + 8 * (q >> 2) + 4 * (lane >> 5);
-                    rv[q] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rrs, vo + cc * g.hw * 4, 0, 0));
-                }
-            }
+        for (int q = 0; q < 16; ++q) rv[q] = f32x2{0.f, 0.f};
+        if (g.res) {  // all 16 loads first (one wait), not a load-use pair per register
 #pragma unroll
             for (int q = 0; q < 16; ++q) {
-                const int c = (q & 3) + 8 * (q >> 2);
-                const float b0 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, bl), c));
-                const float b1 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, bl), c + 4));
-                const int cc = c + 4 * (lane >> 5);
-                const float y = (TWO ? acc[a][b][q] + acs[a][b][q] : acc[a][b][q]) + ((lane >> 5) ? b1 : b0) + rv[q];
-#if G6_EXP == 4
-                if (g.hw >= 0) continue;  // never true at run time: the stores are skipped, all math kept
-#endif
-                __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(y), ors, vo + cc * g.hw * 4, 0, 0);
+                const int cc = (q & 3) + 8 * (q >> 2) + 4 * (lane >> 5);
+                rv[q] = __builtin_bit_cast(f32x2, __builtin_amdgcn_raw_buffer_load_b64(rrs, vo + cc * g.hw * 4, 0, 0));
             }
-            __builtin_amdgcn_sched_barrier(0);
         }
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+            const int c = (q & 3) + 8 * (q >> 2);
+            const float b0 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, bl), c));
+            const float b1 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, bl), c + 4));
+            const float bv = (lane >> 5) ? b1 : b0;
+            const int cc = c + 4 * (lane >> 5);
+            const f32x2 y = {(acc[a][0][q] + acs[a][0][q]) + bv + rv[q].x, (acc[a][1][q] + acs[a][1][q]) + bv + rv[q].y};
+#if G6_EXP == 4
+            if (g.hw >= 0) continue;  // never true at run time: the stores are skipped, all math kept
+#endif
+            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(uvec2, y), ors, vo + cc * g.hw * 4, 0, 0);
+        }
+        nst += 16;
+        __builtin_amdgcn_sched_barrier(0);
     }
+    return nst;
 }
 
 // token-major epilogue: the MFMA ran with X as A and W as B, so register q of tile (a, b) is token
-// 128 ph... = p0 + 64 pq + 32 b + (q&3) + 8(q>>2) + 4(lane>>5) and output feature o0 + (lane & 31):
-// each register row is 32 consecutive features of one token (128 contiguous bytes)
-__device__ __forceinline__ void g6_epilogue_tm(const G6Geom& g, const G6Pos& ps, int ch, int pq, int lane,
+// p0 + 64 pq + 2 r + b, r = (q&3) + 8(q>>2) + 4(lane>>5), and output feature o0 + (lane & 31):
+// each register row is 32 consecutive features of one token (128 contiguous bytes).  Returns
+// the stores issued.
+__device__ __forceinline__ int g6_epilogue_tm(const G6Geom& g, const G6Pos& ps, int ch, int pq, int lane,
                                                const f32x16 (&acc)[2][2], const f32x16 (&acs)[2][2]) {
     const auto ors = __builtin_amdgcn_make_buffer_rsrc(g.y1, (short)0, g.tokens * g.o1 * 4, 0x00020000);
     const auto rrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(g.res ? g.res : g.y1), (short)0,
                                                        g.res ? g.tokens * g.o1 * 4 : 0, 0x00020000);
     const int tok0 = ps.n * g.hw + ps.p0;  // first token row of the tile (image n's plane)
+    int nst = 0;
 #pragma unroll
     for (int a = 0; a < 2; ++a) {
         const int o = ps.cb * G6_CO + 32 * (2 * ch + a) + (lane & 31);
@@ -258,7 +260,7 @@ __device__ __forceinline__ void g6_epilogue_tm(const G6Geom& g, const G6Pos& ps,
         const float bv = g.bias ? g.bias[o] : 0.f;
 #pragma unroll
         for (int b = 0; b < 2; ++b) {
-            const int t0 = tok0 + pq * 64 + b * 32 + 4 * (lane >> 5);
+            const int t0 = tok0 + pq * 64 + b + 8 * (lane >> 5);  // token of r = 4 (lane >> 5)
             float rv[16];
 #pragma unroll
             for (int q = 0; q < 16; ++q) rv[q] = 0.f;
@@ -266,44 +268,50 @@ __device__ __forceinline__ void g6_epilogue_tm(const G6Geom& g, const G6Pos& ps,
 #pragma unroll
                 for (int q = 0; q < 16; ++q)
                     rv[q] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
-                        rrs, ((t0 + (q & 3) + 8 * (q >> 2)) * g.o1 + o) * 4, 0, 0));
+                        rrs, ((t0 + 2 * ((q & 3) + 8 * (q >> 2))) * g.o1 + o) * 4, 0, 0));
             }
 #pragma unroll
             for (int q = 0; q < 16; ++q) {
                 const float y = (acc[a][b][q] + acs[a][b][q]) + bv + rv[q];
                 __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(y), ors,
-                                                      ((t0 + (q & 3) + 8 * (q >> 2)) * g.o1 + o) * 4, 0, 0);
+                                                      ((t0 + 2 * ((q & 3) + 8 * (q >> 2))) * g.o1 + o) * 4, 0, 0);
             }
+            nst += 16;
             __builtin_amdgcn_sched_barrier(0);
         }
     }
+    return nst;
 }
 
 // The workgroup walks a flat stream of k-steps j = (its tile j / nsteps, step j % nsteps): the
-// loads of X(j + 3) and W(j + 2) and the split of X(j + 1) run during the MFMAs of step j, across
-// tile boundaries (raw X in a 4-slot and W in a 3-slot LDS ring filled by direct loads, split X
-// in 2 slots).
-// Eight waves, two per SIMD: one wave's MFMAs cover the other's LDS waits and split work.
+// loads of X(j + 5) and W(j + 3) run during the MFMAs of step j, across tile boundaries (raw X
+// in a 6-slot and W in a 4-slot LDS ring filled by direct loads), and each wave reads its
+// fragments of step j + 1 from LDS into registers during them too: the workgroup's barrier
+// aligns all eight waves' phases, so LDS reads issued after it would leave the MFMAs idle.
 constexpr int G6_THREADS = 512;
+
+#ifndef G6_STORE_CREDIT
+#define G6_STORE_CREDIT 1  // the first k-step after an epilogue does not wait for its stores
+#endif
 
 // LTM / STM: X read token-major ([tokens][k]) / Y written token-major ([tokens][m]); else the
 // per-image channel-major planes ([n][k][hw] / [n][m][hw]).  Tokens of image n are rows
 // n hw .. n hw + hw - 1.
 template <bool LTM, bool STM>
 __global__ __launch_bounds__(G6_THREADS, 1) void k_gemm_x6(G6Geom g) {
-    __shared__ __attribute__((aligned(16))) unsigned char xraw[4][G6_KC * G6_PX * 4];
-    __shared__ __attribute__((aligned(16))) unsigned char xs[2][G6_XB];
-    __shared__ __attribute__((aligned(16))) unsigned char wl[3][G6_WB];
+    __shared__ __attribute__((aligned(16))) unsigned char xraw[G6_NX][G6_KC * G6_PX * 4];
+    __shared__ __attribute__((aligned(16))) unsigned char wl[G6_NW][G6_WB];
     const int tid = threadIdx.x, lane = tid & 63;
     const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int ch = wv & 1, pq = wv >> 1;  // 64 output channels x 64 pixels
     const auto wrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<unsigned short*>(g.wp), (short)0,
                                                        g.cob * g.nsteps * G6_WB, 0x00020000);
+    const unsigned xraw_lds = static_cast<unsigned>(reinterpret_cast<size_t>((lds_void_g*)&xraw[0][0]));
+    const unsigned wl_lds = static_cast<unsigned>(reinterpret_cast<size_t>((lds_void_g*)&wl[0][0]));
     const int G = gridDim.x, b0 = blockIdx.x;
     const int ntile_wg = (g.ntiles - b0 + G - 1) / G;
     const int J = ntile_wg * g.nsteps;
-    // two load streams, advanced one k-step at a time (divisions once per tile): raw X three
-    // steps ahead (4 slots), W two steps ahead (3 slots)
+    // two load streams, advanced one k-step at a time (divisions once per tile)
     struct Cursor { int j, tw, s, slot; G6Pos ps; };
     Cursor cx{0, 0, 0, 0, g6_pos(g, b0)}, cw = cx;
     auto advance = [&](Cursor& c, int nslots) {
@@ -316,26 +324,23 @@ __global__ __launch_bounds__(G6_THREADS, 1) void k_gemm_x6(G6Geom g) {
     };
     auto dma_x = [&]() {
         if (cx.j < J) {
-            if constexpr (LTM) g6_dma_x_tm(g, cx.ps.n * g.hw + cx.ps.p0, cx.s, wv, lane, xraw[cx.slot]);
-            else g6_dma_x(g, cx.ps.n, cx.ps.p0, cx.s, wv, lane, xraw[cx.slot]);
+            const unsigned sl = xraw_lds + cx.slot * (G6_KC * G6_PX * 4);
+            if constexpr (LTM) g6_dma_x_tm(g, cx.ps.n * g.hw + cx.ps.p0, cx.s, wv, lane, sl);
+            else g6_dma_x(g, cx.ps.n, cx.ps.p0, cx.s, wv, lane, sl);
         }
-        advance(cx, 4);
+        advance(cx, G6_NX);
     };
     auto dma_w = [&]() {
-        if (cw.j < J) g6_dma_w(wrs, cw.ps.cb * g.nsteps + cw.s, wv, lane, wl[cw.slot]);
-        advance(cw, 3);
+        if (cw.j < J) g6_dma_w(wrs, cw.ps.cb * g.nsteps + cw.s, wv, lane, wl_lds + cw.slot * G6_WB);
+        advance(cw, G6_NW);
     };
-    // prologue: W 0, 1 and X 0, 1, 2 in flight; split of step 0
+    // prologue: W 0 .. 2 and X 0 .. 4 in flight, then all landed
     dma_w();
-    dma_x();
     dma_w();
-    dma_x();
-    dma_x();
+    dma_w();
+#pragma unroll
+    for (int i = 0; i < G6_NX - 1; ++i) dma_x();
     __builtin_amdgcn_s_waitcnt(g6_vmcnt(0));
-    __builtin_amdgcn_s_barrier();
-    if constexpr (LTM) g6_split_x_tm(xraw[0], xs[0], tid);
-    else g6_split_x(xraw[0], xs[0], tid);
-    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
     __builtin_amdgcn_s_barrier();
 
     const bool four = g6_dma_per_wave(wv) == 4;  // this wave's W loads per step: 2 (else 1)
@@ -343,79 +348,110 @@ __global__ __launch_bounds__(G6_THREADS, 1) void k_gemm_x6(G6Geom g) {
     // small terms' fp32 roundings happen at 2^-8 of the result's magnitude (with one
     // accumulator the error grew past an fp32 GEMM's at K = 768)
     f32x16 acc[2][2], acs[2][2];
-    int j = 0, wslot = 0, xslot1 = 1;  // W slot of step j, X slot of step j + 1
+    int j = 0, wslot = 0, xslot = 0;
+    int nst = 0;  // stores of the previous tile's epilogue (younger than W(j + 2) at its step 0)
+    // step j's W fragments and raw X (read during step j - 1; step 0's here), in two register
+    // sets used alternately (A, B) so that no copy moves them from one step to the next
+    uvec4 fuA[2][3], fuB[2][3];
+    float xrA[2][8], xrB[2][8];
+    auto read_frags = [&](int ws, int xs, uvec4 (&u)[2][3], float (&r)[2][8]) {
+        const uvec4* wq = reinterpret_cast<const uvec4*>(wl[ws]) + lane;
+#pragma unroll
+        for (int a = 0; a < 2; ++a)
+#pragma unroll
+            for (int e = 0; e < 3; ++e) u[a][e] = wq[((2 * ch + a) * 3 + e) * 64];
+        if constexpr (LTM) g6_raw_x_tm(xraw[xs], pq, lane, r);
+        else g6_raw_x(xraw[xs], pq, lane, r);
+    };
+    read_frags(0, 0, fuA, xrA);
+    int s = 0;  // k-step within the tile
+    // One k-step: the next step's fragment reads and this step's split between its MFMAs, then
+    // the loads of W(j + 3) and X(j + 5) (their scalar address work overlaps the MFMAs in
+    // flight), one barrier.
+    auto kstep = [&](const uvec4 (&fu)[2][3], const float (&xr)[2][8], uvec4 (&fun)[2][3],
+                     float (&xrn)[2][8]) {
+        wslot = wslot == G6_NW - 1 ? 0 : wslot + 1;
+        xslot = xslot == G6_NX - 1 ? 0 : xslot + 1;
+        // step j + 1's fragments (in since the last barrier; past the stream's end: unused)
+        read_frags(wslot, xslot, fun, xrn);
+        // step j's X split into its terms
+        uvec4 fv[2][3];
+        g6_split8(xr[0], fv[0]);
+        g6_split8(xr[1], fv[1]);
+#if G6_EXP != 1
+        // the six partial products (small terms first) over the 4 independent accumulators
+        constexpr int TU[6] = {2, 0, 1, 1, 0, 0}, TV[6] = {0, 2, 1, 0, 1, 0};
+#pragma unroll
+        for (int e = 0; e < 6; ++e)
+#pragma unroll
+            for (int b = 0; b < 2; ++b)
+#pragma unroll
+                for (int a = 0; a < 2; ++a) {
+                    if constexpr (STM)  // tokens as the MFMA's rows: features contiguous in C
+                        (e == 5 ? acc : acs)[a][b] = g6_mfma(fv[b][TV[e]], fu[a][TU[e]], (e == 5 ? acc : acs)[a][b]);
+                    else
+                        (e == 5 ? acc : acs)[a][b] = g6_mfma(fu[a][TU[e]], fv[b][TV[e]], (e == 5 ? acc : acs)[a][b]);
+                }
+#endif
+#if G6_SCHED
+        // issue order: the split's first terms, then the MFMAs with the rest of the split and
+        // the next step's fragment reads between them
+        __builtin_amdgcn_sched_group_barrier(0x002, 16, 0);
+#pragma unroll
+        for (int k = 0; k < 24; ++k) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
+            if (k < (LTM ? 10 : 14)) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        }
+#endif
+#if G6_EXP != 3
+        dma_w();  // step j + 3
+        dma_x();  // step j + 5
+#endif
+        // one barrier per k-step, behind which X(j + 2) and W(j + 2) are in (read during
+        // step j + 1).  Younger than W(j + 2) (issued at step j - 1, after X(j + 2)): X(j + 4),
+        // this step's W(j + 3) and X(j + 5) — and at a tile's first step the previous
+        // epilogue's stores
+        if (j + G6_NX - 1 >= J) __builtin_amdgcn_s_waitcnt(0x0070);  // the stream's tail: vmcnt(0)
+#if G6_STORE_CREDIT
+        else if (s == 0 && nst == 32) {
+            if (four) __builtin_amdgcn_s_waitcnt(g6_vmcnt(6 + 32) & ~0x0F00);
+            else __builtin_amdgcn_s_waitcnt(g6_vmcnt(5 + 32) & ~0x0F00);
+        } else if (s == 0 && nst == 16) {
+            if (four) __builtin_amdgcn_s_waitcnt(g6_vmcnt(6 + 16) & ~0x0F00);
+            else __builtin_amdgcn_s_waitcnt(g6_vmcnt(5 + 16) & ~0x0F00);
+        }
+#endif
+        else if (four) __builtin_amdgcn_s_waitcnt(g6_vmcnt(6) & ~0x0F00);
+        else __builtin_amdgcn_s_waitcnt(g6_vmcnt(5) & ~0x0F00);
+        __builtin_amdgcn_s_barrier();
+        ++s, ++j;
+    };
     for (int tw = 0; tw < ntile_wg; ++tw) {
 #pragma unroll
         for (int a = 0; a < 2; ++a)
 #pragma unroll
             for (int b = 0; b < 2; ++b) acc[a][b] = f32x16{}, acs[a][b] = f32x16{};
-        for (int s = 0; s < g.nsteps; ++s, ++j) {
-#if G6_EXP != 3
-            dma_w();  // step j + 2
-            dma_x();  // step j + 3
-#endif
-            // step j's fragments (split X(j) and W(j), both in since the last barrier)
-            const uvec4* wq = reinterpret_cast<const uvec4*>(wl[wslot]) + lane;
-            const unsigned char* xb = xs[j & 1];
-            uvec4 fu[2][3], fv[2][3];
+        s = 0;
+        while (s + 1 < g.nsteps) {
+            kstep(fuA, xrA, fuB, xrB);
+            kstep(fuB, xrB, fuA, xrA);
+        }
+        if (s < g.nsteps) {  // odd step count: one more, and set A back to the current step
+            kstep(fuA, xrA, fuB, xrB);
 #pragma unroll
             for (int a = 0; a < 2; ++a)
 #pragma unroll
-                for (int e = 0; e < 3; ++e) fu[a][e] = wq[((2 * ch + a) * 3 + e) * 64];
+                for (int e = 0; e < 3; ++e) fuA[a][e] = fuB[a][e];
 #pragma unroll
-            for (int b = 0; b < 2; ++b) {
-                const int off = ((pq * 64 + b * 32 + (lane & 31)) * G6_KC + 8 * (lane >> 5)) * 2;
+            for (int b = 0; b < 2; ++b)
 #pragma unroll
-                for (int e = 0; e < 3; ++e)
-                    fv[b][e] = *reinterpret_cast<const uvec4*>(xb + e * G6_PX * G6_KC * 2 + off);
-            }
-#if G6_EXP != 2
-            // X(j + 1)'s split (unconditional: past the stream's end it rewrites an unused slot)
-            if constexpr (LTM) g6_split_x_tm(xraw[xslot1], xs[(j + 1) & 1], tid);
-            else g6_split_x(xraw[xslot1], xs[(j + 1) & 1], tid);
-#endif
-#if G6_EXP != 1
-            // the six partial products (small terms first) over the 4 independent accumulators
-            constexpr int TU[6] = {2, 0, 1, 1, 0, 0}, TV[6] = {0, 2, 1, 0, 1, 0};
-#pragma unroll
-            for (int e = 0; e < 6; ++e)
-#pragma unroll
-                for (int b = 0; b < 2; ++b)
-#pragma unroll
-                    for (int a = 0; a < 2; ++a) {
-                        if constexpr (STM)  // tokens as the MFMA's rows: features contiguous in C
-                            (e == 5 ? acc : acs)[a][b] = g6_mfma(fv[b][TV[e]], fu[a][TU[e]], (e == 5 ? acc : acs)[a][b]);
-                        else
-                            (e == 5 ? acc : acs)[a][b] = g6_mfma(fu[a][TU[e]], fv[b][TV[e]], (e == 5 ? acc : acs)[a][b]);
-                    }
-#endif
-#if G6_SCHED
-            // issue order: the fragment reads, the split's reads, then the MFMAs with the split's
-            // VALU work between them, the split's writes last
-            __builtin_amdgcn_sched_group_barrier(0x100, 12, 0);
-            __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);
-#pragma unroll
-            for (int k = 0; k < 24; ++k) {
-                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-                __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
-            }
-            __builtin_amdgcn_sched_group_barrier(0x200, 3, 0);
-#endif
-            // one barrier per k-step: the split's writes are done (lgkmcnt) and X(j + 2), W(j + 1)
-            // are in — what may still be in flight was issued after X(j + 2): W(j + 2), X(j + 3)
-            if (j + 3 >= J) __builtin_amdgcn_s_waitcnt(0x0070);  // vmcnt(0) lgkmcnt(0)
-            else if (four) __builtin_amdgcn_s_waitcnt(g6_vmcnt(4) & ~0x0F00);
-            else __builtin_amdgcn_s_waitcnt(g6_vmcnt(3) & ~0x0F00);
-            __builtin_amdgcn_s_barrier();
-            wslot = wslot == 2 ? 0 : wslot + 1;
-            xslot1 = xslot1 == 3 ? 0 : xslot1 + 1;
+                for (int i = 0; i < 8; ++i) xrA[b][i] = xrB[b][i];
         }
         const G6Pos ps = g6_pos(g, b0 + tw * G);
-        if constexpr (STM) g6_epilogue_tm(g, ps, ch, pq, lane, acc, acs);
-        else {
-            const int pxb[2] = {ps.p0 + pq * 64, ps.p0 + pq * 64 + 32};
-            g6_epilogue(g, ps.n, ps.cb, pxb, ch, lane, acc, acs);
-        }
+        if constexpr (STM) nst = g6_epilogue_tm(g, ps, ch, pq, lane, acc, acs);
+        else nst = g6_epilogue(g, ps.n, ps.cb, ps.p0 + pq * 64, ch, lane, acc, acs);
+        if (STM && nst > 32) nst = 32;  // 64 stores: credit 32 of them (a lower bound is safe)
     }
 }
 

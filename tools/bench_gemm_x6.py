@@ -41,7 +41,9 @@ def rel(a, b):
 def main():
     lib = _hip.load_library()
     st = lambda: torch.cuda.current_stream().cuda_stream  # noqa: E731
-    for n, c1, c2, co, h, w in CASES:
+    pick = os.environ.get("G6_CASES")  # e.g. "0" or "0,2": a subset of CASES (profiling)
+    cases = [CASES[int(i)] for i in pick.split(",")] if pick else CASES
+    for n, c1, c2, co, h, w in cases:
         hw = h * w
         g = torch.Generator(device="cuda").manual_seed(1)
         x1 = torch.randn(n, c1, h, w, device="cuda", generator=g)
