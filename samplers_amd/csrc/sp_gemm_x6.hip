@@ -23,6 +23,7 @@
 #include "sp_common.h"
 
 #include <algorithm>
+#include <type_traits>
 
 namespace sp {
 
@@ -170,11 +171,15 @@ __device__ __forceinline__ void g6_raw_x(const unsigned char* raw, int pq, int l
     }
 }
 
-// the same from a token-major slot ([256 tokens][16 ch] fp32): 32 contiguous bytes per token
+// the same from a token-major slot ([256 tokens][16 ch] fp32): 32 contiguous bytes per token;
+// PAR: tile b holds the tokens of parity b (as above), else tokens 32 b .. 32 b + 31 (a 64-byte
+// lane stride: half the LDS bank conflicts of the parity order's 128 bytes)
+template <bool PAR>
 __device__ __forceinline__ void g6_raw_x_tm(const unsigned char* raw, int pq, int lane, float (&v)[2][8]) {
 #pragma unroll
     for (int b = 0; b < 2; ++b) {
-        const unsigned char* p = raw + (pq * 64 + 2 * (lane & 31) + b) * 64 + (lane >> 5) * 32;
+        const int tok = PAR ? 2 * (lane & 31) + b : 32 * b + (lane & 31);
+        const unsigned char* p = raw + (pq * 64 + tok) * 64 + (lane >> 5) * 32;
         const uvec4 x = *reinterpret_cast<const uvec4*>(p), y = *reinterpret_cast<const uvec4*>(p + 16);
 #pragma unroll
         for (int i = 0; i < 4; ++i) v[b][i] = __uint_as_float(x[i]), v[b][4 + i] = __uint_as_float(y[i]);
@@ -191,9 +196,11 @@ __device__ __forceinline__ G6Pos g6_pos(const G6Geom& g, int t) {
 }
 
 // epilogue: register q of tile (a, b) = channel 32 (2 ch + a) + (q&3) + 8(q>>2) + 4(lane>>5),
-// pixel px0 + 2 (lane & 31) + b of image n (px0: the wave's first pixel in the plane), so both
-// tiles' registers q form one 8-byte store; bias and residual added, the 32-channel block to y1
-// or y2.  Returns the stores issued (the caller's wait count for the next k-step).
+// pixel px0 + 2 (lane & 31) + b of image n (PAR; px0: the wave's first pixel in the plane), so
+// both tiles' registers q form one 8-byte store — else pixel px0 + 32 b + (lane & 31), one
+// 4-byte store each; bias and residual added, the 32-channel block to y1 or y2.  Returns the
+// stores issued (the caller's wait count for the next k-step).
+template <bool PAR>
 __device__ __forceinline__ int g6_epilogue(const G6Geom& g, int n, int cb, int px0, int ch, int lane,
                                            const f32x16 (&acc)[2][2], const f32x16 (&acs)[2][2]) {
     int nst = 0;
@@ -213,6 +220,33 @@ __device__ __forceinline__ int g6_epilogue(const G6Geom& g, int n, int cb, int p
                                                            (short)0, g.bias ? 32 * 4 : 0, 0x00020000);
         const float bl = g.bias ? __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(brs, (lane & 31) * 4, 0, 0))
                                 : 0.f;
+        if constexpr (!PAR) {
+#pragma unroll
+            for (int b = 0; b < 2; ++b) {
+                const int vb = (px0 + 32 * b + (lane & 31)) * 4;
+                float rs[16];
+#pragma unroll
+                for (int q = 0; q < 16; ++q) rs[q] = 0.f;
+                if (g.res) {
+#pragma unroll
+                    for (int q = 0; q < 16; ++q) {
+                        const int cc = (q & 3) + 8 * (q >> 2) + 4 * (lane >> 5);
+                        rs[q] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rrs, vb + cc * g.hw * 4, 0, 0));
+                    }
+                }
+#pragma unroll
+                for (int q = 0; q < 16; ++q) {
+                    const int c = (q & 3) + 8 * (q >> 2);
+                    const float b0 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, bl), c));
+                    const float b1 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, bl), c + 4));
+                    const float y = (acc[a][b][q] + acs[a][b][q]) + ((lane >> 5) ? b1 : b0) + rs[q];
+                    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(y), ors, vb + (c + 4 * (lane >> 5)) * g.hw * 4, 0, 0);
+                }
+                nst += 16;
+                __builtin_amdgcn_sched_barrier(0);
+            }
+            continue;
+        }
         f32x2 rv[16];
 #pragma unroll
         for (int q = 0; q < 16; ++q) rv[q] = f32x2{0.f, 0.f};
@@ -243,9 +277,10 @@ __device__ __forceinline__ int g6_epilogue(const G6Geom& g, int n, int cb, int p
 }
 
 // token-major epilogue: the MFMA ran with X as A and W as B, so register q of tile (a, b) is token
-// p0 + 64 pq + 2 r + b, r = (q&3) + 8(q>>2) + 4(lane>>5), and output feature o0 + (lane & 31):
-// each register row is 32 consecutive features of one token (128 contiguous bytes).  Returns
-// the stores issued.
+// p0 + 64 pq + 2 r + b (PAR, else + 32 b + r), r = (q&3) + 8(q>>2) + 4(lane>>5), and output
+// feature o0 + (lane & 31): each register row is 32 consecutive features of one token (128
+// contiguous bytes).  Returns the stores issued.
+template <bool PAR>
 __device__ __forceinline__ int g6_epilogue_tm(const G6Geom& g, const G6Pos& ps, int ch, int pq, int lane,
                                                const f32x16 (&acc)[2][2], const f32x16 (&acs)[2][2]) {
     const auto ors = __builtin_amdgcn_make_buffer_rsrc(g.y1, (short)0, g.tokens * g.o1 * 4, 0x00020000);
@@ -260,7 +295,8 @@ __device__ __forceinline__ int g6_epilogue_tm(const G6Geom& g, const G6Pos& ps, 
         const float bv = g.bias ? g.bias[o] : 0.f;
 #pragma unroll
         for (int b = 0; b < 2; ++b) {
-            const int t0 = tok0 + pq * 64 + b + 8 * (lane >> 5);  // token of r = 4 (lane >> 5)
+            constexpr int RS = PAR ? 2 : 1;  // token stride of the register rows
+            const int t0 = tok0 + pq * 64 + (PAR ? b : 32 * b) + RS * 4 * (lane >> 5);  // r = 4 (lane >> 5)
             float rv[16];
 #pragma unroll
             for (int q = 0; q < 16; ++q) rv[q] = 0.f;
@@ -268,13 +304,13 @@ __device__ __forceinline__ int g6_epilogue_tm(const G6Geom& g, const G6Pos& ps, 
 #pragma unroll
                 for (int q = 0; q < 16; ++q)
                     rv[q] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
-                        rrs, ((t0 + 2 * ((q & 3) + 8 * (q >> 2))) * g.o1 + o) * 4, 0, 0));
+                        rrs, ((t0 + RS * ((q & 3) + 8 * (q >> 2))) * g.o1 + o) * 4, 0, 0));
             }
 #pragma unroll
             for (int q = 0; q < 16; ++q) {
                 const float y = (acc[a][b][q] + acs[a][b][q]) + bv + rv[q];
                 __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(y), ors,
-                                                      ((t0 + 2 * ((q & 3) + 8 * (q >> 2))) * g.o1 + o) * 4, 0, 0);
+                                                      ((t0 + RS * ((q & 3) + 8 * (q >> 2))) * g.o1 + o) * 4, 0, 0);
             }
             nst += 16;
             __builtin_amdgcn_sched_barrier(0);
@@ -290,6 +326,9 @@ __device__ __forceinline__ int g6_epilogue_tm(const G6Geom& g, const G6Pos& ps, 
 // aligns all eight waves' phases, so LDS reads issued after it would leave the MFMAs idle.
 constexpr int G6_THREADS = 512;
 
+#ifndef G6_STAGGER
+#define G6_STAGGER 1  // the second wave of each SIMD issues its loads half-way through its MFMAs
+#endif
 #ifndef G6_STORE_CREDIT
 #define G6_STORE_CREDIT 1  // the first k-step after an epilogue does not wait for its stores
 #endif
@@ -297,12 +336,13 @@ constexpr int G6_THREADS = 512;
 // LTM / STM: X read token-major ([tokens][k]) / Y written token-major ([tokens][m]); else the
 // per-image channel-major planes ([n][k][hw] / [n][m][hw]).  Tokens of image n are rows
 // n hw .. n hw + hw - 1.
-template <bool LTM, bool STM>
-__global__ __launch_bounds__(G6_THREADS, 1) void k_gemm_x6(G6Geom g) {
-    __shared__ __attribute__((aligned(16))) unsigned char xraw[G6_NX][G6_KC * G6_PX * 4];
-    __shared__ __attribute__((aligned(16))) unsigned char wl[G6_NW][G6_WB];
+typedef unsigned char G6XSlot[G6_KC * G6_PX * 4];
+typedef unsigned char G6WSlot[G6_WB];
+
+// LATE: this wave issues its loads half-way through its MFMAs (the second wave of each SIMD)
+template <bool LTM, bool STM, bool LATE>
+__device__ __forceinline__ void g6_body(const G6Geom& g, G6XSlot* xraw, G6WSlot* wl, int wv) {
     const int tid = threadIdx.x, lane = tid & 63;
-    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int ch = wv & 1, pq = wv >> 1;  // 64 output channels x 64 pixels
     const auto wrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<unsigned short*>(g.wp), (short)0,
                                                        g.cob * g.nsteps * G6_WB, 0x00020000);
@@ -360,7 +400,7 @@ __global__ __launch_bounds__(G6_THREADS, 1) void k_gemm_x6(G6Geom g) {
         for (int a = 0; a < 2; ++a)
 #pragma unroll
             for (int e = 0; e < 3; ++e) u[a][e] = wq[((2 * ch + a) * 3 + e) * 64];
-        if constexpr (LTM) g6_raw_x_tm(xraw[xs], pq, lane, r);
+        if constexpr (LTM) g6_raw_x_tm<!LTM>(xraw[xs], pq, lane, r);
         else g6_raw_x(xraw[xs], pq, lane, r);
     };
     read_frags(0, 0, fuA, xrA);
@@ -378,36 +418,55 @@ __global__ __launch_bounds__(G6_THREADS, 1) void k_gemm_x6(G6Geom g) {
         uvec4 fv[2][3];
         g6_split8(xr[0], fv[0]);
         g6_split8(xr[1], fv[1]);
+        // the six partial products (small terms first) over the 4 independent accumulators,
+        // terms [LO, HI) of them, with the split's rest and the next step's fragment reads
+        // between the MFMAs
+        auto prods = [&](auto lo_c, auto hi_c) {
+            constexpr int LO = decltype(lo_c)::value, HI = decltype(hi_c)::value;
+            constexpr int TU[6] = {2, 0, 1, 1, 0, 0}, TV[6] = {0, 2, 1, 0, 1, 0};
 #if G6_EXP != 1
-        // the six partial products (small terms first) over the 4 independent accumulators
-        constexpr int TU[6] = {2, 0, 1, 1, 0, 0}, TV[6] = {0, 2, 1, 0, 1, 0};
 #pragma unroll
-        for (int e = 0; e < 6; ++e)
+            for (int e = LO; e < HI; ++e)
 #pragma unroll
-            for (int b = 0; b < 2; ++b)
+                for (int b = 0; b < 2; ++b)
 #pragma unroll
-                for (int a = 0; a < 2; ++a) {
-                    if constexpr (STM)  // tokens as the MFMA's rows: features contiguous in C
-                        (e == 5 ? acc : acs)[a][b] = g6_mfma(fv[b][TV[e]], fu[a][TU[e]], (e == 5 ? acc : acs)[a][b]);
-                    else
-                        (e == 5 ? acc : acs)[a][b] = g6_mfma(fu[a][TU[e]], fv[b][TV[e]], (e == 5 ? acc : acs)[a][b]);
-                }
+                    for (int a = 0; a < 2; ++a) {
+                        if constexpr (STM)  // tokens as the MFMA's rows: features contiguous in C
+                            (e == 5 ? acc : acs)[a][b] = g6_mfma(fv[b][TV[e]], fu[a][TU[e]], (e == 5 ? acc : acs)[a][b]);
+                        else
+                            (e == 5 ? acc : acs)[a][b] = g6_mfma(fu[a][TU[e]], fv[b][TV[e]], (e == 5 ? acc : acs)[a][b]);
+                    }
 #endif
 #if G6_SCHED
-        // issue order: the split's first terms, then the MFMAs with the rest of the split and
-        // the next step's fragment reads between them
-        __builtin_amdgcn_sched_group_barrier(0x002, 16, 0);
+            if constexpr (LO == 0) __builtin_amdgcn_sched_group_barrier(0x002, 16, 0);  // the first terms
 #pragma unroll
-        for (int k = 0; k < 24; ++k) {
-            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-            __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
-            if (k < (LTM ? 10 : 14)) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-        }
+            for (int k = 4 * LO; k < 4 * HI; ++k) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
+                if (k < (LTM ? 10 : 14)) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+            }
 #endif
+        };
+        // the loads of W(j + 3) and X(j + 5): their scalar address work runs while MFMAs are in
+        // the pipe — after all of this wave's, or (the waves sharing a SIMD with the first four)
+        // half-way, so that the two waves of a SIMD never do it at the same time
+        auto dma = [&]() {
 #if G6_EXP != 3
-        dma_w();  // step j + 3
-        dma_x();  // step j + 5
+            dma_w();  // step j + 3
+            dma_x();  // step j + 5
 #endif
+        };
+        if constexpr (LATE) {
+            prods(std::integral_constant<int, 0>{}, std::integral_constant<int, 3>{});
+            __builtin_amdgcn_sched_barrier(0);
+            dma();
+            __builtin_amdgcn_sched_barrier(0);
+            prods(std::integral_constant<int, 3>{}, std::integral_constant<int, 6>{});
+        } else {
+            prods(std::integral_constant<int, 0>{}, std::integral_constant<int, 6>{});
+            __builtin_amdgcn_sched_barrier(0);
+            dma();
+        }
         // one barrier per k-step, behind which X(j + 2) and W(j + 2) are in (read during
         // step j + 1).  Younger than W(j + 2) (issued at step j - 1, after X(j + 2)): X(j + 4),
         // this step's W(j + 3) and X(j + 5) — and at a tile's first step the previous
@@ -449,10 +508,22 @@ __global__ __launch_bounds__(G6_THREADS, 1) void k_gemm_x6(G6Geom g) {
                 for (int i = 0; i < 8; ++i) xrA[b][i] = xrB[b][i];
         }
         const G6Pos ps = g6_pos(g, b0 + tw * G);
-        if constexpr (STM) nst = g6_epilogue_tm(g, ps, ch, pq, lane, acc, acs);
-        else nst = g6_epilogue(g, ps.n, ps.cb, ps.p0 + pq * 64, ch, lane, acc, acs);
-        if (STM && nst > 32) nst = 32;  // 64 stores: credit 32 of them (a lower bound is safe)
+        // tiles hold the pixels of parity b (NCHW X: one ds_read_b64 per channel) or 32 b .. (token
+        // X: fewer LDS bank conflicts)
+        if constexpr (STM) nst = g6_epilogue_tm<!LTM>(g, ps, ch, pq, lane, acc, acs);
+        else nst = g6_epilogue<!LTM>(g, ps.n, ps.cb, ps.p0 + pq * 64, ch, lane, acc, acs);
+        if (nst > 32) nst = 32;  // 64 stores: credit 32 of them (a lower bound is safe)
     }
+}
+
+template <bool LTM, bool STM>
+__global__ __launch_bounds__(G6_THREADS, 1) void k_gemm_x6(G6Geom g) {
+    __shared__ __attribute__((aligned(16))) G6XSlot xraw[G6_NX];
+    __shared__ __attribute__((aligned(16))) G6WSlot wl[G6_NW];
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    // waves w and w + 4 share a SIMD: the second one issues its loads half-way (G6_STAGGER)
+    if (G6_STAGGER && (wv & 4)) g6_body<LTM, STM, true>(g, xraw, wl, wv);
+    else g6_body<LTM, STM, false>(g, xraw, wl, wv);
 }
 
 // the split terms of A element (row, col) of an [M][K] operand into their fragment slots
