@@ -270,6 +270,12 @@ int sp_groupnorm_silu_bwd2(const float* dz, const float* x1, const float* x2, in
  * recomputed that way (a cost, not an error).  set_spin_limit: the poll bound (< 0 default;
  * 0 recomputes every partial not present at the first poll — a test of that path). */
 int sp_groupnorm_single_pass(int32_t enable);
+/* The single-pass kernels' team words live in a library-owned region per (device, stream),
+ * zeroed once and left zero by every launch, so a call issues no memset (default on).  0: use
+ * and zero the caller's workspace each call (also the path taken while a stream is being
+ * captured into a graph and the region would have to grow); < 0 query; returns the previous
+ * setting.  Results are identical either way. */
+int sp_groupnorm_persistent_slots(int32_t enable);
 int64_t sp_groupnorm_team_timeouts(void);
 int sp_groupnorm_set_spin_limit(int32_t spins);
 

@@ -19,6 +19,11 @@
 
 #include "sp_common.h"
 
+#include <algorithm>
+#include <map>
+#include <mutex>
+#include <utility>
+
 // No implicit mul+add contraction: which products the backend fuses depends on the code
 // around them, and the single-pass and two-pass kernels must round identically.
 #pragma clang fp contract(off)
@@ -419,6 +424,35 @@ __device__ __forceinline__ void gnt_publish(uint64_t* slot, float a, float b) {
 
 constexpr int GNT_MAX_CHUNKS = 256;  // chunks per group (words polled per team)
 
+// Self-cleaning words (the slot region is all zero again when a launch ends, so the next
+// launch needs no memset).  A team walks its groups in step: a member publishes group g's words
+// only after it has read all of the previous group's, so once a member has read all of g's words
+// nobody reads the previous group's any more, and it clears its own two words of that group
+// (plain stores, nothing waited for).  The last group's words are cleared by the member that
+// counts itself out of the team last (one returning atomic per workgroup and launch).  With a
+// member that timed out, words may be cleared before it read them: it then recomputes those
+// partials as it does for any absent word, and still clears its own words afterwards.
+__device__ __forceinline__ void gnt_clear_own(uint64_t* slots, int chunks, int64_t gprev, uint32_t m) {
+    if (gprev >= 0 && threadIdx.x == 0) {
+        uint64_t* w = slots + (gprev * chunks + m) * 2;
+        __hip_atomic_store(w, uint64_t(0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(w + 1, uint64_t(0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
+__device__ __forceinline__ void gnt_release_last(uint64_t* slots, int* done, int chunks, int64_t glast,
+                                                 int64_t team) {
+    if (threadIdx.x >= 64) return;  // wave 0
+    int old = 0;
+    if (threadIdx.x == 0)
+        old = __hip_atomic_fetch_add(done + team, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (__builtin_amdgcn_readfirstlane(old) != chunks - 1) return;
+    uint64_t* w = slots + glast * chunks * 2;
+    for (int i = threadIdx.x; i < 2 * chunks; i += 64)
+        __hip_atomic_store(w + i, uint64_t(0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (threadIdx.x == 0) __hip_atomic_store(done + team, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // Block-reduce (a, b) as the two-pass kernels do and publish them as chunk m's words.
 __device__ __forceinline__ void gnt_reduce_publish(float a, float b, float* red, uint64_t* slot) {
     a = wave_sum(a);
@@ -608,7 +642,7 @@ __device__ __forceinline__ void gnp_fwd_group(const float* __restrict__ x, const
                                               float (&vn)[PER][4], GnpBuf& bn, float (*tab)[GNP_MAX_CG],
                                               float* red, float* sv, int* miss, float* __restrict__ z,
                                               float* __restrict__ mean_out,
-                                              float* __restrict__ rstd_out) {
+                                              float* __restrict__ rstd_out, int64_t gprev) {
     const int t = threadIdx.x;
     const GroupCtx c = group_ctx_at<4>(x, G, gi, m);
     if (t < G.Cg) tab[0][t] = bf.ga, tab[1][t] = bf.be, tab[2][t] = bf.bi;
@@ -660,11 +694,12 @@ __device__ __forceinline__ void gnp_fwd_group(const float* __restrict__ x, const
         }
         gnt_store(rz, vo, i, o);  // past the chunk end: dropped
     }
+    gnt_clear_own(slots, G.chunks, gprev, m);
 }
 
 template <bool ACT, int PER>
 __global__ __launch_bounds__(kBlock, SP_GN_FWD_WPC) void k_gn_fwd_pipe(const float* __restrict__ x, GnGeom G,
-                                                           uint64_t* __restrict__ slots, int nteams,
+                                                           uint64_t* __restrict__ slots, int* done, int nteams,
                                                            int64_t ngroups, float* __restrict__ z,
                                                            float* __restrict__ mean_out,
                                                            float* __restrict__ rstd_out) {
@@ -677,19 +712,21 @@ __global__ __launch_bounds__(kBlock, SP_GN_FWD_WPC) void k_gn_fwd_pipe(const flo
     if (gi >= ngroups) return;
     float va[PER][4], vb[PER][4];
     GnpBuf ba, bb;
+    const int64_t team = gi;
     gnp_issue<PER>(x, G, gi, m, va, ba);
     for (;;) {  // two groups per trip: the register buffers are named, not indexed
         int64_t gn = gi + nteams < ngroups ? gi + nteams : -1;
         gnp_fwd_group<ACT, PER>(x, G, slots, gi, gn, m, va, ba, vb, bb, tab[0], red, sv, miss, z,
-                                mean_out, rstd_out);
+                                mean_out, rstd_out, gi - nteams);
         if (gn < 0) break;
         gi = gn;
         gn = gi + nteams < ngroups ? gi + nteams : -1;
         gnp_fwd_group<ACT, PER>(x, G, slots, gi, gn, m, vb, bb, va, ba, tab[1], red, sv, miss, z,
-                                mean_out, rstd_out);
+                                mean_out, rstd_out, gi - nteams);
         if (gn < 0) break;
         gi = gn;
     }
+    gnt_release_last(slots, done, G.chunks, gi, team);
 }
 
 // Backward chunk mm's sums of dy*gamma and dy*gamma*xhat, recomputed from x and dz (the terms
@@ -735,7 +772,8 @@ __device__ __forceinline__ void gnp_bwd_group(
     uint64_t* __restrict__ slots, int64_t gi, int64_t gn, uint32_t m, float (&v)[PER][4],
     float (&g)[PER][4], const GnpBuf& bf, float (&vn)[PER][4], float (&gq)[PER][4], GnpBuf& bn,
     float (*tab)[GNP_MAX_CG], float* red, float* sv, int* miss, float* __restrict__ dx,
-    float* __restrict__ dx2, const float* __restrict__ add1, const float* __restrict__ add2) {
+    float* __restrict__ dx2, const float* __restrict__ add1, const float* __restrict__ add2,
+    int64_t gprev) {
     const int t = threadIdx.x;
     const GroupCtx c = group_ctx_at<4>(x, G, gi, m);
     if (t < G.Cg) tab[0][t] = bf.ga, tab[1][t] = bf.be, tab[2][t] = bf.bi;
@@ -811,13 +849,14 @@ __device__ __forceinline__ void gnp_bwd_group(
         }
         gnt_store(rd, vo, i, o);
     }
+    gnt_clear_own(slots, G.chunks, gprev, m);
 }
 
 template <bool ACT, int PER>
 __global__ __launch_bounds__(kBlock, SP_GN_BWD_WPC) void k_gn_bwd_pipe(
     const float* __restrict__ dz, const float* __restrict__ x, GnGeom G,
     const float* __restrict__ mean_in, const float* __restrict__ rstd_in,
-    uint64_t* __restrict__ slots, int nteams, int64_t ngroups, float* __restrict__ dx,
+    uint64_t* __restrict__ slots, int* done, int nteams, int64_t ngroups, float* __restrict__ dx,
     float* __restrict__ dx2, const float* __restrict__ add1, const float* __restrict__ add2) {
     __shared__ float red[8];
     __shared__ float sv[2 * GNT_MAX_CHUNKS];
@@ -836,18 +875,20 @@ __global__ __launch_bounds__(kBlock, SP_GN_BWD_WPC) void k_gn_bwd_pipe(
 #pragma unroll
         for (int i = 0; i < PER; ++i) gnt_load(rg, vo, i, ga[i]);
     }
+    const int64_t team = gi;
     for (;;) {
         int64_t gn = gi + nteams < ngroups ? gi + nteams : -1;
         gnp_bwd_group<ACT, PER>(dz, x, G, mean_in, rstd_in, slots, gi, gn, m, va, ga, ba, vb, gb,
-                                bb, tab[0], red, sv, miss, dx, dx2, add1, add2);
+                                bb, tab[0], red, sv, miss, dx, dx2, add1, add2, gi - nteams);
         if (gn < 0) break;
         gi = gn;
         gn = gi + nteams < ngroups ? gi + nteams : -1;
         gnp_bwd_group<ACT, PER>(dz, x, G, mean_in, rstd_in, slots, gi, gn, m, vb, gb, bb, va, ga,
-                                ba, tab[1], red, sv, miss, dx, dx2, add1, add2);
+                                ba, tab[1], red, sv, miss, dx, dx2, add1, add2, gi - nteams);
         if (gn < 0) break;
         gi = gn;
     }
+    gnt_release_last(slots, done, G.chunks, gi, team);
 }
 
 // ---- host side --------------------------------------------------------------------------
@@ -874,6 +915,54 @@ static int gn_geom(int64_t n, int32_t c, int64_t hw, int32_t groups, const float
 }
 
 static int g_single_pass = 1;  // sp_groupnorm_single_pass
+#ifndef SP_GN_PERSISTENT
+#define SP_GN_PERSISTENT 1
+#endif
+static int g_persistent = SP_GN_PERSISTENT;  // sp_groupnorm_persistent_slots
+
+// The single-pass kernels' team words and done counts: a library-owned region per (device,
+// stream), zeroed once when allocated — the kernels leave it zero (gnt_settle) — so a call needs
+// no memset.  Without it (disabled, or a stream being captured into a graph when the region
+// would have to grow) the caller's workspace is used and zeroed first.
+struct GntRegion { void* p = nullptr; size_t bytes = 0; };
+static std::mutex g_region_mu;
+static std::map<std::pair<int, hipStream_t>, GntRegion> g_regions;
+
+static int gnt_slots(int64_t ngroups, int chunks, float* work, hipStream_t s, uint64_t** slots, int** done) {
+    const size_t words = (size_t)ngroups * chunks * 16, bytes = words + (size_t)ngroups * 4;
+    int dev = 0;
+    if (g_persistent && hipGetDevice(&dev) == hipSuccess) {
+        std::lock_guard<std::mutex> lk(g_region_mu);
+        GntRegion& r = g_regions[{dev, s}];
+        hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;  // asked only when it must grow
+        if (r.bytes >= bytes || hipStreamIsCapturing(s, &cs) == hipSuccess) {
+            if (r.bytes < bytes && cs == hipStreamCaptureStatusNone) {
+                if (r.p) {  // a kernel on this stream may still use the old region
+                    if (hipStreamSynchronize(s) != hipSuccess) return check_launch("groupnorm slots (sync)");
+                    (void)hipFree(r.p);
+                    r.p = nullptr, r.bytes = 0;
+                }
+                const size_t want = std::max(bytes * 2, (size_t)4 << 20);
+                if (hipMalloc(&r.p, want) == hipSuccess) {
+                    if (hipMemsetAsync(r.p, 0, want, s) != hipSuccess) return check_launch("groupnorm slots (zero)");
+                    r.bytes = want;
+                } else {
+                    (void)hipGetLastError();
+                    r.p = nullptr;
+                }
+            }
+            if (r.bytes >= bytes) {
+                *slots = static_cast<uint64_t*>(r.p);
+                *done = reinterpret_cast<int*>(static_cast<char*>(r.p) + words);
+                return SP_OK;
+            }
+        }
+    }
+    *slots = reinterpret_cast<uint64_t*>(work);
+    *done = reinterpret_cast<int*>(reinterpret_cast<char*>(work) + words);
+    if (hipMemsetAsync(work, 0, bytes, s) != hipSuccess) return check_launch("groupnorm slots (memset)");
+    return SP_OK;
+}
 
 // Teams that fit the chip at once for a single-pass kernel (0: the kernel cannot run).
 static int64_t gnt_teams(const void* kernel, int64_t ngroups, int chunks) {
@@ -895,8 +984,14 @@ extern "C" {
 int64_t sp_groupnorm_workspace(int64_t n, int32_t channels, int64_t hw, int32_t groups) {
     if (n < 0 || channels <= 0 || hw <= 0 || groups <= 0 || channels % groups) return -1;
     const int64_t gs = (int64_t)(channels / groups) * hw;
-    // two-pass: 2 floats per chunk; single pass: 2 64-bit words per chunk
-    return n * groups * ((gs + GN_CHUNK_MIN - 1) / GN_CHUNK_MIN) * 4;
+    // two-pass: 2 floats per chunk; single pass: 2 64-bit words per chunk and a count per group
+    return n * groups * ((gs + GN_CHUNK_MIN - 1) / GN_CHUNK_MIN) * 4 + n * groups;
+}
+
+int sp_groupnorm_persistent_slots(int32_t enable) {
+    const int prev = g_persistent;
+    if (enable >= 0) g_persistent = enable ? 1 : 0;
+    return prev;
 }
 
 int sp_groupnorm_single_pass(int32_t enable) {
@@ -963,13 +1058,13 @@ int sp_groupnorm_silu_fwd2(const float* x, const float* x2, int32_t c1, const fl
                        : (const void*)k_gn_fwd_pipe<false, GN_CHUNK_FWD / 4 / kBlock>;
         const int64_t teams = gnt_teams(kern, ngroups, G.chunks);
         if (teams > 0) {
-            uint64_t* slots = reinterpret_cast<uint64_t*>(work);
-            if (hipMemsetAsync(slots, 0, ngroups * G.chunks * 16, s) != hipSuccess)
-                return check_launch("sp_groupnorm_silu_fwd (slots)");
+            uint64_t* slots;
+            int* done;
+            if (int e = gnt_slots(ngroups, G.chunks, work, s, &slots, &done)) return e;
             const dim3 grid1(static_cast<unsigned>(teams * G.chunks));
             const int nt = static_cast<int>(teams);
 #define SP_GN_FWD_PIPE(AA, PP) \
-    launch(0, k_gn_fwd_pipe<AA, PP>, grid1, blk, s, x, G, slots, nt, ngroups, z, mean, rstd)
+    launch(0, k_gn_fwd_pipe<AA, PP>, grid1, blk, s, x, G, slots, done, nt, ngroups, z, mean, rstd)
             if (chunk == GN_CHUNK_FWD_BIG) {
                 if (act) { SP_GN_FWD_PIPE(true, GN_CHUNK_FWD_BIG / 4 / kBlock); }
                 else { SP_GN_FWD_PIPE(false, GN_CHUNK_FWD_BIG / 4 / kBlock); }
@@ -1030,11 +1125,11 @@ int sp_groupnorm_silu_bwd2(const float* dz, const float* x, const float* x2, int
         auto kern = act ? k_gn_bwd_pipe<true, PER> : k_gn_bwd_pipe<false, PER>;
         const int64_t teams = gnt_teams(reinterpret_cast<const void*>(kern), ngroups, G.chunks);
         if (teams > 0) {
-            uint64_t* slots = reinterpret_cast<uint64_t*>(work);
-            if (hipMemsetAsync(slots, 0, ngroups * G.chunks * 16, s) != hipSuccess)
-                return check_launch("sp_groupnorm_silu_bwd (slots)");
+            uint64_t* slots;
+            int* done;
+            if (int e = gnt_slots(ngroups, G.chunks, work, s, &slots, &done)) return e;
             launch(0, kern, dim3(static_cast<unsigned>(teams * G.chunks)), blk, s, dz, x, G, mean,
-                   rstd, slots, static_cast<int>(teams), ngroups, dx, dx2, add1, add2);
+                   rstd, slots, done, static_cast<int>(teams), ngroups, dx, dx2, add1, add2);
             return check_launch("sp_groupnorm_silu_bwd");
         }
     }

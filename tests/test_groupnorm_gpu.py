@@ -188,13 +188,17 @@ def test_single_pass_matches_two_pass_bitwise(cuda, shape, act):
     a2 = torch.randn(n, c2, h, w, generator=gen).to(cuda) if c2 else None
     outs = []
     prev = lib.sp_groupnorm_single_pass(-1)
+    prev_persistent = lib.sp_groupnorm_persistent_slots(-1)
     recomputed = 0
     try:
         # two-pass; single-pass; single-pass with a poll bound of 0 (every partial not yet
         # published at the first poll is recomputed by the waiting workgroup: the path that
-        # keeps the result exact when a team member is not resident)
-        for mode, spins in ((0, -1), (1, -1), (1, 0)):
+        # keeps the result exact when a team member is not resident); single-pass again (the
+        # library's team-word region must have been left clean by every launch before, the
+        # recomputing ones included); single-pass on the caller's zeroed workspace
+        for mode, spins, persistent in ((0, -1, 1), (1, -1, 1), (1, 0, 1), (1, -1, 1), (1, -1, 0)):
             lib.sp_groupnorm_single_pass(mode)
+            lib.sp_groupnorm_persistent_slots(persistent)
             _hip.check(lib.sp_groupnorm_set_spin_limit(spins), "spin limit")
             before = lib.sp_groupnorm_team_timeouts()
             z, st = gn_forward(layer, x1, x2, cb)
@@ -205,6 +209,7 @@ def test_single_pass_matches_two_pass_bitwise(cuda, shape, act):
                 recomputed = lib.sp_groupnorm_team_timeouts() - before
     finally:
         lib.sp_groupnorm_single_pass(prev)
+        lib.sp_groupnorm_persistent_slots(prev_persistent)
         lib.sp_groupnorm_set_spin_limit(-1)
     for other in outs[1:]:
         for a, b in zip(outs[0], other):
