@@ -1,7 +1,7 @@
 #!/bin/bash
 # Final round-3 measurements on the committed tree (one step per GPU run, each under its own
 # limit; the first failure ends the script).  PART=benches: every bench record and a 2-rank
-# self-launch rehearsal over gloo; PART=profiles: rocprofv3 kernel statistics of the DPS and PSLD
+# self-launch rehearsal over gloo (PART=rest: all but the headline inpaint record); PART=profiles: rocprofv3 kernel statistics of the DPS and PSLD
 # benches.  Output: gpurun_out/final3/.
 set -o pipefail
 PART=${1:-benches}
@@ -10,8 +10,8 @@ O=$R/gpurun_out/final3
 mkdir -p $O
 cd $R
 step() { local t=$1 log=$2; shift 2; echo "[final] $log"; timeout -k 10 $t "$@" > $O/$log 2>&1; local rc=$?; tail -1 $O/$log | cut -c1-160; [ $rc -eq 0 ] || { echo "[final] $log failed rc=$rc"; exit $rc; }; }
-if [ "$PART" = benches ]; then
-  step 300 bench_inpaint.log python -u bench.py
+if [ "$PART" = benches ] || [ "$PART" = rest ]; then
+  [ "$PART" = benches ] && step 300 bench_inpaint.log python -u bench.py
   step 200 bench_blur.log python -u bench.py --config blur --no-cpu-baseline
   step 200 bench_inpaint_512_b16.log python -u bench.py --image 512 --batch 16 --no-cpu-baseline
   step 200 bench_psld.log python -u tools/bench_psld.py
