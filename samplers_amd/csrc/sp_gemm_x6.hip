@@ -98,18 +98,19 @@ constexpr int g6_vmcnt(int n) { return (n & 0xF) | ((n >> 4) << 14) | (0x7 << 4)
 
 // raw X of one k-step -> LDS ring slot ([16 ch][256 px] fp32): 16 direct 1-KB loads, 2 per wave
 // (channel 2 wv + i, lane l: pixels 4l .. 4l + 3)
-__device__ __forceinline__ void g6_dma_x(const G6Geom& g, int n, int p0, int kstep, int wv, int lane,
-                                         unsigned slot) {
+// (xb1 / xb2: image n's planes of x1 / x2, formed once per tile; the channel is a scalar
+// offset, so a load costs a multiply-add, not a 64-bit channel base: the launcher guarantees
+// k hw 4 < 2^31, and hw % 256 == 0 keeps every load inside its plane)
+__device__ __forceinline__ void g6_dma_x(const G6Geom& g, const float* xb1, const float* xb2,
+                                         int p0, int kstep, int wv, int lane, unsigned slot) {
     const int k0 = kstep * G6_KC;
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
         const int c = k0 + 2 * wv + i;
         const bool second = c >= g.c1;
-        const float* base = second ? g.x2 + ((int64_t)n * g.c2 + (c - g.c1)) * g.hw
-                                   : g.x1 + ((int64_t)n * g.c1 + c) * g.hw;
-        const auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), (short)0, g.hw * 4,
-                                                          0x00020000);
-        g6_lds_dma(rs, slot + (2 * wv + i) * 1024, lane * 16, p0 * 4);
+        const auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(second ? xb2 : xb1), (short)0,
+                                                          (second ? g.c2 : g.c1) * g.hw * 4, 0x00020000);
+        g6_lds_dma(rs, slot + (2 * wv + i) * 1024, lane * 16, ((second ? c - g.c1 : c) * g.hw + p0) * 4);
     }
 }
 
@@ -354,21 +355,29 @@ __device__ __forceinline__ void g6_body(const G6Geom& g, G6XSlot* xraw, G6WSlot*
     // two load streams, advanced one k-step at a time (divisions once per tile)
     struct Cursor { int j, tw, s, slot; G6Pos ps; };
     Cursor cx{0, 0, 0, 0, g6_pos(g, b0)}, cw = cx;
+    // the X stream's image bases, renewed when its tile changes
+    const float* xb1 = g.x1 + (int64_t)cx.ps.n * g.c1 * g.hw;
+    const float* xb2 = g.x2 + (int64_t)cx.ps.n * g.c2 * g.hw;
     auto advance = [&](Cursor& c, int nslots) {
         ++c.j;
         c.slot = c.slot + 1 == nslots ? 0 : c.slot + 1;
         if (++c.s == g.nsteps) {
             c.s = 0;
             if (++c.tw < ntile_wg) c.ps = g6_pos(g, b0 + c.tw * G);
+            return true;
         }
+        return false;
     };
     auto dma_x = [&]() {
         if (cx.j < J) {
             const unsigned sl = xraw_lds + cx.slot * (G6_KC * G6_PX * 4);
             if constexpr (LTM) g6_dma_x_tm(g, cx.ps.n * g.hw + cx.ps.p0, cx.s, wv, lane, sl);
-            else g6_dma_x(g, cx.ps.n, cx.ps.p0, cx.s, wv, lane, sl);
+            else g6_dma_x(g, xb1, xb2, cx.ps.p0, cx.s, wv, lane, sl);
         }
-        advance(cx, G6_NX);
+        if (advance(cx, G6_NX) && !LTM) {
+            xb1 = g.x1 + (int64_t)cx.ps.n * g.c1 * g.hw;
+            xb2 = g.x2 + (int64_t)cx.ps.n * g.c2 * g.hw;
+        }
     };
     auto dma_w = [&]() {
         if (cw.j < J) g6_dma_w(wrs, cw.ps.cb * g.nsteps + cw.s, wv, lane, wl_lds + cw.slot * G6_WB);
@@ -560,7 +569,7 @@ extern "C" {
 
 int sp_gemm_x6_supported(int32_t m, int32_t k, int64_t hw) {
     return m >= G6_CO && m % G6_CO == 0 && k >= G6_KC && k % G6_KC == 0 && hw >= G6_PX &&
-           hw % G6_PX == 0 && hw * 32 * 4 < (int64_t(1) << 31);
+           hw % G6_PX == 0 && hw * 32 * 4 < (int64_t(1) << 31) && hw * k * 4 < (int64_t(1) << 31);
 }
 
 int64_t sp_gemm_x6_packed_size(int32_t m, int32_t k) {
