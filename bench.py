@@ -46,7 +46,7 @@ from pathlib import Path
 
 ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
-import samplers_amd  # noqa: E402,F401  (configures the MIOpen find-db / kernel cache)
+import samplers_amd  # noqa: E402,F401
 
 import numpy as np  # noqa: E402
 import torch  # noqa: E402

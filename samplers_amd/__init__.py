@@ -8,6 +8,5 @@ reference; the per-step arithmetic runs in hand-written HIP kernels
 
 __version__ = "0.1.0"
 
-from samplers_amd.runtime import configure_miopen as _configure_miopen
-
-_configure_miopen()
+# MIOpen's find-db seed (samplers_amd/runtime.py) is merged lazily, before the first
+# convolution that falls back to MIOpen (none does in the priors' DPS / PSLD steps).

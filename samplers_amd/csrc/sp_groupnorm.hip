@@ -926,8 +926,12 @@ static int g_persistent = SP_GN_PERSISTENT;  // sp_groupnorm_persistent_slots
 
 // The single-pass kernels' team words and done counts: a library-owned region per (device,
 // stream), zeroed once when allocated — the kernels leave it zero (gnt_settle) — so a call needs
-// no memset.  Without it (disabled, or a stream being captured into a graph when the region
-// would have to grow) the caller's workspace is used and zeroed first.
+// no memset.  Without it (disabled, or a stream being captured into a graph) the caller's
+// workspace is used and zeroed first.  A captured launch never takes the region: a graph may be
+// replayed on another stream while eager work uses the region (two launches would then share
+// team words), and a later eager call that grows the region would free memory the graph's
+// nodes still name.  A captured call's memset is a node of the graph, so each replay starts
+// from zeroed words of its own workspace.
 struct GntRegion { void* p = nullptr; size_t bytes = 0; };
 static std::mutex g_region_mu;
 static std::map<std::pair<int, hipStream_t>, GntRegion> g_regions;
@@ -935,31 +939,30 @@ static std::map<std::pair<int, hipStream_t>, GntRegion> g_regions;
 static int gnt_slots(int64_t ngroups, int chunks, float* work, hipStream_t s, uint64_t** slots, int** done) {
     const size_t words = (size_t)ngroups * chunks * 16, bytes = words + (size_t)ngroups * 4;
     int dev = 0;
-    if (g_persistent && hipGetDevice(&dev) == hipSuccess) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    const bool capturing = hipStreamIsCapturing(s, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone;
+    if (g_persistent && !capturing && hipGetDevice(&dev) == hipSuccess) {
         std::lock_guard<std::mutex> lk(g_region_mu);
         GntRegion& r = g_regions[{dev, s}];
-        hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;  // asked only when it must grow
-        if (r.bytes >= bytes || hipStreamIsCapturing(s, &cs) == hipSuccess) {
-            if (r.bytes < bytes && cs == hipStreamCaptureStatusNone) {
-                if (r.p) {  // a kernel on this stream may still use the old region
-                    if (hipStreamSynchronize(s) != hipSuccess) return check_launch("groupnorm slots (sync)");
-                    (void)hipFree(r.p);
-                    r.p = nullptr, r.bytes = 0;
-                }
-                const size_t want = std::max(bytes * 2, (size_t)4 << 20);
-                if (hipMalloc(&r.p, want) == hipSuccess) {
-                    if (hipMemsetAsync(r.p, 0, want, s) != hipSuccess) return check_launch("groupnorm slots (zero)");
-                    r.bytes = want;
-                } else {
-                    (void)hipGetLastError();
-                    r.p = nullptr;
-                }
+        if (r.bytes < bytes) {
+            if (r.p) {  // a kernel on this stream may still use the old region
+                if (hipStreamSynchronize(s) != hipSuccess) return check_launch("groupnorm slots (sync)");
+                (void)hipFree(r.p);
+                r.p = nullptr, r.bytes = 0;
             }
-            if (r.bytes >= bytes) {
-                *slots = static_cast<uint64_t*>(r.p);
-                *done = reinterpret_cast<int*>(static_cast<char*>(r.p) + words);
-                return SP_OK;
+            const size_t want = std::max(bytes * 2, (size_t)4 << 20);
+            if (hipMalloc(&r.p, want) == hipSuccess) {
+                if (hipMemsetAsync(r.p, 0, want, s) != hipSuccess) return check_launch("groupnorm slots (zero)");
+                r.bytes = want;
+            } else {
+                (void)hipGetLastError();
+                r.p = nullptr;
             }
+        }
+        if (r.bytes >= bytes) {
+            *slots = static_cast<uint64_t*>(r.p);
+            *done = reinterpret_cast<int*>(static_cast<char*>(r.p) + words);
+            return SP_OK;
         }
     }
     *slots = reinterpret_cast<uint64_t*>(work);

@@ -47,44 +47,51 @@ def broadcast_seed(seed: int | None, device: torch.device, group=None) -> int:
 
 
 _MAX_RANK = 8  # trailing dims a gathered shard may have (shape exchange buffer)
+# dtypes a gathered shard may have, by code (exchanged with the shape: an idle rank's
+# placeholder must match the active ranks' dtype byte for byte, or RCCL's all-gather sizes
+# disagree — a bf16 / fp16 network returns in its own dtype)
+_DTYPES = (torch.float32, torch.float16, torch.bfloat16, torch.float64)
 
 
 def _trailing_shape(local: Tensor | None, counts: list[int], rank: int, group=None,
-                    device: torch.device | None = None) -> tuple[int, ...]:
-    """The per-item shape of the gathered tensor, taken from the first rank that holds items.
-    An idle rank (count 0) cannot know it: what a sampler returns depends on its options
-    (PSLD / ReSample with ``decode_output=False`` return latents, not ``x_shape``), so the
-    active ranks' shape is exchanged first (a 72-byte all-gather)."""
-    buf = torch.full((_MAX_RANK + 1,), -1, dtype=torch.int64, device=device)
+                    device: torch.device | None = None) -> tuple[tuple[int, ...], torch.dtype]:
+    """The per-item shape and dtype of the gathered tensor, taken from the first rank that
+    holds items.  An idle rank (count 0) cannot know them: what a sampler returns depends on
+    its options (PSLD / ReSample with ``decode_output=False`` return latents, not
+    ``x_shape``; a reduced-precision network returns its own dtype), so the active ranks'
+    shape and dtype code are exchanged first (an 80-byte all-gather)."""
+    buf = torch.full((_MAX_RANK + 2,), -1, dtype=torch.int64, device=device)
     if local is not None and counts[rank] > 0:
         tail = tuple(local.shape[1:])
         if len(tail) > _MAX_RANK:
             raise ValueError(f"shards with more than {_MAX_RANK} trailing dims")
+        if local.dtype not in _DTYPES:
+            raise ValueError(f"cannot gather shards of dtype {local.dtype}")
         buf[0] = len(tail)
+        buf[1] = _DTYPES.index(local.dtype)
         if tail:
-            buf[1:1 + len(tail)] = torch.tensor(tail, dtype=torch.int64)
-    out = torch.empty((len(counts), _MAX_RANK + 1), dtype=torch.int64, device=device)
+            buf[2:2 + len(tail)] = torch.tensor(tail, dtype=torch.int64)
+    out = torch.empty((len(counts), _MAX_RANK + 2), dtype=torch.int64, device=device)
     dist.all_gather_into_tensor(out.view(-1), buf, group=group)
     first = next(r for r, c in enumerate(counts) if c > 0)
     nd = int(out[first, 0])
-    return tuple(int(v) for v in out[first, 1:1 + nd].tolist())
+    return tuple(int(v) for v in out[first, 2:2 + nd].tolist()), _DTYPES[int(out[first, 1])]
 
 
 def gather_shards(local: Tensor | None, counts: list[int], group=None, *,
-                  device: torch.device | None = None, dtype: torch.dtype = torch.float32) -> Tensor:
+                  device: torch.device | None = None) -> Tensor:
     """All-gather variable-size leading-axis shards into the full tensor on every rank.
     ``local`` may be None on a rank that holds no items (its placeholder takes the trailing
-    shape the active ranks report)."""
+    shape and the dtype the active ranks report)."""
     world = len(counts)
     if world == 1:
         return local
     rank = dist.get_rank(group)
     device = local.device if local is not None else device
     if any(c == 0 for c in counts):
-        tail = _trailing_shape(local, counts, rank, group, device)
+        tail, dtype = _trailing_shape(local, counts, rank, group, device)
         if local is None or counts[rank] == 0:
-            local = torch.empty((0, *tail), device=device, dtype=local.dtype if local is not None
-                                else dtype)
+            local = torch.empty((0, *tail), device=device, dtype=dtype)
     width = max(counts)
     pad = torch.zeros((width, *local.shape[1:]), device=local.device, dtype=local.dtype)
     pad[: local.shape[0]] = local

@@ -217,14 +217,21 @@ class Fp32Boundary:
 
 
 def fp32_view(network):
-    """``network`` itself when it computes in fp32, else an ``Fp32Boundary`` around it.  A
-    network in any other non-float dtype is refused at sampler entry (``TypeError``)."""
+    """``network`` itself when it computes in fp32, else an ``Fp32Boundary`` around it (bf16 /
+    fp16: the samples, guidance and bridge updates are fp32, wider than the network's own
+    dtype).  A float64 network is refused at sampler entry: the reference runs its whole loop in
+    ``epsilon_net.dtype`` (``dps.py:83-87``), and the fp32 hot path would silently return fp32
+    precision in a float64 tensor.  Any other dtype is refused too (``TypeError``)."""
     dt = getattr(network, "dtype", torch.float32)
     if dt == torch.float32:
         return network
-    if dt not in (torch.bfloat16, torch.float16, torch.float64):
+    if dt == torch.float64:
+        raise TypeError("float64 ε-networks are not supported: the MI355X path samples in fp32 "
+                        "(the reference would run the whole loop in float64); cast the network "
+                        "with .to(torch.float32)")
+    if dt not in (torch.bfloat16, torch.float16):
         raise TypeError(f"ε-network dtype {dt} is not a floating-point type the samplers accept "
-                        "(float32, bfloat16, float16, float64)")
+                        "(float32, bfloat16, float16)")
     return Fp32Boundary(network)
 
 

@@ -170,6 +170,15 @@ class GroupNormAct(nn.GroupNorm):
 # 3x3 convolution on fp32 MFMA
 # ---------------------------------------------------------------------------------------
 
+def miopen_fallback(x: Tensor) -> None:
+    """Before a device convolution goes to MIOpen: point its find-db / kernel cache at the
+    seeded in-tree directory (``runtime.ensure_miopen``, once per process)."""
+    if x.is_cuda:
+        from samplers_amd.runtime import ensure_miopen
+
+        ensure_miopen()
+
+
 def conv_backend() -> str:
     """``SAMPLERS_AMD_CONV``: ``auto`` (default: Winograd F(2x2,3x3) tile where its shape
     rules hold, else the direct tile, else MIOpen), ``direct`` (direct tile or MIOpen),
@@ -204,6 +213,7 @@ def conv3x3_forward(module: "Conv3x3", x: Tensor, res: Tensor | None = None,
     bias = module.bias if bias is None else bias.contiguous()
     algo = _conv_algo(lib, cin, cout, h, w, conv_backend())
     if algo is None:
+        miopen_fallback(x)
         y = F.conv2d(x, module.weight, bias, padding=1)
         return y if res is None else y.add_(res)
     x = x.contiguous()
@@ -233,6 +243,7 @@ def conv3x3_input_vjp(module: "Conv3x3", dy: Tensor, x_shape) -> Tensor:
     algo = _conv_algo(lib, cout, cin, h, w, conv_backend())
     dy = dy.contiguous()
     if algo is None:
+        miopen_fallback(dy)
         return torch.nn.grad.conv2d_input(tuple(x_shape), module.weight, dy, padding=1)
     dx = torch.empty(tuple(x_shape), device=dy.device, dtype=torch.float32)
     if algo == "thin":
@@ -311,6 +322,7 @@ class Conv3x3(nn.Conv2d):
             n, cin, h, w = x.shape
             if _conv_algo(lib, cin, self.out_channels, h, w, conv_backend()) is not None:
                 return _Conv3x3Fn.apply(x, self.weight, self.bias, self)
+        miopen_fallback(x)
         return super().forward(x)
 
 
@@ -489,6 +501,7 @@ def conv3x3_stride2(module: nn.Conv2d, x: Tensor, padding: int) -> Tensor:
     resolution where they serve the shape, else torch / MIOpen."""
     if strided_full_supported(module, x):
         return _ConvS2FullFn.apply(x, module.weight, module.bias, module, 0 if padding else 1)
+    miopen_fallback(x)
     return module(x) if padding else module(F.pad(x, (0, 1, 0, 1)))
 
 
@@ -710,6 +723,7 @@ def conv1x1_small(conv: nn.Conv2d, x: Tensor) -> Tensor:
         w2d = conv.weight.detach().reshape(co, c).contiguous()
         b = None if conv.bias is None else conv.bias.detach().contiguous()
         return _Conv1x1SmallFn.apply(x, w2d, b)
+    miopen_fallback(x)
     return conv(x)
 
 

@@ -30,8 +30,8 @@ from torch import Tensor, nn
 
 from .. import _hip
 from .layers import (Conv3x3, GroupNormAct, Linear, SkipGrad, conv3x3_forward, conv3x3_input_vjp,
-                     downsample_conv, gn_backward, gn_forward, proj_nchw_to_tokens, proj_tokens_to_nchw,
-                     upsample_nearest2x)
+                     downsample_conv, gn_backward, gn_forward, miopen_fallback, proj_nchw_to_tokens,
+                     proj_tokens_to_nchw, upsample_nearest2x)
 
 
 @dataclass(frozen=True)
@@ -267,6 +267,7 @@ class ResnetBlock2D(nn.Module):
         # silu(norm2(h + temb_proj)): the time-embedding add rides in the fused norm
         h = self.conv2(self.norm2(h, tb))
         if self.conv_shortcut is not None:
+            miopen_fallback(x)
             x = self.conv_shortcut(x)
         return x + h
 

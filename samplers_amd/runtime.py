@@ -9,6 +9,11 @@ seeds it with ``samplers_amd/miopen_db/*.ufdb.txt`` — solver choices measured
 on MI355X by this project's own runs (a text table of solver names and
 timings, not code).  Existing settings of MIOPEN_USER_DB_PATH /
 MIOPEN_CUSTOM_CACHE_DIR are respected.
+
+The priors' convolutions run on this project's tiles, so MIOpen only serves
+shapes outside the tiles' rules; ``ensure_miopen`` runs the setup once, right
+before the first such fallback (MIOpen reads the variables when torch creates
+its handle, at the first MIOpen convolution), not at import.
 """
 
 from __future__ import annotations
@@ -52,6 +57,17 @@ def configure_miopen() -> Path | None:
     except OSError:
         pass
     return cache
+
+
+_CONFIGURED = [False]
+
+
+def ensure_miopen() -> None:
+    """``configure_miopen`` once per process; called by the MIOpen fallbacks of
+    ``networks/layers.py`` before they reach ``F.conv2d`` / ``nn.Conv2d``."""
+    if not _CONFIGURED[0]:
+        _CONFIGURED[0] = True
+        configure_miopen()
 
 
 def _merge_find_db(src: Path, dst: Path) -> None:

@@ -3,11 +3,27 @@
 from __future__ import annotations
 
 import functools
+import warnings
 from abc import ABC
 
 from samplers_amd import _hip
 from samplers_amd.dtypes import Shape, Tensor
 from samplers_amd.networks.base import EpsilonNetwork, fp32_view, output_dtype
+
+
+_RECOMPUTE_WARNED = [False]
+
+
+def _warn_recomputed(count: int) -> None:
+    """One warning per process when a solve had to recompute GroupNorm team partials: the
+    result is exact, but every such group waited out the spin budget first, so a solve sharing
+    the GPU with another process (team members not resident) can run far slower than usual."""
+    if count > 0 and not _RECOMPUTE_WARNED[0]:
+        _RECOMPUTE_WARNED[0] = True
+        warnings.warn(f"single-pass GroupNorm recomputed {count} chunk partials whose team member "
+                      "was not resident (exact results; each cost a full spin-wait): is another "
+                      "process using this GPU's CUs?  sp_groupnorm_single_pass(0) selects the "
+                      "two-pass kernels", RuntimeWarning, stacklevel=3)
 
 
 def _guarded(call):
@@ -16,6 +32,7 @@ def _guarded(call):
         with _hip.solve_guard() as guard:
             out = call(self, *args, **kwargs)
         self.last_groupnorm_recomputed = guard.recomputed
+        _warn_recomputed(guard.recomputed)
         return out
 
     return run

@@ -355,3 +355,7 @@ def test_fp32_view_of_networks():
     assert b.n == 7
     with pytest.raises(TypeError, match="dtype"):
         fp32_view(Net(torch.int32))
+    # float64: refused with a message saying why (fp32 samples in a float64 tensor would be a
+    # silent precision loss against the reference's float64 loop)
+    with pytest.raises(TypeError, match="float64"):
+        fp32_view(Net(torch.float64))

@@ -155,7 +155,7 @@ LATENT = (2, 2, 3)  # a latent shape unlike SHAPE (PSLD / ReSample with decode_o
 
 
 def coupled_sampler(problem, *, num_reconstructions, seed, sample_offset, group=None,
-                    decode_output=True):
+                    decode_output=True, out_dtype=None):
     """A PSLD-like sampler: every sample is scaled by a batch-global sum of squares,
     reduced over ``group`` three times (one per 'step'); the R axis is always kept.
     ``decode_output=False`` returns a latent-shaped slice, as PSLD / ReSample do."""
@@ -170,42 +170,49 @@ def coupled_sampler(problem, *, num_reconstructions, seed, sample_offset, group=
     if not decode_output:
         out = out.reshape(obs.shape[0], num_reconstructions, -1)[..., :12].reshape(
             obs.shape[0], num_reconstructions, *LATENT)
-    return out
+    return out if out_dtype is None else out.to(out_dtype)  # a bf16 / fp16 network's dtype
 
 
-def _coupled_worker(rank, world, port, batch, R, decode, result_path):
+def _coupled_worker(rank, world, port, batch, R, decode, result_path, out_dtype=None):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         obs = torch.arange(1, batch * N + 1, dtype=torch.float32).reshape(batch, *SHAPE)
         prob = InverseProblem(IdentityOperator(SHAPE), obs, GaussianNoise(0.1))
         out = sharded_call(coupled_sampler, prob, num_reconstructions=R, seed=3,
-                           decode_output=decode)
+                           decode_output=decode, out_dtype=out_dtype)
+        assert out.dtype == (out_dtype or torch.float32)  # the idle rank's too
         if rank == 0:
             torch.save(out, result_path)
         # a second call on the same world reuses the cached subgroup of active ranks
         again = sharded_call(coupled_sampler, prob, num_reconstructions=R, seed=3,
-                             decode_output=decode)
+                             decode_output=decode, out_dtype=out_dtype)
         assert torch.equal(again, out)
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,batch,R,decode", [(2, 5, 1, True), (3, 2, 2, True),
-                                                  (4, 3, 1, False)])
-def test_sharded_coupled_sampler_equals_single_process(tmp_path, world, batch, R, decode):
+@pytest.mark.parametrize("world,batch,R,decode,out_dtype", [
+    (2, 5, 1, True, None), (3, 2, 2, True, None), (4, 3, 1, False, None),
+    (3, 2, 1, True, torch.bfloat16), (3, 1, 2, False, torch.float16)])
+def test_sharded_coupled_sampler_equals_single_process(tmp_path, world, batch, R, decode,
+                                                       out_dtype):
     """(3, 2, 2): one rank holds no observation and must not be waited for by the others'
     per-step reductions (they reduce over the subgroup of active ranks).  (4, 3, 1, False):
     an idle rank while the sampler returns latents — its placeholder shard takes the shape
-    the active ranks report, not x_shape."""
+    the active ranks report, not x_shape.  The reduced-precision cases: an idle rank's
+    placeholder takes the active ranks' dtype (a float32 placeholder beside bf16 shards would
+    make the all-gather's byte counts disagree)."""
     path = tmp_path / "out.pt"
-    mp.spawn(_coupled_worker, args=(world, _free_port(), batch, R, decode, str(path)),
+    mp.spawn(_coupled_worker, args=(world, _free_port(), batch, R, decode, str(path), out_dtype),
              nprocs=world, join=True)
     sharded = torch.load(path, weights_only=True)
     obs = torch.arange(1, batch * N + 1, dtype=torch.float32).reshape(batch, *SHAPE)
     prob = InverseProblem(IdentityOperator(SHAPE), obs, GaussianNoise(0.1))
     single = sharded_call(coupled_sampler, prob, num_reconstructions=R, seed=3,
-                          decode_output=decode)
+                          decode_output=decode, out_dtype=out_dtype)
+    assert sharded.dtype == single.dtype
     assert single.shape == (batch, R, *(SHAPE if decode else LATENT))  # R kept
     assert sharded.shape == single.shape
-    assert torch.allclose(sharded, single, rtol=1e-6, atol=0)
+    rtol = 1e-6 if out_dtype is None else 1e-2
+    assert torch.allclose(sharded.float(), single.float(), rtol=rtol, atol=0)
