@@ -97,15 +97,15 @@ def free_port() -> int:
         return int(s.getsockname()[1])
 
 
-def launch_command(argv: list[str], gpus: int, port: int) -> list[str]:
-    """The torch.distributed.run command that starts `gpus` ranks of this script with the
-    same arguments (one process per GPU, rendezvous on 127.0.0.1)."""
+def launch_command(argv: list[str], gpus: int, port: int, script: str | None = None) -> list[str]:
+    """The torch.distributed.run command that starts `gpus` ranks of `script` (this file by
+    default) with the same arguments (one process per GPU, rendezvous on 127.0.0.1)."""
     return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
             f"--nproc-per-node={gpus}", "--master-addr=127.0.0.1", f"--master-port={port}",
-            str(Path(__file__).resolve()), *argv]
+            str(Path(script or __file__).resolve()), *argv]
 
 
-def self_launch(gpus: int, argv: list[str]) -> int | None:
+def self_launch(gpus: int, argv: list[str], script: str | None = None) -> int | None:
     """`python bench.py --gpus N` without a launcher (no WORLD_SIZE in the environment)
     starts its N ranks itself as a child torch.distributed.run and returns its exit status;
     None when this process is already a rank (or N = 1).  Runs before anything touches the
@@ -118,7 +118,7 @@ def self_launch(gpus: int, argv: list[str]) -> int | None:
     if backend == "nccl" and have < gpus:
         raise SystemExit(f"--gpus {gpus}: only {have} GPU(s) visible (RCCL needs one per rank; "
                          "SAMPLERS_AMD_DIST_BACKEND=gloo rehearses more ranks than GPUs)")
-    cmd = launch_command(argv, gpus, free_port())
+    cmd = launch_command(argv, gpus, free_port(), script)
     log(f"starting {gpus} ranks: {' '.join(cmd[1:])}")
     import subprocess
 
@@ -143,6 +143,43 @@ def setup_dist(gpus: int):
         extra = {"device_id": torch.device("cuda", local)} if backend == "nccl" else {}
         dist.init_process_group(backend, rank=rank, world_size=world, **extra)
     return rank, world, torch.device("cuda", local)
+
+
+def measure_gather(x: torch.Tensor, reps: int = 3) -> dict:
+    """The design's only data-path collective: ``distributed.gather_shards`` of the x-hat
+    shards (one ``all_gather_into_tensor``, RCCL over xGMI with backend "nccl"), as the sampler
+    runs it once at the end of a solve (``dps.py:125-130`` is the result it assembles).  Timed
+    like the steps (barrier + device sync on both sides, max over ranks): the first call (it
+    includes the communicator's lazy setup) and the best of `reps` more.  Returns the
+    collective's record for the JSON line: the backend and world size torch.distributed
+    reports, bytes per rank, gathered bytes, and the times."""
+    from samplers_amd.distributed import gather_shards
+
+    world = dist.get_world_size() if dist.is_initialized() else 1
+    rec = {"op": "all_gather_into_tensor (samplers_amd.distributed.gather_shards)",
+           "backend": dist.get_backend() if dist.is_initialized() else None,
+           "world_size": world, "bytes_per_rank": x.numel() * x.element_size(),
+           "gathered_bytes": x.numel() * x.element_size() * world}
+    if world == 1:
+        return dict(rec, gather_ms=0.0, first_gather_ms=0.0, note="one rank: nothing to gather")
+    sync = torch.cuda.synchronize if x.is_cuda else (lambda: None)
+    counts = [x.shape[0]] * world
+    times = []
+    for _ in range(1 + reps):
+        dist.barrier()
+        sync()
+        t0 = time.perf_counter()
+        full = gather_shards(x, counts)
+        sync()
+        dist.barrier()
+        dt = torch.tensor([time.perf_counter() - t0], dtype=torch.float64,
+                          device=x.device if x.is_cuda else None)
+        dist.all_reduce(dt, op=dist.ReduceOp.MAX)
+        times.append(float(dt.item()) * 1e3)
+    if tuple(full.shape) != (x.shape[0] * world, *x.shape[1:]):
+        raise SystemExit(f"gather returned {tuple(full.shape)}")
+    return dict(rec, gather_ms=round(min(times[1:]), 4), first_gather_ms=round(times[0], 4),
+                gathered_shape=list(full.shape))
 
 
 def build_workload(config: str, batch: int, image: int, rank: int, device):
@@ -415,6 +452,8 @@ def main():
     if not torch.isfinite(x).all():
         raise SystemExit("non-finite samples")
 
+    # the x-hat gather that ends a sharded solve (after the clock: once per solve of 998 steps)
+    collective = measure_gather(x)
     kern = kern_warm if graph is not None else timer.summary()
     kern_steps = args.warmup if graph is not None else args.steps  # steps the records cover
     nbytes = guidance_bytes(n, m, index_bytes)
@@ -489,7 +528,9 @@ def main():
         "config": {"workload": f"{CONFIGS[args.config]}, 3x{args.image}x{args.image}, "
                                "ddpm-celebahq-256 prior, 1000-step DDPM schedule",
                    "global_batch": args.batch * world, "per_gpu_batch": args.batch,
-                   "parallelism": f"sample-batch shards x{world}, no data-path collective",
+                   "parallelism": f"sample-batch shards x{world}, no collective inside a step; "
+                                  "one all-gather of x-hat per solve (timed after the steps: "
+                                  "'collective')",
                    "execution": "hipGraph replay of one captured step" if graph is not None
                    else "eager"},
         "roofline": roofline,
@@ -497,6 +538,10 @@ def main():
         "guidance_kernels": {k: {"avg_ms": round(v["avg_ms"], 5), "GB/s": round(v["gbs"], 1)}
                              for k, v in rl.items()},
         "groupnorm_recomputed_partials": guard.recomputed,
+        "collective": collective,
+        # a whole 1000-step solve (998 guided steps) of the same shards including its gather
+        "solve_rate_incl_gather": round(args.batch * world * 998 / (
+            998 * elapsed / args.steps + collective["gather_ms"] / 1e3), 3),
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         log("timing the CPU baseline ...")

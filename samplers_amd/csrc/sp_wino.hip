@@ -23,12 +23,22 @@
 #include "sp_common.h"
 
 #include <algorithm>
+#include <utility>
 
 namespace sp {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+// f(std::integral_constant<int, I>) for I = B .. E - 1, unrolled at compile time
+template <int B, int E, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+    if constexpr (B < E) {
+        f(std::integral_constant<int, B>{});
+        static_for<B + 1, E>(f);
+    }
+}
 
 // V = B^T d B for a 4x4 window d (row-major), B^T = [[1,0,-1,0],[0,1,1,0],[0,-1,1,0],[0,1,0,-1]]
 __device__ __forceinline__ void wino_in(const float (&d)[16], float (&v)[16]) {
@@ -651,10 +661,28 @@ __global__ __launch_bounds__(kBlock, 1) void k_wino3x3_r(WrGeom g) {
 #ifndef SP_WINO_XI
 #define SP_WINO_XI 1
 #endif
+// Load distances of the ξ-split tile (k-steps ahead of use): the input block DX, U DU.  The
+// wave's vector loads complete in issue order (one vmcnt), so the wait for U(q) also waits for
+// every block load issued before it: the two distances have to grow together, or the shorter
+// one sets the effective depth of both.  Round 4 measured deeper rings (XI_NR = 8 slots, the
+// k loop unrolled 8 steps) in the headline step (profiles/round4/wino/ring_depth_ab.txt):
+// (DX, DU) = (3, 2) 220.1 samples/s, (4, 4) 220.5, (5, 4) 219.8, (5, 5) 218.2, (6, 5) 219.4,
+// (6, 6) 218.7, (7, 6) 218.2 — no gain: the k-steps do not wait on load latency (SQ_WAIT_ANY
+// is 5 % of wave cycles; the MFMA pipe is busy 0.85 of the cycles at the clock the chip holds,
+// profiles/round4/wino/sq_counters.txt).  The shallow ring keeps the registers.
+#ifndef SP_WINO_DX
+#define SP_WINO_DX 3
+#endif
+#ifndef SP_WINO_DU
+#define SP_WINO_DU 2
+#endif
+constexpr int XI_DX = SP_WINO_DX, XI_DU = SP_WINO_DU;
+constexpr int XI_NR = (XI_DX > 3 || XI_DU > 3) ? 8 : 4;  // ring slots = unroll of the k loop
+static_assert(XI_DX >= 2 && XI_DX < XI_NR && XI_DU >= 1 && XI_DU < XI_NR, "ring distances");
 
 struct XiRing {
-    WrX xs[4];
-    WrU us[4];       // u[2 cb + j]: channel block cb, ξ 8H + 4j .. + 3
+    WrX xs[XI_NR];
+    WrU us[XI_NR];   // u[2 cb + j]: channel block cb, ξ 8H + 4j .. + 3
     float v[2][8];   // this wave's half of V (slot i = ξ 8H + i) for the current / next step
 };
 
@@ -684,16 +712,22 @@ __device__ __forceinline__ void xi_half(const WinRow& e0, const WinRow& e1, cons
     }
 }
 
+// One k-step q (ring slot K = q mod XI_NR): MFMAs on U(q) and V(q); beside them the loads of
+// the block of step q + DX and of U(q + DU) (XN / UN: those steps belong to the next tile), the
+// block of step q + 1 staged in LDS, its window read and half of V(q + 1) transformed.
 template <int H, int K, bool FIRST, bool XN, bool UN>
 __device__ __forceinline__ void xi_step(const WrGeom& g, const WrSrc& cur, const WrSrc& nxt,
                                         __amdgpu_buffer_rsrc_t urs, int lane, float* xw,
                                         const WxLane& xl, int q, XiRing& r, f32x16 (&acc)[16]) {
     using GE = WGeo<16>;
+    // q as an opaque scalar: the step's load offsets are computed here from it (two scalar
+    // multiply-adds), not hoisted out of the unrolled loop as XI_NR sets of live SGPRs (spills)
+    asm volatile("" : "+s"(q));
     const WrU& u = r.us[K];
     const float(&vc)[8] = r.v[K & 1];
     float(&vn)[8] = r.v[(K + 1) & 1];
     WinRow e[3];
-    const WrX& xb = r.xs[(K + 1) % 4];  // block of step q + 1
+    const WrX& xb = r.xs[(K + 1) % XI_NR];  // block of step q + 1
 #define XI_MFMA(sl)                                                                               \
     acc[sl] = __builtin_amdgcn_mfma_f32_32x32x2f32(u.u[2 * ((sl) >> 3) + (((sl) & 7) >> 2)][(sl) & 3], \
                                                    vc[(sl) & 7], FIRST ? f32x16{} : acc[sl], 0, 0, 0); \
@@ -702,18 +736,24 @@ __device__ __forceinline__ void xi_step(const WrGeom& g, const WrSrc& cur, const
     asm volatile("" ::: "memory");             \
     __builtin_amdgcn_sched_barrier(0)
     XI_MFMA(0);
-    wr_load_x(XN ? nxt : cur, (XN ? q + 3 - g.nsteps : q + 3) * g.so_step, r.xs[(K + 3) % 4]);
+#if SP_WINO_EXP != 1
+    wr_load_x(XN ? nxt : cur, (XN ? q + XI_DX - g.nsteps : q + XI_DX) * g.so_step, r.xs[(K + XI_DX) % XI_NR]);
+#endif
     XI_WALL;
     XI_MFMA(1);
-    const int uso = (UN ? nxt.uso : cur.uso) + (UN ? q + 2 - g.nsteps : q + 2) * g.u_step * 4;
-    WrU& un = r.us[(K + 2) % 4];
+    const int uso = (UN ? nxt.uso : cur.uso) + (UN ? q + XI_DU - g.nsteps : q + XI_DU) * g.u_step * 4;
+    WrU& un = r.us[(K + XI_DU) % XI_NR];
+#if SP_WINO_EXP != 1
     un.u[0] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(urs, lane * 64 + 32 * H, uso, 0));
     un.u[1] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(urs, lane * 64 + 32 * H + 16, uso, 0));
+#endif
     XI_WALL;
     XI_MFMA(2);
+#if SP_WINO_EXP != 1
     un.u[2] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(urs, lane * 64 + 32 * H, uso + 64 * 64, 0));
     un.u[3] = __builtin_bit_cast(f32x4,
                                  __builtin_amdgcn_raw_buffer_load_b128(urs, lane * 64 + 32 * H + 16, uso + 64 * 64, 0));
+#endif
     XI_WALL;
     XI_MFMA(3);
 #pragma unroll
@@ -745,6 +785,17 @@ __device__ __forceinline__ void xi_step(const WrGeom& g, const WrSrc& cur, const
     XI_WALL;
 #undef XI_MFMA
 #undef XI_WALL
+}
+
+// k-steps p + K0 + K for K in the sequence (p % XI_NR == 0).  LAST: the tile's final XI_NR
+// steps, whose loads beyond the tile's last step fetch the next tile's first steps.
+template <int H, bool FIRST, bool LAST, int K0, int... K>
+__device__ __forceinline__ void xi_steps(std::integer_sequence<int, K...>, const WrGeom& g, const WrSrc& cur,
+                                         const WrSrc& nxt, __amdgpu_buffer_rsrc_t urs, int lane, float* xw,
+                                         const WxLane& xl, int p, XiRing& r, f32x16 (&acc)[16]) {
+    (xi_step<H, K0 + K, FIRST && K0 + K == 0, LAST && (K0 + K + XI_DX >= XI_NR),
+             LAST && (K0 + K + XI_DU >= XI_NR)>(g, cur, nxt, urs, lane, xw, xl, p + K0 + K, r, acc),
+     ...);
 }
 
 // Epilogue: row sums of this wave's ξ rows for both channel blocks; the block the partner
@@ -832,17 +883,16 @@ __device__ __forceinline__ void xi_body(const WrGeom& g, int wv, int lane, float
     WrTile tin = wr_tile<GE>(g, tn < g.ntiles ? tn : t, wq);
     WrSrc nxt = wr_src<GE>(g, tin, wq, lane);
 
+    // prologue in the loop's own issue order: X(s), U(s) for s = 0 .. (the first step's loads
+    // are X(DX), U(DU))
     XiRing r;
-    wr_load_x(cur, 0, r.xs[0]);
-    __builtin_amdgcn_sched_barrier(0);
-    wr_load_x(cur, g.so_step, r.xs[1]);
-    __builtin_amdgcn_sched_barrier(0);
-    xi_load_u<H>(urs, lane, cur.uso, r.us[0]);
-    __builtin_amdgcn_sched_barrier(0);
-    wr_load_x(cur, 2 * g.so_step, r.xs[2]);
-    __builtin_amdgcn_sched_barrier(0);
-    xi_load_u<H>(urs, lane, cur.uso + g.u_step * 4, r.us[1]);
-    __builtin_amdgcn_sched_barrier(0);
+    static_for<0, (XI_DX > XI_DU ? XI_DX : XI_DU)>([&](auto S) {
+        constexpr int s = decltype(S)::value;
+        if constexpr (s < XI_DX) wr_load_x(cur, s * g.so_step, r.xs[s]);
+        __builtin_amdgcn_sched_barrier(0);
+        if constexpr (s < XI_DU) xi_load_u<H>(urs, lane, cur.uso + s * static_cast<int>(g.u_step) * 4, r.us[s]);
+        __builtin_amdgcn_sched_barrier(0);
+    });
     {
         wr_stage_x(xw, xl, r.xs[0]);
         const WinRow e0 = wr_window_row<GE>(xw, xl, H + 0), e1 = wr_window_row<GE>(xw, xl, H + 1),
@@ -850,29 +900,26 @@ __device__ __forceinline__ void xi_body(const WrGeom& g, int wv, int lane, float
         xi_half<H>(e0, e1, e2, r.v[0]);
     }
     f32x16 acc[16];
-    const int last = g.nsteps - 4;
+    const int last = g.nsteps - XI_NR;  // >= XI_NR, a multiple of XI_NR (wino3x3's dispatch rule)
+    constexpr auto ring = std::make_integer_sequence<int, XI_NR>{};
+    // the residual (RES: 64 registers per lane) is loaded two steps before the tile's end, so it
+    // does not hold registers across the deep ring's whole last block
+    constexpr int RES_AT = XI_NR - 2;
     for (;;) {
-        xi_step<H, 0, true, false, false>(g, cur, nxt, urs, lane, xw, xl, 0, r, acc);
-        xi_step<H, 1, false, false, false>(g, cur, nxt, urs, lane, xw, xl, 1, r, acc);
-        xi_step<H, 2, false, false, false>(g, cur, nxt, urs, lane, xw, xl, 2, r, acc);
-        xi_step<H, 3, false, false, false>(g, cur, nxt, urs, lane, xw, xl, 3, r, acc);
-        for (int p = 4; p < last; p += 4) {
-            xi_step<H, 0, false, false, false>(g, cur, nxt, urs, lane, xw, xl, p + 0, r, acc);
-            xi_step<H, 1, false, false, false>(g, cur, nxt, urs, lane, xw, xl, p + 1, r, acc);
-            xi_step<H, 2, false, false, false>(g, cur, nxt, urs, lane, xw, xl, p + 2, r, acc);
-            xi_step<H, 3, false, false, false>(g, cur, nxt, urs, lane, xw, xl, p + 3, r, acc);
-        }
+        xi_steps<H, true, false, 0>(ring, g, cur, nxt, urs, lane, xw, xl, 0, r, acc);
+        for (int p = XI_NR; p < last; p += XI_NR)
+            xi_steps<H, false, false, 0>(ring, g, cur, nxt, urs, lane, xw, xl, p, r, acc);
         WrRes rv;
+        xi_steps<H, false, true, 0>(std::make_integer_sequence<int, RES_AT>{}, g, cur, nxt, urs, lane, xw, xl,
+                                    last, r, acc);
         if constexpr (RES) {
             WrTile tf = ti;
             tf.co0 = ti.co0 + 32 * H;
             wr_load_res<GE>(g, tf, wv, lane, rv);
             __builtin_amdgcn_sched_barrier(0);
         }
-        xi_step<H, 0, false, false, false>(g, cur, nxt, urs, lane, xw, xl, last + 0, r, acc);
-        xi_step<H, 1, false, true, false>(g, cur, nxt, urs, lane, xw, xl, last + 1, r, acc);
-        xi_step<H, 2, false, true, true>(g, cur, nxt, urs, lane, xw, xl, last + 2, r, acc);
-        xi_step<H, 3, false, true, true>(g, cur, nxt, urs, lane, xw, xl, last + 3, r, acc);
+        xi_steps<H, false, true, RES_AT>(std::make_integer_sequence<int, XI_NR - RES_AT>{}, g, cur, nxt, urs, lane,
+                                         xw, xl, last, r, acc);
         xi_epilogue<H, RES>(g, ti, wv, lane, acc, rv, ex);
         t = tn;
         if (t >= g.ntiles) break;
@@ -1016,7 +1063,7 @@ static int wino3x3(int kind, const float* x, const float* up, const float* bias,
     } else if (narrow) {
         if (res) launch_w(kind, flops, k_wino3x3_r<true, 8>, gd, bd, st, g);
         else launch_w(kind, flops, k_wino3x3_r<false, 8>, gd, bd, st, g);
-    } else if (SP_WINO_XI) {
+    } else if (SP_WINO_XI && cin % (2 * XI_NR) == 0 && cin >= 4 * XI_NR) {
         if (res) launch_w(kind, flops, k_wino3x3_xi<true>, gd, bd, st, g);
         else launch_w(kind, flops, k_wino3x3_xi<false>, gd, bd, st, g);
     } else {

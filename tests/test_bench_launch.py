@@ -60,3 +60,43 @@ def test_bench_help_runs_without_gpu():
     out = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--help"], capture_output=True,
                          text=True, timeout=120)
     assert out.returncode == 0 and "--gpus" in out.stdout
+
+
+def _gather_worker(rank, world, port, out_path):
+    import os
+
+    import torch
+    import torch.distributed as dist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        x = torch.full((3, 2, 4, 4), float(rank))
+        rec = bench.measure_gather(x, reps=2)
+        if rank == 0:
+            torch.save(rec, out_path)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_measure_gather_records_the_collective(tmp_path):
+    """The bench line's 'collective' record at world size 2 (gloo on CPU): the backend and world
+    size torch.distributed reports, the bytes, the gathered shape, and finite times."""
+    import torch
+    import torch.multiprocessing as mp
+
+    port = bench.free_port()
+    path = tmp_path / "rec.pt"
+    mp.spawn(_gather_worker, args=(2, port, str(path)), nprocs=2, join=True)
+    rec = torch.load(path, weights_only=True)
+    assert rec["backend"] == "gloo" and rec["world_size"] == 2
+    assert rec["bytes_per_rank"] == 3 * 2 * 4 * 4 * 4 and rec["gathered_bytes"] == 2 * rec["bytes_per_rank"]
+    assert rec["gathered_shape"] == [6, 2, 4, 4]
+    assert 0 < rec["gather_ms"] < 60_000 and 0 < rec["first_gather_ms"] < 60_000
+
+
+def test_measure_gather_single_rank():
+    import torch
+
+    rec = bench.measure_gather(torch.zeros(2, 3))
+    assert rec["world_size"] == 1 and rec["gather_ms"] == 0.0 and rec["backend"] is None

@@ -116,12 +116,15 @@ def test_conv3x3_timing_records_flops(cuda, monkeypatch):
 @pytest.mark.parametrize("shape", [(2, 128, 128, 32, 64), (1, 256, 64, 16, 32), (2, 64, 128, 8, 96),
                                    (3, 64, 192, 24, 64), (3, 128, 64, 16, 16), (2, 64, 128, 32, 16),
                                    (1, 512, 512, 16, 16), (3, 64, 128, 8, 8), (5, 512, 512, 8, 8),
-                                   (8, 128, 64, 8, 8), (64, 512, 512, 8, 8), (12, 256, 128, 8, 8)])
+                                   (8, 128, 64, 8, 8), (64, 512, 512, 8, 8), (12, 256, 128, 8, 8),
+                                   (2, 24, 64, 8, 32), (2, 32, 64, 16, 64), (1, 48, 64, 8, 32)])
 def test_winograd_forward_and_input_vjp(cuda, shape):
     """Winograd F(2x2,3x3) tile: fp32 transforms + exact fp32 MFMA accumulation; the
     transforms add F(2,3) rounding, so the bound is 1e-5 relative L2 (vs 2e-6 direct).
     W = 16 shapes run the 4 x 8-tile wave geometry (the UNet's 16x16 level); 8x8 shapes the
-    same geometry over two images side by side (batches not a multiple of 4 included)."""
+    same geometry over two images side by side (batches not a multiple of 4 included).
+    cin = 24 / 48 (not a multiple of twice the ξ-split tile's ring): the W % 32 layers' other
+    kernel; cin = 32: the ξ-split tile's shortest K (its first and last ring blocks only)."""
     n, cin, cout, h, w = shape
     lib = _hip.load_library()
     assert lib.sp_wino3x3_supported(cin, cout, h, w)
@@ -138,12 +141,12 @@ def test_winograd_forward_and_input_vjp(cuda, shape):
     up = torch.empty(int(lib.sp_wino3x3_packed_size(cin, cout)), device=cuda)
     uv = torch.empty_like(up)
     _hip.check(lib.sp_wino3x3_pack(wg.data_ptr(), cout, cin, 0, up.data_ptr(), st), "pack")
-    _hip.check(lib.sp_wino3x3_pack(wg.data_ptr(), cout, cin, 1, uv.data_ptr(), st), "pack")
     y = torch.empty(n, cout, h, w, device=cuda)
     dx = torch.empty_like(xg)
     _hip.check(lib.sp_wino3x3_fwd(xg.data_ptr(), up.data_ptr(), bg.data_ptr(), n, cin, cout, h, w,
                                   y.data_ptr(), st), "wino fwd")
     if lib.sp_wino3x3_supported(cout, cin, h, w):
+        _hip.check(lib.sp_wino3x3_pack(wg.data_ptr(), cout, cin, 1, uv.data_ptr(), st), "pack")
         _hip.check(lib.sp_wino3x3_bwd_input(dyg.data_ptr(), uv.data_ptr(), n, cin, cout, h, w,
                                             dx.data_ptr(), st), "wino bwd")
         rel = ((dx.double().cpu() - gref).norm() / gref.norm()).item()

@@ -35,7 +35,7 @@ import samplers_amd  # noqa: E402,F401
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
-from bench import MFMA_F32_PEAK_TFLOPS, conv_summary, host_cpu, setup_dist  # noqa: E402
+from bench import MFMA_F32_PEAK_TFLOPS, conv_summary, host_cpu, self_launch, setup_dist  # noqa: E402
 
 VAE_FLOP_PER_SAMPLE = 7.13e12
 # SD 1.5 UNet at 64x64 latents: 0.80 TFLOP forward + 0.92 input VJP (torch FlopCounterMode)
@@ -70,6 +70,10 @@ def main():
     Path(args.heartbeat).parent.mkdir(parents=True, exist_ok=True)
     heartbeat(Path(args.heartbeat))
     torch.backends.cudnn.benchmark = False
+    # `--gpus N` without a launcher starts its N ranks itself (before anything touches the GPU)
+    status = self_launch(args.gpus, sys.argv[1:], script=__file__)
+    if status is not None:
+        sys.exit(status)
     rank, world, dev = setup_dist(args.gpus)
     group = dist.group.WORLD if world > 1 else None
 

@@ -47,7 +47,7 @@ import samplers_amd  # noqa: E402,F401
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
-from bench import MFMA_F32_PEAK_TFLOPS, conv_summary, host_cpu, setup_dist  # noqa: E402
+from bench import MFMA_F32_PEAK_TFLOPS, conv_summary, host_cpu, self_launch, setup_dist  # noqa: E402
 
 sys.path.insert(0, str(ROOT / "tools"))
 from bench_psld import VAE_FLOP_PER_SAMPLE, heartbeat  # noqa: E402
@@ -100,6 +100,10 @@ def main():
     args = p.parse_args()
     Path(args.heartbeat).parent.mkdir(parents=True, exist_ok=True)
     heartbeat(Path(args.heartbeat))
+    # `--gpus N` without a launcher starts its N ranks itself (before anything touches the GPU)
+    status = self_launch(args.gpus, sys.argv[1:], script=__file__)
+    if status is not None:
+        sys.exit(status)
     rank, world, dev = setup_dist(args.gpus)
     group = dist.group.WORLD if world > 1 else None
 
