@@ -113,6 +113,20 @@ int sp_version(void);
 /* Text of the last launch error on this thread ("" if none). */
 const char* sp_last_error(void);
 
+/* Bounds-checked debug build (`make debug` -> samplers_amd/lib/debug/libsamplers_hip.so,
+ * -DSP_DEBUG=1; SURVEY.md §5 "race detection / sanitizers"): the kernels' index / range
+ * invariants (SP_DCHECK) are checked on the device and counted.  No reference counterpart
+ * (the reference has no native code); test and diagnosis tooling.
+ *   sp_debug_build       1 in the debug library, 0 in the release one.
+ *   sp_debug_violations  waits for the device, returns the number of violated checks since the
+ *                        last reset (0 in the release build, < 0 on error); *first_site
+ *                        (nullable) = (source file id << 16) | line of the first one.
+ *   sp_debug_selftest    debug build: one launch whose 64 threads each violate a check (no
+ *                        memory access), to prove the counting works; SP_EINVAL otherwise. */
+int sp_debug_build(void);
+int64_t sp_debug_violations(int32_t reset, int32_t* first_site);
+int sp_debug_selftest(sp_stream_t stream);
+
 /* Number of per-sample partial sums written by sp_dps_residual for `op`
  * (callers allocate batch * sp_rsq_partials(op) floats). */
 int64_t sp_rsq_partials(const sp_op* op);

@@ -14,6 +14,8 @@ from pathlib import Path
 import torch
 
 LIB_PATH = Path(__file__).resolve().parent / "lib" / "libsamplers_hip.so"
+# the bounds-checked debug build (`make debug`; SAMPLERS_HIP_LIB=DEBUG_LIB_PATH selects it)
+DEBUG_LIB_PATH = Path(__file__).resolve().parent / "lib" / "debug" / "libsamplers_hip.so"
 
 SP_OP_IDENTITY, SP_OP_INPAINT, SP_OP_BLUR, SP_OP_MASK = 0, 1, 2, 3
 
@@ -83,6 +85,9 @@ SIGNATURES = {
                                               ctypes.POINTER(ctypes.c_float),
                                               ctypes.POINTER(ctypes.c_double), ctypes.c_int]),
     "sp_last_error": (ctypes.c_char_p, []),
+    "sp_debug_build": (ctypes.c_int, []),
+    "sp_debug_violations": (_I64, [ctypes.c_int32, ctypes.POINTER(ctypes.c_int32)]),
+    "sp_debug_selftest": (ctypes.c_int, [_P]),
     "sp_rsq_partials": (_I64, [_OPP]),
     "sp_vec_partials": (_I64, [_I64]),
     "sp_dps_residual": (ctypes.c_int, [_OPP, _P, _P, _P, _I64, _I64, _COP, _P, _P, _P]),
@@ -226,6 +231,16 @@ def check(status: int, what: str) -> None:
     if status != 0:
         detail = load_library().sp_last_error().decode(errors="replace")
         raise HipLibraryError(f"{what} failed: {_ERRORS.get(status, status)} {detail}".strip())
+
+
+def debug_violations(reset: bool = True) -> tuple[int, str | None]:
+    """(violated SP_DCHECK invariants since the last reset, "file-id:line" of the first) from the
+    bounds-checked debug library; (0, None) under the release library.  Waits for the device."""
+    site = ctypes.c_int32(0)
+    n = int(load_library().sp_debug_violations(int(reset), ctypes.byref(site)))
+    if n < 0:
+        check(n, "sp_debug_violations")
+    return n, (f"{site.value >> 16}:{site.value & 0xFFFF}" if n else None)
 
 
 class solve_guard:

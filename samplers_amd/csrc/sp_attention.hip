@@ -29,6 +29,7 @@
 // 2 d/4 + 4 ceil(d/16), dk/dv 2 d/4 + 8 ceil(d/16) (useful FLOP: 4 d per block entry forward,
 // 10 d backward).
 
+#define SP_TU 10  // debug-build site numbering (sp_common.h SP_DCHECK)
 #include "sp_common.h"
 
 #include <algorithm>
@@ -139,6 +140,7 @@ __global__ __launch_bounds__(kBlock) void k_attn_fwd(const float* __restrict__ q
     const int64_t base = at_base(blockIdx.y, heads, n, rs, D);
     const int q0 = blockIdx.x * G::WB + wv * G::QT * 16;
     const int64_t kvb = kv.base(blockIdx.y, heads, D);
+    SP_DCHECK(rs >= heads * D && ro >= heads * D && (int64_t)blockIdx.x * G::WB < n && kv.m > 0);
     const float* __restrict__ kb = k + kvb;
     const float* __restrict__ vb = v + kvb;
     const int m_keys = kv.m;

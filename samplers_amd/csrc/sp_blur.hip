@@ -24,6 +24,7 @@
 
 #include <utility>
 
+#define SP_TU 2  // debug-build site numbering (sp_common.h SP_DCHECK)
 #include "sp_common.h"
 
 namespace sp {
@@ -807,6 +808,9 @@ __global__ __launch_bounds__(64 * G, 2) void k_blur_dps_reg(
     const bool flip = sg & 1;  // odd segments sweep bottom-up (see k_blur_dps_dma)
     const int s0 = flip ? H - (sg + 1) * SEG : sg * SEG;
     const bool top = s0 == 0;  // the only segments that meet an image edge in sweep coordinates
+    // the unit's segment inside its plane, the plane inside the batch, partials in range
+    SP_DCHECK(s0 >= 0 && s0 + SEG <= H && H % SEG == 0 && op.width == SWID && c < C &&
+              c * nseg + sg < P && (int64_t)b * C * nseg < (int64_t)units);
     const int64_t plane = (int64_t)H * SWID;
     const int pbytes = static_cast<int>(plane * 4);
     const auto xr = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(x + pl * plane), (short)0, pbytes, 0x00020000);

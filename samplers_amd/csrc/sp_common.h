@@ -17,6 +17,48 @@ namespace sp {
 #define SP_NT_STORE 0
 #endif
 
+// ---------------------------------------------------------------------------
+// Bounds-checked debug build (`make debug`: -DSP_DEBUG=1, samplers_amd/lib/debug/).
+// SP_DCHECK(cond) states an index / range invariant of a kernel.  In the debug build a
+// violated one is counted in a per-translation-unit device word, with the site of the first
+// (SP_TU << 16 | __LINE__; SP_TU numbers the source files, 0 = this header); the kernel then
+// goes on unchanged (a check never alters what a kernel reads or writes — the buffer range
+// checks of the release build stay as they are), and sp_debug_violations() reads the counts
+// after a device sync.  The release build compiles the checks away.
+// ---------------------------------------------------------------------------
+#ifndef SP_DEBUG
+#define SP_DEBUG 0
+#endif
+#ifndef SP_TU
+#define SP_TU 0
+#endif
+#if SP_DEBUG
+static __device__ unsigned int g_dcheck[2];  // violations, first site
+__attribute__((unused)) static __device__ __noinline__ void dcheck_fail(unsigned site) {
+    if (atomicAdd(&g_dcheck[0], 1u) == 0u) atomicExch(&g_dcheck[1], site);
+}
+#define SP_DCHECK(cond)                                                     \
+    do {                                                                    \
+        if (!(cond)) ::sp::dcheck_fail((unsigned(SP_TU) << 16) | __LINE__); \
+    } while (0)
+// host side: every translation unit registers a reader of its two words (sp_dps.hip)
+typedef int (*dcheck_reader)(unsigned* out, int reset);
+void dcheck_register(dcheck_reader r);
+static int dcheck_read_tu(unsigned* out, int reset) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_dcheck), sizeof(g_dcheck)) != hipSuccess) return -1;
+    if (reset) {
+        const unsigned zero[2] = {0u, 0u};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_dcheck), zero, sizeof(zero)) != hipSuccess) return -1;
+    }
+    return 0;
+}
+static const int g_dcheck_registered = (dcheck_register(&dcheck_read_tu), 0);
+#else
+#define SP_DCHECK(cond) \
+    do {                \
+    } while (0)
+#endif
+
 constexpr int kBlock = 256;       // 4 waves of 64 lanes
 constexpr int kIter = SP_KITER;   // float4 groups per thread per block (elementwise kernels)
 

@@ -19,6 +19,7 @@
 // fp32-MFMA peak on the UNet/VAE layer shapes (MIOpen: 104-130); 4x8 / 8x4 / 8x8 /
 // 2x8 (channels x rows) tiles measured 133 / 114-121 / 126-129 / 132-136.
 
+#define SP_TU 5  // debug-build site numbering (sp_common.h SP_DCHECK)
 #include "sp_common.h"
 
 namespace sp {
@@ -102,6 +103,8 @@ __global__ __launch_bounds__(kBlock, SP_CONV_MINB) void k_conv3x3(const float* _
     const int n = blockIdx.x / per_img, t = blockIdx.x - n * per_img;
     const int h0 = (t / tiles_w) * CV_TPH, w0 = (t - (t / tiles_w) * tiles_w) * CV_TPW;
     const int co0 = blockIdx.y * CV_M;
+    SP_DCHECK(W % CV_TPW == 0 && H % CV_TPH == 0 && co0 + CV_M <= cout && cin % CV_CI == 0 &&
+              h0 + CV_TPH <= H && w0 + CV_TPW <= W);
     const int64_t plane = (int64_t)H * W;
     const float* __restrict__ xn = x + (int64_t)n * cin * plane;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, hh = lane >> 5, l = lane & 31;

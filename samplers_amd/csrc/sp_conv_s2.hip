@@ -23,6 +23,7 @@
 // output channel) and one packed weight chunk (4 co x 9 taps x 128 ci).  The stores write
 // both column phases of a row as one float2 per lane.
 
+#define SP_TU 8  // debug-build site numbering (sp_common.h SP_DCHECK)
 #include "sp_common.h"
 
 namespace sp {
@@ -115,6 +116,8 @@ __global__ __launch_bounds__(kBlock, 2) void k_conv3x3_s2(const float* __restric
     const int n = blockIdx.x / per_img, t = blockIdx.x - n * per_img;
     const int h0 = (t / tiles_w) * S2_TPH, w0 = (t - (t / tiles_w) * tiles_w) * S2_TPW;
     const int co0 = blockIdx.y * S2_M;
+    SP_DCHECK(Wo % S2_TPW == 0 && Ho % S2_TPH == 0 && co0 + S2_M <= cout && cin % S2_CI == 0 &&
+              h0 + S2_TPH <= Ho && w0 + S2_TPW <= Wo);
     const int64_t plane = (int64_t)H * W, oplane = (int64_t)Ho * Wo;
     const float* __restrict__ xn = x + (int64_t)n * cin * plane;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, hh = lane >> 5, l = lane & 31;
@@ -236,6 +239,8 @@ __global__ __launch_bounds__(kBlock, 2) void k_conv3x3_s2_bwd(const float* __res
     const int n = blockIdx.x / per_img, t = blockIdx.x - n * per_img;
     const int i0 = (t / tiles_w) * S2B_TH, j0 = (t - (t / tiles_w) * tiles_w) * S2B_TW;
     const int ci0 = blockIdx.y * S2B_M;
+    SP_DCHECK(Wo % S2B_TW == 0 && Ho % S2B_TH == 0 && ci0 + S2B_M <= cin && cout % S2B_CO == 0 &&
+              i0 + S2B_TH <= Ho && j0 + S2B_TW <= Wo);
     const int64_t plane = (int64_t)H * W, oplane = (int64_t)Ho * Wo;
     const float* __restrict__ dyn = dy + (int64_t)n * cout * oplane;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, hh = lane >> 5, l = lane & 31;

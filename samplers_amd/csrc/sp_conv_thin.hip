@@ -20,6 +20,7 @@
 // Round 3: the 8 x 64 tile with two pixels per thread and scalar FMAs (no prefetch) ran the
 // UNet's conv_out (64 x 128 -> 3 at 256^2) in 725 us = 0.38 of HBM peak on its 2.2 GB input.
 
+#define SP_TU 7  // debug-build site numbering (sp_common.h SP_DCHECK)
 #include "sp_common.h"
 
 namespace sp {
@@ -61,6 +62,7 @@ __device__ __forceinline__ void thin_block(int& tile, int& cob, int64_t& n) {
     tile = static_cast<int>(l % X);
     cob = static_cast<int>((l / X) % Y);
     n = l / (X * Y);
+    SP_DCHECK(l < T && n < gridDim.z);  // the remap is a permutation of the grid
 }
 
 typedef float tn_f2 __attribute__((ext_vector_type(2)));

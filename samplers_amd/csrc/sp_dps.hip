@@ -15,6 +15,7 @@
 #include <mutex>
 #include <vector>
 
+#define SP_TU 1  // debug-build site numbering (sp_common.h SP_DCHECK)
 #include "sp_common.h"
 
 namespace sp {
@@ -33,6 +34,18 @@ int check_launch(const char* what) {
     }
     return SP_OK;
 }
+
+#if SP_DEBUG
+// readers of every translation unit's debug words (SP_DCHECK), registered at load time
+static std::vector<dcheck_reader>& dcheck_readers() {
+    static std::vector<dcheck_reader> v;
+    return v;
+}
+void dcheck_register(dcheck_reader r) { dcheck_readers().push_back(r); }
+
+// debug build self-test: every thread of one block states a false invariant (no memory access)
+__global__ void k_dcheck_selftest(int limit) { SP_DCHECK(static_cast<int>(threadIdx.x) < limit); }
+#endif
 
 struct TimingRecord {
     int kind;
@@ -121,6 +134,7 @@ __global__ __launch_bounds__(kBlock) void k_dps_residual(sp_op op, const float* 
                     if ((bits[it] >> e) & 1u) yv[it][e] = yb[r];
                     r += (bits[it] >> e) & 1u;
                 }
+                SP_DCHECK(r <= op.m);  // packed observation index inside the row
             }
         }
     }
@@ -143,6 +157,7 @@ __global__ __launch_bounds__(kBlock) void k_dps_residual(sp_op op, const float* 
         }
     }
     const float t = block_sum(acc, red);
+    SP_DCHECK(static_cast<int>(blockIdx.x) < P);
     if (threadIdx.x == 0) partial[b * P + blockIdx.x] = t;
 }
 
@@ -209,9 +224,11 @@ __global__ __launch_bounds__(kBlock, SP_UPD_WAVES) void k_dps_update(
                     if ((bits[it] >> e) & 1u) yv[it][e] = yb[r];
                     r += (bits[it] >> e) & 1u;
                 }
+                SP_DCHECK(r <= op.m);
             }
         }
     }
+    SP_DCHECK(!partial || P > 0);
     const float inv_a = 1.f / c.a;
     // DPS: gamma / (||r_b|| + eps); without partials a fixed factor (PGDM, PSLD)
     const float scale =
@@ -324,6 +341,7 @@ __global__ __launch_bounds__(kBlock) void k_inpaint_gather(sp_op op, const float
 #pragma unroll
         for (int e = 0; e < V; ++e)
             if ((bits >> e) & 1u) y[b * op.m + rank++] = xv[e];
+        SP_DCHECK(rank <= op.m);
     }
 }
 
@@ -341,6 +359,7 @@ __global__ __launch_bounds__(kBlock) void k_inpaint_scatter(sp_op op, const floa
         inpaint_lookup(op, j, bits, rank);
 #pragma unroll
         for (int e = 0; e < V; ++e) xv[e] = ((bits >> e) & 1u) ? y[b * op.m + rank++] : 0.f;
+        SP_DCHECK(rank <= op.m);
         store_v<V>(x + b * n + j, xv);
     }
 }
@@ -407,6 +426,36 @@ using namespace sp;
 extern "C" {
 
 int sp_version(void) { return 101; }
+
+int sp_debug_build(void) { return SP_DEBUG; }
+
+int64_t sp_debug_violations(int32_t reset, int32_t* first_site) {
+    if (first_site) *first_site = 0;
+#if SP_DEBUG
+    if (hipDeviceSynchronize() != hipSuccess) return check_launch("sp_debug_violations");
+    int64_t total = 0;
+    for (dcheck_reader r : dcheck_readers()) {
+        unsigned w[2] = {0u, 0u};
+        if (r(w, reset) != 0) return check_launch("sp_debug_violations (read)");
+        if (w[0] && first_site && !*first_site) *first_site = static_cast<int32_t>(w[1]);
+        total += w[0];
+    }
+    return total;
+#else
+    (void)reset;
+    return 0;
+#endif
+}
+
+int sp_debug_selftest(sp_stream_t stream) {
+#if SP_DEBUG
+    launch(0, k_dcheck_selftest, dim3(1), dim3(64), static_cast<hipStream_t>(stream), 0);
+    return check_launch("sp_debug_selftest");
+#else
+    (void)stream;
+    return SP_EINVAL;
+#endif
+}
 
 int sp_timing_enable(int on) {
     std::lock_guard<std::mutex> lock(g_timing_mu);

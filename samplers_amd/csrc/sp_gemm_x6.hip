@@ -20,6 +20,7 @@
 // = two adjacent pixels, one per pixel tile) and splits them into the three bf16 terms in
 // registers right before its MFMAs.
 
+#define SP_TU 11  // debug-build site numbering (sp_common.h SP_DCHECK)
 #include "sp_common.h"
 
 #include <algorithm>
@@ -193,6 +194,9 @@ __device__ __forceinline__ G6Pos g6_pos(const G6Geom& g, int t) {
     const int lb = (g.ntiles & 7) ? t : (t & 7) * (g.ntiles >> 3) + (t >> 3);
     const int cb = lb % g.cob, rest = lb / g.cob;
     const int n = rest / g.ptiles;
+    // the tile inside the grid's work, its pixels inside the plane (or the token rows)
+    SP_DCHECK(t >= 0 && t < g.ntiles && lb < g.ntiles && cb * G6_CO < g.o1 + g.o2 + G6_CO &&
+              (rest - n * g.ptiles + 1) * G6_PX <= (g.tokens ? g.tokens : g.hw));
     return G6Pos{n, (rest - n * g.ptiles) * G6_PX, cb};
 }
 

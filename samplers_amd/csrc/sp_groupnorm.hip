@@ -17,6 +17,7 @@
 // element (removes the cancellation of plain sum/sum-of-squares); chunk partials are
 // combined in a fixed order (deterministic).  All four passes are HBM-bound.
 
+#define SP_TU 4  // debug-build site numbering (sp_common.h SP_DCHECK)
 #include "sp_common.h"
 
 #include <algorithm>
@@ -157,6 +158,7 @@ __device__ __forceinline__ GroupCtx group_ctx_at(const float* base, const GnGeom
     const uint32_t nv = G.gs / V, per = G.chunk / V;
     c.lo = chunk * per;
     c.hi = min(nv, c.lo + per);
+    SP_DCHECK(chunk < static_cast<uint32_t>(G.chunks) && c.lo < nv && G.chunk % V == 0 && c.g < G.G);
     return c;
 }
 
@@ -649,6 +651,7 @@ __device__ __forceinline__ void gnp_fwd_group(const float* __restrict__ x, const
                                               float* __restrict__ rstd_out, int64_t gprev) {
     const int t = threadIdx.x;
     const GroupCtx c = group_ctx_at<4>(x, G, gi, m);
+    SP_DCHECK(G.Cg <= GNP_MAX_CG);  // the group's channels fit the LDS table
     if (t < G.Cg) tab[0][t] = bf.ga, tab[1][t] = bf.be, tab[2][t] = bf.bi;
     __syncthreads();
     const float K = bf.kx + bf.kb;
@@ -714,6 +717,9 @@ __global__ __launch_bounds__(kBlock, SP_GN_FWD_WPC) void k_gn_fwd_pipe(const flo
     const uint32_t m = blockIdx.x % G.chunks;
     int64_t gi = blockIdx.x / G.chunks;
     if (gi >= ngroups) return;
+    // a chunk fits the registers the kernel was built for; the team words of every group it
+    // visits lie in the region sized for ngroups
+    SP_DCHECK(G.chunk / 4 <= PER * kBlock && G.chunks <= GNT_MAX_CHUNKS && nteams > 0);
     float va[PER][4], vb[PER][4];
     GnpBuf ba, bb;
     const int64_t team = gi;
@@ -780,6 +786,7 @@ __device__ __forceinline__ void gnp_bwd_group(
     int64_t gprev) {
     const int t = threadIdx.x;
     const GroupCtx c = group_ctx_at<4>(x, G, gi, m);
+    SP_DCHECK(G.Cg <= GNP_MAX_CG);  // the group's channels fit the LDS table
     if (t < G.Cg) tab[0][t] = bf.ga, tab[1][t] = bf.be, tab[2][t] = bf.bi;
     __syncthreads();
     const float mean = mean_in[gi], rstd = rstd_in[gi];
@@ -869,6 +876,7 @@ __global__ __launch_bounds__(kBlock, SP_GN_BWD_WPC) void k_gn_bwd_pipe(
     const uint32_t m = blockIdx.x % G.chunks;
     int64_t gi = blockIdx.x / G.chunks;
     if (gi >= ngroups) return;
+    SP_DCHECK(G.chunk / 4 <= PER * kBlock && G.chunks <= GNT_MAX_CHUNKS && nteams > 0);
     float va[PER][4], ga[PER][4], vb[PER][4], gb[PER][4];
     GnpBuf ba, bb;
     gnp_issue<PER>(x, G, gi, m, va, ba);

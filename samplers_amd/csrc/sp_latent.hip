@@ -13,6 +13,7 @@
 
 #include <algorithm>
 
+#define SP_TU 3  // debug-build site numbering (sp_common.h SP_DCHECK)
 #include "sp_common.h"
 
 namespace sp {
@@ -61,6 +62,7 @@ __global__ __launch_bounds__(kBlock) void k_psld_pixel(sp_op op, const float* __
         store_v<V>(atr + b * n + j, ar);
     }
     const float t = block_sum(acc, red);
+    SP_DCHECK(static_cast<int>(blockIdx.x) < P);
     if (threadIdx.x == 0) partial[b * P + blockIdx.x] = t;
 }
 
@@ -266,6 +268,7 @@ __global__ __launch_bounds__(kBlock) void k_pixel_opt(sp_op op, float* __restric
         store_v<V>(vb + j, vv);
     }
     const float t = block_sum(acc, red);
+    SP_DCHECK(static_cast<int>(blockIdx.x) < P);
     if (threadIdx.x == 0) partial[b * P + blockIdx.x] = t;
 }
 

@@ -9,6 +9,7 @@
 // All of them stream HBM: one wave per LayerNorm row (C = 320 / 640 / 1280 channels held
 // in registers, two wave reductions), float4 lanes for GEGLU.  fp32 throughout.
 
+#define SP_TU 12  // debug-build site numbering (sp_common.h SP_DCHECK)
 #include "sp_common.h"
 
 #include <algorithm>
@@ -44,6 +45,7 @@ __global__ __launch_bounds__(kBlock) void k_layernorm_fwd(const float* __restric
     const int64_t r = (int64_t)blockIdx.x * LN_ROWS + (threadIdx.x >> 6);
     if (r >= rows) return;
     const int c4 = c >> 2;
+    SP_DCHECK(c % 4 == 0 && c4 <= NV * 64);  // the row fits the lane's registers
     float4 v[NV];
     ln_load<NV>(x + r * c, c4, lane, v);
     float s = 0.f;

@@ -5,6 +5,7 @@
 // (one float4 of x / dx), two 32-byte row pieces of the 2x image (4 float4) on the other
 // side.  The VJP sums each block in torch's loop order ((0,0) + (0,1)) + (1,0)) + (1,1).
 
+#define SP_TU 9  // debug-build site numbering (sp_common.h SP_DCHECK)
 #include "sp_common.h"
 
 namespace sp {
@@ -18,6 +19,7 @@ __global__ __launch_bounds__(kBlock) void k_upsample2x(const float* __restrict__
     if (t >= rows * w4) return;
     const int64_t r = t / w4;  // input row (plane * h + i)
     const int j = static_cast<int>(t - r * w4);
+    SP_DCHECK(r < rows && j < w4);
     const up_f4 v = reinterpret_cast<const up_f4*>(x)[t];
     const up_f4 lo{v[0], v[0], v[1], v[1]}, hi{v[2], v[2], v[3], v[3]};
     up_f4* o = reinterpret_cast<up_f4*>(y) + (2 * r) * (2 * w4) + 2 * j;

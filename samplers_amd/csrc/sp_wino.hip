@@ -20,6 +20,7 @@
 // usual F(2,3) rounding (|coefficients| <= 1, one 0.5 factor), comparable to MIOpen's
 // own Winograd f2x3 solver that these layers ran on before.
 
+#define SP_TU 6  // debug-build site numbering (sp_common.h SP_DCHECK)
 #include "sp_common.h"
 
 #include <algorithm>
@@ -234,6 +235,7 @@ __device__ __forceinline__ WrTile wr_tile(const WrGeom& g, int t, int wv) {
     // share one), so consecutive logical tiles (the channel blocks of one tile group, then
     // its neighbours) share an L2
     int lb = (g.ntiles & 7) ? t : (t & 7) * (g.ntiles >> 3) + (t >> 3);
+    SP_DCHECK(t >= 0 && t < g.ntiles && lb < g.ntiles);
     int kh = 0;
     if constexpr (GE::SPLIT) kh = lb & 1, lb >>= 1;
     const int co_blk = lb % g.cob, rest = lb / g.cob;
@@ -273,6 +275,18 @@ __device__ __forceinline__ WrSrc wr_src(const WrGeom& g, const WrTile& ti, int w
     s.uso = __builtin_amdgcn_readfirstlane(
         static_cast<int>(((GE::SPLIT ? (int64_t)ti.kh * g.nsteps * g.u_step : 0) +
                           (int64_t)(ti.co0 >> 5) * 64 * 16) * 4));
+#if SP_DEBUG
+    {   // every k-step's input pieces inside this tile's planes, U rows inside the packed U
+        const int64_t span = nimg ? (int64_t)(nimg * g.cin - kofs) * g.plane * 4 : 0;
+        const int64_t last = (int64_t)(g.nsteps - 1) * g.so_step;
+        SP_DCHECK(s.oa == OOB || (s.oa >= 0 && s.oa + last + 16 <= span));
+        SP_DCHECK(s.ob == OOB || (s.ob >= 0 && s.ob + last + 16 <= span));
+        SP_DCHECK(s.oh == OOB || (s.oh >= 0 && s.oh + last + 4 <= span));
+        SP_DCHECK(s.uso >= 0 && (int64_t)s.uso + ((int64_t)(g.nsteps - 1) * g.u_step + 64 * 16) * 4 <=
+                                   (int64_t)g.nsteps * g.ksplit * g.u_step * 4);
+        SP_DCHECK(ti.co0 + 32 <= g.cout && ti.n < g.batch);
+    }
+#endif
     return s;
 }
 
@@ -495,6 +509,9 @@ __device__ __forceinline__ void wr_epilogue(const WrGeom& g, const WrTile& ti, i
         g.out + wr_img0<GE>(g, ti, wv) * g.cout * g.plane, (short)0,
         wr_nimg<GE>(g, ti, wv) * g.cout * g.plane * 4, 0x00020000);
     const int vo = wr_out_voff<GE>(g, ti, wv, lane);
+    // the lane's last output row (channel co0 + 27 + 4 hh, second image row) inside the images
+    SP_DCHECK(wr_nimg<GE>(g, ti, wv) == 0 || GE::MOSAIC ||
+              (int64_t)vo + (27 * (int64_t)g.plane + g.W) * 4 + 8 <= (int64_t)wr_nimg<GE>(g, ti, wv) * g.cout * g.plane * 4);
     // bias[co0 + (lane & 31)] in one register, each row's two values (channels c and c + 4)
     // read out with v_readlane; no bias: a zero-length buffer, whose loads return 0.
     // (Sixteen vector bias registers here get hoisted and spilled while the next tile's
@@ -827,6 +844,7 @@ __device__ __forceinline__ void xi_epilogue(const WrGeom& g, const WrTile& ti, i
     const auto ors = __builtin_amdgcn_make_buffer_rsrc(g.out + (int64_t)tf.n * g.cout * g.plane, (short)0,
                                                        g.cout * g.plane * 4, 0x00020000);
     const int vo = wr_out_voff<GE>(g, tf, wv, lane);
+    SP_DCHECK(tf.n < g.batch && (int64_t)vo + (27 * (int64_t)g.plane + g.W) * 4 + 8 <= (int64_t)g.cout * g.plane * 4);
     const auto brs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(g.bias ? g.bias : g.up), (short)0,
                                                        g.bias ? g.cout * 4 : 0, 0x00020000);
     const float bl = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(brs, (tf.co0 + l) * 4, 0, 0));

@@ -402,6 +402,7 @@ class DPSSampler(PosteriorSampler, Generic[Condition_co]):
         micro_batch: int | None = None,
         timer: KernelTimer | None = None,
         graph: bool = False,
+        callback: Callable[[int, Tensor], None] | None = None,
         **kwargs,
     ) -> Tensor:
         """Run DPS; returns ``(*batch_shape, R, *x_shape)`` (R squeezed when 1).
@@ -412,7 +413,9 @@ class DPSSampler(PosteriorSampler, Generic[Condition_co]):
         flat sample (multi-GPU, keeps Philox streams shard-invariant);
         ``micro_batch`` bounds how many samples share one prior forward+VJP;
         ``graph=True`` replays one hipGraph-captured step for every iteration
-        (``samplers.graph``; Philox noise only) — same samples, no per-launch host work.
+        (``samplers.graph``; Philox noise only) — same samples, no per-launch host work;
+        ``callback(i, x)`` is called after guided iteration ``i`` with the flat sample (a view of
+        the working buffer: copy it to keep it; not with ``graph=True``).
         """
         if args or kwargs:
             print(f"Warning: Unused args={args}, kwargs={kwargs} in DPSSampler")
@@ -458,6 +461,8 @@ class DPSSampler(PosteriorSampler, Generic[Condition_co]):
                         xi = torch.randn_like(x)
                     step(x, i, ts[i], ts[i - 1], ts[0], xi=xi, seed=seed,
                          sample_offset=sample_offset)
+                    if callback is not None:
+                        callback(i, x)
 
             x0_final = view.unflatten(step.predict_x0(x, ts[1]))
             if num_reconstructions == 1 and not keep_reconstruction_dim:

@@ -44,7 +44,14 @@ def test_inpaint_operator_full_size_bit_exact(cuda):
     assert np.array_equal(back, ref)
 
 
-def test_dps_passes_full_size(cuda):
+def _record_max_err(record, v, v_ref, out, out_ref):
+    """max |error| / max |reference| of pass 1's v and pass 2's x' (the tests' 2e-5 bound)."""
+    record("pass1_v_max_err_over_max", float(np.abs(v - v_ref).max() / np.abs(v_ref).max()), 2e-5)
+    record("pass2_x_max_err_over_max", float(np.abs(out - out_ref).max() / np.abs(out_ref).max()),
+           2e-5)
+
+
+def test_dps_passes_full_size(cuda, parity_record):
     op = RandomInpaintingOperator(SHAPE, 0.5, seed=1).to(cuda)
     desc = op.hip_descriptor()
     m = int(desc.m)
@@ -71,11 +78,12 @@ def test_dps_passes_full_size(cuda):
     np.testing.assert_allclose(part.sum(1).cpu().numpy(), rsq_ref, rtol=2e-5)
     out_ref = closed_form.update_pass(x.numpy(), eps.numpy(), v_ref, w.numpy(), rsq_ref,
                                       xi.numpy(), a, k, 0.97, 0.11, 0.05, 1.0)
+    _record_max_err(parity_record, v.cpu().numpy(), v_ref, out.cpu().numpy(), out_ref)
     np.testing.assert_allclose(out.cpu().numpy(), out_ref, rtol=0,
                                atol=2e-5 * np.abs(out_ref).max())
 
 
-def test_blur_passes_full_size(cuda):
+def test_blur_passes_full_size(cuda, parity_record):
     """configs[2]'s two passes at 3 x 256 x 256, 8 samples: the streaming residual pass and
     the update pass (bridge + injected noise + guidance through the re-read v)."""
     b = 8
@@ -102,6 +110,7 @@ def test_blur_passes_full_size(cuda):
     np.testing.assert_allclose(part.sum(1).cpu().numpy(), rsq_ref, rtol=2e-5)
     out_ref = closed_form.update_pass(x.numpy(), eps.numpy(), v_ref, w.numpy(), rsq_ref,
                                       xi.numpy(), a, k, 0.9, 0.2, 0.1, 1.0)
+    _record_max_err(parity_record, v.cpu().numpy(), v_ref, out.cpu().numpy(), out_ref)
     np.testing.assert_allclose(out.cpu().numpy(), out_ref, rtol=0,
                                atol=2e-5 * np.abs(out_ref).max())
 

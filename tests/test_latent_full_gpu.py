@@ -46,9 +46,11 @@ def _fwd_vjp(module_fn, x: torch.Tensor, cot: torch.Tensor):
     return out.detach().cpu(), g.detach().cpu()
 
 
-def _check(name, gpu, cpu):
+def _check(name, gpu, cpu, record=None):
     for tag, a, b in zip(("out", "vjp"), gpu, cpu):
         err = si.relative_error(a, b)
+        if record is not None:
+            record(f"{tag}_rel_l2", err, TOL, module=name)
         assert err < TOL, f"{name} {tag}: rel L2 {err:.3e}"
 
 
@@ -60,7 +62,7 @@ def vae_pair():
     return cpu, copy.deepcopy(cpu).to("cuda:0")
 
 
-def test_vae_decode_512_fwd_vjp_matches_cpu(cuda, vae_pair):
+def test_vae_decode_512_fwd_vjp_matches_cpu(cuda, vae_pair, parity_record):
     cpu, gpu = vae_pair
     gen = torch.Generator().manual_seed(0)
     z = torch.randn(1, 4, 64, 64, generator=gen)
@@ -71,10 +73,10 @@ def test_vae_decode_512_fwd_vjp_matches_cpu(cuda, vae_pair):
     assert any("gn_fwd" in n for n in names), "decoder GroupNorm not on the HIP kernel"
     assert any("upsample2x" in n for n in names)
     assert any("conv3x3_thin" in n for n in names)  # conv_out 128 -> 3
-    _check("decode", got, _fwd_vjp(cpu.decode, z, cot))
+    _check("decode", got, _fwd_vjp(cpu.decode, z, cot), parity_record)
 
 
-def test_vae_encode_512_fwd_vjp_matches_cpu(cuda, vae_pair):
+def test_vae_encode_512_fwd_vjp_matches_cpu(cuda, vae_pair, parity_record):
     cpu, gpu = vae_pair
     gen = torch.Generator().manual_seed(1)
     x = torch.rand(1, 3, 512, 512, generator=gen) * 2 - 1
@@ -83,18 +85,18 @@ def test_vae_encode_512_fwd_vjp_matches_cpu(cuda, vae_pair):
     names = _kernel_names(lambda: gpu.encode_mean(x.to(cuda)))
     assert any("conv3x3_s2" in n for n in names), "encoder downsampling not on the stride-2 tile"
     assert any("wino3x3" in n for n in names)
-    _check("encode", got, _fwd_vjp(cpu.encode_mean, x, cot))
+    _check("encode", got, _fwd_vjp(cpu.encode_mean, x, cot), parity_record)
 
 
-def test_vae_decode_128_batch_matches_cpu(cuda, vae_pair):
+def test_vae_decode_128_batch_matches_cpu(cuda, vae_pair, parity_record):
     cpu, gpu = vae_pair
     gen = torch.Generator().manual_seed(2)
     z = torch.randn(3, 4, 16, 16, generator=gen)
     cot = torch.randn(3, 3, 128, 128, generator=gen)
-    _check("decode128", _fwd_vjp(gpu.decode, z.to(cuda), cot), _fwd_vjp(cpu.decode, z, cot))
+    _check("decode128", _fwd_vjp(gpu.decode, z.to(cuda), cot), _fwd_vjp(cpu.decode, z, cot), parity_record)
 
 
-def test_sd15_unet_fwd_vjp_matches_cpu(cuda):
+def test_sd15_unet_fwd_vjp_matches_cpu(cuda, parity_record):
     """The 859.5 M-parameter SD 1.5 ε-UNet at 4x64x64, cross-attending to a 77x768
     context (``stable_diffusion.py:306-313``): forward + input VJP."""
     from samplers_amd.networks.unet2d_condition import build_unet_condition, null_context
@@ -108,12 +110,12 @@ def test_sd15_unet_fwd_vjp_matches_cpu(cuda):
     got = _fwd_vjp(lambda v: gpu(v, 601, ctx.to(cuda)), z.to(cuda), cot)
     names = _kernel_names(lambda: gpu(z.to(cuda), 601, ctx.to(cuda)))
     assert any("wino3x3" in n for n in names) and any("gn_fwd" in n for n in names)
-    _check("sd15-unet", got, _fwd_vjp(lambda v: cpu(v, 601, ctx), z, cot))
+    _check("sd15-unet", got, _fwd_vjp(lambda v: cpu(v, 601, ctx), z, cot), parity_record)
     del gpu
     torch.cuda.empty_cache()
 
 
-def test_celebahq_unet_full_size_fwd_vjp_matches_cpu(cuda):
+def test_celebahq_unet_full_size_fwd_vjp_matches_cpu(cuda, parity_record):
     """The headline prior (ddpm-celebahq-256, 6 levels, 113.7 M) at 3x256², B=2."""
     from samplers_amd.networks.unet2d import build_unet
 
@@ -126,7 +128,7 @@ def test_celebahq_unet_full_size_fwd_vjp_matches_cpu(cuda):
     names = _kernel_names(lambda: gpu(x.to(cuda), 999))
     for k in ("wino3x3", "gn_fwd", "conv3x3_s2", "conv3x3_thin", "upsample2x"):
         assert any(k in n for n in names), k
-    _check("celebahq-unet", got, _fwd_vjp(lambda v: cpu(v, 999), x, cot))
+    _check("celebahq-unet", got, _fwd_vjp(lambda v: cpu(v, 999), x, cot), parity_record)
     del gpu
     torch.cuda.empty_cache()
 
@@ -162,7 +164,7 @@ def _center_gather(shape):
     return op, apply, adjoint
 
 
-def test_psld_step_512_sd15_matches_oracle(cuda):
+def test_psld_step_512_sd15_matches_oracle(cuda, parity_record):
     """One PSLD iteration (``psld.py:118-153``: ε-UNet fwd, decode fwd, pixel pass, encode fwd,
     encode / decode / UNet VJPs, bridge update) at B=2, centre inpainting (configs[3])."""
     from oracle.latent_loops import psld_reference
@@ -191,10 +193,11 @@ def test_psld_step_512_sd15_matches_oracle(cuda):
                          lambda v: cpu.encode(v, differentiable=True), y, z0,
                          lambda k: xi, steps_limit=1)
     err = si.relative_error(z.cpu(), ref)
+    parity_record("latent_rel_l2", err, TOL, sampler="PSLD", guided_steps=1, batch=b, image=list(shape))
     assert err < TOL, err
 
 
-def test_resample_512_sd15_matches_oracle(cuda):
+def test_resample_512_sd15_matches_oracle(cuda, parity_record):
     """A short ReSample run (``resample.py:99-224``) at 3x512², B=1, Poisson: ε-DDIM steps, the
     DPS conditioning through the decoder VJP, a time-travel block with pixel-space hard
     consistency + encode + stochastic resampling, and the final latent-space optimisation
@@ -228,4 +231,6 @@ def test_resample_512_sd15_matches_oracle(cuda):
                              time_travel_interval=kw["time_travel_interval"],
                              stage_splits=kw["stage_splits"])
     err = si.relative_error(out.cpu(), ref.reshape(out.shape))
+    parity_record("x0_rel_l2", err, TOL, sampler="ReSample", noise="poisson", batch=b,
+                  image=list(shape), max_optimization_iters=kw["max_optimization_iters"])
     assert err < TOL, err

@@ -18,6 +18,12 @@ attention, the guidance passes) along a trajectory is bounded:
 
 Tolerance: relative L2 <= 2e-4 on the returned x̂ (fp32 on both sides; one prior call agrees
 to ~1e-5, see test_latent_full_gpu.py; the steps compound it roughly linearly).
+
+Long horizon (round 4): ``DPSSampler.__call__`` with the full UNet for 50 guided iterations at
+3x256², B = 1, inpainting, against the oracle loop on the CPU (about 80 s of CPU time); the
+sample is compared after 1, 2, 5, 10, 25 and 50 iterations (``callback``) and the final x̂ at
+the end, every error appended to ``gpurun_out/parity_record.jsonl`` (``parity_record``), so the
+drift's growth with the step count is on record, not only the final bound.
 """
 
 from __future__ import annotations
@@ -63,7 +69,7 @@ def _dps_problem(kind: str, shape, b: int, device):
 
 
 @pytest.mark.parametrize("kind", ["inpaint", "blur"])
-def test_dps_trajectory_celebahq_unet_matches_oracle(cuda, kind):
+def test_dps_trajectory_celebahq_unet_matches_oracle(cuda, kind, parity_record):
     from oracle import dps_loop
     from samplers_amd.networks.ddpm import DDPMNetwork
     from samplers_amd.networks.unet2d import build_unet
@@ -89,10 +95,12 @@ def test_dps_trajectory_celebahq_unet_matches_oracle(cuda, kind):
     assert torch.isfinite(out).all()
     err = si.relative_error(out, ref)
     print(f"DPS {kind}: {steps - 2} guided steps + final x0, rel L2 vs oracle {err:.3e}")
+    parity_record("x0_rel_l2", err, TOL, sampler="DPS", operator=kind, guided_steps=steps - 2,
+                  batch=b, image=list(shape))
     assert err < TOL, f"DPS {kind}: {steps - 2} steps, rel L2 {err:.3e}"
 
 
-def test_psld_trajectory_sd15_cfg_matches_oracle(cuda):
+def test_psld_trajectory_sd15_cfg_matches_oracle(cuda, parity_record):
     from oracle.latent_loops import psld_reference
     from samplers_amd.inverse_problem import InverseProblem
     from samplers_amd.networks.latent import LatentDiffusionNetwork, StableDiffusionCondition
@@ -137,4 +145,88 @@ def test_psld_trajectory_sd15_cfg_matches_oracle(cuda):
     assert torch.isfinite(out).all()
     err = si.relative_error(out, ref.reshape(out.shape))
     print(f"PSLD SD1.5 CFG: 3 guided steps + final decode, rel L2 vs oracle {err:.3e}")
+    parity_record("x0_rel_l2", err, TOL, sampler="PSLD", cfg=True, guided_steps=3, batch=b,
+                  image=list(shape))
     assert err < TOL, f"PSLD CFG: 3 steps, rel L2 {err:.3e}"
+
+
+LONG_CHECKPOINTS = (1, 2, 5, 10, 25, 50)
+LONG_TOL = 1e-3  # the sample after k guided iterations and the final x̂, relative L2
+
+
+def _heartbeat(what: str, every: float = 20.0):
+    """A line on the real stderr every `every` s while a long CPU oracle runs (pytest captures
+    the test's own output; a silent minute reads as a hung GPU test on the pool)."""
+    import sys
+    import threading
+    import time
+
+    stop = threading.Event()
+    t0 = time.perf_counter()
+
+    def run():
+        while not stop.wait(every):
+            print(f"[{what}] still running at {time.perf_counter() - t0:.0f}s", file=sys.__stderr__,
+                  flush=True)
+
+    threading.Thread(target=run, daemon=True).start()
+    return stop
+
+
+@pytest.mark.timeout(900)
+def test_dps_long_trajectory_celebahq_unet_matches_oracle(cuda, parity_record):
+    """50 guided DPS iterations with the full prior (dps.py:90-122 runs N - 2 of them; the
+    headline's N = 1000 is 998), the sample checked along the way and the final x̂ at the end."""
+    from oracle import dps_loop
+    from samplers_amd.networks.ddpm import DDPMNetwork
+    from samplers_amd.networks.unet2d import build_unet
+    from samplers_amd.samplers import DPSSampler
+
+    shape, b, guided = (3, 256, 256), 1, LONG_CHECKPOINTS[-1]
+    steps = guided + 2
+    problem, apply, y = _dps_problem("inpaint", shape, b, cuda)
+    gen = torch.Generator().manual_seed(31)
+    init = torch.randn((b, *shape), generator=gen)
+    xi = {i: torch.randn((b, *shape), generator=gen) for i in range(steps - 1, 1, -1)}
+
+    net = DDPMNetwork.from_config(seed=0, device=cuda)
+    seen: dict[int, torch.Tensor] = {}
+
+    def keep(i, x):
+        done = steps - 1 - i + 1  # guided iterations finished (i runs steps-1 .. 2)
+        if done in LONG_CHECKPOINTS:
+            seen[done] = x.detach().cpu().clone()
+
+    fn = lambda k, i, s: (init if k == "init" else xi[i]).to(cuda)  # noqa: E731
+    out = DPSSampler(net)(problem, num_sampling_steps=steps, gamma=1.0, eta=1.0, noise_fn=fn,
+                          callback=keep).cpu()
+    assert sorted(seen) == list(LONG_CHECKPOINTS)
+
+    stop = _heartbeat("long DPS oracle")
+    try:
+        unet = build_unet(seed=0)
+        acp = net.alphas_cumprod.cpu()
+        ts = net.schedule.set_timesteps(steps).flip(0).tolist()
+        lp = dps_loop.gaussian_log_prob(0.05)
+        eps = lambda v, t: unet(v, t)  # noqa: E731
+        sample, done, errs = init, 0, {}
+        for c in LONG_CHECKPOINTS:
+            i_cur = steps - 1 - done  # the next loop index of dps.py's loop
+            sample = dps_loop.dps_reference(eps, acp, ts[:i_cur + 1], apply, lp, y, sample,
+                                            lambda i: xi[i], gamma=1.0, eta=1.0,
+                                            steps_limit=c - done, return_sample=True)
+            done = c
+            errs[c] = si.relative_error(seen[c], sample)
+            parity_record("sample_rel_l2", errs[c], LONG_TOL, sampler="DPS", operator="inpaint",
+                          guided_steps=c, of=guided, batch=b, image=list(shape))
+        ref = dps_loop.dps_reference(eps, acp, ts[:2], apply, lp, y, sample, lambda i: xi[i],
+                                     gamma=1.0, eta=1.0)
+    finally:
+        stop.set()
+    err = si.relative_error(out, ref)
+    parity_record("x0_rel_l2", err, LONG_TOL, sampler="DPS", operator="inpaint",
+                  guided_steps=guided, batch=b, image=list(shape))
+    print("DPS long trajectory: " + ", ".join(f"{k}: {v:.2e}" for k, v in errs.items())
+          + f"; final x0 {err:.2e}")
+    assert all(v < LONG_TOL for v in errs.values()), errs
+    assert err < LONG_TOL, err
