@@ -390,6 +390,18 @@ int sp_wino3x3_fwd_res(const float* x, const float* up, const float* bias, const
 int sp_wino3x3_bwd_input(const float* dy, const float* up_vjp, int64_t n, int32_t cin,
                          int32_t cout, int32_t height, int32_t width, float* dx,
                          sp_stream_t stream);
+/* Split-K forms (round 4): where the launch's tiles leave CUs idle (small batches, the
+ * low-resolution levels) K is cut into up to 32 parts, each part's partial output stored to
+ * the caller's workspace and the parts summed in a fixed order (+ bias, + res) by a reduce
+ * launch — deterministic.  sp_wino3x3_workspace = the bytes a shape's split needs (0: the
+ * shape fills the chip unsplit); a smaller (or NULL) workspace runs unsplit.  res nullable. */
+int64_t sp_wino3x3_workspace(int64_t n, int32_t cin, int32_t cout, int32_t height, int32_t width);
+int sp_wino3x3_fwd_ws(const float* x, const float* up, const float* bias, const float* res,
+                      int64_t n, int32_t cin, int32_t cout, int32_t height, int32_t width,
+                      float* y, float* ws, int64_t ws_bytes, sp_stream_t stream);
+int sp_wino3x3_bwd_input_ws(const float* dy, const float* up_vjp, int64_t n, int32_t cin,
+                            int32_t cout, int32_t height, int32_t width, float* dx, float* ws,
+                            int64_t ws_bytes, sp_stream_t stream);
 
 /* 1x1 convolution as a per-pixel GEMM on bf16 MFMAs over exact three-term splits of the fp32
  * operands (fp32-class error): Y[n][co][p] = sum_k W[co][k] X[n][k][p] (+ bias[co]) (+ res),

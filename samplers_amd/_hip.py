@@ -197,6 +197,12 @@ SIGNATURES = {
     "sp_groupnorm_set_spin_limit": (ctypes.c_int, [ctypes.c_int32]),
     "sp_wino3x3_fwd_res": (ctypes.c_int, [_P, _P, _P, _P, _I64, ctypes.c_int32, ctypes.c_int32,
                                           ctypes.c_int32, ctypes.c_int32, _P, _P]),
+    "sp_wino3x3_workspace": (_I64, [_I64, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
+                                    ctypes.c_int32]),
+    "sp_wino3x3_fwd_ws": (ctypes.c_int, [_P, _P, _P, _P, _I64, ctypes.c_int32, ctypes.c_int32,
+                                         ctypes.c_int32, ctypes.c_int32, _P, _P, _I64, _P]),
+    "sp_wino3x3_bwd_input_ws": (ctypes.c_int, [_P, _P, _I64, ctypes.c_int32, ctypes.c_int32,
+                                               ctypes.c_int32, ctypes.c_int32, _P, _P, _I64, _P]),
 }
 
 _lib = None

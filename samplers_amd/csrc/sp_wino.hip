@@ -154,7 +154,7 @@ constexpr int WR_CO = 64;   // output channels per workgroup (2 waves x 32)
                          // burst, 2 two bursts (see wr_step)
 #endif
 #ifndef SP_WINO_SPLITK
-#define SP_WINO_SPLITK 1  // split K over two workgroups where the 8x8 mosaic leaves CUs idle
+#define SP_WINO_SPLITK 32  // most split-K parts a launch may use (1: no split)
 #endif
 constexpr int WR_NS = 4;    // unroll of the k-step ring (cin % (2 WR_NS) == 0)
 // Tile geometry of a wave: 32 tiles (the MFMA's N) as TRW tile rows x TCW tile columns.
@@ -164,8 +164,10 @@ constexpr int WR_NS = 4;    // unroll of the k-step ring (cin % (2 WR_NS) == 0)
 template <int TCW_, bool MOSAIC_ = false, bool SPLIT_ = false>
 struct WGeo {
     static constexpr int TCW = TCW_;
-    // SPLIT (8x8 mosaic at small tile counts): K halved over two workgroups, partial outputs
-    // added atomically into the zeroed output (a compile-time variant: the other kernels keep
+    // SPLIT (launches whose tiles leave CUs idle: small batches, the low-resolution levels):
+    // K cut into g.ksplit parts, one tile each; part kh stores its partial sums (no bias, no
+    // residual) to workspace slice kh, and k_wino_split_reduce adds the slices in order, the
+    // bias and the residual (deterministic; a compile-time variant: the other kernels keep
     // their register allocation)
     static constexpr bool SPLIT = SPLIT_;
     // MOSAIC (8x8 images, the UNet's 8x8 level): the W = 16 geometry over two images side by
@@ -214,7 +216,9 @@ struct WrGeom {
     int64_t u_step;                   // floats of packed U per k-step
     int so_step;                      // bytes of input per k-step (two channels)
     int nsteps;                       // k-steps per tile (of one split-K part)
-    int ksplit;                       // 2 for the SPLIT kernels, else 1
+    int ksplit;                       // split-K parts of the SPLIT kernels, else 1
+    float* ws;                        // SPLIT: the parts' partial outputs [ksplit][batch][cout][H][W]
+    int64_t ws_stride;                // floats per part slice
 };
 
 // First image of a wave's data and how many of its images exist (MOSAIC: 2 per wave).
@@ -237,7 +241,7 @@ __device__ __forceinline__ WrTile wr_tile(const WrGeom& g, int t, int wv) {
     int lb = (g.ntiles & 7) ? t : (t & 7) * (g.ntiles >> 3) + (t >> 3);
     SP_DCHECK(t >= 0 && t < g.ntiles && lb < g.ntiles);
     int kh = 0;
-    if constexpr (GE::SPLIT) kh = lb & 1, lb >>= 1;
+    if constexpr (GE::SPLIT) kh = lb % g.ksplit, lb /= g.ksplit;
     const int co_blk = lb % g.cob, rest = lb / g.cob;
     if constexpr (GE::MOSAIC)  // four images per workgroup, two per wave
         return WrTile{4 * rest, 0, 0, co_blk * WR_CO + 32 * (wv & 1), kh};
@@ -277,11 +281,14 @@ __device__ __forceinline__ WrSrc wr_src(const WrGeom& g, const WrTile& ti, int w
                           (int64_t)(ti.co0 >> 5) * 64 * 16) * 4));
 #if SP_DEBUG
     {   // every k-step's input pieces inside this tile's planes, U rows inside the packed U
+        // (a MOSAIC wave whose second image, or both, lie past the batch addresses them anyway:
+        // its buffer's range is cut to the images that exist, which read as zeros)
         const int64_t span = nimg ? (int64_t)(nimg * g.cin - kofs) * g.plane * 4 : 0;
         const int64_t last = (int64_t)(g.nsteps - 1) * g.so_step;
-        SP_DCHECK(s.oa == OOB || (s.oa >= 0 && s.oa + last + 16 <= span));
-        SP_DCHECK(s.ob == OOB || (s.ob >= 0 && s.ob + last + 16 <= span));
-        SP_DCHECK(s.oh == OOB || (s.oh >= 0 && s.oh + last + 4 <= span));
+        const bool full = !GE::MOSAIC || nimg == 2;
+        SP_DCHECK(s.oa == OOB || (s.oa >= 0 && (!full || s.oa + last + 16 <= span)));
+        SP_DCHECK(s.ob == OOB || (s.ob >= 0 && (!full || s.ob + last + 16 <= span)));
+        SP_DCHECK(s.oh == OOB || (s.oh >= 0 && (!full || s.oh + last + 4 <= span)));
         SP_DCHECK(s.uso >= 0 && (int64_t)s.uso + ((int64_t)(g.nsteps - 1) * g.u_step + 64 * 16) * 4 <=
                                    (int64_t)g.nsteps * g.ksplit * g.u_step * 4);
         SP_DCHECK(ti.co0 + 32 <= g.cout && ti.n < g.batch);
@@ -485,7 +492,7 @@ __device__ __forceinline__ void wr_load_res(const WrGeom& g, const WrTile& ti, i
                                             WrRes& rv) {
     const auto rrs = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<float*>(g.res) + wr_img0<GE>(g, ti, wv) * g.cout * g.plane, (short)0,
-        GE::SPLIT && ti.kh ? 0 : wr_nimg<GE>(g, ti, wv) * g.cout * g.plane * 4, 0x00020000);  // part 0 only
+        wr_nimg<GE>(g, ti, wv) * g.cout * g.plane * 4, 0x00020000);
     const int vo = wr_out_voff<GE>(g, ti, wv, lane);
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
@@ -495,18 +502,15 @@ __device__ __forceinline__ void wr_load_res(const WrGeom& g, const WrTile& ti, i
     }
 }
 
-// SPLIT epilogue: buffer_atomic_add_f32 (device-coherent RMW, no return) on a scalar
-// resource, one 32-bit lane offset, no branch
-__device__ __forceinline__ void wr_atomic_add(float v, __amdgpu_buffer_rsrc_t r, int voff) {
-    asm volatile("buffer_atomic_add_f32 %0, %1, %2, 0 offen" : : "v"(v), "v"(voff), "s"(r) : "memory");
-}
-
 template <class GE, bool RES>
 __device__ __forceinline__ void wr_epilogue(const WrGeom& g, const WrTile& ti, int wv, int lane,
                                             const f32x16 (&acc)[16], const WrRes& rv) {
+    static_assert(!(GE::SPLIT && RES), "split-K parts add no residual (the reduce does)");
     const int hh = lane >> 5, l = lane & 31;
+    // SPLIT: part kh's slice of the workspace, laid out like the output
+    float* const obase = GE::SPLIT ? g.ws + (int64_t)ti.kh * g.ws_stride : g.out;
     const auto ors = __builtin_amdgcn_make_buffer_rsrc(
-        g.out + wr_img0<GE>(g, ti, wv) * g.cout * g.plane, (short)0,
+        obase + wr_img0<GE>(g, ti, wv) * g.cout * g.plane, (short)0,
         wr_nimg<GE>(g, ti, wv) * g.cout * g.plane * 4, 0x00020000);
     const int vo = wr_out_voff<GE>(g, ti, wv, lane);
     // the lane's last output row (channel co0 + 27 + 4 hh, second image row) inside the images
@@ -518,16 +522,7 @@ __device__ __forceinline__ void wr_epilogue(const WrGeom& g, const WrTile& ti, i
     // operands are live.)
     const auto brs = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<float*>(g.bias ? g.bias : g.up), (short)0,
-        g.bias && !(GE::SPLIT && ti.kh) ? g.cout * 4 : 0, 0x00020000);  // SPLIT: part 0 only
-    // SPLIT: the same output range as `ors`, from wave-uniform (scalar) values, for the
-    // inline-asm atomics (out-of-range lanes dropped by the range check, like the stores)
-    __amdgpu_buffer_rsrc_t ars;
-    if constexpr (GE::SPLIT)
-        ars = __builtin_amdgcn_make_buffer_rsrc(
-            g.out + (int64_t)__builtin_amdgcn_readfirstlane(static_cast<int>(wr_img0<GE>(g, ti, wv))) *
-                        g.cout * g.plane,
-            (short)0, __builtin_amdgcn_readfirstlane(wr_nimg<GE>(g, ti, wv)) * g.cout * g.plane * 4,
-            0x00020000);
+        g.bias && !GE::SPLIT ? g.cout * 4 : 0, 0x00020000);  // SPLIT: the reduce adds it
     const float bl = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(brs, (ti.co0 + l) * 4, 0, 0));
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
@@ -550,15 +545,8 @@ __device__ __forceinline__ void wr_epilogue(const WrGeom& g, const WrTile& ti, i
         f32x2 y0 = {s0[0] + s0[1] + s0[2] + bv, s1[0] + s1[1] + s1[2] + bv};
         f32x2 y1 = {s0[1] - s0[2] - s0[3] + bv, s1[1] - s1[2] - s1[3] + bv};
         if constexpr (RES) y0 += rv.v[r][0], y1 += rv.v[r][1];
-        if constexpr (!GE::SPLIT) {
-            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, y0), ors, vo, so, 0);
-            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, y1), ors, vo, so + g.W * 4, 0);
-        } else {  // this part's share into the zeroed output: two addends, order-independent
-            wr_atomic_add(y0[0], ars, vo + so);
-            wr_atomic_add(y0[1], ars, vo + so + 4);
-            wr_atomic_add(y1[0], ars, vo + so + g.W * 4);
-            wr_atomic_add(y1[1], ars, vo + so + g.W * 4 + 4);
-        }
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, y0), ors, vo, so, 0);
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, y1), ors, vo, so + g.W * 4, 0);
         // one register row at a time: the next tile's operands are live across the
         // epilogue, so its accumulator reads must not all be hoisted
         __builtin_amdgcn_sched_barrier(0);
@@ -962,6 +950,23 @@ __global__ __launch_bounds__(kBlock, 1) void k_wino3x3_xi(WrGeom g) {
     else xi_body<RES, 0>(g, wv, lane, xw, ex);
 }
 
+// Split-K reduce: out = (((ws_0 + ws_1) + ws_2) + ...) + bias[c] (+ res), four outputs per
+// thread (plane % 4 == 0), the parts added in a fixed order (bitwise reproducible)
+__global__ __launch_bounds__(kBlock) void k_wino_split_reduce(const float* __restrict__ ws, int ks,
+                                                              int64_t stride4, int plane4, int cout,
+                                                              const float* __restrict__ bias,
+                                                              const float* __restrict__ res,
+                                                              float* __restrict__ out) {
+    const f32x4* w4 = reinterpret_cast<const f32x4*>(ws);
+    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < stride4; i += (int64_t)gridDim.x * kBlock) {
+        f32x4 a = w4[i];
+        for (int k = 1; k < ks; ++k) a += w4[(int64_t)k * stride4 + i];
+        if (bias) a += bias[(i / plane4) % cout];
+        if (res) a += reinterpret_cast<const f32x4*>(res)[i];
+        reinterpret_cast<f32x4*>(out)[i] = a;
+    }
+}
+
 // Pack for k_wino3x3_r (U = G g G^T per (co, ci), G = [[1,0,0],[.5,.5,.5],[.5,-.5,.5],[0,0,1]]): up[((kin / 2 * (cout_p / 32) + orow / 32) * 64 + lane) * 16 + xi],
 // lane = 32 (kin & 1) + orow % 32.
 __global__ void k_wino3x3_pack(const float* __restrict__ w, int cout, int cin, int flip,
@@ -1024,9 +1029,30 @@ static int cu_count() {
     return cached[dev];
 }
 
+// Split-K parts for a launch of `tiles` tiles over cin input channels: doubled while the
+// doubled count still fits one persistent wave of workgroups and every part keeps at least two
+// rings of k-steps (k_wino3x3_r's first and last blocks)
+static int wino_ksplit(int64_t tiles, int32_t cin) {
+    const int nst = cin / 2;
+    int ks = 1;
+    while (ks * 2 <= SP_WINO_SPLITK && tiles * ks * 2 <= cu_count() && nst % (ks * 2 * WR_NS) == 0 &&
+           nst / (ks * 2) >= 2 * WR_NS)
+        ks *= 2;
+    return ks;
+}
+
+static int64_t wino_tiles(int64_t n, int32_t cout, int32_t height, int32_t width) {
+    const bool mosaic = width == 8;
+    const bool narrow = !mosaic && width % WGeo<16>::WG_COLS != 0;
+    const int wg_rows = narrow ? WGeo<8>::WG_ROWS : WGeo<16>::WG_ROWS;
+    const int wg_cols = narrow ? WGeo<8>::WG_COLS : WGeo<16>::WG_COLS;
+    return mosaic ? (n + 3) / 4 * (cout / WR_CO) : n * (height / wg_rows) * (width / wg_cols) * (cout / WR_CO);
+}
+
 static int wino3x3(int kind, const float* x, const float* up, const float* bias,
                    const float* res, int64_t n, int32_t cin, int32_t cout, int32_t height,
-                   int32_t width, float* y, sp_stream_t stream, const char* what) {
+                   int32_t width, float* y, float* ws, size_t ws_bytes, sp_stream_t stream,
+                   const char* what) {
     if (!sp_wino3x3_supported(cin, cout, height, width) || n < 0) return SP_EINVAL;
     if (n == 0) return SP_OK;
     if (!x || !up || !y) return SP_EINVAL;
@@ -1034,15 +1060,17 @@ static int wino3x3(int kind, const float* x, const float* up, const float* bias,
     const bool narrow = !mosaic && width % WGeo<16>::WG_COLS != 0;  // the W = 16 geometry
     const int wg_rows = narrow ? WGeo<8>::WG_ROWS : WGeo<16>::WG_ROWS;
     const int wg_cols = narrow ? WGeo<8>::WG_COLS : WGeo<16>::WG_COLS;
-    const int64_t tiles = mosaic ? (n + 3) / 4 * (cout / WR_CO)
-                                 : n * (height / wg_rows) * (width / wg_cols) * (cout / WR_CO);
+    const int64_t tiles = wino_tiles(n, cout, height, width);
     // per-sample planes are addressed by 32-bit buffer offsets (bytes < 2^31)
     if (tiles >= (int64_t(1) << 31) || (int64_t)cin * height * width * 4 >= (int64_t(1) << 31) ||
         (int64_t)cout * height * width * 4 >= (int64_t(1) << 31))
         return SP_EINVAL;
-    // the UNet's 8x8 level is 128 mosaic tiles at B = 64, half the CUs: split K in two there
-    const int ksplit = SP_WINO_SPLITK && mosaic && 2 * tiles <= cu_count() && cin % 16 == 0 && cin >= 32
-                           ? 2 : 1;
+    // split K where the tiles leave CUs idle (small batches, the low-resolution levels), when
+    // the caller's workspace holds every part's partial output
+    const int64_t out_floats = n * cout * (int64_t)height * width;
+    int ksplit = ws ? wino_ksplit(tiles, cin) : 1;
+    if (ksplit > 1 && ws_bytes < (size_t)ksplit * out_floats * sizeof(float)) ksplit = 1;
+    if (tiles * ksplit >= (int64_t(1) << 31)) ksplit = 1;
     WrGeom g;
     g.x = x;
     g.up = up;
@@ -1056,6 +1084,8 @@ static int wino3x3(int kind, const float* x, const float* up, const float* bias,
     g.plane = height * width;
     g.ntiles = static_cast<int>(tiles * ksplit);
     g.ksplit = ksplit;
+    g.ws = ksplit > 1 ? ws : nullptr;
+    g.ws_stride = out_floats;
     g.cob = cout / WR_CO;
     g.tiles_w = mosaic ? 1 : width / wg_cols;
     g.per_img = mosaic ? 1 : g.tiles_w * (height / wg_rows);
@@ -1070,11 +1100,15 @@ static int wino3x3(int kind, const float* x, const float* up, const float* bias,
     const double flops = 8.0 * n * cin * cout * height * width;
     const dim3 gd(static_cast<unsigned>(grid)), bd(kBlock);
     hipStream_t st = static_cast<hipStream_t>(stream);
-    if (ksplit > 1 && hipMemsetAsync(y, 0, (size_t)n * cout * height * width * sizeof(float), st) != hipSuccess)
-        return check_launch(what);
     if (ksplit > 1) {
-        if (res) launch_w(kind, flops, k_wino3x3_r<true, 8, true, true>, gd, bd, st, g);
-        else launch_w(kind, flops, k_wino3x3_r<false, 8, true, true>, gd, bd, st, g);
+        if (mosaic) launch_w(kind, flops, k_wino3x3_r<false, 8, true, true>, gd, bd, st, g);
+        else if (narrow) launch_w(kind, flops, k_wino3x3_r<false, 8, false, true>, gd, bd, st, g);
+        else launch_w(kind, flops, k_wino3x3_r<false, 16, false, true>, gd, bd, st, g);
+        // the parts' sum + bias + residual (plane % 4 == 0 on every supported geometry)
+        const int64_t v4 = out_floats / 4;
+        const unsigned rb = static_cast<unsigned>(std::min<int64_t>((v4 + kBlock - 1) / kBlock, 4 * cu_count()));
+        launch(0, k_wino_split_reduce, dim3(rb), dim3(kBlock), st, static_cast<const float*>(ws), ksplit, v4,
+               height * width / 4, cout, bias, res, y);
     } else if (mosaic) {
         if (res) launch_w(kind, flops, k_wino3x3_r<true, 8, true>, gd, bd, st, g);
         else launch_w(kind, flops, k_wino3x3_r<false, 8, true>, gd, bd, st, g);
@@ -1091,25 +1125,49 @@ static int wino3x3(int kind, const float* x, const float* up, const float* bias,
     return check_launch(what);
 }
 
+int64_t sp_wino3x3_workspace(int64_t n, int32_t cin, int32_t cout, int32_t height, int32_t width) {
+    if (!sp_wino3x3_supported(cin, cout, height, width) || n <= 0) return 0;
+    const int ks = wino_ksplit(wino_tiles(n, cout, height, width), cin);
+    return ks > 1 ? (int64_t)ks * n * cout * height * width * (int64_t)sizeof(float) : 0;
+}
+
 int sp_wino3x3_fwd(const float* x, const float* up, const float* bias, int64_t n, int32_t cin,
                    int32_t cout, int32_t height, int32_t width, float* y, sp_stream_t stream) {
-    return wino3x3(TK_WINO3X3_FWD, x, up, bias, nullptr, n, cin, cout, height, width, y, stream,
-                   "sp_wino3x3_fwd");
+    return wino3x3(TK_WINO3X3_FWD, x, up, bias, nullptr, n, cin, cout, height, width, y, nullptr, 0,
+                   stream, "sp_wino3x3_fwd");
 }
 
 int sp_wino3x3_fwd_res(const float* x, const float* up, const float* bias, const float* res,
                        int64_t n, int32_t cin, int32_t cout, int32_t height, int32_t width,
                        float* y, sp_stream_t stream) {
     if (!res || res == y) return SP_EINVAL;
-    return wino3x3(TK_WINO3X3_FWD, x, up, bias, res, n, cin, cout, height, width, y, stream,
-                   "sp_wino3x3_fwd_res");
+    return wino3x3(TK_WINO3X3_FWD, x, up, bias, res, n, cin, cout, height, width, y, nullptr, 0,
+                   stream, "sp_wino3x3_fwd_res");
 }
 
 int sp_wino3x3_bwd_input(const float* dy, const float* up_vjp, int64_t n, int32_t cin,
                          int32_t cout, int32_t height, int32_t width, float* dx,
                          sp_stream_t stream) {
     return wino3x3(TK_WINO3X3_BWD_INPUT, dy, up_vjp, nullptr, nullptr, n, cout, cin, height,
-                   width, dx, stream, "sp_wino3x3_bwd_input");
+                   width, dx, nullptr, 0, stream, "sp_wino3x3_bwd_input");
+}
+
+int sp_wino3x3_fwd_ws(const float* x, const float* up, const float* bias, const float* res,
+                      int64_t n, int32_t cin, int32_t cout, int32_t height, int32_t width,
+                      float* y, float* ws, int64_t ws_bytes, sp_stream_t stream) {
+    if (res == y && res) return SP_EINVAL;
+    if (ws && (ws == y || ws_bytes < 0)) return SP_EINVAL;
+    return wino3x3(TK_WINO3X3_FWD, x, up, bias, res, n, cin, cout, height, width, y, ws,
+                   static_cast<size_t>(ws_bytes > 0 ? ws_bytes : 0), stream, "sp_wino3x3_fwd_ws");
+}
+
+int sp_wino3x3_bwd_input_ws(const float* dy, const float* up_vjp, int64_t n, int32_t cin,
+                            int32_t cout, int32_t height, int32_t width, float* dx, float* ws,
+                            int64_t ws_bytes, sp_stream_t stream) {
+    if (ws && (ws == dx || ws_bytes < 0)) return SP_EINVAL;
+    return wino3x3(TK_WINO3X3_BWD_INPUT, dy, up_vjp, nullptr, nullptr, n, cout, cin, height,
+                   width, dx, ws, static_cast<size_t>(ws_bytes > 0 ? ws_bytes : 0), stream,
+                   "sp_wino3x3_bwd_input_ws");
 }
 
 }  // extern "C"

@@ -224,15 +224,28 @@ def conv3x3_forward(module: "Conv3x3", x: Tensor, res: Tensor | None = None,
                                            _hip.stream_of(x)), "sp_conv3x3_thin_fwd")
         return y if res is None else y.add_(res)
     pk = tile_pack(module, algo, False)
-    if algo == "wino" and res is not None:
-        _hip.check(lib.sp_wino3x3_fwd_res(_hip.ptr(x), _hip.ptr(pk), _hip.ptr(bias),
-                                          _hip.ptr(res.contiguous()), n, cin, cout, h, w,
-                                          _hip.ptr(y), _hip.stream_of(x)), "sp_wino3x3_fwd_res")
+    if algo == "wino":
+        # split-K where the tiles leave CUs idle (small batches, low-resolution levels)
+        ws = _wino_workspace(lib, n, cin, cout, h, w, x.device)  # held until queued
+        _hip.check(lib.sp_wino3x3_fwd_ws(_hip.ptr(x), _hip.ptr(pk), _hip.ptr(bias),
+                                         None if res is None else _hip.ptr(res.contiguous()), n,
+                                         cin, cout, h, w, _hip.ptr(y), _hip.ptr(ws),
+                                         0 if ws is None else ws.numel() * 4, _hip.stream_of(x)),
+                   "sp_wino3x3_fwd_ws")
         return y
-    fn = lib.sp_wino3x3_fwd if algo == "wino" else lib.sp_conv3x3_fwd
-    _hip.check(fn(_hip.ptr(x), _hip.ptr(pk), _hip.ptr(bias), n, cin, cout, h, w, _hip.ptr(y),
-                  _hip.stream_of(x)), f"sp_{algo}_conv3x3_fwd")
+    _hip.check(lib.sp_conv3x3_fwd(_hip.ptr(x), _hip.ptr(pk), _hip.ptr(bias), n, cin, cout, h, w,
+                                  _hip.ptr(y), _hip.stream_of(x)), "sp_direct_conv3x3_fwd")
     return y if res is None else y.add_(res)
+
+
+def _wino_workspace(lib, n: int, cin: int, cout: int, h: int, w: int, device) -> Tensor | None:
+    """A workspace for the Winograd tile's split-K parts, or None when the shape fills the
+    chip unsplit (sp_wino3x3_workspace).  From torch's caching allocator on the launch
+    stream, so a graph capture records it and a later reuse is ordered after the launch."""
+    nb = int(lib.sp_wino3x3_workspace(n, cin, cout, h, w))
+    if nb <= 0:
+        return None
+    return torch.empty(nb // 4, device=device, dtype=torch.float32)
 
 
 def conv3x3_input_vjp(module: "Conv3x3", dy: Tensor, x_shape) -> Tensor:
@@ -251,9 +264,16 @@ def conv3x3_input_vjp(module: "Conv3x3", dy: Tensor, x_shape) -> Tensor:
                                                  n, cin, cout, h, w, _hip.ptr(dx),
                                                  _hip.stream_of(dy)), "sp_conv3x3_thin_bwd_input")
         return dx
-    fn = lib.sp_wino3x3_bwd_input if algo == "wino" else lib.sp_conv3x3_bwd_input
-    _hip.check(fn(_hip.ptr(dy), _hip.ptr(tile_pack(module, algo, True)), n, cin, cout, h, w,
-                  _hip.ptr(dx), _hip.stream_of(dy)), f"sp_{algo}_conv3x3_bwd_input")
+    if algo == "wino":
+        ws = _wino_workspace(lib, n, cout, cin, h, w, dy.device)  # the VJP's K is cout
+        _hip.check(lib.sp_wino3x3_bwd_input_ws(_hip.ptr(dy), _hip.ptr(tile_pack(module, algo, True)),
+                                               n, cin, cout, h, w, _hip.ptr(dx), _hip.ptr(ws),
+                                               0 if ws is None else ws.numel() * 4,
+                                               _hip.stream_of(dy)), "sp_wino3x3_bwd_input_ws")
+        return dx
+    _hip.check(lib.sp_conv3x3_bwd_input(_hip.ptr(dy), _hip.ptr(tile_pack(module, algo, True)), n, cin,
+                                        cout, h, w, _hip.ptr(dx), _hip.stream_of(dy)),
+               "sp_direct_conv3x3_bwd_input")
     return dx
 
 

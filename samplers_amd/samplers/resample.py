@@ -246,6 +246,8 @@ class ReSampleSampler(PosteriorSampler, Generic[Condition_co]):
         shared = dist.is_initialized() and dist.get_world_size(cons.group) > 1
         part = torch.empty(b, int(lib.sp_rsq_partials(cons.desc)), device=x.device) if fused else None
         ss = torch.empty(1, device=x.device)
+        losses = self._loss_log(max_iters, x.device)
+        it = -1
         for it in range(max_iters):
             c = adamw_coefficients(it + 1, 1e-2)
             if fused:
@@ -266,10 +268,11 @@ class ReSampleSampler(PosteriorSampler, Generic[Condition_co]):
                                                    _hip.ptr(v_), x.numel(), c, _hip.ptr(stop),
                                                    stream), "sp_adamw_step_until")
                 parts, count = ss, 1
-            _hip.check(lib.sp_opt_check(_hip.ptr(parts), count, tot, thr, _hip.ptr(stop), None,
-                                        stream), "sp_opt_check")
+            _hip.check(lib.sp_opt_check(_hip.ptr(parts), count, tot, thr, _hip.ptr(stop),
+                                        _hip.ptr(losses) + 4 * it, stream), "sp_opt_check")
             if (it + 1) % check_every == 0 and int(stop.item()):
                 break
+        self._log_solve("pixel", losses, it + 1, max_iters)
         return x
 
     def _latent_optimization(self, z0: Tensor, cons: _Consistency, total: int, eps: float,
@@ -292,6 +295,8 @@ class ReSampleSampler(PosteriorSampler, Generic[Condition_co]):
         events = [torch.cuda.Event(), torch.cuda.Event()]
         stream = _hip.stream_of(z)
         tot, thr = float(np.float32(total)), float(eps) ** 2
+        losses = self._loss_log(max_iters, z.device)
+        itr = -1
         for itr in range(max_iters):
             with torch.enable_grad():
                 zr = z.detach().requires_grad_(True)
@@ -304,7 +309,8 @@ class ReSampleSampler(PosteriorSampler, Generic[Condition_co]):
                                                _hip.ptr(v_), z.numel(), c, _hip.ptr(stop), stream),
                        "sp_adamw_step_until")
             _hip.check(lib.sp_opt_check_plateau(_hip.ptr(ss), 1, tot, thr, itr, plateau_from,
-                                                _hip.ptr(prev), _hip.ptr(stop), None, stream),
+                                                _hip.ptr(prev), _hip.ptr(stop),
+                                                _hip.ptr(losses) + 4 * itr, stream),
                        "sp_opt_check_plateau")
             slot = itr & 1
             flags[slot:slot + 1].copy_(stop, non_blocking=True)
@@ -313,7 +319,26 @@ class ReSampleSampler(PosteriorSampler, Generic[Condition_co]):
                 events[slot ^ 1].synchronize()
                 if int(flags[slot ^ 1]):
                     break
+        self._log_solve("latent", losses, itr + 1, max_iters)
         return z
+
+    @staticmethod
+    def _loss_log(max_iters: int, device) -> Tensor:
+        """Per-iteration losses of one hard-consistency solve, written by the device check
+        (``loss_out``); a check after the stop writes nothing, so the entries left NaN count
+        the iterations the stopping rule skipped."""
+        return torch.full((max(max_iters, 1),), float("nan"), device=device)
+
+    def _log_solve(self, kind: str, losses: Tensor, trips: int, max_iters: int) -> None:
+        """Append one solve's record to ``self.optimization_log`` (reset per ``__call__``):
+        the iterations the reference's stopping rule ran (``resample_kernels.py:32-93``),
+        the host loop's trips (a few more: the flag is read late), the final loss."""
+        done = losses[:trips]
+        ran = int(torch.isfinite(done).sum())
+        last = float(done[ran - 1]) if ran else float("nan")
+        self.__dict__.setdefault("optimization_log", []).append(
+            {"kind": kind, "iterations": ran, "host_trips": trips, "max_iters": max_iters,
+             "stopped_early": ran < max_iters, "final_loss": last})
 
     def _resample(self, z_opt: Tensor, snapshot: Tensor, a_prev: float, sigma: float,
                   noise: Tensor | None, seed: int, key: int, offset: int) -> Tensor:
@@ -347,7 +372,10 @@ class ReSampleSampler(PosteriorSampler, Generic[Condition_co]):
         group=None,
     ) -> Tensor:
         """Run ReSample; ``scale`` is accepted and unused, as in the reference
-        (its DPS step size is ½ᾱ_t, ``resample.py:145-146``)."""
+        (its DPS step size is ½ᾱ_t, ``resample.py:145-146``).  Afterwards
+        ``optimization_log`` lists every hard-consistency solve of the call (pixel / latent,
+        the AdamW iterations the stopping rules ran, the final loss)."""
+        self.optimization_log = []
         x_shape: Shape = inverse_problem.operator.x_shape
         batch_shape: Shape = inverse_problem.batch_shape
         x_view = BatchView(batch_shape, num_reconstructions, x_shape)

@@ -155,6 +155,62 @@ def test_winograd_forward_and_input_vjp(cuda, shape):
     assert rel < 1e-5, rel
 
 
+@pytest.mark.parametrize("shape", [(1, 128, 128, 128, 128), (1, 256, 256, 64, 64), (1, 512, 512, 32, 32),
+                                   (1, 512, 512, 16, 16), (1, 512, 512, 8, 8), (3, 256, 128, 8, 8),
+                                   (2, 64, 128, 32, 64)])
+def test_winograd_split_k_workspace(cuda, shape):
+    """Split-K (round 4): the small-batch / low-resolution launches cut K into 2-32 parts whose
+    partial outputs go to a workspace and are summed in a fixed order with the bias and the
+    residual.  Forward (bias + residual) and input VJP against fp64, bitwise-repeatable, and
+    equal to the unsplit launch to fp32 rounding."""
+    n, cin, cout, h, w = shape
+    lib = _hip.load_library()
+    ws_f = int(lib.sp_wino3x3_workspace(n, cin, cout, h, w))
+    ws_b = int(lib.sp_wino3x3_workspace(n, cout, cin, h, w))
+    assert ws_f > 0  # every shape here under-fills the chip unsplit
+    g = torch.Generator().manual_seed(41 + sum(shape))
+    x = torch.randn(n, cin, h, w, generator=g)
+    wt = torch.randn(cout, cin, 3, 3, generator=g) * (cin * 9) ** -0.5
+    b = torch.randn(cout, generator=g)
+    res = torch.randn(n, cout, h, w, generator=g)
+    dy = torch.randn(n, cout, h, w, generator=g)
+    xd = x.double().requires_grad_()
+    ref = F.conv2d(xd, wt.double(), b.double(), padding=1)
+    (gref,) = torch.autograd.grad(ref, xd, dy.double())
+    ref = ref.detach() + res.double()
+    st = torch.cuda.current_stream().cuda_stream
+    xg, wg, bg, rg, dyg = x.to(cuda), wt.to(cuda), b.to(cuda), res.to(cuda), dy.to(cuda)
+    up = torch.empty(int(lib.sp_wino3x3_packed_size(cin, cout)), device=cuda)
+    uv = torch.empty_like(up)
+    _hip.check(lib.sp_wino3x3_pack(wg.data_ptr(), cout, cin, 0, up.data_ptr(), st), "pack")
+    _hip.check(lib.sp_wino3x3_pack(wg.data_ptr(), cout, cin, 1, uv.data_ptr(), st), "pack")
+
+    def fwd(ws_bytes):
+        y = torch.empty(n, cout, h, w, device=cuda)
+        ws = torch.full((max(ws_bytes, 4) // 4,), float("nan"), device=cuda)  # NaN: unread parts show
+        _hip.check(lib.sp_wino3x3_fwd_ws(xg.data_ptr(), up.data_ptr(), bg.data_ptr(), rg.data_ptr(), n, cin,
+                                         cout, h, w, y.data_ptr(), ws.data_ptr() if ws_bytes else None,
+                                         ws_bytes, st), "wino fwd ws")
+        return y
+
+    def vjp(ws_bytes):
+        dx = torch.empty(n, cin, h, w, device=cuda)
+        ws = torch.full((max(ws_bytes, 4) // 4,), float("nan"), device=cuda)
+        _hip.check(lib.sp_wino3x3_bwd_input_ws(dyg.data_ptr(), uv.data_ptr(), n, cin, cout, h, w,
+                                               dx.data_ptr(), ws.data_ptr() if ws_bytes else None,
+                                               ws_bytes, st), "wino vjp ws")
+        return dx
+
+    y1, y2, y0 = fwd(ws_f), fwd(ws_f), fwd(0)
+    assert torch.equal(y1, y2)
+    assert ((y1.double().cpu() - ref).norm() / ref.norm()).item() < 1e-5
+    assert ((y1 - y0).norm() / y0.norm()).item() < 1e-6
+    d1, d2, d0 = vjp(ws_b), vjp(ws_b), vjp(0)
+    assert torch.equal(d1, d2)
+    assert ((d1.double().cpu() - gref).norm() / gref.norm()).item() < 1e-5
+    assert ((d1 - d0).norm() / d0.norm()).item() < 1e-6
+
+
 def test_winograd_residual_epilogue(cuda):
     """sp_wino3x3_fwd_res = sp_wino3x3_fwd + res, exactly (the add happens once, in fp32)."""
     from samplers_amd.networks.layers import Conv3x3, conv3x3_forward

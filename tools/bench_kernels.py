@@ -1,4 +1,5 @@
-"""Time the fused DPS passes in isolation (B=64, 3x256x256) for one library build.
+"""Time the fused DPS passes in isolation (B=64, 3x256x256; BATCH / IMAGE override) for one
+library build.
 
     SAMPLERS_HIP_LIB=build/variants/lib_k8.so python tools/bench_kernels.py [label]
 
@@ -50,8 +51,9 @@ def main():
     label = sys.argv[1] if len(sys.argv) > 1 else os.environ.get("SAMPLERS_HIP_LIB", "default")
     lib = _hip.load_library()
     dev = torch.device("cuda")
-    B, shape = 64, (3, 256, 256)
-    n = 3 * 256 * 256
+    img = int(os.environ.get("IMAGE", "256"))
+    B, shape = int(os.environ.get("BATCH", "64")), (3, img, img)
+    n = 3 * img * img
     st = torch.cuda.current_stream().cuda_stream
     # achievable HBM bandwidth reference: device copy of 4 buffers' worth
     src = torch.randn(B, n, device=dev)
@@ -85,7 +87,8 @@ def main():
         b2 = 4 * ((5 if needs_v else 4) * n + (0 if needs_v else m)) * B
         for kname, fn, nb in (("dps_residual", k1, b1), ("dps_update", k2, b2)):
             us = timeit(fn)
-            print(json.dumps({"lib": label, "op": name, "kernel": kname, "us": round(us, 2),
+            print(json.dumps({"lib": label, "op": name, "kernel": kname, "batch": B, "image": img,
+                              "us": round(us, 2),
                               "GB/s": round(nb / us / 1e3, 1), "frac": round(nb / us / 1e3 / 8000, 3)}),
                   flush=True)
 

@@ -92,8 +92,13 @@ def main():
                    help="also time one whole ReSampleSampler.__call__ with N sampling steps "
                         "(time travel every 5 indices, the reference's stopping rules, "
                         "--max-iters AdamW iterations at most)")
-    p.add_argument("--max-iters", type=int, default=220,
-                   help="max_optimization_iters of the whole call (the plateau rule needs > 200)")
+    p.add_argument("--max-iters", type=int, default=2000,
+                   help="max_optimization_iters of the whole call (resample.py:56 default 2000; "
+                        "the plateau rule needs > 200)")
+    p.add_argument("--time-travel-interval", type=int, default=10,
+                   help="time_travel_interval of the whole call (resample.py:59 default 10)")
+    p.add_argument("--full-batch", type=int, default=0,
+                   help="samples per rank of the whole call (default: --batch)")
     p.add_argument("--cpu-baseline", action="store_true",
                    help="also time one main-loop iteration and one latent AdamW iteration of "
                         "oracle/resample_loop.py on the host cores (batch 1)")
@@ -185,15 +190,23 @@ def main():
         # the reference's stopping rules (resample_kernels.py:32-93)
         from samplers_amd.inverse_problem import InverseProblem
 
-        prob = InverseProblem(op, y, noise)
+        fb = args.full_batch or b
+        prob = InverseProblem(op, y[:fb], noise)
         kw = dict(num_sampling_steps=args.full_call, max_optimization_iters=args.max_iters,
-                  time_travel_interval=5, seed=seed, sample_offset=off, group=group,
-                  condition=StableDiffusionCondition(prompt=[""] * b))
+                  time_travel_interval=args.time_travel_interval, seed=seed, sample_offset=off,
+                  group=group, condition=StableDiffusionCondition(prompt=[""] * fb))
         wall = timed(lambda: sampler(prob, **kw), 1, "full call", world, rank)
+        log = getattr(sampler, "optimization_log", [])
         full = {"num_sampling_steps": args.full_call, "guided_iterations": args.full_call - 2,
-                "max_optimization_iters": args.max_iters, "time_travel_interval": 5,
-                "wall_s": round(wall, 2), "gpu_s_per_sample": round(wall / b, 3),
-                "samples_x_steps_per_s": round(b * world * (args.full_call - 2) / wall, 4)}
+                "batch_per_gpu": fb, "max_optimization_iters": args.max_iters,
+                "time_travel_interval": args.time_travel_interval,
+                "wall_s": round(wall, 2), "gpu_s_per_sample": round(wall / fb, 3),
+                "samples_x_steps_per_s": round(fb * world * (args.full_call - 2) / wall, 4),
+                # every hard-consistency solve: the AdamW iterations the reference's stopping
+                # rules ran (loss below eps^2; latent: from iteration 200 a rising loss)
+                "solves": log,
+                "adamw_iterations": {k: sum(r["iterations"] for r in log if r["kind"] == k)
+                                     for k in ("pixel", "latent")}}
     cpu = None
     if args.cpu_baseline and rank == 0:
         cpu = cpu_baseline_resample(args.image)
