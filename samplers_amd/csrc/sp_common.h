@@ -135,6 +135,21 @@ __device__ __forceinline__ float sum_partials(const float* __restrict__ p, int P
     return wave_sum(s);
 }
 
+// The same total for a whole block of kBlock threads: wave w adds its quarter of the partials
+// (lane-strided), the four wave sums meet in LDS in a fixed order — deterministic and equal in
+// every block of the sample, a quarter of sum_partials' loads per wave (at 3x512² P = 384:
+// the update pass spent 8 µs of 50 re-reading them, round 4).  Every thread must call it.
+__device__ __forceinline__ float block_sum_partials(const float* __restrict__ p, int P, float* lds4) {
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int q = (P + 3) >> 2, lo = w * q, hi = min(P, lo + q);
+    float s = 0.f;
+    for (int i = lo + lane; i < hi; i += 64) s += p[i];
+    s = wave_sum(s);
+    if (lane == 0) lds4[w] = s;
+    __syncthreads();
+    return (lds4[0] + lds4[1]) + (lds4[2] + lds4[3]);
+}
+
 // ---------------------------------------------------------------------------
 // Vector access
 // ---------------------------------------------------------------------------

@@ -231,8 +231,9 @@ __global__ __launch_bounds__(kBlock, SP_UPD_WAVES) void k_dps_update(
     SP_DCHECK(!partial || P > 0);
     const float inv_a = 1.f / c.a;
     // DPS: gamma / (||r_b|| + eps); without partials a fixed factor (PGDM, PSLD)
+    __shared__ float red4[4];
     const float scale =
-        partial ? c.gamma / (sqrtf(sum_partials(partial + b * P, P)) + c.norm_eps) : c.gamma;
+        partial ? c.gamma / (sqrtf(block_sum_partials(partial + b * P, P, red4)) + c.norm_eps) : c.gamma;
 #pragma unroll
     for (int it = 0; it < kIter; ++it) {
         const int64_t j = j0 + it * (kBlock * V);

@@ -65,6 +65,37 @@ def timestep_embedding(t: Tensor, dim: int, *, flip_sin_to_cos: bool, freq_shift
     return emb
 
 
+def temb_projections(model: nn.Module, emb: Tensor) -> dict[int, Tensor]:
+    """Every ResnetBlock2D's ``time_emb_proj(silu(emb))`` of ``model`` at once: one SiLU and one
+    batched GEMM per projection width (the blocks' weights stacked, cached on the model) instead
+    of a SiLU, a copy and a GEMM per block — 3 launches instead of ~70 per UNet forward, which
+    is most of the step's launches at batch 1.  Returns {id(block): [B, C] contiguous}; empty
+    when a projection is trainable (the per-block path keeps the gradients)."""
+    blocks = [m for m in model.modules() if isinstance(m, ResnetBlock2D) and m.time_emb_proj is not None]
+    if not blocks or any(p.requires_grad for b in blocks for p in b.time_emb_proj.parameters()):
+        return {}
+    key = (emb.device, emb.dtype, tuple((id(b.time_emb_proj.weight), b.time_emb_proj.weight._version,
+                                         b.time_emb_proj.bias._version) for b in blocks))
+    cache = model.__dict__.setdefault("_temb_stacks", {})
+    if cache.get("key") != key:
+        groups: dict[int, list] = {}
+        for b in blocks:
+            groups.setdefault(b.time_emb_proj.out_features, []).append(b)
+        cache.clear()
+        cache["key"] = key
+        cache["groups"] = [
+            ([id(b) for b in members],
+             torch.stack([b.time_emb_proj.weight.detach().t() for b in members]).to(emb.device, emb.dtype),
+             torch.stack([b.time_emb_proj.bias.detach()[None] for b in members]).to(emb.device, emb.dtype))
+            for members in groups.values()]
+    s = F.silu(emb)
+    out = {}
+    for ids, wt, bias in cache["groups"]:
+        y = torch.baddbmm(bias, s.expand(len(ids), *s.shape), wt)  # [blocks][B][C]
+        out.update(zip(ids, y.unbind(0)))
+    return out
+
+
 class TimestepEmbedding(nn.Module):
     def __init__(self, in_dim: int, out_dim: int) -> None:
         super().__init__()
@@ -238,12 +269,15 @@ class ResnetBlock2D(nn.Module):
                 and x[0, 0].numel() % 4 == 0)
 
     def forward(self, x: Tensor, temb: Tensor | None = None, skip: Tensor | None = None,
-                box_in: SkipGrad | None = None, box_out: SkipGrad | None = None) -> Tensor:
+                box_in: SkipGrad | None = None, box_out: SkipGrad | None = None,
+                tb: Tensor | None = None) -> Tensor:
         """``box_in``: ``x`` is a UNet skip tensor (the mailbox of its up-block gradient);
-        ``box_out``: the mailbox of ``skip`` (see ``SkipGrad``)."""
+        ``box_out``: the mailbox of ``skip`` (see ``SkipGrad``); ``tb``: this block's
+        ``time_emb_proj(silu(temb))`` already computed (``temb_projections``)."""
         if box_in is not None and skip is not None:
             raise ValueError("box_in (x is a skip tensor) and skip (an up-block input) are exclusive")
-        tb = self.time_emb_proj(F.silu(temb)) if self.time_emb_proj is not None else None
+        if tb is None and self.time_emb_proj is not None:
+            tb = self.time_emb_proj(F.silu(temb))
         if (self._fusable(x) and (skip is None or skip.dtype == x.dtype)
                 and (box_in is None or box_in.enabled)):
             x1 = x.contiguous()
@@ -280,6 +314,34 @@ def attention_backend() -> str:
     return os.environ.get("SAMPLERS_AMD_ATTN", "gemm").lower()
 
 
+def _score_chunks(b: int, n: int, m: int) -> int:
+    """Query-row chunks of a score GEMM (n x m scores, one per batch entry).  hipBLASLt serves
+    the 16² level's 256 x 256 x 512 product with one 256 x 256 macro tile per batch entry (one
+    CU at b = 1: 119 µs); cut into row chunks (k repeated per chunk) it spreads over more
+    workgroups: 23 µs at b = 1 (8 chunks), 74 vs 120 µs at b = 64 (4 chunks).  The VAE's
+    4096-token scores already fill the chip (chunking measured slower at b >= 2).
+    tools/bench_score_gemm.py, profiles/round4/score_gemm.jsonl."""
+    if n * m > 1024 * 1024 or n % 8:
+        return 1
+    return 4 if b >= 32 else 8
+
+
+def score_gemm(a: Tensor, bm: Tensor, alpha: float, out: Tensor) -> Tensor:
+    """out[i] = alpha · a[i] bm[i]ᵀ for a (b, n, d), bm (b, m, d) (strided views allowed),
+    out (b, n, m) contiguous; query rows chunked where that fills the chip (``_score_chunks``)."""
+    b, n, d = a.shape
+    m = bm.shape[1]
+    ch = _score_chunks(b, n, m)
+    if ch == 1:
+        return torch.baddbmm(out, a, bm.transpose(1, 2), beta=0.0, alpha=alpha, out=out)
+    r = n // ch
+    ac = a.reshape(b * ch, r, d)  # a view: the chunks of a batch entry are consecutive rows
+    bc = bm.unsqueeze(1).expand(b, ch, m, d).reshape(b * ch, m, d)
+    oc = out.view(b * ch, r, m)
+    torch.baddbmm(oc, ac, bc.transpose(1, 2), beta=0.0, alpha=alpha, out=oc)
+    return out
+
+
 class _ScoreAttentionQKV(torch.autograd.Function):
     """``_ScoreAttention`` on the fused projection's output ``qkv`` ([b][n][3c], q, k, v its
     thirds read in place); the VJP writes dq, dk, dv straight into one [b][n][3c] cotangent
@@ -292,8 +354,7 @@ class _ScoreAttentionQKV(torch.autograd.Function):
         c = c3 // 3
         q, k, v = qkv.split(c, dim=-1)
         scale = 1.0 / math.sqrt(c)
-        p = torch.baddbmm(torch.empty(b, n, n, device=qkv.device, dtype=qkv.dtype), q, k.transpose(1, 2),
-                          beta=0.0, alpha=scale)
+        p = score_gemm(q, k, scale, torch.empty(b, n, n, device=qkv.device, dtype=qkv.dtype))
         _hip.check(lib.sp_softmax_rows(_hip.ptr(p), b * n, n, None, _hip.stream_of(p)), "sp_softmax_rows")
         ctx.save_for_backward(qkv, p)
         ctx.scale = scale
@@ -309,7 +370,7 @@ class _ScoreAttentionQKV(torch.autograd.Function):
         dqkv = torch.empty_like(qkv)
         dq, dk, dv = dqkv.split(c, dim=-1)
         torch.bmm(p.transpose(1, 2), dout, out=dv)
-        ds = torch.bmm(dout, v.transpose(1, 2))
+        ds = score_gemm(dout, v, 1.0, torch.empty(b, n, n, device=qkv.device, dtype=qkv.dtype))
         _hip.check(lib.sp_softmax_bwd_rows(_hip.ptr(p), _hip.ptr(ds), b * n, n, ctx.scale, _hip.stream_of(ds)),
                    "sp_softmax_bwd_rows")
         torch.bmm(ds, k, out=dq)
@@ -329,8 +390,7 @@ class _ScoreAttention(torch.autograd.Function):
         bh, n, d = q.shape
         m = k.shape[1]
         scale = 1.0 / math.sqrt(d)
-        p = torch.baddbmm(torch.empty(bh, n, m, device=q.device, dtype=q.dtype), q, k.transpose(1, 2),
-                          beta=0.0, alpha=scale)
+        p = score_gemm(q, k, scale, torch.empty(bh, n, m, device=q.device, dtype=q.dtype))
         _hip.check(lib.sp_softmax_rows(_hip.ptr(p), bh * n, m, None, _hip.stream_of(p)), "sp_softmax_rows")
         ctx.save_for_backward(q, k, v, p)
         ctx.scale = scale
@@ -345,7 +405,7 @@ class _ScoreAttention(torch.autograd.Function):
         dv = torch.bmm(p.transpose(1, 2), dout) if need_v else None
         dq = dk = None
         if need_q or need_k:
-            ds = torch.bmm(dout, v.transpose(1, 2))
+            ds = score_gemm(dout, v, 1.0, torch.empty(bh, n, m, device=dout.device, dtype=dout.dtype))
             _hip.check(lib.sp_softmax_bwd_rows(_hip.ptr(p), _hip.ptr(ds), bh * n, m, ctx.scale,
                                                _hip.stream_of(ds)), "sp_softmax_bwd_rows")
             dq = torch.bmm(ds, k) if need_q else None
@@ -524,6 +584,7 @@ class UNet2DModel(nn.Module):
             flip_sin_to_cos=cfg.flip_sin_to_cos, freq_shift=cfg.freq_shift,
         ).to(sample.dtype)
         emb = self.time_embedding(t_emb)
+        tbs = temb_projections(self, emb)
 
         # every skip tensor has two consumers (the next down-path layer and an up-block
         # resnet); with grad on the device their gradients meet inside the down-path
@@ -534,7 +595,7 @@ class UNet2DModel(nn.Module):
         skips, boxes = [h], [new_box()]
         for lvl in self.down_blocks:
             for j, res in enumerate(lvl.resnets):
-                h = res(h, emb, box_in=boxes[-1] if skips[-1] is h else None)
+                h = res(h, emb, box_in=boxes[-1] if skips[-1] is h else None, tb=tbs.get(id(res)))
                 if len(lvl.attentions):
                     h = lvl.attentions[j](h)
                 skips.append(h)
@@ -544,13 +605,14 @@ class UNet2DModel(nn.Module):
                 skips.append(h)
                 boxes.append(new_box())
 
-        h = self.mid_block.resnets[0](h, emb, box_in=boxes[-1])
+        m0, m1 = self.mid_block.resnets
+        h = m0(h, emb, box_in=boxes[-1], tb=tbs.get(id(m0)))
         h = self.mid_block.attentions[0](h)
-        h = self.mid_block.resnets[1](h, emb)
+        h = m1(h, emb, tb=tbs.get(id(m1)))
 
         for lvl in self.up_blocks:
             for j, res in enumerate(lvl.resnets):
-                h = res(h, emb, skip=skips.pop(), box_out=boxes.pop())
+                h = res(h, emb, skip=skips.pop(), box_out=boxes.pop(), tb=tbs.get(id(res)))
                 if len(lvl.attentions):
                     h = lvl.attentions[j](h)
             if lvl.upsamplers is not None:

@@ -36,7 +36,7 @@ from .attention import (attention, fused_cross_attention, fused_cross_supported,
                         fused_qkv_supported)
 from .layers import (Conv3x3, GroupNormAct, LayerNorm, Linear, SkipGrad, conv3x3_stride2, geglu,
                      linear, proj_nchw_to_tokens, proj_tokens_to_nchw)
-from .unet2d import ResnetBlock2D, TimestepEmbedding, Upsample2D, timestep_embedding
+from .unet2d import ResnetBlock2D, TimestepEmbedding, Upsample2D, temb_projections, timestep_embedding
 
 
 @dataclass(frozen=True)
@@ -281,6 +281,7 @@ class UNet2DConditionModel(nn.Module):
                                    flip_sin_to_cos=cfg.flip_sin_to_cos,
                                    freq_shift=cfg.freq_shift).to(sample.dtype)
         emb = self.time_embedding(t_emb)
+        tbs = temb_projections(self, emb)  # every block's time-embedding projection at once
         ctx = encoder_hidden_states.to(sample.dtype)
 
         # skip tensors' two gradients meet inside the down-path consumer's VJP kernel
@@ -291,7 +292,7 @@ class UNet2DConditionModel(nn.Module):
         skips, boxes = [h], [new_box()]
         for lvl in self.down_blocks:
             for j, res in enumerate(lvl.resnets):
-                h = res(h, emb, box_in=boxes[-1] if skips[-1] is h else None)
+                h = res(h, emb, box_in=boxes[-1] if skips[-1] is h else None, tb=tbs.get(id(res)))
                 if len(lvl.attentions):
                     h = lvl.attentions[j](h, ctx)
                 skips.append(h)
@@ -301,13 +302,14 @@ class UNet2DConditionModel(nn.Module):
                 skips.append(h)
                 boxes.append(new_box())
 
-        h = self.mid_block.resnets[0](h, emb, box_in=boxes[-1])
+        m0, m1 = self.mid_block.resnets
+        h = m0(h, emb, box_in=boxes[-1], tb=tbs.get(id(m0)))
         h = self.mid_block.attentions[0](h, ctx)
-        h = self.mid_block.resnets[1](h, emb)
+        h = m1(h, emb, tb=tbs.get(id(m1)))
 
         for lvl in self.up_blocks:
             for j, res in enumerate(lvl.resnets):
-                h = res(h, emb, skip=skips.pop(), box_out=boxes.pop())
+                h = res(h, emb, skip=skips.pop(), box_out=boxes.pop(), tb=tbs.get(id(res)))
                 if len(lvl.attentions):
                     h = lvl.attentions[j](h, ctx)
             if lvl.upsamplers is not None:

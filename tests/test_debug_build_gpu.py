@@ -64,10 +64,13 @@ for op in (RandomInpaintingOperator(shape, 0.5, seed=1).to(dev),
     assert n == 0, (type(op).__name__, n, site)
 del net, step
 
-from samplers_amd.networks.latent import LatentDiffusionNetwork
+from samplers_amd.networks.latent import LatentDiffusionNetwork, StableDiffusionCondition
 from samplers_amd.samplers.psld import FusedPSLDStep
 lnet = LatentDiffusionNetwork.from_config(seed=0, device=dev)
 lnet.set_sampling_parameters(4, batch_size=1)
+# CFG on (distinct prompt embeddings): the doubled batch, cross-attention to real contexts
+lnet.set_condition(StableDiffusionCondition(prompt=None, prompt_embeds=torch.randn(1, 77, 768),
+                                            guidance_scale=7.5))
 op = CenterInpaintingOperator(shape, 0.5).to(dev)
 y = op.apply(torch.rand((1, *shape), device=dev) * 2 - 1)
 prob = InverseProblem(op, y, GaussianNoise(0.05).to(dev))
