@@ -170,6 +170,28 @@ def _is_gaussian(noise) -> bool:
         c.__name__ == "GaussianNoise" for c in type(noise).__mro__)
 
 
+def _loss_log(max_iters: int, device) -> Tensor:
+    """Per-iteration losses of one hard-consistency solve, written by the device check
+    (``loss_out``); a check after the stop writes nothing, so the entries left NaN count the
+    iterations the stopping rule skipped."""
+    return torch.full((max(max_iters, 1),), float("nan"), device=device)
+
+
+def _log_solve(owner, kind: str, losses: Tensor, trips: int, max_iters: int) -> None:
+    """Append one solve's record to ``owner.optimization_log`` (the sampler's; reset per
+    ``__call__``; nothing when there is no owner): the iterations the reference's stopping rule
+    ran (``resample_kernels.py:32-93``), the host loop's trips (a few more: the flag is read
+    late), the final loss."""
+    if owner is None:
+        return
+    done = losses[:max(trips, 0)]
+    ran = int(torch.isfinite(done).sum())
+    last = float(done[ran - 1]) if ran else float("nan")
+    owner.__dict__.setdefault("optimization_log", []).append(
+        {"kind": kind, "iterations": ran, "host_trips": trips, "max_iters": max_iters,
+         "stopped_early": ran < max_iters, "final_loss": last})
+
+
 def make_consistency(operator, y_rows: Tensor, y_div: int, group=None) -> _Consistency:
     if getattr(operator, "hip_descriptor", lambda: None)() is None:
         return _GenericConsistency(operator, y_rows, y_div, group)
@@ -246,7 +268,7 @@ class ReSampleSampler(PosteriorSampler, Generic[Condition_co]):
         shared = dist.is_initialized() and dist.get_world_size(cons.group) > 1
         part = torch.empty(b, int(lib.sp_rsq_partials(cons.desc)), device=x.device) if fused else None
         ss = torch.empty(1, device=x.device)
-        losses = self._loss_log(max_iters, x.device)
+        losses = _loss_log(max_iters, x.device)
         it = -1
         for it in range(max_iters):
             c = adamw_coefficients(it + 1, 1e-2)
@@ -272,7 +294,7 @@ class ReSampleSampler(PosteriorSampler, Generic[Condition_co]):
                                         _hip.ptr(losses) + 4 * it, stream), "sp_opt_check")
             if (it + 1) % check_every == 0 and int(stop.item()):
                 break
-        self._log_solve("pixel", losses, it + 1, max_iters)
+        _log_solve(self, "pixel", losses, it + 1, max_iters)
         return x
 
     def _latent_optimization(self, z0: Tensor, cons: _Consistency, total: int, eps: float,
@@ -295,7 +317,7 @@ class ReSampleSampler(PosteriorSampler, Generic[Condition_co]):
         events = [torch.cuda.Event(), torch.cuda.Event()]
         stream = _hip.stream_of(z)
         tot, thr = float(np.float32(total)), float(eps) ** 2
-        losses = self._loss_log(max_iters, z.device)
+        losses = _loss_log(max_iters, z.device)
         itr = -1
         for itr in range(max_iters):
             with torch.enable_grad():
@@ -319,26 +341,8 @@ class ReSampleSampler(PosteriorSampler, Generic[Condition_co]):
                 events[slot ^ 1].synchronize()
                 if int(flags[slot ^ 1]):
                     break
-        self._log_solve("latent", losses, itr + 1, max_iters)
+        _log_solve(self, "latent", losses, itr + 1, max_iters)
         return z
-
-    @staticmethod
-    def _loss_log(max_iters: int, device) -> Tensor:
-        """Per-iteration losses of one hard-consistency solve, written by the device check
-        (``loss_out``); a check after the stop writes nothing, so the entries left NaN count
-        the iterations the stopping rule skipped."""
-        return torch.full((max(max_iters, 1),), float("nan"), device=device)
-
-    def _log_solve(self, kind: str, losses: Tensor, trips: int, max_iters: int) -> None:
-        """Append one solve's record to ``self.optimization_log`` (reset per ``__call__``):
-        the iterations the reference's stopping rule ran (``resample_kernels.py:32-93``),
-        the host loop's trips (a few more: the flag is read late), the final loss."""
-        done = losses[:trips]
-        ran = int(torch.isfinite(done).sum())
-        last = float(done[ran - 1]) if ran else float("nan")
-        self.__dict__.setdefault("optimization_log", []).append(
-            {"kind": kind, "iterations": ran, "host_trips": trips, "max_iters": max_iters,
-             "stopped_early": ran < max_iters, "final_loss": last})
 
     def _resample(self, z_opt: Tensor, snapshot: Tensor, a_prev: float, sigma: float,
                   noise: Tensor | None, seed: int, key: int, offset: int) -> Tensor:

@@ -6,6 +6,8 @@ fp32 oracle to the reference bit-exactly).  PGDM amplifies perturbations strongl
 these stand-in priors (its outputs reach 1e7), hence the per-case bound.
 """
 
+import types
+
 import numpy as np
 import pytest
 import torch
@@ -271,8 +273,12 @@ def test_pixel_optimization_device_stop_matches_reference_loop(cuda, kind):
     ref, ref_losses = reference(2000, thr)
     assert len(ref_losses) == stop_at + 1
     cons = _Consistency(op, y.to(cuda), 1)
-    out = ReSampleSampler._pixel_optimization(None, x0.to(cuda), cons, total, thr ** 0.5, 2000)
+    holder = types.SimpleNamespace()  # stands in for the sampler: receives the solve's record
+    out = ReSampleSampler._pixel_optimization(holder, x0.to(cuda), cons, total, thr ** 0.5, 2000)
     err = float((out.cpu() - ref).norm() / ref.norm())
+    (rec,) = holder.optimization_log  # the iterations the stopping rule ran, from the device
+    assert rec["kind"] == "pixel" and rec["iterations"] == stop_at + 1 and rec["stopped_early"]
+    assert abs(rec["final_loss"] - ref_losses[-1]) <= 1e-5 * abs(ref_losses[-1])
     one_more, _ = reference(stop_at + 2)
     assert err < 1e-5, err
     assert float((one_more - ref).norm() / ref.norm()) > 100 * max(err, 1e-7)
