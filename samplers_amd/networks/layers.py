@@ -542,6 +542,18 @@ def downsample_conv(module: nn.Conv2d, x: Tensor, box: SkipGrad | None = None) -
 # nn.Linear on token-major activations: fp32 arithmetic on the bf16 MFMAs (csrc/sp_gemm_x6.hip)
 # ---------------------------------------------------------------------------------------
 
+def x6_enough_tiles(rows: int, cols: int) -> bool:
+    """Whether a bf16x6 GEMM call of ``rows`` pixels / tokens x ``cols`` output features fills
+    enough of the chip: at least ``SAMPLERS_AMD_X6_MIN_TILES`` (default 128) of its 256 x 128
+    output tiles.  Below that (batch 1, the low-resolution levels) its persistent tiles walk a
+    long K loop on a few CUs and hipBLASLt's fp32 GEMM, with smaller tiles, is the faster of the
+    two; 0 keeps x6 wherever its shape rules hold."""
+    import os
+
+    need = int(os.environ.get("SAMPLERS_AMD_X6_MIN_TILES", "128"))
+    return need <= 0 or -(-rows // 256) * -(-cols // 128) >= need
+
+
 def linear_backend() -> str:
     """``SAMPLERS_AMD_LINEAR``: ``x6`` (default: ``sp_linear_x6`` where its shape rules hold —
     exact three-term bf16 splits of the fp32 operands, six partial products, fp32
@@ -622,7 +634,7 @@ def linear(x: Tensor, module: nn.Module, w2d: Tensor | None = None, bias: Tensor
             and (bias is None or not bias.requires_grad) and linear_backend() == "x6"
             and (res is None or (res.dtype == torch.float32 and res.numel() == t * m))):
         lib = _hip.load_library()
-        if lib.sp_linear_x6_supported(t, k, m):
+        if lib.sp_linear_x6_supported(t, k, m) and x6_enough_tiles(t, m):
             return _LinearX6Fn.apply(x, w2d, bias, module, w2d, res, box)
     if box is not None:
         box.enabled = False
@@ -671,7 +683,8 @@ class _ProjLayoutFn(torch.autograd.Function):
 def _layout_ok(x: Tensor, w2d: Tensor, n: int, hw: int) -> bool:
     m, k = w2d.shape
     return (x.is_cuda and x.dtype == torch.float32 and not w2d.requires_grad and linear_backend() == "x6"
-            and bool(_hip.load_library().sp_gemm_x6_layout_supported(n, hw, k, m)))
+            and bool(_hip.load_library().sp_gemm_x6_layout_supported(n, hw, k, m))
+            and x6_enough_tiles(n * hw, m))
 
 
 def proj_nchw_to_tokens(x: Tensor, module, w2d: Tensor | None = None, bias: Tensor | None = None) -> Tensor:

@@ -31,7 +31,7 @@ from torch import Tensor, nn
 from .. import _hip
 from .layers import (Conv3x3, GroupNormAct, Linear, SkipGrad, conv3x3_forward, conv3x3_input_vjp,
                      downsample_conv, gn_backward, gn_forward, miopen_fallback, proj_nchw_to_tokens,
-                     proj_tokens_to_nchw, upsample_nearest2x)
+                     proj_tokens_to_nchw, upsample_nearest2x, x6_enough_tiles)
 
 
 @dataclass(frozen=True)
@@ -136,10 +136,11 @@ def _pointwise_pack(conv: nn.Conv2d, trans: bool) -> Tensor:
     return cache[trans]
 
 
-def _x6_ok(m: int, c1: int, c2: int, o1: int, o2: int, hw: int) -> bool:
+def _x6_ok(m: int, c1: int, c2: int, o1: int, o2: int, hw: int, n: int) -> bool:
     lib = _hip.load_library()
     return (_shortcut_backend() == "x6" and bool(lib.sp_gemm_x6_supported(m, c1 + c2, hw))
-            and c1 % 8 == 0 and c2 % 8 == 0 and o1 % 32 == 0 and o2 % 32 == 0)
+            and c1 % 8 == 0 and c2 % 8 == 0 and o1 % 32 == 0 and o2 % 32 == 0
+            and x6_enough_tiles(n * hw, o1 + o2))
 
 
 def _shortcut_forward(conv: nn.Conv2d, x1: Tensor, x2: Tensor | None) -> Tensor:
@@ -152,7 +153,7 @@ def _shortcut_forward(conv: nn.Conv2d, x1: Tensor, x2: Tensor | None) -> Tensor:
     c2 = 0 if x2 is None else x2.shape[1]
     cout = conv.out_channels
     hw = x1[0, 0].numel()
-    if _x6_ok(cout, c1, c2, cout, 0, hw):
+    if _x6_ok(cout, c1, c2, cout, 0, hw, n):
         lib = _hip.load_library()
         x1 = x1.contiguous()
         x2 = None if x2 is None else x2.contiguous()
@@ -174,7 +175,7 @@ def _shortcut_input_vjp(conv: nn.Conv2d, dy: Tensor, c1: int, c2: int) -> tuple[
     or two fp32 batched GEMMs."""
     n, cout = dy.shape[:2]
     hw = dy[0, 0].numel()
-    if _x6_ok(c1 + c2, cout, 0, c1, c2, hw):
+    if _x6_ok(c1 + c2, cout, 0, c1, c2, hw, n):
         lib = _hip.load_library()
         dy = dy.contiguous()
         d1 = torch.empty((n, c1) + tuple(dy.shape[2:]), device=dy.device, dtype=torch.float32)
