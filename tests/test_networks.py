@@ -114,3 +114,47 @@ def test_from_pretrained_never_fetches(tmp_path):
 
     with pytest.raises(FileNotFoundError, match="never fetches"):
         DDPMNetwork.from_pretrained("google/ddpm-celebahq-256", cache_dir=str(tmp_path))
+
+
+def test_batched_time_embedding_projections_equal_per_block():
+    """unet2d.temb_projections: every ResnetBlock's time_emb_proj(silu(temb)) from one batched
+    GEMM per projection width equals the per-block nn.Linear (to fp32 rounding), contiguous
+    [B, C] per block; the whole UNet forward agrees with the per-block path; trainable
+    projections fall back to the per-block path (gradients reach the parameters)."""
+    import torch.nn.functional as F
+
+    from samplers_amd.networks.unet2d import ResnetBlock2D, UNet2DConfig, build_unet, temb_projections
+
+    cfg = UNet2DConfig(sample_size=16, block_out_channels=(32, 64), attention_levels=(1,),
+                       layers_per_block=1)
+    net = build_unet(cfg, seed=1)
+    emb = net.time_embedding(torch.randn(3, 32))
+    tbs = temb_projections(net, emb)
+    blocks = [m for m in net.modules() if isinstance(m, ResnetBlock2D) and m.time_emb_proj is not None]
+    assert len(tbs) == len(blocks) > 0
+    for b in blocks:
+        ref = b.time_emb_proj(F.silu(emb))
+        assert tbs[id(b)].is_contiguous() and tbs[id(b)].shape == ref.shape
+        torch.testing.assert_close(tbs[id(b)], ref, rtol=1e-6, atol=1e-6)
+    x = torch.randn(3, 3, 16, 16)
+    y = net(x, 321)
+    blocks[0].time_emb_proj.weight.requires_grad_(True)  # -> per-block path
+    assert temb_projections(net, emb) == {}
+    y2 = net(x, 321)
+    torch.testing.assert_close(y, y2, rtol=1e-5, atol=1e-5)
+
+
+def test_score_gemm_chunks_equal_plain_bmm():
+    """unet2d.score_gemm: query-row chunks (k repeated per chunk) give alpha q kᵀ for strided
+    q / k views (the thirds of a fused projection), at the chunk counts the size rule picks."""
+    from samplers_amd.networks.unet2d import _score_chunks, score_gemm
+
+    assert _score_chunks(1, 256, 256) == 8 and _score_chunks(64, 256, 256) == 4
+    assert _score_chunks(2, 4096, 4096) == 1
+    g = torch.Generator().manual_seed(2)
+    for b, n, d in ((1, 256, 64), (2, 64, 32), (40, 64, 16)):
+        qkv = torch.randn(b, n, 3 * d, generator=g)
+        q, k, _ = qkv.split(d, dim=-1)
+        out = torch.empty(b, n, n)
+        score_gemm(q, k, 0.25, out)
+        torch.testing.assert_close(out, 0.25 * q @ k.transpose(1, 2), rtol=1e-5, atol=1e-5)
