@@ -543,14 +543,14 @@ def downsample_conv(module: nn.Conv2d, x: Tensor, box: SkipGrad | None = None) -
 # ---------------------------------------------------------------------------------------
 
 def x6_enough_tiles(rows: int, cols: int) -> bool:
-    """Whether a bf16x6 GEMM call of ``rows`` pixels / tokens x ``cols`` output features fills
-    enough of the chip: at least ``SAMPLERS_AMD_X6_MIN_TILES`` (default 128) of its 256 x 128
-    output tiles.  Below that (batch 1, the low-resolution levels) its persistent tiles walk a
-    long K loop on a few CUs and hipBLASLt's fp32 GEMM, with smaller tiles, is the faster of the
-    two; 0 keeps x6 wherever its shape rules hold."""
+    """Whether a bf16x6 GEMM call of ``rows`` pixels / tokens x ``cols`` output features should
+    run on the x6 tile: at least ``SAMPLERS_AMD_X6_MIN_TILES`` of its 256 x 128 output tiles
+    (default 0: always — measured, round 4: sending the calls below 128 tiles to hipBLASLt's
+    fp32 GEMM made the batch-1 DPS step 14.6 -> 28.1 ms, hipBLASLt's choices for these small
+    shapes being worse still; profiles/round4/b1/x6_min_tiles_ab.txt)."""
     import os
 
-    need = int(os.environ.get("SAMPLERS_AMD_X6_MIN_TILES", "128"))
+    need = int(os.environ.get("SAMPLERS_AMD_X6_MIN_TILES", "0"))
     return need <= 0 or -(-rows // 256) * -(-cols // 128) >= need
 
 

@@ -362,14 +362,14 @@ def test_fp32_view_of_networks():
 
 
 def test_x6_size_rule(monkeypatch):
-    """The bf16x6 GEMMs serve a call only with >= SAMPLERS_AMD_X6_MIN_TILES 256 x 128 output
-    tiles (default 128); 0 disables the rule."""
+    """SAMPLERS_AMD_X6_MIN_TILES: the bf16x6 GEMMs serve a call only with at least that many
+    256 x 128 output tiles; the default (0) keeps them everywhere their shape rules hold."""
     from samplers_amd.networks.layers import x6_enough_tiles
 
     monkeypatch.delenv("SAMPLERS_AMD_X6_MIN_TILES", raising=False)
+    assert x6_enough_tiles(256, 128) and x6_enough_tiles(1 * 32 * 32, 512)
+    monkeypatch.setenv("SAMPLERS_AMD_X6_MIN_TILES", "128")
     assert x6_enough_tiles(64 * 256 * 256, 128)         # headline 256² level: 16384 tiles
     assert x6_enough_tiles(64 * 16 * 16, 512)           # headline 16² level: 256 tiles
     assert not x6_enough_tiles(1 * 32 * 32, 512)        # batch 1, 32² level: 16 tiles
     assert x6_enough_tiles(1 * 256 * 256, 128)          # batch 1, 256² level: 256 tiles
-    monkeypatch.setenv("SAMPLERS_AMD_X6_MIN_TILES", "0")
-    assert x6_enough_tiles(256, 128)
