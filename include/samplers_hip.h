@@ -372,6 +372,18 @@ int sp_conv3x3_s2_fwd(const float* x, const float* wp, const float* bias, int64_
 int sp_conv3x3_s2_bwd_input(const float* dy, const float* wp_vjp, int64_t n, int32_t cin,
                             int32_t cout, int32_t height, int32_t width, int32_t accumulate,
                             float* dx, sp_stream_t stream);
+/* Split-K forms (a workspace; same results to fp32 rounding, bitwise reproducible): a launch
+ * whose workgroups fill less than half the CUs (batch 1) runs 2-16 parts over K that store
+ * partial sums to ws, then adds them in a fixed order (+ bias, or onto dx with accumulate).
+ * sp_conv3x3_s2_workspace = the bytes a launch needs, 0 = not split (ws may be NULL). */
+int64_t sp_conv3x3_s2_workspace(int64_t n, int32_t cin, int32_t cout, int32_t height, int32_t width,
+                                int32_t input_vjp);
+int sp_conv3x3_s2_fwd_ws(const float* x, const float* wp, const float* bias, int64_t n, int32_t cin,
+                         int32_t cout, int32_t height, int32_t width, float* y, float* ws, int64_t ws_bytes,
+                         sp_stream_t stream);
+int sp_conv3x3_s2_bwd_input_ws(const float* dy, const float* wp_vjp, int64_t n, int32_t cin,
+                               int32_t cout, int32_t height, int32_t width, int32_t accumulate,
+                               float* dx, float* ws, int64_t ws_bytes, sp_stream_t stream);
 
 /* The same layers by Winograd F(2x2,3x3) on fp32 MFMA (2.25x fewer multiplies; the
  * transforms add F(2,3) rounding, as MIOpen's Winograd solver does).  up = U = G g G^T
@@ -435,6 +447,22 @@ int sp_gemm_x6_layout_supported(int64_t n, int64_t hw, int32_t k, int32_t m);
 int sp_gemm_x6_layout(const float* x, const float* wp, const float* bias, const float* res, int64_t n,
                       int64_t hw, int32_t k, int32_t m, int32_t in_tm, int32_t out_tm, float* y,
                       sp_stream_t stream);
+
+/* Split-K forms of the three (same arguments, plus a workspace): a launch whose tiles fill
+ * less than half the CUs (batch 1, the 16² / 8² levels) runs 2-16 K parts that store their
+ * partial products to ws, then adds them in a fixed order with the bias and the residual
+ * (bitwise reproducible).  sp_gemm_x6_workspace(n, hw, k, m) = the bytes a launch over n
+ * images of hw pixels (sp_linear_x6: n = 1, hw = tokens), K = k, M = m needs; 0 = not split
+ * (ws may be NULL; a NULL or short ws runs unsplit). */
+int64_t sp_gemm_x6_workspace(int64_t n, int64_t hw, int32_t k, int32_t m);
+int sp_gemm_x6_ws(const float* x1, int32_t c1, const float* x2, int32_t c2, const float* wp,
+                  const float* bias, const float* res, int64_t n, int64_t hw, float* y1, int32_t o1,
+                  float* y2, int32_t o2, float* ws, int64_t ws_bytes, sp_stream_t stream);
+int sp_linear_x6_ws(const float* x, const float* wp, const float* bias, const float* res, int64_t tokens,
+                    int32_t k, int32_t m, float* y, float* ws, int64_t ws_bytes, sp_stream_t stream);
+int sp_gemm_x6_layout_ws(const float* x, const float* wp, const float* bias, const float* res, int64_t n,
+                         int64_t hw, int32_t k, int32_t m, int32_t in_tm, int32_t out_tm, float* y, float* ws,
+                         int64_t ws_bytes, sp_stream_t stream);
 
 /* Fused self-attention softmax(q k^T * scale) v of the SD 1.5 eps-UNet's transformer blocks
  * (attn1 over the latent tokens; diffusers UNet2DConditionModel, stable_diffusion.py:306-313;

@@ -146,6 +146,12 @@ SIGNATURES = {
                                          ctypes.c_int32, ctypes.c_int32, _P, _P]),
     "sp_conv3x3_s2_bwd_input": (ctypes.c_int, [_P, _P, _I64, ctypes.c_int32, ctypes.c_int32,
                                                ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, _P, _P]),
+    "sp_conv3x3_s2_workspace": (_I64, [_I64, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
+                                       ctypes.c_int32]),
+    "sp_conv3x3_s2_fwd_ws": (ctypes.c_int, [_P, _P, _P, _I64, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
+                                            ctypes.c_int32, _P, _P, _I64, _P]),
+    "sp_conv3x3_s2_bwd_input_ws": (ctypes.c_int, [_P, _P, _I64, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
+                                                  ctypes.c_int32, ctypes.c_int32, _P, _P, _I64, _P]),
     "sp_wino3x3_supported": (ctypes.c_int, [ctypes.c_int32] * 4),
     "sp_gemm_x6_supported": (ctypes.c_int, [ctypes.c_int32, ctypes.c_int32, _I64]),
     "sp_gemm_x6_packed_size": (_I64, [ctypes.c_int32, ctypes.c_int32]),
@@ -157,6 +163,13 @@ SIGNATURES = {
     "sp_gemm_x6_layout_supported": (ctypes.c_int, [_I64, _I64, ctypes.c_int32, ctypes.c_int32]),
     "sp_gemm_x6_layout": (ctypes.c_int, [_P, _P, _P, _P, _I64, _I64, ctypes.c_int32, ctypes.c_int32,
                                          ctypes.c_int32, ctypes.c_int32, _P, _P]),
+    "sp_gemm_x6_workspace": (_I64, [_I64, _I64, ctypes.c_int32, ctypes.c_int32]),
+    "sp_gemm_x6_ws": (ctypes.c_int, [_P, ctypes.c_int32, _P, ctypes.c_int32, _P, _P, _P, _I64, _I64,
+                                     _P, ctypes.c_int32, _P, ctypes.c_int32, _P, _I64, _P]),
+    "sp_linear_x6_ws": (ctypes.c_int, [_P, _P, _P, _P, _I64, ctypes.c_int32, ctypes.c_int32, _P, _P, _I64,
+                                       _P]),
+    "sp_gemm_x6_layout_ws": (ctypes.c_int, [_P, _P, _P, _P, _I64, _I64, ctypes.c_int32, ctypes.c_int32,
+                                            ctypes.c_int32, ctypes.c_int32, _P, _P, _I64, _P]),
     "sp_layernorm_supported": (ctypes.c_int, [_I64, ctypes.c_int32]),
     "sp_layernorm_fwd": (ctypes.c_int, [_P, _P, _P, _I64, ctypes.c_int32, _F, _P, _P, _P, _P]),
     "sp_layernorm_bwd": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _I64, ctypes.c_int32, _P, _P]),
@@ -280,7 +293,14 @@ def ptr(t: torch.Tensor | None) -> int | None:
     return t.data_ptr()
 
 
+_raw_stream = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+
+
 def stream_of(t: torch.Tensor) -> int:
+    """The handle of torch's current stream on t's device (the raw accessor: no Stream object
+    per call, which at batch 1 is a measurable part of a launch's host cost)."""
+    if _raw_stream is not None:
+        return _raw_stream(t.get_device())
     return torch.cuda.current_stream(t.device).cuda_stream
 
 

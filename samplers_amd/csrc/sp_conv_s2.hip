@@ -103,11 +103,14 @@ __device__ __forceinline__ void s2_store(float* As, float* Ps, int tid, const S2
     }
 }
 
+// split-K (blockIdx.z = part kh of gridDim.z): the part runs input-channel chunks
+// kh cper .. + cper - 1 and stores its partial sums (no bias) to out + kh ws_stride;
+// k_s2_split_reduce adds the parts.  Unsplit: gridDim.z = 1, cper = all chunks.
 __global__ __launch_bounds__(kBlock, 2) void k_conv3x3_s2(const float* __restrict__ x,
                                                           const float* __restrict__ wp,
                                                           const float* __restrict__ bias,
                                                           float* __restrict__ out, int cin, int cout,
-                                                          int H, int W) {
+                                                          int H, int W, int cper, int64_t ws_stride) {
     __shared__ __attribute__((aligned(16))) float As[2][S2_K * S2_M];
     __shared__ __attribute__((aligned(16))) float Ps[2][S2_CI * S2_PATCH];
 
@@ -122,7 +125,9 @@ __global__ __launch_bounds__(kBlock, 2) void k_conv3x3_s2(const float* __restric
     const float* __restrict__ xn = x + (int64_t)n * cin * plane;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, hh = lane >> 5, l = lane & 31;
     const int m_w = (wv & 1) * 64, prow = (wv >> 1) * S2_NR;
-    const int nchunks = cin / S2_CI;
+    const int cbeg = blockIdx.z * cper, cend = cbeg + cper;
+    SP_DCHECK(cend <= cin / S2_CI);
+    out += blockIdx.z * ws_stride;
 
     S2Stage st;
     s2_f32x16 acc[2][S2_NR];
@@ -131,12 +136,12 @@ __global__ __launch_bounds__(kBlock, 2) void k_conv3x3_s2(const float* __restric
 #pragma unroll
         for (int b = 0; b < S2_NR; ++b) acc[a][b] = s2_f32x16{};
 
-    s2_load(wp, xn, 0, cout, co0, 2 * h0, 2 * w0, H, W, plane, tid, st);
+    s2_load(wp, xn, cbeg, cout, co0, 2 * h0, 2 * w0, H, W, plane, tid, st);
     s2_store(As[0], Ps[0], tid, st);
     __syncthreads();
-    for (int cc = 0; cc < nchunks; ++cc) {
-        const int buf = cc & 1;
-        if (cc + 1 < nchunks) s2_load(wp, xn, cc + 1, cout, co0, 2 * h0, 2 * w0, H, W, plane, tid, st);
+    for (int cc = cbeg; cc < cend; ++cc) {
+        const int buf = (cc - cbeg) & 1;
+        if (cc + 1 < cend) s2_load(wp, xn, cc + 1, cout, co0, 2 * h0, 2 * w0, H, W, plane, tid, st);
         const float* Ab = &As[buf][(S2_KH * hh) * S2_M + m_w + l];
         const float* Pb = &Ps[buf][(S2_CI / 2 * hh) * S2_PATCH + 2 * prow * S2_RS + l];
 #pragma unroll
@@ -153,7 +158,7 @@ __global__ __launch_bounds__(kBlock, 2) void k_conv3x3_s2(const float* __restric
                 acc[1][ni] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b[ni], acc[1][ni], 0, 0, 0);
             }
         }
-        if (cc + 1 < nchunks) s2_store(As[buf ^ 1], Ps[buf ^ 1], tid, st);
+        if (cc + 1 < cend) s2_store(As[buf ^ 1], Ps[buf ^ 1], tid, st);
         __syncthreads();
     }
 
@@ -227,10 +232,12 @@ __device__ __forceinline__ void s2b_store(float* As, float* Ps, int tid, const S
     }
 }
 
+// split-K as k_conv3x3_s2 (parts over the output-channel chunks; acc_in 0 for parts)
 __global__ __launch_bounds__(kBlock, 2) void k_conv3x3_s2_bwd(const float* __restrict__ dy,
                                                               const float* __restrict__ wp,
                                                               float* __restrict__ dx, int cin,
-                                                              int cout, int H, int W, int acc_in) {
+                                                              int cout, int H, int W, int acc_in,
+                                                              int cper, int64_t ws_stride) {
     __shared__ __attribute__((aligned(16))) float As[2][S2B_K * S2B_M];
     __shared__ float Ps[2][S2B_CO * S2B_PATCH];
 
@@ -245,19 +252,21 @@ __global__ __launch_bounds__(kBlock, 2) void k_conv3x3_s2_bwd(const float* __res
     const float* __restrict__ dyn = dy + (int64_t)n * cout * oplane;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, hh = lane >> 5, l = lane & 31;
     const int m_w = (wv & 1) * 64, rw = wv >> 1;
-    const int nchunks = cout / S2B_CO;
+    const int cbeg = blockIdx.z * cper, cend = cbeg + cper;
+    SP_DCHECK(cend <= cout / S2B_CO && (gridDim.z == 1 || !acc_in));
+    dx += blockIdx.z * ws_stride;
 
     S2BStage st;
     s2_f32x16 acc[4][2];  // [phase p * 2 + q][ci tile]
 #pragma unroll
     for (int a = 0; a < 4; ++a) acc[a][0] = s2_f32x16{}, acc[a][1] = s2_f32x16{};
 
-    s2b_load(wp, dyn, 0, cin, ci0, i0, j0, Ho, Wo, oplane, tid, st);
+    s2b_load(wp, dyn, cbeg, cin, ci0, i0, j0, Ho, Wo, oplane, tid, st);
     s2b_store(As[0], Ps[0], tid, st);
     __syncthreads();
-    for (int cc = 0; cc < nchunks; ++cc) {
-        const int buf = cc & 1;
-        if (cc + 1 < nchunks) s2b_load(wp, dyn, cc + 1, cin, ci0, i0, j0, Ho, Wo, oplane, tid, st);
+    for (int cc = cbeg; cc < cend; ++cc) {
+        const int buf = (cc - cbeg) & 1;
+        if (cc + 1 < cend) s2b_load(wp, dyn, cc + 1, cin, ci0, i0, j0, Ho, Wo, oplane, tid, st);
         // lane half h carries output channel co_l = kc + 2h
         const float* Ab = &As[buf][(2 * hh) * 9 * S2B_M + m_w + l];
         const float* Pb = &Ps[buf][(2 * hh) * S2B_PATCH + rw * S2B_PW + l];
@@ -281,7 +290,7 @@ __global__ __launch_bounds__(kBlock, 2) void k_conv3x3_s2_bwd(const float* __res
                             ap[mt * 32], bv[a >> 1][b >> 1], acc[ph][mt], 0, 0, 0);
                 }
         }
-        if (cc + 1 < nchunks) s2b_store(As[buf ^ 1], Ps[buf ^ 1], tid, st);
+        if (cc + 1 < cend) s2b_store(As[buf ^ 1], Ps[buf ^ 1], tid, st);
         __syncthreads();
     }
 
@@ -305,6 +314,22 @@ __global__ __launch_bounds__(kBlock, 2) void k_conv3x3_s2_bwd(const float* __res
     }
 }
 
+// Split-K reduce: out = (acc ? out : 0) + (((ws_0 + ws_1) + ws_2) + ...) + bias[c], four
+// elements per thread (plane % 4 == 0), the parts added in a fixed order (bitwise reproducible)
+__global__ __launch_bounds__(256) void k_s2_split_reduce(const float* __restrict__ ws, int ks, int64_t stride,
+                                                         int64_t total4, int64_t plane, int channels,
+                                                         const float* __restrict__ bias, int acc,
+                                                         float* __restrict__ out) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= total4) return;
+    const int64_t e = 4 * i;
+    s2_f32x4 v = *reinterpret_cast<const s2_f32x4*>(ws + e);
+    for (int p = 1; p < ks; ++p) v += *reinterpret_cast<const s2_f32x4*>(ws + p * stride + e);
+    if (bias) v += bias[(e / plane) % channels];
+    if (acc) v = *reinterpret_cast<const s2_f32x4*>(out + e) + v;
+    *reinterpret_cast<s2_f32x4*>(out + e) = v;
+}
+
 // Forward: wp[(cc*36 + ci_l*9 + a*3 + b)*cout + co] (sp_conv3x3_pack's layout); input VJP:
 // wp[(cc*36 + co_l*9 + a*3 + b)*cin + ci] (no flip: the phases index the taps directly).
 __global__ void k_conv3x3_s2_pack(const float* __restrict__ w, int cout, int cin, int vjp,
@@ -325,7 +350,44 @@ __global__ void k_conv3x3_s2_pack(const float* __restrict__ w, int cout, int cin
 
 using namespace sp;
 
+static int s2_cu_count() {
+    static int cached[64] = {};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+    if (!cached[dev]) {
+        int v = 0;
+        if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0)
+            v = 256;
+        cached[dev] = v;
+    }
+    return cached[dev];
+}
+
+// split-K parts for `blocks` workgroups over `nchunks` K chunks: doubled while the workgroups
+// still fit the CUs, up to 16 parts of >= 4 chunks (at batch 1 the 128² -> 64² and 64² -> 32²
+// downsamplers are 16 and 8 workgroups walking 32-64 chunks, 150-300 us unsplit)
+static int s2_ksplit(int64_t blocks, int nchunks) {
+    const int cus = s2_cu_count();
+    int ks = 1;
+    while (ks < 16 && blocks * ks * 2 <= cus && nchunks % (ks * 2) == 0 && nchunks / (ks * 2) >= 4) ks *= 2;
+    return ks;
+}
+
+static int s2_parts(int64_t n, int32_t cin, int32_t cout, int32_t height, int32_t width, int vjp) {
+    if (!vjp) return s2_ksplit(n * (height / 2 / S2_TPH) * (width / 2 / S2_TPW) * (cout / S2_M), cin / S2_CI);
+    return s2_ksplit(n * (height / 2 / S2B_TH) * (width / 2 / S2B_TW) * (cin / S2B_M), cout / S2B_CO);
+}
+
 extern "C" {
+
+int64_t sp_conv3x3_s2_workspace(int64_t n, int32_t cin, int32_t cout, int32_t height, int32_t width,
+                                int32_t input_vjp) {
+    if (n <= 0 || !sp_conv3x3_s2_supported(cin, cout, height, width, input_vjp)) return 0;
+    const int ks = s2_parts(n, cin, cout, height, width, input_vjp);
+    if (ks <= 1) return 0;
+    const int64_t outf = input_vjp ? n * cin * (int64_t)height * width : n * cout * (int64_t)(height / 2) * (width / 2);
+    return 4 * ks * outf;
+}
 
 int sp_conv3x3_s2_supported(int32_t cin, int32_t cout, int32_t height, int32_t width,
                             int32_t input_vjp) {
@@ -348,6 +410,12 @@ int sp_conv3x3_s2_pack(const float* w, int32_t cout, int32_t cin, int32_t input_
 
 int sp_conv3x3_s2_fwd(const float* x, const float* wp, const float* bias, int64_t n, int32_t cin,
                       int32_t cout, int32_t height, int32_t width, float* y, sp_stream_t stream) {
+    return sp_conv3x3_s2_fwd_ws(x, wp, bias, n, cin, cout, height, width, y, nullptr, 0, stream);
+}
+
+int sp_conv3x3_s2_fwd_ws(const float* x, const float* wp, const float* bias, int64_t n, int32_t cin,
+                         int32_t cout, int32_t height, int32_t width, float* y, float* ws, int64_t ws_bytes,
+                         sp_stream_t stream) {
     if (!sp_conv3x3_s2_supported(cin, cout, height, width, 0) || n < 0) return SP_EINVAL;
     if (n == 0) return SP_OK;
     if (!x || !wp || !y) return SP_EINVAL;
@@ -355,15 +423,28 @@ int sp_conv3x3_s2_fwd(const float* x, const float* wp, const float* bias, int64_
     if (tiles >= (int64_t(1) << 31) || (int64_t)cin * height * width >= (int64_t(1) << 31))
         return SP_EINVAL;
     const double flops = 18.0 * n * cin * cout * (height / 2) * (width / 2);
-    launch_w(TK_CONV3X3_FWD, flops, k_conv3x3_s2, dim3(static_cast<unsigned>(tiles), cout / S2_M),
-             dim3(kBlock), static_cast<hipStream_t>(stream), x, wp, bias, y, cin, cout, height,
-             width);
+    const int64_t need = sp_conv3x3_s2_workspace(n, cin, cout, height, width, 0);
+    const int ks = ws && need > 0 && ws_bytes >= need ? s2_parts(n, cin, cout, height, width, 0) : 1;
+    const int64_t outf = n * cout * (int64_t)(height / 2) * (width / 2);
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    launch_w(TK_CONV3X3_FWD, flops, k_conv3x3_s2, dim3(static_cast<unsigned>(tiles), cout / S2_M, ks),
+             dim3(kBlock), s, x, wp, ks > 1 ? nullptr : bias, ks > 1 ? ws : y, cin, cout, height, width,
+             cin / S2_CI / ks, outf);
+    if (ks > 1)
+        launch(0, k_s2_split_reduce, dim3(static_cast<unsigned>((outf / 4 + 255) / 256)), dim3(256), s, ws, ks,
+               outf, outf / 4, (int64_t)(height / 2) * (width / 2), cout, bias, 0, y);
     return check_launch("sp_conv3x3_s2_fwd");
 }
 
 int sp_conv3x3_s2_bwd_input(const float* dy, const float* wp_vjp, int64_t n, int32_t cin,
                             int32_t cout, int32_t height, int32_t width, int32_t accumulate,
                             float* dx, sp_stream_t stream) {
+    return sp_conv3x3_s2_bwd_input_ws(dy, wp_vjp, n, cin, cout, height, width, accumulate, dx, nullptr, 0, stream);
+}
+
+int sp_conv3x3_s2_bwd_input_ws(const float* dy, const float* wp_vjp, int64_t n, int32_t cin,
+                               int32_t cout, int32_t height, int32_t width, int32_t accumulate,
+                               float* dx, float* ws, int64_t ws_bytes, sp_stream_t stream) {
     if (!sp_conv3x3_s2_supported(cin, cout, height, width, 1) || n < 0) return SP_EINVAL;
     if (n == 0) return SP_OK;
     if (!dy || !wp_vjp || !dx) return SP_EINVAL;
@@ -371,10 +452,17 @@ int sp_conv3x3_s2_bwd_input(const float* dy, const float* wp_vjp, int64_t n, int
     if (tiles >= (int64_t(1) << 31) || (int64_t)cin * height * width >= (int64_t(1) << 31))
         return SP_EINVAL;
     const double flops = 18.0 * n * cin * cout * (height / 2) * (width / 2);
+    const int64_t need = sp_conv3x3_s2_workspace(n, cin, cout, height, width, 1);
+    const int ks = ws && need > 0 && ws_bytes >= need ? s2_parts(n, cin, cout, height, width, 1) : 1;
+    const int64_t outf = n * cin * (int64_t)height * width;
+    hipStream_t s = static_cast<hipStream_t>(stream);
     launch_w(TK_CONV3X3_BWD_INPUT, flops, k_conv3x3_s2_bwd,
-             dim3(static_cast<unsigned>(tiles), cin / S2B_M), dim3(kBlock),
-             static_cast<hipStream_t>(stream), dy, wp_vjp, dx, cin, cout, height, width,
-             accumulate ? 1 : 0);
+             dim3(static_cast<unsigned>(tiles), cin / S2B_M, ks), dim3(kBlock), s, dy, wp_vjp,
+             ks > 1 ? ws : dx, cin, cout, height, width, ks > 1 ? 0 : (accumulate ? 1 : 0), cout / S2B_CO / ks,
+             outf);
+    if (ks > 1)
+        launch(0, k_s2_split_reduce, dim3(static_cast<unsigned>((outf / 4 + 255) / 256)), dim3(256), s, ws, ks,
+               outf, outf / 4, (int64_t)height * width, cin, nullptr, accumulate ? 1 : 0, dx);
     return check_launch("sp_conv3x3_s2_bwd_input");
 }
 

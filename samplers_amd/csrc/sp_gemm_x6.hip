@@ -30,6 +30,7 @@ namespace sp {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned uvec4 __attribute__((ext_vector_type(4)));
 typedef unsigned uvec2 __attribute__((ext_vector_type(2)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
@@ -58,8 +59,14 @@ struct G6Geom {
     const float* bias;    // nullable, per output channel (o1 + o2)
     const float* res;     // nullable, shaped like y1 (o2 == 0 only)
     int c1, c2, o1, o2, hw;
-    int ntiles, cob, ptiles, nsteps;
+    int ntiles, cob, ptiles, nsteps;  // ntiles: work items = output tiles x ksplit
     int tokens;           // token-major operands: rows of x1 / y1 (images x hw)
+    // split-K (under-filled launches): item (tile, kh) runs k-steps kh kper .. + kper - 1 and
+    // stores its partial product (no bias, no residual) to ws + kh ws_stride, laid out as a
+    // single output of o1 + o2 channels; k_g6_split_reduce adds the parts.  ksplit 1: ws NULL.
+    int ksplit, kper;
+    float* ws;
+    int64_t ws_stride;
     // token-major operands (k_gemm_x6<LTM, STM>, nn.Linear on [tokens][features]): x1 is
     // [tokens][c1] and / or y1 [tokens][o1] with o1 % 32 (W's rows padded to 128 with zeros),
     // one input and output
@@ -188,16 +195,19 @@ __device__ __forceinline__ void g6_raw_x_tm(const unsigned char* raw, int pq, in
     }
 }
 
-struct G6Pos { int n, p0, cb; };
+struct G6Pos { int n, p0, cb, kh; };
 __device__ __forceinline__ G6Pos g6_pos(const G6Geom& g, int t) {
     // XCD-aware: the output-channel blocks of one pixel tile on one XCD (shared X lines)
-    const int lb = (g.ntiles & 7) ? t : (t & 7) * (g.ntiles >> 3) + (t >> 3);
+    const int lb0 = (g.ntiles & 7) ? t : (t & 7) * (g.ntiles >> 3) + (t >> 3);
+    const int kh = lb0 % g.ksplit, lb = lb0 / g.ksplit;
     const int cb = lb % g.cob, rest = lb / g.cob;
     const int n = rest / g.ptiles;
-    // the tile inside the grid's work, its pixels inside the plane (or the token rows)
-    SP_DCHECK(t >= 0 && t < g.ntiles && lb < g.ntiles && cb * G6_CO < g.o1 + g.o2 + G6_CO &&
-              (rest - n * g.ptiles + 1) * G6_PX <= (g.tokens ? g.tokens : g.hw));
-    return G6Pos{n, (rest - n * g.ptiles) * G6_PX, cb};
+    // the item inside the grid's work, its pixels inside the plane (or the token rows), its
+    // k-steps inside K
+    SP_DCHECK(t >= 0 && t < g.ntiles && lb0 < g.ntiles && cb * G6_CO < g.o1 + g.o2 + G6_CO &&
+              (rest - n * g.ptiles + 1) * G6_PX <= (g.tokens ? g.tokens : g.hw) &&
+              (kh + 1) * g.kper <= g.nsteps);
+    return G6Pos{n, (rest - n * g.ptiles) * G6_PX, cb, kh};
 }
 
 // epilogue: register q of tile (a, b) = channel 32 (2 ch + a) + (q&3) + 8(q>>2) + 4(lane>>5),
@@ -355,7 +365,7 @@ __device__ __forceinline__ void g6_body(const G6Geom& g, G6XSlot* xraw, G6WSlot*
     const unsigned wl_lds = static_cast<unsigned>(reinterpret_cast<size_t>((lds_void_g*)&wl[0][0]));
     const int G = gridDim.x, b0 = blockIdx.x;
     const int ntile_wg = (g.ntiles - b0 + G - 1) / G;
-    const int J = ntile_wg * g.nsteps;
+    const int J = ntile_wg * g.kper;
     // two load streams, advanced one k-step at a time (divisions once per tile)
     struct Cursor { int j, tw, s, slot; G6Pos ps; };
     Cursor cx{0, 0, 0, 0, g6_pos(g, b0)}, cw = cx;
@@ -365,7 +375,7 @@ __device__ __forceinline__ void g6_body(const G6Geom& g, G6XSlot* xraw, G6WSlot*
     auto advance = [&](Cursor& c, int nslots) {
         ++c.j;
         c.slot = c.slot + 1 == nslots ? 0 : c.slot + 1;
-        if (++c.s == g.nsteps) {
+        if (++c.s == g.kper) {
             c.s = 0;
             if (++c.tw < ntile_wg) c.ps = g6_pos(g, b0 + c.tw * G);
             return true;
@@ -375,8 +385,9 @@ __device__ __forceinline__ void g6_body(const G6Geom& g, G6XSlot* xraw, G6WSlot*
     auto dma_x = [&]() {
         if (cx.j < J) {
             const unsigned sl = xraw_lds + cx.slot * (G6_KC * G6_PX * 4);
-            if constexpr (LTM) g6_dma_x_tm(g, cx.ps.n * g.hw + cx.ps.p0, cx.s, wv, lane, sl);
-            else g6_dma_x(g, xb1, xb2, cx.ps.p0, cx.s, wv, lane, sl);
+            const int ks = cx.ps.kh * g.kper + cx.s;  // the k-step inside K
+            if constexpr (LTM) g6_dma_x_tm(g, cx.ps.n * g.hw + cx.ps.p0, ks, wv, lane, sl);
+            else g6_dma_x(g, xb1, xb2, cx.ps.p0, ks, wv, lane, sl);
         }
         if (advance(cx, G6_NX) && !LTM) {
             xb1 = g.x1 + (int64_t)cx.ps.n * g.c1 * g.hw;
@@ -384,7 +395,8 @@ __device__ __forceinline__ void g6_body(const G6Geom& g, G6XSlot* xraw, G6WSlot*
         }
     };
     auto dma_w = [&]() {
-        if (cw.j < J) g6_dma_w(wrs, cw.ps.cb * g.nsteps + cw.s, wv, lane, wl_lds + cw.slot * G6_WB);
+        if (cw.j < J)
+            g6_dma_w(wrs, cw.ps.cb * g.nsteps + cw.ps.kh * g.kper + cw.s, wv, lane, wl_lds + cw.slot * G6_WB);
         advance(cw, G6_NW);
     };
     // prologue: W 0 .. 2 and X 0 .. 4 in flight, then all landed
@@ -505,11 +517,11 @@ __device__ __forceinline__ void g6_body(const G6Geom& g, G6XSlot* xraw, G6WSlot*
 #pragma unroll
             for (int b = 0; b < 2; ++b) acc[a][b] = f32x16{}, acs[a][b] = f32x16{};
         s = 0;
-        while (s + 1 < g.nsteps) {
+        while (s + 1 < g.kper) {
             kstep(fuA, xrA, fuB, xrB);
             kstep(fuB, xrB, fuA, xrA);
         }
-        if (s < g.nsteps) {  // odd step count: one more, and set A back to the current step
+        if (s < g.kper) {  // odd step count: one more, and set A back to the current step
             kstep(fuA, xrA, fuB, xrB);
 #pragma unroll
             for (int a = 0; a < 2; ++a)
@@ -521,10 +533,20 @@ __device__ __forceinline__ void g6_body(const G6Geom& g, G6XSlot* xraw, G6WSlot*
                 for (int i = 0; i < 8; ++i) xrA[b][i] = xrB[b][i];
         }
         const G6Pos ps = g6_pos(g, b0 + tw * G);
+        // split-K: the part goes to its workspace slice as a single output of all m channels
+        G6Geom ge = g;
+        if (g.ksplit > 1) {
+            ge.y1 = g.ws + ps.kh * g.ws_stride;
+            ge.y2 = nullptr;
+            ge.o1 = g.o1 + g.o2;
+            ge.o2 = 0;
+            ge.bias = nullptr;
+            ge.res = nullptr;
+        }
         // tiles hold the pixels of parity b (NCHW X: one ds_read_b64 per channel) or 32 b .. (token
         // X: fewer LDS bank conflicts)
-        if constexpr (STM) nst = g6_epilogue_tm<!LTM>(g, ps, ch, pq, lane, acc, acs);
-        else nst = g6_epilogue<!LTM>(g, ps.n, ps.cb, ps.p0 + pq * 64, ch, lane, acc, acs);
+        if constexpr (STM) nst = g6_epilogue_tm<!LTM>(ge, ps, ch, pq, lane, acc, acs);
+        else nst = g6_epilogue<!LTM>(ge, ps.n, ps.cb, ps.p0 + pq * 64, ch, lane, acc, acs);
         if (nst > 32) nst = 32;  // 64 stores: credit 32 of them (a lower bound is safe)
     }
 }
@@ -564,10 +586,98 @@ __global__ void k_gemm_x6_pack(const float* __restrict__ w, int m, int k, int tr
     g6_pack_store(wp, v, row, col, k);
 }
 
+// Split-K reduce: y = (((ws_0 + ws_1) + ws_2) + ...) + bias[c] (+ res), four elements per
+// thread, the parts added in a fixed order (bitwise reproducible).  ws slices are laid out as
+// one output of m channels: [n][m][hw] (stm = 0; channels < o1 go to y1 [n][o1][hw], the rest
+// to y2 [n][o2][hw]) or [tokens][m] (stm = 1, y1 only); res is shaped like y1 (o2 == 0 only).
+__global__ __launch_bounds__(256) void k_g6_split_reduce(const float* __restrict__ ws, int ks, int64_t stride,
+                                                         int64_t total4, int m, int hw, int stm, int o1, int o2,
+                                                         const float* __restrict__ bias,
+                                                         const float* __restrict__ res, float* __restrict__ y1,
+                                                         float* __restrict__ y2) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= total4) return;
+    const int64_t e = 4 * i;
+    f32x4 acc = *reinterpret_cast<const f32x4*>(ws + e);
+    for (int p = 1; p < ks; ++p) acc += *reinterpret_cast<const f32x4*>(ws + p * stride + e);
+    if (stm) {
+        const int c = static_cast<int>(e % m);  // four consecutive channels (m % 4 == 0)
+        if (bias) acc += f32x4{bias[c], bias[c + 1], bias[c + 2], bias[c + 3]};
+        if (res) acc += *reinterpret_cast<const f32x4*>(res + e);
+        *reinterpret_cast<f32x4*>(y1 + e) = acc;
+        return;
+    }
+    const int64_t img = e / ((int64_t)m * hw);
+    const int64_t rem = e - img * m * hw;
+    const int c = static_cast<int>(rem / hw), p = static_cast<int>(rem - (int64_t)c * hw);
+    if (bias) acc += bias[c];
+    if (c < o1) {
+        const int64_t o = (img * o1 + c) * hw + p;
+        SP_DCHECK(o + 4 <= total4 * 4);
+        if (res) acc += *reinterpret_cast<const f32x4*>(res + o);
+        *reinterpret_cast<f32x4*>(y1 + o) = acc;
+    } else {
+        *reinterpret_cast<f32x4*>(y2 + (img * o2 + (c - o1)) * hw + p) = acc;
+    }
+}
+
 
 }  // namespace sp
 
 using namespace sp;
+
+
+static int g6_cu_count() {
+    static int cached[64] = {};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+    if (!cached[dev]) {
+        int v = 0;
+        if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0)
+            v = 256;
+        cached[dev] = v;
+    }
+    return cached[dev];
+}
+
+// Split-K parts for a launch of `tiles` output tiles over `nsteps` k-steps: doubled while the
+// items still fit half the CUs, up to 16 parts of >= 2 k-steps (a launch that fills the chip
+// is not split).  At batch 1 the 16² / 8² levels' projections are 1-16 tiles with 16-32
+// k-steps, one k-step chain per CU (40-80 us) without it.
+static int g6_ksplit(int64_t tiles, int nsteps) {
+    const int cus = g6_cu_count();
+    int ks = 1;
+    while (ks < 16 && tiles * ks * 2 <= cus && nsteps % (ks * 2) == 0 && nsteps / (ks * 2) >= 2) ks *= 2;
+    return ks;
+}
+
+// split-K workspace: ks slices of n * hw * m floats (0: the launch is not split)
+static int64_t g6_ws_floats(int64_t tiles, int nsteps, int64_t n, int64_t hw, int m) {
+    const int ks = g6_ksplit(tiles, nsteps);
+    return ks > 1 ? (int64_t)ks * n * hw * m : 0;
+}
+
+// launch k_gemm_x6<LTM, STM> over g (tiles = output tiles), split when ws allows it, then the
+// reduce into y1 / y2 with g's bias and residual
+template <bool LTM, bool STM>
+static int g6_launch(G6Geom g, int64_t tiles, int64_t n, float* ws, int64_t ws_bytes, hipStream_t s) {
+    const int m = g.o1 + g.o2;
+    const int64_t need = g6_ws_floats(tiles, g.nsteps, n, g.hw, m);
+    const int ks = ws && need > 0 && ws_bytes >= need * 4 ? g6_ksplit(tiles, g.nsteps) : 1;
+    g.ksplit = ks;
+    g.kper = g.nsteps / ks;
+    g.ws = ks > 1 ? ws : nullptr;
+    g.ws_stride = n * g.hw * m;
+    g.ntiles = static_cast<int>(tiles * ks);
+    const int grid = static_cast<int>(std::min<int64_t>(g.ntiles, g6_cu_count()));
+    launch(0, k_gemm_x6<LTM, STM>, dim3(grid), dim3(G6_THREADS), s, g);
+    if (ks > 1) {
+        const int64_t total4 = n * g.hw * m / 4;
+        launch(0, k_g6_split_reduce, dim3(static_cast<unsigned>((total4 + 255) / 256)), dim3(256), s, ws, ks,
+               g.ws_stride, total4, m, g.hw, STM ? 1 : 0, g.o1, g.o2, g.bias, g.res, g.y1, g.y2);
+    }
+    return SP_OK;
+}
 
 extern "C" {
 
@@ -588,22 +698,21 @@ int sp_gemm_x6_pack(const float* w, int32_t m, int32_t k, int32_t trans, float* 
     return check_launch("sp_gemm_x6_pack");
 }
 
-static int g6_cu_count() {
-    static int cached[64] = {};
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
-    if (!cached[dev]) {
-        int v = 0;
-        if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0)
-            v = 256;
-        cached[dev] = v;
-    }
-    return cached[dev];
+int64_t sp_gemm_x6_workspace(int64_t n, int64_t hw, int32_t k, int32_t m) {
+    if (n <= 0 || hw < G6_PX || hw % G6_PX || k < G6_KC || k % G6_KC || m < 32 || m % 32) return 0;
+    const int64_t tiles = n * (hw / G6_PX) * ((m + G6_CO - 1) / G6_CO);
+    return 4 * g6_ws_floats(tiles, k / G6_KC, n, hw, m);
 }
 
 int sp_gemm_x6(const float* x1, int32_t c1, const float* x2, int32_t c2, const float* wp,
                const float* bias, const float* res, int64_t n, int64_t hw, float* y1, int32_t o1,
                float* y2, int32_t o2, sp_stream_t stream) {
+    return sp_gemm_x6_ws(x1, c1, x2, c2, wp, bias, res, n, hw, y1, o1, y2, o2, nullptr, 0, stream);
+}
+
+int sp_gemm_x6_ws(const float* x1, int32_t c1, const float* x2, int32_t c2, const float* wp,
+                  const float* bias, const float* res, int64_t n, int64_t hw, float* y1, int32_t o1,
+                  float* y2, int32_t o2, float* ws, int64_t ws_bytes, sp_stream_t stream) {
     const int k = c1 + c2, m = o1 + o2;
     if (!sp_gemm_x6_supported(m, k, hw) || n < 0 || c1 <= 0 || o1 <= 0 || c2 < 0 || o2 < 0)
         return SP_EINVAL;
@@ -613,7 +722,7 @@ int sp_gemm_x6(const float* x1, int32_t c1, const float* x2, int32_t c2, const f
     if (!x1 || !wp || !y1) return SP_EINVAL;
     const int64_t tiles = n * (hw / G6_PX) * (m / G6_CO);
     if (tiles >= (int64_t(1) << 31)) return SP_EINVAL;
-    G6Geom g;
+    G6Geom g = {};
     g.x1 = x1;
     g.x2 = x2;
     g.wp = reinterpret_cast<const unsigned short*>(wp);
@@ -630,9 +739,8 @@ int sp_gemm_x6(const float* x1, int32_t c1, const float* x2, int32_t c2, const f
     g.cob = m / G6_CO;
     g.ptiles = static_cast<int>(hw / G6_PX);
     g.nsteps = k / G6_KC;
-    const int grid = static_cast<int>(std::min<int64_t>(tiles, g6_cu_count()));
     g.tokens = 0;
-    launch(0, k_gemm_x6<false, false>, dim3(grid), dim3(G6_THREADS), static_cast<hipStream_t>(stream), g);
+    g6_launch<false, false>(g, tiles, n, ws, ws_bytes, static_cast<hipStream_t>(stream));
     return check_launch("sp_gemm_x6");
 }
 
@@ -645,6 +753,11 @@ int sp_linear_x6_supported(int64_t tokens, int32_t k, int32_t m) {
 // W packed by sp_gemm_x6_pack(w, m, k, 0) (or trans = 1 from W^T for the input VJP).
 int sp_linear_x6(const float* x, const float* wp, const float* bias, const float* res, int64_t tokens,
                  int32_t k, int32_t m, float* y, sp_stream_t stream) {
+    return sp_linear_x6_ws(x, wp, bias, res, tokens, k, m, y, nullptr, 0, stream);
+}
+
+int sp_linear_x6_ws(const float* x, const float* wp, const float* bias, const float* res, int64_t tokens,
+                    int32_t k, int32_t m, float* y, float* ws, int64_t ws_bytes, sp_stream_t stream) {
     if (!sp_linear_x6_supported(tokens, k, m)) return SP_EINVAL;
     if (!x || !wp || !y || (res && res == y)) return SP_EINVAL;
     const int cob = (m + G6_CO - 1) / G6_CO;
@@ -663,8 +776,7 @@ int sp_linear_x6(const float* x, const float* wp, const float* bias, const float
     g.ptiles = static_cast<int>(tokens / G6_PX);  // one "image" of all tokens
     g.nsteps = k / G6_KC;
     g.tokens = static_cast<int>(tokens);
-    const int grid = static_cast<int>(std::min<int64_t>(tiles, g6_cu_count()));
-    launch(0, k_gemm_x6<true, true>, dim3(grid), dim3(G6_THREADS), static_cast<hipStream_t>(stream), g);
+    g6_launch<true, true>(g, tiles, 1, ws, ws_bytes, static_cast<hipStream_t>(stream));
     return check_launch("sp_linear_x6");
 }
 
@@ -679,6 +791,12 @@ int sp_gemm_x6_layout_supported(int64_t n, int64_t hw, int32_t k, int32_t m) {
 int sp_gemm_x6_layout(const float* x, const float* wp, const float* bias, const float* res, int64_t n,
                       int64_t hw, int32_t k, int32_t m, int32_t in_tm, int32_t out_tm, float* y,
                       sp_stream_t stream) {
+    return sp_gemm_x6_layout_ws(x, wp, bias, res, n, hw, k, m, in_tm, out_tm, y, nullptr, 0, stream);
+}
+
+int sp_gemm_x6_layout_ws(const float* x, const float* wp, const float* bias, const float* res, int64_t n,
+                         int64_t hw, int32_t k, int32_t m, int32_t in_tm, int32_t out_tm, float* y, float* ws,
+                         int64_t ws_bytes, sp_stream_t stream) {
     if (!sp_gemm_x6_layout_supported(n, hw, k, m)) return SP_EINVAL;
     if (n == 0) return SP_OK;
     if (!x || !wp || !y || (res && res == y) || x == y) return SP_EINVAL;
@@ -693,17 +811,15 @@ int sp_gemm_x6_layout(const float* x, const float* wp, const float* bias, const 
     g.o1 = m;
     g.hw = static_cast<int>(hw);
     g.ptiles = static_cast<int>(hw / G6_PX);
-    g.ntiles = static_cast<int>(n * g.ptiles * cob);
+    const int64_t tiles = n * g.ptiles * cob;
     g.cob = cob;
     g.nsteps = k / G6_KC;
     g.tokens = static_cast<int>(n * hw);
-    const int grid = static_cast<int>(std::min<int64_t>(g.ntiles, g6_cu_count()));
-    const dim3 gd(grid), bd(G6_THREADS);
     hipStream_t s = static_cast<hipStream_t>(stream);
-    if (in_tm && out_tm) launch(0, k_gemm_x6<true, true>, gd, bd, s, g);
-    else if (in_tm) launch(0, k_gemm_x6<true, false>, gd, bd, s, g);
-    else if (out_tm) launch(0, k_gemm_x6<false, true>, gd, bd, s, g);
-    else launch(0, k_gemm_x6<false, false>, gd, bd, s, g);
+    if (in_tm && out_tm) g6_launch<true, true>(g, tiles, n, ws, ws_bytes, s);
+    else if (in_tm) g6_launch<true, false>(g, tiles, n, ws, ws_bytes, s);
+    else if (out_tm) g6_launch<false, true>(g, tiles, n, ws, ws_bytes, s);
+    else g6_launch<false, false>(g, tiles, n, ws, ws_bytes, s);
     return check_launch("sp_gemm_x6_layout");
 }
 

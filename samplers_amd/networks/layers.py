@@ -248,6 +248,17 @@ def _wino_workspace(lib, n: int, cin: int, cout: int, h: int, w: int, device) ->
     return torch.empty(nb // 4, device=device, dtype=torch.float32)
 
 
+def x6_workspace(lib, n: int, hw: int, k: int, m: int, device) -> tuple[Tensor | None, int]:
+    """The bf16x6 GEMM's split-K workspace for an under-filled launch (sp_gemm_x6_workspace;
+    n images of hw pixels, or n = 1 and hw = tokens), and its size in bytes; (None, 0) when the
+    launch fills the chip unsplit.  Torch's caching allocator on the launch stream, as
+    _wino_workspace; the caller holds it until the launch is queued."""
+    nb = int(lib.sp_gemm_x6_workspace(n, hw, k, m))
+    if nb <= 0:
+        return None, 0
+    return torch.empty(nb // 4, device=device, dtype=torch.float32), nb
+
+
 def conv3x3_input_vjp(module: "Conv3x3", dy: Tensor, x_shape) -> Tensor:
     """d conv(x) / dx applied to dy (weights frozen)."""
     lib = _hip.load_library()
@@ -435,6 +446,15 @@ class SkipGrad:
         return g
 
 
+def _s2_workspace(lib, n: int, cin: int, cout: int, h: int, w: int, vjp: int, device) -> tuple[Tensor | None, int]:
+    """The stride-2 tile's split-K workspace for an under-filled launch (sp_conv3x3_s2_workspace)
+    and its bytes, or (None, 0); allocated as _wino_workspace."""
+    nb = int(lib.sp_conv3x3_s2_workspace(n, cin, cout, h, w, vjp))
+    if nb <= 0:
+        return None, 0
+    return torch.empty(nb // 4, device=device, dtype=torch.float32), nb
+
+
 class _ConvS2Fn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, module, box=None):
@@ -443,9 +463,10 @@ class _ConvS2Fn(torch.autograd.Function):
         n, cin, h, w = x.shape
         cout = module.out_channels
         y = torch.empty(n, cout, h // 2, w // 2, device=x.device, dtype=torch.float32)
-        _hip.check(lib.sp_conv3x3_s2_fwd(_hip.ptr(x), _hip.ptr(_s2_packed(module, False)),
-                                         _hip.ptr(bias.contiguous()) if bias is not None else None,
-                                         n, cin, cout, h, w, _hip.ptr(y), _hip.stream_of(x)),
+        ws, nb = _s2_workspace(lib, n, cin, cout, h, w, 0, x.device)
+        _hip.check(lib.sp_conv3x3_s2_fwd_ws(_hip.ptr(x), _hip.ptr(_s2_packed(module, False)),
+                                            _hip.ptr(bias.contiguous()) if bias is not None else None,
+                                            n, cin, cout, h, w, _hip.ptr(y), _hip.ptr(ws), nb, _hip.stream_of(x)),
                    "sp_conv3x3_s2_fwd")
         ctx.module = module
         ctx.box = box
@@ -464,10 +485,11 @@ class _ConvS2Fn(torch.autograd.Function):
             acc = dx is not None
             if dx is None:
                 dx = torch.empty(tuple(ctx.x_shape), device=dy.device, dtype=torch.float32)
-            _hip.check(lib.sp_conv3x3_s2_bwd_input(_hip.ptr(dy.contiguous()),
-                                                   _hip.ptr(_s2_packed(ctx.module, True)),
-                                                   n, cin, ctx.module.out_channels, h, w, int(acc),
-                                                   _hip.ptr(dx), _hip.stream_of(dy)),
+            ws, nb = _s2_workspace(lib, n, cin, ctx.module.out_channels, h, w, 1, dy.device)
+            _hip.check(lib.sp_conv3x3_s2_bwd_input_ws(_hip.ptr(dy.contiguous()),
+                                                      _hip.ptr(_s2_packed(ctx.module, True)),
+                                                      n, cin, ctx.module.out_channels, h, w, int(acc),
+                                                      _hip.ptr(dx), _hip.ptr(ws), nb, _hip.stream_of(dy)),
                        "sp_conv3x3_s2_bwd_input")
         return dx, None, None, None, None
 
@@ -592,9 +614,11 @@ class _LinearX6Fn(torch.autograd.Function):
         t = x2.shape[0]
         y = torch.empty(t, m, device=x.device, dtype=torch.float32)
         r2 = None if res is None else res.reshape(t, m).contiguous()
-        _hip.check(lib.sp_linear_x6(_hip.ptr(x2), _hip.ptr(_linear_pack(module, w2d, False)),
-                                    _hip.ptr(None if bias is None else bias.detach().contiguous()),
-                                    _hip.ptr(r2), t, k, m, _hip.ptr(y), _hip.stream_of(x2)), "sp_linear_x6")
+        ws, nb = x6_workspace(lib, 1, t, k, m, x.device)
+        _hip.check(lib.sp_linear_x6_ws(_hip.ptr(x2), _hip.ptr(_linear_pack(module, w2d, False)),
+                                       _hip.ptr(None if bias is None else bias.detach().contiguous()),
+                                       _hip.ptr(r2), t, k, m, _hip.ptr(y), _hip.ptr(ws), nb, _hip.stream_of(x2)),
+                   "sp_linear_x6")
         ctx.module, ctx.w2d, ctx.shape = module, w2d, x.shape
         ctx.box = box if res is not None else None
         return y.reshape(*x.shape[:-1], m)
@@ -608,8 +632,9 @@ class _LinearX6Fn(torch.autograd.Function):
         d2 = dy.reshape(-1, m).contiguous()
         t = d2.shape[0]
         dx = torch.empty(t, k, device=dy.device, dtype=torch.float32)
-        _hip.check(lib.sp_linear_x6(_hip.ptr(d2), _hip.ptr(_linear_pack(ctx.module, ctx.w2d, True)), None, None,
-                                    t, m, k, _hip.ptr(dx), _hip.stream_of(d2)), "sp_linear_x6")
+        ws, nb = x6_workspace(lib, 1, t, m, k, dy.device)
+        _hip.check(lib.sp_linear_x6_ws(_hip.ptr(d2), _hip.ptr(_linear_pack(ctx.module, ctx.w2d, True)), None, None,
+                                       t, m, k, _hip.ptr(dx), _hip.ptr(ws), nb, _hip.stream_of(d2)), "sp_linear_x6")
         dres = None
         if ctx.needs_input_grad[5]:
             if ctx.box is not None and ctx.box.enabled:
@@ -652,10 +677,11 @@ class _ProjLayoutFn(torch.autograd.Function):
         xc = x.contiguous()
         y = torch.empty((n * hw, m) if out_tm else (n, m, hw), device=x.device, dtype=torch.float32)
         rc = None if res is None else res.contiguous()
-        _hip.check(lib.sp_gemm_x6_layout(_hip.ptr(xc), _hip.ptr(_linear_pack(module, w2d, False)),
-                                         _hip.ptr(None if bias is None else bias.detach().contiguous()),
-                                         _hip.ptr(rc), n, hw, k, m, int(in_tm), int(out_tm), _hip.ptr(y),
-                                         _hip.stream_of(xc)), "sp_gemm_x6_layout")
+        ws, nb = x6_workspace(lib, n, hw, k, m, x.device)
+        _hip.check(lib.sp_gemm_x6_layout_ws(_hip.ptr(xc), _hip.ptr(_linear_pack(module, w2d, False)),
+                                            _hip.ptr(None if bias is None else bias.detach().contiguous()),
+                                            _hip.ptr(rc), n, hw, k, m, int(in_tm), int(out_tm), _hip.ptr(y),
+                                            _hip.ptr(ws), nb, _hip.stream_of(xc)), "sp_gemm_x6_layout")
         ctx.module, ctx.w2d, ctx.geo, ctx.shape = module, w2d, (n, hw, in_tm, out_tm), x.shape
         ctx.res_shape = None if res is None else res.shape
         ctx.box = box if res is not None else None
@@ -668,9 +694,10 @@ class _ProjLayoutFn(torch.autograd.Function):
         n, hw, in_tm, out_tm = ctx.geo
         dc = dy.contiguous()
         dx = torch.empty((n * hw, k) if in_tm else (n, k, hw), device=dy.device, dtype=torch.float32)
-        _hip.check(lib.sp_gemm_x6_layout(_hip.ptr(dc), _hip.ptr(_linear_pack(ctx.module, ctx.w2d, True)),
-                                         None, None, n, hw, m, k, int(out_tm), int(in_tm), _hip.ptr(dx),
-                                         _hip.stream_of(dc)), "sp_gemm_x6_layout")
+        ws, nb = x6_workspace(lib, n, hw, m, k, dy.device)
+        _hip.check(lib.sp_gemm_x6_layout_ws(_hip.ptr(dc), _hip.ptr(_linear_pack(ctx.module, ctx.w2d, True)),
+                                            None, None, n, hw, m, k, int(out_tm), int(in_tm), _hip.ptr(dx),
+                                            _hip.ptr(ws), nb, _hip.stream_of(dc)), "sp_gemm_x6_layout")
         dres = None
         if ctx.res_shape is not None and ctx.needs_input_grad[9]:
             if ctx.box is not None and ctx.box.enabled:

@@ -31,7 +31,7 @@ from torch import Tensor, nn
 from .. import _hip
 from .layers import (Conv3x3, GroupNormAct, Linear, SkipGrad, conv3x3_forward, conv3x3_input_vjp,
                      downsample_conv, gn_backward, gn_forward, miopen_fallback, proj_nchw_to_tokens,
-                     proj_tokens_to_nchw, upsample_nearest2x, x6_enough_tiles)
+                     proj_tokens_to_nchw, upsample_nearest2x, x6_enough_tiles, x6_workspace)
 
 
 @dataclass(frozen=True)
@@ -158,9 +158,10 @@ def _shortcut_forward(conv: nn.Conv2d, x1: Tensor, x2: Tensor | None) -> Tensor:
         x1 = x1.contiguous()
         x2 = None if x2 is None else x2.contiguous()
         y = torch.empty((n, cout) + tuple(x1.shape[2:]), device=x1.device, dtype=torch.float32)
-        _hip.check(lib.sp_gemm_x6(_hip.ptr(x1), c1, _hip.ptr(x2), c2, _hip.ptr(_pointwise_pack(conv, False)),
-                                  None, None, n, hw, _hip.ptr(y), cout, None, 0, _hip.stream_of(x1)),
-                   "sp_gemm_x6")
+        ws, nb = x6_workspace(lib, n, hw, c1 + c2, cout, x1.device)
+        _hip.check(lib.sp_gemm_x6_ws(_hip.ptr(x1), c1, _hip.ptr(x2), c2, _hip.ptr(_pointwise_pack(conv, False)),
+                                     None, None, n, hw, _hip.ptr(y), cout, None, 0, _hip.ptr(ws), nb,
+                                     _hip.stream_of(x1)), "sp_gemm_x6")
         return y
     w = conv.weight[:, :, 0, 0]
     y = torch.matmul(w[:, :c1], x1.reshape(n, c1, -1))
@@ -180,14 +181,32 @@ def _shortcut_input_vjp(conv: nn.Conv2d, dy: Tensor, c1: int, c2: int) -> tuple[
         dy = dy.contiguous()
         d1 = torch.empty((n, c1) + tuple(dy.shape[2:]), device=dy.device, dtype=torch.float32)
         d2 = torch.empty((n, c2) + tuple(dy.shape[2:]), device=dy.device, dtype=torch.float32) if c2 else None
-        _hip.check(lib.sp_gemm_x6(_hip.ptr(dy), cout, None, 0, _hip.ptr(_pointwise_pack(conv, True)), None, None,
-                                  n, hw, _hip.ptr(d1), c1, _hip.ptr(d2), c2, _hip.stream_of(dy)), "sp_gemm_x6")
+        ws, nb = x6_workspace(lib, n, hw, cout, c1 + c2, dy.device)
+        _hip.check(lib.sp_gemm_x6_ws(_hip.ptr(dy), cout, None, 0, _hip.ptr(_pointwise_pack(conv, True)), None, None,
+                                     n, hw, _hip.ptr(d1), c1, _hip.ptr(d2), c2, _hip.ptr(ws), nb,
+                                     _hip.stream_of(dy)), "sp_gemm_x6")
         return d1, d2
     dyv = dy.reshape(n, cout, -1)
     w = conv.weight[:, :, 0, 0]
     d1 = torch.matmul(w[:, :c1].t(), dyv).reshape((n, c1) + tuple(dy.shape[2:]))
     d2 = None if not c2 else torch.matmul(w[:, c1:].t(), dyv).reshape((n, c2) + tuple(dy.shape[2:]))
     return d1, d2
+
+
+def _folded_bias(block: "ResnetBlock2D") -> Tensor | None:
+    """conv2.bias + conv_shortcut.bias (the shortcut's bias rides in conv2's epilogue), cached
+    on the block while both are unchanged (frozen weights: one add per weight update instead
+    of one launch per forward — ~20 per UNet forward, host-bound at batch 1)."""
+    b2, bs = block.conv2.bias, block.conv_shortcut.bias
+    if bs is None or b2 is None:
+        return bs if b2 is None else b2
+    key = (b2.data_ptr(), b2._version, bs.data_ptr(), bs._version)
+    hit = block.__dict__.get("_folded_bias")
+    if hit is None or hit[0] != key:
+        with torch.no_grad():
+            hit = (key, b2 + bs)
+        block.__dict__["_folded_bias"] = hit
+    return hit[1]
 
 
 class _ResnetBlockFn(torch.autograd.Function):
@@ -214,8 +233,7 @@ class _ResnetBlockFn(torch.autograd.Function):
             short = x1
         else:
             short = _shortcut_forward(block.conv_shortcut, x1, x2)
-            if block.conv_shortcut.bias is not None:
-                bias = block.conv_shortcut.bias if bias is None else bias + block.conv_shortcut.bias
+            bias = _folded_bias(block)
         out = conv3x3_forward(block.conv2, z2, res=short, bias=bias)
         ctx.block = block
         ctx.box_in, ctx.box_out = box_in, box_out
@@ -265,9 +283,12 @@ class ResnetBlock2D(nn.Module):
         self.conv_shortcut = nn.Conv2d(cin, cout, 1) if cin != cout else None
 
     def _fusable(self, x: Tensor) -> bool:
+        params = self.__dict__.get("_param_list")
+        if params is None:  # fixed after construction; walking the submodules per call is host time
+            params = self.__dict__["_param_list"] = list(self.parameters())
         return (x.is_cuda and x.dtype == torch.float32 and x.dim() == 4
-                and not any(p.requires_grad for p in self.parameters())
-                and x[0, 0].numel() % 4 == 0)
+                and not any(p.requires_grad for p in params)
+                and (x.shape[2] * x.shape[3]) % 4 == 0)
 
     def forward(self, x: Tensor, temb: Tensor | None = None, skip: Tensor | None = None,
                 box_in: SkipGrad | None = None, box_out: SkipGrad | None = None,
@@ -574,18 +595,63 @@ class UNet2DModel(nn.Module):
         self.conv_norm_out = GroupNormAct(g, ch[0], eps=eps, act=True)
         self.conv_out = Conv3x3(ch[0], config.out_channels)
 
+    def _timestep_rows(self, timestep: Tensor | int, sample: Tensor) -> tuple[Tensor, dict] | None:
+        """(emb, {block: time_emb_proj(silu(emb))}) for a host timestep from a table over
+        t = 0 .. T-1 built once per device / dtype / weight version (frozen time-embedding
+        weights only): a step then launches no sinusoid, MLP or projection kernels and copies
+        no timestep to the device (at batch 1 each is a host-bound launch; the H2D copy of a
+        pageable tensor also waits on the stream).  At batch 1 the rows are views of the table;
+        at larger batches the row is expanded and projected per step (4 launches).  None (the
+        per-step path) for device or per-sample timesteps, or trainable weights."""
+        if torch.is_tensor(timestep):
+            if timestep.is_cuda or timestep.numel() != 1 or timestep.is_floating_point():
+                return None
+            t = int(timestep.reshape(-1)[0])
+        elif isinstance(timestep, int):
+            t = timestep
+        else:
+            return None
+        params = self.__dict__.get("_t_params")
+        if params is None:  # the module tree is fixed after construction
+            blocks = [m for m in self.modules() if isinstance(m, ResnetBlock2D) and m.time_emb_proj is not None]
+            params = list(self.time_embedding.parameters()) + [p for b in blocks for p in b.time_emb_proj.parameters()]
+            self.__dict__["_t_params"] = params
+        if t < 0 or not sample.is_cuda or any(p.requires_grad for p in params):
+            return None
+        key = (sample.device, sample.dtype, tuple((p.data_ptr(), p._version) for p in params))
+        tab = self.__dict__.get("_t_rows")
+        if tab is None or tab[0] != key or t >= tab[1].shape[0]:
+            cfg = self.config
+            with torch.no_grad():
+                ts = torch.arange(max(1000, t + 1), device=sample.device)
+                t_emb = timestep_embedding(ts, cfg.block_out_channels[0], flip_sin_to_cos=cfg.flip_sin_to_cos,
+                                           freq_shift=cfg.freq_shift).to(sample.dtype)
+                emb_all = self.time_embedding(t_emb)
+                tab = (key, emb_all, temb_projections(self, emb_all))
+            self.__dict__["_t_rows"] = tab
+        _, emb_all, tbs_all = tab
+        b = sample.shape[0]
+        if b == 1:
+            return emb_all[t:t + 1], {k: v[t:t + 1] for k, v in tbs_all.items()}
+        emb = emb_all[t:t + 1].expand(b, -1)
+        return emb, temb_projections(self, emb)
+
     def forward(self, sample: Tensor, timestep: Tensor | int) -> Tensor:
         cfg = self.config
         b = sample.shape[0]
-        if not torch.is_tensor(timestep):
-            timestep = torch.tensor([timestep], dtype=torch.long, device=sample.device)
-        timestep = timestep.reshape(-1).to(sample.device).expand(b)
-        t_emb = timestep_embedding(
-            timestep, cfg.block_out_channels[0],
-            flip_sin_to_cos=cfg.flip_sin_to_cos, freq_shift=cfg.freq_shift,
-        ).to(sample.dtype)
-        emb = self.time_embedding(t_emb)
-        tbs = temb_projections(self, emb)
+        table = self._timestep_rows(timestep, sample)
+        if table is not None:
+            emb, tbs = table
+        else:
+            if not torch.is_tensor(timestep):
+                timestep = torch.tensor([timestep], dtype=torch.long, device=sample.device)
+            timestep = timestep.reshape(-1).to(sample.device).expand(b)
+            t_emb = timestep_embedding(
+                timestep, cfg.block_out_channels[0],
+                flip_sin_to_cos=cfg.flip_sin_to_cos, freq_shift=cfg.freq_shift,
+            ).to(sample.dtype)
+            emb = self.time_embedding(t_emb)
+            tbs = temb_projections(self, emb)
 
         # every skip tensor has two consumers (the next down-path layer and an up-block
         # resnet); with grad on the device their gradients meet inside the down-path

@@ -351,6 +351,51 @@ def test_downsample_stride2_forward_and_input_vjp(cuda, shape):
         assert torch.equal(dxa, base.to(cuda) + dx)
 
 
+@pytest.mark.parametrize("shape", [(1, 256, 256, 64, 64), (1, 128, 128, 128, 128), (2, 128, 128, 32, 64)])
+def test_downsample_stride2_split_k(cuda, shape):
+    """The split-K stride-2 launches (sp_conv3x3_s2_*_ws; batch-1 downsamplers): against fp64,
+    bitwise repeatable, and the accumulating VJP equals base + the split VJP bitwise."""
+    n, cin, cout, h, w = shape
+    lib = _hip.load_library()
+    nf = int(lib.sp_conv3x3_s2_workspace(n, cin, cout, h, w, 0))
+    nv = int(lib.sp_conv3x3_s2_workspace(n, cin, cout, h, w, 1))
+    assert nf > 0 and nv > 0
+    g = torch.Generator().manual_seed(sum(shape) + 11)
+    x = torch.randn(n, cin, h, w, generator=g)
+    W = torch.randn(cout, cin, 3, 3, generator=g) * (cin * 9) ** -0.5
+    b = torch.randn(cout, generator=g) * 0.1
+    dy = torch.randn(n, cout, h // 2, w // 2, generator=g)
+    xd = x.double().requires_grad_()
+    ref = F.conv2d(F.pad(xd, (0, 1, 0, 1)), W.double(), b.double(), stride=2)
+    (gref,) = torch.autograd.grad(ref, xd, dy.double())
+    wg, bg, xc, dyc = W.to(cuda), b.to(cuda), x.to(cuda), dy.to(cuda)
+    wp = torch.empty(cin * cout * 9, device=cuda)
+    wv = torch.empty(cin * cout * 9, device=cuda)
+    _hip.check(lib.sp_conv3x3_s2_pack(_hip.ptr(wg), cout, cin, 0, _hip.ptr(wp), None), "pack")
+    _hip.check(lib.sp_conv3x3_s2_pack(_hip.ptr(wg), cout, cin, 1, _hip.ptr(wv), None), "pack vjp")
+    wsf = torch.empty(nf // 4, device=cuda)
+    wsv = torch.empty(nv // 4, device=cuda)
+    ys, dxs = [], []
+    for _ in range(2):
+        y = torch.full((n, cout, h // 2, w // 2), float("nan"), device=cuda)
+        _hip.check(lib.sp_conv3x3_s2_fwd_ws(_hip.ptr(xc), _hip.ptr(wp), _hip.ptr(bg), n, cin, cout, h, w,
+                                            _hip.ptr(y), _hip.ptr(wsf), nf, None), "fwd_ws")
+        dx = torch.full((n, cin, h, w), float("nan"), device=cuda)
+        _hip.check(lib.sp_conv3x3_s2_bwd_input_ws(_hip.ptr(dyc), _hip.ptr(wv), n, cin, cout, h, w, 0,
+                                                  _hip.ptr(dx), _hip.ptr(wsv), nv, None), "bwd_ws")
+        ys.append(y)
+        dxs.append(dx)
+    base = torch.randn(n, cin, h, w, generator=g).to(cuda)
+    dxa = base.clone()
+    _hip.check(lib.sp_conv3x3_s2_bwd_input_ws(_hip.ptr(dyc), _hip.ptr(wv), n, cin, cout, h, w, 1,
+                                              _hip.ptr(dxa), _hip.ptr(wsv), nv, None), "bwd_ws acc")
+    torch.cuda.synchronize()
+    assert torch.equal(ys[0], ys[1]) and torch.equal(dxs[0], dxs[1])
+    _check(ys[0], ref.detach())
+    _check(dxs[0], gref)
+    assert torch.equal(dxa, base + dxs[0])
+
+
 def test_downsample_stride2_rejects_bad_shapes():
     lib = _hip.load_library()
     assert not lib.sp_conv3x3_s2_supported(128, 128, 33, 64, 0)   # odd height

@@ -167,3 +167,76 @@ def test_linear_x6_input_vjp(cuda):
                "sp_linear_x6")
     torch.cuda.synchronize()
     assert _rel(dx, ref) < 1e-6
+
+
+# --- split-K (the _ws entry points): under-filled launches cut K into parts ---------------
+
+SPLIT_CASES = [  # kind, n, hw, k, m, o2, in_tm, out_tm, extras
+    ("gemm", 2, 256, 128, 128, 0, 0, 0, True),
+    ("gemm", 1, 256, 512, 256, 0, 0, 0, True),
+    ("gemm", 2, 512, 128, 128, 64, 0, 0, True),     # two outputs (the shortcut VJP form)
+    ("linear", 1, 256, 512, 320, 0, 1, 1, True),
+    ("linear", 1, 512, 768, 1280, 0, 1, 1, False),
+    ("layout", 1, 256, 512, 512, 0, 1, 0, True),    # the 16² attention's proj_out at batch 1
+    ("layout", 2, 256, 320, 640, 0, 0, 1, True),
+    ("layout", 1, 256, 256, 96, 0, 1, 1, False),
+]
+
+
+@pytest.mark.parametrize("case", SPLIT_CASES)
+def test_x6_split_k_workspace(cuda, case):
+    """A launch whose tiles fill less than half the CUs splits K (sp_gemm_x6_workspace > 0):
+    against fp64 within the unsplit bound, bitwise repeatable, and equal to the unsplit launch
+    to fp32 rounding; a NULL workspace runs unsplit."""
+    kind, n, hw, k, m, o2, in_tm, out_tm, extras = case
+    lib = _hip.load_library()
+    nb = int(lib.sp_gemm_x6_workspace(n, hw, k, m))
+    assert nb > 0
+    o1 = m - o2
+    g = torch.Generator().manual_seed(n + hw + k + m)
+    x = torch.randn(n, k, hw, generator=g)                      # [n][k][hw]
+    W = torch.randn(m, k, generator=g) * k ** -0.5
+    bias = torch.randn(m, generator=g) if extras else None
+    res = torch.randn(n, o1, hw, generator=g) if extras and not o2 else None
+    ref = torch.einsum("ok,nkp->nop", W.double(), x.double())  # [n][m][hw]
+    t32 = torch.einsum("ok,nkp->nop", W.to(cuda), x.to(cuda))
+    if bias is not None:
+        ref, t32 = ref + bias.double()[None, :, None], t32 + bias.to(cuda)[None, :, None]
+    if res is not None:
+        ref, t32 = ref + res.double(), t32 + res.to(cuda)
+    tm = lambda a: a.transpose(1, 2).reshape(n * hw, a.shape[1]).contiguous()  # noqa: E731
+    st = torch.cuda.current_stream().cuda_stream
+    wp = torch.empty(int(lib.sp_gemm_x6_packed_size(m, k)), device=cuda)
+    wg = W.to(cuda)
+    _hip.check(lib.sp_gemm_x6_pack(wg.data_ptr(), m, k, 0, wp.data_ptr(), st), "pack")
+    xg = (tm(x) if in_tm else x).to(cuda)
+    bg = None if bias is None else bias.to(cuda)
+    rg = None if res is None else (tm(res) if out_tm else res).to(cuda)
+    p = lambda t: None if t is None else t.data_ptr()  # noqa: E731
+    ws = torch.empty(nb // 4, device=cuda)
+
+    def run(ws_ptr, ws_bytes):
+        if kind == "gemm":
+            y1 = torch.full((n, o1, hw), float("nan"), device=cuda)
+            y2 = torch.full((n, o2, hw), float("nan"), device=cuda) if o2 else None
+            _hip.check(lib.sp_gemm_x6_ws(xg.data_ptr(), k, None, 0, wp.data_ptr(), p(bg), p(rg), n, hw,
+                                         y1.data_ptr(), o1, p(y2), o2, ws_ptr, ws_bytes, st), "sp_gemm_x6_ws")
+            return y1 if y2 is None else torch.cat([y1, y2], 1)
+        y = torch.full((n * hw, m) if out_tm else (n, m, hw), float("nan"), device=cuda)
+        if kind == "linear":
+            _hip.check(lib.sp_linear_x6_ws(xg.data_ptr(), wp.data_ptr(), p(bg), p(rg), n * hw, k, m,
+                                           y.data_ptr(), ws_ptr, ws_bytes, st), "sp_linear_x6_ws")
+        else:
+            _hip.check(lib.sp_gemm_x6_layout_ws(xg.data_ptr(), wp.data_ptr(), p(bg), p(rg), n, hw, k, m,
+                                                in_tm, out_tm, y.data_ptr(), ws_ptr, ws_bytes, st),
+                       "sp_gemm_x6_layout_ws")
+        return y.reshape(n, hw, m).transpose(1, 2) if out_tm else y
+
+    ys = [run(ws.data_ptr(), nb) for _ in range(3)]
+    y0 = run(None, 0)                       # unsplit
+    torch.cuda.synchronize()
+    assert torch.isfinite(ys[0]).all()
+    assert all(torch.equal(ys[0], y) for y in ys[1:])
+    e6, e32 = _rel(ys[0], ref), _rel(t32, ref)
+    assert e6 <= 1.5 * e32 + 1e-9 and e6 < 1e-6, (e6, e32)
+    assert _rel(ys[0], y0.double().cpu()) < 3e-7

@@ -52,3 +52,25 @@ def test_graph_requires_philox(cuda):
     prob = _problem("identity", cuda)
     with pytest.raises(ValueError, match="Philox"):
         DPSSampler(net)(prob, num_sampling_steps=4, rng="torch", graph=True)
+
+
+@pytest.mark.parametrize("b", [1, 3])
+def test_timestep_table_matches_per_step_embedding(cuda, b):
+    """A host timestep reads the UNet's timestep table (UNet2DModel._timestep_rows: sinusoid,
+    MLP and every block's projection precomputed for t = 0 .. 999); a device timestep takes the
+    per-step path.  Both give the same ε to GEMM rounding, and the table rows at batch 1 are
+    views (no per-step launches)."""
+    net = DDPMNetwork.from_config(CFG, seed=0, device=cuda)
+    unet = net.unet
+    x = torch.randn(b, 3, 32, 32, generator=torch.Generator().manual_seed(b)).to(cuda)
+    with torch.no_grad():
+        for t in (0, 17, 999):
+            rows = unet._timestep_rows(t, x)
+            assert rows is not None
+            if b == 1:
+                assert rows[0]._base is unet.__dict__["_t_rows"][1]
+            e_tab = unet(x, t)
+            e_dev = unet(x, torch.tensor([t], device=cuda))
+            rel = ((e_tab - e_dev).norm() / e_dev.norm()).item()
+            assert rel < 1e-5, (t, rel)
+    assert unet._timestep_rows(torch.tensor([5], device=cuda), x) is None

@@ -46,11 +46,38 @@ def main():
             lib.sp_groupnorm_single_pass(mode)
             tf = timed(lambda: gn_forward(layer, x))
             tb = timed(lambda: gn_backward(layer, dz, x, None, None, st))
-            print(json.dumps({"shape": shape, "single_pass": mode,
-                              "fwd_us": round(tf * 1e6, 1), "bwd_us": round(tb * 1e6, 1),
-                              "fwd_GBps_min_traffic": round(2 * nbytes / tf / 1e9),
-                              "bwd_GBps_min_traffic": round(3 * nbytes / tb / 1e9)}), flush=True)
+            rec = {"shape": shape, "single_pass": mode,
+                   "fwd_us": round(tf * 1e6, 1), "bwd_us": round(tb * 1e6, 1),
+                   "fwd_GBps_min_traffic": round(2 * nbytes / tf / 1e9),
+                   "bwd_GBps_min_traffic": round(3 * nbytes / tb / 1e9)}
+            if mode == 0:
+                # the two-pass kernels one by one: the apply alone is what a forward whose
+                # statistics came from the producing convolution's epilogue would cost
+                rec["kernels_us"] = kernel_times(lambda: (gn_forward(layer, x),
+                                                          gn_backward(layer, dz, x, None, None, st)))
+            print(json.dumps(rec), flush=True)
         lib.sp_groupnorm_single_pass(1)
+
+
+def kernel_times(fn, reps=10):
+    """Mean device time per launch of each kernel fn launches (torch profiler)."""
+    from torch.profiler import ProfilerActivity, profile
+
+    fn()
+    torch.cuda.synchronize()
+    with profile(activities=[ProfilerActivity.CUDA]) as prof:
+        for _ in range(reps):
+            fn()
+        torch.cuda.synchronize()
+    out = {}
+    for ev in prof.key_averages():
+        if ev.device_type.name == "CUDA" and ev.count:
+            name = ev.key.split("(")[0].replace("void ", "")[:48]
+            t = getattr(ev, "device_time_total", None)
+            if t is None:
+                t = ev.cuda_time_total
+            out[name] = round(t / ev.count, 1)
+    return out
 
 
 if __name__ == "__main__":
