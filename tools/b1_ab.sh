@@ -14,3 +14,4 @@ timeout -k 10 200 python -u -m cProfile -o $O/b1.cprof bench.py --config identit
 python -c "import pstats; s=pstats.Stats('$O/b1.cprof'); s.sort_stats('tottime').print_stats(45)" > $O/cprof_tottime.txt
 python -c "import pstats; s=pstats.Stats('$O/b1.cprof'); s.sort_stats('cumulative').print_stats(60)" > $O/cprof_cum.txt
 R=$(pwd); cd /tmp && export TMPDIR=/tmp && timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $R/$O/prof_b1 -o run -- python3 $R/bench.py --config identity --batch 1 --steps 20 --warmup 3 --no-cpu-baseline > $R/$O/prof_b1.log 2>&1
+cd $R && timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $R/$O/prof_b64 -o run -- python3 $R/bench.py --steps 5 --no-cpu-baseline > $R/$O/prof_b64.log 2>&1
