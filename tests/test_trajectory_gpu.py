@@ -230,3 +230,60 @@ def test_dps_long_trajectory_celebahq_unet_matches_oracle(cuda, parity_record):
           + f"; final x0 {err:.2e}")
     assert all(v < LONG_TOL for v in errs.values()), errs
     assert err < LONG_TOL, err
+
+
+@pytest.mark.timeout(900)
+def test_psld_long_trajectory_sd15_cfg_matches_oracle(cuda, parity_record):
+    """20 guided PSLD iterations through the SD 1.5 VAE and ε-UNet with CFG on (psld.py's loop
+    over the PNDM timesteps), batch 1 at 3x256²: the final x̂ against oracle/latent_loops.py on
+    the CPU with the same weights and injected noise."""
+    from oracle.latent_loops import psld_reference
+    from samplers_amd.inverse_problem import InverseProblem
+    from samplers_amd.networks.latent import LatentDiffusionNetwork, StableDiffusionCondition
+    from samplers_amd.noise import GaussianNoise
+    from samplers_amd.operators import CenterInpaintingOperator
+    from samplers_amd.samplers.psld import PSLDSampler
+
+    b, shape, steps = 1, (3, 256, 256), 21  # PNDM list of 21: 20 guided iterations
+    lshape = (4, 32, 32)
+    gen = torch.Generator().manual_seed(23)
+    cond = StableDiffusionCondition(prompt=None, prompt_embeds=torch.randn(b, 77, 768, generator=gen),
+                                    guidance_scale=7.5)
+    op = CenterInpaintingOperator(shape, 0.5)
+    kept = op._kept_indices.cpu()
+    n = int(np.prod(shape))
+
+    def apply(v):
+        return v.reshape(v.shape[0], -1)[:, kept]
+
+    def adjoint(v):
+        out = torch.zeros(v.shape[0], n, dtype=v.dtype)
+        out = out.index_put((torch.arange(v.shape[0])[:, None], kept[None, :]), v)
+        return out.reshape(v.shape[0], *shape)
+
+    x_true = si.fixture_x_true(b, shape, 24)
+    y = apply(x_true) + 0.05 * torch.randn(b, kept.numel(), generator=gen)
+    z0 = torch.randn(b, *lshape, generator=gen)
+    xi = {i: torch.randn(b, *lshape, generator=gen) for i in range(steps + 2)}
+
+    cpu = LatentDiffusionNetwork.from_config(seed=0)
+    gpu = copy.deepcopy(cpu).to(cuda)
+    fn = lambda k, i, s: (z0 if k == "init" else xi[i]).to(cuda)  # noqa: E731
+    problem = InverseProblem(op.to(cuda), y.to(cuda), GaussianNoise(0.05).to(cuda))
+    out = PSLDSampler(gpu)(problem, num_sampling_steps=steps, condition=cond, noise_fn=fn).cpu()
+
+    stop = _heartbeat("long PSLD oracle")
+    try:
+        cpu.set_sampling_parameters(steps, batch_size=b)
+        cpu.set_condition(cond)
+        ref = psld_reference(lambda v, t: cpu(v, t), cpu.alphas_cumprod, cpu.timesteps_host, apply,
+                             adjoint, lambda v: cpu.decode(v, differentiable=True),
+                             lambda v: cpu.encode(v, differentiable=True), y, z0, lambda i: xi[i])
+    finally:
+        stop.set()
+    assert torch.isfinite(out).all()
+    err = si.relative_error(out, ref.reshape(out.shape))
+    print(f"PSLD SD1.5 CFG: {steps - 1} guided steps + final decode, rel L2 vs oracle {err:.3e}")
+    parity_record("x0_rel_l2", err, LONG_TOL, sampler="PSLD", cfg=True, guided_steps=steps - 1, batch=b,
+                  image=list(shape))
+    assert err < LONG_TOL, f"PSLD CFG: {steps - 1} steps, rel L2 {err:.3e}"
