@@ -944,6 +944,15 @@ struct GntRegion { void* p = nullptr; size_t bytes = 0; };
 static std::mutex g_region_mu;
 static std::map<std::pair<int, hipStream_t>, GntRegion> g_regions;
 
+// A stream being captured into a graph takes the two-pass kernels (bit-identical results): a
+// replayed graph let the single-pass teams wait on members that were not resident at B = 64
+// (1.27 M recomputed partials, 3.3x the eager step; profiles/round4/graph/), and the two-pass
+// form waits on nobody.
+static bool gn_capturing(hipStream_t s) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    return hipStreamIsCapturing(s, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone;
+}
+
 static int gnt_slots(int64_t ngroups, int chunks, float* work, hipStream_t s, uint64_t** slots, int** done) {
     const size_t words = (size_t)ngroups * chunks * 16, bytes = words + (size_t)ngroups * 4;
     int dev = 0;
@@ -1061,7 +1070,7 @@ int sp_groupnorm_silu_fwd2(const float* x, const float* x2, int32_t c1, const fl
     if (!x || !z || !mean || !rstd || !work) return SP_EINVAL;
     hipStream_t s = static_cast<hipStream_t>(stream);
     const dim3 blk(kBlock);
-    if (V == 4 && g_single_pass && G.Cg <= GNP_MAX_CG && G.chunks <= GNT_MAX_CHUNKS &&
+    if (V == 4 && g_single_pass && !gn_capturing(s) && G.Cg <= GNP_MAX_CG && G.chunks <= GNT_MAX_CHUNKS &&
         (!x2 || (int64_t)(c1 % G.Cg) * hw % chunk == 0)) {
         const int64_t ngroups = n * groups;
         const void* kern;
@@ -1133,7 +1142,7 @@ int sp_groupnorm_silu_bwd2(const float* dz, const float* x, const float* x2, int
     G.add1b = add1b;
     hipStream_t s = static_cast<hipStream_t>(stream);
     const dim3 blk(kBlock);
-    if (V == 4 && g_single_pass && G.Cg <= GNP_MAX_CG && G.chunks <= GNT_MAX_CHUNKS &&
+    if (V == 4 && g_single_pass && !gn_capturing(s) && G.Cg <= GNP_MAX_CG && G.chunks <= GNT_MAX_CHUNKS &&
         (!x2 || (int64_t)(c1 % G.Cg) * hw % GN_CHUNK_BWD == 0)) {
         const int64_t ngroups = n * groups;
         constexpr int PER = GN_CHUNK_BWD / 4 / kBlock;
