@@ -196,17 +196,19 @@ __device__ __forceinline__ void g6_raw_x_tm(const unsigned char* raw, int pq, in
 }
 
 struct G6Pos { int n, p0, cb, kh; };
+// SPLIT: the split-K kernels (a compile-time variant: the unsplit ones keep their registers)
+template <bool SPLIT>
 __device__ __forceinline__ G6Pos g6_pos(const G6Geom& g, int t) {
     // XCD-aware: the output-channel blocks of one pixel tile on one XCD (shared X lines)
     const int lb0 = (g.ntiles & 7) ? t : (t & 7) * (g.ntiles >> 3) + (t >> 3);
-    const int kh = lb0 % g.ksplit, lb = lb0 / g.ksplit;
+    const int kh = SPLIT ? lb0 % g.ksplit : 0, lb = SPLIT ? lb0 / g.ksplit : lb0;
     const int cb = lb % g.cob, rest = lb / g.cob;
     const int n = rest / g.ptiles;
     // the item inside the grid's work, its pixels inside the plane (or the token rows), its
     // k-steps inside K
     SP_DCHECK(t >= 0 && t < g.ntiles && lb0 < g.ntiles && cb * G6_CO < g.o1 + g.o2 + G6_CO &&
               (rest - n * g.ptiles + 1) * G6_PX <= (g.tokens ? g.tokens : g.hw) &&
-              (kh + 1) * g.kper <= g.nsteps);
+              (!SPLIT || (kh + 1) * g.kper <= g.nsteps));
     return G6Pos{n, (rest - n * g.ptiles) * G6_PX, cb, kh};
 }
 
@@ -355,8 +357,9 @@ typedef unsigned char G6XSlot[G6_KC * G6_PX * 4];
 typedef unsigned char G6WSlot[G6_WB];
 
 // LATE: this wave issues its loads half-way through its MFMAs (the second wave of each SIMD)
-template <bool LTM, bool STM, bool LATE>
+template <bool LTM, bool STM, bool LATE, bool SPLIT>
 __device__ __forceinline__ void g6_body(const G6Geom& g, G6XSlot* xraw, G6WSlot* wl, int wv) {
+    const int kper = SPLIT ? g.kper : g.nsteps;  // k-steps per work item
     const int tid = threadIdx.x, lane = tid & 63;
     const int ch = wv & 1, pq = wv >> 1;  // 64 output channels x 64 pixels
     const auto wrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<unsigned short*>(g.wp), (short)0,
@@ -365,19 +368,19 @@ __device__ __forceinline__ void g6_body(const G6Geom& g, G6XSlot* xraw, G6WSlot*
     const unsigned wl_lds = static_cast<unsigned>(reinterpret_cast<size_t>((lds_void_g*)&wl[0][0]));
     const int G = gridDim.x, b0 = blockIdx.x;
     const int ntile_wg = (g.ntiles - b0 + G - 1) / G;
-    const int J = ntile_wg * g.kper;
+    const int J = ntile_wg * kper;
     // two load streams, advanced one k-step at a time (divisions once per tile)
     struct Cursor { int j, tw, s, slot; G6Pos ps; };
-    Cursor cx{0, 0, 0, 0, g6_pos(g, b0)}, cw = cx;
+    Cursor cx{0, 0, 0, 0, g6_pos<SPLIT>(g, b0)}, cw = cx;
     // the X stream's image bases, renewed when its tile changes
     const float* xb1 = g.x1 + (int64_t)cx.ps.n * g.c1 * g.hw;
     const float* xb2 = g.x2 + (int64_t)cx.ps.n * g.c2 * g.hw;
     auto advance = [&](Cursor& c, int nslots) {
         ++c.j;
         c.slot = c.slot + 1 == nslots ? 0 : c.slot + 1;
-        if (++c.s == g.kper) {
+        if (++c.s == kper) {
             c.s = 0;
-            if (++c.tw < ntile_wg) c.ps = g6_pos(g, b0 + c.tw * G);
+            if (++c.tw < ntile_wg) c.ps = g6_pos<SPLIT>(g, b0 + c.tw * G);
             return true;
         }
         return false;
@@ -385,7 +388,7 @@ __device__ __forceinline__ void g6_body(const G6Geom& g, G6XSlot* xraw, G6WSlot*
     auto dma_x = [&]() {
         if (cx.j < J) {
             const unsigned sl = xraw_lds + cx.slot * (G6_KC * G6_PX * 4);
-            const int ks = cx.ps.kh * g.kper + cx.s;  // the k-step inside K
+            const int ks = SPLIT ? cx.ps.kh * kper + cx.s : cx.s;  // the k-step inside K
             if constexpr (LTM) g6_dma_x_tm(g, cx.ps.n * g.hw + cx.ps.p0, ks, wv, lane, sl);
             else g6_dma_x(g, xb1, xb2, cx.ps.p0, ks, wv, lane, sl);
         }
@@ -396,7 +399,8 @@ __device__ __forceinline__ void g6_body(const G6Geom& g, G6XSlot* xraw, G6WSlot*
     };
     auto dma_w = [&]() {
         if (cw.j < J)
-            g6_dma_w(wrs, cw.ps.cb * g.nsteps + cw.ps.kh * g.kper + cw.s, wv, lane, wl_lds + cw.slot * G6_WB);
+            g6_dma_w(wrs, cw.ps.cb * g.nsteps + (SPLIT ? cw.ps.kh * kper : 0) + cw.s, wv, lane,
+                     wl_lds + cw.slot * G6_WB);
         advance(cw, G6_NW);
     };
     // prologue: W 0 .. 2 and X 0 .. 4 in flight, then all landed
@@ -517,11 +521,11 @@ __device__ __forceinline__ void g6_body(const G6Geom& g, G6XSlot* xraw, G6WSlot*
 #pragma unroll
             for (int b = 0; b < 2; ++b) acc[a][b] = f32x16{}, acs[a][b] = f32x16{};
         s = 0;
-        while (s + 1 < g.kper) {
+        while (s + 1 < kper) {
             kstep(fuA, xrA, fuB, xrB);
             kstep(fuB, xrB, fuA, xrA);
         }
-        if (s < g.kper) {  // odd step count: one more, and set A back to the current step
+        if (s < kper) {  // odd step count: one more, and set A back to the current step
             kstep(fuA, xrA, fuB, xrB);
 #pragma unroll
             for (int a = 0; a < 2; ++a)
@@ -532,10 +536,10 @@ __device__ __forceinline__ void g6_body(const G6Geom& g, G6XSlot* xraw, G6WSlot*
 #pragma unroll
                 for (int i = 0; i < 8; ++i) xrA[b][i] = xrB[b][i];
         }
-        const G6Pos ps = g6_pos(g, b0 + tw * G);
+        const G6Pos ps = g6_pos<SPLIT>(g, b0 + tw * G);
         // split-K: the part goes to its workspace slice as a single output of all m channels
         G6Geom ge = g;
-        if (g.ksplit > 1) {
+        if (SPLIT) {
             ge.y1 = g.ws + ps.kh * g.ws_stride;
             ge.y2 = nullptr;
             ge.o1 = g.o1 + g.o2;
@@ -551,14 +555,14 @@ __device__ __forceinline__ void g6_body(const G6Geom& g, G6XSlot* xraw, G6WSlot*
     }
 }
 
-template <bool LTM, bool STM>
+template <bool LTM, bool STM, bool SPLIT = false>
 __global__ __launch_bounds__(G6_THREADS, 1) void k_gemm_x6(G6Geom g) {
     __shared__ __attribute__((aligned(16))) G6XSlot xraw[G6_NX];
     __shared__ __attribute__((aligned(16))) G6WSlot wl[G6_NW];
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     // waves w and w + 4 share a SIMD: the second one issues its loads half-way (G6_STAGGER)
-    if (G6_STAGGER && (wv & 4)) g6_body<LTM, STM, true>(g, xraw, wl, wv);
-    else g6_body<LTM, STM, false>(g, xraw, wl, wv);
+    if (G6_STAGGER && (wv & 4)) g6_body<LTM, STM, true, SPLIT>(g, xraw, wl, wv);
+    else g6_body<LTM, STM, false, SPLIT>(g, xraw, wl, wv);
 }
 
 // the split terms of A element (row, col) of an [M][K] operand into their fragment slots
@@ -670,7 +674,8 @@ static int g6_launch(G6Geom g, int64_t tiles, int64_t n, float* ws, int64_t ws_b
     g.ws_stride = n * g.hw * m;
     g.ntiles = static_cast<int>(tiles * ks);
     const int grid = static_cast<int>(std::min<int64_t>(g.ntiles, g6_cu_count()));
-    launch(0, k_gemm_x6<LTM, STM>, dim3(grid), dim3(G6_THREADS), s, g);
+    if (ks > 1) launch(0, k_gemm_x6<LTM, STM, true>, dim3(grid), dim3(G6_THREADS), s, g);
+    else launch(0, k_gemm_x6<LTM, STM>, dim3(grid), dim3(G6_THREADS), s, g);
     if (ks > 1) {
         const int64_t total4 = n * g.hw * m / 4;
         launch(0, k_g6_split_reduce, dim3(static_cast<unsigned>((total4 + 255) / 256)), dim3(256), s, ws, ks,
