@@ -29,6 +29,27 @@ def group_norm_act_torch(x: Tensor, groups: int, weight: Tensor | None, bias: Te
     return F.silu(y) if act else y
 
 
+# Per-shape answers of the library's pure shape queries (tile support, workspace sizes), cached:
+# at batch 1 a step makes ~600 launches and each query is a ctypes round trip on the host path.
+_shape_cache: dict = {}
+
+
+def _query(fn_name: str, *args: int) -> int:
+    key = (fn_name, args)
+    v = _shape_cache.get(key)
+    if v is None:
+        v = _shape_cache[key] = int(getattr(_hip.load_library(), fn_name)(*args))
+    return v
+
+
+def _hw(t: Tensor) -> int:
+    """Pixels per channel plane of an [n][c][...] tensor (1 for [n][c])."""
+    hw = 1
+    for d in t.shape[2:]:
+        hw *= d
+    return hw
+
+
 def gn_forward(norm: "GroupNormAct", x1: Tensor, x2: Tensor | None = None,
                chan_bias: Tensor | None = None) -> tuple[Tensor, Tensor]:
     """HIP GroupNorm(+bias)(+SiLU) forward over x1, or over cat(x1, x2) along channels read in
@@ -36,16 +57,17 @@ def gn_forward(norm: "GroupNormAct", x1: Tensor, x2: Tensor | None = None,
     lib = _hip.load_library()
     n, c1 = x1.shape[0], x1.shape[1]
     c = c1 + (x2.shape[1] if x2 is not None else 0)
-    hw = x1[0, 0].numel() if x1.numel() else 1
+    hw = _hw(x1) if x1.numel() else 1
+    g = norm.num_groups
     z = torch.empty((n, c) + tuple(x1.shape[2:]), device=x1.device, dtype=torch.float32)
-    stats = torch.empty(2, n * norm.num_groups, device=x1.device, dtype=torch.float32)
-    work = torch.empty(max(int(lib.sp_groupnorm_workspace(n, c, hw, norm.num_groups)), 1),
-                       device=x1.device, dtype=torch.float32)
+    stats = torch.empty(2, n * g, device=x1.device, dtype=torch.float32)
+    work = torch.empty(max(_query("sp_groupnorm_workspace", n, c, hw, g), 1), device=x1.device,
+                       dtype=torch.float32)
+    sp = _hip.ptr(stats)
     _hip.check(lib.sp_groupnorm_silu_fwd2(
         _hip.ptr(x1), _hip.ptr(x2), c1, _hip.ptr(chan_bias), _hip.ptr(norm.weight),
-        _hip.ptr(norm.bias), n, c, hw, norm.num_groups, float(norm.eps), int(norm.act),
-        _hip.ptr(z), _hip.ptr(stats[0]), _hip.ptr(stats[1]), _hip.ptr(work),
-        _hip.stream_of(x1)), "sp_groupnorm_silu_fwd2")
+        _hip.ptr(norm.bias), n, c, hw, g, float(norm.eps), int(norm.act),
+        _hip.ptr(z), sp, sp + 4 * n * g, _hip.ptr(work), _hip.stream_of(x1)), "sp_groupnorm_silu_fwd2")
     return z, stats
 
 
@@ -59,15 +81,17 @@ def gn_backward(norm: "GroupNormAct", dz: Tensor, x1: Tensor, x2: Tensor | None,
     lib = _hip.load_library()
     n, c1 = x1.shape[0], x1.shape[1]
     c = dz.shape[1]
-    hw = x1[0, 0].numel() if x1.numel() else 1
+    hw = _hw(x1) if x1.numel() else 1
+    g = norm.num_groups
     dx1 = torch.empty_like(x1) if out1 is None else out1
     dx2 = None if x2 is None else (torch.empty_like(x2) if out2 is None else out2)
-    work = torch.empty(max(int(lib.sp_groupnorm_workspace(n, c, hw, norm.num_groups)), 1),
-                       device=x1.device, dtype=torch.float32)
+    work = torch.empty(max(_query("sp_groupnorm_workspace", n, c, hw, g), 1), device=x1.device,
+                       dtype=torch.float32)
+    sp = _hip.ptr(stats)
     _hip.check(lib.sp_groupnorm_silu_bwd2(
         _hip.ptr(dz.contiguous()), _hip.ptr(x1), _hip.ptr(x2), c1, _hip.ptr(chan_bias),
-        _hip.ptr(norm.weight), _hip.ptr(norm.bias), _hip.ptr(stats[0]), _hip.ptr(stats[1]), n, c,
-        hw, norm.num_groups, int(norm.act), _hip.ptr(dx1), _hip.ptr(dx2), _hip.ptr(add1),
+        _hip.ptr(norm.weight), _hip.ptr(norm.bias), sp, sp + 4 * n * g, n, c,
+        hw, g, int(norm.act), _hip.ptr(dx1), _hip.ptr(dx2), _hip.ptr(add1),
         _hip.ptr(add2), _hip.ptr(add1b), _hip.ptr(work), _hip.stream_of(x1)), "sp_groupnorm_silu_bwd2")
     return dx1, dx2
 
@@ -77,11 +101,11 @@ class _GroupNormActFn(torch.autograd.Function):
     def forward(ctx, x, weight, bias, chan_bias, groups: int, eps: float, act: bool, box=None):
         lib = _hip.load_library()
         n, c = x.shape[0], x.shape[1]
-        hw = x[0, 0].numel() if x.numel() else 1
+        hw = _hw(x) if x.numel() else 1
         x = x.contiguous()
         z = torch.empty_like(x)
         stats = torch.empty(2, n * groups, device=x.device, dtype=torch.float32)
-        work = torch.empty(max(int(lib.sp_groupnorm_workspace(n, c, hw, groups)), 1),
+        work = torch.empty(max(_query("sp_groupnorm_workspace", n, c, hw, groups), 1),
                            device=x.device, dtype=torch.float32)
         cb = None if chan_bias is None else chan_bias.contiguous()
         _hip.check(lib.sp_groupnorm_silu_fwd(
@@ -99,10 +123,10 @@ class _GroupNormActFn(torch.autograd.Function):
         groups, eps, act = ctx.cfg
         lib = _hip.load_library()
         n, c = x.shape[0], x.shape[1]
-        hw = x[0, 0].numel() if x.numel() else 1
+        hw = _hw(x) if x.numel() else 1
         dz = dz.contiguous()
         dx = torch.empty_like(x)
-        work = torch.empty(max(int(lib.sp_groupnorm_workspace(n, c, hw, groups)), 1),
+        work = torch.empty(max(_query("sp_groupnorm_workspace", n, c, hw, groups), 1),
                            device=x.device, dtype=torch.float32)
         add = ctx.box.take() if ctx.box is not None else None
         if add is not None:  # the residual branch's gradient of x, summed in the VJP kernel
@@ -193,11 +217,11 @@ def conv_backend() -> str:
 def _conv_algo(lib, cin: int, cout: int, h: int, w: int, backend: str) -> str | None:
     if backend == "miopen":
         return None
-    if backend == "auto" and lib.sp_wino3x3_supported(cin, cout, h, w):
+    if backend == "auto" and _query("sp_wino3x3_supported", cin, cout, h, w):
         return "wino"
-    if lib.sp_conv3x3_supported(cin, cout, h, w):
+    if _query("sp_conv3x3_supported", cin, cout, h, w):
         return "direct"
-    if lib.sp_conv3x3_thin_supported(cin, cout, h, w):
+    if _query("sp_conv3x3_thin_supported", cin, cout, h, w):
         return "thin"  # few channels on one side (conv_in / conv_out): VALU direct conv
     return None
 
@@ -242,7 +266,7 @@ def _wino_workspace(lib, n: int, cin: int, cout: int, h: int, w: int, device) ->
     """A workspace for the Winograd tile's split-K parts, or None when the shape fills the
     chip unsplit (sp_wino3x3_workspace).  From torch's caching allocator on the launch
     stream, so a graph capture records it and a later reuse is ordered after the launch."""
-    nb = int(lib.sp_wino3x3_workspace(n, cin, cout, h, w))
+    nb = _query("sp_wino3x3_workspace", n, cin, cout, h, w)
     if nb <= 0:
         return None
     return torch.empty(nb // 4, device=device, dtype=torch.float32)
@@ -253,7 +277,7 @@ def x6_workspace(lib, n: int, hw: int, k: int, m: int, device) -> tuple[Tensor |
     n images of hw pixels, or n = 1 and hw = tokens), and its size in bytes; (None, 0) when the
     launch fills the chip unsplit.  Torch's caching allocator on the launch stream, as
     _wino_workspace; the caller holds it until the launch is queued."""
-    nb = int(lib.sp_gemm_x6_workspace(n, hw, k, m))
+    nb = _query("sp_gemm_x6_workspace", n, hw, k, m)
     if nb <= 0:
         return None, 0
     return torch.empty(nb // 4, device=device, dtype=torch.float32), nb
@@ -449,7 +473,7 @@ class SkipGrad:
 def _s2_workspace(lib, n: int, cin: int, cout: int, h: int, w: int, vjp: int, device) -> tuple[Tensor | None, int]:
     """The stride-2 tile's split-K workspace for an under-filled launch (sp_conv3x3_s2_workspace)
     and its bytes, or (None, 0); allocated as _wino_workspace."""
-    nb = int(lib.sp_conv3x3_s2_workspace(n, cin, cout, h, w, vjp))
+    nb = _query("sp_conv3x3_s2_workspace", n, cin, cout, h, w, vjp)
     if nb <= 0:
         return None, 0
     return torch.empty(nb // 4, device=device, dtype=torch.float32), nb
@@ -658,8 +682,7 @@ def linear(x: Tensor, module: nn.Module, w2d: Tensor | None = None, bias: Tensor
     if (x.is_cuda and x.dtype == torch.float32 and not w2d.requires_grad
             and (bias is None or not bias.requires_grad) and linear_backend() == "x6"
             and (res is None or (res.dtype == torch.float32 and res.numel() == t * m))):
-        lib = _hip.load_library()
-        if lib.sp_linear_x6_supported(t, k, m) and x6_enough_tiles(t, m):
+        if _query("sp_linear_x6_supported", t, k, m) and x6_enough_tiles(t, m):
             return _LinearX6Fn.apply(x, w2d, bias, module, w2d, res, box)
     if box is not None:
         box.enabled = False

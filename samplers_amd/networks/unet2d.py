@@ -31,7 +31,7 @@ from torch import Tensor, nn
 from .. import _hip
 from .layers import (Conv3x3, GroupNormAct, Linear, SkipGrad, conv3x3_forward, conv3x3_input_vjp,
                      downsample_conv, gn_backward, gn_forward, miopen_fallback, proj_nchw_to_tokens,
-                     proj_tokens_to_nchw, upsample_nearest2x, x6_enough_tiles, x6_workspace)
+                     proj_tokens_to_nchw, upsample_nearest2x, x6_enough_tiles, x6_workspace, _query)
 
 
 @dataclass(frozen=True)
@@ -137,8 +137,7 @@ def _pointwise_pack(conv: nn.Conv2d, trans: bool) -> Tensor:
 
 
 def _x6_ok(m: int, c1: int, c2: int, o1: int, o2: int, hw: int, n: int) -> bool:
-    lib = _hip.load_library()
-    return (_shortcut_backend() == "x6" and bool(lib.sp_gemm_x6_supported(m, c1 + c2, hw))
+    return (_shortcut_backend() == "x6" and bool(_query("sp_gemm_x6_supported", m, c1 + c2, hw))
             and c1 % 8 == 0 and c2 % 8 == 0 and o1 % 32 == 0 and o2 % 32 == 0
             and x6_enough_tiles(n * hw, o1 + o2))
 

@@ -2,7 +2,7 @@
 final gather reproduce the single-process result exactly."""
 
 import os
-import socket
+import tempfile
 
 import numpy as np
 import pytest
@@ -33,14 +33,14 @@ def fake_sampler(problem, *, num_reconstructions, seed, sample_offset, keep_reco
 
 
 def _free_port():
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        return s.getsockname()[1]
+    """A rendezvous for the workers: a FileStore path (file:// init), not a TCP port — a port
+    picked free here can be taken by another socket before rank 0 binds it (a rare flaky
+    failure of these tests); gloo's own pair connections use OS-assigned ports."""
+    return "file://" + os.path.join(tempfile.mkdtemp(prefix="sp_rdv_"), "store")
 
 
 def _worker(rank, world, port, batch, R, result_path):
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dist.init_process_group("gloo", init_method=port, rank=rank, world_size=world)
     try:
         obs = torch.arange(batch * N, dtype=torch.float32).reshape(batch, *SHAPE)
         prob = InverseProblem(IdentityOperator(SHAPE), obs, GaussianNoise(0.1))
@@ -99,8 +99,7 @@ def _norm_worker(rank, world, port, result_path):
     from samplers_amd.samplers.psld import generic_pixel_terms
     from samplers_amd.samplers.resample import _GenericConsistency
 
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dist.init_process_group("gloo", init_method=port, rank=rank, world_size=world)
     try:
         out = _norm_terms(si, generic_pixel_terms, _GenericConsistency, all_reduce_sum_,
                           rank, world)
@@ -174,8 +173,7 @@ def coupled_sampler(problem, *, num_reconstructions, seed, sample_offset, group=
 
 
 def _coupled_worker(rank, world, port, batch, R, decode, result_path, out_dtype=None):
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dist.init_process_group("gloo", init_method=port, rank=rank, world_size=world)
     try:
         obs = torch.arange(1, batch * N + 1, dtype=torch.float32).reshape(batch, *SHAPE)
         prob = InverseProblem(IdentityOperator(SHAPE), obs, GaussianNoise(0.1))
