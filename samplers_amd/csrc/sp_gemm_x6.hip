@@ -41,7 +41,7 @@ typedef __attribute__((address_space(3))) void lds_void_g;
 #endif
 #ifndef G6_EXP
 #define G6_EXP 0  // diagnostics only (wrong results, timing): 1 no MFMAs, 2 no split, 3 no loads,
-                  // 4 no output stores
+                  // 4 no output stores, 5 X loads from one cached 2 KB (no X stream from HBM)
 #endif
 constexpr int G6_CO = 128;     // output channels per workgroup
 constexpr int G6_PX = 256;     // pixels per workgroup
@@ -389,8 +389,14 @@ __device__ __forceinline__ void g6_body(const G6Geom& g, G6XSlot* xraw, G6WSlot*
         if (cx.j < J) {
             const unsigned sl = xraw_lds + cx.slot * (G6_KC * G6_PX * 4);
             const int ks = SPLIT ? cx.ps.kh * kper + cx.s : cx.s;  // the k-step inside K
+#if G6_EXP == 5  // diagnostics (wrong results): the same DMA pieces, all from one cached 2 KB
+            (void)ks;
+            g6_lds_dma(wrs, sl + (2 * wv) * 1024, lane * 16, 0);
+            g6_lds_dma(wrs, sl + (2 * wv + 1) * 1024, lane * 16, 1024);
+#else
             if constexpr (LTM) g6_dma_x_tm(g, cx.ps.n * g.hw + cx.ps.p0, ks, wv, lane, sl);
             else g6_dma_x(g, xb1, xb2, cx.ps.p0, ks, wv, lane, sl);
+#endif
         }
         if (advance(cx, G6_NX) && !LTM) {
             xb1 = g.x1 + (int64_t)cx.ps.n * g.c1 * g.hw;
