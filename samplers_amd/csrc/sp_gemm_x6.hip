@@ -326,6 +326,9 @@ __device__ __forceinline__ int g6_epilogue_tm(const G6Geom& g, const G6Pos& ps, 
 #pragma unroll
             for (int q = 0; q < 16; ++q) {
                 const float y = (acc[a][b][q] + acs[a][b][q]) + bv + rv[q];
+#if G6_EXP == 4
+                if (g.hw >= 0) continue;  // never true at run time: the stores are skipped, all math kept
+#endif
                 __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(y), ors,
                                                       ((t0 + RS * ((q & 3) + 8 * (q >> 2))) * g.o1 + o) * 4, 0, 0);
             }
