@@ -147,7 +147,8 @@ __device__ __forceinline__ void wino_filter(const float (&g)[9], float (&u)[16])
 constexpr int WR_CO = 64;   // output channels per workgroup (2 waves x 32)
 #ifndef SP_WINO_EXP
 #define SP_WINO_EXP 0  // diagnostics only: 1 = no loads in the k loop, 2 = no output stores,
-                       // 3 = no input transform (wrong results, timing only)
+                       // 3 = no input transform, 6 = the ξ-split tile without its epilogue
+                       // (wrong results, timing only)
 #endif
 #ifndef SP_WINO_BURST
 #define SP_WINO_BURST 1  // the transform's placement in the k-step: 0 one row per MFMA gap, 1 one
@@ -926,6 +927,9 @@ __device__ __forceinline__ void xi_body(const WrGeom& g, int wv, int lane, float
         }
         xi_steps<H, false, true, RES_AT>(std::make_integer_sequence<int, XI_NR - RES_AT>{}, g, cur, nxt, urs, lane,
                                          xw, xl, last, r, acc);
+#if SP_WINO_EXP == 6
+        if (g.W < 0)  // never true at run time: no epilogue (the MFMAs stay live)
+#endif
         xi_epilogue<H, RES>(g, ti, wv, lane, acc, rv, ex);
         t = tn;
         if (t >= g.ntiles) break;
