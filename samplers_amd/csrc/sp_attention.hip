@@ -56,6 +56,11 @@ struct AtGeo {
     static constexpr int NF4 = (SB * D / 4 + kBlock - 1) / kBlock;  // float4 per thread per tensor
 };
 
+// 2^x as the bare v_exp_f32: exp2f adds a range check and rescale for results below 2^-126
+// (five instructions per score); here x <= 0 and such weights vanish beside the row's largest
+// (2^0) in every sum they enter.  exp2(-inf) = 0 as before.
+__device__ __forceinline__ float at_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
+
 __device__ __forceinline__ at_f4 at_mfma(float a, float b, at_f4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
@@ -194,22 +199,29 @@ __global__ __launch_bounds__(kBlock) void k_attn_fwd(const float* __restrict__ q
 #pragma unroll
                         for (int t = 0; t < G::QT; ++t) s[t][i] = -INFINITY;
             }
-            float p[G::QT][4];
+            float p[G::QT][4], corr[G::QT];
+            bool moved = false;
 #pragma unroll
             for (int t = 0; t < G::QT; ++t) {
                 const float mn = fmaxf(m[t], at_colmax(at_max4(s[t])));
-                const float corr = exp2f(m[t] - mn);  // 0 on the first block (m = -inf)
+                corr[t] = at_exp2(m[t] - mn);  // 0 on the first block (m = -inf)
+                moved |= corr[t] != 1.f;
                 m[t] = mn;
                 float ps = 0.f;
 #pragma unroll
                 for (int i = 0; i < 4; ++i) {
-                    p[t][i] = exp2f(s[t][i] - mn);
+                    p[t][i] = at_exp2(s[t][i] - mn);
                     ps += p[t][i];
                 }
-                l[t] = fmaf(l[t], corr, ps);  // this lane's partial row sum
-#pragma unroll
-                for (int dt = 0; dt < G::DT; ++dt) o[t][dt] *= corr;
+                l[t] = fmaf(l[t], corr[t], ps);  // this lane's partial row sum
             }
+            // rescale the outputs only when some query's running max moved (a wave-uniform
+            // branch; skipping a multiply by exactly 1 changes no bit)
+            if (__builtin_amdgcn_ballot_w64(moved))
+#pragma unroll
+                for (int t = 0; t < G::QT; ++t)
+#pragma unroll
+                    for (int dt = 0; dt < G::DT; ++dt) o[t][dt] *= corr[t];
             // O^T += V^T P^T: k-step i takes key 4 kl + i (A: V[key][dt*16 + li])
             const float* vr = Vs + (sb * 16 + 4 * kl) * G::DP + li;
 #pragma unroll
@@ -346,7 +358,7 @@ __global__ __launch_bounds__(kBlock) void k_attn_dq(const float* __restrict__ q,
 #pragma unroll
             for (int t = 0; t < G::QT; ++t)
 #pragma unroll
-                for (int i = 0; i < 4; ++i) ds[t][i] = exp2f(s[t][i] - ls[t]) * (dp[t][i] - de[t]);
+                for (int i = 0; i < 4; ++i) ds[t][i] = at_exp2(s[t][i] - ls[t]) * (dp[t][i] - de[t]);
             // dQ^T += K^T dS^T: k-step i takes key 4 kl + i (A: K[key][dt*16 + li])
             const float* kt = Ks + (sb * 16 + 4 * kl) * G::DP + li;
 #pragma unroll
@@ -456,7 +468,7 @@ __global__ __launch_bounds__(kBlock) void k_attn_dkv(const float* __restrict__ q
             for (int t = 0; t < G::QT; ++t)
 #pragma unroll
                 for (int i = 0; i < 4; ++i) {
-                    p[t][i] = exp2f(s[t][i] - pl[i]);
+                    p[t][i] = at_exp2(s[t][i] - pl[i]);
                     ds[t][i] = p[t][i] * (dp[t][i] - pe[i]);
                 }
             // dV^T += dO^T P, dK^T += Q^T dS: k-step i takes query 4 kl + i
