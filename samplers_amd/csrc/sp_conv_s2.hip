@@ -65,19 +65,25 @@ __device__ __forceinline__ void s2_load(const float* __restrict__ wp, const floa
         if (i < S2_NA - 1 || idx < S2_A4)
             st.a[i] = *reinterpret_cast<const s2_f32x4*>(src + (int64_t)(idx >> 5) * cout + (idx & 31) * 4);
     }
-    const float* xc = xn + (int64_t)cc * S2_CI * plane;
+    // the patch by buffer loads over this chunk's planes: a position outside the image (the
+    // zero row / column of the padding) gets an offset past the buffer, which reads as 0 — no
+    // branches or zero-fill moves around the loads
+    constexpr int OOB = 0x7FFFFFF0;
+    const auto xrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(xn + (int64_t)cc * S2_CI * plane),
+                                                       (short)0, static_cast<int>(S2_CI * plane * 4), 0x00020000);
 #pragma unroll
     for (int i = 0; i < S2_NP; ++i) {
         const int idx = tid + kBlock * i;
         const int q = idx & 15, rc = idx >> 4, ci = rc / S2_PR, row = rc - ci * S2_PR;
         const bool ok = (i < S2_NP - 1 || idx < S2_F4) && r0 + row < H;
-        st.p[i] = ok ? *reinterpret_cast<const s2_f32x4*>(xc + ci * plane + (int64_t)(r0 + row) * W + c0 + 4 * q)
-                     : s2_f32x4{};
+        const int off = ok ? static_cast<int>((ci * plane + (int64_t)(r0 + row) * W + c0 + 4 * q) * 4) : OOB;
+        st.p[i] = __builtin_bit_cast(s2_f32x4, __builtin_amdgcn_raw_buffer_load_b128(xrs, off, 0, 0));
     }
     {
         const int ci = tid / S2_PR, row = tid - ci * S2_PR;
         const bool ok = tid < S2_TAIL && r0 + row < H && c0 + 64 < W;
-        st.t = ok ? xc[ci * plane + (int64_t)(r0 + row) * W + c0 + 64] : 0.f;
+        const int off = ok ? static_cast<int>((ci * plane + (int64_t)(r0 + row) * W + c0 + 64) * 4) : OOB;
+        st.t = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xrs, off, 0, 0));
     }
 }
 
@@ -93,8 +99,12 @@ __device__ __forceinline__ void s2_store(float* As, float* Ps, int tid, const S2
         const int q = idx & 15, rc = idx >> 4, ci = rc / S2_PR, row = rc - ci * S2_PR;
         if (i < S2_NP - 1 || idx < S2_F4) {
             float* d = Ps + ci * S2_PATCH + row * S2_RS + 2 * q;
-            *reinterpret_cast<s2_f32x2*>(d) = s2_f32x2{st.p[i][0], st.p[i][2]};           // even
-            *reinterpret_cast<s2_f32x2*>(d + S2_HALF) = s2_f32x2{st.p[i][1], st.p[i][3]};  // odd
+            // two ds_write2_b32 of (even, odd) element pairs: float2 stores of (p0, p2) and
+            // (p1, p3) cost four register moves per piece to form the pairs (the empty asm keeps
+            // the compiler from merging the dword stores back into them)
+            d[0] = st.p[i][0], d[S2_HALF] = st.p[i][1];
+            asm volatile("" ::: "memory");
+            d[1] = st.p[i][2], d[S2_HALF + 1] = st.p[i][3];
         }
     }
     if (tid < S2_TAIL) {
@@ -205,7 +215,10 @@ __device__ __forceinline__ void s2b_load(const float* __restrict__ wp, const flo
         if (i < S2B_NA - 1 || idx < S2B_A4)
             st.a[i] = *reinterpret_cast<const s2_f32x4*>(src + (int64_t)(idx >> 5) * cin + (idx & 31) * 4);
     }
-    const float* dc = dyn + (int64_t)cc * S2B_CO * oplane;
+    // the dy patch by buffer loads (outside the image: an offset past the buffer, read as 0)
+    constexpr int OOB = 0x7FFFFFF0;
+    const auto drs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(dyn + (int64_t)cc * S2B_CO * oplane),
+                                                       (short)0, static_cast<int>(S2B_CO * oplane * 4), 0x00020000);
 #pragma unroll
     for (int i = 0; i < S2B_NP; ++i) {
         const int idx = tid + kBlock * i;
@@ -213,7 +226,8 @@ __device__ __forceinline__ void s2b_load(const float* __restrict__ wp, const flo
         const int pr = rem / 33, pc = rem - pr * 33;
         const int gi = i0 - 1 + pr, gj = j0 - 1 + pc;
         const bool ok = idx < S2B_PN && gi >= 0 && gj >= 0 && gi < Ho && gj < Wo;
-        st.p[i] = ok ? dc[co * oplane + (int64_t)gi * Wo + gj] : 0.f;
+        const int off = ok ? static_cast<int>((co * oplane + (int64_t)gi * Wo + gj) * 4) : OOB;
+        st.p[i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(drs, off, 0, 0));
     }
 }
 
