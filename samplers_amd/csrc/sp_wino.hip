@@ -676,6 +676,9 @@ __global__ __launch_bounds__(kBlock, 1) void k_wino3x3_r(WrGeom g) {
 // (6, 6) 218.7, (7, 6) 218.2 — no gain: the k-steps do not wait on load latency (SQ_WAIT_ANY
 // is 5 % of wave cycles; the MFMA pipe is busy 0.85 of the cycles at the clock the chip holds,
 // profiles/round4/wino/sq_counters.txt).  The shallow ring keeps the registers.
+#ifndef SP_WINO_XI16
+#define SP_WINO_XI16 1  // the ξ-split tile on the W = 16 geometry too (the UNets' 16x16 levels)
+#endif
 #ifndef SP_WINO_DX
 #define SP_WINO_DX 3
 #endif
@@ -721,11 +724,11 @@ __device__ __forceinline__ void xi_half(const WinRow& e0, const WinRow& e1, cons
 // One k-step q (ring slot K = q mod XI_NR): MFMAs on U(q) and V(q); beside them the loads of
 // the block of step q + DX and of U(q + DU) (XN / UN: those steps belong to the next tile), the
 // block of step q + 1 staged in LDS, its window read and half of V(q + 1) transformed.
-template <int H, int K, bool FIRST, bool XN, bool UN>
+template <class GE, int H, int K, bool FIRST, bool XN, bool UN>
 __device__ __forceinline__ void xi_step(const WrGeom& g, const WrSrc& cur, const WrSrc& nxt,
                                         __amdgpu_buffer_rsrc_t urs, int lane, float* xw,
                                         const WxLane& xl, int q, XiRing& r, f32x16 (&acc)[16]) {
-    using GE = WGeo<16>;
+    // (GE: the W % 32 geometry or the W = 16 one)
     // q as an opaque scalar: the step's load offsets are computed here from it (two scalar
     // multiply-adds), not hoisted out of the unrolled loop as XI_NR sets of live SGPRs (spills)
     asm volatile("" : "+s"(q));
@@ -795,11 +798,11 @@ __device__ __forceinline__ void xi_step(const WrGeom& g, const WrSrc& cur, const
 
 // k-steps p + K0 + K for K in the sequence (p % XI_NR == 0).  LAST: the tile's final XI_NR
 // steps, whose loads beyond the tile's last step fetch the next tile's first steps.
-template <int H, bool FIRST, bool LAST, int K0, int... K>
+template <class GE, int H, bool FIRST, bool LAST, int K0, int... K>
 __device__ __forceinline__ void xi_steps(std::integer_sequence<int, K...>, const WrGeom& g, const WrSrc& cur,
                                          const WrSrc& nxt, __amdgpu_buffer_rsrc_t urs, int lane, float* xw,
                                          const WxLane& xl, int p, XiRing& r, f32x16 (&acc)[16]) {
-    (xi_step<H, K0 + K, FIRST && K0 + K == 0, LAST && (K0 + K + XI_DX >= XI_NR),
+    (xi_step<GE, H, K0 + K, FIRST && K0 + K == 0, LAST && (K0 + K + XI_DX >= XI_NR),
              LAST && (K0 + K + XI_DU >= XI_NR)>(g, cur, nxt, urs, lane, xw, xl, p + K0 + K, r, acc),
      ...);
 }
@@ -807,10 +810,10 @@ __device__ __forceinline__ void xi_steps(std::integer_sequence<int, K...>, const
 // Epilogue: row sums of this wave's ξ rows for both channel blocks; the block the partner
 // completes goes through LDS, the partner's rows of this wave's block come back; then the
 // output transform, bias, residual and stores as wr_epilogue (same order of operations).
-template <int H, bool RES>
+template <class GE, int H, bool RES>
 __device__ __forceinline__ void xi_epilogue(const WrGeom& g, const WrTile& ti, int wv, int lane,
                                             const f32x16 (&acc)[16], const WrRes& rv, float* ex) {
-    using GE = WGeo<16>;
+
     float* mine = ex + H * XI_EX;          // written by this wave (the partner's block)
     const float* theirs = ex + (1 - H) * XI_EX;
 #pragma unroll
@@ -865,9 +868,9 @@ __device__ __forceinline__ void xi_epilogue(const WrGeom& g, const WrTile& ti, i
     __builtin_amdgcn_s_barrier();
 }
 
-template <bool RES, int H>
+template <class GE, bool RES, int H>
 __device__ __forceinline__ void xi_body(const WrGeom& g, int wv, int lane, float* xw, float* ex) {
-    using GE = WGeo<16>;
+
     const int wq = wv & ~1;  // tile geometry of channel half 0 (the pair covers all 64 channels)
     WxLane xl;
     {
@@ -913,11 +916,11 @@ __device__ __forceinline__ void xi_body(const WrGeom& g, int wv, int lane, float
     // does not hold registers across the deep ring's whole last block
     constexpr int RES_AT = XI_NR - 2;
     for (;;) {
-        xi_steps<H, true, false, 0>(ring, g, cur, nxt, urs, lane, xw, xl, 0, r, acc);
+        xi_steps<GE, H, true, false, 0>(ring, g, cur, nxt, urs, lane, xw, xl, 0, r, acc);
         for (int p = XI_NR; p < last; p += XI_NR)
-            xi_steps<H, false, false, 0>(ring, g, cur, nxt, urs, lane, xw, xl, p, r, acc);
+            xi_steps<GE, H, false, false, 0>(ring, g, cur, nxt, urs, lane, xw, xl, p, r, acc);
         WrRes rv;
-        xi_steps<H, false, true, 0>(std::make_integer_sequence<int, RES_AT>{}, g, cur, nxt, urs, lane, xw, xl,
+        xi_steps<GE, H, false, true, 0>(std::make_integer_sequence<int, RES_AT>{}, g, cur, nxt, urs, lane, xw, xl,
                                     last, r, acc);
         if constexpr (RES) {
             WrTile tf = ti;
@@ -925,12 +928,12 @@ __device__ __forceinline__ void xi_body(const WrGeom& g, int wv, int lane, float
             wr_load_res<GE>(g, tf, wv, lane, rv);
             __builtin_amdgcn_sched_barrier(0);
         }
-        xi_steps<H, false, true, RES_AT>(std::make_integer_sequence<int, XI_NR - RES_AT>{}, g, cur, nxt, urs, lane,
+        xi_steps<GE, H, false, true, RES_AT>(std::make_integer_sequence<int, XI_NR - RES_AT>{}, g, cur, nxt, urs, lane,
                                          xw, xl, last, r, acc);
 #if SP_WINO_EXP == 6
         if (g.W < 0)  // never true at run time: no epilogue (the MFMAs stay live)
 #endif
-        xi_epilogue<H, RES>(g, ti, wv, lane, acc, rv, ex);
+        xi_epilogue<GE, H, RES>(g, ti, wv, lane, acc, rv, ex);
         t = tn;
         if (t >= g.ntiles) break;
         ti = tin;
@@ -941,17 +944,17 @@ __device__ __forceinline__ void xi_body(const WrGeom& g, int wv, int lane, float
     }
 }
 
-template <bool RES>
+template <bool RES, int TCW>
 __global__ __launch_bounds__(kBlock, 1) void k_wino3x3_xi(WrGeom g) {
-    using GE = WGeo<16>;
+    using GE = WGeo<TCW>;
     __shared__ __attribute__((aligned(16))) float xlds[4 * GE::WAVE];
     __shared__ __attribute__((aligned(16))) float exlds[2 * 2 * XI_EX];  // [pair][writer][...]
     const int lane = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     float* const xw = xlds + wv * GE::WAVE;
     float* const ex = exlds + (wv >> 1) * 2 * XI_EX;
-    if (wv & 1) xi_body<RES, 1>(g, wv, lane, xw, ex);
-    else xi_body<RES, 0>(g, wv, lane, xw, ex);
+    if (wv & 1) xi_body<GE, RES, 1>(g, wv, lane, xw, ex);
+    else xi_body<GE, RES, 0>(g, wv, lane, xw, ex);
 }
 
 // Split-K reduce: out = (((ws_0 + ws_1) + ws_2) + ...) + bias[c] (+ res), four outputs per
@@ -1117,11 +1120,18 @@ static int wino3x3(int kind, const float* x, const float* up, const float* bias,
         if (res) launch_w(kind, flops, k_wino3x3_r<true, 8, true>, gd, bd, st, g);
         else launch_w(kind, flops, k_wino3x3_r<false, 8, true>, gd, bd, st, g);
     } else if (narrow) {
+#if SP_WINO_XI16
+        if (SP_WINO_XI && cin % (2 * XI_NR) == 0 && cin >= 4 * XI_NR) {  // the ξ-split tile, W = 16
+            if (res) launch_w(kind, flops, k_wino3x3_xi<true, 8>, gd, bd, st, g);
+            else launch_w(kind, flops, k_wino3x3_xi<false, 8>, gd, bd, st, g);
+            return check_launch(what);
+        }
+#endif
         if (res) launch_w(kind, flops, k_wino3x3_r<true, 8>, gd, bd, st, g);
         else launch_w(kind, flops, k_wino3x3_r<false, 8>, gd, bd, st, g);
     } else if (SP_WINO_XI && cin % (2 * XI_NR) == 0 && cin >= 4 * XI_NR) {
-        if (res) launch_w(kind, flops, k_wino3x3_xi<true>, gd, bd, st, g);
-        else launch_w(kind, flops, k_wino3x3_xi<false>, gd, bd, st, g);
+        if (res) launch_w(kind, flops, k_wino3x3_xi<true, 16>, gd, bd, st, g);
+        else launch_w(kind, flops, k_wino3x3_xi<false, 16>, gd, bd, st, g);
     } else {
         if (res) launch_w(kind, flops, k_wino3x3_r<true, 16>, gd, bd, st, g);
         else launch_w(kind, flops, k_wino3x3_r<false, 16>, gd, bd, st, g);
