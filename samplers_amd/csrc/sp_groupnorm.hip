@@ -460,6 +460,19 @@ __device__ __forceinline__ void gnt_release_last(uint64_t* slots, int* done, int
 }
 
 // Block-reduce (a, b) as the two-pass kernels do and publish them as chunk m's words.
+// threadIdx.x re-read opaque to the compiler: values derived from it (LDS addresses, buffer
+// offsets) are then formed where they are used instead of being held live across a group —
+// in the VJP kernel (256 VGPRs: two groups' chunks and the addends in flight) such values were
+// spilled to scratch, and each reload's vmcnt(0) waited for the next group's chunk loads
+// (OPQ = false: the plain index, the forward kernels' form, which did not spill and measured
+// ~1 % faster with it)
+template <bool OPQ = true>
+__device__ __forceinline__ int gn_tid() {
+    int t = threadIdx.x;
+    if constexpr (OPQ) asm volatile("" : "+v"(t));
+    return t;
+}
+
 __device__ __forceinline__ void gnt_reduce_publish(float a, float b, float* red, uint64_t* slot) {
     a = wave_sum(a);
     b = wave_sum(b);
@@ -519,13 +532,13 @@ struct GnpBuf {  // one group's per-thread prefetch state besides the chunk itse
 // Issue the loads of group gi's chunk m and its per-channel state.  live == false: the chunk
 // loads get an empty range (no memory access, zeros) — the caller issues them anyway so that
 // the code after the prefetch has one path (see gnp_poll_finish).
-template <int PER>
+template <int PER, bool OPQ = false>
 __device__ __forceinline__ void gnp_issue(const float* __restrict__ base, const GnGeom& G,
                                           int64_t gi, uint32_t m, float (&v)[PER][4], GnpBuf& b,
                                           bool live = true) {
     const GroupCtx c = group_ctx_at<4>(base, G, gi, m);
     const auto r = gnt_rsrc(c.x, c.lo, live ? c.hi : 0u);
-    const uint32_t vo = (c.lo + threadIdx.x) * 16;
+    const uint32_t vo = (c.lo + gn_tid<OPQ>()) * 16;
 #pragma unroll
     for (int i = 0; i < PER; ++i) gnt_load(r, vo, i, v[i]);
     // every thread loads, from the input itself where a table is absent (threads t >= Cg
@@ -544,9 +557,10 @@ __device__ __forceinline__ void gnp_issue(const float* __restrict__ base, const 
 
 // Poll words of a team: every thread issues its loads (threads past the team re-read word 0),
 // so the loads precede anything issued after this call.
+template <bool OPQ = false>
 __device__ __forceinline__ void gnp_poll_issue(const uint64_t* slots, int chunks, uint64_t& wa,
                                                uint64_t& wb) {
-    const int t = threadIdx.x < chunks ? threadIdx.x : 0;
+    const int tt = gn_tid<OPQ>(), t = tt < chunks ? tt : 0;
     wa = __hip_atomic_load(slots + 2 * t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     wb = __hip_atomic_load(slots + 2 * t + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -557,11 +571,11 @@ __device__ __forceinline__ void gnp_poll_issue(const uint64_t* slots, int chunks
 // the compiler merges paths and waits for everything).  Words still absent after the poll
 // bound are recomputed by the whole workgroup with `recompute(mm, a, b)` (a block-wide call
 // that leaves chunk mm's two partials in thread 0's a, b).
-template <typename Recompute>
+template <bool OPQ = false, typename Recompute>
 __device__ __forceinline__ void gnp_poll_finish(const uint64_t* slots, int chunks, uint64_t wa,
                                                 uint64_t wb, float* sv, int* miss, float& a,
                                                 float& b, Recompute recompute) {
-    const int t = threadIdx.x;
+    const int t = gn_tid<OPQ>();
     bool ready = (wa >> 32) && (wb >> 32);
     if (t == 0) miss[GNT_MAX_CHUNKS] = 0;
     if ((t < chunks) & !ready) {
@@ -827,10 +841,10 @@ __device__ __forceinline__ void gnp_bwd_group(
         }
     }
     uint64_t wa, wb;
-    gnp_poll_issue(gslots, G.chunks, wa, wb);
+    gnp_poll_issue<true>(gslots, G.chunks, wa, wb);
     {
         const int64_t gq_i = gn >= 0 ? gn : gi;
-        gnp_issue<PER>(x, G, gq_i, m, vn, bn, gn >= 0);
+        gnp_issue<PER, true>(x, G, gq_i, m, vn, bn, gn >= 0);
         const auto rg = gnt_rsrc(Parts<const float>{dz + gq_i * (int64_t)G.gs,
                                                     dz + gq_i * (int64_t)G.gs, G.gs},
                                  c.lo, gn >= 0 ? c.hi : 0u);
@@ -838,7 +852,7 @@ __device__ __forceinline__ void gnp_bwd_group(
         for (int i = 0; i < PER; ++i) gnt_load(rg, vo, i, gq[i]);
     }
     float A, B;
-    gnp_poll_finish(gslots, G.chunks, wa, wb, sv, miss, A, B, [&](int mm, float& ra, float& rb) {
+    gnp_poll_finish<true>(gslots, G.chunks, wa, wb, sv, miss, A, B, [&](int mm, float& ra, float& rb) {
         gnp_bwd_recompute<ACT, PER>(dz, x, G, gi, static_cast<uint32_t>(mm), mean, rstd, tab, red,
                                     ra, rb);
     });
