@@ -162,6 +162,9 @@ def measure_gather(x: torch.Tensor, reps: int = 3) -> dict:
            "gathered_bytes": x.numel() * x.element_size() * world}
     if world == 1:
         return dict(rec, gather_ms=0.0, first_gather_ms=0.0, note="one rank: nothing to gather")
+    if rec["backend"] == "gloo":
+        rec["rehearsal"] = ("gloo through host memory, ranks sharing the visible GPUs: checks the "
+                            "sharded path and its gather, not a measurement of RCCL over xGMI")
     sync = torch.cuda.synchronize if x.is_cuda else (lambda: None)
     counts = [x.shape[0]] * world
     times = []
@@ -178,8 +181,11 @@ def measure_gather(x: torch.Tensor, reps: int = 3) -> dict:
         times.append(float(dt.item()) * 1e3)
     if tuple(full.shape) != (x.shape[0] * world, *x.shape[1:]):
         raise SystemExit(f"gather returned {tuple(full.shape)}")
+    rank = dist.get_rank()
+    if not torch.equal(full[rank * x.shape[0]:(rank + 1) * x.shape[0]], x):
+        raise SystemExit(f"rank {rank}: its slice of the gathered x differs from its shard")
     return dict(rec, gather_ms=round(min(times[1:]), 4), first_gather_ms=round(times[0], 4),
-                gathered_shape=list(full.shape))
+                gathered_shape=list(full.shape), own_slice_checked=True)
 
 
 def build_workload(config: str, batch: int, image: int, rank: int, device):

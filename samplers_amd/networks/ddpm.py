@@ -11,9 +11,7 @@ the UNet is called with the raw scheduler timestep, so
 
 from __future__ import annotations
 
-import json
 from dataclasses import dataclass
-from pathlib import Path
 from typing import Any
 
 import numpy as np
@@ -59,10 +57,6 @@ class DDPMSchedule:
         return self.timesteps
 
 
-_LEGACY_ATTN_KEYS = {".query.": ".to_q.", ".key.": ".to_k.", ".value.": ".to_v.",
-                     ".proj_attn.": ".to_out.0."}
-
-
 class DDPMNetwork(EpsilonNetwork[NoCondition]):
     """ε-network over a pixel-space UNet and a DDPM schedule."""
 
@@ -92,21 +86,13 @@ class DDPMNetwork(EpsilonNetwork[NoCondition]):
         ``unet/config.json`` and ``scheduler/scheduler_config.json``).  Nothing
         is downloaded: a hub name without a local copy raises ``FileNotFoundError``.
         """
-        root = Path(pretrained_model_name_or_path)
-        if cache_dir is not None and not root.exists():
-            root = Path(cache_dir) / pretrained_model_name_or_path
-        weights = root / "unet" / "diffusion_pytorch_model.safetensors"
-        if not weights.exists():
-            raise FileNotFoundError(
-                f"no local checkpoint at {weights}; this build never fetches weights "
-                "(use DDPMNetwork.from_config for a random-weight prior)"
-            )
-        from safetensors.torch import load_file
+        from .checkpoint import load_state, meta_module, read_json, resolve_root, weights_path
 
+        root = resolve_root(pretrained_model_name_or_path, cache_dir, ("unet",),
+                            pipeline_kwargs.get("variant"), "DDPMNetwork.from_config")
         config = CELEBAHQ_256
-        cfg_path = root / "unet" / "config.json"
-        if cfg_path.exists():
-            raw = json.loads(cfg_path.read_text())
+        raw = read_json(root / "unet" / "config.json")
+        if raw:
             attn = tuple(i for i, t in enumerate(raw.get("down_block_types", [])) if "Attn" in t)
             config = UNet2DConfig(
                 sample_size=raw.get("sample_size", 256),
@@ -122,24 +108,18 @@ class DDPMNetwork(EpsilonNetwork[NoCondition]):
                 attention_head_dim=raw.get("attention_head_dim"),
             )
         schedule = DDPMSchedule()
-        sch_path = root / "scheduler" / "scheduler_config.json"
-        if sch_path.exists():
-            raw = json.loads(sch_path.read_text())
+        raw = read_json(root / "scheduler" / "scheduler_config.json")
+        if raw:
             schedule = DDPMSchedule(
                 num_train_timesteps=raw.get("num_train_timesteps", 1000),
                 beta_start=raw.get("beta_start", 1e-4), beta_end=raw.get("beta_end", 0.02),
                 beta_schedule=raw.get("beta_schedule", "linear"),
                 steps_offset=raw.get("steps_offset", 0),
             )
-        unet = UNet2DModel(config)
-        state = load_file(str(weights))
-        fixed = {}
-        for k, v in state.items():
-            for old, new in _LEGACY_ATTN_KEYS.items():
-                k = k.replace(old, new)
-            fixed[k] = v
-        unet.load_state_dict(fixed)
-        unet = unet.to(device=device, dtype=torch_dtype or torch.float32)
+        unet = meta_module(UNet2DModel, config)
+        load_state(unet, weights_path(root, "unet", pipeline_kwargs.get("variant")),
+                   dtype=torch_dtype or torch.float32)
+        unet = unet.to(device=device)
         return cls(unet, schedule)
 
     def forward(self, sample: Tensor, t: Tensor | int) -> Tensor:

@@ -133,8 +133,42 @@ class LatentDiffusionNetwork(LatentEpsilonNetwork[StableDiffusionCondition]):
         return cls(unet, build_vae(vae_config, seed=seed + 1, device=device, dtype=dt))
 
     @classmethod
-    def from_pretrained(cls, *args, **kwargs):
-        raise NotImplementedError("no offline Stable Diffusion checkpoint; use from_config")
+    def from_pretrained(cls, pretrained_model_name_or_path: str, cache_dir: str | None = None,
+                        torch_dtype: DType = None, device: Device = None, *,
+                        variant: str | None = None, null_prompt_embeds: Tensor | None = None,
+                        **pipeline_kwargs: Any) -> "LatentDiffusionNetwork":
+        """Load a diffusers-layout Stable Diffusion checkpoint from a LOCAL directory
+        (``stable_diffusion.py:89-105`` loads the pipeline by hub name).
+
+        Reads ``unet/`` and ``vae/`` (``diffusion_pytorch_model[.variant].safetensors`` +
+        ``config.json``) and ``scheduler/scheduler_config.json`` (PNDM with
+        ``skip_prk_steps``, DDIM or DDPM, ``leading`` spacing); nothing is downloaded, so a hub
+        name without a local copy raises ``FileNotFoundError``.  The text encoder is not read
+        (out of scope, module doc): conditions come as ``prompt_embeds``, and the empty prompt
+        maps to ``null_prompt_embeds`` — the caller's CLIP embedding of ``""`` (1 x 77 x 768),
+        else the synthetic null context.  Weights are computed in fp32 unless ``torch_dtype``
+        says otherwise (fp16 variants are upcast)."""
+        from .checkpoint import load_state, meta_module, read_json, resolve_root, weights_path
+
+        root = resolve_root(pretrained_model_name_or_path, cache_dir, ("unet", "vae"), variant,
+                            "LatentDiffusionNetwork.from_config")
+        dt = torch_dtype or torch.float32
+        unet_config = unet_condition_config_from_json(read_json(root / "unet" / "config.json"))
+        vae_config = vae_config_from_json(read_json(root / "vae" / "config.json"))
+        schedule, pndm = schedule_from_json(read_json(root / "scheduler" / "scheduler_config.json"))
+        unet = meta_module(UNet2DConditionModel, unet_config)
+        load_state(unet, weights_path(root, "unet", variant), dtype=dt)
+        vae = meta_module(AutoencoderKL, vae_config)
+        load_state(vae, weights_path(root, "vae", variant), dtype=dt)
+        net = cls(unet.to(device=device), vae.to(device=device), schedule=schedule, pndm=pndm)
+        if null_prompt_embeds is not None:
+            want = tuple(net.null_prompt_embeds.shape)
+            if tuple(null_prompt_embeds.shape[-2:]) != want[-2:]:
+                raise ValueError(f"null_prompt_embeds: expected (1, {want[1]}, {want[2]}), "
+                                 f"got {tuple(null_prompt_embeds.shape)}")
+            net.null_prompt_embeds = null_prompt_embeds.reshape(want).to(
+                device=net.null_prompt_embeds.device, dtype=dt)
+        return net
 
     # -- conditioning --------------------------------------------------------------------
 
@@ -263,3 +297,107 @@ class LatentDiffusionNetwork(LatentEpsilonNetwork[StableDiffusionCondition]):
         super().to(*args, **kwargs)
         self._acp_host = None
         return self
+
+
+# ---------------------------------------------------------------------------------------------
+# diffusers config.json -> this build's configs (from_pretrained)
+# ---------------------------------------------------------------------------------------------
+
+def _only(raw: dict, key: str, allowed, what: str) -> None:
+    if key in raw and raw[key] not in allowed:
+        raise NotImplementedError(f"{what}: {key}={raw[key]!r} is not supported (supported: {allowed})")
+
+
+def unet_condition_config_from_json(raw: dict) -> UNet2DConditionConfig:
+    """diffusers ``UNet2DConditionModel`` config -> ``UNet2DConditionConfig`` (SD 1.x layout:
+    CrossAttnDownBlock2D levels, conv ``proj_in`` / ``proj_out``, one head count).  Missing keys
+    take SD 1.5's values; other architectures raise ``NotImplementedError``."""
+    d = SD15_UNET
+    if not raw:
+        return d
+    what = "unet/config.json"
+    _only(raw, "act_fn", ("silu",), what)
+    _only(raw, "use_linear_projection", (False,), what)
+    _only(raw, "center_input_sample", (False,), what)
+    _only(raw, "mid_block_type", ("UNetMidBlock2DCrossAttn", None), what)
+    _only(raw, "class_embed_type", (None,), what)
+    _only(raw, "addition_embed_type", (None,), what)
+    _only(raw, "upcast_attention", (False, None), what)
+    _only(raw, "time_embedding_type", ("positional",), what)
+    for key in ("transformer_layers_per_block", "layers_per_block", "cross_attention_dim"):
+        if isinstance(raw.get(key), (list, tuple)):
+            raise NotImplementedError(f"{what}: per-level {key} is not supported")
+    heads = raw.get("num_attention_heads") or raw.get("attention_head_dim", d.attention_heads)
+    if isinstance(heads, (list, tuple)):
+        if len(set(heads)) != 1:
+            raise NotImplementedError(f"{what}: per-level head counts {heads} are not supported")
+        heads = heads[0]
+    down = raw.get("down_block_types")
+    levels = d.cross_attention_levels
+    if down is not None:
+        levels = tuple(i for i, t in enumerate(down) if t.startswith("CrossAttn"))
+        up = raw.get("up_block_types")
+        if up is not None and tuple(i for i, t in enumerate(reversed(up)) if t.startswith("CrossAttn")) != levels:
+            raise NotImplementedError(f"{what}: up blocks do not mirror the down blocks")
+    return UNet2DConditionConfig(
+        sample_size=raw.get("sample_size", d.sample_size),
+        in_channels=raw.get("in_channels", d.in_channels),
+        out_channels=raw.get("out_channels", d.out_channels),
+        block_out_channels=tuple(raw.get("block_out_channels", d.block_out_channels)),
+        cross_attention_levels=levels,
+        layers_per_block=raw.get("layers_per_block", d.layers_per_block),
+        attention_heads=int(heads),
+        cross_attention_dim=raw.get("cross_attention_dim", d.cross_attention_dim),
+        norm_num_groups=raw.get("norm_num_groups", d.norm_num_groups),
+        norm_eps=raw.get("norm_eps", d.norm_eps),
+        flip_sin_to_cos=raw.get("flip_sin_to_cos", d.flip_sin_to_cos),
+        freq_shift=raw.get("freq_shift", d.freq_shift),
+    )
+
+
+def vae_config_from_json(raw: dict) -> VAEConfig:
+    """diffusers ``AutoencoderKL`` config -> ``VAEConfig`` (missing keys: SD 1.5's)."""
+    d = SD15_VAE
+    if not raw:
+        return d
+    _only(raw, "act_fn", ("silu",), "vae/config.json")
+    _only(raw, "use_quant_conv", (True,), "vae/config.json")
+    _only(raw, "use_post_quant_conv", (True,), "vae/config.json")
+    return VAEConfig(
+        in_channels=raw.get("in_channels", d.in_channels),
+        out_channels=raw.get("out_channels", d.out_channels),
+        latent_channels=raw.get("latent_channels", d.latent_channels),
+        block_out_channels=tuple(raw.get("block_out_channels", d.block_out_channels)),
+        layers_per_block=raw.get("layers_per_block", d.layers_per_block),
+        norm_num_groups=raw.get("norm_num_groups", d.norm_num_groups),
+        norm_eps=raw.get("norm_eps", d.norm_eps),
+        scaling_factor=raw.get("scaling_factor") or d.scaling_factor,
+    )
+
+
+def schedule_from_json(raw: dict) -> tuple[DDPMSchedule, bool]:
+    """``scheduler_config.json`` -> (schedule, pndm).  The reference's pipeline keeps its own
+    scheduler (SD 1.5 ships ``PNDMScheduler(skip_prk_steps=True)``); its ``alphas_cumprod``
+    and timestep list are what the samplers read (``stable_diffusion.py:72-75, 130-133``).
+    Supported: PNDM with ``skip_prk_steps``, DDIM and DDPM, ``leading`` spacing, epsilon
+    prediction."""
+    if not raw:
+        return DDPMSchedule(beta_start=0.00085, beta_end=0.012, beta_schedule="scaled_linear",
+                            steps_offset=1), True
+    what = "scheduler/scheduler_config.json"
+    cls = raw.get("_class_name", "PNDMScheduler")
+    if cls not in ("PNDMScheduler", "DDIMScheduler", "DDPMScheduler"):
+        raise NotImplementedError(f"{what}: {cls} is not supported")
+    _only(raw, "prediction_type", ("epsilon",), what)
+    _only(raw, "timestep_spacing", ("leading",), what)
+    if raw.get("trained_betas") is not None:
+        raise NotImplementedError(f"{what}: trained_betas are not supported")
+    pndm = cls == "PNDMScheduler"
+    if pndm and not raw.get("skip_prk_steps", False):
+        raise NotImplementedError(f"{what}: PNDM with Runge-Kutta warm-up steps is not supported")
+    schedule = DDPMSchedule(num_train_timesteps=raw.get("num_train_timesteps", 1000),
+                            beta_start=raw.get("beta_start", 0.00085),
+                            beta_end=raw.get("beta_end", 0.012),
+                            beta_schedule=raw.get("beta_schedule", "scaled_linear"),
+                            steps_offset=raw.get("steps_offset", 0))
+    return schedule, pndm

@@ -18,6 +18,7 @@ import torch.nn.functional as F
 from torch import Tensor, nn
 
 from .. import _hip
+from ..runtime import split_k_enabled
 
 
 def group_norm_act_torch(x: Tensor, groups: int, weight: Tensor | None, bias: Tensor | None,
@@ -266,7 +267,7 @@ def _wino_workspace(lib, n: int, cin: int, cout: int, h: int, w: int, device) ->
     """A workspace for the Winograd tile's split-K parts, or None when the shape fills the
     chip unsplit (sp_wino3x3_workspace).  From torch's caching allocator on the launch
     stream, so a graph capture records it and a later reuse is ordered after the launch."""
-    nb = _query("sp_wino3x3_workspace", n, cin, cout, h, w)
+    nb = _query("sp_wino3x3_workspace", n, cin, cout, h, w) if split_k_enabled() else 0
     if nb <= 0:
         return None
     return torch.empty(nb // 4, device=device, dtype=torch.float32)
@@ -277,7 +278,7 @@ def x6_workspace(lib, n: int, hw: int, k: int, m: int, device) -> tuple[Tensor |
     n images of hw pixels, or n = 1 and hw = tokens), and its size in bytes; (None, 0) when the
     launch fills the chip unsplit.  Torch's caching allocator on the launch stream, as
     _wino_workspace; the caller holds it until the launch is queued."""
-    nb = _query("sp_gemm_x6_workspace", n, hw, k, m)
+    nb = _query("sp_gemm_x6_workspace", n, hw, k, m) if split_k_enabled() else 0
     if nb <= 0:
         return None, 0
     return torch.empty(nb // 4, device=device, dtype=torch.float32), nb
@@ -473,7 +474,7 @@ class SkipGrad:
 def _s2_workspace(lib, n: int, cin: int, cout: int, h: int, w: int, vjp: int, device) -> tuple[Tensor | None, int]:
     """The stride-2 tile's split-K workspace for an under-filled launch (sp_conv3x3_s2_workspace)
     and its bytes, or (None, 0); allocated as _wino_workspace."""
-    nb = _query("sp_conv3x3_s2_workspace", n, cin, cout, h, w, vjp)
+    nb = _query("sp_conv3x3_s2_workspace", n, cin, cout, h, w, vjp) if split_k_enabled() else 0
     if nb <= 0:
         return None, 0
     return torch.empty(nb // 4, device=device, dtype=torch.float32), nb

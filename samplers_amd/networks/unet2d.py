@@ -29,6 +29,7 @@ import torch.nn.functional as F
 from torch import Tensor, nn
 
 from .. import _hip
+from ..runtime import batch_invariant_enabled
 from .layers import (Conv3x3, GroupNormAct, Linear, SkipGrad, conv3x3_forward, conv3x3_input_vjp,
                      downsample_conv, gn_backward, gn_forward, miopen_fallback, proj_nchw_to_tokens,
                      proj_tokens_to_nchw, upsample_nearest2x, x6_enough_tiles, x6_workspace, _query)
@@ -74,8 +75,9 @@ def temb_projections(model: nn.Module, emb: Tensor) -> dict[int, Tensor]:
     blocks = [m for m in model.modules() if isinstance(m, ResnetBlock2D) and m.time_emb_proj is not None]
     if not blocks or any(p.requires_grad for b in blocks for p in b.time_emb_proj.parameters()):
         return {}
-    key = (emb.device, emb.dtype, tuple((id(b.time_emb_proj.weight), b.time_emb_proj.weight._version,
-                                         b.time_emb_proj.bias._version) for b in blocks))
+    key = (emb.device, emb.dtype, tuple((b.time_emb_proj.weight.data_ptr(), b.time_emb_proj.weight._version,
+                                         b.time_emb_proj.bias.data_ptr(), b.time_emb_proj.bias._version)
+                                        for b in blocks))
     cache = model.__dict__.setdefault("_temb_stacks", {})
     if cache.get("key") != key:
         groups: dict[int, list] = {}
@@ -347,11 +349,27 @@ def _score_chunks(b: int, n: int, m: int) -> int:
     return 4 if b >= 32 else 8
 
 
+def bmm(a: Tensor, bm: Tensor, out: Tensor | None = None) -> Tensor:
+    """``torch.bmm``; in batch-invariant mode (``runtime.batch_invariant``) one GEMM per batch
+    entry, so hipBLASLt's algorithm (and summation order) does not follow the batch count."""
+    if not batch_invariant_enabled() or a.shape[0] == 1:
+        return torch.bmm(a, bm) if out is None else torch.bmm(a, bm, out=out)
+    if out is None:
+        out = torch.empty(a.shape[0], a.shape[1], bm.shape[2], device=a.device, dtype=a.dtype)
+    for i in range(a.shape[0]):
+        torch.bmm(a[i:i + 1], bm[i:i + 1], out=out[i:i + 1])
+    return out
+
+
 def score_gemm(a: Tensor, bm: Tensor, alpha: float, out: Tensor) -> Tensor:
     """out[i] = alpha · a[i] bm[i]ᵀ for a (b, n, d), bm (b, m, d) (strided views allowed),
     out (b, n, m) contiguous; query rows chunked where that fills the chip (``_score_chunks``)."""
     b, n, d = a.shape
     m = bm.shape[1]
+    if batch_invariant_enabled() and b > 1:  # one batch entry per GEMM (``bmm``)
+        for i in range(b):
+            score_gemm(a[i:i + 1], bm[i:i + 1], alpha, out[i:i + 1])
+        return out
     ch = _score_chunks(b, n, m)
     if ch == 1:
         return torch.baddbmm(out, a, bm.transpose(1, 2), beta=0.0, alpha=alpha, out=out)
@@ -379,7 +397,7 @@ class _ScoreAttentionQKV(torch.autograd.Function):
         _hip.check(lib.sp_softmax_rows(_hip.ptr(p), b * n, n, None, _hip.stream_of(p)), "sp_softmax_rows")
         ctx.save_for_backward(qkv, p)
         ctx.scale = scale
-        return torch.bmm(p, v)
+        return bmm(p, v)
 
     @staticmethod
     def backward(ctx, dout: Tensor):
@@ -390,12 +408,12 @@ class _ScoreAttentionQKV(torch.autograd.Function):
         q, k, v = qkv.split(c, dim=-1)
         dqkv = torch.empty_like(qkv)
         dq, dk, dv = dqkv.split(c, dim=-1)
-        torch.bmm(p.transpose(1, 2), dout, out=dv)
+        bmm(p.transpose(1, 2), dout, out=dv)
         ds = score_gemm(dout, v, 1.0, torch.empty(b, n, n, device=qkv.device, dtype=qkv.dtype))
         _hip.check(lib.sp_softmax_bwd_rows(_hip.ptr(p), _hip.ptr(ds), b * n, n, ctx.scale, _hip.stream_of(ds)),
                    "sp_softmax_bwd_rows")
-        torch.bmm(ds, k, out=dq)
-        torch.bmm(ds.transpose(1, 2), q, out=dk)
+        bmm(ds, k, out=dq)
+        bmm(ds.transpose(1, 2), q, out=dk)
         return dqkv
 
 
@@ -415,7 +433,7 @@ class _ScoreAttention(torch.autograd.Function):
         _hip.check(lib.sp_softmax_rows(_hip.ptr(p), bh * n, m, None, _hip.stream_of(p)), "sp_softmax_rows")
         ctx.save_for_backward(q, k, v, p)
         ctx.scale = scale
-        return torch.bmm(p, v)
+        return bmm(p, v)
 
     @staticmethod
     def backward(ctx, dout: Tensor):
@@ -423,14 +441,14 @@ class _ScoreAttention(torch.autograd.Function):
         lib = _hip.load_library()
         bh, n, m = p.shape
         need_q, need_k, need_v = ctx.needs_input_grad[:3]
-        dv = torch.bmm(p.transpose(1, 2), dout) if need_v else None
+        dv = bmm(p.transpose(1, 2), dout) if need_v else None
         dq = dk = None
         if need_q or need_k:
             ds = score_gemm(dout, v, 1.0, torch.empty(bh, n, m, device=dout.device, dtype=dout.dtype))
             _hip.check(lib.sp_softmax_bwd_rows(_hip.ptr(p), _hip.ptr(ds), bh * n, m, ctx.scale,
                                                _hip.stream_of(ds)), "sp_softmax_bwd_rows")
-            dq = torch.bmm(ds, k) if need_q else None
-            dk = torch.bmm(ds.transpose(1, 2), q) if need_k else None
+            dq = bmm(ds, k) if need_q else None
+            dk = bmm(ds.transpose(1, 2), q) if need_k else None
         return dq, dk, dv
 
 

@@ -18,11 +18,71 @@ its handle, at the first MIOpen convolution), not at import.
 
 from __future__ import annotations
 
+import contextlib
 import os
 from pathlib import Path
 
 PACKAGE = Path(__file__).resolve().parent
 SEED_DB = PACKAGE / "miopen_db"
+
+# Batch-dependent kernel choices.  Split-K (§3 "Round 4"): a launch whose tiles
+# leave CUs idle cuts K into parts and adds them in a fixed order; the parts are chosen per
+# launch from its tile count.  hipBLASLt (the d = 512 attention's score / value GEMMs) picks its
+# algorithm per problem size, batch count included.  So the same sample is summed in a different
+# order at a different batch size (micro_batch, world size) and agrees to fp32 rounding only.
+# ``batch_invariant(True)`` removes both: every launch unsplit and those GEMMs issued one batch
+# entry at a time, so a sharded or micro-batched solve is bitwise the single-process one.
+def _env_on(name: str, default: str) -> bool:
+    return os.environ.get(name, default).lower() not in ("0", "off", "false", "")
+
+
+_FLAGS = {"split_k": _env_on("SAMPLERS_AMD_SPLIT_K", "1"),
+          "batch_invariant": _env_on("SAMPLERS_AMD_BATCH_INVARIANT", "0")}
+
+
+def split_k_enabled() -> bool:
+    return _FLAGS["split_k"] and not _FLAGS["batch_invariant"]
+
+
+def batch_invariant_enabled() -> bool:
+    return _FLAGS["batch_invariant"]
+
+
+def _set(flag: str, enabled: bool) -> bool:
+    prev = _FLAGS[flag]
+    _FLAGS[flag] = bool(enabled)
+    return prev
+
+
+def set_split_k(enabled: bool) -> bool:
+    """Enable / disable split-K for under-filled launches; returns the previous setting."""
+    return _set("split_k", enabled)
+
+
+def set_batch_invariant(enabled: bool) -> bool:
+    """Batch-invariant summation order for every launch (module comment); returns the previous
+    setting."""
+    return _set("batch_invariant", enabled)
+
+
+@contextlib.contextmanager
+def split_k(enabled: bool):
+    """``with split_k(False): ...`` — no split-K launches inside the block."""
+    prev = set_split_k(enabled)
+    try:
+        yield
+    finally:
+        set_split_k(prev)
+
+
+@contextlib.contextmanager
+def batch_invariant(enabled: bool = True):
+    """``with batch_invariant(): ...`` — results independent of the batch a sample is in."""
+    prev = set_batch_invariant(enabled)
+    try:
+        yield
+    finally:
+        set_batch_invariant(prev)
 
 
 def _writable_cache_dir() -> Path:

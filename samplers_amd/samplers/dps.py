@@ -447,6 +447,9 @@ class DPSSampler(PosteriorSampler, Generic[Condition_co]):
                     raise ValueError("graph=True needs natively implemented plugins")
                 if noise_fn is not None or rng != "philox":
                     raise ValueError("graph=True needs the in-kernel Philox noise (rng='philox')")
+                if callback is not None:
+                    raise ValueError("graph=True replays the steps without returning to the host: "
+                                     "no per-iteration callback")
                 from .graph import GraphedStepLoop, schedule_for
 
                 GraphedStepLoop(step, x, schedule_for(ts), seed=seed,

@@ -170,26 +170,39 @@ def _is_gaussian(noise) -> bool:
         c.__name__ == "GaussianNoise" for c in type(noise).__mro__)
 
 
+_NOT_RUN = -1.0  # loss-log entry of an iteration the stopping rule skipped (losses are >= 0)
+
+
 def _loss_log(max_iters: int, device) -> Tensor:
     """Per-iteration losses of one hard-consistency solve, written by the device check
-    (``loss_out``); a check after the stop writes nothing, so the entries left NaN count the
-    iterations the stopping rule skipped."""
-    return torch.full((max(max_iters, 1),), float("nan"), device=device)
+    (``loss_out``); a check after the stop writes nothing, so the entries left at ``_NOT_RUN``
+    count the iterations the stopping rule skipped (a loss that genuinely went inf / NaN is
+    still counted as run)."""
+    return torch.full((max(max_iters, 1),), _NOT_RUN, device=device)
 
 
 def _log_solve(owner, kind: str, losses: Tensor, trips: int, max_iters: int) -> None:
-    """Append one solve's record to ``owner.optimization_log`` (the sampler's; reset per
-    ``__call__``; nothing when there is no owner): the iterations the reference's stopping rule
-    ran (``resample_kernels.py:32-93``), the host loop's trips (a few more: the flag is read
-    late), the final loss."""
+    """Queue one solve's record for ``owner.optimization_log`` (the sampler's; reset per
+    ``__call__``; nothing when there is no owner).  No host sync here: the device loss log is
+    kept and read once, at the end of the call (``_finish_log``)."""
     if owner is None:
         return
-    done = losses[:max(trips, 0)]
-    ran = int(torch.isfinite(done).sum())
-    last = float(done[ran - 1]) if ran else float("nan")
-    owner.__dict__.setdefault("optimization_log", []).append(
-        {"kind": kind, "iterations": ran, "host_trips": trips, "max_iters": max_iters,
-         "stopped_early": ran < max_iters, "final_loss": last})
+    owner.__dict__.setdefault("_pending_log", []).append((kind, losses, trips, max_iters))
+
+
+def _finish_log(owner) -> None:
+    """Turn the queued solves into ``optimization_log`` records: the iterations the reference's
+    stopping rule ran (``resample_kernels.py:32-93``), the host loop's trips (``loop_trips``: a
+    few more than ran, since the flag is read late — not host synchronisations), the final
+    loss."""
+    pending = owner.__dict__.pop("_pending_log", [])
+    log = owner.__dict__.setdefault("optimization_log", [])
+    for kind, losses, trips, max_iters in pending:
+        done = losses[:max(trips, 0)].cpu()
+        ran = int((done != _NOT_RUN).sum())
+        last = float(done[ran - 1]) if ran else float("nan")
+        log.append({"kind": kind, "iterations": ran, "loop_trips": trips, "max_iters": max_iters,
+                    "stopped_early": ran < max_iters, "final_loss": last})
 
 
 def make_consistency(operator, y_rows: Tensor, y_div: int, group=None) -> _Consistency:
@@ -380,6 +393,7 @@ class ReSampleSampler(PosteriorSampler, Generic[Condition_co]):
         ``optimization_log`` lists every hard-consistency solve of the call (pixel / latent,
         the AdamW iterations the stopping rules ran, the final loss)."""
         self.optimization_log = []
+        self._pending_log = []
         x_shape: Shape = inverse_problem.operator.x_shape
         batch_shape: Shape = inverse_problem.batch_shape
         x_view = BatchView(batch_shape, num_reconstructions, x_shape)
@@ -451,6 +465,7 @@ class ReSampleSampler(PosteriorSampler, Generic[Condition_co]):
                     z = self._resample(z_opt, snapshot, float(a_prev), sigma,
                                        draw("resample", key, z_opt), seed, key, off)
             final_z0 = self._latent_optimization(z, cons, total, eps, max_optimization_iters)
+            _finish_log(self)
             if decode_output:
                 return self._as_output(x_view.unflatten(net.decode(final_z0, differentiable=False)))
             return self._as_output(z_view.unflatten(final_z0))

@@ -235,7 +235,7 @@ def test_pixel_optimization_device_stop_matches_reference_loop(cuda, kind):
     the threshold is placed between two consecutive losses of the reference, at an
     iteration that is not a multiple of the host's flag-check interval."""
     from samplers_amd.operators import GaussianBlurOperator, get_mask_random
-    from samplers_amd.samplers.resample import ReSampleSampler, _Consistency
+    from samplers_amd.samplers.resample import ReSampleSampler, _Consistency, _finish_log
 
     torch.manual_seed(0)
     shape, b = (3, 16, 24), 2
@@ -276,6 +276,7 @@ def test_pixel_optimization_device_stop_matches_reference_loop(cuda, kind):
     holder = types.SimpleNamespace()  # stands in for the sampler: receives the solve's record
     out = ReSampleSampler._pixel_optimization(holder, x0.to(cuda), cons, total, thr ** 0.5, 2000)
     err = float((out.cpu() - ref).norm() / ref.norm())
+    _finish_log(holder)  # the sampler reads the queued loss logs once, at the end of its call
     (rec,) = holder.optimization_log  # the iterations the stopping rule ran, from the device
     assert rec["kind"] == "pixel" and rec["iterations"] == stop_at + 1 and rec["stopped_early"]
     assert abs(rec["final_loss"] - ref_losses[-1]) <= 1e-5 * abs(ref_losses[-1])

@@ -1,6 +1,7 @@
 """Prior modules on the CPU: architecture sizes, diffusers-compatible parameter names, the
 fused-norm layer's CPU semantics."""
 
+import pytest
 import torch
 
 from samplers_amd.networks.layers import GroupNormAct, Linear, linear
@@ -158,3 +159,99 @@ def test_score_gemm_chunks_equal_plain_bmm():
         out = torch.empty(b, n, n)
         score_gemm(q, k, 0.25, out)
         torch.testing.assert_close(out, 0.25 * q @ k.transpose(1, 2), rtol=1e-5, atol=1e-5)
+
+
+def _tiny_sd_dir(tmp_path, legacy_vae: bool):
+    """A diffusers-layout SD directory with a tiny UNet2DConditionModel + AutoencoderKL, key
+    names as diffusers writes them (``legacy_vae``: the VAE attention under the pre-0.14 names
+    query / key / value / proj_attn with 1x1-conv-shaped weights, as older exports store it)."""
+    import json
+
+    from safetensors.torch import save_file
+
+    from samplers_amd.networks.latent import LatentDiffusionNetwork
+    from samplers_amd.networks.unet2d_condition import UNet2DConditionConfig
+    from samplers_amd.networks.vae import VAEConfig
+
+    ucfg = UNet2DConditionConfig(sample_size=8, block_out_channels=(32, 64), cross_attention_levels=(0,),
+                                 layers_per_block=1, attention_heads=2, cross_attention_dim=24,
+                                 norm_num_groups=8)
+    vcfg = VAEConfig(block_out_channels=(16, 32), layers_per_block=1, norm_num_groups=8)
+    src = LatentDiffusionNetwork.from_config(ucfg, vcfg, seed=5)
+    for comp, mod in (("unet", src.unet), ("vae", src.vae)):
+        (tmp_path / comp).mkdir()
+        state = {}
+        for k, v in mod.state_dict().items():
+            if comp == "vae" and legacy_vae and ".attentions." in k:
+                k = (k.replace(".to_q.", ".query.").replace(".to_k.", ".key.")
+                     .replace(".to_v.", ".value.").replace(".to_out.0.", ".proj_attn."))
+                if v.dim() == 2:
+                    v = v[:, :, None, None]
+            state[k] = v.contiguous()
+        save_file(state, str(tmp_path / comp / "diffusion_pytorch_model.safetensors"))
+    (tmp_path / "unet" / "config.json").write_text(json.dumps({
+        "_class_name": "UNet2DConditionModel", "act_fn": "silu", "attention_head_dim": 2,
+        "block_out_channels": [32, 64], "center_input_sample": False, "cross_attention_dim": 24,
+        "down_block_types": ["CrossAttnDownBlock2D", "DownBlock2D"], "flip_sin_to_cos": True,
+        "freq_shift": 0, "in_channels": 4, "layers_per_block": 1, "norm_eps": 1e-5,
+        "norm_num_groups": 8, "out_channels": 4, "sample_size": 8,
+        "up_block_types": ["UpBlock2D", "CrossAttnUpBlock2D"]}))
+    (tmp_path / "vae" / "config.json").write_text(json.dumps({
+        "_class_name": "AutoencoderKL", "act_fn": "silu", "block_out_channels": [16, 32],
+        "in_channels": 3, "latent_channels": 4, "layers_per_block": 1, "norm_num_groups": 8,
+        "out_channels": 3, "sample_size": 16}))
+    (tmp_path / "scheduler").mkdir()
+    (tmp_path / "scheduler" / "scheduler_config.json").write_text(json.dumps({
+        "_class_name": "PNDMScheduler", "beta_end": 0.012, "beta_schedule": "scaled_linear",
+        "beta_start": 0.00085, "num_train_timesteps": 1000, "set_alpha_to_one": False,
+        "skip_prk_steps": True, "steps_offset": 1, "trained_betas": None}))
+    return src, ucfg
+
+
+@pytest.mark.parametrize("legacy_vae", [False, True])
+def test_sd_from_pretrained_loads_a_local_diffusers_layout_checkpoint(tmp_path, legacy_vae):
+    """f4 (stable_diffusion.py:89-105 loads the pipeline by hub name): ``unet/``, ``vae/`` and
+    ``scheduler/`` of a local diffusers-layout directory round-trip to the same modules, ε,
+    decode and encode, and the PNDM timestep list."""
+    from samplers_amd.networks.latent import LatentDiffusionNetwork, StableDiffusionCondition
+
+    src, ucfg = _tiny_sd_dir(tmp_path, legacy_vae)
+    ctx = torch.randn(1, ucfg.context_tokens, 24, generator=torch.Generator().manual_seed(3))
+    net = LatentDiffusionNetwork.from_pretrained(str(tmp_path), null_prompt_embeds=ctx)
+    for a, b in ((src.unet, net.unet), (src.vae, net.vae)):
+        sa, sb = a.state_dict(), b.state_dict()
+        assert list(sa) == list(sb)
+        for k in sa:
+            assert torch.equal(sa[k], sb[k]), k
+    assert torch.equal(net.alphas_cumprod, src.alphas_cumprod)
+    assert torch.equal(net.null_prompt_embeds, ctx)
+    src.null_prompt_embeds = ctx.clone()
+    g = torch.Generator().manual_seed(4)
+    z = torch.randn(2, 4, 8, 8, generator=g)
+    x = torch.rand(2, 3, 16, 16, generator=g) * 2 - 1
+    for m in (src, net):
+        m.set_sampling_parameters(10, batch_size=1)
+        m.set_condition(StableDiffusionCondition())
+    with torch.no_grad():
+        assert torch.equal(net(z, 501), src(z, 501))
+        assert torch.equal(net.decode(z), src.decode(z))
+        assert torch.equal(net.encode(x), src.encode(x))
+    assert net.timesteps_host == src.timesteps_host
+
+
+def test_sd_from_pretrained_never_fetches_and_rejects_unsupported(tmp_path):
+    import json
+
+    from samplers_amd.networks.latent import LatentDiffusionNetwork
+
+    with pytest.raises(FileNotFoundError, match="never fetches"):
+        LatentDiffusionNetwork.from_pretrained("runwayml/stable-diffusion-v1-5", cache_dir=str(tmp_path))
+    _tiny_sd_dir(tmp_path, False)
+    sch = tmp_path / "scheduler" / "scheduler_config.json"
+    raw = json.loads(sch.read_text())
+    sch.write_text(json.dumps(dict(raw, skip_prk_steps=False)))
+    with pytest.raises(NotImplementedError, match="Runge-Kutta"):
+        LatentDiffusionNetwork.from_pretrained(str(tmp_path))
+    sch.write_text(json.dumps(dict(raw, prediction_type="v_prediction")))
+    with pytest.raises(NotImplementedError, match="prediction_type"):
+        LatentDiffusionNetwork.from_pretrained(str(tmp_path))

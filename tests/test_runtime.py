@@ -24,3 +24,37 @@ def test_find_db_seed_copy(tmp_path: Path):
     dst = tmp_path / src.name
     runtime._merge_find_db(src, dst)
     assert dst.read_text().splitlines() == [l for l in src.read_text().splitlines() if "=" in l]
+
+
+def test_batch_invariant_mode_turns_split_k_off_and_restores():
+    """runtime.batch_invariant / split_k: split-K is off inside either block, the
+    previous settings come back after it, and the split-K workspace helpers then hand out no
+    workspace (so no launch is split) without asking the library."""
+    from samplers_amd import runtime
+    from samplers_amd.networks import layers
+
+    assert runtime.split_k_enabled() and not runtime.batch_invariant_enabled()
+    with runtime.batch_invariant():
+        assert runtime.batch_invariant_enabled() and not runtime.split_k_enabled()
+        assert layers._wino_workspace(None, 1, 128, 128, 8, 8, "cpu") is None
+        assert layers.x6_workspace(None, 1, 64, 128, 128, "cpu") == (None, 0)
+        assert layers._s2_workspace(None, 1, 128, 128, 16, 16, 0, "cpu") == (None, 0)
+    assert runtime.split_k_enabled() and not runtime.batch_invariant_enabled()
+    with runtime.split_k(False):
+        assert not runtime.split_k_enabled() and not runtime.batch_invariant_enabled()
+    assert runtime.split_k_enabled()
+
+
+def test_batch_invariant_bmm_equals_torch_bmm():
+    import torch
+
+    from samplers_amd import runtime
+    from samplers_amd.networks.unet2d import bmm, score_gemm
+
+    g = torch.Generator().manual_seed(0)
+    a, b = torch.randn(5, 16, 8, generator=g), torch.randn(5, 8, 12, generator=g)
+    with runtime.batch_invariant():
+        out = bmm(a, b)
+        s = score_gemm(a, b.transpose(1, 2), 0.5, torch.empty(5, 16, 12))
+    torch.testing.assert_close(out, torch.bmm(a, b))
+    torch.testing.assert_close(s, 0.5 * torch.bmm(a, b))
