@@ -262,17 +262,23 @@ int sp_groupnorm_silu_bwd(const float* dz, const float* x, const float* chan_bia
  * channels - c1; x2 NULL: one tensor), read in place — the up-path ResnetBlocks'
  * torch.cat([h, skip]) is never materialised.  The backward writes the input VJP into the
  * two parts (dx1, dx2) and adds the optional addends (add1, add2: e.g. the residual
- * branch's gradient; an addend may alias its output). */
+ * branch's gradient; an addend may alias its output).
+ * team (or NULL): the caller's region for the single-pass kernels' team words, team_bytes
+ * >= sp_groupnorm_team_bytes(); zeroed once by the caller (e.g. at allocation), left zero by
+ * every launch, and used by one stream at a time — then a call issues no memset.  NULL: the
+ * words live in `work`, zeroed by a memset each call (what sp_groupnorm_silu_fwd / _bwd do).
+ * The library allocates nothing. */
 int sp_groupnorm_silu_fwd2(const float* x1, const float* x2, int32_t c1, const float* chan_bias,
                            const float* gamma, const float* beta, int64_t n, int32_t channels,
                            int64_t hw, int32_t groups, float eps, int32_t act, float* z,
-                           float* mean, float* rstd, float* work, sp_stream_t stream);
+                           float* mean, float* rstd, float* work, void* team, int64_t team_bytes,
+                           sp_stream_t stream);
 int sp_groupnorm_silu_bwd2(const float* dz, const float* x1, const float* x2, int32_t c1,
                            const float* chan_bias, const float* gamma, const float* beta,
                            const float* mean, const float* rstd, int64_t n, int32_t channels,
                            int64_t hw, int32_t groups, int32_t act, float* dx1, float* dx2,
                            const float* add1, const float* add2, const float* add1b,
-                           float* work, sp_stream_t stream);
+                           float* work, void* team, int64_t team_bytes, sp_stream_t stream);
 
 /* Single-pass GroupNorm (default on): a team of workgroups per group keeps the group in
  * registers across its reduction (forward reads x once, backward x and dz once).  enable:
@@ -284,12 +290,7 @@ int sp_groupnorm_silu_bwd2(const float* dz, const float* x1, const float* x2, in
  * recomputed that way (a cost, not an error).  set_spin_limit: the poll bound (< 0 default;
  * 0 recomputes every partial not present at the first poll — a test of that path). */
 int sp_groupnorm_single_pass(int32_t enable);
-/* The single-pass kernels' team words live in a library-owned region per (device, stream),
- * zeroed once and left zero by every launch, so a call issues no memset (default on).  0: use
- * and zero the caller's workspace each call (also the path taken while a stream is being
- * captured into a graph and the region would have to grow); < 0 query; returns the previous
- * setting.  Results are identical either way. */
-int sp_groupnorm_persistent_slots(int32_t enable);
+int64_t sp_groupnorm_team_bytes(int64_t n, int32_t channels, int64_t hw, int32_t groups);
 int64_t sp_groupnorm_team_timeouts(void);
 int sp_groupnorm_set_spin_limit(int32_t spins);
 

@@ -200,12 +200,13 @@ SIGNATURES = {
                                              _I64, ctypes.c_int32, ctypes.c_int32, _P, _P, _P]),
     "sp_groupnorm_silu_fwd2": (ctypes.c_int, [_P, _P, ctypes.c_int32, _P, _P, _P, _I64,
                                               ctypes.c_int32, _I64, ctypes.c_int32, _F,
-                                              ctypes.c_int32, _P, _P, _P, _P, _P]),
+                                              ctypes.c_int32, _P, _P, _P, _P, _P, _I64, _P]),
     "sp_groupnorm_silu_bwd2": (ctypes.c_int, [_P, _P, _P, ctypes.c_int32, _P, _P, _P, _P, _P,
                                               _I64, ctypes.c_int32, _I64, ctypes.c_int32,
-                                              ctypes.c_int32, _P, _P, _P, _P, _P, _P, _P]),
+                                              ctypes.c_int32, _P, _P, _P, _P, _P, _P, _P, _I64,
+                                              _P]),
     "sp_groupnorm_single_pass": (ctypes.c_int, [ctypes.c_int32]),
-    "sp_groupnorm_persistent_slots": (ctypes.c_int, [ctypes.c_int32]),
+    "sp_groupnorm_team_bytes": (_I64, [_I64, ctypes.c_int32, _I64, ctypes.c_int32]),
     "sp_groupnorm_team_timeouts": (_I64, []),
     "sp_groupnorm_set_spin_limit": (ctypes.c_int, [ctypes.c_int32]),
     "sp_wino3x3_fwd_res": (ctypes.c_int, [_P, _P, _P, _P, _I64, ctypes.c_int32, ctypes.c_int32,

@@ -21,8 +21,6 @@
 #include "sp_common.h"
 
 #include <algorithm>
-#include <map>
-#include <mutex>
 #include <utility>
 
 // No implicit mul+add contraction: which products the backend fuses depends on the code
@@ -941,22 +939,6 @@ static int gn_geom(int64_t n, int32_t c, int64_t hw, int32_t groups, const float
 }
 
 static int g_single_pass = 1;  // sp_groupnorm_single_pass
-#ifndef SP_GN_PERSISTENT
-#define SP_GN_PERSISTENT 1
-#endif
-static int g_persistent = SP_GN_PERSISTENT;  // sp_groupnorm_persistent_slots
-
-// The single-pass kernels' team words and done counts: a library-owned region per (device,
-// stream), zeroed once when allocated — the kernels leave it zero (gnt_settle) — so a call needs
-// no memset.  Without it (disabled, or a stream being captured into a graph) the caller's
-// workspace is used and zeroed first.  A captured launch never takes the region: a graph may be
-// replayed on another stream while eager work uses the region (two launches would then share
-// team words), and a later eager call that grows the region would free memory the graph's
-// nodes still name.  A captured call's memset is a node of the graph, so each replay starts
-// from zeroed words of its own workspace.
-struct GntRegion { void* p = nullptr; size_t bytes = 0; };
-static std::mutex g_region_mu;
-static std::map<std::pair<int, hipStream_t>, GntRegion> g_regions;
 
 // A stream being captured into a graph takes the two-pass kernels (bit-identical results): a
 // replayed graph let the single-pass teams wait on members that were not resident at B = 64
@@ -967,34 +949,22 @@ static bool gn_capturing(hipStream_t s) {
     return hipStreamIsCapturing(s, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone;
 }
 
-static int gnt_slots(int64_t ngroups, int chunks, float* work, hipStream_t s, uint64_t** slots, int** done) {
-    const size_t words = (size_t)ngroups * chunks * 16, bytes = words + (size_t)ngroups * 4;
-    int dev = 0;
-    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-    const bool capturing = hipStreamIsCapturing(s, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone;
-    if (g_persistent && !capturing && hipGetDevice(&dev) == hipSuccess) {
-        std::lock_guard<std::mutex> lk(g_region_mu);
-        GntRegion& r = g_regions[{dev, s}];
-        if (r.bytes < bytes) {
-            if (r.p) {  // a kernel on this stream may still use the old region
-                if (hipStreamSynchronize(s) != hipSuccess) return check_launch("groupnorm slots (sync)");
-                (void)hipFree(r.p);
-                r.p = nullptr, r.bytes = 0;
-            }
-            const size_t want = std::max(bytes * 2, (size_t)4 << 20);
-            if (hipMalloc(&r.p, want) == hipSuccess) {
-                if (hipMemsetAsync(r.p, 0, want, s) != hipSuccess) return check_launch("groupnorm slots (zero)");
-                r.bytes = want;
-            } else {
-                (void)hipGetLastError();
-                r.p = nullptr;
-            }
-        }
-        if (r.bytes >= bytes) {
-            *slots = static_cast<uint64_t*>(r.p);
-            *done = reinterpret_cast<int*>(static_cast<char*>(r.p) + words);
-            return SP_OK;
-        }
+// Bytes of the single-pass kernels' team region: two 64-bit words per chunk and a done count per
+// group, at the smallest chunk either direction uses (an upper bound for both).
+static int64_t gnt_region_bytes(int64_t ngroups, int chunks) { return ngroups * chunks * 16 + ngroups * 4; }
+
+// The single-pass kernels' team words and done counts.  `team` (the caller's, team_bytes long,
+// zeroed once by the caller and left zero by every launch — gnt_clear_own / gnt_release_last —
+// so a call needs no memset), else the call's workspace, zeroed first.  The library allocates
+// nothing: a caller that keeps one zeroed region per stream saves the memset launch.
+static int gnt_slots(int64_t ngroups, int chunks, float* work, void* team, int64_t team_bytes,
+                     hipStream_t s, uint64_t** slots, int** done) {
+    const int64_t words = ngroups * chunks * 16, bytes = gnt_region_bytes(ngroups, chunks);
+    if (team) {
+        if (team_bytes < bytes) return SP_EINVAL;
+        *slots = static_cast<uint64_t*>(team);
+        *done = reinterpret_cast<int*>(static_cast<char*>(team) + words);
+        return SP_OK;
     }
     *slots = reinterpret_cast<uint64_t*>(work);
     *done = reinterpret_cast<int*>(reinterpret_cast<char*>(work) + words);
@@ -1026,10 +996,10 @@ int64_t sp_groupnorm_workspace(int64_t n, int32_t channels, int64_t hw, int32_t 
     return n * groups * ((gs + GN_CHUNK_MIN - 1) / GN_CHUNK_MIN) * 4 + n * groups;
 }
 
-int sp_groupnorm_persistent_slots(int32_t enable) {
-    const int prev = g_persistent;
-    if (enable >= 0) g_persistent = enable ? 1 : 0;
-    return prev;
+int64_t sp_groupnorm_team_bytes(int64_t n, int32_t channels, int64_t hw, int32_t groups) {
+    if (n < 0 || channels <= 0 || hw <= 0 || groups <= 0 || channels % groups) return -1;
+    const int64_t gs = (int64_t)(channels / groups) * hw;
+    return gnt_region_bytes(n * groups, static_cast<int>((gs + GN_CHUNK_MIN - 1) / GN_CHUNK_MIN));
 }
 
 int sp_groupnorm_single_pass(int32_t enable) {
@@ -1066,13 +1036,14 @@ int sp_groupnorm_silu_fwd(const float* x, const float* chan_bias, const float* g
                           int32_t groups, float eps, int32_t act, float* z, float* mean,
                           float* rstd, float* work, sp_stream_t stream) {
     return sp_groupnorm_silu_fwd2(x, nullptr, channels, chan_bias, gamma, beta, n, channels, hw,
-                                  groups, eps, act, z, mean, rstd, work, stream);
+                                  groups, eps, act, z, mean, rstd, work, nullptr, 0, stream);
 }
 
 int sp_groupnorm_silu_fwd2(const float* x, const float* x2, int32_t c1, const float* chan_bias,
                            const float* gamma, const float* beta, int64_t n, int32_t channels,
                            int64_t hw, int32_t groups, float eps, int32_t act, float* z,
-                           float* mean, float* rstd, float* work, sp_stream_t stream) {
+                           float* mean, float* rstd, float* work, void* team, int64_t team_bytes,
+                           sp_stream_t stream) {
     GnGeom G;
     int V;
     dim3 grid;
@@ -1098,7 +1069,7 @@ int sp_groupnorm_silu_fwd2(const float* x, const float* x2, int32_t c1, const fl
         if (teams > 0) {
             uint64_t* slots;
             int* done;
-            if (int e = gnt_slots(ngroups, G.chunks, work, s, &slots, &done)) return e;
+            if (int e = gnt_slots(ngroups, G.chunks, work, team, team_bytes, s, &slots, &done)) return e;
             const dim3 grid1(static_cast<unsigned>(teams * G.chunks));
             const int nt = static_cast<int>(teams);
 #define SP_GN_FWD_PIPE(AA, PP) \
@@ -1133,7 +1104,7 @@ int sp_groupnorm_silu_bwd(const float* dz, const float* x, const float* chan_bia
                           sp_stream_t stream) {
     return sp_groupnorm_silu_bwd2(dz, x, nullptr, channels, chan_bias, gamma, beta, mean, rstd,
                                   n, channels, hw, groups, act, dx, nullptr, nullptr, nullptr,
-                                  nullptr, work, stream);
+                                  nullptr, work, nullptr, 0, stream);
 }
 
 int sp_groupnorm_silu_bwd2(const float* dz, const float* x, const float* x2, int32_t c1,
@@ -1141,7 +1112,7 @@ int sp_groupnorm_silu_bwd2(const float* dz, const float* x, const float* x2, int
                            const float* mean, const float* rstd, int64_t n, int32_t channels,
                            int64_t hw, int32_t groups, int32_t act, float* dx, float* dx2,
                            const float* add1, const float* add2, const float* add1b,
-                           float* work, sp_stream_t stream) {
+                           float* work, void* team, int64_t team_bytes, sp_stream_t stream) {
     GnGeom G;
     int V;
     dim3 grid;
@@ -1165,7 +1136,7 @@ int sp_groupnorm_silu_bwd2(const float* dz, const float* x, const float* x2, int
         if (teams > 0) {
             uint64_t* slots;
             int* done;
-            if (int e = gnt_slots(ngroups, G.chunks, work, s, &slots, &done)) return e;
+            if (int e = gnt_slots(ngroups, G.chunks, work, team, team_bytes, s, &slots, &done)) return e;
             launch(0, kern, dim3(static_cast<unsigned>(teams * G.chunks)), blk, s, dz, x, G, mean,
                    rstd, slots, done, static_cast<int>(teams), ngroups, dx, dx2, add1, add2);
             return check_launch("sp_groupnorm_silu_bwd");

@@ -6,7 +6,7 @@ applies SiLU to its output — the ``norm -> silu`` pairs and the ``h + temb`` a
 diffusers' ``ResnetBlock2D`` that the reference's priors run
 (``/root/reference/samplers/networks/diffusers/ddpm.py:40-43``,
 ``stable_diffusion.py:330-345``).  On device tensors it runs the HIP kernels of
-``csrc/sp_groupnorm.hip`` (``sp_groupnorm_silu_fwd/bwd``) through a
+``csrc/sp_groupnorm.hip`` (``sp_groupnorm_silu_fwd2/bwd2``) through a
 ``torch.autograd.Function`` whose backward is the fused input VJP; on CPU tensors
 (the oracle's CPU baseline and the CPU tests) it is plain torch.
 """
@@ -51,6 +51,43 @@ def _hw(t: Tensor) -> int:
     return hw
 
 
+# The single-pass GroupNorm kernels' team words (sp_groupnorm_team_bytes): one zeroed region per
+# (device, stream), owned here and handed to every call on that stream (the kernels leave it
+# zero, so no call needs a memset).  The library allocates nothing.  Grown by
+# replacement: the old region goes back to torch's caching allocator on the same stream, so any
+# reuse of it is ordered after the launches that still name it.  Never used while a stream is
+# being captured into a graph (those calls take the two-pass kernels; a region allocated inside
+# a capture would belong to the graph's pool).  SAMPLERS_AMD_GN_TEAM=0: no region (the library
+# then zeroes words in the call's workspace, one memset per call).
+_team_regions: dict = {}
+
+
+def _team_enabled() -> bool:
+    import os
+
+    return os.environ.get("SAMPLERS_AMD_GN_TEAM", "1").lower() not in ("0", "off", "false")
+
+
+def gn_team_region(x: Tensor, n: int, c: int, hw: int, groups: int) -> tuple[Tensor | None, int]:
+    """(region, bytes) for a GroupNorm call on x's device and the current stream, or (None, 0)."""
+    if not _team_enabled() or torch.cuda.is_current_stream_capturing():
+        return None, 0
+    need = _query("sp_groupnorm_team_bytes", n, c, hw, groups)
+    if need <= 0:
+        return None, 0
+    key = (x.device.index, _hip.stream_of(x))
+    t = _team_regions.get(key)
+    if t is None or t.numel() < need:
+        size = max(need * 2, 4 << 20)
+        t = _team_regions[key] = torch.zeros(size, device=x.device, dtype=torch.uint8)
+    return t, t.numel()
+
+
+def release_team_regions() -> None:
+    """Drop the cached team regions (e.g. before destroying a stream they were used on)."""
+    _team_regions.clear()
+
+
 def gn_forward(norm: "GroupNormAct", x1: Tensor, x2: Tensor | None = None,
                chan_bias: Tensor | None = None) -> tuple[Tensor, Tensor]:
     """HIP GroupNorm(+bias)(+SiLU) forward over x1, or over cat(x1, x2) along channels read in
@@ -64,11 +101,13 @@ def gn_forward(norm: "GroupNormAct", x1: Tensor, x2: Tensor | None = None,
     stats = torch.empty(2, n * g, device=x1.device, dtype=torch.float32)
     work = torch.empty(max(_query("sp_groupnorm_workspace", n, c, hw, g), 1), device=x1.device,
                        dtype=torch.float32)
+    team, tb = gn_team_region(x1, n, c, hw, g)
     sp = _hip.ptr(stats)
     _hip.check(lib.sp_groupnorm_silu_fwd2(
         _hip.ptr(x1), _hip.ptr(x2), c1, _hip.ptr(chan_bias), _hip.ptr(norm.weight),
         _hip.ptr(norm.bias), n, c, hw, g, float(norm.eps), int(norm.act),
-        _hip.ptr(z), sp, sp + 4 * n * g, _hip.ptr(work), _hip.stream_of(x1)), "sp_groupnorm_silu_fwd2")
+        _hip.ptr(z), sp, sp + 4 * n * g, _hip.ptr(work), _hip.ptr(team), tb, _hip.stream_of(x1)),
+        "sp_groupnorm_silu_fwd2")
     return z, stats
 
 
@@ -88,12 +127,14 @@ def gn_backward(norm: "GroupNormAct", dz: Tensor, x1: Tensor, x2: Tensor | None,
     dx2 = None if x2 is None else (torch.empty_like(x2) if out2 is None else out2)
     work = torch.empty(max(_query("sp_groupnorm_workspace", n, c, hw, g), 1), device=x1.device,
                        dtype=torch.float32)
+    team, tb = gn_team_region(x1, n, c, hw, g)
     sp = _hip.ptr(stats)
     _hip.check(lib.sp_groupnorm_silu_bwd2(
         _hip.ptr(dz.contiguous()), _hip.ptr(x1), _hip.ptr(x2), c1, _hip.ptr(chan_bias),
         _hip.ptr(norm.weight), _hip.ptr(norm.bias), sp, sp + 4 * n * g, n, c,
         hw, g, int(norm.act), _hip.ptr(dx1), _hip.ptr(dx2), _hip.ptr(add1),
-        _hip.ptr(add2), _hip.ptr(add1b), _hip.ptr(work), _hip.stream_of(x1)), "sp_groupnorm_silu_bwd2")
+        _hip.ptr(add2), _hip.ptr(add1b), _hip.ptr(work), _hip.ptr(team), tb, _hip.stream_of(x1)),
+        "sp_groupnorm_silu_bwd2")
     return dx1, dx2
 
 
@@ -109,10 +150,11 @@ class _GroupNormActFn(torch.autograd.Function):
         work = torch.empty(max(_query("sp_groupnorm_workspace", n, c, hw, groups), 1),
                            device=x.device, dtype=torch.float32)
         cb = None if chan_bias is None else chan_bias.contiguous()
-        _hip.check(lib.sp_groupnorm_silu_fwd(
-            _hip.ptr(x), _hip.ptr(cb), _hip.ptr(weight), _hip.ptr(bias), n, c, hw, groups,
+        team, tb = gn_team_region(x, n, c, hw, groups)
+        _hip.check(lib.sp_groupnorm_silu_fwd2(
+            _hip.ptr(x), None, c, _hip.ptr(cb), _hip.ptr(weight), _hip.ptr(bias), n, c, hw, groups,
             float(eps), int(act), _hip.ptr(z), _hip.ptr(stats[0]), _hip.ptr(stats[1]),
-            _hip.ptr(work), _hip.stream_of(x)), "sp_groupnorm_silu_fwd")
+            _hip.ptr(work), _hip.ptr(team), tb, _hip.stream_of(x)), "sp_groupnorm_silu_fwd2")
         ctx.save_for_backward(x, weight, bias, cb, stats)
         ctx.cfg = (groups, float(eps), bool(act))
         ctx.box = box
@@ -130,17 +172,13 @@ class _GroupNormActFn(torch.autograd.Function):
         work = torch.empty(max(_query("sp_groupnorm_workspace", n, c, hw, groups), 1),
                            device=x.device, dtype=torch.float32)
         add = ctx.box.take() if ctx.box is not None else None
-        if add is not None:  # the residual branch's gradient of x, summed in the VJP kernel
-            _hip.check(lib.sp_groupnorm_silu_bwd2(
-                _hip.ptr(dz), _hip.ptr(x), None, c, _hip.ptr(cb), _hip.ptr(weight), _hip.ptr(bias),
-                _hip.ptr(stats[0]), _hip.ptr(stats[1]), n, c, hw, groups, int(act), _hip.ptr(dx), None,
-                _hip.ptr(add.contiguous()), None, None, _hip.ptr(work), _hip.stream_of(x)),
-                "sp_groupnorm_silu_bwd2")
-        else:
-            _hip.check(lib.sp_groupnorm_silu_bwd(
-                _hip.ptr(dz), _hip.ptr(x), _hip.ptr(cb), _hip.ptr(weight), _hip.ptr(bias),
-                _hip.ptr(stats[0]), _hip.ptr(stats[1]), n, c, hw, groups, int(act), _hip.ptr(dx),
-                _hip.ptr(work), _hip.stream_of(x)), "sp_groupnorm_silu_bwd")
+        add = None if add is None else add.contiguous()  # the residual branch's gradient of x
+        team, tb = gn_team_region(x, n, c, hw, groups)
+        _hip.check(lib.sp_groupnorm_silu_bwd2(
+            _hip.ptr(dz), _hip.ptr(x), None, c, _hip.ptr(cb), _hip.ptr(weight), _hip.ptr(bias),
+            _hip.ptr(stats[0]), _hip.ptr(stats[1]), n, c, hw, groups, int(act), _hip.ptr(dx), None,
+            _hip.ptr(add), None, None, _hip.ptr(work), _hip.ptr(team), tb, _hip.stream_of(x)),
+            "sp_groupnorm_silu_bwd2")
         d_w = d_b = d_cb = None
         need_w, need_b, need_cb = ctx.needs_input_grad[1], ctx.needs_input_grad[2], ctx.needs_input_grad[3]
         if need_cb:

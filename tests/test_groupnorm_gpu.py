@@ -164,12 +164,12 @@ def test_fused_resnet_blocks_match_cpu(cuda):
     (1, 256, 128, 128, 128, 32),  # a group straddles the parts at a chunk boundary (UNet 128^2)
 ])
 @pytest.mark.parametrize("act", [True, False])
-def test_single_pass_matches_two_pass_bitwise(cuda, shape, act):
+def test_single_pass_matches_two_pass_bitwise(cuda, shape, act, monkeypatch):
     """The single-pass team kernels (one workgroup per chunk, chunk partials exchanged through
     agent-scope atomics) against the two-pass kernels: same chunking, same summation order,
     so the forward output, statistics and the input VJP agree bit for bit."""
     from samplers_amd import _hip
-    from samplers_amd.networks.layers import gn_backward, gn_forward
+    from samplers_amd.networks.layers import _team_regions, gn_backward, gn_forward
 
     lib = _hip.load_library()
     n, c1, c2, h, w, g = shape
@@ -188,17 +188,17 @@ def test_single_pass_matches_two_pass_bitwise(cuda, shape, act):
     a2 = torch.randn(n, c2, h, w, generator=gen).to(cuda) if c2 else None
     outs = []
     prev = lib.sp_groupnorm_single_pass(-1)
-    prev_persistent = lib.sp_groupnorm_persistent_slots(-1)
     recomputed = 0
     try:
         # two-pass; single-pass; single-pass with a poll bound of 0 (every partial not yet
         # published at the first poll is recomputed by the waiting workgroup: the path that
         # keeps the result exact when a team member is not resident); single-pass again (the
-        # library's team-word region must have been left clean by every launch before, the
-        # recomputing ones included); single-pass on the caller's zeroed workspace
-        for mode, spins, persistent in ((0, -1, 1), (1, -1, 1), (1, 0, 1), (1, -1, 1), (1, -1, 0)):
+        # caller's team region, layers.gn_team_region, must have been left clean by every launch
+        # before, the recomputing ones included); single-pass on the call's zeroed workspace
+        # (no team region: SAMPLERS_AMD_GN_TEAM=0)
+        for mode, spins, team in ((0, -1, "1"), (1, -1, "1"), (1, 0, "1"), (1, -1, "1"), (1, -1, "0")):
             lib.sp_groupnorm_single_pass(mode)
-            lib.sp_groupnorm_persistent_slots(persistent)
+            monkeypatch.setenv("SAMPLERS_AMD_GN_TEAM", team)
             _hip.check(lib.sp_groupnorm_set_spin_limit(spins), "spin limit")
             before = lib.sp_groupnorm_team_timeouts()
             z, st = gn_forward(layer, x1, x2, cb)
@@ -207,9 +207,11 @@ def test_single_pass_matches_two_pass_bitwise(cuda, shape, act):
             outs.append((z, st, d1, d2))
             if spins == 0:
                 recomputed = lib.sp_groupnorm_team_timeouts() - before
+        assert _team_regions  # the single-pass launches ran on a caller-owned region
+        for region in _team_regions.values():
+            assert int(region.count_nonzero()) == 0  # every launch left its region zero
     finally:
         lib.sp_groupnorm_single_pass(prev)
-        lib.sp_groupnorm_persistent_slots(prev_persistent)
         lib.sp_groupnorm_set_spin_limit(-1)
     for other in outs[1:]:
         for a, b in zip(outs[0], other):
