@@ -66,15 +66,15 @@ def timestep_embedding(t: Tensor, dim: int, *, flip_sin_to_cos: bool, freq_shift
     return emb
 
 
-def temb_projections(model: nn.Module, emb: Tensor) -> dict[int, Tensor]:
+def temb_projection_groups(model: nn.Module, emb: Tensor) -> list[tuple[list[int], Tensor]]:
     """Every ResnetBlock2D's ``time_emb_proj(silu(emb))`` of ``model`` at once: one SiLU and one
     batched GEMM per projection width (the blocks' weights stacked, cached on the model) instead
     of a SiLU, a copy and a GEMM per block — 3 launches instead of ~70 per UNet forward, which
-    is most of the step's launches at batch 1.  Returns {id(block): [B, C] contiguous}; empty
-    when a projection is trainable (the per-block path keeps the gradients)."""
+    is most of the step's launches at batch 1.  Returns [(block ids, [blocks][B][C])] per width;
+    empty when a projection is trainable (the per-block path keeps the gradients)."""
     blocks = [m for m in model.modules() if isinstance(m, ResnetBlock2D) and m.time_emb_proj is not None]
     if not blocks or any(p.requires_grad for b in blocks for p in b.time_emb_proj.parameters()):
-        return {}
+        return []
     key = (emb.device, emb.dtype, tuple((b.time_emb_proj.weight.data_ptr(), b.time_emb_proj.weight._version,
                                          b.time_emb_proj.bias.data_ptr(), b.time_emb_proj.bias._version)
                                         for b in blocks))
@@ -91,9 +91,16 @@ def temb_projections(model: nn.Module, emb: Tensor) -> dict[int, Tensor]:
              torch.stack([b.time_emb_proj.bias.detach()[None] for b in members]).to(emb.device, emb.dtype))
             for members in groups.values()]
     s = F.silu(emb)
+    return [(ids, torch.baddbmm(bias, s.expand(len(ids), *s.shape), wt))  # [blocks][B][C]
+            for ids, wt, bias in cache["groups"]]
+
+
+def temb_projections(model: nn.Module, emb: Tensor) -> dict[int, Tensor]:
+    """Every ResnetBlock2D's ``time_emb_proj(silu(emb))`` of ``model`` at once (see
+    ``temb_projection_groups``): {id(block): [B, C] contiguous}; empty when a projection is
+    trainable (the per-block path keeps the gradients)."""
     out = {}
-    for ids, wt, bias in cache["groups"]:
-        y = torch.baddbmm(bias, s.expand(len(ids), *s.shape), wt)  # [blocks][B][C]
+    for ids, y in temb_projection_groups(model, emb):
         out.update(zip(ids, y.unbind(0)))
     return out
 
@@ -164,6 +171,9 @@ def _shortcut_forward(conv: nn.Conv2d, x1: Tensor, x2: Tensor | None) -> Tensor:
                                      None, None, n, hw, _hip.ptr(y), cout, None, 0, _hip.ptr(ws), nb,
                                      _hip.stream_of(x1)), "sp_gemm_x6")
         return y
+    if batch_invariant_enabled() and n > 1:  # hipBLASLt's algorithm follows the batch count
+        return torch.cat([_shortcut_forward(conv, x1[i:i + 1], None if x2 is None else x2[i:i + 1])
+                          for i in range(n)])
     w = conv.weight[:, :, 0, 0]
     y = torch.matmul(w[:, :c1], x1.reshape(n, c1, -1))
     if x2 is not None:
@@ -187,6 +197,10 @@ def _shortcut_input_vjp(conv: nn.Conv2d, dy: Tensor, c1: int, c2: int) -> tuple[
                                      n, hw, _hip.ptr(d1), c1, _hip.ptr(d2), c2, _hip.ptr(ws), nb,
                                      _hip.stream_of(dy)), "sp_gemm_x6")
         return d1, d2
+    if batch_invariant_enabled() and n > 1:
+        parts = [_shortcut_input_vjp(conv, dy[i:i + 1], c1, c2) for i in range(n)]
+        return (torch.cat([p[0] for p in parts]),
+                None if not c2 else torch.cat([p[1] for p in parts]))
     dyv = dy.reshape(n, cout, -1)
     w = conv.weight[:, :, 0, 0]
     d1 = torch.matmul(w[:, :c1].t(), dyv).reshape((n, c1) + tuple(dy.shape[2:]))
@@ -618,8 +632,10 @@ class UNet2DModel(nn.Module):
         weights only): a step then launches no sinusoid, MLP or projection kernels and copies
         no timestep to the device (at batch 1 each is a host-bound launch; the H2D copy of a
         pageable tensor also waits on the stream).  At batch 1 the rows are views of the table;
-        at larger batches the row is expanded and projected per step (4 launches).  None (the
-        per-step path) for device or per-sample timesteps, or trainable weights."""
+        at larger batches the table row is broadcast to the batch (one copy per projection
+        width), so the values are the same at every batch size (a projection recomputed at M = B
+        rows would round differently from the table's M = T: DESIGN.md §6).  None (the per-step
+        path) for device or per-sample timesteps, or trainable weights."""
         if torch.is_tensor(timestep):
             if timestep.is_cuda or timestep.numel() != 1 or timestep.is_floating_point():
                 return None
@@ -644,14 +660,17 @@ class UNet2DModel(nn.Module):
                 t_emb = timestep_embedding(ts, cfg.block_out_channels[0], flip_sin_to_cos=cfg.flip_sin_to_cos,
                                            freq_shift=cfg.freq_shift).to(sample.dtype)
                 emb_all = self.time_embedding(t_emb)
-                tab = (key, emb_all, temb_projections(self, emb_all))
+                tab = (key, emb_all, temb_projection_groups(self, emb_all))
             self.__dict__["_t_rows"] = tab
-        _, emb_all, tbs_all = tab
+        _, emb_all, groups = tab
         b = sample.shape[0]
-        if b == 1:
-            return emb_all[t:t + 1], {k: v[t:t + 1] for k, v in tbs_all.items()}
-        emb = emb_all[t:t + 1].expand(b, -1)
-        return emb, temb_projections(self, emb)
+        out = {}
+        for ids, y in groups:  # y: [blocks][T][C]
+            rows = y[:, t:t + 1]
+            if b > 1:
+                rows = rows.expand(len(ids), b, y.shape[2]).contiguous()
+            out.update(zip(ids, rows.unbind(0)))
+        return emb_all[t:t + 1].expand(b, -1), out
 
     def forward(self, sample: Tensor, timestep: Tensor | int) -> Tensor:
         cfg = self.config
