@@ -258,10 +258,13 @@ __device__ __forceinline__ WrSrc wr_src(const WrGeom& g, const WrTile& ti, int w
     const int row0 = GE::MOSAIC ? -1 : ti.oh0 + 2 * GE::TRW * (wv >> 1) - 1;  // first input row
     const int ka = lane % GE::PPR, rca = lane / GE::PPR, rcb = 64 / GE::PPR + ((lane / GE::PPR) & 3);
     const int rch = (lane % (2 * GE::RC)) >> 1, side = lane & 1;
+    // split-K part kh reads input channels kofs .. kofs + 2 nsteps - 1 (and the matching U)
+    const int kofs = GE::SPLIT ? ti.kh * 2 * g.nsteps : 0, nimg = wr_nimg<GE>(g, ti, wv);
     auto goff = [&](int rc, int col) {
         const int ci = rc / GE::ROWS, gr = row0 + rc % GE::ROWS;
-        if constexpr (GE::MOSAIC) {  // virtual column -> (image, column); rows 0..7
-            return (unsigned)gr < (unsigned)g.H && col >= 0 && col < 2 * g.W
+        if constexpr (GE::MOSAIC) {  // virtual column -> (image, column); rows 0..7; a column of
+                                     // an image past the batch reads zeros (OOB)
+            return (unsigned)gr < (unsigned)g.H && col >= 0 && col < 2 * g.W && (col >> 3) < nimg
                        ? ((col >> 3) * g.cin * g.plane + ci * g.plane + gr * g.W + (col & 7)) * 4
                        : OOB;
         }
@@ -269,8 +272,6 @@ __device__ __forceinline__ WrSrc wr_src(const WrGeom& g, const WrTile& ti, int w
                    ? (ci * g.plane + gr * g.W + col) * 4 : OOB;
     };
     WrSrc s;
-    // split-K part kh reads input channels kofs .. kofs + 2 nsteps - 1 (and the matching U)
-    const int kofs = GE::SPLIT ? ti.kh * 2 * g.nsteps : 0, nimg = wr_nimg<GE>(g, ti, wv);
     s.rs = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<float*>(g.x + wr_img0<GE>(g, ti, wv) * g.cin * g.plane + (int64_t)kofs * g.plane),
         (short)0, nimg ? (nimg * g.cin - kofs) * g.plane * 4 : 0, 0x00020000);
@@ -281,15 +282,13 @@ __device__ __forceinline__ WrSrc wr_src(const WrGeom& g, const WrTile& ti, int w
         static_cast<int>(((GE::SPLIT ? (int64_t)ti.kh * g.nsteps * g.u_step : 0) +
                           (int64_t)(ti.co0 >> 5) * 64 * 16) * 4));
 #if SP_DEBUG
-    {   // every k-step's input pieces inside this tile's planes, U rows inside the packed U
-        // (a MOSAIC wave whose second image, or both, lie past the batch addresses them anyway:
-        // its buffer's range is cut to the images that exist, which read as zeros)
+    {   // every k-step's input pieces inside this tile's planes — of the images that exist (a
+        // MOSAIC wave's pieces of an image past the batch are OOB) —, U rows inside the packed U
         const int64_t span = nimg ? (int64_t)(nimg * g.cin - kofs) * g.plane * 4 : 0;
         const int64_t last = (int64_t)(g.nsteps - 1) * g.so_step;
-        const bool full = !GE::MOSAIC || nimg == 2;
-        SP_DCHECK(s.oa == OOB || (s.oa >= 0 && (!full || s.oa + last + 16 <= span)));
-        SP_DCHECK(s.ob == OOB || (s.ob >= 0 && (!full || s.ob + last + 16 <= span)));
-        SP_DCHECK(s.oh == OOB || (s.oh >= 0 && (!full || s.oh + last + 4 <= span)));
+        SP_DCHECK(s.oa == OOB || (s.oa >= 0 && s.oa + last + 16 <= span));
+        SP_DCHECK(s.ob == OOB || (s.ob >= 0 && s.ob + last + 16 <= span));
+        SP_DCHECK(s.oh == OOB || (s.oh >= 0 && s.oh + last + 4 <= span));
         SP_DCHECK(s.uso >= 0 && (int64_t)s.uso + ((int64_t)(g.nsteps - 1) * g.u_step + 64 * 16) * 4 <=
                                    (int64_t)g.nsteps * g.ksplit * g.u_step * 4);
         SP_DCHECK(ti.co0 + 32 <= g.cout && ti.n < g.batch);

@@ -18,7 +18,7 @@ import torch.nn.functional as F
 from torch import Tensor, nn
 
 from .. import _hip
-from ..runtime import split_k_enabled
+from ..runtime import batch_invariant_enabled, split_k_enabled
 
 
 def group_norm_act_torch(x: Tensor, groups: int, weight: Tensor | None, bias: Tensor | None,
@@ -716,6 +716,13 @@ def linear(x: Tensor, module: nn.Module, w2d: Tensor | None = None, bias: Tensor
     when the residual's other consumer (a ``LayerNorm`` given the same box) adds it in its VJP."""
     w2d = module.weight if w2d is None else w2d
     bias = getattr(module, "bias", None) if bias is None else bias
+    if batch_invariant_enabled() and x.dim() == 3 and x.shape[0] > 1:
+        # one batch entry per call: the backend (x6 tile or hipBLASLt) and hipBLASLt's algorithm
+        # are chosen from the token count, which would otherwise include the batch
+        if box is not None:
+            box.enabled = False
+        y = torch.cat([linear(x[i:i + 1], module, w2d, bias) for i in range(x.shape[0])])
+        return y if res is None else y + res
     m, k = w2d.shape
     t = x.numel() // k if x.dim() else 0
     if (x.is_cuda and x.dtype == torch.float32 and not w2d.requires_grad
