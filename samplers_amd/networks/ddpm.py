@@ -60,6 +60,10 @@ class DDPMSchedule:
 class DDPMNetwork(EpsilonNetwork[NoCondition]):
     """ε-network over a pixel-space UNet and a DDPM schedule."""
 
+    # its UNet runs on this project's kernels and torch's caching allocator only, so a DPS step
+    # over it can be captured into a hipGraph (DPSSampler's default replay at small batches)
+    graph_capturable = True
+
     def __init__(self, unet: UNet2DModel, schedule: DDPMSchedule | None = None):
         schedule = schedule or DDPMSchedule()
         acp = schedule.alphas_cumprod

@@ -364,6 +364,34 @@ def make_dps_step(network, inverse_problem, observation_rows, y_div, **kw):
     return GenericDPSStep(network, inverse_problem, observation_rows, y_div, **kw)
 
 
+# hipGraph replay by default (tools/graph_sweep.sh): below this flat batch a step is
+# host-bound (a few hundred short launches) and replay is faster; above it the eager step wins
+# (captured GroupNorm runs its two-pass kernels).  Capture costs about three steps (two warm-up
+# steps and the capture), so short solves stay eager.
+GRAPH_AUTO_MAX_BATCH = 16
+GRAPH_AUTO_MIN_STEPS = 8
+
+
+def graph_auto(step, x: Tensor, guided_steps: int, *, rng: str, noise_fn, callback,
+               micro_batch: int | None) -> bool:
+    """Whether ``DPSSampler(graph=None)`` replays a captured step: the fused HIP step (native
+    operator and noise plugins), in-kernel Philox noise, no callback / kernel timer /
+    micro-batching, a flat batch of at most ``GRAPH_AUTO_MAX_BATCH`` and at least
+    ``GRAPH_AUTO_MIN_STEPS`` guided iterations, and a prior that declares itself capturable
+    (``graph_capturable``: this project's priors, whose layers run on HIP kernels and
+    allocate nothing outside torch's caching allocator; a third-party network stays eager
+    unless it sets the flag).  ``SAMPLERS_AMD_GRAPH=0`` turns the automatic choice off."""
+    import os
+
+    if os.environ.get("SAMPLERS_AMD_GRAPH", "auto").lower() in ("0", "off", "false", "eager"):
+        return False
+    return (getattr(step.network, "graph_capturable", False)
+            and isinstance(step, FusedDPSStep) and not isinstance(step, GenericDPSStep)
+            and step.timer is None and rng == "philox" and noise_fn is None and callback is None
+            and (not micro_batch or micro_batch >= x.shape[0]) and x.is_cuda
+            and 0 < x.shape[0] <= GRAPH_AUTO_MAX_BATCH and guided_steps >= GRAPH_AUTO_MIN_STEPS)
+
+
 def initial_sample(shape: tuple, device: torch.device, *, rng: str, seed: int, sample_offset: int,
                    noise_fn: NoiseFn | None) -> Tensor:
     """x_T ~ N(0, I) (``dps.py:83-87``)."""
@@ -401,7 +429,7 @@ class DPSSampler(PosteriorSampler, Generic[Condition_co]):
         sample_offset: int = 0,
         micro_batch: int | None = None,
         timer: KernelTimer | None = None,
-        graph: bool = False,
+        graph: bool | None = None,
         callback: Callable[[int, Tensor], None] | None = None,
         **kwargs,
     ) -> Tensor:
@@ -414,6 +442,9 @@ class DPSSampler(PosteriorSampler, Generic[Condition_co]):
         ``micro_batch`` bounds how many samples share one prior forward+VJP;
         ``graph=True`` replays one hipGraph-captured step for every iteration
         (``samplers.graph``; Philox noise only) — same samples, no per-launch host work;
+        ``graph=None`` (default) does so where it pays (``graph_auto``: native plugins, Philox
+        noise, no callback / timer / micro-batching, a small batch and enough steps), else
+        runs eagerly; ``graph=False`` always runs eagerly;
         ``callback(i, x)`` is called after guided iteration ``i`` with the flat sample (a view of
         the working buffer: copy it to keep it; not with ``graph=True``).
         """
@@ -442,6 +473,10 @@ class DPSSampler(PosteriorSampler, Generic[Condition_co]):
             x = initial_sample(view.flat_shape, net.device, rng=rng, seed=seed,
                                sample_offset=sample_offset, noise_fn=noise_fn)
             ts = host_timesteps(net)
+            if graph is None:
+                graph = graph_auto(step, x, len(ts) - 2, rng=rng, noise_fn=noise_fn,
+                                   callback=callback, micro_batch=micro_batch)
+            self.execution = "graph" if graph else "eager"  # what the last call ran
             if graph:
                 if not isinstance(step, FusedDPSStep) or isinstance(step, GenericDPSStep):
                     raise ValueError("graph=True needs natively implemented plugins")

@@ -74,3 +74,34 @@ def test_timestep_table_matches_per_step_embedding(cuda, b):
             rel = ((e_tab - e_dev).norm() / e_dev.norm()).item()
             assert rel < 1e-5, (t, rel)
     assert unet._timestep_rows(torch.tensor([5], device=cuda), x) is None
+
+
+def test_default_replays_small_batches_and_matches_eager(cuda):
+    """DPSSampler(graph=None) — the default — replays a captured step for this project's prior
+    at a small batch with enough steps (samples equal to the eager solve), stays eager for a
+    larger batch, few steps, a callback or a third-party network."""
+    from samplers_amd.samplers import dps as dps_mod
+
+    net = DDPMNetwork.from_config(CFG, seed=0, device=cuda)
+    prob = _problem("inpaint", cuda, b=2)
+    s = DPSSampler(net)
+    auto = s(prob, num_sampling_steps=12, gamma=0.5, seed=77)
+    assert s.execution == "graph"
+    eager = s(prob, num_sampling_steps=12, gamma=0.5, seed=77, graph=False)
+    assert s.execution == "eager"
+    rel = ((auto - eager).norm() / eager.norm()).item()
+    assert rel < 1e-5, rel
+    s(prob, num_sampling_steps=4, gamma=0.5, seed=77)  # 2 guided steps: capture does not pay
+    assert s.execution == "eager"
+    s(prob, num_sampling_steps=12, gamma=0.5, seed=77, callback=lambda i, x: None)
+    assert s.execution == "eager"
+    big = _problem("inpaint", cuda, b=dps_mod.GRAPH_AUTO_MAX_BATCH + 1)
+    s(big, num_sampling_steps=12, gamma=0.5, seed=77)
+    assert s.execution == "eager"
+
+
+def test_graph_with_callback_raises(cuda):
+    net = DDPMNetwork.from_config(CFG, seed=0, device=cuda)
+    with pytest.raises(ValueError, match="callback"):
+        DPSSampler(net)(_problem("identity", cuda), num_sampling_steps=8, graph=True,
+                        callback=lambda i, x: None)
