@@ -539,6 +539,9 @@ def main():
                                   "'collective')",
                    "execution": "hipGraph replay of one captured step" if graph is not None
                    else "eager"},
+        # gloo over ranks sharing GPUs (SAMPLERS_AMD_DIST_BACKEND=gloo): a rehearsal of the sharded
+        # path and its gather, not a throughput measurement
+        "rehearsal": bool(world > 1 and collective.get("backend") == "gloo"),
         "roofline": roofline,
         "guidance_roofline": guidance_roofline,
         "guidance_kernels": {k: {"avg_ms": round(v["avg_ms"], 5), "GB/s": round(v["gbs"], 1)}

@@ -364,11 +364,12 @@ def make_dps_step(network, inverse_problem, observation_rows, y_div, **kw):
     return GenericDPSStep(network, inverse_problem, observation_rows, y_div, **kw)
 
 
-# hipGraph replay by default (tools/graph_sweep.sh): below this flat batch a step is
-# host-bound (a few hundred short launches) and replay is faster; above it the eager step wins
-# (captured GroupNorm runs its two-pass kernels).  Capture costs about three steps (two warm-up
-# steps and the capture), so short solves stay eager.
-GRAPH_AUTO_MAX_BATCH = 16
+# hipGraph replay by default (tools/graph_sweep.sh, profiles/round5/graph_sweep/): at a
+# flat batch of 1 a step is host-bound (a few hundred short launches): 13.3 ms eager, 9.9 ms
+# replayed; from 2 on the GPU sets the step and the eager one wins (14.0 vs 14.2 ms at 2, 142 vs
+# 153 ms at 32: a captured GroupNorm runs its two-pass kernels).  Capture costs about three
+# steps (two warm-up steps and the capture), so short solves stay eager.
+GRAPH_AUTO_MAX_BATCH = 1
 GRAPH_AUTO_MIN_STEPS = 8
 
 

@@ -83,7 +83,7 @@ def test_default_replays_small_batches_and_matches_eager(cuda):
     from samplers_amd.samplers import dps as dps_mod
 
     net = DDPMNetwork.from_config(CFG, seed=0, device=cuda)
-    prob = _problem("inpaint", cuda, b=2)
+    prob = _problem("inpaint", cuda, b=dps_mod.GRAPH_AUTO_MAX_BATCH)
     s = DPSSampler(net)
     auto = s(prob, num_sampling_steps=12, gamma=0.5, seed=77)
     assert s.execution == "graph"
