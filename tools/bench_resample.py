@@ -183,6 +183,12 @@ def main():
                     "avg_launch_ms": round(conv["ms"] / conv["count"], 4),
                     "share_of_iteration": round(conv["ms"] / (args.latent_iters * lat_s * 1e3), 4)}
 
+    # one epsilon-form DDIM step alone (the time-travel re-noising steps: UNet forward only)
+    ddim_s = timed(lambda: sampler._ddim_eps(z, ts[5], ts[4], 1.0, None, seed, 5, off), 2, "ddim",
+                   world, rank)
+    projection = project_full_call(len(ts), args.max_iters, args.time_travel_interval, step_s,
+                                   ddim_s, pix_s, lat_s, b * world)
+
     full = None
     if args.full_call:
         # one whole ReSample solve: main loop, time travel (pixel-space hard consistency in
@@ -210,6 +216,14 @@ def main():
     cpu = None
     if args.cpu_baseline and rank == 0:
         cpu = cpu_baseline_resample(args.image)
+        # the same whole call on the host at batch 1, from its two measured iterations (a time-
+        # travel DDIM step priced as a main-loop iteration, the pixel solves' AdamW as free:
+        # both favour the CPU)
+        c = projection
+        cpu_wall = (c["main_loop_iterations"] + c["time_travel_ddim_steps"]) / cpu["value"] + \
+            c["latent_solves"] * args.max_iters * cpu["latent_iter_s"]
+        cpu["projected_full_call_s_batch1"] = round(cpu_wall, 1)
+        cpu["samples_per_s_whole_call"] = round(1 / cpu_wall, 7)
 
     n = b * shape[0] * args.image * args.image
     peak_gib = round(torch.cuda.max_memory_allocated() / 2**30, 1)
@@ -237,9 +251,43 @@ def main():
         "peak_gib": peak_gib,
         "vae_flop_per_sample_step": VAE_FLOP_PER_SAMPLE,
         "roofline": roofline,
+        "ddim_step_ms": round(ddim_s * 1e3, 2),
+        "pixel_iters_timed": args.pixel_iters, "latent_iters_timed": args.latent_iters,
+        "projected_full_call": projection,
         "full_call": full,
         "cpu_baseline": cpu,
     }), flush=True)
+
+
+def project_full_call(n_ts: int, max_iters: int, interval: int, step_s: float, ddim_s: float,
+                      pix_s: float, lat_s: float, batch: int, inter: int = 5, splits: int = 3) -> dict:
+    """A whole ReSampleSampler.__call__ at these settings from the measured per-iteration costs:
+    the sampler's own loop control (samplers/resample.py __call__, resample.py:131-228) walked
+    without running it, counting main-loop iterations, time-travel DDIM steps and the pixel- /
+    latent-space solves, each solve priced at ``max_iters`` AdamW iterations (every solve of the
+    random-init prior ran all of them: profiles/round4/secondary/)."""
+    total = n_ts - 1
+    split = total // splits
+    main = travel = pix = lat = 0
+    for idx in range(n_ts - 1, 1, -1):
+        main += 1
+        if idx <= total - split and idx % interval == 0:
+            travel += sum(1 for kk in range(idx, max(idx - inter, 1), -1) if kk > 1)
+            if idx >= split:
+                pix += 1
+            else:
+                lat += 1
+    lat += 1  # the final latent-space solve
+    parts = {"main_loop": main * step_s, "time_travel_ddim": travel * ddim_s,
+             "pixel_solves": pix * max_iters * pix_s, "latent_solves": lat * max_iters * lat_s}
+    wall = sum(parts.values())
+    return {"main_loop_iterations": main, "time_travel_ddim_steps": travel, "pixel_solves": pix,
+            "latent_solves": lat, "adamw_iterations_per_solve": max_iters,
+            "seconds": {k: round(v, 1) for k, v in parts.items()}, "wall_s": round(wall, 1),
+            "samples_per_s_whole_call": round(batch / wall, 5),
+            "samples_x_guided_steps_per_s": round(batch * (n_ts - 2) / wall, 4),
+            "basis": "measured per-iteration costs of this run x the loop's counts (no solve "
+                     "stopped early: the stopping rules never fired on the random-init prior)"}
 
 
 def cpu_baseline_resample(image: int) -> dict:
