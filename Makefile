@@ -7,7 +7,7 @@ SRC := samplers_amd/csrc/sp_dps.hip samplers_amd/csrc/sp_blur.hip samplers_amd/c
        samplers_amd/csrc/sp_groupnorm.hip samplers_amd/csrc/sp_conv.hip \
        samplers_amd/csrc/sp_wino.hip samplers_amd/csrc/sp_conv_thin.hip \
        samplers_amd/csrc/sp_conv_s2.hip samplers_amd/csrc/sp_upsample.hip \
-       samplers_amd/csrc/sp_attention.hip \
+       samplers_amd/csrc/sp_attention.hip samplers_amd/csrc/sp_attention6.hip \
        samplers_amd/csrc/sp_gemm_x6.hip samplers_amd/csrc/sp_transformer.hip
 OBJ := $(patsubst samplers_amd/csrc/%.hip,build/%.o,$(SRC))
 LIB := samplers_amd/lib/libsamplers_hip.so
@@ -25,7 +25,7 @@ debug: $(DLIB)
 build/sp_wino.o build/debug/sp_wino.o: EXTRA := -fno-slp-vectorize
 # the attention kernels keep their accumulators in VGPRs: in the AGPR form the compiler copied
 # every score / output block between the two register files around each MFMA
-build/sp_attention.o build/debug/sp_attention.o: EXTRA := -mllvm -amdgpu-mfma-vgpr-form=1
+build/sp_attention.o build/debug/sp_attention.o build/sp_attention6.o build/debug/sp_attention6.o: EXTRA := -mllvm -amdgpu-mfma-vgpr-form=1
 
 build/%.o: samplers_amd/csrc/%.hip samplers_amd/csrc/sp_common.h include/samplers_hip.h
 	@mkdir -p build

@@ -496,6 +496,24 @@ int sp_attention_bwd_mh(const float* q, const float* k, const float* v, const fl
                         const float* dout, const float* lse, int64_t batch, int32_t heads, int64_t n,
                         int64_t m, int32_t d, int32_t rs, int32_t rs_kv, int64_t kv_batch, int32_t ro,
                         float scale, float* delta, float* dq, float* dk, float* dv, sp_stream_t stream);
+/* Self-attention forward on the bf16 MFMA datapath over exact three-term splits of the fp32
+ * operands (six partial products per product, fp32 accumulation; error at or below the
+ * exact-fp32 kernel's), head dims 40 / 80, n % 128 == 0; q / k / v rows of stride rs, out rows
+ * of stride ro, lse as sp_attention_fwd_mh.  sp_attention_fwd / _fwd_mh route self-attention
+ * at these shapes here while sp_attention_bf16x6 is on (default; 0: the exact-fp32 kernel,
+ * < 0 query; returns the previous setting). */
+int sp_attention6_supported(int64_t batch, int32_t heads, int64_t n, int32_t d);
+int sp_attention6_fwd_mh(const float* q, const float* k, const float* v, int64_t batch, int32_t heads, int64_t n,
+                         int32_t d, int32_t rs, int32_t ro, float scale, float* out, float* lse,
+                         sp_stream_t stream);
+/* ws (or NULL): sp_attention6_workspace() bytes, where K and V are split into their bf16 terms
+ * once per head instead of once per 128-query workgroup. */
+int64_t sp_attention6_workspace(int64_t batch, int32_t heads, int64_t n, int32_t d);
+int sp_attention6_fwd_ws(const float* q, const float* k, const float* v, int64_t batch, int32_t heads, int64_t n,
+                         int32_t d, int32_t rs, int32_t ro, float scale, float* out, float* lse, void* ws,
+                         int64_t ws_bytes, sp_stream_t stream);
+int sp_attention_bf16x6(int32_t enable);
+int sp_attention_bf16x6_enabled(void);
 
 /* Transformer-block glue of the SD 1.5 eps-UNet (diffusers BasicTransformerBlock,
  * stable_diffusion.py:306-313): torch.nn.LayerNorm over the C channels of token-major rows

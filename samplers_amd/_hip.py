@@ -135,6 +135,14 @@ SIGNATURES = {
     "sp_attention_bwd": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _I64, _I64, ctypes.c_int32, _F,
                                         _P, _P, _P, _P, _P]),
     "sp_attention_mh_supported": (ctypes.c_int, [_I64, ctypes.c_int32, _I64, _I64, ctypes.c_int32]),
+    "sp_attention6_supported": (ctypes.c_int, [_I64, ctypes.c_int32, _I64, ctypes.c_int32]),
+    "sp_attention6_fwd_mh": (ctypes.c_int, [_P, _P, _P, _I64, ctypes.c_int32, _I64, ctypes.c_int32,
+                                            ctypes.c_int32, ctypes.c_int32, _F, _P, _P, _P]),
+    "sp_attention6_workspace": (_I64, [_I64, ctypes.c_int32, _I64, ctypes.c_int32]),
+    "sp_attention6_fwd_ws": (ctypes.c_int, [_P, _P, _P, _I64, ctypes.c_int32, _I64, ctypes.c_int32,
+                                            ctypes.c_int32, ctypes.c_int32, _F, _P, _P, _P, _I64, _P]),
+    "sp_attention_bf16x6": (ctypes.c_int, [ctypes.c_int32]),
+    "sp_attention_bf16x6_enabled": (ctypes.c_int, []),
     "sp_attention_fwd_mh": (ctypes.c_int, [_P, _P, _P, _I64, ctypes.c_int32, _I64, _I64, ctypes.c_int32,
                                            ctypes.c_int32, ctypes.c_int32, _I64, ctypes.c_int32, _F, _P, _P,
                                            _P]),

@@ -575,6 +575,11 @@ int sp_attention_fwd_mh(const float* q, const float* k, const float* v, int64_t 
                         int32_t ro, float scale, float* out, float* lse, sp_stream_t stream) {
     if (!mh_ok(batch, heads, n, m, d, rs, ro, rs_kv, kv_batch) || !q || !k || !v || !out || !lse)
         return SP_EINVAL;
+    // self-attention at the split-bf16 kernel's shapes runs there (sp_attention6.hip) unless
+    // sp_attention_bf16x6(0) asked for the exact-fp32 kernel
+    if (sp_attention_bf16x6_enabled() && m == n && kv_batch == batch && rs_kv == rs &&
+        sp_attention6_supported(batch, heads, n, d))
+        return sp_attention6_fwd_mh(q, k, v, batch, heads, n, d, rs, ro, scale, out, lse, stream);
     hipStream_t s = static_cast<hipStream_t>(stream);
     const int64_t bh = batch * heads;
     const AtKV kv{static_cast<int>(m), rs_kv, kv_batch == 1 && batch > 1};

@@ -101,6 +101,26 @@ def _gemm_backward(q: Tensor, k: Tensor, v: Tensor, out: Tensor, lse: Tensor, do
 FUSED_BWD_MIN_TOKENS = 512
 
 
+def split_bf16_forward(q: Tensor, k: Tensor, v: Tensor, batch: int, heads: int, n: int, d: int, rs: int,
+                       ro: int, scale: float, out: Tensor, lse: Tensor, offsets=(0, 0, 0)) -> bool:
+    """Self-attention forward on the split-bf16 kernel (``csrc/sp_attention6.hip``: fp32 operands
+    as exact three-term bf16 splits on the bf16 MFMAs, error at or below the exact-fp32
+    kernel's) with a workspace for K and V split once per head; False when the library's
+    setting (``sp_attention_bf16x6``) or the shape leaves the call to the fp32 kernel."""
+    from .. import _hip
+
+    lib = _hip.load_library()
+    if not (lib.sp_attention_bf16x6_enabled() and lib.sp_attention6_supported(batch, heads, n, d)):
+        return False
+    nb = int(lib.sp_attention6_workspace(batch, heads, n, d))
+    ws = torch.empty(nb, device=q.device, dtype=torch.uint8)
+    _hip.check(lib.sp_attention6_fwd_ws(q.data_ptr() + offsets[0], k.data_ptr() + offsets[1],
+                                        v.data_ptr() + offsets[2], batch, heads, n, d, rs, ro, scale,
+                                        _hip.ptr(out), _hip.ptr(lse), _hip.ptr(ws), nb, _hip.stream_of(q)),
+               "sp_attention6_fwd_ws")
+    return True
+
+
 class _FusedAttention(torch.autograd.Function):
     """Self-attention on the fused fp32-MFMA kernels (``csrc/sp_attention.hip``): no score
     matrix in HBM, forward or VJP; saves q, k, v, the output and the row log-sum-exp."""
@@ -114,9 +134,10 @@ class _FusedAttention(torch.autograd.Function):
         scale = 1.0 / math.sqrt(d)
         out = torch.empty_like(q)
         lse = torch.empty(bh, n, device=q.device, dtype=q.dtype)
-        _hip.check(lib.sp_attention_fwd(_hip.ptr(q), _hip.ptr(k), _hip.ptr(v), bh, n, d, scale,
-                                        _hip.ptr(out), _hip.ptr(lse), _hip.stream_of(q)),
-                   "sp_attention_fwd")
+        if not split_bf16_forward(q, k, v, bh, 1, n, d, d, d, scale, out, lse):
+            _hip.check(lib.sp_attention_fwd(_hip.ptr(q), _hip.ptr(k), _hip.ptr(v), bh, n, d, scale,
+                                            _hip.ptr(out), _hip.ptr(lse), _hip.stream_of(q)),
+                       "sp_attention_fwd")
         ctx.save_for_backward(q, k, v, out, lse)
         ctx.scale = scale
         return out
@@ -162,9 +183,11 @@ class _FusedQKVAttention(torch.autograd.Function):
         out = torch.empty(b, n, c, device=qkv.device, dtype=torch.float32)
         lse = torch.empty(b * heads, n, device=qkv.device, dtype=torch.float32)
         base = qkv.data_ptr()
-        _hip.check(lib.sp_attention_fwd_mh(base, base + 4 * c, base + 8 * c, b, heads, n, n, d, c3, c3, b, c,
-                                           scale, _hip.ptr(out), _hip.ptr(lse), _hip.stream_of(qkv)),
-                   "sp_attention_fwd_mh")
+        if not split_bf16_forward(qkv, qkv, qkv, b, heads, n, d, c3, c, scale, out, lse,
+                                  offsets=(0, 4 * c, 8 * c)):
+            _hip.check(lib.sp_attention_fwd_mh(base, base + 4 * c, base + 8 * c, b, heads, n, n, d, c3, c3, b,
+                                               c, scale, _hip.ptr(out), _hip.ptr(lse), _hip.stream_of(qkv)),
+                       "sp_attention_fwd_mh")
         ctx.save_for_backward(qkv, out, lse)
         ctx.heads, ctx.scale = heads, scale
         return out

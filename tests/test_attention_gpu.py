@@ -56,7 +56,7 @@ def test_fused_self_attention_matches_fp64(cuda, bh, n, d):
         grads = torch.autograd.grad(out, (qg, kg, vg), do.to(cuda))
         torch.cuda.synchronize()
     names = {e.name for e in prof.events() if e.device_type.name == "CUDA"}
-    assert any("k_attn_fwd" in x for x in names)
+    assert any("k_attn_fwd" in x or "k_attn6_fwd" in x for x in names)
     fused_bwd = n >= FUSED_BWD_MIN_TOKENS
     assert any("k_attn_dkv" in x for x in names) == fused_bwd
     if fused_bwd:
@@ -91,3 +91,60 @@ def test_fused_attention_falls_back_for_cross_attention(cuda):
     assert not fused_supported(q, k)
     out = attention(q, k, torch.randn(2, 77, 40, device=cuda))
     assert out.shape == q.shape
+
+
+@pytest.mark.parametrize("b,heads,n,d", [(2, 4, 4096, 40), (3, 2, 1024, 80), (1, 8, 256, 40)])
+def test_split_bf16_attention_forward_no_worse_than_fp32(cuda, b, heads, n, d, parity_record):
+    """The split-bf16 forward (csrc/sp_attention6.hip, the default for self-attention at head
+    dims 40 / 80) on the fused projection's strided layout (q, k, v the thirds of one
+    [b][n][3 heads d] tensor) against fp64: its error is no worse than the exact-fp32 kernel's
+    on the same inputs (both measured here; bound 1.25x + 1e-8), output and lse, and < 1e-5."""
+    from samplers_amd import _hip
+
+    lib = _hip.load_library()
+    c = heads * d
+    g = torch.Generator().manual_seed(n + d)
+    qkv = torch.randn(b, n, 3 * c, generator=g) * 1.5
+    q, k, v = (qkv[..., i * c:(i + 1) * c].reshape(b, n, heads, d).transpose(1, 2).double() for i in range(3))
+    s = (q @ k.transpose(-1, -2)) / d ** 0.5
+    ref = (torch.softmax(s, dim=-1) @ v).transpose(1, 2).reshape(b, n, c)
+    lse_ref = torch.logsumexp(s, dim=-1).reshape(b * heads, n)
+    x = qkv.to(cuda)
+    base = x.data_ptr()
+    res, outs = {}, {}
+    prev = lib.sp_attention_bf16x6(-1)
+    try:
+        for mode in ("ws", 1, 0):  # split-bf16 with pre-split K / V, in-kernel split, exact fp32
+            lib.sp_attention_bf16x6(0 if mode == 0 else 1)
+            out = torch.full((b, n, c), float("nan"), device=cuda)
+            lse = torch.full((b * heads, n), float("nan"), device=cuda)
+            if mode == "ws":
+                nb = lib.sp_attention6_workspace(b, heads, n, d)
+                ws = torch.full((nb,), 255, dtype=torch.uint8, device=cuda)  # NaN patterns until written
+                _hip.check(lib.sp_attention6_fwd_ws(base, base + 4 * c, base + 8 * c, b, heads, n, d, 3 * c, c,
+                                                    d ** -0.5, _hip.ptr(out), _hip.ptr(lse), _hip.ptr(ws), nb,
+                                                    None), "fwd_ws")
+            else:
+                _hip.check(lib.sp_attention_fwd_mh(base, base + 4 * c, base + 8 * c, b, heads, n, n, d, 3 * c,
+                                                   3 * c, b, c, d ** -0.5, _hip.ptr(out), _hip.ptr(lse), None),
+                           "fwd")
+            torch.cuda.synchronize()
+            outs[mode] = (out, lse)
+            res[mode] = (_rel(out.cpu().double(), ref), float((lse.cpu().double() - lse_ref).abs().max()))
+    finally:
+        lib.sp_attention_bf16x6(prev)
+    # the same split terms in the same order either way
+    assert torch.equal(outs["ws"][0], outs[1][0]) and torch.equal(outs["ws"][1], outs[1][1])
+    (e6, l6), (e32, l32) = res[1], res[0]
+    parity_record("attn_fwd_rel_l2", e6, 1e-5, kernel="split-bf16", fp32_kernel=e32, n=n, d=d)
+    assert e6 < 1e-5 and e6 <= 1.25 * e32 + 1e-8, (e6, e32)
+    assert l6 <= 1.25 * l32 + 1e-6, (l6, l32)
+
+
+def test_split_bf16_attention_supported_shapes(cuda):
+    from samplers_amd import _hip
+
+    lib = _hip.load_library()
+    assert lib.sp_attention6_supported(32, 8, 4096, 40) and lib.sp_attention6_supported(32, 8, 1024, 80)
+    assert not lib.sp_attention6_supported(32, 8, 256, 160)  # d = 160: the fp32 kernel
+    assert not lib.sp_attention6_supported(2, 8, 200, 40)    # n % 128

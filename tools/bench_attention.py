@@ -30,8 +30,13 @@ def timed(fn, reps=3):
 
 
 def main():
+    from samplers_amd import _hip
+
     dev = torch.device("cuda:0")
-    for bh, n, d in SHAPES:
+    lib = _hip.load_library()
+    modes = sys.argv[1:] or ["x6", "fp32"]  # the forward's kernel: split-bf16 (pre-split K / V) or exact fp32
+    for (bh, n, d), mode in [(sh, md) for sh in SHAPES for md in modes]:
+        lib.sp_attention_bf16x6(1 if mode == "x6" else 0)
         g = torch.Generator(device=dev).manual_seed(0)
         q, k, v = (torch.randn(bh, n, d, device=dev, generator=g).requires_grad_() for _ in range(3))
         do = torch.randn(bh, n, d, device=dev, generator=g)
@@ -46,7 +51,7 @@ def main():
 
         tf, tb = timed(fwd), timed(fwd_bwd)
         flop = 4.0 * bh * n * n * d
-        print(json.dumps({"bh": bh, "n": n, "d": d, "fwd_ms": round(tf, 3),
+        print(json.dumps({"bh": bh, "n": n, "d": d, "fwd_kernel": mode, "fwd_ms": round(tf, 3),
                           "fwd_bwd_ms": round(tb, 3), "fwd_tflops": round(flop / tf / 1e9, 1),
                           "fwd_bwd_tflops": round(3.5 * flop / tb / 1e9, 1)}), flush=True)
 
