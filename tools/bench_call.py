@@ -1,0 +1,64 @@
+"""A whole ``DPSSampler.__call__`` at its defaults (BASELINE configs[0]: identity operator,
+GaussianNoise(0.05), the ddpm-celebahq-256 prior, batch 1 on the GPU), timed end to end:
+
+    python tools/bench_call.py [--batch 1 --steps 1000]
+
+Reports the wall time of one call (after an untimed one: MIOpen / allocator warm-up and, on the
+default path, the step's hipGraph capture happen inside every call and are included), the time
+per guided iteration (``steps - 2`` of them, ``dps.py:90-122``), the execution the default
+chose (``DPSSampler.execution``: hipGraph replay at batch 1, eager above) and the same call
+forced eager (``graph=False``).  One JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import sys
+import time
+from pathlib import Path
+
+sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+import torch  # noqa: E402
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("--batch", type=int, default=1)
+    p.add_argument("--steps", type=int, default=1000)
+    p.add_argument("--image", type=int, default=256)
+    args = p.parse_args()
+    from samplers_amd.inverse_problem import InverseProblem
+    from samplers_amd.networks.ddpm import DDPMNetwork
+    from samplers_amd.noise import GaussianNoise
+    from samplers_amd.operators import IdentityOperator
+    from samplers_amd.samplers import DPSSampler
+
+    dev = torch.device("cuda:0")
+    shape = (3, args.image, args.image)
+    gen = torch.Generator().manual_seed(7)
+    x_true = torch.rand((args.batch, *shape), generator=gen) * 2 - 1
+    y = (x_true + 0.05 * torch.randn(x_true.shape, generator=gen)).to(dev)
+    prob = InverseProblem(IdentityOperator(shape), y, GaussianNoise(0.05).to(dev))
+    net = DDPMNetwork.from_config(seed=0, device=dev)
+    sampler = DPSSampler(net)
+    rec = {"workload": f"DPS + Identity + GaussianNoise(0.05), 3x{args.image}², batch {args.batch}, "
+                       f"{args.steps}-step schedule ({args.steps - 2} guided iterations), "
+                       "ddpm-celebahq-256 architecture (random init)"}
+    for label, kw in (("default", {}), ("eager", {"graph": False})):
+        sampler(prob, num_sampling_steps=args.steps, seed=1, **kw)  # warm
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        out = sampler(prob, num_sampling_steps=args.steps, seed=1, **kw)
+        torch.cuda.synchronize()
+        wall = time.perf_counter() - t0
+        if not torch.isfinite(out).all():
+            raise SystemExit("non-finite result")
+        rec[label] = {"execution": sampler.execution, "call_s": round(wall, 4),
+                      "ms_per_guided_step": round(wall / (args.steps - 2) * 1e3, 3),
+                      "samples_per_s": round(args.batch * (args.steps - 2) / wall, 2)}
+        print(f"[bench_call] {label}: {rec[label]}", file=sys.stderr, flush=True)
+    print(json.dumps(rec), flush=True)
+
+
+if __name__ == "__main__":
+    main()
