@@ -105,6 +105,54 @@ def temb_projections(model: nn.Module, emb: Tensor) -> dict[int, Tensor]:
     return out
 
 
+def timestep_rows(model: nn.Module, timestep: Tensor | int, sample: Tensor) -> tuple[Tensor, dict] | None:
+    """(emb, {block: time_emb_proj(silu(emb))}) of a UNet (``UNet2DModel``,
+    ``UNet2DConditionModel``: a ``time_embedding`` MLP, ResnetBlock2D projections) for a host
+    timestep from a table over t = 0 .. T-1 built once per device / dtype / weight version (frozen time-embedding
+    weights only): a step then launches no sinusoid, MLP or projection kernels and copies
+    no timestep to the device (at batch 1 each is a host-bound launch; the H2D copy of a
+    pageable tensor also waits on the stream).  At batch 1 the rows are views of the table;
+    at larger batches the table row is broadcast to the batch (one copy per projection
+    width), so the values are the same at every batch size (a projection recomputed at M = B
+    rows would round differently from the table's M = T: DESIGN.md §6).  None (the per-step
+    path) for device or per-sample timesteps, or trainable weights."""
+    if torch.is_tensor(timestep):
+        if timestep.is_cuda or timestep.numel() != 1 or timestep.is_floating_point():
+            return None
+        t = int(timestep.reshape(-1)[0])
+    elif isinstance(timestep, int):
+        t = timestep
+    else:
+        return None
+    params = model.__dict__.get("_t_params")
+    if params is None:  # the module tree is fixed after construction
+        blocks = [m for m in model.modules() if isinstance(m, ResnetBlock2D) and m.time_emb_proj is not None]
+        params = list(model.time_embedding.parameters()) + [p for b in blocks for p in b.time_emb_proj.parameters()]
+        model.__dict__["_t_params"] = params
+    if t < 0 or not sample.is_cuda or any(p.requires_grad for p in params):
+        return None
+    key = (sample.device, sample.dtype, tuple((p.data_ptr(), p._version) for p in params))
+    tab = model.__dict__.get("_t_rows")
+    if tab is None or tab[0] != key or t >= tab[1].shape[0]:
+        cfg = model.config
+        with torch.no_grad():
+            ts = torch.arange(max(1000, t + 1), device=sample.device)
+            t_emb = timestep_embedding(ts, cfg.block_out_channels[0], flip_sin_to_cos=cfg.flip_sin_to_cos,
+                                       freq_shift=cfg.freq_shift).to(sample.dtype)
+            emb_all = model.time_embedding(t_emb)
+            tab = (key, emb_all, temb_projection_groups(model, emb_all))
+        model.__dict__["_t_rows"] = tab
+    _, emb_all, groups = tab
+    b = sample.shape[0]
+    out = {}
+    for ids, y in groups:  # y: [blocks][T][C]
+        rows = y[:, t:t + 1]
+        if b > 1:
+            rows = rows.expand(len(ids), b, y.shape[2]).contiguous()
+        out.update(zip(ids, rows.unbind(0)))
+    return emb_all[t:t + 1].expand(b, -1), out
+
+
 class TimestepEmbedding(nn.Module):
     def __init__(self, in_dim: int, out_dim: int) -> None:
         super().__init__()
@@ -627,50 +675,7 @@ class UNet2DModel(nn.Module):
         self.conv_out = Conv3x3(ch[0], config.out_channels)
 
     def _timestep_rows(self, timestep: Tensor | int, sample: Tensor) -> tuple[Tensor, dict] | None:
-        """(emb, {block: time_emb_proj(silu(emb))}) for a host timestep from a table over
-        t = 0 .. T-1 built once per device / dtype / weight version (frozen time-embedding
-        weights only): a step then launches no sinusoid, MLP or projection kernels and copies
-        no timestep to the device (at batch 1 each is a host-bound launch; the H2D copy of a
-        pageable tensor also waits on the stream).  At batch 1 the rows are views of the table;
-        at larger batches the table row is broadcast to the batch (one copy per projection
-        width), so the values are the same at every batch size (a projection recomputed at M = B
-        rows would round differently from the table's M = T: DESIGN.md §6).  None (the per-step
-        path) for device or per-sample timesteps, or trainable weights."""
-        if torch.is_tensor(timestep):
-            if timestep.is_cuda or timestep.numel() != 1 or timestep.is_floating_point():
-                return None
-            t = int(timestep.reshape(-1)[0])
-        elif isinstance(timestep, int):
-            t = timestep
-        else:
-            return None
-        params = self.__dict__.get("_t_params")
-        if params is None:  # the module tree is fixed after construction
-            blocks = [m for m in self.modules() if isinstance(m, ResnetBlock2D) and m.time_emb_proj is not None]
-            params = list(self.time_embedding.parameters()) + [p for b in blocks for p in b.time_emb_proj.parameters()]
-            self.__dict__["_t_params"] = params
-        if t < 0 or not sample.is_cuda or any(p.requires_grad for p in params):
-            return None
-        key = (sample.device, sample.dtype, tuple((p.data_ptr(), p._version) for p in params))
-        tab = self.__dict__.get("_t_rows")
-        if tab is None or tab[0] != key or t >= tab[1].shape[0]:
-            cfg = self.config
-            with torch.no_grad():
-                ts = torch.arange(max(1000, t + 1), device=sample.device)
-                t_emb = timestep_embedding(ts, cfg.block_out_channels[0], flip_sin_to_cos=cfg.flip_sin_to_cos,
-                                           freq_shift=cfg.freq_shift).to(sample.dtype)
-                emb_all = self.time_embedding(t_emb)
-                tab = (key, emb_all, temb_projection_groups(self, emb_all))
-            self.__dict__["_t_rows"] = tab
-        _, emb_all, groups = tab
-        b = sample.shape[0]
-        out = {}
-        for ids, y in groups:  # y: [blocks][T][C]
-            rows = y[:, t:t + 1]
-            if b > 1:
-                rows = rows.expand(len(ids), b, y.shape[2]).contiguous()
-            out.update(zip(ids, rows.unbind(0)))
-        return emb_all[t:t + 1].expand(b, -1), out
+        return timestep_rows(self, timestep, sample)
 
     def forward(self, sample: Tensor, timestep: Tensor | int) -> Tensor:
         cfg = self.config

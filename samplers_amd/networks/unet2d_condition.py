@@ -36,7 +36,8 @@ from .attention import (attention, fused_cross_attention, fused_cross_supported,
                         fused_qkv_supported)
 from .layers import (Conv3x3, GroupNormAct, LayerNorm, Linear, SkipGrad, conv3x3_stride2, geglu,
                      linear, proj_nchw_to_tokens, proj_tokens_to_nchw)
-from .unet2d import ResnetBlock2D, TimestepEmbedding, Upsample2D, temb_projections, timestep_embedding
+from .unet2d import (ResnetBlock2D, TimestepEmbedding, Upsample2D, temb_projections, timestep_embedding,
+                     timestep_rows)
 
 
 @dataclass(frozen=True)
@@ -274,14 +275,18 @@ class UNet2DConditionModel(nn.Module):
     def forward(self, sample: Tensor, timestep: Tensor | int, encoder_hidden_states: Tensor) -> Tensor:
         cfg = self.config
         b = sample.shape[0]
-        if not torch.is_tensor(timestep):
-            timestep = torch.tensor([timestep], dtype=torch.long, device=sample.device)
-        timestep = timestep.reshape(-1).to(sample.device).expand(b)
-        t_emb = timestep_embedding(timestep, cfg.block_out_channels[0],
-                                   flip_sin_to_cos=cfg.flip_sin_to_cos,
-                                   freq_shift=cfg.freq_shift).to(sample.dtype)
-        emb = self.time_embedding(t_emb)
-        tbs = temb_projections(self, emb)  # every block's time-embedding projection at once
+        table = timestep_rows(self, timestep, sample)  # host timestep: rows of a table over t
+        if table is not None:
+            emb, tbs = table
+        else:
+            if not torch.is_tensor(timestep):
+                timestep = torch.tensor([timestep], dtype=torch.long, device=sample.device)
+            timestep = timestep.reshape(-1).to(sample.device).expand(b)
+            t_emb = timestep_embedding(timestep, cfg.block_out_channels[0],
+                                       flip_sin_to_cos=cfg.flip_sin_to_cos,
+                                       freq_shift=cfg.freq_shift).to(sample.dtype)
+            emb = self.time_embedding(t_emb)
+            tbs = temb_projections(self, emb)  # every block's time-embedding projection at once
         ctx = encoder_hidden_states.to(sample.dtype)
 
         # skip tensors' two gradients meet inside the down-path consumer's VJP kernel
