@@ -364,12 +364,14 @@ def make_dps_step(network, inverse_problem, observation_rows, y_div, **kw):
     return GenericDPSStep(network, inverse_problem, observation_rows, y_div, **kw)
 
 
-# hipGraph replay by default (tools/graph_sweep.sh, profiles/round5/graph_sweep/): at a
-# flat batch of 1 a step is host-bound (a few hundred short launches): 13.3 ms eager, 9.9 ms
-# replayed; from 2 on the GPU sets the step and the eager one wins (14.0 vs 14.2 ms at 2, 142 vs
-# 153 ms at 32: a captured GroupNorm runs its two-pass kernels).  Capture costs about three
-# steps (two warm-up steps and the capture), so short solves stay eager.
-GRAPH_AUTO_MAX_BATCH = 1
+# hipGraph replay by default where it pays: below GRAPH_AUTO_MAX_BATCH samples.
+# Measured (profiles/round5/final/bench_call_b1.json): a whole 1000-step call at batch 1 runs
+# 9.47 ms per step eager and 10.05 ms replayed — the captured step runs GroupNorm's two-pass
+# kernels, and the eager step is no longer host-bound once no per-launch timing events are
+# attached (bench.py's B = 1 eager figure, 11.4 ms, carries them); from batch 2 on the eager step
+# wins by more (tools/graph_sweep.sh).  So the automatic choice is off (0); graph=True replays.
+# Capture costs about three steps (two warm-up steps and the capture), so short solves stay eager.
+GRAPH_AUTO_MAX_BATCH = 0
 GRAPH_AUTO_MIN_STEPS = 8
 
 

@@ -76,14 +76,16 @@ def test_timestep_table_matches_per_step_embedding(cuda, b):
     assert unet._timestep_rows(torch.tensor([5], device=cuda), x) is None
 
 
-def test_default_replays_small_batches_and_matches_eager(cuda):
+def test_default_replays_small_batches_and_matches_eager(cuda, monkeypatch):
     """DPSSampler(graph=None) — the default — replays a captured step for this project's prior
-    at a small batch with enough steps (samples equal to the eager solve), stays eager for a
-    larger batch, few steps, a callback or a third-party network."""
+    below GRAPH_AUTO_MAX_BATCH samples with enough steps (samples equal to the eager solve), and
+    stays eager for a larger batch, few steps, a callback or a third-party network.  (The shipped
+    threshold is 0 — eager measured faster, dps.py — so the rule is exercised at 1 here.)"""
     from samplers_amd.samplers import dps as dps_mod
 
+    monkeypatch.setattr(dps_mod, "GRAPH_AUTO_MAX_BATCH", 1)
     net = DDPMNetwork.from_config(CFG, seed=0, device=cuda)
-    prob = _problem("inpaint", cuda, b=dps_mod.GRAPH_AUTO_MAX_BATCH)
+    prob = _problem("inpaint", cuda, b=1)
     s = DPSSampler(net)
     auto = s(prob, num_sampling_steps=12, gamma=0.5, seed=77)
     assert s.execution == "graph"
@@ -105,3 +107,12 @@ def test_graph_with_callback_raises(cuda):
     with pytest.raises(ValueError, match="callback"):
         DPSSampler(net)(_problem("identity", cuda), num_sampling_steps=8, graph=True,
                         callback=lambda i, x: None)
+
+
+def test_default_is_eager_at_the_shipped_threshold(cuda):
+    from samplers_amd.samplers import dps as dps_mod
+
+    net = DDPMNetwork.from_config(CFG, seed=0, device=cuda)
+    s = DPSSampler(net)
+    s(_problem("identity", cuda, b=1), num_sampling_steps=12, gamma=0.5, seed=3)
+    assert s.execution == ("graph" if dps_mod.GRAPH_AUTO_MAX_BATCH >= 1 else "eager")
