@@ -283,3 +283,38 @@ def test_pixel_optimization_device_stop_matches_reference_loop(cuda, kind):
     one_more, _ = reference(stop_at + 2)
     assert err < 1e-5, err
     assert float((one_more - ref).norm() / ref.norm()) > 100 * max(err, 1e-7)
+
+
+@pytest.mark.parametrize("steps,interval", [(30, 10), (24, 5), (101, 10)])
+def test_resample_whole_call_projection_counts_match_the_sampler(cuda, steps, interval):
+    """tools/bench_resample.py projects a whole ReSample call from per-iteration costs times the
+    loop's counts (project_full_call walks resample.py's loop control without running it).  The
+    counts must be the sampler's own: the pixel- and latent-space solves its optimization_log
+    records, run here with stand-in priors (max_optimization_iters = 2: a few launches each)."""
+    import importlib.util
+    import pathlib
+
+    from samplers_amd.inverse_problem import InverseProblem
+    from samplers_amd.noise import PoissonNoise
+    from samplers_amd.operators import IdentityOperator
+    from samplers_amd.samplers.resample import ReSampleSampler
+
+    path = pathlib.Path(__file__).resolve().parents[1] / "tools" / "bench_resample.py"
+    spec = importlib.util.spec_from_file_location("bench_resample_tool", path)
+    tool = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(tool)
+    shape = (3, 16, 16)
+    net = si.make_samplers_amd_latent_net("linear", 0.1, device=cuda)
+    x = si.fixture_x_true(1, shape, 3)
+    y = torch.poisson((x + 1) * 8, generator=torch.Generator().manual_seed(4)) / 8 - 1
+    prob = InverseProblem(IdentityOperator(shape), y.to(cuda), PoissonNoise(1.0).to(cuda))
+    sampler = ReSampleSampler(net)
+    sampler(prob, num_sampling_steps=steps, max_optimization_iters=2, time_travel_interval=interval,
+            seed=5)
+    log = sampler.optimization_log
+    net.set_sampling_parameters(steps, batch_size=1)
+    proj = tool.project_full_call(len(net.timesteps_host), 2, interval, 1.0, 1.0, 1.0, 1.0, 1)
+    assert proj["pixel_solves"] == sum(r["kind"] == "pixel" for r in log)
+    assert proj["latent_solves"] == sum(r["kind"] == "latent" for r in log)
+    assert proj["main_loop_iterations"] == len(net.timesteps_host) - 2
+    assert all(r["loop_trips"] >= r["iterations"] for r in log)

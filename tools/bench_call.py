@@ -8,8 +8,9 @@ iterations over the wall time of the call, the final prediction included:
 Reports the wall time of one call (after an untimed one: MIOpen / allocator warm-up and, on the
 default path, the step's hipGraph capture happen inside every call and are included), the time
 per guided iteration (``steps - 2`` of them, ``dps.py:90-122``), the execution the default
-chose (``DPSSampler.execution``: hipGraph replay at batch 1, eager above) and the same call
-forced eager (``graph=False``).  One JSON line.
+chose (``DPSSampler.execution``: eager at every batch with the shipped
+``GRAPH_AUTO_MAX_BATCH = 0``; ``SAMPLERS_AMD_GRAPH=1`` opts in to hipGraph replay) and the same
+call forced eager (``graph=False``).  One JSON line.
 """
 from __future__ import annotations
 
