@@ -17,6 +17,7 @@ from __future__ import annotations
 import argparse
 import json
 import sys
+import threading
 import time
 from pathlib import Path
 
@@ -33,6 +34,15 @@ def main():
     p.add_argument("--modes", default="default,eager", help="default (graph=None) and / or eager")
     p.add_argument("--warm-steps", type=int, default=0, help="steps of the untimed call (0: --steps)")
     args = p.parse_args()
+    # a long call (configs[1]: ~5 min) prints nothing until it ends: report progress every 30 s
+    start = time.perf_counter()
+
+    def heartbeat():
+        while True:
+            time.sleep(30)
+            print(f"[bench_call] {time.perf_counter() - start:.0f} s", file=sys.stderr, flush=True)
+
+    threading.Thread(target=heartbeat, daemon=True).start()
     from samplers_amd.inverse_problem import InverseProblem
     from samplers_amd.networks.ddpm import DDPMNetwork
     from samplers_amd.noise import GaussianNoise
