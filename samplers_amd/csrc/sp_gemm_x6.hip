@@ -41,8 +41,18 @@ typedef __attribute__((address_space(3))) void lds_void_g;
 #endif
 #ifndef G6_EXP
 #define G6_EXP 0  // diagnostics only (wrong results, timing): 1 no MFMAs, 2 no split, 3 no loads,
-                  // 4 no output stores, 5 X loads from one cached 2 KB (no X stream from HBM)
+                  // 4 no output stores, 5 X loads from one cached 2 KB (no X stream from HBM),
+                  // 6 MFMAs only (no loads, no split, no stores)
 #endif
+#define G6_NO_SPLIT (G6_EXP == 2 || G6_EXP == 6)
+#define G6_NO_LOADS (G6_EXP == 3 || G6_EXP == 6)
+#define G6_NO_STORES (G6_EXP == 4 || G6_EXP == 6)
+#ifndef G6_W4
+#define G6_W4 0  // 4 waves (one per SIMD), each 128 channels x 64 pixels, instead of 8 x (64 x 64)
+#endif
+constexpr int G6_WAVES = G6_W4 ? 4 : 8;
+constexpr int G6_NA = G6_W4 ? 4 : 2;        // 32-channel blocks per wave
+constexpr int G6_XP = 16 / G6_WAVES;        // X pieces (1 KB) per wave and k-step
 constexpr int G6_CO = 128;     // output channels per workgroup
 constexpr int G6_PX = 256;     // pixels per workgroup
 constexpr int G6_KC = 16;      // input channels per k-step
@@ -113,12 +123,12 @@ __device__ __forceinline__ void g6_dma_x(const G6Geom& g, const float* xb1, cons
                                          int p0, int kstep, int wv, int lane, unsigned slot) {
     const int k0 = kstep * G6_KC;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-        const int c = k0 + 2 * wv + i;
+    for (int i = 0; i < G6_XP; ++i) {
+        const int c = k0 + G6_XP * wv + i;
         const bool second = c >= g.c1;
         const auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(second ? xb2 : xb1), (short)0,
                                                           (second ? g.c2 : g.c1) * g.hw * 4, 0x00020000);
-        g6_lds_dma(rs, slot + (2 * wv + i) * 1024, lane * 16, ((second ? c - g.c1 : c) * g.hw + p0) * 4);
+        g6_lds_dma(rs, slot + (G6_XP * wv + i) * 1024, lane * 16, ((second ? c - g.c1 : c) * g.hw + p0) * 4);
     }
 }
 
@@ -130,9 +140,9 @@ __device__ __forceinline__ void g6_dma_x_tm(const G6Geom& g, int p0, int kstep, 
                                                       0x00020000);
     const int vo = ((lane >> 2) * g.c1 + 4 * (lane & 3)) * 4;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-        const int t0 = p0 + 16 * (2 * wv + i);
-        g6_lds_dma(rs, slot + (2 * wv + i) * 1024, vo, (t0 * g.c1 + kstep * G6_KC) * 4);
+    for (int i = 0; i < G6_XP; ++i) {
+        const int t0 = p0 + 16 * (G6_XP * wv + i);
+        g6_lds_dma(rs, slot + (G6_XP * wv + i) * 1024, vo, (t0 * g.c1 + kstep * G6_KC) * 4);
     }
 }
 
@@ -141,20 +151,23 @@ __device__ __forceinline__ void g6_dma_x_tm(const G6Geom& g, int p0, int kstep, 
 __device__ __forceinline__ void g6_dma_w(__amdgpu_buffer_rsrc_t wrs, int stage, int wv, int lane,
                                          unsigned wb) {
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-        const int chunk = i == 0 ? wv : 8 + wv;
+    for (int i = 0; i < (12 + G6_WAVES - 1) / G6_WAVES; ++i) {
+        const int chunk = wv + G6_WAVES * i;
         if (chunk < 12)
             g6_lds_dma(wrs, wb + chunk * 1024, lane * 16, stage * G6_WB + chunk * 1024);
     }
 }
-// vm ops a wave issues per k-step (2 X + 2 or 1 W)
-__device__ __forceinline__ int g6_dma_per_wave(int wv) { return wv < 4 ? 4 : 3; }
+// vm ops a wave issues per k-step (8 waves: 2 X + 2 or 1 W; 4 waves: 4 X + 3 W)
+__device__ __forceinline__ int g6_dma_per_wave(int wv) { return G6_W4 ? 7 : wv < 4 ? 4 : 3; }
+// loads younger than W(j + 2) at the end of step j: X(j + 4), W(j + 3), X(j + 5)
+constexpr int G6_YOUNG_A = G6_W4 ? 11 : 6;  // waves with the larger W share (all of them at 4 waves)
+constexpr int G6_YOUNG_B = G6_W4 ? 11 : 5;
 
 // eight fp32 values (channels c0 .. c0 + 7 of one pixel) -> the lane's three bf16 term fragments
 __device__ __forceinline__ void g6_split8(const float (&v)[8], uvec4 (&t)[3]) {
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-#if G6_EXP == 2
+#if G6_NO_SPLIT
         const unsigned a = __float_as_uint(v[2 * q]), b = __float_as_uint(v[2 * q + 1]);
         t[0][q] = t[1][q] = t[2][q] = g6_pack(a, b);
 #else
@@ -219,12 +232,12 @@ __device__ __forceinline__ G6Pos g6_pos(const G6Geom& g, int t) {
 // stores issued (the caller's wait count for the next k-step).
 template <bool PAR>
 __device__ __forceinline__ int g6_epilogue(const G6Geom& g, int n, int cb, int px0, int ch, int lane,
-                                           const f32x16 (&acc)[2][2], const f32x16 (&acs)[2][2]) {
+                                           const f32x16 (&acc)[G6_NA][2], const f32x16 (&acs)[G6_NA][2]) {
     int nst = 0;
     const int vo = (px0 + 2 * (lane & 31)) * 4;
 #pragma unroll
-    for (int a = 0; a < 2; ++a) {
-        const int co0 = cb * G6_CO + 32 * (2 * ch + a);  // first channel of the 32-block
+    for (int a = 0; a < G6_NA; ++a) {
+        const int co0 = cb * G6_CO + 32 * (G6_NA * ch + a);  // first channel of the 32-block
         if (co0 >= g.o1 + g.o2) continue;  // padded rows of W (uniform)
         const bool second = co0 >= g.o1;
         float* yb = second ? g.y2 + ((int64_t)n * g.o2 + (co0 - g.o1)) * g.hw
@@ -282,7 +295,7 @@ __device__ __forceinline__ int g6_epilogue(const G6Geom& g, int n, int cb, int p
             const float bv = (lane >> 5) ? b1 : b0;
             const int cc = c + 4 * (lane >> 5);
             const f32x2 y = {(acc[a][0][q] + acs[a][0][q]) + bv + rv[q].x, (acc[a][1][q] + acs[a][1][q]) + bv + rv[q].y};
-#if G6_EXP == 4
+#if G6_NO_STORES
             if (g.hw >= 0) continue;  // never true at run time: the stores are skipped, all math kept
 #endif
             __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(uvec2, y), ors, vo + cc * g.hw * 4, 0, 0);
@@ -299,16 +312,16 @@ __device__ __forceinline__ int g6_epilogue(const G6Geom& g, int n, int cb, int p
 // contiguous bytes).  Returns the stores issued.
 template <bool PAR>
 __device__ __forceinline__ int g6_epilogue_tm(const G6Geom& g, const G6Pos& ps, int ch, int pq, int lane,
-                                               const f32x16 (&acc)[2][2], const f32x16 (&acs)[2][2]) {
+                                               const f32x16 (&acc)[G6_NA][2], const f32x16 (&acs)[G6_NA][2]) {
     const auto ors = __builtin_amdgcn_make_buffer_rsrc(g.y1, (short)0, g.tokens * g.o1 * 4, 0x00020000);
     const auto rrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(g.res ? g.res : g.y1), (short)0,
                                                        g.res ? g.tokens * g.o1 * 4 : 0, 0x00020000);
     const int tok0 = ps.n * g.hw + ps.p0;  // first token row of the tile (image n's plane)
     int nst = 0;
 #pragma unroll
-    for (int a = 0; a < 2; ++a) {
-        const int o = ps.cb * G6_CO + 32 * (2 * ch + a) + (lane & 31);
-        if (ps.cb * G6_CO + 32 * (2 * ch + a) >= g.o1) continue;  // padded rows of W (uniform)
+    for (int a = 0; a < G6_NA; ++a) {
+        const int o = ps.cb * G6_CO + 32 * (G6_NA * ch + a) + (lane & 31);
+        if (ps.cb * G6_CO + 32 * (G6_NA * ch + a) >= g.o1) continue;  // padded rows of W (uniform)
         const float bv = g.bias ? g.bias[o] : 0.f;
 #pragma unroll
         for (int b = 0; b < 2; ++b) {
@@ -326,7 +339,7 @@ __device__ __forceinline__ int g6_epilogue_tm(const G6Geom& g, const G6Pos& ps, 
 #pragma unroll
             for (int q = 0; q < 16; ++q) {
                 const float y = (acc[a][b][q] + acs[a][b][q]) + bv + rv[q];
-#if G6_EXP == 4
+#if G6_NO_STORES
                 if (g.hw >= 0) continue;  // never true at run time: the stores are skipped, all math kept
 #endif
                 __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(y), ors,
@@ -344,7 +357,7 @@ __device__ __forceinline__ int g6_epilogue_tm(const G6Geom& g, const G6Pos& ps, 
 // in a 6-slot and W in a 4-slot LDS ring filled by direct loads), and each wave reads its
 // fragments of step j + 1 from LDS into registers during them too: the workgroup's barrier
 // aligns all eight waves' phases, so LDS reads issued after it would leave the MFMAs idle.
-constexpr int G6_THREADS = 512;
+constexpr int G6_THREADS = 64 * G6_WAVES;
 
 #ifndef G6_STAGGER
 #define G6_STAGGER 1  // the second wave of each SIMD issues its loads half-way through its MFMAs
@@ -364,7 +377,8 @@ template <bool LTM, bool STM, bool LATE, bool SPLIT>
 __device__ __forceinline__ void g6_body(const G6Geom& g, G6XSlot* xraw, G6WSlot* wl, int wv) {
     const int kper = SPLIT ? g.kper : g.nsteps;  // k-steps per work item
     const int tid = threadIdx.x, lane = tid & 63;
-    const int ch = wv & 1, pq = wv >> 1;  // 64 output channels x 64 pixels
+    // 8 waves: 64 output channels (block ch) x 64 pixels (quarter pq); 4 waves: 128 x 64
+    const int ch = G6_W4 ? 0 : wv & 1, pq = G6_W4 ? wv : wv >> 1;
     const auto wrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<unsigned short*>(g.wp), (short)0,
                                                        g.cob * g.nsteps * G6_WB, 0x00020000);
     const unsigned xraw_lds = static_cast<unsigned>(reinterpret_cast<size_t>((lds_void_g*)&xraw[0][0]));
@@ -421,23 +435,25 @@ __device__ __forceinline__ void g6_body(const G6Geom& g, G6XSlot* xraw, G6WSlot*
     __builtin_amdgcn_s_waitcnt(g6_vmcnt(0));
     __builtin_amdgcn_s_barrier();
 
-    const bool four = g6_dma_per_wave(wv) == 4;  // this wave's W loads per step: 2 (else 1)
+    const bool four = G6_W4 || g6_dma_per_wave(wv) == 4;  // this wave's W loads per step: 2 (else 1; 3 at 4 waves)
     // two accumulators per tile: the leading product (hi x hi) and the five small terms, so the
     // small terms' fp32 roundings happen at 2^-8 of the result's magnitude (with one
     // accumulator the error grew past an fp32 GEMM's at K = 768)
-    f32x16 acc[2][2], acs[2][2];
+    f32x16 acc[G6_NA][2], acs[G6_NA][2];
     int j = 0, wslot = 0, xslot = 0;
     int nst = 0;  // stores of the previous tile's epilogue (younger than W(j + 2) at its step 0)
     // step j's W fragments and raw X (read during step j - 1; step 0's here), in two register
     // sets used alternately (A, B) so that no copy moves them from one step to the next
-    uvec4 fuA[2][3], fuB[2][3];
+    uvec4 fuA[G6_NA][3], fuB[G6_NA][3];
     float xrA[2][8], xrB[2][8];
-    auto read_frags = [&](int ws, int xs, uvec4 (&u)[2][3], float (&r)[2][8]) {
-        const uvec4* wq = reinterpret_cast<const uvec4*>(wl[ws]) + lane;
+    auto read_frags = [&](int ws, int xs, uvec4 (&u)[G6_NA][3], float (&r)[2][8]) {
+        if constexpr (!G6_W4) {  // (4 waves: W read at the start of its own step, kstep)
+            const uvec4* wq = reinterpret_cast<const uvec4*>(wl[ws]) + lane;
 #pragma unroll
-        for (int a = 0; a < 2; ++a)
+            for (int a = 0; a < G6_NA; ++a)
 #pragma unroll
-            for (int e = 0; e < 3; ++e) u[a][e] = wq[((2 * ch + a) * 3 + e) * 64];
+                for (int e = 0; e < 3; ++e) u[a][e] = wq[((G6_NA * ch + a) * 3 + e) * 64];
+        }
         if constexpr (LTM) g6_raw_x_tm<!LTM>(xraw[xs], pq, lane, r);
         else g6_raw_x(xraw[xs], pq, lane, r);
     };
@@ -446,8 +462,19 @@ __device__ __forceinline__ void g6_body(const G6Geom& g, G6XSlot* xraw, G6WSlot*
     // One k-step: the next step's fragment reads and this step's split between its MFMAs, then
     // the loads of W(j + 3) and X(j + 5) (their scalar address work overlaps the MFMAs in
     // flight), one barrier.
-    auto kstep = [&](const uvec4 (&fu)[2][3], const float (&xr)[2][8], uvec4 (&fun)[2][3],
+    auto kstep = [&](const uvec4 (&fu)[G6_NA][3], const float (&xr)[2][8], uvec4 (&fun)[G6_NA][3],
                      float (&xrn)[2][8]) {
+        // 4 waves: no second register set for W (a wave's 128 channels x 3 terms = 48 VGPRs);
+        // this step's fragments are read first and the MFMAs wait for them in order
+        uvec4 fw[G6_NA][3];
+        if constexpr (G6_W4) {
+            const uvec4* wq = reinterpret_cast<const uvec4*>(wl[wslot]) + lane;
+#pragma unroll
+            for (int a = 0; a < G6_NA; ++a)
+#pragma unroll
+                for (int e = 0; e < 3; ++e) fw[a][e] = wq[(a * 3 + e) * 64];
+        }
+        const uvec4(&fuse)[G6_NA][3] = G6_W4 ? fw : fu;
         wslot = wslot == G6_NW - 1 ? 0 : wslot + 1;
         xslot = xslot == G6_NX - 1 ? 0 : xslot + 1;
         // step j + 1's fragments (in since the last barrier; past the stream's end: unused)
@@ -468,20 +495,24 @@ __device__ __forceinline__ void g6_body(const G6Geom& g, G6XSlot* xraw, G6WSlot*
 #pragma unroll
                 for (int b = 0; b < 2; ++b)
 #pragma unroll
-                    for (int a = 0; a < 2; ++a) {
+                    for (int a = 0; a < G6_NA; ++a) {
                         if constexpr (STM)  // tokens as the MFMA's rows: features contiguous in C
-                            (e == 5 ? acc : acs)[a][b] = g6_mfma(fv[b][TV[e]], fu[a][TU[e]], (e == 5 ? acc : acs)[a][b]);
+                            (e == 5 ? acc : acs)[a][b] = g6_mfma(fv[b][TV[e]], fuse[a][TU[e]], (e == 5 ? acc : acs)[a][b]);
                         else
-                            (e == 5 ? acc : acs)[a][b] = g6_mfma(fu[a][TU[e]], fv[b][TV[e]], (e == 5 ? acc : acs)[a][b]);
+                            (e == 5 ? acc : acs)[a][b] = g6_mfma(fuse[a][TU[e]], fv[b][TV[e]], (e == 5 ? acc : acs)[a][b]);
                     }
 #endif
 #if G6_SCHED
+            if constexpr (G6_W4 && LO == 0) __builtin_amdgcn_sched_group_barrier(0x100, 3 * G6_NA, 0);  // W
             if constexpr (LO == 0) __builtin_amdgcn_sched_group_barrier(0x002, 16, 0);  // the first terms
+            // per MFMA: the split's rest (3 VALU at 8 waves, 2 at 4) and one of the next step's
+            // fragment reads (W: 3 NA b128; X: 8 b64 or 4 b128 token-major)
+            constexpr int MPT = 2 * G6_NA, NV = G6_W4 ? 2 : 3, ND = (G6_W4 ? 0 : 3 * G6_NA) + (LTM ? 4 : 8);
 #pragma unroll
-            for (int k = 4 * LO; k < 4 * HI; ++k) {
+            for (int k = MPT * LO; k < MPT * HI; ++k) {
                 __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-                __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
-                if (k < (LTM ? 10 : 14)) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x002, NV, 0);
+                if (k < ND) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
             }
 #endif
         };
@@ -489,7 +520,7 @@ __device__ __forceinline__ void g6_body(const G6Geom& g, G6XSlot* xraw, G6WSlot*
         // the pipe — after all of this wave's, or (the waves sharing a SIMD with the first four)
         // half-way, so that the two waves of a SIMD never do it at the same time
         auto dma = [&]() {
-#if G6_EXP != 3
+#if !G6_NO_LOADS
             dma_w();  // step j + 3
             dma_x();  // step j + 5
 #endif
@@ -512,21 +543,21 @@ __device__ __forceinline__ void g6_body(const G6Geom& g, G6XSlot* xraw, G6WSlot*
         if (j + G6_NX - 1 >= J) __builtin_amdgcn_s_waitcnt(0x0070);  // the stream's tail: vmcnt(0)
 #if G6_STORE_CREDIT
         else if (s == 0 && nst == 32) {
-            if (four) __builtin_amdgcn_s_waitcnt(g6_vmcnt(6 + 32) & ~0x0F00);
-            else __builtin_amdgcn_s_waitcnt(g6_vmcnt(5 + 32) & ~0x0F00);
+            if (four) __builtin_amdgcn_s_waitcnt(g6_vmcnt(G6_YOUNG_A + 32) & ~0x0F00);
+            else __builtin_amdgcn_s_waitcnt(g6_vmcnt(G6_YOUNG_B + 32) & ~0x0F00);
         } else if (s == 0 && nst == 16) {
-            if (four) __builtin_amdgcn_s_waitcnt(g6_vmcnt(6 + 16) & ~0x0F00);
-            else __builtin_amdgcn_s_waitcnt(g6_vmcnt(5 + 16) & ~0x0F00);
+            if (four) __builtin_amdgcn_s_waitcnt(g6_vmcnt(G6_YOUNG_A + 16) & ~0x0F00);
+            else __builtin_amdgcn_s_waitcnt(g6_vmcnt(G6_YOUNG_B + 16) & ~0x0F00);
         }
 #endif
-        else if (four) __builtin_amdgcn_s_waitcnt(g6_vmcnt(6) & ~0x0F00);
-        else __builtin_amdgcn_s_waitcnt(g6_vmcnt(5) & ~0x0F00);
+        else if (four) __builtin_amdgcn_s_waitcnt(g6_vmcnt(G6_YOUNG_A) & ~0x0F00);
+        else __builtin_amdgcn_s_waitcnt(g6_vmcnt(G6_YOUNG_B) & ~0x0F00);
         __builtin_amdgcn_s_barrier();
         ++s, ++j;
     };
     for (int tw = 0; tw < ntile_wg; ++tw) {
 #pragma unroll
-        for (int a = 0; a < 2; ++a)
+        for (int a = 0; a < G6_NA; ++a)
 #pragma unroll
             for (int b = 0; b < 2; ++b) acc[a][b] = f32x16{}, acs[a][b] = f32x16{};
         s = 0;
@@ -537,7 +568,7 @@ __device__ __forceinline__ void g6_body(const G6Geom& g, G6XSlot* xraw, G6WSlot*
         if (s < kper) {  // odd step count: one more, and set A back to the current step
             kstep(fuA, xrA, fuB, xrB);
 #pragma unroll
-            for (int a = 0; a < 2; ++a)
+            for (int a = 0; a < G6_NA; ++a)
 #pragma unroll
                 for (int e = 0; e < 3; ++e) fuA[a][e] = fuB[a][e];
 #pragma unroll
@@ -569,8 +600,9 @@ __global__ __launch_bounds__(G6_THREADS, 1) void k_gemm_x6(G6Geom g) {
     __shared__ __attribute__((aligned(16))) G6XSlot xraw[G6_NX];
     __shared__ __attribute__((aligned(16))) G6WSlot wl[G6_NW];
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    // waves w and w + 4 share a SIMD: the second one issues its loads half-way (G6_STAGGER)
-    if (G6_STAGGER && (wv & 4)) g6_body<LTM, STM, true, SPLIT>(g, xraw, wl, wv);
+    // waves w and w + 4 share a SIMD: the second one issues its loads half-way (G6_STAGGER);
+    // at 4 waves (one per SIMD) every wave issues them half-way, between its MFMAs
+    if (G6_W4 || (G6_STAGGER && (wv & 4))) g6_body<LTM, STM, true, SPLIT>(g, xraw, wl, wv);
     else g6_body<LTM, STM, false, SPLIT>(g, xraw, wl, wv);
 }
 
