@@ -42,9 +42,24 @@ constexpr int A6_QW = 32;                    // queries per wave
 constexpr int A6_WB = A6_WAVES * A6_QW;      // queries per workgroup
 constexpr float A6_LAZY = 8.f;               // log2 headroom of the lazily moved running max
 
+#ifndef A6_EXP
+#define A6_EXP 0  // diagnostics only: 7 = each 32x32x16 MFMA replaced by two 16x16x32 ones on the same
+                  // operands (the same MACs, wrong results): the clock the chip holds per MFMA shape
+#endif
 __device__ __forceinline__ a6_f16 a6_mfma(a6_u4 a, a6_u4 b, a6_f16 c) {
+#if A6_EXP == 7
+    typedef float a6_f4 __attribute__((ext_vector_type(4)));
+    a6_f4 c0 = {c[0], c[1], c[2], c[3]}, c1 = {c[4], c[5], c[6], c[7]};
+    c0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(a6_bf8, a), __builtin_bit_cast(a6_bf8, b), c0,
+                                                 0, 0, 0);
+    c1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(a6_bf8, b), __builtin_bit_cast(a6_bf8, a), c1,
+                                                 0, 0, 0);
+    c[0] = c0[0], c[1] = c0[1], c[2] = c0[2], c[3] = c0[3], c[4] = c1[0], c[5] = c1[1], c[6] = c1[2], c[7] = c1[3];
+    return c;
+#else
     return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(a6_bf8, a), __builtin_bit_cast(a6_bf8, b), c,
                                                    0, 0, 0);
+#endif
 }
 
 // the bf16 halves (upper 16 bits) of a and b as one dword: a low, b high

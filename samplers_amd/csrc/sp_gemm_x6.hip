@@ -42,7 +42,8 @@ typedef __attribute__((address_space(3))) void lds_void_g;
 #ifndef G6_EXP
 #define G6_EXP 0  // diagnostics only (wrong results, timing): 1 no MFMAs, 2 no split, 3 no loads,
                   // 4 no output stores, 5 X loads from one cached 2 KB (no X stream from HBM),
-                  // 6 MFMAs only (no loads, no split, no stores)
+                  // 6 MFMAs only (no loads, no split, no stores), 7 each 32x32x16 MFMA replaced by
+                  // two 16x16x32 ones on the same operands (the same MACs; the clock the chip holds)
 #endif
 #define G6_NO_SPLIT (G6_EXP == 2 || G6_EXP == 6)
 #define G6_NO_LOADS (G6_EXP == 3 || G6_EXP == 6)
@@ -93,8 +94,18 @@ __device__ __forceinline__ unsigned g6_pack(unsigned a, unsigned b) {
     return __builtin_amdgcn_perm(b, a, 0x07060302u);
 }
 __device__ __forceinline__ f32x16 g6_mfma(uvec4 a, uvec4 b, f32x16 c) {
+#if G6_EXP == 7
+    f32x4 c0 = {c[0], c[1], c[2], c[3]}, c1 = {c[4], c[5], c[6], c[7]};
+    c0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b),
+                                                 c0, 0, 0, 0);
+    c1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, b), __builtin_bit_cast(bf16x8, a),
+                                                 c1, 0, 0, 0);
+    c[0] = c0[0], c[1] = c0[1], c[2] = c0[2], c[3] = c0[3], c[4] = c1[0], c[5] = c1[1], c[6] = c1[2], c[7] = c1[3];
+    return c;
+#else
     return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a),
                                                    __builtin_bit_cast(bf16x8, b), c, 0, 0, 0);
+#endif
 }
 
 // direct global->LDS load (64 lanes x 16 B to lds .. lds + 1 KB) written as inline asm: the
