@@ -43,7 +43,8 @@ typedef __attribute__((address_space(3))) void lds_void_g;
 #define G6_EXP 0  // diagnostics only (wrong results, timing): 1 no MFMAs, 2 no split, 3 no loads,
                   // 4 no output stores, 5 X loads from one cached 2 KB (no X stream from HBM),
                   // 6 MFMAs only (no loads, no split, no stores), 7 each 32x32x16 MFMA replaced by
-                  // two 16x16x32 ones on the same operands (the same MACs; the clock the chip holds)
+                  // two 16x16x32 ones on the same operands (the same MACs; the clock the chip holds),
+                  // 8 no k-step barrier (the waves drift: races on the LDS ring; timing only)
 #endif
 #define G6_NO_SPLIT (G6_EXP == 2 || G6_EXP == 6)
 #define G6_NO_LOADS (G6_EXP == 3 || G6_EXP == 6)
@@ -563,7 +564,9 @@ __device__ __forceinline__ void g6_body(const G6Geom& g, G6XSlot* xraw, G6WSlot*
 #endif
         else if (four) __builtin_amdgcn_s_waitcnt(g6_vmcnt(G6_YOUNG_A) & ~0x0F00);
         else __builtin_amdgcn_s_waitcnt(g6_vmcnt(G6_YOUNG_B) & ~0x0F00);
+#if G6_EXP != 8
         __builtin_amdgcn_s_barrier();
+#endif
         ++s, ++j;
     };
     for (int tw = 0; tw < ntile_wg; ++tw) {
