@@ -59,8 +59,14 @@ constexpr int G6_CO = 128;     // output channels per workgroup
 constexpr int G6_PX = 256;     // pixels per workgroup
 constexpr int G6_KC = 16;      // input channels per k-step
 constexpr int G6_WB = 4 * 3 * 64 * 16;        // bytes of W fragments per k-step (12 KB)
-constexpr int G6_NX = 6;       // raw X ring slots: X of k-step j + 5 loads during step j
-constexpr int G6_NW = 4;       // W ring slots: W of k-step j + 3 loads during step j
+#ifndef G6_NX_SLOTS
+#define G6_NX_SLOTS 6
+#endif
+#ifndef G6_NW_SLOTS
+#define G6_NW_SLOTS 4
+#endif
+constexpr int G6_NX = G6_NX_SLOTS;  // raw X ring slots: X of k-step j + 5 loads during step j
+constexpr int G6_NW = G6_NW_SLOTS;  // W ring slots: W of k-step j + 3 loads during step j
 
 struct G6Geom {
     const float* x1;
