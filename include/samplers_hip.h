@@ -415,6 +415,20 @@ int sp_wino3x3_fwd_ws(const float* x, const float* up, const float* bias, const 
 int sp_wino3x3_bwd_input_ws(const float* dy, const float* up_vjp, int64_t n, int32_t cin,
                             int32_t cout, int32_t height, int32_t width, float* dx, float* ws,
                             int64_t ws_bytes, sp_stream_t stream);
+/* Round 5: diffusers' Upsample2D (nearest 2x upsample, then this conv) fused into the tile, so
+ * the upsampled tensor is never written (reference call sites: the UNet / VAE up blocks behind
+ * ddpm.py:40-43 and stable_diffusion.py:330-336).  height x width = the conv's (upsampled) size.
+ * sp_wino3x3_fwd_up: x is the [n][cin][height/2][width/2] source, y the [n][cout][height][width]
+ * conv output (+ bias).  sp_wino3x3_bwd_input_pool: the input VJP of conv(upsample(x)), dy
+ * [n][cout][height][width] -> dx [n][cin][height/2][width/2] (each 2x2 block's sum in
+ * sp_upsample2x_vjp's order: bitwise the unfused pair's result when that runs unsplit).
+ * Unsplit (no workspace); sp_wino3x3_up_supported says where both directions run. */
+int sp_wino3x3_up_supported(int32_t cin, int32_t cout, int32_t height, int32_t width);
+int sp_wino3x3_fwd_up(const float* x, const float* up, const float* bias, int64_t n, int32_t cin,
+                      int32_t cout, int32_t height, int32_t width, float* y, sp_stream_t stream);
+int sp_wino3x3_bwd_input_pool(const float* dy, const float* up_vjp, int64_t n, int32_t cin,
+                              int32_t cout, int32_t height, int32_t width, float* dx,
+                              sp_stream_t stream);
 
 /* 1x1 convolution as a per-pixel GEMM on bf16 MFMAs over exact three-term splits of the fp32
  * operands (fp32-class error): Y[n][co][p] = sum_k W[co][k] X[n][k][p] (+ bias[co]) (+ res),

@@ -225,6 +225,11 @@ SIGNATURES = {
                                          ctypes.c_int32, ctypes.c_int32, _P, _P, _I64, _P]),
     "sp_wino3x3_bwd_input_ws": (ctypes.c_int, [_P, _P, _I64, ctypes.c_int32, ctypes.c_int32,
                                                ctypes.c_int32, ctypes.c_int32, _P, _P, _I64, _P]),
+    "sp_wino3x3_up_supported": (ctypes.c_int, [ctypes.c_int32] * 4),
+    "sp_wino3x3_fwd_up": (ctypes.c_int, [_P, _P, _P, _I64, ctypes.c_int32, ctypes.c_int32,
+                                         ctypes.c_int32, ctypes.c_int32, _P, _P]),
+    "sp_wino3x3_bwd_input_pool": (ctypes.c_int, [_P, _P, _I64, ctypes.c_int32, ctypes.c_int32,
+                                                 ctypes.c_int32, ctypes.c_int32, _P, _P]),
 }
 
 _lib = None

@@ -162,9 +162,16 @@ constexpr int WR_NS = 4;    // unroll of the k-step ring (cin % (2 WR_NS) == 0)
 // TCW = 16 (images with W % 32 == 0): 2 x 16 tiles = 4 x 32 outputs; TCW = 8 (W = 16, the
 // UNet's 16x16 level): 4 x 8 tiles = 8 x 16 outputs.  A workgroup stacks two waves' rows
 // (and two 32-channel halves): 64 co x (4 TRW) x (2 TCW) outputs.
-template <int TCW_, bool MOSAIC_ = false, bool SPLIT_ = false>
+template <int TCW_, bool MOSAIC_ = false, bool SPLIT_ = false, int UP_ = 0>
 struct WGeo {
     static constexpr int TCW = TCW_;
+    // UP (diffusers Upsample2D: a nearest 2x upsample feeding this conv, fused; the W % 32
+    // geometry of the xi tile, unsplit): 1 = the input is the half-resolution source, each
+    // 16-byte piece of an upsampled row loaded as the 8 source bytes it repeats; 2 = the
+    // output (the input VJP of conv(upsample(x))) summed over each 2x2 block into the
+    // half-resolution gradient in the epilogue, in the upsample VJP's order.  Either way the
+    // upsampled tensor is never written.
+    static constexpr int UP = UP_;
     // SPLIT (launches whose tiles leave CUs idle: small batches, the low-resolution levels):
     // K cut into g.ksplit parts, one tile each; part kh stores its partial sums (no bias, no
     // residual) to workspace slice kh, and k_wino_split_reduce adds the slices in order, the
@@ -220,6 +227,7 @@ struct WrGeom {
     int ksplit;                       // split-K parts of the SPLIT kernels, else 1
     float* ws;                        // SPLIT: the parts' partial outputs [ksplit][batch][cout][H][W]
     int64_t ws_stride;                // floats per part slice
+    int hplane, Wh;                   // UP: the half-resolution plane (H/2 x W/2) and row
 };
 
 // First image of a wave's data and how many of its images exist (MOSAIC: 2 per wave).
@@ -268,13 +276,17 @@ __device__ __forceinline__ WrSrc wr_src(const WrGeom& g, const WrTile& ti, int w
                        ? ((col >> 3) * g.cin * g.plane + ci * g.plane + gr * g.W + (col & 7)) * 4
                        : OOB;
         }
+        if constexpr (GE::UP == 1)  // upsampled (row, col) -> its source pixel (col even for pieces)
+            return ((unsigned)gr < (unsigned)g.H && (unsigned)col < (unsigned)g.W)
+                       ? (ci * g.hplane + (gr >> 1) * g.Wh + (col >> 1)) * 4 : OOB;
         return ((unsigned)gr < (unsigned)g.H && (unsigned)col < (unsigned)g.W)
                    ? (ci * g.plane + gr * g.W + col) * 4 : OOB;
     };
+    const int pin = GE::UP == 1 ? g.hplane : g.plane;  // floats per input plane
     WrSrc s;
     s.rs = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<float*>(g.x + wr_img0<GE>(g, ti, wv) * g.cin * g.plane + (int64_t)kofs * g.plane),
-        (short)0, nimg ? (nimg * g.cin - kofs) * g.plane * 4 : 0, 0x00020000);
+        const_cast<float*>(g.x + wr_img0<GE>(g, ti, wv) * g.cin * pin + (int64_t)kofs * pin),
+        (short)0, nimg ? (nimg * g.cin - kofs) * pin * 4 : 0, 0x00020000);
     s.oa = goff(rca, ti.ow0 + 4 * ka);
     s.ob = goff(rcb, ti.ow0 + 4 * ka);
     s.oh = GE::MOSAIC ? OOB : goff(rch, side ? ti.ow0 + 2 * GE::TCW : ti.ow0 - 1);
@@ -284,10 +296,11 @@ __device__ __forceinline__ WrSrc wr_src(const WrGeom& g, const WrTile& ti, int w
 #if SP_DEBUG
     {   // every k-step's input pieces inside this tile's planes — of the images that exist (a
         // MOSAIC wave's pieces of an image past the batch are OOB) —, U rows inside the packed U
-        const int64_t span = nimg ? (int64_t)(nimg * g.cin - kofs) * g.plane * 4 : 0;
+        const int64_t span = nimg ? (int64_t)(nimg * g.cin - kofs) * pin * 4 : 0;
         const int64_t last = (int64_t)(g.nsteps - 1) * g.so_step;
-        SP_DCHECK(s.oa == OOB || (s.oa >= 0 && s.oa + last + 16 <= span));
-        SP_DCHECK(s.ob == OOB || (s.ob >= 0 && s.ob + last + 16 <= span));
+        constexpr int piece = GE::UP == 1 ? 8 : 16;
+        SP_DCHECK(s.oa == OOB || (s.oa >= 0 && s.oa + last + piece <= span));
+        SP_DCHECK(s.ob == OOB || (s.ob >= 0 && s.ob + last + piece <= span));
         SP_DCHECK(s.oh == OOB || (s.oh >= 0 && s.oh + last + 4 <= span));
         SP_DCHECK(s.uso >= 0 && (int64_t)s.uso + ((int64_t)(g.nsteps - 1) * g.u_step + 64 * 16) * 4 <=
                                    (int64_t)g.nsteps * g.ksplit * g.u_step * 4);
@@ -297,9 +310,17 @@ __device__ __forceinline__ WrSrc wr_src(const WrGeom& g, const WrTile& ti, int w
     return s;
 }
 
+template <class GE>
 __device__ __forceinline__ void wr_load_x(const WrSrc& s, int so, WrX& x) {
-    x.a = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(s.rs, s.oa, so, 0));
-    x.b = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(s.rs, s.ob, so, 0));
+    if constexpr (GE::UP == 1) {  // four upsampled columns = two source pixels, each twice
+        const f32x2 a = __builtin_bit_cast(f32x2, __builtin_amdgcn_raw_buffer_load_b64(s.rs, s.oa, so, 0));
+        const f32x2 b = __builtin_bit_cast(f32x2, __builtin_amdgcn_raw_buffer_load_b64(s.rs, s.ob, so, 0));
+        x.a = f32x4{a.x, a.x, a.y, a.y};
+        x.b = f32x4{b.x, b.x, b.y, b.y};
+    } else {
+        x.a = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(s.rs, s.oa, so, 0));
+        x.b = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(s.rs, s.ob, so, 0));
+    }
     x.h = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(s.rs, s.oh, so, 0));
 }
 
@@ -368,7 +389,7 @@ __device__ __forceinline__ void wr_step(const WrGeom& g, const WrSrc& cur, const
     __builtin_amdgcn_sched_barrier(0)
     WR_MFMA(0);
 #if SP_WINO_EXP != 1
-    wr_load_x(XN ? nxt : cur, (XN ? q + 3 - g.nsteps : q + 3) * g.so_step, r.xs[(K + 3) % 4]);
+    wr_load_x<GE>(XN ? nxt : cur, (XN ? q + 3 - g.nsteps : q + 3) * g.so_step, r.xs[(K + 3) % 4]);
 #endif
     WR_WALL;
     WR_MFMA(1);
@@ -599,13 +620,13 @@ __global__ __launch_bounds__(kBlock, 1) void k_wino3x3_r(WrGeom g) {
 
     // prologue in the loop's own issue order (..., X(q+1), U(q), X(q+2), U(q+1))
     WrRing r;
-    wr_load_x(cur, 0, r.xs[0]);
+    wr_load_x<GE>(cur, 0, r.xs[0]);
     __builtin_amdgcn_sched_barrier(0);
-    wr_load_x(cur, g.so_step, r.xs[1]);
+    wr_load_x<GE>(cur, g.so_step, r.xs[1]);
     __builtin_amdgcn_sched_barrier(0);
     wr_load_u(urs, lane, cur.uso, r.us[0]);
     __builtin_amdgcn_sched_barrier(0);
-    wr_load_x(cur, 2 * g.so_step, r.xs[2]);
+    wr_load_x<GE>(cur, 2 * g.so_step, r.xs[2]);
     __builtin_amdgcn_sched_barrier(0);
     wr_load_u(urs, lane, cur.uso + g.u_step * 4, r.us[1]);
     __builtin_amdgcn_sched_barrier(0);
@@ -745,7 +766,7 @@ __device__ __forceinline__ void xi_step(const WrGeom& g, const WrSrc& cur, const
     __builtin_amdgcn_sched_barrier(0)
     XI_MFMA(0);
 #if SP_WINO_EXP != 1
-    wr_load_x(XN ? nxt : cur, (XN ? q + XI_DX - g.nsteps : q + XI_DX) * g.so_step, r.xs[(K + XI_DX) % XI_NR]);
+    wr_load_x<GE>(XN ? nxt : cur, (XN ? q + XI_DX - g.nsteps : q + XI_DX) * g.so_step, r.xs[(K + XI_DX) % XI_NR]);
 #endif
     XI_WALL;
     XI_MFMA(1);
@@ -832,10 +853,18 @@ __device__ __forceinline__ void xi_epilogue(const WrGeom& g, const WrTile& ti, i
     WrTile tf = ti;
     tf.co0 = ti.co0 + 32 * H;  // this wave completes channel block H
     const int hh = lane >> 5, l = lane & 31;
-    const auto ors = __builtin_amdgcn_make_buffer_rsrc(g.out + (int64_t)tf.n * g.cout * g.plane, (short)0,
-                                                       g.cout * g.plane * 4, 0x00020000);
-    const int vo = wr_out_voff<GE>(g, tf, wv, lane);
-    SP_DCHECK(tf.n < g.batch && (int64_t)vo + (27 * (int64_t)g.plane + g.W) * 4 + 8 <= (int64_t)g.cout * g.plane * 4);
+    static_assert(!(GE::UP == 2 && RES), "the pooled input VJP adds no residual");
+    const int pout = GE::UP == 2 ? g.hplane : g.plane;  // floats per output plane
+    const auto ors = __builtin_amdgcn_make_buffer_rsrc(g.out + (int64_t)tf.n * g.cout * pout, (short)0,
+                                                       g.cout * pout * 4, 0x00020000);
+    int vo = wr_out_voff<GE>(g, tf, wv, lane);
+    if constexpr (GE::UP == 2) {  // the lane's 2x2 block -> its half-resolution pixel
+        const int tr = GE::TRW * (wv >> 1) + l / GE::TCW, tc = l % GE::TCW;
+        vo = ((tf.co0 + 4 * hh) * g.hplane + (tf.oh0 / 2 + tr) * g.Wh + tf.ow0 / 2 + tc) * 4;
+        SP_DCHECK(tf.n < g.batch && (int64_t)vo + 27 * (int64_t)g.hplane * 4 + 4 <= (int64_t)g.cout * g.hplane * 4);
+    } else {
+        SP_DCHECK(tf.n < g.batch && (int64_t)vo + (27 * (int64_t)g.plane + g.W) * 4 + 8 <= (int64_t)g.cout * g.plane * 4);
+    }
     const auto brs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(g.bias ? g.bias : g.up), (short)0,
                                                        g.bias ? g.cout * 4 : 0, 0x00020000);
     const float bl = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(brs, (tf.co0 + l) * 4, 0, 0));
@@ -855,12 +884,17 @@ __device__ __forceinline__ void xi_epilogue(const WrGeom& g, const WrTile& ti, i
         const float b0 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, bl), c));
         const float b1 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, bl), c + 4));
         const float bv = hh ? b1 : b0;
-        const int so = c * g.plane * 4;
+        const int so = c * pout * 4;
         f32x2 y0 = {s0[0] + s0[1] + s0[2] + bv, s1[0] + s1[1] + s1[2] + bv};
         f32x2 y1 = {s0[1] - s0[2] - s0[3] + bv, s1[1] - s1[2] - s1[3] + bv};
         if constexpr (RES) y0 += rv.v[rr][0], y1 += rv.v[rr][1];
-        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, y0), ors, vo, so, 0);
-        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, y1), ors, vo, so + g.W * 4, 0);
+        if constexpr (GE::UP == 2) {  // k_upsample2x_vjp's order: ((row 0) + row 1, left first)
+            const float p = ((y0.x + y0.y) + y1.x) + y1.y;
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(p), ors, vo, so, 0);
+        } else {
+            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, y0), ors, vo, so, 0);
+            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, y1), ors, vo, so + g.W * 4, 0);
+        }
         __builtin_amdgcn_sched_barrier(0);
     }
     __builtin_amdgcn_s_waitcnt(0xc07f);  // the partner's rows are read before it writes again
@@ -897,7 +931,7 @@ __device__ __forceinline__ void xi_body(const WrGeom& g, int wv, int lane, float
     XiRing r;
     static_for<0, (XI_DX > XI_DU ? XI_DX : XI_DU)>([&](auto S) {
         constexpr int s = decltype(S)::value;
-        if constexpr (s < XI_DX) wr_load_x(cur, s * g.so_step, r.xs[s]);
+        if constexpr (s < XI_DX) wr_load_x<GE>(cur, s * g.so_step, r.xs[s]);
         __builtin_amdgcn_sched_barrier(0);
         if constexpr (s < XI_DU) xi_load_u<H>(urs, lane, cur.uso + s * static_cast<int>(g.u_step) * 4, r.us[s]);
         __builtin_amdgcn_sched_barrier(0);
@@ -943,9 +977,9 @@ __device__ __forceinline__ void xi_body(const WrGeom& g, int wv, int lane, float
     }
 }
 
-template <bool RES, int TCW>
+template <bool RES, int TCW, int UP = 0>
 __global__ __launch_bounds__(kBlock, 1) void k_wino3x3_xi(WrGeom g) {
-    using GE = WGeo<TCW>;
+    using GE = WGeo<TCW, false, false, UP>;
     __shared__ __attribute__((aligned(16))) float xlds[4 * GE::WAVE];
     __shared__ __attribute__((aligned(16))) float exlds[2 * 2 * XI_EX];  // [pair][writer][...]
     const int lane = threadIdx.x & 63;
@@ -1055,11 +1089,20 @@ static int64_t wino_tiles(int64_t n, int32_t cout, int32_t height, int32_t width
     return mosaic ? (n + 3) / 4 * (cout / WR_CO) : n * (height / wg_rows) * (width / wg_cols) * (cout / WR_CO);
 }
 
+// the xi tile serves the launch (W % 32 geometry, K a multiple of its ring)
+static bool wino_xi(int32_t cin, int32_t height, int32_t width) {
+    return SP_WINO_XI && width % WGeo<16>::WG_COLS == 0 && height % WGeo<16>::WG_ROWS == 0 &&
+           cin % (2 * XI_NR) == 0 && cin >= 4 * XI_NR;
+}
+
+// up_mode (Upsample2D fused, height x width the conv's = the upsampled size): 1 = x is the
+// half-resolution source, 2 = y is the half-resolution 2x2-block sum; the xi tile, unsplit.
 static int wino3x3(int kind, const float* x, const float* up, const float* bias,
                    const float* res, int64_t n, int32_t cin, int32_t cout, int32_t height,
                    int32_t width, float* y, float* ws, size_t ws_bytes, sp_stream_t stream,
-                   const char* what) {
+                   const char* what, int up_mode = 0) {
     if (!sp_wino3x3_supported(cin, cout, height, width) || n < 0) return SP_EINVAL;
+    if (up_mode && (!wino_xi(cin, height, width) || res)) return SP_EINVAL;
     if (n == 0) return SP_OK;
     if (!x || !up || !y) return SP_EINVAL;
     const bool mosaic = width == 8;                     // 8x8 images, 4 per workgroup
@@ -1074,7 +1117,7 @@ static int wino3x3(int kind, const float* x, const float* up, const float* bias,
     // split K where the tiles leave CUs idle (small batches, the low-resolution levels), when
     // the caller's workspace holds every part's partial output
     const int64_t out_floats = n * cout * (int64_t)height * width;
-    int ksplit = ws ? wino_ksplit(tiles, cin) : 1;
+    int ksplit = ws && !up_mode ? wino_ksplit(tiles, cin) : 1;
     if (ksplit > 1 && ws_bytes < (size_t)ksplit * out_floats * sizeof(float)) ksplit = 1;
     if (tiles * ksplit >= (int64_t(1) << 31)) ksplit = 1;
     WrGeom g;
@@ -1097,7 +1140,9 @@ static int wino3x3(int kind, const float* x, const float* up, const float* bias,
     g.per_img = mosaic ? 1 : g.tiles_w * (height / wg_rows);
     g.batch = n;
     g.u_step = (int64_t)cout * 32;
-    g.so_step = 2 * height * width * 4;
+    g.hplane = (height / 2) * (width / 2);
+    g.Wh = width / 2;
+    g.so_step = 2 * (up_mode == 1 ? g.hplane : height * width) * 4;
     g.nsteps = cin / 2 / ksplit;
     // one persistent workgroup per CU (a 512-register wave per SIMD: one workgroup fits)
     const int grid = static_cast<int>(std::min<int64_t>(tiles * ksplit, cu_count()));
@@ -1106,6 +1151,14 @@ static int wino3x3(int kind, const float* x, const float* up, const float* bias,
     const double flops = 8.0 * n * cin * cout * height * width;
     const dim3 gd(static_cast<unsigned>(grid)), bd(kBlock);
     hipStream_t st = static_cast<hipStream_t>(stream);
+    if (up_mode == 1) {
+        launch_w(kind, flops, k_wino3x3_xi<false, 16, 1>, gd, bd, st, g);
+        return check_launch(what);
+    }
+    if (up_mode == 2) {
+        launch_w(kind, flops, k_wino3x3_xi<false, 16, 2>, gd, bd, st, g);
+        return check_launch(what);
+    }
     if (ksplit > 1) {
         if (mosaic) launch_w(kind, flops, k_wino3x3_r<false, 8, true, true>, gd, bd, st, g);
         else if (narrow) launch_w(kind, flops, k_wino3x3_r<false, 8, false, true>, gd, bd, st, g);
@@ -1172,6 +1225,27 @@ int sp_wino3x3_fwd_ws(const float* x, const float* up, const float* bias, const 
     if (ws && (ws == y || ws_bytes < 0)) return SP_EINVAL;
     return wino3x3(TK_WINO3X3_FWD, x, up, bias, res, n, cin, cout, height, width, y, ws,
                    static_cast<size_t>(ws_bytes > 0 ? ws_bytes : 0), stream, "sp_wino3x3_fwd_ws");
+}
+
+int sp_wino3x3_up_supported(int32_t cin, int32_t cout, int32_t height, int32_t width) {
+    // forward (K = cin) and input VJP (K = cout) both on the xi tile, even upsampled sizes
+    return sp_wino3x3_supported(cin, cout, height, width) && sp_wino3x3_supported(cout, cin, height, width) &&
+           wino_xi(cin, height, width) && wino_xi(cout, height, width) && height % 2 == 0 && width % 2 == 0;
+}
+
+int sp_wino3x3_fwd_up(const float* x, const float* up, const float* bias, int64_t n, int32_t cin,
+                      int32_t cout, int32_t height, int32_t width, float* y, sp_stream_t stream) {
+    if (!sp_wino3x3_up_supported(cin, cout, height, width)) return SP_EINVAL;
+    return wino3x3(TK_WINO3X3_FWD, x, up, bias, nullptr, n, cin, cout, height, width, y, nullptr, 0,
+                   stream, "sp_wino3x3_fwd_up", 1);
+}
+
+int sp_wino3x3_bwd_input_pool(const float* dy, const float* up_vjp, int64_t n, int32_t cin,
+                              int32_t cout, int32_t height, int32_t width, float* dx,
+                              sp_stream_t stream) {
+    if (!sp_wino3x3_up_supported(cin, cout, height, width)) return SP_EINVAL;
+    return wino3x3(TK_WINO3X3_BWD_INPUT, dy, up_vjp, nullptr, nullptr, n, cout, cin, height, width, dx,
+                   nullptr, 0, stream, "sp_wino3x3_bwd_input_pool", 2);
 }
 
 int sp_wino3x3_bwd_input_ws(const float* dy, const float* up_vjp, int64_t n, int32_t cin,

@@ -446,6 +446,67 @@ class _Upsample2xFn(torch.autograd.Function):
         return _upsample2x_call("sp_upsample2x_vjp", dy, ctx.x_shape)
 
 
+def _upconv_enabled() -> bool:
+    import os
+
+    return os.environ.get("SAMPLERS_AMD_UPCONV", "1").lower() not in ("0", "off", "false")
+
+
+def upsample_conv_supported(module: "Conv3x3", x: Tensor) -> bool:
+    """``module(upsample_nearest2x(x))`` (diffusers Upsample2D) runs fused on the Winograd tile
+    (``sp_wino3x3_fwd_up`` / ``sp_wino3x3_bwd_input_pool``): the upsampled tensor is never
+    written.  Frozen weights only, and only where the unfused launches would not split K (an
+    under-filled launch keeps the split unfused pair, which is faster there); the results are
+    then bitwise the unfused pair's.  ``SAMPLERS_AMD_UPCONV=0`` turns it off."""
+    if not (x.is_cuda and x.dtype == torch.float32 and x.dim() == 4 and x.numel() > 0):
+        return False
+    if not _upconv_enabled() or conv_backend() != "auto" or module.weight.requires_grad:
+        return False
+    n, cin, h, w = x.shape
+    cout = module.out_channels
+    if not _query("sp_wino3x3_up_supported", cin, cout, 2 * h, 2 * w):
+        return False
+    return not split_k_enabled() or (_query("sp_wino3x3_workspace", n, cin, cout, 2 * h, 2 * w) <= 0 and
+                                     _query("sp_wino3x3_workspace", n, cout, cin, 2 * h, 2 * w) <= 0)
+
+
+class _UpsampleConv3x3Fn(torch.autograd.Function):
+    """conv(upsample_nearest2x(x)) with the upsample inside the Winograd tile's input loads, and
+    its VJP's 2x2 block sums inside the input-VJP tile's epilogue (``csrc/sp_wino.hip``, UP)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, module):
+        lib = _hip.load_library()
+        n, cin, h, w = x.shape
+        cout = module.out_channels
+        ctx.module, ctx.x_shape = module, x.shape
+        x = x.contiguous()
+        y = torch.empty(n, cout, 2 * h, 2 * w, device=x.device, dtype=torch.float32)
+        _hip.check(lib.sp_wino3x3_fwd_up(_hip.ptr(x), _hip.ptr(tile_pack(module, "wino", False)),
+                                         _hip.ptr(bias), n, cin, cout, 2 * h, 2 * w, _hip.ptr(y),
+                                         _hip.stream_of(x)), "sp_wino3x3_fwd_up")
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        lib = _hip.load_library()
+        n, cin, h, w = ctx.x_shape
+        cout = ctx.module.out_channels
+        dy = dy.contiguous()
+        dx = torch.empty(tuple(ctx.x_shape), device=dy.device, dtype=torch.float32)
+        _hip.check(lib.sp_wino3x3_bwd_input_pool(_hip.ptr(dy), _hip.ptr(tile_pack(ctx.module, "wino", True)),
+                                                 n, cin, cout, 2 * h, 2 * w, _hip.ptr(dx),
+                                                 _hip.stream_of(dy)), "sp_wino3x3_bwd_input_pool")
+        return dx, None, None, None
+
+
+def upsample_conv(module: "Conv3x3", x: Tensor) -> Tensor:
+    """``module(upsample_nearest2x(x))``: fused where ``upsample_conv_supported``, else the pair."""
+    if upsample_conv_supported(module, x):
+        return _UpsampleConv3x3Fn.apply(x, module.weight, module.bias, module)
+    return module(upsample_nearest2x(x))
+
+
 def upsample_nearest2x(x: Tensor) -> Tensor:
     """``F.interpolate(x, scale_factor=2.0, mode="nearest")``: the streaming kernels of
     ``csrc/sp_upsample.hip`` (forward and the 2x2-block-sum VJP) on fp32 CUDA tensors whose

@@ -32,7 +32,8 @@ from .. import _hip
 from ..runtime import batch_invariant_enabled
 from .layers import (Conv3x3, GroupNormAct, Linear, SkipGrad, conv3x3_forward, conv3x3_input_vjp,
                      downsample_conv, gn_backward, gn_forward, miopen_fallback, proj_nchw_to_tokens,
-                     proj_tokens_to_nchw, upsample_nearest2x, x6_enough_tiles, x6_workspace, _query)
+                     proj_tokens_to_nchw, upsample_conv, upsample_nearest2x, x6_enough_tiles, x6_workspace,
+                     _query)
 
 
 @dataclass(frozen=True)
@@ -614,7 +615,7 @@ class Upsample2D(nn.Module):
         self.conv = Conv3x3(channels, channels)
 
     def forward(self, x: Tensor) -> Tensor:
-        return self.conv(upsample_nearest2x(x))
+        return upsample_conv(self.conv, x)
 
 
 class _Level(nn.Module):

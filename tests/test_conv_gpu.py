@@ -502,3 +502,116 @@ def test_default_tile_error_vs_fp64(cuda, shape):
     torch.cuda.synchronize()
     rel = lambda a, b: ((a.double().cpu() - b).norm() / b.norm()).item()  # noqa: E731
     assert rel(y, ref) < 1e-6 and rel(dx, gref) < 1e-6, (rel(y, ref), rel(dx, gref))
+
+
+UPCONV_SHAPES = [  # n, c (cin = cout, diffusers Upsample2D), source h, w
+    (2, 128, 16, 16),
+    (1, 256, 16, 32),
+    (2, 64, 32, 32),
+    (1, 512, 16, 16),
+]
+
+
+def _upconv_operands(shape, cuda):
+    n, c, h, w = shape
+    g = torch.Generator().manual_seed(sum(shape) + 7)
+    x = torch.randn(n, c, h, w, generator=g)
+    wt = torch.randn(c, c, 3, 3, generator=g) * (c * 9) ** -0.5
+    b = torch.randn(c, generator=g) * 0.1
+    dy = torch.randn(n, c, 2 * h, 2 * w, generator=g)
+    return x, wt, b, dy
+
+
+@pytest.mark.parametrize("shape", UPCONV_SHAPES)
+def test_winograd_fused_upsample_matches_the_unfused_pair(cuda, shape):
+    """Upsample2D fused into the Winograd tile (sp_wino3x3_fwd_up / sp_wino3x3_bwd_input_pool):
+    the forward equals the unsplit tile on the materialised upsample bitwise (the same values
+    reach the same LDS image), the input VJP equals sp_wino3x3_bwd_input followed by
+    sp_upsample2x_vjp bitwise (the epilogue sums each 2x2 block in the upsample VJP's order),
+    and both agree with fp64 conv2d(interpolate(x)) to the tile's usual bound."""
+    from samplers_amd.networks.layers import upsample_nearest2x
+
+    n, c, h, w = shape
+    H, W = 2 * h, 2 * w
+    lib = _hip.load_library()
+    assert lib.sp_wino3x3_up_supported(c, c, H, W)
+    x, wt, b, dy = _upconv_operands(shape, cuda)
+    st = torch.cuda.current_stream().cuda_stream
+    xg, wg, bg, dyg = x.to(cuda), wt.to(cuda), b.to(cuda), dy.to(cuda)
+    up = torch.empty(c * c * 16, device=cuda)
+    uv = torch.empty_like(up)
+    assert lib.sp_wino3x3_pack(_hip.ptr(wg), c, c, 0, _hip.ptr(up), st) == 0
+    assert lib.sp_wino3x3_pack(_hip.ptr(wg), c, c, 1, _hip.ptr(uv), st) == 0
+    # fused
+    y = torch.empty(n, c, H, W, device=cuda)
+    assert lib.sp_wino3x3_fwd_up(_hip.ptr(xg), _hip.ptr(up), _hip.ptr(bg), n, c, c, H, W, _hip.ptr(y), st) == 0
+    dx = torch.empty(n, c, h, w, device=cuda)
+    assert lib.sp_wino3x3_bwd_input_pool(_hip.ptr(dyg), _hip.ptr(uv), n, c, c, H, W, _hip.ptr(dx), st) == 0
+    # the unfused pair, unsplit
+    xu = upsample_nearest2x(xg).contiguous()
+    yr = torch.empty_like(y)
+    assert lib.sp_wino3x3_fwd(_hip.ptr(xu), _hip.ptr(up), _hip.ptr(bg), n, c, c, H, W, _hip.ptr(yr), st) == 0
+    gu = torch.empty(n, c, H, W, device=cuda)
+    assert lib.sp_wino3x3_bwd_input(_hip.ptr(dyg), _hip.ptr(uv), n, c, c, H, W, _hip.ptr(gu), st) == 0
+    dxr = torch.empty_like(dx)
+    assert lib.sp_upsample2x_vjp(_hip.ptr(gu), n * c, h, w, _hip.ptr(dxr), st) == 0  # source dims
+    torch.cuda.synchronize()
+    assert torch.equal(y, yr)
+    assert torch.equal(dx, dxr)
+    # fp64
+    xd = x.double().requires_grad_()
+    ref = F.conv2d(F.interpolate(xd, scale_factor=2.0, mode="nearest"), wt.double(), b.double(), padding=1)
+    (gref,) = torch.autograd.grad(ref, xd, dy.double())
+    _check(y, ref.detach(), 5)
+    _check(dx, gref, 5)
+
+
+def test_winograd_fused_upsample_rejects_unsupported(cuda):
+    lib = _hip.load_library()
+    assert not lib.sp_wino3x3_up_supported(128, 128, 16, 16)   # W = 16: the narrow geometry
+    assert not lib.sp_wino3x3_up_supported(32, 128, 32, 32)    # VJP output channels % 64
+    assert not lib.sp_wino3x3_up_supported(8, 64, 32, 32)      # K below the xi ring
+    assert lib.sp_wino3x3_up_supported(128, 128, 32, 32)
+    bad = torch.empty(16, device=cuda)
+    st = torch.cuda.current_stream().cuda_stream
+    assert lib.sp_wino3x3_fwd_up(_hip.ptr(bad), _hip.ptr(bad), None, 1, 128, 128, 16, 16,
+                                 _hip.ptr(bad), st) != 0
+
+
+def test_upsample2d_module_fused_equals_unfused(cuda, monkeypatch):
+    """Upsample2D (unet2d.py) through autograd: the fused path (default) and the unfused pair
+    (SAMPLERS_AMD_UPCONV=0) give bitwise-equal outputs and input gradients at a shape whose
+    unfused launches run unsplit; under-filled shapes keep the (split) unfused pair."""
+    from samplers_amd.networks import layers
+    from samplers_amd.networks.unet2d import Upsample2D
+
+    n, c, h, w = 8, 128, 32, 32  # 64x64 output: 256 tiles, unsplit
+    g = torch.Generator().manual_seed(11)
+    m = Upsample2D(c)
+    with torch.no_grad():
+        m.conv.weight.normal_(0, (c * 9) ** -0.5, generator=g)
+        m.conv.bias.normal_(0, 0.1, generator=g)
+    m = m.to(cuda).requires_grad_(False)
+    x = torch.randn(n, c, h, w, generator=g).to(cuda)
+    dy = torch.randn(n, c, 2 * h, 2 * w, generator=g).to(cuda)
+    assert layers.upsample_conv_supported(m.conv, x)
+    assert not layers.upsample_conv_supported(m.conv, x[:1])  # one image: the pair splits K
+
+    calls = []
+    orig = layers._UpsampleConv3x3Fn.apply
+    monkeypatch.setattr(layers._UpsampleConv3x3Fn, "apply", lambda *a: calls.append(1) or orig(*a))
+
+    def run():
+        xr = x.clone().requires_grad_()
+        out = m(xr)
+        (gx,) = torch.autograd.grad(out, xr, dy)
+        return out.detach(), gx
+
+    y1, g1 = run()
+    assert calls
+    monkeypatch.setenv("SAMPLERS_AMD_UPCONV", "0")
+    calls.clear()
+    y0, g0 = run()
+    assert not calls
+    assert torch.equal(y1, y0)
+    assert torch.equal(g1, g0)

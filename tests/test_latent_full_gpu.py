@@ -71,7 +71,9 @@ def test_vae_decode_512_fwd_vjp_matches_cpu(cuda, vae_pair, parity_record):
     names = _kernel_names(lambda: gpu.decode(z.to(cuda)))
     assert any("wino3x3" in n for n in names), "decoder 3x3 convs not on the Winograd tile"
     assert any("gn_fwd" in n for n in names), "decoder GroupNorm not on the HIP kernel"
-    assert any("upsample2x" in n for n in names)
+    # the Upsample2D blocks: the upsample inside the Winograd tile's loads (round 5), or the
+    # streaming upsample kernel where the fused tile does not serve the shape
+    assert any("k_wino3x3_xi<false, 16, 1>" in n or "upsample2x" in n for n in names)
     assert any("conv3x3_thin" in n for n in names)  # conv_out 128 -> 3
     _check("decode", got, _fwd_vjp(cpu.decode, z, cot), parity_record)
 
