@@ -8,7 +8,8 @@ SRC := samplers_amd/csrc/sp_dps.hip samplers_amd/csrc/sp_blur.hip samplers_amd/c
        samplers_amd/csrc/sp_wino.hip samplers_amd/csrc/sp_conv_thin.hip \
        samplers_amd/csrc/sp_conv_s2.hip samplers_amd/csrc/sp_upsample.hip \
        samplers_amd/csrc/sp_attention.hip samplers_amd/csrc/sp_attention6.hip \
-       samplers_amd/csrc/sp_gemm_x6.hip samplers_amd/csrc/sp_transformer.hip
+       samplers_amd/csrc/sp_gemm_x6.hip samplers_amd/csrc/sp_transformer.hip \
+       samplers_amd/csrc/sp_bf16.hip
 OBJ := $(patsubst samplers_amd/csrc/%.hip,build/%.o,$(SRC))
 LIB := samplers_amd/lib/libsamplers_hip.so
 # bounds-checked debug build (SP_DCHECK index / range invariants counted on the device,

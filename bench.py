@@ -54,6 +54,7 @@ import torch.distributed as dist  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec, MI355X_MICROARCH.md
 MFMA_F32_PEAK_TFLOPS = 157.3  # dense fp32 MFMA (v_mfma_f32_32x32x2_f32), MI355X_MICROARCH.md
+MFMA_BF16_PEAK_TFLOPS = 2516.6  # dense bf16 MFMA: 256 CUs x 4 SIMDs x 1024 FLOP/clk x 2.4 GHz (~2.5 PF)
 
 # DPS workloads of BASELINE.json (configs[0..2]); inpaint is the headline metric's config
 CONFIGS = {
@@ -231,10 +232,11 @@ def load_pmc() -> dict:
         return {}
 
 
-def conv_summary(kern: dict) -> dict | None:
-    """The prior's 3x3 convolution tiles (Winograd F(2x2,3x3) and direct, fwd + input VJP):
-    count, ms, executed MFMA FLOPs, and direct-convolution-equivalent FLOPs."""
-    names = ("wino3x3_fwd", "wino3x3_bwd_input", "conv3x3_fwd", "conv3x3_bwd_input")
+def conv_summary(kern: dict, names=("wino3x3_fwd", "wino3x3_bwd_input", "conv3x3_fwd",
+                                    "conv3x3_bwd_input")) -> dict | None:
+    """The prior's 3x3 convolution tiles (Winograd F(2x2,3x3) and direct, fwd + input VJP;
+    ``names=("conv3x3_bf16",)``: the bf16 implicit-GEMM tile): count, ms, executed MFMA FLOPs,
+    and direct-convolution-equivalent FLOPs."""
     parts = {k: kern[k] for k in names if k in kern}
     if not parts:
         return None

@@ -105,7 +105,8 @@ int sp_timing_enable(int on);
 int sp_timing_collect(int32_t* kinds, float* ms, int max_records);
 /* As sp_timing_collect, plus each launch's algorithmic work: samples for kinds 1-2 (DPS
  * passes), FLOPs for kinds 3-4 (sp_conv3x3_fwd / _bwd_input: 18*N*Cin*Cout*H*W) and
- * executed MFMA FLOPs for kinds 5-6 (sp_wino3x3_fwd / _bwd_input: 8*N*Cin*Cout*H*W). */
+ * executed MFMA FLOPs for kinds 5-6 (sp_wino3x3_fwd / _bwd_input: 8*N*Cin*Cout*H*W) and FLOPs
+ * for kind 7 (sp_conv3x3_bf16, forward or input VJP: 18*N*Cin*Cout*H*W). */
 int sp_timing_collect_work(int32_t* kinds, float* ms, double* work, int max_records);
 
 /* Library / ABI version (major*10000 + minor*100 + patch). */
@@ -558,6 +559,39 @@ int sp_softmax_bwd_rows(const float* p, float* dp, int64_t rows, int32_t n, floa
 int sp_conv1x1_small_supported(int32_t cin, int32_t cout, int64_t hw);
 int sp_conv1x1_small(const float* x, const float* w, const float* b, int64_t n, int32_t cin, int32_t cout,
                      int64_t hw, int32_t trans, float* y, sp_stream_t stream);
+
+/* ---- The priors at reduced precision (bf16), NHWC activations (csrc/sp_bf16.hip) ----------
+ * The reference's adapters take any torch_dtype and its PSLD driver runs SD 1.5 in bf16
+ * (reference: samplers/networks/diffusers/stable_diffusion.py:90-101, ddpm.py:23-34,
+ * scripts/run_psld.py:14-20).  These entry points are the bf16 layers of those priors:
+ * activations channels-last ([n][h][w][c]) bf16, bf16 MFMA operands, fp32 accumulation and
+ * fp32 statistics.  Device pointers; bf16 buffers are passed as void*. */
+int sp_conv3x3_bf16_supported(int32_t cin, int32_t cout, int32_t h, int32_t w);
+/* bf16 elements of the packed weights: [ceil(cout/64)][cin/16][9 taps][64 co][16 ci] */
+int64_t sp_conv3x3_bf16_packed_size(int32_t cin, int32_t cout);
+/* y = conv3x3(x) + bias (+ res): stride 1, padding 1 (diffusers' ResnetBlock2D / conv_in /
+ * conv_out / Upsample2D convolutions); the input VJP is the same call with the pack of
+ * W'[ci][co][2-ky][2-kx].  bias fp32 [cout] or NULL, res bf16 like y or NULL. */
+int sp_conv3x3_bf16(const void* x, const void* wp, const float* bias, const void* res, int64_t n, int32_t cin,
+                    int32_t cout, int32_t h, int32_t w, void* y, sp_stream_t stream);
+int sp_groupnorm_bf16_supported(int32_t c1, int32_t c2, int32_t groups);
+int64_t sp_groupnorm_bf16_workspace(int64_t n, int32_t c, int64_t hw);
+/* z = act(GroupNorm(cat(x1, x2) + chan_bias) * gamma + beta) over NHWC bf16 parts (channel
+ * concatenation read in place); stats = [mean | rstd] per (n, group), fp32. */
+int sp_groupnorm_bf16_fwd(const void* x1, const void* x2, int32_t c1, int32_t c2, const float* chan_bias,
+                          const float* gamma, const float* beta, int64_t n, int64_t hw, int32_t groups, float eps,
+                          int32_t act, void* z, float* stats, void* ws, int64_t ws_bytes, sp_stream_t stream);
+/* its input VJP into the parts' layouts (+ addends; outputs may alias them) */
+int sp_groupnorm_bf16_bwd(const void* dz, const void* x1, const void* x2, int32_t c1, int32_t c2,
+                          const float* chan_bias, const float* gamma, const float* beta, const float* stats,
+                          int64_t n, int64_t hw, int32_t groups, int32_t act, void* dx1, void* dx2, const void* add1,
+                          const void* add2, const void* add1b, void* ws, int64_t ws_bytes, sp_stream_t stream);
+int sp_attention_bf16_supported(int64_t batch, int32_t heads, int64_t n, int64_t m, int32_t d);
+/* multi-head softmax(q k^T scale) v on bf16 token rows (self: m = n; cross: kv_shared = 1 for
+ * one context row for the whole batch); lse [batch heads][n] fp32 for the VJP. */
+int sp_attention_bf16_fwd(const void* q, const void* k, const void* v, int64_t batch, int32_t heads, int64_t n,
+                          int64_t m, int32_t d, int32_t rsq, int32_t rskv, int32_t kv_shared, int32_t ro, float scale,
+                          void* out, float* lse, sp_stream_t stream);
 
 #ifdef __cplusplus
 }

@@ -230,6 +230,21 @@ SIGNATURES = {
                                          ctypes.c_int32, ctypes.c_int32, _P, _P]),
     "sp_wino3x3_bwd_input_pool": (ctypes.c_int, [_P, _P, _I64, ctypes.c_int32, ctypes.c_int32,
                                                  ctypes.c_int32, ctypes.c_int32, _P, _P]),
+    "sp_conv3x3_bf16_supported": (ctypes.c_int, [ctypes.c_int32] * 4),
+    "sp_conv3x3_bf16_packed_size": (_I64, [ctypes.c_int32, ctypes.c_int32]),
+    "sp_conv3x3_bf16": (ctypes.c_int, [_P, _P, _P, _P, _I64, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
+                                       ctypes.c_int32, _P, _P]),
+    "sp_groupnorm_bf16_supported": (ctypes.c_int, [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32]),
+    "sp_groupnorm_bf16_workspace": (_I64, [_I64, ctypes.c_int32, _I64]),
+    "sp_groupnorm_bf16_fwd": (ctypes.c_int, [_P, _P, ctypes.c_int32, ctypes.c_int32, _P, _P, _P, _I64, _I64,
+                                             ctypes.c_int32, _F, ctypes.c_int32, _P, _P, _P, _I64, _P]),
+    "sp_groupnorm_bf16_bwd": (ctypes.c_int, [_P, _P, _P, ctypes.c_int32, ctypes.c_int32, _P, _P, _P, _P, _I64,
+                                             _I64, ctypes.c_int32, ctypes.c_int32, _P, _P, _P, _P, _P, _P, _I64,
+                                             _P]),
+    "sp_attention_bf16_supported": (ctypes.c_int, [_I64, ctypes.c_int32, _I64, _I64, ctypes.c_int32]),
+    "sp_attention_bf16_fwd": (ctypes.c_int, [_P, _P, _P, _I64, ctypes.c_int32, _I64, _I64, ctypes.c_int32,
+                                             ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, _F,
+                                             _P, _P, _P]),
 }
 
 _lib = None

@@ -1,0 +1,908 @@
+// The priors at the reference's reduced precision (scripts/run_psld.py:14-20 runs SD 1.5 in bf16;
+// stable_diffusion.py:90-101 / ddpm.py:23-34 take any torch_dtype): bf16 activations in HBM,
+// bf16 operands on the bf16 MFMAs, fp32 accumulation and fp32 statistics.
+//
+// Layout: channels-last (NHWC) activations.  The 3x3 convolution is an implicit GEMM whose
+// contraction runs over (tap, input channel); with the channels innermost, the eight channels a
+// lane feeds to one MFMA are 16 contiguous bytes of one pixel, so the input patch is staged
+// into LDS as [pixel][16 channels] rows and every MFMA operand is one ds_read_b128 — no
+// transposes anywhere (NCHW would put the contraction index at a stride of H*W).  The same
+// layout is the token layout of the transformer blocks ([b][h w][c]).
+//
+//   k_conv3x3_bf16<TC>   3x3 / stride 1 / padding 1 convolution (+ fp32 bias, + bf16 residual)
+//                        and, with the flipped / transposed weight pack, its input VJP
+//   k_gnb_stats / _final / _apply / _bwd_*   GroupNorm(+per-(n,c) bias)(+SiLU) forward and
+//                        input VJP: per-chunk channel partial sums (shifted), a per-group
+//                        finalize in fp64, and a streaming apply — two reads and one write of
+//                        the bf16 tensor forward
+//   k_attnb_fwd<D>       multi-head attention softmax(q k^T / sqrt(d)) v on bf16 q / k / v
+//                        (self or cross, keys past m masked), output bf16, row log-sum-exp fp32
+//
+// C layout of v_mfma_f32_32x32x16_bf16: register i of lane l is row (i&3) + 8(i>>2) + 4(l>>5),
+// column l&31; A/B fragments: lane l holds A[row l&31][k 8(l>>5) + j] / B[k 8(l>>5) + j][col l&31],
+// j = 0..7 (cdna_hip_programming.md §3).
+
+#define SP_TU 14  // debug-build site numbering (sp_common.h SP_DCHECK)
+#include "sp_common.h"
+
+#include <algorithm>
+#include <cmath>
+
+namespace sp {
+
+typedef float bq_f16 __attribute__((ext_vector_type(16)));
+typedef unsigned bq_u4 __attribute__((ext_vector_type(4)));
+typedef unsigned bq_u2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bq_bf8 __attribute__((ext_vector_type(8)));
+typedef unsigned short u16;
+
+__device__ __forceinline__ bq_f16 bq_mfma(bq_u4 a, bq_u4 b, bq_f16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bq_bf8, a), __builtin_bit_cast(bq_bf8, b), c,
+                                                   0, 0, 0);
+}
+
+__device__ __forceinline__ float bf_lo(unsigned u) { return __uint_as_float(u << 16); }
+__device__ __forceinline__ float bf_hi(unsigned u) { return __uint_as_float(u & 0xffff0000u); }
+__device__ __forceinline__ float bf1(u16 v) { return __uint_as_float(static_cast<unsigned>(v) << 16); }
+// round to nearest even (v_cvt_pk_bf16_f32)
+__device__ __forceinline__ u16 f2bf(float f) { return __builtin_bit_cast(u16, static_cast<__bf16>(f)); }
+__device__ __forceinline__ unsigned pk2(float a, float b) {
+    return static_cast<unsigned>(f2bf(a)) | (static_cast<unsigned>(f2bf(b)) << 16);
+}
+__device__ __forceinline__ void unpack8(bq_u4 v, float (&f)[8]) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) f[2 * i] = bf_lo(v[i]), f[2 * i + 1] = bf_hi(v[i]);
+}
+__device__ __forceinline__ bq_u4 pack8(const float (&f)[8]) {
+    return bq_u4{pk2(f[0], f[1]), pk2(f[2], f[3]), pk2(f[4], f[5]), pk2(f[6], f[7])};
+}
+__device__ __forceinline__ float silu_f(float y) { return y * __builtin_amdgcn_rcpf(1.f + __expf(-y)); }
+
+// ---------------------------------------------------------------------------------------------
+// 3x3 convolution, NHWC, implicit GEMM on v_mfma_f32_32x32x16_bf16.
+//
+// Workgroup: 64 output channels x 512 output pixels, 4 waves; wave w holds all 64 channels of
+// pixels 128 w .. 128 w + 127 (2 x 4 MFMA tiles of 32 x 32: channels as A rows, pixels as B
+// columns, 128 accumulators).  The 512 pixels are TR "virtual rows" of TC columns: TC = 32 for
+// W % 32 == 0 (16 image rows of one sample), TC = W = H for the 16 / 8 / 4 levels (S whole
+// samples per tile, each with its own zero halo rows).  The contraction is staged 16 input
+// channels at a time: the weights of the stage ([tap][64 co][16 ci]) and the input patch
+// ([S (SR + 2) rows][TC + 2 cols][16 ci], zero halo) go to LDS as 48-byte rows (32 bytes + 16
+// pad: the 16 lanes of a ds_read_b128 group then read 16 distinct 4-bank slots for any start
+// pixel), 9 taps x 8 MFMAs per wave per stage; the next stage's global loads are issued into
+// registers before the current stage's MFMAs.
+// ---------------------------------------------------------------------------------------------
+template <int TC>
+struct CvGeo {
+    static_assert(TC == 32 || TC == 16 || TC == 8 || TC == 4, "tile width");
+    static constexpr int PX = 512;
+    static constexpr int TR = PX / TC;                // virtual rows per tile
+    static constexpr int SR = TC == 32 ? 16 : TC;     // image rows per sample segment
+    static constexpr int S = TR / SR;                 // sample segments per tile
+    static constexpr int PW = TC + 2;                 // patch columns
+    static constexpr int PH = S * (SR + 2);           // patch rows
+    static constexpr int PQ = PH * PW;                // patch pixels
+    static constexpr int RB = 48;                     // LDS bytes per row
+    static constexpr int WROWS = 9 * 64;              // weight rows per stage
+    static constexpr int LW = WROWS * RB;
+    static constexpr int LP = PQ * RB;
+    static constexpr int NW = (WROWS * 2 + kBlock - 1) / kBlock;  // 16-byte weight pieces per thread
+    static constexpr int NP = (PQ * 2 + kBlock - 1) / kBlock;     // 16-byte patch pieces per thread
+};
+
+template <int TC>
+__global__ __launch_bounds__(kBlock, 2) void k_conv3x3_bf16(const u16* __restrict__ x, const u16* __restrict__ wp,
+                                                         const float* __restrict__ bias, const u16* __restrict__ res,
+                                                         int n, int cin, int cout, int h, int w,
+                                                         u16* __restrict__ y) {
+    using G = CvGeo<TC>;
+    __shared__ __attribute__((aligned(16))) char lds[G::LW + G::LP];
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, r = lane & 31, hh = lane >> 5;
+    const int cb = blockIdx.x, pt = blockIdx.y;
+    int n0, h0, c0;
+    if constexpr (TC == 32) {
+        const int strips = w >> 5, rowblk = h / G::SR;
+        c0 = (pt % strips) * 32;
+        const int t = pt / strips;
+        h0 = (t % rowblk) * G::SR;
+        n0 = t / rowblk;
+    } else {
+        c0 = 0, h0 = 0, n0 = pt * G::S;
+    }
+    const int nci = cin >> 4;
+    const bq_u4* __restrict__ wsrc = reinterpret_cast<const bq_u4*>(wp + (int64_t)cb * nci * (9 * 64 * 16));
+
+    // per-thread patch pieces: global element offset (channel 0 of the stage) or -1 (halo / past the batch)
+    int64_t poff[G::NP];
+#pragma unroll
+    for (int k = 0; k < G::NP; ++k) {
+        const int i = tid + k * kBlock;
+        poff[k] = -1;
+        if (i < 2 * G::PQ) {
+            const int q = i >> 1, half = i & 1;
+            const int prow = q / G::PW, pcol = q - prow * G::PW;
+            const int seg = prow / (G::SR + 2), pr = prow - seg * (G::SR + 2);
+            const int nn = n0 + seg, hi = h0 + pr - 1, wi = c0 + pcol - 1;
+            if (nn < n && (unsigned)hi < (unsigned)h && (unsigned)wi < (unsigned)w)
+                poff[k] = (((int64_t)nn * h + hi) * w + wi) * cin + half * 8;
+        }
+    }
+    bq_u4 sw[G::NW], spx[G::NP];
+    auto gload = [&](int ks) {
+        const bq_u4* __restrict__ ws = wsrc + (int64_t)ks * (9 * 64 * 2);
+#pragma unroll
+        for (int k = 0; k < G::NW; ++k) {
+            const int i = tid + k * kBlock;
+            if (i < G::WROWS * 2) sw[k] = ws[i];
+        }
+#pragma unroll
+        for (int k = 0; k < G::NP; ++k)
+            spx[k] = poff[k] >= 0 ? *reinterpret_cast<const bq_u4*>(x + poff[k] + ks * 16) : bq_u4{0u, 0u, 0u, 0u};
+    };
+    auto lstore = [&]() {
+#pragma unroll
+        for (int k = 0; k < G::NW; ++k) {
+            const int i = tid + k * kBlock;
+            if (i < G::WROWS * 2) *reinterpret_cast<bq_u4*>(lds + (i >> 1) * G::RB + (i & 1) * 16) = sw[k];
+        }
+#pragma unroll
+        for (int k = 0; k < G::NP; ++k) {
+            const int i = tid + k * kBlock;
+            if (i < 2 * G::PQ) *reinterpret_cast<bq_u4*>(lds + G::LW + (i >> 1) * G::RB + (i & 1) * 16) = spx[k];
+        }
+    };
+
+    // B-operand base of each of the wave's 4 pixel tiles (tap (0, 0)); tap (dy, dx) adds dy PW + dx
+    int qb[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int p = 128 * wv + 32 * j + r, vr = p / TC, col = p - vr * TC;
+        const int seg = vr / G::SR, rr = vr - seg * G::SR;
+        qb[j] = ((seg * (G::SR + 2) + rr) * G::PW + col) * G::RB + hh * 16;
+    }
+    bq_f16 acc[2][4];
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[a][j] = bq_f16{};
+
+    gload(0);
+    for (int ks = 0; ks < nci; ++ks) {
+        __syncthreads();  // the previous stage's fragment reads are done
+        lstore();
+        __syncthreads();
+        if (ks + 1 < nci) gload(ks + 1);
+        const char* __restrict__ wl = lds + r * G::RB + hh * 16;
+        const char* __restrict__ pl = lds + G::LW;
+#pragma unroll
+        for (int t = 0; t < 9; ++t) {
+            const int dy = t / 3, dx = t - 3 * (t / 3);
+            const bq_u4 a0 = *reinterpret_cast<const bq_u4*>(wl + (t * 64) * G::RB);
+            const bq_u4 a1 = *reinterpret_cast<const bq_u4*>(wl + (t * 64 + 32) * G::RB);
+            bq_u4 b[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) b[j] = *reinterpret_cast<const bq_u4*>(pl + qb[j] + (dy * G::PW + dx) * G::RB);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                acc[0][j] = bq_mfma(a0, b[j], acc[0][j]);
+                acc[1][j] = bq_mfma(a1, b[j], acc[1][j]);
+            }
+        }
+    }
+
+    // epilogue: lane (pixel r of tile j) holds channels 64 cb + 32 a + 8 g + 4 hh + e in register 4 g + e
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int p = 128 * wv + 32 * j + r, vr = p / TC, col = p - vr * TC;
+        const int seg = vr / G::SR, rr = vr - seg * G::SR;
+        const int nn = n0 + seg;
+        if (nn >= n) continue;
+        const int64_t obase = (((int64_t)nn * h + h0 + rr) * w + c0 + col) * cout;
+        SP_DCHECK(h0 + rr < h && c0 + col < w);
+#pragma unroll
+        for (int a = 0; a < 2; ++a)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const int co = cb * 64 + 32 * a + 8 * g + 4 * hh;
+                float v[4];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) v[e] = acc[a][j][4 * g + e];
+                if (co + 4 <= cout && (cout & 3) == 0) {
+                    if (bias) {
+                        const float4 bb = *reinterpret_cast<const float4*>(bias + co);
+                        v[0] += bb.x, v[1] += bb.y, v[2] += bb.z, v[3] += bb.w;
+                    }
+                    if (res) {
+                        const bq_u2 rv = *reinterpret_cast<const bq_u2*>(res + obase + co);
+                        v[0] += bf_lo(rv.x), v[1] += bf_hi(rv.x), v[2] += bf_lo(rv.y), v[3] += bf_hi(rv.y);
+                    }
+                    *reinterpret_cast<bq_u2*>(y + obase + co) = bq_u2{pk2(v[0], v[1]), pk2(v[2], v[3])};
+                } else {
+#pragma unroll
+                    for (int e = 0; e < 4; ++e)
+                        if (co + e < cout) {
+                            float t = v[e] + (bias ? bias[co + e] : 0.f);
+                            if (res) t += bf1(res[obase + co + e]);
+                            y[obase + co + e] = f2bf(t);
+                        }
+                }
+            }
+    }
+}
+
+static int conv_tc(int h, int w) {
+    if (w % 32 == 0 && h % 16 == 0) return 32;
+    if (h == w && (w == 16 || w == 8 || w == 4)) return w;
+    return 0;
+}
+
+template <int TC>
+static void conv_bf16_launch(const u16* x, const u16* wp, const float* bias, const u16* res, int n, int cin,
+                             int cout, int h, int w, u16* y, hipStream_t s) {
+    using G = CvGeo<TC>;
+    const int cbn = (cout + 63) / 64;
+    int64_t tiles;
+    if constexpr (TC == 32)
+        tiles = (int64_t)n * (h / G::SR) * (w / 32);
+    else
+        tiles = (n + G::S - 1) / G::S;
+    const double flops = 18.0 * n * (double)h * w * cin * cout;
+    launch_w(TK_CONV_BF16, flops, k_conv3x3_bf16<TC>, dim3(cbn, static_cast<unsigned>(tiles)), dim3(kBlock), s, x, wp,
+             bias, res, n, cin, cout, h, w, y);
+}
+
+// ---------------------------------------------------------------------------------------------
+// GroupNorm over NHWC bf16 (groups of consecutive channels), fp32 statistics.
+//
+// stats pass (grid: chunks x batch): thread (vector column j, pixel row) accumulates, for its 8
+// channels, either the shifted sums  sum (x~ - s_c), sum (x~ - s_c)^2  (x~ = x + chan_bias,
+// s_c = x~ at the sample's first pixel: no cancellation when |mean| >> std), or for the VJP
+// sum g, sum g xhat (g = dy' gamma); the pixel rows of a column meet in LDS in a fixed order and
+// one partial per (sample, chunk, channel) is written.  finalize (one wave per (sample, group),
+// fp64, fixed order): forward -> mean, rstd and the per-(n, c) affine of the apply
+// (y = x sc + sh); VJP -> the per-(n, c) coefficients of dx = A dy' + B x + D.
+// ---------------------------------------------------------------------------------------------
+constexpr int GNB_TARGET_BLOCKS = 2048;
+
+struct GnbGeo {
+    int cv, rows, chunks, chunk_px;
+};
+
+static GnbGeo gnb_geo(int64_t n, int c, int64_t hw) {
+    GnbGeo g;
+    g.cv = c / 8;
+    g.rows = g.cv >= kBlock ? 1 : kBlock / g.cv;
+    int64_t want = std::max<int64_t>(1, (GNB_TARGET_BLOCKS + n - 1) / n);
+    int64_t maxc = std::max<int64_t>(1, hw / (4 * g.rows));
+    int64_t ch = std::min<int64_t>(want, maxc);
+    ch = std::min<int64_t>(ch, 1024);
+    g.chunk_px = static_cast<int>((hw + ch - 1) / ch);
+    g.chunks = static_cast<int>((hw + g.chunk_px - 1) / g.chunk_px);
+    return g;
+}
+
+// one 16-byte vector (8 channels, column j) of pixel p of sample nn, from the part that holds it
+__device__ __forceinline__ bq_u4 gnb_ld(const u16* __restrict__ x1, const u16* __restrict__ x2, int c1, int c2,
+                                        int64_t nn, int64_t hw, int64_t p, int j) {
+    const int ch = 8 * j;
+    if (ch < c1) return *reinterpret_cast<const bq_u4*>(x1 + ((nn * hw + p) * c1 + ch));
+    return *reinterpret_cast<const bq_u4*>(x2 + ((nn * hw + p) * c2 + ch - c1));
+}
+
+// MODE 0: forward shifted sums; MODE 1: VJP sums (g, g xhat) given per-(n,c) coefs
+// co = [sc | sh | xs | xo] (each n x c fp32) and gamma (c fp32)
+template <int MODE, bool ACT>
+__global__ __launch_bounds__(kBlock) void k_gnb_stats(const u16* __restrict__ x1, const u16* __restrict__ x2, int c1,
+                                                      int c2, const float* __restrict__ cbias,
+                                                      const u16* __restrict__ dz, const float* __restrict__ co,
+                                                      const float* __restrict__ gamma, int64_t hw, int chunk_px,
+                                                      float* __restrict__ part) {
+    __shared__ float red[kBlock * 16];
+    const int c = c1 + c2, cv = c / 8, nn = blockIdx.y, chunk = blockIdx.x, tid = threadIdx.x;
+    const int64_t nc = (int64_t)gridDim.y * c;
+    const int64_t p0 = (int64_t)chunk * chunk_px, p1 = std::min<int64_t>(hw, p0 + chunk_px);
+    for (int jb = 0; jb < cv; jb += kBlock) {  // column blocks (cv > 256 only: 2560 channels)
+        const int colw = std::min(cv - jb, kBlock);
+        const int rows_here = kBlock / colw;
+        const int j = jb + tid % colw, row = tid / colw;
+        const bool active = row < rows_here;
+        float s1[8] = {}, s2[8] = {};
+        if (active) {
+            float sh[8] = {}, cbv[8] = {}, k0[8], k1[8], k2[8], k3[8], gm[8];
+            if (cbias) {
+                const float4 a = *reinterpret_cast<const float4*>(cbias + (int64_t)nn * c + 8 * j);
+                const float4 b = *reinterpret_cast<const float4*>(cbias + (int64_t)nn * c + 8 * j + 4);
+                cbv[0] = a.x, cbv[1] = a.y, cbv[2] = a.z, cbv[3] = a.w, cbv[4] = b.x, cbv[5] = b.y, cbv[6] = b.z,
+                cbv[7] = b.w;
+            }
+            if constexpr (MODE == 0) {
+                float f[8];
+                unpack8(gnb_ld(x1, x2, c1, c2, nn, hw, 0, j), f);
+#pragma unroll
+                for (int e = 0; e < 8; ++e) sh[e] = f[e] + cbv[e];
+            } else {
+#pragma unroll
+                for (int e = 0; e < 8; ++e) {
+                    const int64_t ix = (int64_t)nn * c + 8 * j + e;
+                    k0[e] = co[ix], k1[e] = co[nc + ix], k2[e] = co[2 * nc + ix], k3[e] = co[3 * nc + ix];
+                    gm[e] = gamma[8 * j + e];
+                }
+            }
+            for (int64_t p = p0 + row; p < p1; p += rows_here) {
+                float f[8];
+                unpack8(gnb_ld(x1, x2, c1, c2, nn, hw, p, j), f);
+                if constexpr (MODE == 0) {
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) {
+                        const float d = f[e] + cbv[e] - sh[e];
+                        s1[e] += d;
+                        s2[e] = fmaf(d, d, s2[e]);
+                    }
+                } else {
+                    float dv[8];
+                    unpack8(*reinterpret_cast<const bq_u4*>(dz + ((int64_t)nn * hw + p) * c + 8 * j), dv);
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) {
+                        const float yv = fmaf(f[e], k0[e], k1[e]);
+                        float d = dv[e];
+                        if constexpr (ACT) {
+                            const float sg = __builtin_amdgcn_rcpf(1.f + __expf(-yv));
+                            d *= sg * (1.f + yv * (1.f - sg));
+                        }
+                        const float g = d * gm[e];
+                        const float xh = fmaf(f[e], k2[e], k3[e]);
+                        s1[e] += g;
+                        s2[e] = fmaf(g, xh, s2[e]);
+                    }
+                }
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int e = 0; e < 8; ++e) red[tid * 16 + e] = s1[e], red[tid * 16 + 8 + e] = s2[e];
+        __syncthreads();
+        // column reduce: thread t < colw sums rows 0 .. rows_here-1 of column t in order
+        if (tid < colw) {
+            float a1[8] = {}, a2[8] = {};
+            for (int rr = 0; rr < rows_here; ++rr) {
+                const float* src = red + (rr * colw + tid) * 16;
+#pragma unroll
+                for (int e = 0; e < 8; ++e) a1[e] += src[e], a2[e] += src[8 + e];
+            }
+            // partials [n][chunk][2][c]
+            float* dst = part + (((int64_t)nn * gridDim.x + chunk) * 2) * c + 8 * (jb + tid);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) dst[e] = a1[e], dst[c + e] = a2[e];
+        }
+    }
+}
+
+__device__ __forceinline__ double wave_sum_d(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+// forward finalize: one wave per (n, group).  stats = [mean | rstd] (n*groups each);
+// co = [sc | sh] (n*c each): y = x sc + sh.
+__global__ __launch_bounds__(64) void k_gnb_final_fwd(const u16* __restrict__ x1, const u16* __restrict__ x2, int c1,
+                                                      int c2, const float* __restrict__ cbias,
+                                                      const float* __restrict__ part, int chunks, int64_t hw,
+                                                      int groups, float eps, const float* __restrict__ gamma,
+                                                      const float* __restrict__ beta, float* __restrict__ stats,
+                                                      float* __restrict__ co) {
+    const int c = c1 + c2, cpg = c / groups, g = blockIdx.x, nn = blockIdx.y, lane = threadIdx.x;
+    const int64_t ng = (int64_t)gridDim.y * groups;
+    double sa = 0.0, sx = 0.0;
+    // pass 1: group sum of x~ (shift s_c re-read from the sample's first pixel)
+    for (int cc = lane; cc < cpg; cc += 64) {
+        const int ch = g * cpg + cc;
+        const float cbv = cbias ? cbias[(int64_t)nn * c + ch] : 0.f;
+        const float s = (ch < c1 ? bf1(x1[(int64_t)nn * hw * c1 + ch]) : bf1(x2[(int64_t)nn * hw * c2 + ch - c1])) + cbv;
+        double a = 0.0;
+        for (int k = 0; k < chunks; ++k) a += part[(((int64_t)nn * chunks + k) * 2) * c + ch];
+        sa += a + (double)hw * s;
+    }
+    const double cnt = (double)hw * cpg;
+    const double mean = wave_sum_d(sa) / cnt;
+    for (int cc = lane; cc < cpg; cc += 64) {
+        const int ch = g * cpg + cc;
+        const float cbv = cbias ? cbias[(int64_t)nn * c + ch] : 0.f;
+        const float s = (ch < c1 ? bf1(x1[(int64_t)nn * hw * c1 + ch]) : bf1(x2[(int64_t)nn * hw * c2 + ch - c1])) + cbv;
+        double a = 0.0, b = 0.0;
+        for (int k = 0; k < chunks; ++k) {
+            const float* pp = part + (((int64_t)nn * chunks + k) * 2) * c + ch;
+            a += pp[0];
+            b += pp[c];
+        }
+        const double dm = (double)s - mean;
+        sx += b + 2.0 * dm * a + (double)hw * dm * dm;
+    }
+    const double var = std::max(0.0, wave_sum_d(sx) / cnt);
+    const float rstd = (float)(1.0 / sqrt(var + (double)eps));
+    const float meanf = (float)mean;
+    if (lane == 0) stats[(int64_t)nn * groups + g] = meanf, stats[ng + (int64_t)nn * groups + g] = rstd;
+    const int64_t nc = (int64_t)gridDim.y * c;
+    for (int cc = lane; cc < cpg; cc += 64) {
+        const int ch = g * cpg + cc;
+        const float cbv = cbias ? cbias[(int64_t)nn * c + ch] : 0.f;
+        const float sc = rstd * (gamma ? gamma[ch] : 1.f);
+        co[(int64_t)nn * c + ch] = sc;
+        co[nc + (int64_t)nn * c + ch] = (beta ? beta[ch] : 0.f) + (cbv - meanf) * sc;
+    }
+}
+
+// per-(n, c) coefficients for the VJP from the forward's stats: co = [sc | sh | xs | xo]
+// (y = x sc + sh, xhat = x xs + xo)
+__global__ void k_gnb_coefs(const float* __restrict__ stats, const float* __restrict__ cbias,
+                            const float* __restrict__ gamma, const float* __restrict__ beta, int n, int c,
+                            int groups, float* __restrict__ co) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x, nc = (int64_t)n * c;
+    if (i >= nc) return;
+    const int nn = static_cast<int>(i / c), ch = static_cast<int>(i - (int64_t)nn * c), g = ch / (c / groups);
+    const float mean = stats[(int64_t)nn * groups + g], rstd = stats[(int64_t)n * groups + (int64_t)nn * groups + g];
+    const float cbv = cbias ? cbias[i] : 0.f;
+    const float sc = rstd * (gamma ? gamma[ch] : 1.f);
+    co[i] = sc;
+    co[nc + i] = (beta ? beta[ch] : 0.f) + (cbv - mean) * sc;
+    co[2 * nc + i] = rstd;
+    co[3 * nc + i] = (cbv - mean) * rstd;
+}
+
+// VJP finalize: one wave per (n, group): m1 = mean(g), m2 = mean(g xhat) over the group ->
+// dx = A dy' + B x + D with A = rstd gamma_c, B = -rstd^2 m2, D = -rstd (m1 + m2 xo_c);
+// co2 = [A | B | D]
+__global__ __launch_bounds__(64) void k_gnb_final_bwd(const float* __restrict__ part, int chunks, int64_t hw, int c,
+                                                      int groups, const float* __restrict__ stats,
+                                                      const float* __restrict__ gamma, const float* __restrict__ co,
+                                                      float* __restrict__ co2) {
+    const int cpg = c / groups, g = blockIdx.x, nn = blockIdx.y, lane = threadIdx.x, n = gridDim.y;
+    double s1 = 0.0, s2 = 0.0;
+    for (int cc = lane; cc < cpg; cc += 64) {
+        const int ch = g * cpg + cc;
+        for (int k = 0; k < chunks; ++k) {
+            const float* pp = part + (((int64_t)nn * chunks + k) * 2) * c + ch;
+            s1 += pp[0];
+            s2 += pp[c];
+        }
+    }
+    const double cnt = (double)hw * cpg;
+    const float m1 = (float)(wave_sum_d(s1) / cnt), m2 = (float)(wave_sum_d(s2) / cnt);
+    const float rstd = stats[(int64_t)n * groups + (int64_t)nn * groups + g];
+    const int64_t nc = (int64_t)n * c;
+    for (int cc = lane; cc < cpg; cc += 64) {
+        const int ch = g * cpg + cc;
+        const int64_t i = (int64_t)nn * c + ch;
+        co2[i] = rstd * (gamma ? gamma[ch] : 1.f);
+        co2[nc + i] = -rstd * rstd * m2;
+        co2[2 * nc + i] = -rstd * (m1 + m2 * co[3 * nc + i]);
+    }
+}
+
+// forward apply: z = act(x sc + sh) over the concatenated channels (one 16-byte vector per
+// thread-iteration; the (n, c) coefficients stay in L2)
+template <bool ACT>
+__global__ __launch_bounds__(kBlock) void k_gnb_apply(const u16* __restrict__ x1, const u16* __restrict__ x2, int c1,
+                                                      int c2, const float* __restrict__ co, int64_t n, int64_t hw,
+                                                      u16* __restrict__ z) {
+    const int c = c1 + c2, cv = c / 8;
+    const int64_t total = n * hw * cv, nc = n * c;
+    for (int64_t v = (int64_t)blockIdx.x * kBlock + threadIdx.x; v < total; v += (int64_t)gridDim.x * kBlock) {
+        const int j = static_cast<int>(v % cv);
+        const int64_t pix = v / cv, nn = pix / hw, p = pix - nn * hw;
+        float f[8];
+        unpack8(gnb_ld(x1, x2, c1, c2, nn, hw, p, j), f);
+        const float* sc = co + nn * c + 8 * j;
+        const float* sh = co + nc + nn * c + 8 * j;
+        const float4 a0 = *reinterpret_cast<const float4*>(sc), a1 = *reinterpret_cast<const float4*>(sc + 4);
+        const float4 b0 = *reinterpret_cast<const float4*>(sh), b1 = *reinterpret_cast<const float4*>(sh + 4);
+        const float sa[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+        const float sb[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            const float yv = fmaf(f[e], sa[e], sb[e]);
+            f[e] = ACT ? silu_f(yv) : yv;
+        }
+        *reinterpret_cast<bq_u4*>(z + pix * c + 8 * j) = pack8(f);
+    }
+}
+
+// VJP apply: dx = A dy' + B x + D (+ add1 / add2 / add1b), written to the parts' layouts
+template <bool ACT>
+__global__ __launch_bounds__(kBlock) void k_gnb_bwd_apply(const u16* __restrict__ dz, const u16* __restrict__ x1,
+                                                          const u16* __restrict__ x2, int c1, int c2,
+                                                          const float* __restrict__ co, const float* __restrict__ co2,
+                                                          int64_t n, int64_t hw, u16* __restrict__ dx1,
+                                                          u16* __restrict__ dx2, const u16* __restrict__ add1,
+                                                          const u16* __restrict__ add2,
+                                                          const u16* __restrict__ add1b) {
+    const int c = c1 + c2, cv = c / 8;
+    const int64_t total = n * hw * cv, nc = n * c;
+    for (int64_t v = (int64_t)blockIdx.x * kBlock + threadIdx.x; v < total; v += (int64_t)gridDim.x * kBlock) {
+        const int j = static_cast<int>(v % cv);
+        const int64_t pix = v / cv, nn = pix / hw, p = pix - nn * hw;
+        float f[8], d[8];
+        unpack8(gnb_ld(x1, x2, c1, c2, nn, hw, p, j), f);
+        unpack8(*reinterpret_cast<const bq_u4*>(dz + pix * c + 8 * j), d);
+        const int64_t ci = nn * c + 8 * j;
+        float o[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            float dd = d[e];
+            if constexpr (ACT) {
+                const float yv = fmaf(f[e], co[ci + e], co[nc + ci + e]);
+                const float sg = __builtin_amdgcn_rcpf(1.f + __expf(-yv));
+                dd *= sg * (1.f + yv * (1.f - sg));
+            }
+            o[e] = fmaf(co2[ci + e], dd, fmaf(co2[nc + ci + e], f[e], co2[2 * nc + ci + e]));
+        }
+        const int ch = 8 * j;
+        const bool first = ch < c1;
+        const int64_t off = first ? (nn * hw + p) * c1 + ch : (nn * hw + p) * c2 + ch - c1;
+        const u16* a = first ? add1 : add2;
+        if (a) {
+            float t[8];
+            unpack8(*reinterpret_cast<const bq_u4*>(a + off), t);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) o[e] += t[e];
+        }
+        if (first && add1b) {
+            float t[8];
+            unpack8(*reinterpret_cast<const bq_u4*>(add1b + off), t);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) o[e] += t[e];
+        }
+        *reinterpret_cast<bq_u4*>((first ? dx1 : dx2) + off) = pack8(o);
+    }
+}
+
+static unsigned stream_blocks(int64_t vectors) {
+    return static_cast<unsigned>(std::max<int64_t>(1, std::min<int64_t>((vectors + kBlock - 1) / kBlock, 256 * 16)));
+}
+
+// ---------------------------------------------------------------------------------------------
+// Multi-head attention on bf16 q / k / v (the SD 1.5 UNet's attn1 / attn2 at the reference's
+// bf16): the structure of k_attn6_fwd (sp_attention6.hip) with one bf16 term per operand.
+// Per wave 32 queries; per 32-key block S^T = K Q^T (K rows from LDS as A, Q^T in registers as
+// B, d padded to 16), the softmax on the lane-local query column (scores scaled by
+// scale log2 e in fp32), O^T += V^T P^T with P^T packed to bf16 straight from the S^T
+// accumulators (key order inside the MFMA's K = the C layout's, V^T staged in that order).
+// Keys past m are masked (-inf); queries past n are computed on zero rows and not stored.
+// ---------------------------------------------------------------------------------------------
+constexpr float AB_LOG2E = 1.4426950408889634f;
+constexpr float AB_LN2 = 0.6931471805599453f;
+constexpr int AB_QW = 32, AB_WB = 4 * AB_QW;
+constexpr float AB_LAZY = 8.f;
+
+__device__ __forceinline__ int ab_pos(int k) { return (k & ~12) | ((k & 4) << 1) | ((k & 8) >> 1); }
+
+template <int D>
+struct AbGeo {
+    static_assert(D % 8 == 0 && D <= 160, "head dim");
+    static constexpr int DK = (D + 15) / 16;
+    static constexpr int DKP = DK * 16;
+    static constexpr int DT = (D + 31) / 32;
+    static constexpr int SB = 64;
+    static constexpr int KROW = DKP + 8;   // bf16 per K row in LDS
+    static constexpr int VROW = SB + 8;    // bf16 per V^T row
+    static constexpr int NKU = (SB * (D / 8) + kBlock - 1) / kBlock;          // K 16-byte pieces per thread
+    static constexpr int NVU = (SB / 2 * (D / 8) + kBlock - 1) / kBlock;      // V (2 keys x 8 d) units
+};
+
+template <int D>
+__global__ __launch_bounds__(kBlock) void k_attnb_fwd(const u16* __restrict__ q, const u16* __restrict__ k,
+                                                      const u16* __restrict__ v, int n, int m, int heads,
+                                                      int rsq, int rskv, int kv_shared, int ro, float sl2,
+                                                      u16* __restrict__ out, float* __restrict__ lse) {
+    using G = AbGeo<D>;
+    __shared__ __attribute__((aligned(16))) u16 Ks[G::SB * G::KROW];
+    __shared__ __attribute__((aligned(16))) u16 Vs[G::DT * 32 * G::VROW];
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, r = lane & 31, hh = lane >> 5;
+    const int bh = blockIdx.y, b = bh / heads, hd = bh - b * heads;
+    const int q0 = blockIdx.x * AB_WB + wv * AB_QW;
+    const u16* __restrict__ qb = q + (int64_t)b * n * rsq + hd * D;
+    const int64_t kvb = (kv_shared ? 0 : (int64_t)b * m * rskv) + hd * D;
+
+    if constexpr (G::DKP > D) {  // K's padding columns: zero once
+        for (int i = tid; i < G::SB; i += kBlock)
+#pragma unroll
+            for (int cc = D; cc < G::DKP; cc += 2) *reinterpret_cast<unsigned*>(Ks + i * G::KROW + cc) = 0u;
+    }
+    // Q^T as B: lane (query r, half hh) holds Q[q0 + r][16 s + 8 hh + j]
+    bq_u4 qf[G::DK];
+    const int qq = q0 + r;
+#pragma unroll
+    for (int s = 0; s < G::DK; ++s) {
+        const int d0 = 16 * s + 8 * hh;
+        qf[s] = (d0 + 8 <= D && qq < n) ? *reinterpret_cast<const bq_u4*>(qb + (int64_t)qq * rsq + d0)
+                                        : bq_u4{0u, 0u, 0u, 0u};
+    }
+    bq_f16 o[G::DT];
+#pragma unroll
+    for (int dt = 0; dt < G::DT; ++dt) o[dt] = bq_f16{};
+    float mx = -INFINITY, l = 0.f;
+
+    const int nst = (m + G::SB - 1) / G::SB;
+    bq_u4 kr[G::NKU], vr[G::NVU][2];
+    auto load_stage = [&](int si) {
+        const int kbase = si * G::SB;
+#pragma unroll
+        for (int j = 0; j < G::NKU; ++j) {
+            const int i = tid + j * kBlock;
+            if (i < G::SB * (D / 8)) {
+                const int row = i / (D / 8), col = 8 * (i - row * (D / 8));
+                kr[j] = kbase + row < m ? *reinterpret_cast<const bq_u4*>(k + kvb + (int64_t)(kbase + row) * rskv + col)
+                                        : bq_u4{0u, 0u, 0u, 0u};
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < G::NVU; ++j) {
+            const int u = tid + j * kBlock;
+            if (u < G::SB / 2 * (D / 8)) {
+                const int p = u / (D / 8), d0 = 8 * (u - p * (D / 8));
+                const int k0 = kbase + 2 * p;
+                vr[j][0] = k0 < m ? *reinterpret_cast<const bq_u4*>(v + kvb + (int64_t)k0 * rskv + d0)
+                                  : bq_u4{0u, 0u, 0u, 0u};
+                vr[j][1] = k0 + 1 < m ? *reinterpret_cast<const bq_u4*>(v + kvb + (int64_t)(k0 + 1) * rskv + d0)
+                                      : bq_u4{0u, 0u, 0u, 0u};
+            }
+        }
+    };
+    auto store_stage = [&]() {
+#pragma unroll
+        for (int j = 0; j < G::NKU; ++j) {
+            const int i = tid + j * kBlock;
+            if (i < G::SB * (D / 8)) {
+                const int row = i / (D / 8), col = 8 * (i - row * (D / 8));
+                *reinterpret_cast<bq_u4*>(Ks + row * G::KROW + col) = kr[j];
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < G::NVU; ++j) {
+            const int u = tid + j * kBlock;
+            if (u < G::SB / 2 * (D / 8)) {
+                const int p = u / (D / 8), d0 = 8 * (u - p * (D / 8));
+                const int key = 2 * p, pos = (key & ~15) | ab_pos(key & 15);  // keys 2p, 2p + 1 adjacent
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const unsigned a = vr[j][0][e], c = vr[j][1][e];
+                    // d0 + 2e: (key 2p, key 2p + 1) low halves; d0 + 2e + 1: high halves
+                    *reinterpret_cast<unsigned*>(Vs + (d0 + 2 * e) * G::VROW + pos) = (a & 0xffffu) | (c << 16);
+                    *reinterpret_cast<unsigned*>(Vs + (d0 + 2 * e + 1) * G::VROW + pos) = (a >> 16) | (c & 0xffff0000u);
+                }
+            }
+        }
+    };
+    load_stage(0);
+    for (int si = 0; si < nst; ++si) {
+        __syncthreads();
+        store_stage();
+        __syncthreads();
+        if (si + 1 < nst) load_stage(si + 1);
+        const int kbase = si * G::SB;
+#pragma unroll
+        for (int kb32 = 0; kb32 < G::SB / 32; ++kb32) {
+            if (kbase + kb32 * 32 >= m) break;  // wave-uniform
+            bq_f16 sv = bq_f16{};
+#pragma unroll
+            for (int s = 0; s < G::DK; ++s) {
+                const bq_u4 kf = *reinterpret_cast<const bq_u4*>(Ks + (kb32 * 32 + r) * G::KROW + 16 * s + 8 * hh);
+                sv = bq_mfma(kf, qf[s], sv);
+            }
+            float bm = -INFINITY;
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                const int key = kbase + kb32 * 32 + (i & 3) + 8 * (i >> 2) + 4 * hh;
+                sv[i] = key < m ? sv[i] * sl2 : -INFINITY;
+                bm = fmaxf(bm, sv[i]);
+            }
+            bm = fmaxf(bm, __shfl_xor(bm, 32));
+            const float mn = bm > mx + AB_LAZY ? bm : mx;
+            const float corr = __builtin_amdgcn_exp2f(mx - mn);
+            mx = mn;
+            float p[16], ps = 0.f;
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                p[i] = __builtin_amdgcn_exp2f(sv[i] - mn);
+                ps += p[i];
+            }
+            l = fmaf(l, corr, ps);
+            if (__builtin_amdgcn_ballot_w64(corr != 1.f))
+#pragma unroll
+                for (int dt = 0; dt < G::DT; ++dt) o[dt] *= corr;
+            bq_u4 pf[2];
+#pragma unroll
+            for (int kk = 0; kk < 2; ++kk)
+                pf[kk] = bq_u4{pk2(p[8 * kk], p[8 * kk + 1]), pk2(p[8 * kk + 2], p[8 * kk + 3]),
+                               pk2(p[8 * kk + 4], p[8 * kk + 5]), pk2(p[8 * kk + 6], p[8 * kk + 7])};
+#pragma unroll
+            for (int dt = 0; dt < G::DT; ++dt)
+#pragma unroll
+                for (int kk = 0; kk < 2; ++kk) {
+                    const bq_u4 vf = *reinterpret_cast<const bq_u4*>(Vs + (dt * 32 + r) * G::VROW + kb32 * 32 + kk * 16 + 8 * hh);
+                    o[dt] = bq_mfma(vf, pf[kk], o[dt]);
+                }
+        }
+    }
+    const float tot = l + __shfl_xor(l, 32);
+    const float inv = 1.f / tot;
+    if (qq >= n) return;
+    u16* orow = out + (int64_t)b * n * ro + hd * D + (int64_t)qq * ro;
+#pragma unroll
+    for (int dt = 0; dt < G::DT; ++dt)
+#pragma unroll
+        for (int g4 = 0; g4 < 4; ++g4) {
+            const int d0 = 32 * dt + 8 * g4 + 4 * hh;
+            if (d0 + 4 <= D)
+                *reinterpret_cast<bq_u2*>(orow + d0) = bq_u2{pk2(o[dt][4 * g4] * inv, o[dt][4 * g4 + 1] * inv),
+                                                             pk2(o[dt][4 * g4 + 2] * inv, o[dt][4 * g4 + 3] * inv)};
+        }
+    if (hh == 0) lse[(int64_t)bh * n + qq] = (mx + log2f(tot)) * AB_LN2;
+}
+
+template <int D>
+static void attnb_launch(const u16* q, const u16* k, const u16* v, int64_t batch, int heads, int64_t n, int64_t m,
+                         int rsq, int rskv, int kv_shared, int ro, float scale, u16* out, float* lse, hipStream_t s) {
+    const dim3 grid(static_cast<unsigned>((n + AB_WB - 1) / AB_WB), static_cast<unsigned>(batch * heads));
+    launch(0, k_attnb_fwd<D>, grid, dim3(kBlock), s, q, k, v, static_cast<int>(n), static_cast<int>(m), heads, rsq,
+           rskv, kv_shared, ro, scale * AB_LOG2E, out, lse);
+}
+
+}  // namespace sp
+
+using namespace sp;
+
+extern "C" {
+
+// ---- 3x3 convolution ------------------------------------------------------------------------
+
+int sp_conv3x3_bf16_supported(int32_t cin, int32_t cout, int32_t h, int32_t w) {
+    return cin > 0 && cin % 16 == 0 && cout > 0 && conv_tc(h, w) != 0;
+}
+
+// elements (bf16) of the packed weights: [ceil(cout/64)][cin/16][9][64][16]
+int64_t sp_conv3x3_bf16_packed_size(int32_t cin, int32_t cout) {
+    return (int64_t)((cout + 63) / 64) * 64 * cin * 9;
+}
+
+// y[n][h][w][cout] = conv3x3(x[n][h][w][cin], W) + bias (+ res), NHWC bf16, fp32 accumulation.
+// wp: packed as [co block of 64][ci block of 16][tap 3 ky + kx][64 co][16 ci] (rows past cout
+// zero); the input VJP is the same call with the pack of W'[ci][co][2-ky][2-kx].
+int sp_conv3x3_bf16(const void* x, const void* wp, const float* bias, const void* res, int64_t n, int32_t cin,
+                    int32_t cout, int32_t h, int32_t w, void* y, sp_stream_t stream) {
+    if (!x || !wp || !y || n <= 0 || !sp_conv3x3_bf16_supported(cin, cout, h, w)) return SP_EINVAL;
+    if (n * h * (int64_t)w * std::max(cin, cout) >= (int64_t(1) << 40) || n >= (int64_t(1) << 30)) return SP_EINVAL;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const u16* xx = static_cast<const u16*>(x);
+    const u16* ww = static_cast<const u16*>(wp);
+    const u16* rr = static_cast<const u16*>(res);
+    u16* yy = static_cast<u16*>(y);
+    const int ni = static_cast<int>(n);
+    switch (conv_tc(h, w)) {
+        case 32: conv_bf16_launch<32>(xx, ww, bias, rr, ni, cin, cout, h, w, yy, s); break;
+        case 16: conv_bf16_launch<16>(xx, ww, bias, rr, ni, cin, cout, h, w, yy, s); break;
+        case 8: conv_bf16_launch<8>(xx, ww, bias, rr, ni, cin, cout, h, w, yy, s); break;
+        default: conv_bf16_launch<4>(xx, ww, bias, rr, ni, cin, cout, h, w, yy, s); break;
+    }
+    return check_launch("sp_conv3x3_bf16");
+}
+
+// ---- GroupNorm ------------------------------------------------------------------------------
+
+int sp_groupnorm_bf16_supported(int32_t c1, int32_t c2, int32_t groups) {
+    const int c = c1 + c2;
+    return c1 > 0 && c1 % 8 == 0 && c2 >= 0 && c2 % 8 == 0 && groups > 0 && c % groups == 0 && c <= 8 * 1024;
+}
+
+// workspace bytes (fp32): partials [n][chunks][2][c] + coefficients [4][n][c] + [3][n][c]
+int64_t sp_groupnorm_bf16_workspace(int64_t n, int32_t c, int64_t hw) {
+    const GnbGeo g = gnb_geo(n, c, hw);
+    return 4 * (n * g.chunks * 2 * (int64_t)c + 7 * n * (int64_t)c);
+}
+
+// z[n][hw][c] = act(GroupNorm(cat(x1, x2) + chan_bias[n][c]) * gamma + beta), NHWC bf16;
+// stats = [mean | rstd] (2 n groups fp32, for the VJP); gamma / beta / chan_bias fp32 or NULL.
+int sp_groupnorm_bf16_fwd(const void* x1, const void* x2, int32_t c1, int32_t c2, const float* chan_bias,
+                          const float* gamma, const float* beta, int64_t n, int64_t hw, int32_t groups, float eps,
+                          int32_t act, void* z, float* stats, void* ws, int64_t ws_bytes, sp_stream_t stream) {
+    if (!x1 || (c2 && !x2) || !z || !stats || !ws || n <= 0 || hw <= 0 || !sp_groupnorm_bf16_supported(c1, c2, groups))
+        return SP_EINVAL;
+    const int c = c1 + c2;
+    if (ws_bytes < sp_groupnorm_bf16_workspace(n, c, hw) || n * hw * c >= (int64_t(1) << 40) || n > 65535)
+        return SP_EINVAL;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const GnbGeo g = gnb_geo(n, c, hw);
+    float* part = static_cast<float*>(ws);
+    float* co = part + n * g.chunks * 2 * (int64_t)c;
+    const u16* a = static_cast<const u16*>(x1);
+    const u16* b = static_cast<const u16*>(x2);
+    launch(0, k_gnb_stats<0, false>, dim3(g.chunks, static_cast<unsigned>(n)), dim3(kBlock), s, a, b, c1, c2,
+           chan_bias, static_cast<const u16*>(nullptr), static_cast<const float*>(nullptr),
+           static_cast<const float*>(nullptr), hw, g.chunk_px, part);
+    launch(0, k_gnb_final_fwd, dim3(groups, static_cast<unsigned>(n)), dim3(64), s, a, b, c1, c2, chan_bias,
+           static_cast<const float*>(part), g.chunks, hw, groups, eps, gamma, beta, stats, co);
+    const unsigned blocks = stream_blocks(n * hw * (c / 8));
+    if (act)
+        launch(0, k_gnb_apply<true>, dim3(blocks), dim3(kBlock), s, a, b, c1, c2, static_cast<const float*>(co), n, hw,
+               static_cast<u16*>(z));
+    else
+        launch(0, k_gnb_apply<false>, dim3(blocks), dim3(kBlock), s, a, b, c1, c2, static_cast<const float*>(co), n,
+               hw, static_cast<u16*>(z));
+    return check_launch("sp_groupnorm_bf16_fwd");
+}
+
+// input VJP of sp_groupnorm_bf16_fwd given its stats: dx1 / dx2 (the parts' layouts) =
+// GN^T dz (+ add1 / add2, + add1b into dx1); the outputs may alias the addends.
+int sp_groupnorm_bf16_bwd(const void* dz, const void* x1, const void* x2, int32_t c1, int32_t c2,
+                          const float* chan_bias, const float* gamma, const float* beta, const float* stats,
+                          int64_t n, int64_t hw, int32_t groups, int32_t act, void* dx1, void* dx2, const void* add1,
+                          const void* add2, const void* add1b, void* ws, int64_t ws_bytes, sp_stream_t stream) {
+    if (!dz || !x1 || (c2 && (!x2 || !dx2)) || !dx1 || !stats || !ws || n <= 0 || hw <= 0 ||
+        !sp_groupnorm_bf16_supported(c1, c2, groups))
+        return SP_EINVAL;
+    const int c = c1 + c2;
+    if (ws_bytes < sp_groupnorm_bf16_workspace(n, c, hw) || n * hw * c >= (int64_t(1) << 40) || n > 65535)
+        return SP_EINVAL;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const GnbGeo g = gnb_geo(n, c, hw);
+    float* part = static_cast<float*>(ws);
+    float* co = part + n * g.chunks * 2 * (int64_t)c;
+    float* co2 = co + 4 * n * (int64_t)c;
+    const u16* a = static_cast<const u16*>(x1);
+    const u16* b = static_cast<const u16*>(x2);
+    const u16* d = static_cast<const u16*>(dz);
+    const int64_t nc = n * c;
+    launch(0, k_gnb_coefs, dim3(static_cast<unsigned>((nc + kBlock - 1) / kBlock)), dim3(kBlock), s, stats, chan_bias,
+           gamma, beta, static_cast<int>(n), c, groups, co);
+    if (act)
+        launch(0, k_gnb_stats<1, true>, dim3(g.chunks, static_cast<unsigned>(n)), dim3(kBlock), s, a, b, c1, c2,
+               chan_bias, d, static_cast<const float*>(co), gamma, hw, g.chunk_px, part);
+    else
+        launch(0, k_gnb_stats<1, false>, dim3(g.chunks, static_cast<unsigned>(n)), dim3(kBlock), s, a, b, c1, c2,
+               chan_bias, d, static_cast<const float*>(co), gamma, hw, g.chunk_px, part);
+    launch(0, k_gnb_final_bwd, dim3(groups, static_cast<unsigned>(n)), dim3(64), s, static_cast<const float*>(part),
+           g.chunks, hw, c, groups, stats, gamma, static_cast<const float*>(co), co2);
+    const unsigned blocks = stream_blocks(n * hw * (c / 8));
+    if (act)
+        launch(0, k_gnb_bwd_apply<true>, dim3(blocks), dim3(kBlock), s, d, a, b, c1, c2, static_cast<const float*>(co),
+               static_cast<const float*>(co2), n, hw, static_cast<u16*>(dx1), static_cast<u16*>(dx2),
+               static_cast<const u16*>(add1), static_cast<const u16*>(add2), static_cast<const u16*>(add1b));
+    else
+        launch(0, k_gnb_bwd_apply<false>, dim3(blocks), dim3(kBlock), s, d, a, b, c1, c2, static_cast<const float*>(co),
+               static_cast<const float*>(co2), n, hw, static_cast<u16*>(dx1), static_cast<u16*>(dx2),
+               static_cast<const u16*>(add1), static_cast<const u16*>(add2), static_cast<const u16*>(add1b));
+    return check_launch("sp_groupnorm_bf16_bwd");
+}
+
+// ---- attention ------------------------------------------------------------------------------
+
+int sp_attention_bf16_supported(int64_t batch, int32_t heads, int64_t n, int64_t m, int32_t d) {
+    if (batch <= 0 || heads <= 0 || batch * heads > 65535 || n <= 0 || m <= 0 || n > (int64_t(1) << 24) ||
+        m > (int64_t(1) << 24))
+        return 0;
+    return d == 40 || d == 64 || d == 80 || d == 160;
+}
+
+// out[b][i][h d .. h d + d) = softmax(q k^T scale) v for head h: q rows of stride rsq
+// ([batch][n][rsq]), k / v rows of stride rskv ([batch or 1 (kv_shared)][m][rskv]), out rows of
+// stride ro; bf16 in and out, lse [batch heads][n] fp32 (natural log).  Pointers at head 0.
+int sp_attention_bf16_fwd(const void* q, const void* k, const void* v, int64_t batch, int32_t heads, int64_t n,
+                          int64_t m, int32_t d, int32_t rsq, int32_t rskv, int32_t kv_shared, int32_t ro, float scale,
+                          void* out, float* lse, sp_stream_t stream) {
+    if (!q || !k || !v || !out || !lse || !sp_attention_bf16_supported(batch, heads, n, m, d)) return SP_EINVAL;
+    if (rsq < heads * d || rskv < heads * d || ro < heads * d || rsq % 8 || rskv % 8 || ro % 4) return SP_EINVAL;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const u16* qq = static_cast<const u16*>(q);
+    const u16* kk = static_cast<const u16*>(k);
+    const u16* vv = static_cast<const u16*>(v);
+    u16* oo = static_cast<u16*>(out);
+    switch (d) {
+        case 40: attnb_launch<40>(qq, kk, vv, batch, heads, n, m, rsq, rskv, kv_shared, ro, scale, oo, lse, s); break;
+        case 64: attnb_launch<64>(qq, kk, vv, batch, heads, n, m, rsq, rskv, kv_shared, ro, scale, oo, lse, s); break;
+        case 80: attnb_launch<80>(qq, kk, vv, batch, heads, n, m, rsq, rskv, kv_shared, ro, scale, oo, lse, s); break;
+        default: attnb_launch<160>(qq, kk, vv, batch, heads, n, m, rsq, rskv, kv_shared, ro, scale, oo, lse, s); break;
+    }
+    return check_launch("sp_attention_bf16_fwd");
+}
+
+}  // extern "C"

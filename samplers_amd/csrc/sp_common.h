@@ -239,7 +239,8 @@ enum {
     TK_CONV3X3_FWD = 3,
     TK_CONV3X3_BWD_INPUT = 4,
     TK_WINO3X3_FWD = 5,
-    TK_WINO3X3_BWD_INPUT = 6
+    TK_WINO3X3_BWD_INPUT = 6,
+    TK_CONV_BF16 = 7
 };
 
 template <typename K, typename... Args>

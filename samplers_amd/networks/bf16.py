@@ -1,0 +1,376 @@
+"""The priors' layers at bf16 — the reference's reduced-precision runs on this project's kernels.
+
+The reference's adapters take any ``torch_dtype`` (``/root/reference/samplers/networks/diffusers/
+stable_diffusion.py:90-101``, ``ddpm.py:23-34``) and its PSLD driver runs SD 1.5 in bf16
+(``scripts/run_psld.py:14-20``).  With a bf16 network the layers of ``unet2d.py``,
+``unet2d_condition.py`` and ``vae.py`` dispatch here on the device:
+
+* activations are channels-last bf16 (``torch.channels_last``: the memory is [n][h][w][c]);
+  the transformer blocks' token rows ([b][h w][c]) are then views, no transposes;
+* 3x3 convolutions (stride 1; the stride-2 downsamplers at full resolution read at every other
+  position) and their input VJPs on ``sp_conv3x3_bf16`` (implicit GEMM on the bf16 MFMAs, fp32
+  accumulation, bias and residual in the epilogue);
+* GroupNorm(+time-embedding bias)(+SiLU) and its input VJP on ``sp_groupnorm_bf16_fwd/bwd``
+  (fp32 statistics);
+* the SD UNet's self- and cross-attention forward on ``sp_attention_bf16_fwd`` (flash-style,
+  scores never in HBM); its VJP runs the exact-fp32 fused kernels on the inputs widened to fp32;
+* 1x1 convolutions and linears are bf16 GEMMs (hipBLASLt through ``F.linear``); LayerNorm,
+  GEGLU and the d = 512 single-head attention (score matrix kept) are torch bf16 ops.
+
+Semantics follow PyTorch's bf16 modules (fp32 accumulation / statistics, one rounding to bf16
+per layer output), which is what the reference computes in bf16.  Every entry here raises
+``HipLibraryError`` when the library is missing: there is no silent CPU fallback.
+"""
+
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.nn.functional as F
+from torch import Tensor, nn
+
+from .. import _hip
+
+BF16 = torch.bfloat16
+CL = torch.channels_last
+
+
+def is_bf16_device(x: Tensor) -> bool:
+    return x.is_cuda and x.dtype == BF16
+
+
+def nhwc(t: Tensor) -> Tensor:
+    """``t`` (n, c, h, w) with [n][h][w][c] memory."""
+    return t if t.is_contiguous(memory_format=CL) else t.contiguous(memory_format=CL)
+
+
+def _p(t: Tensor | None, *, cl: bool = True) -> int | None:
+    """Device pointer of a bf16 tensor laid out as the kernels read it (channels-last for 4-d)."""
+    if t is None:
+        return None
+    if not t.is_cuda or t.dtype != BF16:
+        raise _hip.HipLibraryError(f"bf16 path needs bf16 device tensors, got {t.dtype} on {t.device}")
+    ok = t.is_contiguous(memory_format=CL) if (cl and t.dim() == 4) else t.is_contiguous()
+    if not ok:
+        raise _hip.HipLibraryError("bf16 path needs channels-last / contiguous tensors")
+    return t.data_ptr()
+
+
+def _f32(t: Tensor | None) -> Tensor | None:
+    return None if t is None else t.detach().to(torch.float32).contiguous()
+
+
+def _cached(module: nn.Module, name: str, key, build):
+    cache = module.__dict__.setdefault("_bf16_cache", {})
+    hit = cache.get(name)
+    if hit is None or hit[0] != key:
+        with torch.no_grad():
+            hit = (key, build())
+        cache[name] = hit
+    return hit[1]
+
+
+def _wkey(*ts: Tensor | None):
+    return tuple((None if t is None else (t.data_ptr(), t._version, t.device, t.dtype)) for t in ts)
+
+
+# ---------------------------------------------------------------------------------------------
+# 3x3 convolution
+# ---------------------------------------------------------------------------------------------
+
+def _ceil(a: int, b: int) -> int:
+    return -(-a // b) * b
+
+
+def conv_pack(module: nn.Module, vjp: bool) -> Tensor:
+    """``module``'s 3x3 weights as sp_conv3x3_bf16 reads them: [co block of 64][ci block of 16]
+    [tap][64 co][16 ci] bf16, zero-padded; ``vjp``: the pack of W'[ci][co][2-ky][2-kx]."""
+    w = module.weight
+
+    def build():
+        wt = w.detach()
+        if vjp:
+            wt = wt.transpose(0, 1).flip(2, 3)
+        co, ci = wt.shape[:2]
+        cop, cip = _ceil(co, 64), _ceil(ci, 16)
+        wp = torch.zeros(cop, cip, 3, 3, device=w.device, dtype=torch.float32)
+        wp[:co, :ci] = wt.float()
+        wp = wp.reshape(cop // 64, 64, cip // 16, 16, 9).permute(0, 2, 4, 1, 3).contiguous()
+        return wp.to(BF16)
+
+    return _cached(module, f"pack{int(vjp)}", _wkey(w), build)
+
+
+def _bias_f32(module: nn.Module, bias: Tensor | None) -> Tensor | None:
+    if bias is None:
+        return None
+    return _cached(module, f"bias{id(bias)}", _wkey(bias), lambda: bias.detach().float().contiguous())
+
+
+def _pad_channels(x: Tensor, c: int) -> Tensor:
+    """x (n, c0, h, w) zero-padded to c channels (differentiable; channels-last result)."""
+    if x.shape[1] == c:
+        return nhwc(x)
+    n, c0, h, w = x.shape
+    out = torch.empty(n, c, h, w, device=x.device, dtype=x.dtype, memory_format=CL).zero_()
+    out[:, :c0] = x  # autograd: the gradient of x is the first c0 channels
+    return out
+
+
+def _conv_launch(x: Tensor, pack: Tensor, bias: Tensor | None, res: Tensor | None, cout: int) -> Tensor:
+    lib = _hip.load_library()
+    n, cin, h, w = x.shape
+    y = torch.empty(n, cout, h, w, device=x.device, dtype=BF16, memory_format=CL)
+    _hip.check(lib.sp_conv3x3_bf16(_p(x), _p(pack, cl=False), None if bias is None else bias.data_ptr(), _p(res), n,
+                                   cin, cout, h, w, _p(y), _hip.stream_of(x)), "sp_conv3x3_bf16")
+    return y
+
+
+class _ConvBf16Fn(torch.autograd.Function):
+    """conv3x3(x) + bias (+ res) on sp_conv3x3_bf16; the input VJP on the same kernel with the
+    flipped / transposed pack (weights frozen); the residual's gradient is dy itself."""
+
+    @staticmethod
+    def forward(ctx, x, res, module, bias):
+        ctx.module, ctx.cin, ctx.has_res = module, x.shape[1], res is not None
+        return _conv_launch(x, conv_pack(module, False), bias, res, module.weight.shape[0])
+
+    @staticmethod
+    def backward(ctx, dy):
+        module = ctx.module
+        cout = module.weight.shape[0]
+        dx = None
+        if ctx.needs_input_grad[0]:
+            d = _pad_channels(dy.to(BF16), _ceil(cout, 16))
+            dx = _conv_launch(d, conv_pack(module, True), None, None, ctx.cin)
+        dres = dy if (ctx.has_res and ctx.needs_input_grad[1]) else None
+        return dx, dres, None, None
+
+
+def conv_supported(module: nn.Module, x: Tensor) -> bool:
+    if not (is_bf16_device(x) and x.dim() == 4) or module.weight.requires_grad:
+        return False
+    if tuple(module.weight.shape[2:]) != (3, 3):
+        return False
+    n, cin, h, w = x.shape
+    return bool(_hip.load_library().sp_conv3x3_bf16_supported(_ceil(cin, 16), module.weight.shape[0], h, w))
+
+
+def conv3x3(module: nn.Module, x: Tensor, res: Tensor | None = None, bias: Tensor | None = None) -> Tensor:
+    """``module(x)`` (3x3, stride 1, padding 1) + ``res`` on the bf16 tile; ``bias`` overrides the
+    module's.  Inputs with fewer than 16-multiple channels (conv_in: 3 / 4) are zero-padded."""
+    cin = x.shape[1]
+    xp = _pad_channels(x, _ceil(cin, 16))
+    b = module.bias if bias is None else bias
+    r = None if res is None else nhwc(res.to(BF16))
+    return _ConvBf16Fn.apply(xp, r, module, _bias_f32(module, b))
+
+
+class _StridedBf16Fn(torch.autograd.Function):
+    """A 3x3 / stride-2 convolution as the stride-1 one at full resolution read at every other
+    position (``phase`` 0: padding 1; 1: diffusers' padding (0, 1, 0, 1)); VJP: dy scattered to
+    those positions, then the stride-1 input VJP."""
+
+    @staticmethod
+    def forward(ctx, x, module, bias, phase):
+        ctx.module, ctx.phase, ctx.xs = module, phase, x.shape
+        y = _conv_launch(x, conv_pack(module, False), bias, None, module.weight.shape[0])
+        return nhwc(y[:, :, phase::2, phase::2])
+
+    @staticmethod
+    def backward(ctx, dy):
+        module = ctx.module
+        n, cin, h, w = ctx.xs
+        cout = module.weight.shape[0]
+        full = torch.empty(n, _ceil(cout, 16), h, w, device=dy.device, dtype=BF16, memory_format=CL).zero_()
+        full[:, :cout, ctx.phase::2, ctx.phase::2] = dy
+        return _conv_launch(full, conv_pack(module, True), None, None, cin), None, None, None
+
+
+def conv3x3_stride2(module: nn.Module, x: Tensor, padding: int) -> Tensor:
+    xp = _pad_channels(x, _ceil(x.shape[1], 16))
+    return _StridedBf16Fn.apply(xp, module, _bias_f32(module, module.bias), 0 if padding else 1)
+
+
+def strided_supported(module: nn.Module, x: Tensor) -> bool:
+    return conv_supported(module, x) and x.shape[2] % 2 == 0 and x.shape[3] % 2 == 0
+
+
+def pointwise(x: Tensor, weight: Tensor, bias: Tensor | None) -> Tensor:
+    """A 1x1 convolution of channels-last x as one bf16 GEMM over its pixel rows (hipBLASLt)."""
+    n, c, h, w = x.shape
+    co = weight.shape[0]
+    rows = nhwc(x).permute(0, 2, 3, 1).reshape(n * h * w, c)
+    y = F.linear(rows, weight.reshape(co, c), bias)
+    return y.reshape(n, h, w, co).permute(0, 3, 1, 2)
+
+
+# ---------------------------------------------------------------------------------------------
+# GroupNorm (+ per-(n, c) bias) (+ SiLU)
+# ---------------------------------------------------------------------------------------------
+
+def _gn_params(norm: nn.GroupNorm) -> tuple[Tensor | None, Tensor | None]:
+    return (_cached(norm, "gamma", _wkey(norm.weight), lambda: _f32(norm.weight)) if norm.weight is not None else None,
+            _cached(norm, "beta", _wkey(norm.bias), lambda: _f32(norm.bias)) if norm.bias is not None else None)
+
+
+def _gn_ws(lib, n: int, c: int, hw: int, device) -> tuple[Tensor, int]:
+    nb = int(lib.sp_groupnorm_bf16_workspace(n, c, hw))
+    return torch.empty(nb, device=device, dtype=torch.uint8), nb
+
+
+class _GroupNormBf16Fn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x1, x2, norm, cb):
+        lib = _hip.load_library()
+        n, c1, h, w = x1.shape
+        c2 = 0 if x2 is None else x2.shape[1]
+        c, hw, g = c1 + c2, h * w, norm.num_groups
+        gamma, beta = _gn_params(norm)
+        z = torch.empty(n, c, h, w, device=x1.device, dtype=BF16, memory_format=CL)
+        stats = torch.empty(2, n * g, device=x1.device, dtype=torch.float32)
+        ws, nb = _gn_ws(lib, n, c, hw, x1.device)
+        _hip.check(lib.sp_groupnorm_bf16_fwd(_p(x1), _p(x2), c1, c2, None if cb is None else cb.data_ptr(),
+                                             None if gamma is None else gamma.data_ptr(),
+                                             None if beta is None else beta.data_ptr(), n, hw, g, float(norm.eps),
+                                             int(norm.act), _p(z), stats.data_ptr(), ws.data_ptr(), nb,
+                                             _hip.stream_of(x1)), "sp_groupnorm_bf16_fwd")
+        ctx.save_for_backward(x1, x2, cb, stats)
+        ctx.norm = norm
+        return z
+
+    @staticmethod
+    def backward(ctx, dz):
+        x1, x2, cb, stats = ctx.saved_tensors
+        norm = ctx.norm
+        lib = _hip.load_library()
+        n, c1, h, w = x1.shape
+        c2 = 0 if x2 is None else x2.shape[1]
+        gamma, beta = _gn_params(norm)
+        dz = nhwc(dz.to(BF16))
+        dx1 = torch.empty_like(x1, memory_format=CL)
+        dx2 = None if x2 is None else torch.empty_like(x2, memory_format=CL)
+        ws, nb = _gn_ws(lib, n, c1 + c2, h * w, x1.device)
+        _hip.check(lib.sp_groupnorm_bf16_bwd(_p(dz), _p(x1), _p(x2), c1, c2, None if cb is None else cb.data_ptr(),
+                                             None if gamma is None else gamma.data_ptr(),
+                                             None if beta is None else beta.data_ptr(), stats.data_ptr(), n, h * w,
+                                             norm.num_groups, int(norm.act), _p(dx1), _p(dx2), None, None, None,
+                                             ws.data_ptr(), nb, _hip.stream_of(dz)), "sp_groupnorm_bf16_bwd")
+        return dx1, dx2, None, None
+
+
+def group_norm_supported(norm: nn.GroupNorm, x: Tensor, c2: int = 0) -> bool:
+    if not (is_bf16_device(x) and x.dim() == 4) or any(p.requires_grad for p in norm.parameters()):
+        return False
+    return bool(_hip.load_library().sp_groupnorm_bf16_supported(x.shape[1], c2, norm.num_groups))
+
+
+def group_norm(norm: nn.GroupNorm, x1: Tensor, x2: Tensor | None = None, chan_bias: Tensor | None = None) -> Tensor:
+    """``act(GroupNorm(cat(x1, x2) + chan_bias[:, :, None, None]))`` (``norm.act``: SiLU), the two
+    parts read in place."""
+    cb = None if chan_bias is None else chan_bias.detach().to(torch.float32).reshape(x1.shape[0], -1).contiguous()
+    return _GroupNormBf16Fn.apply(nhwc(x1), None if x2 is None else nhwc(x2), norm, cb)
+
+
+# ---------------------------------------------------------------------------------------------
+# multi-head attention (SD 1.5 UNet: head dims 40 / 80 / 160, 4096 .. 64 tokens, 77 context rows)
+# ---------------------------------------------------------------------------------------------
+
+def attention_supported(b: int, heads: int, n: int, m: int, d: int) -> bool:
+    return bool(_hip.load_library().sp_attention_bf16_supported(b, heads, n, m, d))
+
+
+def _attn_fwd(q: Tensor, k: Tensor, v: Tensor, b: int, heads: int, n: int, m: int, d: int, rsq: int, rskv: int,
+              kv_shared: bool, offs=(0, 0, 0)) -> tuple[Tensor, Tensor]:
+    lib = _hip.load_library()
+    c = heads * d
+    out = torch.empty(b, n, c, device=q.device, dtype=BF16)
+    lse = torch.empty(b * heads, n, device=q.device, dtype=torch.float32)
+    _hip.check(lib.sp_attention_bf16_fwd(_p(q, cl=False) + offs[0], _p(k, cl=False) + offs[1],
+                                         _p(v, cl=False) + offs[2], b, heads, n, m, d, rsq, rskv, int(kv_shared), c,
+                                         1.0 / math.sqrt(d), _p(out, cl=False), lse.data_ptr(), _hip.stream_of(q)),
+               "sp_attention_bf16_fwd")
+    return out, lse
+
+
+class _SelfAttnBf16Fn(torch.autograd.Function):
+    """Self-attention on the fused projection's bf16 output qkv ([b][n][3 heads d], q, k, v its
+    thirds read in place).  VJP: the exact-fp32 fused kernels (sp_attention_bwd_mh) on q, k, v,
+    the output and its cotangent widened to fp32, the cotangent of qkv rounded back to bf16."""
+
+    @staticmethod
+    def forward(ctx, qkv, heads):
+        b, n, c3 = qkv.shape
+        c = c3 // 3
+        d = c // heads
+        qkv = qkv.contiguous()
+        out, lse = _attn_fwd(qkv, qkv, qkv, b, heads, n, n, d, c3, c3, False, offs=(0, 2 * c, 4 * c))
+        ctx.save_for_backward(qkv, out, lse)
+        ctx.heads = heads
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        qkv, out, lse = ctx.saved_tensors
+        lib = _hip.load_library()
+        b, n, c3 = qkv.shape
+        c = c3 // 3
+        heads = ctx.heads
+        d = c // heads
+        q32, o32, do32 = qkv.float(), out.float(), dout.float().contiguous()
+        dqkv = torch.empty_like(q32)
+        delta = torch.empty(b * heads, n, device=qkv.device, dtype=torch.float32)
+        base, dbase = q32.data_ptr(), dqkv.data_ptr()
+        _hip.check(lib.sp_attention_bwd_mh(base, base + 4 * c, base + 8 * c, _hip.ptr(o32), _hip.ptr(do32),
+                                           _hip.ptr(lse), b, heads, n, n, d, c3, c3, b, c, 1.0 / math.sqrt(d),
+                                           _hip.ptr(delta), dbase, dbase + 4 * c, dbase + 8 * c,
+                                           _hip.stream_of(do32)), "sp_attention_bwd_mh")
+        return dqkv.to(BF16), None
+
+
+class _CrossAttnBf16Fn(torch.autograd.Function):
+    """Cross-attention of bf16 token rows q ([b][n][heads d]) to a context's k, v ([bc][m][heads
+    d], bc = 1 or b); VJP dq only (the context is a constant of the prior's call), on the fp32
+    kernels as above."""
+
+    @staticmethod
+    def forward(ctx, q, k, v, heads):
+        b, n, c = q.shape
+        bc, m, _ = k.shape
+        d = c // heads
+        q, k, v = q.contiguous(), k.contiguous(), v.contiguous()
+        out, lse = _attn_fwd(q, k, v, b, heads, n, m, d, c, c, bc == 1)
+        ctx.save_for_backward(q, k, v, out, lse)
+        ctx.heads = heads
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        q, k, v, out, lse = ctx.saved_tensors
+        lib = _hip.load_library()
+        b, n, c = q.shape
+        bc, m, _ = k.shape
+        heads = ctx.heads
+        q32, k32, v32, o32 = q.float(), k.float(), v.float(), out.float()
+        do32 = dout.float().contiguous()
+        dq = torch.empty_like(q32)
+        delta = torch.empty(b * heads, n, device=q.device, dtype=torch.float32)
+        _hip.check(lib.sp_attention_bwd_mh(_hip.ptr(q32), _hip.ptr(k32), _hip.ptr(v32), _hip.ptr(o32),
+                                           _hip.ptr(do32), _hip.ptr(lse), b, heads, n, m, c // heads, c, c, bc, c,
+                                           1.0 / math.sqrt(c // heads), _hip.ptr(delta), _hip.ptr(dq), None, None,
+                                           _hip.stream_of(do32)), "sp_attention_bwd_mh")
+        return dq.to(BF16), None, None, None
+
+
+def self_attention(qkv: Tensor, heads: int) -> Tensor:
+    return _SelfAttnBf16Fn.apply(qkv, heads)
+
+
+def cross_attention(q: Tensor, k: Tensor, v: Tensor, heads: int) -> Tensor:
+    return _CrossAttnBf16Fn.apply(q, k, v, heads)
+
+
+def fp32_vjp_supported(b: int, heads: int, n: int, m: int, d: int) -> bool:
+    """The fp32 fused VJP kernels serve this shape (they carry the bf16 forward's VJP)."""
+    return bool(_hip.load_library().sp_attention_mh_supported(b, heads, n, m, d))

@@ -144,6 +144,12 @@ class DDPMNetwork(EpsilonNetwork[NoCondition]):
     def is_condition_initialized(self) -> bool:
         return True
 
+    @property
+    def dtype(self) -> torch.dtype:
+        """The prior's parameter dtype, as the reference's ``_pipeline.dtype`` (``ddpm.py:86-89``):
+        ``from_config`` / ``from_pretrained(torch_dtype=torch.bfloat16)`` gives a bf16 network."""
+        return next(self.unet.parameters()).dtype
+
     def to(self, *args, **kwargs):
         super().to(*args, **kwargs)
         self._acp_host = None

@@ -245,6 +245,12 @@ class LatentDiffusionNetwork(LatentEpsilonNetwork[StableDiffusionCondition]):
     def is_condition_initialized(self) -> bool:
         return self._conditioning is not None
 
+    @property
+    def dtype(self) -> torch.dtype:
+        """The priors' parameter dtype, as the reference's ``_pipeline.dtype``
+        (``stable_diffusion.py:353-356``): ``torch_dtype=torch.bfloat16`` gives a bf16 network."""
+        return next(self.unet.parameters()).dtype
+
     def clear_condition(self):
         self._conditioning = None
 

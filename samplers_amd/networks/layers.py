@@ -221,7 +221,15 @@ class GroupNormAct(nn.GroupNorm):
             return group_norm_act_torch(x, self.num_groups, self.weight, self.bias, self.eps,
                                         self.act, chan_bias)
         if x.dtype != torch.float32:
-            raise _hip.HipLibraryError(f"GroupNormAct computes in fp32, got {x.dtype}")
+            # reduced-precision priors (the reference's bf16 / fp16 runs): bf16 on the NHWC
+            # kernels (networks/bf16.py), fp16 on torch's GroupNorm
+            if box is not None:
+                box.enabled = False
+            from . import bf16
+            if bf16.group_norm_supported(self, x):
+                return bf16.group_norm(self, x, None, chan_bias)
+            return group_norm_act_torch(x, self.num_groups, self.weight, self.bias, self.eps, self.act,
+                                        chan_bias)
         return _GroupNormActFn.apply(x, self.weight, self.bias, chan_bias, self.num_groups,
                                      self.eps, self.act, box)
 
@@ -411,6 +419,10 @@ class Conv3x3(nn.Conv2d):
         return tile_pack(self, algo, input_vjp)
 
     def forward(self, x: Tensor) -> Tensor:
+        if x.is_cuda and x.dtype == torch.bfloat16:
+            from . import bf16
+            if bf16.conv_supported(self, x):
+                return bf16.conv3x3(self, x)
         if x.is_cuda and x.dtype == torch.float32 and x.dim() == 4:
             lib = _hip.load_library()
             n, cin, h, w = x.shape
@@ -665,6 +677,10 @@ def conv3x3_stride2(module: nn.Conv2d, x: Tensor, padding: int) -> Tensor:
     """``module(x)`` for a 3x3 / stride-2 ``nn.Conv2d`` with ``padding=1`` (``padding=1``), or
     ``module(F.pad(x, (0, 1, 0, 1)))`` with ``padding=0``, through the stride-1 tiles at full
     resolution where they serve the shape, else torch / MIOpen."""
+    if x.is_cuda and x.dtype == torch.bfloat16:
+        from . import bf16
+        if bf16.strided_supported(module, x):
+            return bf16.conv3x3_stride2(module, x, padding)
     if strided_full_supported(module, x):
         return _ConvS2FullFn.apply(x, module.weight, module.bias, module, 0 if padding else 1)
     miopen_fallback(x)
@@ -676,6 +692,10 @@ def downsample_conv(module: nn.Conv2d, x: Tensor, box: SkipGrad | None = None) -
     (diffusers' Downsample2D with downsample_padding=0): the stride-2 MFMA tile
     (``csrc/sp_conv_s2.hip``) where its shape rules hold, else the stride-1 tiles at full
     resolution (``conv3x3_stride2``), else MIOpen on the padded input."""
+    if x.is_cuda and x.dtype == torch.bfloat16:
+        if box is not None:
+            box.enabled = False
+        return conv3x3_stride2(module, x, padding=0)
     if downsample_s2_supported(module, x) and not module.weight.requires_grad:
         return _ConvS2Fn.apply(x, module.weight, module.bias, module,
                                box if box is not None and box.enabled else None)
@@ -907,6 +927,9 @@ def conv1x1_small(conv: nn.Conv2d, x: Tensor) -> Tensor:
     """``conv(x)`` for the VAE's 4- / 8-channel 1x1 quant convs on a HIP kernel (CUDA fp32,
     frozen weights), else torch."""
     co, c = conv.weight.shape[:2]
+    if x.is_cuda and x.dtype == torch.bfloat16 and not conv.weight.requires_grad:
+        from . import bf16
+        return bf16.pointwise(x, conv.weight, conv.bias)
     if (x.is_cuda and x.dtype == torch.float32 and not conv.weight.requires_grad
             and (conv.bias is None or not conv.bias.requires_grad)
             and _hip.load_library().sp_conv1x1_small_supported(c, co, x.shape[2] * x.shape[3])):

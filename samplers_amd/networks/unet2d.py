@@ -346,6 +346,36 @@ class ResnetBlock2D(nn.Module):
         self.conv2 = Conv3x3(cout, cout)
         self.conv_shortcut = nn.Conv2d(cin, cout, 1) if cin != cout else None
 
+    def _frozen(self) -> bool:
+        params = self.__dict__.get("_param_list")
+        if params is None:
+            params = self.__dict__["_param_list"] = list(self.parameters())
+        return not any(p.requires_grad for p in params)
+
+    def _forward_bf16(self, x: Tensor, skip: Tensor | None, tb: Tensor | None, box_in: SkipGrad | None,
+                      box_out: SkipGrad | None) -> Tensor:
+        """The block at bf16 on the NHWC kernels (networks/bf16.py): GN1 over cat(x, skip) read in
+        place, conv1, GN2 with the time-embedding bias, conv2 with the shortcut added in its
+        epilogue; autograd sums the skip gradients (the SkipGrad hand-offs are fp32-only)."""
+        from . import bf16
+
+        for box in (box_in, box_out):
+            if box is not None:
+                box.enabled = False
+        c2 = 0 if skip is None else skip.shape[1]
+        if bf16.group_norm_supported(self.norm1, x, c2):
+            z1 = bf16.group_norm(self.norm1, x, skip)
+        else:
+            z1 = self.norm1(x if skip is None else torch.cat([x, skip], dim=1))
+        h = self.conv1(z1)
+        z2 = self.norm2(h, tb)
+        xin = x if skip is None else torch.cat([bf16.nhwc(x), bf16.nhwc(skip)], dim=1)
+        short = xin if self.conv_shortcut is None else bf16.pointwise(xin, self.conv_shortcut.weight,
+                                                                         self.conv_shortcut.bias)
+        if bf16.conv_supported(self.conv2, z2):
+            return bf16.conv3x3(self.conv2, z2, res=short)
+        return self.conv2(z2) + short
+
     def _fusable(self, x: Tensor) -> bool:
         params = self.__dict__.get("_param_list")
         if params is None:  # fixed after construction; walking the submodules per call is host time
@@ -364,6 +394,8 @@ class ResnetBlock2D(nn.Module):
             raise ValueError("box_in (x is a skip tensor) and skip (an up-block input) are exclusive")
         if tb is None and self.time_emb_proj is not None:
             tb = self.time_emb_proj(F.silu(temb))
+        if x.is_cuda and x.dtype == torch.bfloat16 and self._frozen():
+            return self._forward_bf16(x, skip, tb, box_in, box_out)
         if (self._fusable(x) and (skip is None or skip.dtype == x.dtype)
                 and (box_in is None or box_in.enabled)):
             x1 = x.contiguous()
@@ -574,7 +606,7 @@ class SpatialSelfAttention(nn.Module):
 
     def forward(self, x: Tensor) -> Tensor:
         b, c, h, w = x.shape
-        fast = (self.heads == 1 and x.is_cuda and not self.to_q.weight.requires_grad
+        fast = (self.heads == 1 and x.is_cuda and x.dtype == torch.float32 and not self.to_q.weight.requires_grad
                 and attention_backend() == "gemm"
                 and bool(_hip.load_library().sp_softmax_rows_supported(b * h * w, h * w)))
         box = SkipGrad() if fast and torch.is_grad_enabled() else None  # x's residual gradient
@@ -727,7 +759,13 @@ class UNet2DModel(nn.Module):
             if lvl.upsamplers is not None:
                 h = lvl.upsamplers[0](h)
 
-        return self.conv_out(self.conv_norm_out(h))
+        return _as_nchw(self.conv_out(self.conv_norm_out(h)))
+
+
+def _as_nchw(y: Tensor) -> Tensor:
+    """The network's output in the NCHW layout the samplers read (the bf16 layers return
+    channels-last tensors; fp32 outputs are already NCHW)."""
+    return y if y.is_contiguous() else y.contiguous()
 
 
 def build_unet(config: UNet2DConfig = CELEBAHQ_256, *, seed: int = 0, device=None,

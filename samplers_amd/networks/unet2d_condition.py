@@ -36,8 +36,8 @@ from .attention import (attention, fused_cross_attention, fused_cross_supported,
                         fused_qkv_supported)
 from .layers import (Conv3x3, GroupNormAct, LayerNorm, Linear, SkipGrad, conv3x3_stride2, geglu,
                      linear, proj_nchw_to_tokens, proj_tokens_to_nchw)
-from .unet2d import (ResnetBlock2D, TimestepEmbedding, Upsample2D, temb_projections, timestep_embedding,
-                     timestep_rows)
+from .unet2d import (ResnetBlock2D, TimestepEmbedding, Upsample2D, _as_nchw, temb_projections,
+                     timestep_embedding, timestep_rows)
 
 
 @dataclass(frozen=True)
@@ -99,11 +99,34 @@ class Attention(nn.Module):
         h = self.heads
         return t.reshape(b, n, h, c // h).transpose(1, 2).reshape(b * h, n, c // h)
 
+    def _forward_bf16(self, x: Tensor, context: Tensor | None) -> Tensor | None:
+        """bf16 attention on the fused kernels (networks/bf16.py), or None where they do not
+        serve the shape."""
+        from . import bf16
+
+        b, n, c = x.shape
+        d = c // self.heads
+        if context is None:
+            if not (bf16.attention_supported(b, self.heads, n, n, d) and bf16.fp32_vjp_supported(b, self.heads, n, n, d)):
+                return None
+            qkv = torch.nn.functional.linear(x, self._qkv_weight().weight)
+            return bf16.self_attention(qkv, self.heads)
+        bc, m = context.shape[0], context.shape[1]
+        if bc not in (1, b) or context.requires_grad or not (
+                bf16.attention_supported(b, self.heads, n, m, d) and bf16.fp32_vjp_supported(b, self.heads, n, m, d)):
+            return None
+        q, k, v = self.to_q(x), self.to_k(context), self.to_v(context)
+        return bf16.cross_attention(q, k, v, self.heads)
+
     def forward(self, x: Tensor, context: Tensor | None = None, res: Tensor | None = None,
                 box: SkipGrad | None = None) -> Tensor:
         """``res`` is added in ``to_out``'s epilogue (the block's residual); ``box`` carries
         its gradient to the LayerNorm VJP that adds it (``layers.linear``)."""
         b, n, c = x.shape
+        if x.is_cuda and x.dtype == torch.bfloat16 and not self.to_q.weight.requires_grad:
+            o = self._forward_bf16(x, context)
+            if o is not None:
+                return self.to_out[0](o, res, box)
         if context is None and not self.to_q.weight.requires_grad and fused_qkv_supported(x, self.heads):
             # one projection for q, k, v; attention reads its thirds in place
             h = self._qkv_weight()
@@ -320,7 +343,7 @@ class UNet2DConditionModel(nn.Module):
             if lvl.upsamplers is not None:
                 h = lvl.upsamplers[0](h)
 
-        return self.conv_out(self.conv_norm_out(h))
+        return _as_nchw(self.conv_out(self.conv_norm_out(h)))
 
 
 def null_context(config: UNet2DConditionConfig = SD15_UNET, *, seed: int = 7,

@@ -22,7 +22,7 @@ import torch.nn.functional as F
 from torch import Tensor, nn
 
 from .layers import Conv3x3, GroupNormAct, conv1x1_small
-from .unet2d import Downsample2D, ResnetBlock2D, SpatialSelfAttention, Upsample2D
+from .unet2d import Downsample2D, ResnetBlock2D, SpatialSelfAttention, Upsample2D, _as_nchw
 
 
 @dataclass(frozen=True)
@@ -131,10 +131,10 @@ class AutoencoderKL(nn.Module):
 
     def encode_mean(self, x: Tensor) -> Tensor:
         moments = conv1x1_small(self.quant_conv, self.encoder(x))
-        return moments[:, : self.config.latent_channels]
+        return _as_nchw(moments[:, : self.config.latent_channels])
 
     def decode(self, z: Tensor) -> Tensor:
-        return self.decoder(conv1x1_small(self.post_quant_conv, z))
+        return _as_nchw(self.decoder(conv1x1_small(self.post_quant_conv, z)))
 
 
 def build_vae(config: VAEConfig = SD15_VAE, *, seed: int = 0, device=None,

@@ -63,7 +63,7 @@ class KernelTimer:
     """
 
     _KIND = {1: "dps_residual", 2: "dps_update", 3: "conv3x3_fwd", 4: "conv3x3_bwd_input",
-             5: "wino3x3_fwd", 6: "wino3x3_bwd_input"}
+             5: "wino3x3_fwd", 6: "wino3x3_bwd_input", 7: "conv3x3_bf16"}
     _CAP = 1 << 16
 
     def __init__(self) -> None:

@@ -1,0 +1,330 @@
+"""The priors at the reference's reduced precision (bf16) on this project's kernels
+(``csrc/sp_bf16.hip`` through ``networks/bf16.py``).
+
+The reference runs its priors in whatever ``torch_dtype`` it is given; its PSLD driver uses SD 1.5
+in bf16 (``/root/reference/scripts/run_psld.py:14-20``, ``stable_diffusion.py:90-101``).  What is
+pinned here, and at what tolerance (relative L2 unless said otherwise):
+
+* each kernel against fp32 arithmetic on the same bf16-rounded operands: the kernels compute in
+  fp32 and round once per output, so the bound is the bf16 rounding of the output (unit
+  roundoff 2^-9; RMS of the relative rounding ~1.1e-3): conv / GroupNorm forward 3e-3, input VJPs
+  5e-3, attention (P rounded to bf16 for the P V product as well) 1e-2;
+* whole priors (SD 1.5 ε-UNet, VAE decode / encode, the ddpm-celebahq-256 UNet): bf16 on the GPU
+  against the same bf16 modules on the CPU (torch's own bf16 layers: oneDNN convolutions, ATen
+  GroupNorm / softmax), and both against the fp32 module: the GPU's bf16 error relative to fp32
+  may be at most 1.5x the CPU bf16 error (+1e-3) — the device path is as close to the fp32
+  network as torch's own bf16 run is (measured: 0.8x); the direct GPU-bf16 / CPU-bf16 distance is
+  about the two independent bf16 errors combined (1e-2 .. 4.5e-2 over ~60 layers and their VJPs),
+  bounded at 1e-1;
+* a PSLD solve through the bf16 SD 1.5 priors against ``oracle/latent_loops.py`` driving the same
+  bf16 modules on the CPU behind the same fp32 boundary (the sample, guidance and DDIM updates
+  in fp32, the networks in bf16): bound ``PSLD_BF16_TOL``; the device kernels are asserted by name
+  (no MIOpen convolution runs).
+"""
+
+from __future__ import annotations
+
+import copy
+import math
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+import stand_ins as si
+
+pytestmark = pytest.mark.gpu
+
+BF = torch.bfloat16
+PSLD_BF16_TOL = 3e-2
+
+
+def _rel(a, b) -> float:
+    return si.relative_error(a.float().cpu(), b.float().cpu())
+
+
+def _kernel_names(fn) -> set[str]:
+    from torch.profiler import ProfilerActivity, profile
+
+    with profile(activities=[ProfilerActivity.CUDA]) as prof:
+        fn()
+        torch.cuda.synchronize()
+    return {e.name for e in prof.events() if e.device_type.name == "CUDA"}
+
+
+def _no_miopen_conv(names: set[str]) -> None:
+    bad = {n for n in names if ("conv" in n.lower() or "miopen" in n.lower() or "igemm" in n.lower())
+           and "k_conv3x3_bf16" not in n}
+    assert not bad, f"convolutions outside sp::k_conv3x3_bf16: {sorted(bad)[:5]}"
+
+
+# ---- kernels ------------------------------------------------------------------------------------
+
+CONV_SHAPES = [
+    (2, 16, 64, 32, 32), (1, 320, 320, 64, 64), (3, 64, 128, 16, 16), (5, 32, 64, 8, 8),
+    (2, 64, 64, 4, 4), (1, 4, 320, 32, 32), (2, 128, 3, 64, 64), (2, 320, 4, 32, 32), (1, 640, 1280, 8, 8),
+]
+
+
+@pytest.mark.parametrize("shape", CONV_SHAPES, ids=lambda s: "x".join(map(str, s)))
+def test_conv3x3_bf16_fwd_vjp_matches_fp32(cuda, shape, parity_record):
+    from samplers_amd.networks.layers import Conv3x3
+
+    n, cin, cout, h, w = shape
+    torch.manual_seed(1)
+    conv = Conv3x3(cin, cout).to(BF).requires_grad_(False)
+    x = torch.randn(n, cin, h, w).to(BF)
+    dy = torch.randn(n, cout, h, w).to(BF)
+    g = copy.deepcopy(conv).to(cuda)
+    xr = x.to(cuda).requires_grad_(True)
+    with torch.enable_grad():
+        y = g(xr)
+    (dx,) = torch.autograd.grad(y, xr, dy.to(cuda))
+    assert y.dtype == BF and y.is_contiguous(memory_format=torch.channels_last)
+    wf, bfv = conv.weight.float(), conv.bias.float()
+    ref = F.conv2d(x.float(), wf, bfv, padding=1)
+    ref_dx = torch.nn.grad.conv2d_input(x.shape, wf, dy.float(), padding=1)
+    e, ed = _rel(y, ref), _rel(dx, ref_dx)
+    parity_record("conv_bf16_rel_l2", e, 3e-3, shape=list(shape))
+    parity_record("conv_bf16_vjp_rel_l2", ed, 5e-3, shape=list(shape))
+    assert e < 3e-3 and ed < 5e-3, (e, ed)
+
+
+def test_conv3x3_bf16_residual_and_repeatable(cuda):
+    from samplers_amd.networks import bf16
+    from samplers_amd.networks.layers import Conv3x3
+
+    torch.manual_seed(2)
+    conv = Conv3x3(64, 128).to(device=cuda, dtype=BF).requires_grad_(False)
+    x = torch.randn(2, 64, 32, 32, device=cuda).to(BF)
+    res = torch.randn(2, 128, 32, 32, device=cuda).to(BF)
+    y1 = bf16.conv3x3(conv, x, res=res)
+    y2 = bf16.conv3x3(conv, x, res=res)
+    assert torch.equal(y1, y2)  # fixed summation order
+    ref = F.conv2d(x.float(), conv.weight.float(), conv.bias.float(), padding=1) + res.float()
+    assert _rel(y1, ref) < 3e-3
+
+
+@pytest.mark.parametrize("c1,c2,hw,act,bias", [(320, 0, 64, True, True), (640, 640, 16, True, False),
+                                               (128, 0, 128, False, False), (1280, 1280, 8, True, True),
+                                               (512, 0, 32, True, False)])
+def test_groupnorm_bf16_fwd_vjp_matches_fp32(cuda, c1, c2, hw, act, bias, parity_record):
+    from samplers_amd.networks import bf16
+    from samplers_amd.networks.layers import GroupNormAct
+
+    torch.manual_seed(3)
+    n, c = 3, c1 + c2
+    norm = GroupNormAct(32, c, eps=1e-5, act=act)
+    with torch.no_grad():
+        norm.weight.copy_(1 + 0.2 * torch.randn(c))
+        norm.bias.copy_(0.1 * torch.randn(c))
+    norm = norm.to(device=cuda, dtype=BF).requires_grad_(False)
+    x1 = (torch.randn(n, c1, hw, hw) * 2 + 3).to(BF)   # a mean far from 0: the shifted sums
+    x2 = None if not c2 else (torch.randn(n, c2, hw, hw) - 1).to(BF)
+    cb = (torch.randn(n, c) * 0.5).to(BF) if bias else None
+    dz = torch.randn(n, c, hw, hw).to(BF)
+
+    x1g = x1.to(cuda).requires_grad_(True)
+    x2g = None if x2 is None else x2.to(cuda).requires_grad_(True)
+    with torch.enable_grad():
+        z = bf16.group_norm(norm, x1g, x2g, None if cb is None else cb.to(cuda))
+    grads = torch.autograd.grad(z, [t for t in (x1g, x2g) if t is not None], dz.to(cuda))
+
+    xs = [x1.float().requires_grad_(True)] + ([] if x2 is None else [x2.float().requires_grad_(True)])
+    with torch.enable_grad():
+        xf = torch.cat(xs, 1)
+        if cb is not None:
+            xf = xf + cb.float()[:, :, None, None]
+        ref = F.group_norm(xf, 32, norm.weight.float().cpu(), norm.bias.float().cpu(), 1e-5)
+        if act:
+            ref = F.silu(ref)
+    rg = torch.autograd.grad(ref, xs, dz.float())
+    e = _rel(z, ref)
+    ev = max(_rel(a, b) for a, b in zip(grads, rg))
+    parity_record("gn_bf16_rel_l2", e, 3e-3, c=[c1, c2], hw=hw)
+    parity_record("gn_bf16_vjp_rel_l2", ev, 5e-3, c=[c1, c2], hw=hw)
+    assert e < 3e-3 and ev < 5e-3, (e, ev)
+
+
+def _attn_ref(q, k, v):
+    s = q @ k.transpose(-1, -2) / math.sqrt(q.shape[-1])
+    return torch.softmax(s, -1) @ v
+
+
+@pytest.mark.parametrize("n,heads,d", [(4096, 8, 40), (1024, 8, 80), (256, 8, 160), (64, 8, 160)])
+def test_attention_bf16_self_fwd_vjp(cuda, n, heads, d, parity_record):
+    from samplers_amd.networks import bf16
+
+    torch.manual_seed(4)
+    b, c = 2, heads * d
+    if not (bf16.attention_supported(b, heads, n, n, d) and bf16.fp32_vjp_supported(b, heads, n, n, d)):
+        pytest.skip("shape not served by the fused kernels")
+    qkv = torch.randn(b, n, 3 * c).to(BF)
+    do = torch.randn(b, n, c).to(BF)
+    g = qkv.to(cuda).requires_grad_(True)
+    with torch.enable_grad():
+        o = bf16.self_attention(g, heads)
+    (dg,) = torch.autograd.grad(o, g, do.to(cuda))
+    qf = qkv.float().requires_grad_(True)
+    with torch.enable_grad():
+        q, k, v = (t.reshape(b, n, heads, d).transpose(1, 2) for t in qf.split(c, -1))
+        ref = _attn_ref(q, k, v).transpose(1, 2).reshape(b, n, c)
+    (rg,) = torch.autograd.grad(ref, qf, do.float())
+    e, ev = _rel(o, ref), _rel(dg, rg)
+    parity_record("attn_bf16_rel_l2", e, 1e-2, n=n, d=d)
+    parity_record("attn_bf16_vjp_rel_l2", ev, 1e-2, n=n, d=d)
+    assert e < 1e-2 and ev < 1e-2, (e, ev)
+
+
+def test_attention_bf16_cross_77_context(cuda):
+    from samplers_amd.networks import bf16
+
+    torch.manual_seed(5)
+    b, n, m, heads, d = 2, 1024, 77, 8, 80
+    c = heads * d
+    q = torch.randn(b, n, c).to(BF)
+    k = torch.randn(1, m, c).to(BF)
+    v = torch.randn(1, m, c).to(BF)
+    do = torch.randn(b, n, c).to(BF)
+    qg = q.to(cuda).requires_grad_(True)
+    with torch.enable_grad():
+        o = bf16.cross_attention(qg, k.to(cuda), v.to(cuda), heads)
+    (dq,) = torch.autograd.grad(o, qg, do.to(cuda))
+    qf = q.float().requires_grad_(True)
+    with torch.enable_grad():
+        sp = lambda t, bb: t.reshape(bb, -1, heads, d).transpose(1, 2)  # noqa: E731
+        ref = _attn_ref(sp(qf, b), sp(k.float(), 1), sp(v.float(), 1)).transpose(1, 2).reshape(b, n, c)
+    (rq,) = torch.autograd.grad(ref, qf, do.float())
+    assert _rel(o, ref) < 1e-2 and _rel(dq, rq) < 1e-2
+
+
+# ---- whole priors -----------------------------------------------------------------------------
+
+def _fwd_vjp(fn, x, cot):
+    xr = x.detach().clone().requires_grad_(True)
+    with torch.enable_grad():
+        out = fn(xr)
+    (g,) = torch.autograd.grad(out, xr, grad_outputs=cot.to(device=out.device, dtype=out.dtype))
+    return out.detach().float().cpu(), g.detach().float().cpu()
+
+
+def _triple(name, fn_gpu, fn_cpu_bf, fn_cpu_32, x, cot, parity_record, direct_tol):
+    """GPU bf16 vs CPU bf16 (direct), and both vs CPU fp32 (GPU error <= 1.5 x CPU error + 1e-3)."""
+    g = _fwd_vjp(fn_gpu, x.to("cuda:0", BF), cot.to(BF))
+    c = _fwd_vjp(fn_cpu_bf, x.to(BF), cot.to(BF))
+    r = _fwd_vjp(fn_cpu_32, x.float(), cot.float())
+    for tag, a, bb, rr in zip(("out", "vjp"), g, c, r):
+        direct = _rel(a, bb)
+        eg, ec = _rel(a, rr), _rel(bb, rr)
+        parity_record(f"{tag}_gpu_bf16_vs_cpu_bf16", direct, direct_tol, module=name)
+        parity_record(f"{tag}_gpu_bf16_vs_fp32", eg, 1.5 * ec + 1e-3, module=name, cpu_bf16_vs_fp32=ec)
+        print(f"{name} {tag}: gpu-bf16 vs cpu-bf16 {direct:.3e}; vs fp32: gpu {eg:.3e}, cpu {ec:.3e}")
+        assert direct < direct_tol, f"{name} {tag}: {direct:.3e}"
+        assert eg <= 1.5 * ec + 1e-3, f"{name} {tag}: gpu {eg:.3e} vs cpu {ec:.3e}"
+
+
+def test_sd15_unet_bf16_fwd_vjp(cuda, parity_record):
+    from samplers_amd.networks.unet2d_condition import build_unet_condition, null_context
+
+    cpu32 = build_unet_condition(seed=0)
+    cpubf = copy.deepcopy(cpu32).to(BF)
+    gpu = copy.deepcopy(cpubf).to(cuda)
+    gen = torch.Generator().manual_seed(6)
+    x = torch.randn(2, 4, 32, 32, generator=gen)
+    cot = torch.randn(2, 4, 32, 32, generator=gen)
+    ctx = null_context()
+    _triple("sd15_unet", lambda v: gpu(v, 501, ctx.to(cuda, BF)), lambda v: cpubf(v, 501, ctx.to(BF)),
+            lambda v: cpu32(v, 501, ctx), x, cot, parity_record, 1e-1)
+    names = _kernel_names(lambda: gpu(x.to(cuda, BF), 501, ctx.to(cuda, BF)))
+    assert any("k_conv3x3_bf16" in s for s in names) and any("k_gnb_apply" in s for s in names)
+    assert any("k_attnb_fwd" in s for s in names)
+    _no_miopen_conv(names)
+
+
+def test_vae_bf16_decode_encode(cuda, parity_record):
+    from samplers_amd.networks.vae import build_vae
+
+    cpu32 = build_vae(seed=1)
+    cpubf = copy.deepcopy(cpu32).to(BF)
+    gpu = copy.deepcopy(cpubf).to(cuda)
+    gen = torch.Generator().manual_seed(7)
+    z = torch.randn(1, 4, 32, 32, generator=gen)
+    cz = torch.randn(1, 3, 256, 256, generator=gen)
+    _triple("vae_decode", gpu.decode, cpubf.decode, cpu32.decode, z, cz, parity_record, 1e-1)
+    x = torch.rand(1, 3, 256, 256, generator=gen) * 2 - 1
+    cx = torch.randn(1, 4, 32, 32, generator=gen)
+    _triple("vae_encode", gpu.encode_mean, cpubf.encode_mean, cpu32.encode_mean, x, cx, parity_record, 1e-1)
+    names = _kernel_names(lambda: gpu.decode(z.to(cuda, BF)))
+    assert any("k_conv3x3_bf16" in s for s in names)
+    _no_miopen_conv(names)
+
+
+def test_celebahq_unet_bf16_fwd_vjp(cuda, parity_record):
+    from samplers_amd.networks.unet2d import build_unet
+
+    cpu32 = build_unet(seed=0)
+    cpubf = copy.deepcopy(cpu32).to(BF)
+    gpu = copy.deepcopy(cpubf).to(cuda)
+    gen = torch.Generator().manual_seed(8)
+    x = torch.randn(1, 3, 256, 256, generator=gen)
+    cot = torch.randn(1, 3, 256, 256, generator=gen)
+    _triple("celebahq_unet", lambda v: gpu(v, 500), lambda v: cpubf(v, 500), lambda v: cpu32(v, 500), x, cot,
+            parity_record, 1e-1)
+
+
+def test_psld_bf16_sd15_matches_oracle(cuda, parity_record):
+    """PSLDSampler with LatentDiffusionNetwork.from_config(torch_dtype=bf16): 3 guided iterations +
+    the final decode at 3x256², B = 2, centre inpainting, vs oracle/latent_loops.py with the same
+    bf16 modules on the CPU behind the same fp32 boundary (networks in bf16, the loop in fp32)."""
+    from oracle.latent_loops import psld_reference
+    from samplers_amd.inverse_problem import InverseProblem
+    from samplers_amd.networks.latent import LatentDiffusionNetwork, StableDiffusionCondition
+    from samplers_amd.noise import GaussianNoise
+    from samplers_amd.operators import CenterInpaintingOperator
+    from samplers_amd.samplers.psld import PSLDSampler
+
+    b, shape, steps = 2, (3, 256, 256), 4
+    lshape = (4, 32, 32)
+    gen = torch.Generator().manual_seed(21)
+    op = CenterInpaintingOperator(shape, 0.5)
+    kept = op._kept_indices.cpu()
+    n = int(np.prod(shape))
+
+    def apply(v):
+        return v.reshape(v.shape[0], -1)[:, kept]
+
+    def adjoint(v):
+        out = torch.zeros(v.shape[0], n, dtype=v.dtype)
+        out = out.index_put((torch.arange(v.shape[0])[:, None], kept[None, :]), v)
+        return out.reshape(v.shape[0], *shape)
+
+    x_true = si.fixture_x_true(b, shape, 22)
+    y = apply(x_true) + 0.05 * torch.randn(b, kept.numel(), generator=gen)
+    z0 = torch.randn(b, *lshape, generator=gen)
+    xi = {i: torch.randn(b, *lshape, generator=gen) for i in range(16)}
+
+    cpu = LatentDiffusionNetwork.from_config(seed=0, torch_dtype=BF)
+    assert cpu.dtype == BF
+    gpu = copy.deepcopy(cpu).to(cuda)
+    fn = lambda k, i, s: (z0 if k == "init" else xi[i]).to(cuda)  # noqa: E731
+    problem = InverseProblem(op.to(cuda), y.to(cuda), GaussianNoise(0.05).to(cuda))
+    cond = StableDiffusionCondition(prompt=[""] * b)  # as run_psld.py:39; CFG of equal rows collapses
+    names = _kernel_names(lambda: PSLDSampler(gpu)(problem, num_sampling_steps=steps, noise_fn=fn, condition=cond))
+    out = PSLDSampler(gpu)(problem, num_sampling_steps=steps, noise_fn=fn, condition=cond)
+    assert out.dtype == BF and torch.isfinite(out.float()).all()
+    for k in ("k_conv3x3_bf16", "k_gnb_apply", "k_gnb_bwd_apply", "k_attnb_fwd", "k_psld_pixel"):
+        assert any(k in s for s in names), k
+    _no_miopen_conv(names)
+
+    cpu.set_sampling_parameters(steps, batch_size=b)
+    cpu.set_condition(cond)
+    f32 = lambda t: t.to(torch.float32)  # noqa: E731
+    ref = psld_reference(lambda v, t: f32(cpu(v.to(BF), t)), cpu.alphas_cumprod.float(), cpu.timesteps_host,
+                         apply, adjoint, lambda v: f32(cpu.decode(v.to(BF), differentiable=True)),
+                         lambda v: f32(cpu.encode(v.to(BF), differentiable=True)), y, z0, lambda i: xi[i])
+    err = _rel(out, ref.reshape(out.shape))
+    print(f"PSLD bf16 SD1.5: 3 guided steps + decode, rel L2 vs the bf16 oracle {err:.3e}")
+    parity_record("x0_rel_l2", err, PSLD_BF16_TOL, sampler="PSLD", dtype="bf16", guided_steps=3, batch=b,
+                  image=list(shape))
+    assert err < PSLD_BF16_TOL, err

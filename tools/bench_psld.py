@@ -35,7 +35,8 @@ import samplers_amd  # noqa: E402,F401
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
-from bench import MFMA_F32_PEAK_TFLOPS, conv_summary, host_cpu, self_launch, setup_dist  # noqa: E402
+from bench import (MFMA_BF16_PEAK_TFLOPS, MFMA_F32_PEAK_TFLOPS, conv_summary, host_cpu, self_launch,  # noqa: E402
+                   setup_dist)
 
 VAE_FLOP_PER_SAMPLE = 7.13e12
 # SD 1.5 UNet at 64x64 latents: 0.80 TFLOP forward + 0.92 input VJP (torch FlopCounterMode)
@@ -63,6 +64,10 @@ def main():
     p.add_argument("--cfg", action="store_true",
                    help="classifier-free guidance on: distinct (seeded random) prompt embeddings, "
                         "guidance 7.5, so the UNet batch doubles (stable_diffusion.py:300-320)")
+    p.add_argument("--dtype", choices=("fp32", "bf16"), default="fp32",
+                   help="the priors' dtype: bf16 = the reference's own PSLD run (scripts/run_psld.py:14-20, "
+                        "torch_dtype=torch.bfloat16) on the bf16 NHWC kernels; the sample, guidance and "
+                        "DDIM update stay fp32 (networks.base.Fp32Boundary)")
     p.add_argument("--cpu-baseline", action="store_true",
                    help="also time one PSLD iteration of oracle/latent_loops.py on the host cores "
                         "(batch 1, same networks)")
@@ -92,7 +97,8 @@ def main():
     x_true = (torch.rand((args.batch, *shape), generator=gen) * 2 - 1).to(dev)
     y = op.apply(x_true)
     y = y + (0.05 * torch.randn(tuple(y.shape), generator=gen)).to(dev)
-    net = LatentDiffusionNetwork.from_config(seed=0, device=dev)
+    dtype = torch.bfloat16 if args.dtype == "bf16" else torch.float32
+    net = LatentDiffusionNetwork.from_config(seed=0, device=dev, torch_dtype=dtype)
     net.set_sampling_parameters(100, batch_size=args.batch)
     if args.cfg:  # distinct conditional / unconditional contexts: the doubled-batch path
         pe = torch.randn(args.batch, 77, 768, generator=torch.Generator().manual_seed(77))
@@ -102,7 +108,9 @@ def main():
     net.set_condition(cond)
     problem = InverseProblem(op, y, GaussianNoise(0.05).to(dev))
     lat = tuple(net.get_latent_shape(shape))
-    step = FusedPSLDStep(net, problem, y.reshape(args.batch, -1), 1, lat, group=group)
+    from samplers_amd.networks.base import fp32_view
+
+    step = FusedPSLDStep(fp32_view(net), problem, y.reshape(args.batch, -1), 1, lat, group=group)
     seed, off = 20260101, rank * args.batch
     z = initial_sample((args.batch, *lat), dev, rng="philox", seed=seed, sample_offset=off,
                        noise_fn=None)
@@ -145,21 +153,25 @@ def main():
     if not torch.isfinite(z).all():
         raise SystemExit("non-finite latents")
     ms = dt / args.steps * 1e3
-    conv = conv_summary(timer.summary())
+    bf = args.dtype == "bf16"
+    conv = conv_summary(timer.summary(), ("conv3x3_bf16",)) if bf else conv_summary(timer.summary())
     timer.close()
     roofline = None
+    peak = MFMA_BF16_PEAK_TFLOPS if bf else MFMA_F32_PEAK_TFLOPS
     if conv:
         roofline = {"kernel": "3x3 conv tiles (" + " + ".join(conv["kernels"]) + ")",
                     "bound": "mfma", "achieved": round(conv["tflops"], 2),
-                    "peak": MFMA_F32_PEAK_TFLOPS, "unit": "TFLOP/s",
-                    "frac": round(conv["tflops"] / MFMA_F32_PEAK_TFLOPS, 4), "traffic": None,
+                    "peak": peak, "unit": "TFLOP/s",
+                    "frac": round(conv["tflops"] / peak, 4), "traffic": None,
                     "algorithmic_flops_per_launch": conv["flops"] / conv["count"],
-                    "flops_basis": "executed MFMA FLOPs (Winograd: 8*N*Cin*Cout*H*W, direct: 18*...)",
+                    "flops_basis": ("bf16 implicit GEMM: 18*N*Cin*Cout*H*W per launch (forward or input VJP), "
+                                    "dense bf16 MFMA peak" if bf else
+                                    "executed MFMA FLOPs (Winograd: 8*N*Cin*Cout*H*W, direct: 18*...)"),
                     "avg_launch_ms": round(conv["ms"] / conv["count"], 4),
                     "share_of_step": round(conv["ms"] / args.steps / ms, 4)}
     cpu = None
     if args.cpu_baseline and rank == 0:
-        cpu = cpu_baseline_psld(args.image, cond if args.cfg else None)
+        cpu = cpu_baseline_psld(args.image, cond if args.cfg else None, dtype)
     if world > 1:
         dist.destroy_process_group()
     if rank != 0:
@@ -170,7 +182,7 @@ def main():
         "unit": "samples/sec (batch×steps/s)",
         "n_gpus": world, "scaling": "weak", "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(ms, 2),
-        "higher_is_better": True, "dtype": "f32",
+        "higher_is_better": True, "dtype": "bf16" if bf else "f32",
         "data": "synthetic (seeded U(-1,1) images, centre mask, sigma=0.05); random-init SD1.5 "
                 "VAE + SD1.5 UNet2DConditionModel architecture (859.5 M, null 77x768 context)",
         "config": {"workload": f"PSLD + CenterInpainting(0.5) + GaussianNoise(0.05), 3x{args.image}²",
@@ -186,10 +198,10 @@ def main():
     }), flush=True)
 
 
-def cpu_baseline_psld(image: int, cond) -> dict:
+def cpu_baseline_psld(image: int, cond, dtype=torch.float32) -> dict:
     """One PSLD iteration (oracle/latent_loops.py, psld.py:118-153 semantics) at batch 1 on
-    the host cores with the same random-init SD 1.5 networks (CPU copies), at the CPU share
-    the job is given (bench.host_cpu)."""
+    the host cores with the same random-init SD 1.5 networks (CPU copies, in ``dtype`` behind the
+    same fp32 boundary as the device run), at the CPU share the job is given (bench.host_cpu)."""
     import numpy as np
 
     from oracle.latent_loops import psld_reference
@@ -199,7 +211,7 @@ def cpu_baseline_psld(image: int, cond) -> dict:
     host = host_cpu()
     torch.set_num_threads(host["cpu_share"])
     shape = (3, image, image)
-    net = LatentDiffusionNetwork.from_config(seed=0)
+    net = LatentDiffusionNetwork.from_config(seed=0, torch_dtype=dtype)
     net.set_sampling_parameters(100, batch_size=1)
     if cond is not None:
         cond = StableDiffusionCondition(prompt=None, prompt_embeds=cond.prompt_embeds[:1],
@@ -221,16 +233,18 @@ def cpu_baseline_psld(image: int, cond) -> dict:
     z = torch.randn(1, *net.get_latent_shape(shape), generator=gen)
     ts = net.timesteps_host
     t0 = time.perf_counter()
-    psld_reference(lambda v, t: net(v, t), net.alphas_cumprod, ts, apply, adjoint,
-                   lambda v: net.decode(v, differentiable=True),
-                   lambda v: net.encode(v, differentiable=True), y, z,
+    f32 = lambda t: t.to(torch.float32)  # noqa: E731
+    psld_reference(lambda v, t: f32(net(v.to(dtype), t)), net.alphas_cumprod.float(), ts, apply, adjoint,
+                   lambda v: f32(net.decode(v.to(dtype), differentiable=True)),
+                   lambda v: f32(net.encode(v.to(dtype), differentiable=True)), y, z,
                    lambda i: torch.randn(z.shape, generator=gen), steps_limit=1)
     dt = time.perf_counter() - t0
     return {"value": round(1 / dt, 5), "unit": "samples/sec (batch×steps/s)",
             "cores": host["cpu_share"], "kind": "port", "cpu_model": host["model"],
             "sample": f"one PSLD iteration of oracle/latent_loops.py at batch 1, 3x{image}², "
                       f"same random-init SD 1.5 VAE + UNet{' with CFG' if cond is not None else ''}, "
-                      f"fp32, torch-CPU {torch.__version__}: {dt:.1f} s"}
+                      f"{'bf16 networks behind the fp32 boundary' if dtype == torch.bfloat16 else 'fp32'}, "
+                      f"torch-CPU {torch.__version__}: {dt:.1f} s"}
 
 
 if __name__ == "__main__":

@@ -1,0 +1,32 @@
+#!/bin/bash
+# Round-6 GPU steps: every GPU step under its own time limit, chained so that a crash or a
+# timeout ends the call (no retries).  Usage: tools/r6_gpu.sh STEP...
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+OUT=gpurun_out/r6
+mkdir -p "$OUT"
+( while sleep 30; do date +%T >> "$OUT/heartbeat"; done ) &
+HB=$!
+trap 'kill $HB 2>/dev/null' EXIT
+run() {  # run NAME SECONDS CMD...: log to $OUT/NAME.log; stop on a signal / timeout exit
+    local name=$1 secs=$2; shift 2
+    echo "== $name: $*" | tee -a "$OUT/steps.log"
+    timeout -k 10 "$secs" "$@" > "$OUT/$name.log" 2>&1
+    local rc=$?
+    echo "== $name rc=$rc" | tee -a "$OUT/steps.log"
+    tail -5 "$OUT/$name.log"
+    if [ $rc -ge 124 ]; then echo "stopping after $name (rc $rc)"; exit $rc; fi
+    return 0
+}
+for step in "$@"; do
+    case $step in
+        parity1000) run parity1000 600 python -u tools/parity_1000.py --phase gpu ;;
+        bf16tests) run bf16_tests 900 python -u -m pytest tests/test_bf16_gpu.py -v --timeout 400 --timeout-method thread ;;
+        bf16kern) run bf16_kern 600 python -u -m pytest tests/test_bf16_gpu.py -v --timeout 300 --timeout-method thread -k "conv3x3 or groupnorm or attention" ;;
+        psldbf16) run psld_bf16 900 python -u tools/bench_psld.py --dtype bf16 --steps 3 --warmup 2 --cpu-baseline ;;
+        psldbf16q) run psld_bf16 600 python -u tools/bench_psld.py --dtype bf16 --steps 3 --warmup 2 ;;
+        psldbf16prof) run psld_bf16_prof 900 rocprofv3 --kernel-trace --stats -d "$OUT/prof_psld_bf16" -o run -- python -u tools/bench_psld.py --dtype bf16 --steps 2 --warmup 1 ;;
+        gputests) run gpu_tests 1100 python -u -m pytest tests -m gpu -q --timeout 400 --timeout-method thread ;;
+        *) echo "unknown step $step"; exit 2 ;;
+    esac
+done
