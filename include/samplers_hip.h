@@ -574,6 +574,13 @@ int64_t sp_conv3x3_bf16_packed_size(int32_t cin, int32_t cout);
  * W'[ci][co][2-ky][2-kx].  bias fp32 [cout] or NULL, res bf16 like y or NULL. */
 int sp_conv3x3_bf16(const void* x, const void* wp, const float* bias, const void* res, int64_t n, int32_t cin,
                     int32_t cout, int32_t h, int32_t w, void* y, sp_stream_t stream);
+/* y = conv3x3(upsample_nearest2x(x)) + bias (+ res) (diffusers' Upsample2D): x [n][h/2][w/2][cin],
+ * y [n][h][w][cout] — the upsampled tensor is never written; its VJP is sp_conv3x3_bf16 with the
+ * VJP pack at full resolution followed by sp_pool2x2_bf16. */
+int sp_conv3x3_bf16_up(const void* x, const void* wp, const float* bias, const void* res, int64_t n, int32_t cin,
+                       int32_t cout, int32_t h, int32_t w, void* y, sp_stream_t stream);
+/* dx[n][h/2][w/2][c] = 2x2 block sums of dz[n][h][w][c], NHWC bf16 (c % 8 == 0) */
+int sp_pool2x2_bf16(const void* dz, int64_t n, int32_t c, int32_t h, int32_t w, void* dx, sp_stream_t stream);
 int sp_groupnorm_bf16_supported(int32_t c1, int32_t c2, int32_t groups);
 int64_t sp_groupnorm_bf16_workspace(int64_t n, int32_t c, int64_t hw);
 /* z = act(GroupNorm(cat(x1, x2) + chan_bias) * gamma + beta) over NHWC bf16 parts (channel

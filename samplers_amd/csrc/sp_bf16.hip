@@ -90,8 +90,11 @@ struct CvGeo {
     static constexpr int NP = (PQ * 2 + kBlock - 1) / kBlock;     // 16-byte patch pieces per thread
 };
 
-template <int TC>
-__global__ __launch_bounds__(kBlock, 2) void k_conv3x3_bf16(const u16* __restrict__ x, const u16* __restrict__ wp,
+// UP: the input is the half-resolution tensor of diffusers' Upsample2D and the patch reads
+// pixel (h >> 1, w >> 1) of it for full-resolution pixel (h, w): conv(upsample_nearest2x(x))
+// without the upsampled tensor in HBM.
+template <int TC, bool UP>
+__global__ __launch_bounds__(kBlock, TC == 4 ? 1 : 2) void k_conv3x3_bf16(const u16* __restrict__ x, const u16* __restrict__ wp,
                                                          const float* __restrict__ bias, const u16* __restrict__ res,
                                                          int n, int cin, int cout, int h, int w,
                                                          u16* __restrict__ y) {
@@ -123,8 +126,12 @@ __global__ __launch_bounds__(kBlock, 2) void k_conv3x3_bf16(const u16* __restric
             const int prow = q / G::PW, pcol = q - prow * G::PW;
             const int seg = prow / (G::SR + 2), pr = prow - seg * (G::SR + 2);
             const int nn = n0 + seg, hi = h0 + pr - 1, wi = c0 + pcol - 1;
-            if (nn < n && (unsigned)hi < (unsigned)h && (unsigned)wi < (unsigned)w)
-                poff[k] = (((int64_t)nn * h + hi) * w + wi) * cin + half * 8;
+            if (nn < n && (unsigned)hi < (unsigned)h && (unsigned)wi < (unsigned)w) {
+                if constexpr (UP)
+                    poff[k] = (((int64_t)nn * (h >> 1) + (hi >> 1)) * (w >> 1) + (wi >> 1)) * cin + half * 8;
+                else
+                    poff[k] = (((int64_t)nn * h + hi) * w + wi) * cin + half * 8;
+            }
         }
     }
     bq_u4 sw[G::NW], spx[G::NP];
@@ -230,13 +237,15 @@ __global__ __launch_bounds__(kBlock, 2) void k_conv3x3_bf16(const u16* __restric
     }
 }
 
+static unsigned stream_blocks(int64_t vectors);
+
 static int conv_tc(int h, int w) {
     if (w % 32 == 0 && h % 16 == 0) return 32;
     if (h == w && (w == 16 || w == 8 || w == 4)) return w;
     return 0;
 }
 
-template <int TC>
+template <int TC, bool UP>
 static void conv_bf16_launch(const u16* x, const u16* wp, const float* bias, const u16* res, int n, int cin,
                              int cout, int h, int w, u16* y, hipStream_t s) {
     using G = CvGeo<TC>;
@@ -247,8 +256,33 @@ static void conv_bf16_launch(const u16* x, const u16* wp, const float* bias, con
     else
         tiles = (n + G::S - 1) / G::S;
     const double flops = 18.0 * n * (double)h * w * cin * cout;
-    launch_w(TK_CONV_BF16, flops, k_conv3x3_bf16<TC>, dim3(cbn, static_cast<unsigned>(tiles)), dim3(kBlock), s, x, wp,
-             bias, res, n, cin, cout, h, w, y);
+    launch_w(TK_CONV_BF16, flops, k_conv3x3_bf16<TC, UP>, dim3(cbn, static_cast<unsigned>(tiles)), dim3(kBlock), s, x,
+             wp, bias, res, n, cin, cout, h, w, y);
+}
+
+// Upsample2D's VJP after the full-resolution input VJP: dx[n][i][j][c] = sum of the 2 x 2 block
+// dz[n][2i + a][2j + b][c] (fp32 sum, one rounding), 8 channels per thread-iteration
+__global__ __launch_bounds__(kBlock) void k_pool2x2_bf16(const u16* __restrict__ dz, int64_t n, int c, int hs, int ws,
+                                                         u16* __restrict__ dx) {
+    const int cv = c / 8;
+    const int64_t total = n * hs * ws * cv;
+    for (int64_t v = (int64_t)blockIdx.x * kBlock + threadIdx.x; v < total; v += (int64_t)gridDim.x * kBlock) {
+        const int j = static_cast<int>(v % cv);
+        const int64_t pix = v / cv, nn = pix / ((int64_t)hs * ws), rem = pix - nn * hs * ws;
+        const int i = static_cast<int>(rem / ws), jj = static_cast<int>(rem - (int64_t)i * ws);
+        float acc[8] = {};
+#pragma unroll
+        for (int a = 0; a < 2; ++a)
+#pragma unroll
+            for (int b = 0; b < 2; ++b) {
+                float f[8];
+                unpack8(*reinterpret_cast<const bq_u4*>(
+                            dz + (((nn * 2 * hs + 2 * i + a) * (2 * ws) + 2 * jj + b) * c + 8 * j)), f);
+#pragma unroll
+                for (int e = 0; e < 8; ++e) acc[e] += f[e];
+            }
+        *reinterpret_cast<bq_u4*>(dx + pix * c + 8 * j) = pack8(acc);
+    }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -768,9 +802,10 @@ int64_t sp_conv3x3_bf16_packed_size(int32_t cin, int32_t cout) {
 // y[n][h][w][cout] = conv3x3(x[n][h][w][cin], W) + bias (+ res), NHWC bf16, fp32 accumulation.
 // wp: packed as [co block of 64][ci block of 16][tap 3 ky + kx][64 co][16 ci] (rows past cout
 // zero); the input VJP is the same call with the pack of W'[ci][co][2-ky][2-kx].
-int sp_conv3x3_bf16(const void* x, const void* wp, const float* bias, const void* res, int64_t n, int32_t cin,
-                    int32_t cout, int32_t h, int32_t w, void* y, sp_stream_t stream) {
+static int conv_bf16_call(const void* x, const void* wp, const float* bias, const void* res, int64_t n, int32_t cin,
+                          int32_t cout, int32_t h, int32_t w, void* y, sp_stream_t stream, bool up) {
     if (!x || !wp || !y || n <= 0 || !sp_conv3x3_bf16_supported(cin, cout, h, w)) return SP_EINVAL;
+    if (up && (h % 2 || w % 2)) return SP_EINVAL;
     if (n * h * (int64_t)w * std::max(cin, cout) >= (int64_t(1) << 40) || n >= (int64_t(1) << 30)) return SP_EINVAL;
     hipStream_t s = static_cast<hipStream_t>(stream);
     const u16* xx = static_cast<const u16*>(x);
@@ -778,13 +813,43 @@ int sp_conv3x3_bf16(const void* x, const void* wp, const float* bias, const void
     const u16* rr = static_cast<const u16*>(res);
     u16* yy = static_cast<u16*>(y);
     const int ni = static_cast<int>(n);
+    if (up) {
+        switch (conv_tc(h, w)) {
+            case 32: conv_bf16_launch<32, true>(xx, ww, bias, rr, ni, cin, cout, h, w, yy, s); break;
+            case 16: conv_bf16_launch<16, true>(xx, ww, bias, rr, ni, cin, cout, h, w, yy, s); break;
+            case 8: conv_bf16_launch<8, true>(xx, ww, bias, rr, ni, cin, cout, h, w, yy, s); break;
+            default: conv_bf16_launch<4, true>(xx, ww, bias, rr, ni, cin, cout, h, w, yy, s); break;
+        }
+        return check_launch("sp_conv3x3_bf16_up");
+    }
     switch (conv_tc(h, w)) {
-        case 32: conv_bf16_launch<32>(xx, ww, bias, rr, ni, cin, cout, h, w, yy, s); break;
-        case 16: conv_bf16_launch<16>(xx, ww, bias, rr, ni, cin, cout, h, w, yy, s); break;
-        case 8: conv_bf16_launch<8>(xx, ww, bias, rr, ni, cin, cout, h, w, yy, s); break;
-        default: conv_bf16_launch<4>(xx, ww, bias, rr, ni, cin, cout, h, w, yy, s); break;
+        case 32: conv_bf16_launch<32, false>(xx, ww, bias, rr, ni, cin, cout, h, w, yy, s); break;
+        case 16: conv_bf16_launch<16, false>(xx, ww, bias, rr, ni, cin, cout, h, w, yy, s); break;
+        case 8: conv_bf16_launch<8, false>(xx, ww, bias, rr, ni, cin, cout, h, w, yy, s); break;
+        default: conv_bf16_launch<4, false>(xx, ww, bias, rr, ni, cin, cout, h, w, yy, s); break;
     }
     return check_launch("sp_conv3x3_bf16");
+}
+
+int sp_conv3x3_bf16(const void* x, const void* wp, const float* bias, const void* res, int64_t n, int32_t cin,
+                    int32_t cout, int32_t h, int32_t w, void* y, sp_stream_t stream) {
+    return conv_bf16_call(x, wp, bias, res, n, cin, cout, h, w, y, stream, false);
+}
+
+// y = conv3x3(upsample_nearest2x(x)) + bias (+ res): x [n][h/2][w/2][cin], y [n][h][w][cout]
+int sp_conv3x3_bf16_up(const void* x, const void* wp, const float* bias, const void* res, int64_t n, int32_t cin,
+                       int32_t cout, int32_t h, int32_t w, void* y, sp_stream_t stream) {
+    return conv_bf16_call(x, wp, bias, res, n, cin, cout, h, w, y, stream, true);
+}
+
+// dx[n][h/2][w/2][c] = 2 x 2 block sums of dz[n][h][w][c] (Upsample2D's VJP), NHWC bf16
+int sp_pool2x2_bf16(const void* dz, int64_t n, int32_t c, int32_t h, int32_t w, void* dx, sp_stream_t stream) {
+    if (!dz || !dx || n <= 0 || c <= 0 || c % 8 || h <= 0 || w <= 0 || h % 2 || w % 2) return SP_EINVAL;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const int64_t vec = n * (h / 2) * (int64_t)(w / 2) * (c / 8);
+    launch(0, k_pool2x2_bf16, dim3(stream_blocks(vec)), dim3(kBlock), s, static_cast<const u16*>(dz), n, c, h / 2,
+           w / 2, static_cast<u16*>(dx));
+    return check_launch("sp_pool2x2_bf16");
 }
 
 // ---- GroupNorm ------------------------------------------------------------------------------

@@ -101,6 +101,12 @@ def _gemm_backward(q: Tensor, k: Tensor, v: Tensor, out: Tensor, lse: Tensor, do
 FUSED_BWD_MIN_TOKENS = 512
 
 
+# Above this many bytes of pre-split K / V images (~1.9x the fp32 K + V of the call: 2.5 GB for
+# SD's 4096-token attn1 at batch 128) the split-bf16 forward splits per workgroup instead
+# (sp_attention6_fwd_ws with no workspace: same results, one split per 128-query workgroup).
+SPLIT_WS_MAX_BYTES = int(os.environ.get("SAMPLERS_AMD_ATTN6_WS_MIB", "1024")) * 2**20
+
+
 def split_bf16_forward(q: Tensor, k: Tensor, v: Tensor, batch: int, heads: int, n: int, d: int, rs: int,
                        ro: int, scale: float, out: Tensor, lse: Tensor, offsets=(0, 0, 0)) -> bool:
     """Self-attention forward on the split-bf16 kernel (``csrc/sp_attention6.hip``: fp32 operands
@@ -113,10 +119,13 @@ def split_bf16_forward(q: Tensor, k: Tensor, v: Tensor, batch: int, heads: int, 
     if not (lib.sp_attention_bf16x6_enabled() and lib.sp_attention6_supported(batch, heads, n, d)):
         return False
     nb = int(lib.sp_attention6_workspace(batch, heads, n, d))
-    ws = torch.empty(nb, device=q.device, dtype=torch.uint8)
+    if nb > SPLIT_WS_MAX_BYTES:  # the per-workgroup split form needs no workspace
+        nb = 0
+    ws = torch.empty(max(nb, 1), device=q.device, dtype=torch.uint8)
     _hip.check(lib.sp_attention6_fwd_ws(q.data_ptr() + offsets[0], k.data_ptr() + offsets[1],
                                         v.data_ptr() + offsets[2], batch, heads, n, d, rs, ro, scale,
-                                        _hip.ptr(out), _hip.ptr(lse), _hip.ptr(ws), nb, _hip.stream_of(q)),
+                                        _hip.ptr(out), _hip.ptr(lse), _hip.ptr(ws) if nb else None, nb,
+                                        _hip.stream_of(q)),
                "sp_attention6_fwd_ws")
     return True
 

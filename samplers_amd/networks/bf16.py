@@ -167,6 +167,47 @@ def conv3x3(module: nn.Module, x: Tensor, res: Tensor | None = None, bias: Tenso
     return _ConvBf16Fn.apply(xp, r, module, _bias_f32(module, b))
 
 
+class _UpConvBf16Fn(torch.autograd.Function):
+    """conv3x3(upsample_nearest2x(x)) (diffusers Upsample2D) on sp_conv3x3_bf16_up: the patch
+    reads the half-resolution pixel, the upsampled tensor is never written; VJP: the
+    full-resolution input VJP, then the 2 x 2 block sums (sp_pool2x2_bf16)."""
+
+    @staticmethod
+    def forward(ctx, x, module, bias):
+        lib = _hip.load_library()
+        n, cin, h, w = x.shape
+        cout = module.weight.shape[0]
+        ctx.module, ctx.xs = module, x.shape
+        y = torch.empty(n, cout, 2 * h, 2 * w, device=x.device, dtype=BF16, memory_format=CL)
+        _hip.check(lib.sp_conv3x3_bf16_up(_p(x), _p(conv_pack(module, False), cl=False),
+                                          None if bias is None else bias.data_ptr(), None, n, cin, cout, 2 * h,
+                                          2 * w, _p(y), _hip.stream_of(x)), "sp_conv3x3_bf16_up")
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        lib = _hip.load_library()
+        module = ctx.module
+        n, cin, h, w = ctx.xs
+        cout = module.weight.shape[0]
+        d = _pad_channels(dy.to(BF16), _ceil(cout, 16))
+        full = _conv_launch(d, conv_pack(module, True), None, None, cin)
+        dx = torch.empty(n, cin, h, w, device=dy.device, dtype=BF16, memory_format=CL)
+        _hip.check(lib.sp_pool2x2_bf16(_p(full), n, cin, 2 * h, 2 * w, _p(dx), _hip.stream_of(dy)),
+                   "sp_pool2x2_bf16")
+        return dx, None, None
+
+
+def upsample_conv_supported(module: nn.Module, x: Tensor) -> bool:
+    return (is_bf16_device(x) and x.dim() == 4 and x.shape[1] % 16 == 0 and not module.weight.requires_grad
+            and bool(_hip.load_library().sp_conv3x3_bf16_supported(x.shape[1], module.weight.shape[0],
+                                                                   2 * x.shape[2], 2 * x.shape[3])))
+
+
+def upsample_conv3x3(module: nn.Module, x: Tensor) -> Tensor:
+    return _UpConvBf16Fn.apply(nhwc(x), module, _bias_f32(module, module.bias))
+
+
 class _StridedBf16Fn(torch.autograd.Function):
     """A 3x3 / stride-2 convolution as the stride-1 one at full resolution read at every other
     position (``phase`` 0: padding 1; 1: diffusers' padding (0, 1, 0, 1)); VJP: dy scattered to

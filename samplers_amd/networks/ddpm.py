@@ -61,7 +61,8 @@ class DDPMNetwork(EpsilonNetwork[NoCondition]):
     """ε-network over a pixel-space UNet and a DDPM schedule."""
 
     # its UNet runs on this project's kernels and torch's caching allocator only, so a DPS step
-    # over it can be captured into a hipGraph (DPSSampler's default replay at small batches)
+    # over it can be captured into a hipGraph (DPSSampler(graph=True); the automatic replay rule,
+    # dps.graph_auto, is off: GRAPH_AUTO_MAX_BATCH = 0, replay measured slower at every batch)
     graph_capturable = True
 
     def __init__(self, unet: UNet2DModel, schedule: DDPMSchedule | None = None):

@@ -145,8 +145,9 @@ class LatentDiffusionNetwork(LatentEpsilonNetwork[StableDiffusionCondition]):
         ``skip_prk_steps``, DDIM or DDPM, ``leading`` spacing); nothing is downloaded, so a hub
         name without a local copy raises ``FileNotFoundError``.  The text encoder is not read
         (out of scope, module doc): conditions come as ``prompt_embeds``, and the empty prompt
-        maps to ``null_prompt_embeds`` — the caller's CLIP embedding of ``""`` (1 x 77 x 768),
-        else the synthetic null context.  Weights are computed in fp32 unless ``torch_dtype``
+        maps to ``null_prompt_embeds`` — the caller's CLIP embedding of ``""`` (77 x 768 or
+        1 x 77 x 768); without it an empty prompt raises (the synthetic null context stands in
+        for random weights only).  Weights are computed in fp32 unless ``torch_dtype``
         says otherwise (fp16 variants are upcast)."""
         from .checkpoint import load_state, meta_module, read_json, resolve_root, weights_path
 
@@ -161,11 +162,16 @@ class LatentDiffusionNetwork(LatentEpsilonNetwork[StableDiffusionCondition]):
         vae = meta_module(AutoencoderKL, vae_config)
         load_state(vae, weights_path(root, "vae", variant), dtype=dt)
         net = cls(unet.to(device=device), vae.to(device=device), schedule=schedule, pndm=pndm)
-        if null_prompt_embeds is not None:
+        if null_prompt_embeds is None:
+            # real weights with the synthetic null context would condition every empty prompt on
+            # a random tensor: empty prompts raise until real embeddings are supplied (_embed)
+            net._null_context_synthetic = True
+        else:
             want = tuple(net.null_prompt_embeds.shape)
-            if tuple(null_prompt_embeds.shape[-2:]) != want[-2:]:
-                raise ValueError(f"null_prompt_embeds: expected (1, {want[1]}, {want[2]}), "
-                                 f"got {tuple(null_prompt_embeds.shape)}")
+            got = tuple(null_prompt_embeds.shape)
+            if got[-2:] != want[-2:] or null_prompt_embeds.numel() != want[1] * want[2]:
+                raise ValueError(f"null_prompt_embeds: expected the CLIP embedding of '' as ({want[1]}, {want[2]}) "
+                                 f"or (1, {want[1]}, {want[2]}), got {got}")
             net.null_prompt_embeds = null_prompt_embeds.reshape(want).to(
                 device=net.null_prompt_embeds.device, dtype=dt)
         return net
@@ -178,6 +184,11 @@ class LatentDiffusionNetwork(LatentEpsilonNetwork[StableDiffusionCondition]):
         if any(p != "" for p in prompts):
             raise NotImplementedError(
                 f"no text encoder offline: pass {what}_embeds instead of a non-empty {what}")
+        if getattr(self, "_null_context_synthetic", False):
+            raise ValueError(
+                f"this network was loaded from a checkpoint without null_prompt_embeds: the empty {what} "
+                "needs the CLIP embedding of '' (pass null_prompt_embeds= to from_pretrained, or "
+                f"{what}_embeds in the condition); the synthetic null context is for random weights only")
         return self.null_prompt_embeds.expand(len(prompts), -1, -1)
 
     def set_condition(self, condition: StableDiffusionCondition | None) -> None:

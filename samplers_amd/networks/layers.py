@@ -514,6 +514,10 @@ class _UpsampleConv3x3Fn(torch.autograd.Function):
 
 def upsample_conv(module: "Conv3x3", x: Tensor) -> Tensor:
     """``module(upsample_nearest2x(x))``: fused where ``upsample_conv_supported``, else the pair."""
+    if x.is_cuda and x.dtype == torch.bfloat16:
+        from . import bf16
+        if bf16.upsample_conv_supported(module, x):
+            return bf16.upsample_conv3x3(module, x)
     if upsample_conv_supported(module, x):
         return _UpsampleConv3x3Fn.apply(x, module.weight, module.bias, module)
     return module(upsample_nearest2x(x))
@@ -870,6 +874,10 @@ def proj_nchw_to_tokens(x: Tensor, module, w2d: Tensor | None = None, bias: Tens
     ``(b, h w, c_out)``: the transpose happens in the GEMM's stores (HIP, CUDA fp32, frozen
     weights), else reshape + transpose + linear in torch."""
     b, c, h, w = x.shape
+    if batch_invariant_enabled() and b > 1 and x.is_cuda:
+        # one sample per call: the backend (x6 tile or hipBLASLt) follows the per-call row count
+        # (sp_gemm_x6_layout_supported's size guard, hipBLASLt's algorithm), never the batch
+        return torch.cat([proj_nchw_to_tokens(x[i:i + 1], module, w2d, bias) for i in range(b)])
     w2d = module.weight.reshape(module.weight.shape[0], c) if w2d is None else w2d
     bias = getattr(module, "bias", None) if bias is None else bias
     co = w2d.shape[0]
@@ -886,6 +894,11 @@ def proj_tokens_to_nchw(tokens: Tensor, module, res: Tensor, w2d: Tensor | None 
     to the norm that reads ``res`` (``GroupNormAct(..., box=box)``)."""
     b, co, h, w = res.shape
     c = tokens.shape[-1]
+    if batch_invariant_enabled() and b > 1 and tokens.is_cuda:  # one sample per call, as above
+        if box is not None:
+            box.enabled = False
+        return torch.cat([proj_tokens_to_nchw(tokens[i:i + 1], module, res[i:i + 1], w2d, bias)
+                          for i in range(b)])
     w2d = module.weight.reshape(co, c) if w2d is None else w2d
     bias = getattr(module, "bias", None) if bias is None else bias
     if _layout_ok(tokens, w2d, b, h * w) and res.dtype == torch.float32:

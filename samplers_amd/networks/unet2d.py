@@ -125,11 +125,15 @@ def timestep_rows(model: nn.Module, timestep: Tensor | int, sample: Tensor) -> t
         t = timestep
     else:
         return None
-    params = model.__dict__.get("_t_params")
-    if params is None:  # the module tree is fixed after construction
+    slots = model.__dict__.get("_t_slots")
+    if slots is None:  # the module tree is fixed after construction; its Parameter objects are not
         blocks = [m for m in model.modules() if isinstance(m, ResnetBlock2D) and m.time_emb_proj is not None]
-        params = list(model.time_embedding.parameters()) + [p for b in blocks for p in b.time_emb_proj.parameters()]
-        model.__dict__["_t_params"] = params
+        mods = [model.time_embedding.linear_1, model.time_embedding.linear_2] + [b.time_emb_proj for b in blocks]
+        slots = model.__dict__["_t_slots"] = [(m, name) for m in mods for name in ("weight", "bias")
+                                              if m._parameters.get(name) is not None]
+    # read the live parameters (load_state_dict(..., assign=True) replaces the objects): the table
+    # key below then follows a replaced tensor as it follows an in-place update
+    params = [m._parameters[name] for m, name in slots]
     if t < 0 or not sample.is_cuda or any(p.requires_grad for p in params):
         return None
     key = (sample.device, sample.dtype, tuple((p.data_ptr(), p._version) for p in params))

@@ -445,9 +445,11 @@ class DPSSampler(PosteriorSampler, Generic[Condition_co]):
         ``micro_batch`` bounds how many samples share one prior forward+VJP;
         ``graph=True`` replays one hipGraph-captured step for every iteration
         (``samplers.graph``; Philox noise only) — same samples, no per-launch host work;
-        ``graph=None`` (default) does so where it pays (``graph_auto``: native plugins, Philox
-        noise, no callback / timer / micro-batching, a small batch and enough steps), else
-        runs eagerly; ``graph=False`` always runs eagerly;
+        ``graph=None`` (default) applies the automatic rule ``graph_auto`` (native plugins,
+        Philox noise, no callback / timer / micro-batching, a flat batch of at most
+        ``GRAPH_AUTO_MAX_BATCH`` and enough steps) — currently **off**: ``GRAPH_AUTO_MAX_BATCH``
+        is 0 because replay measured slower than eager at every batch, so
+        ``graph=None`` runs eagerly; ``graph=False`` always runs eagerly;
         ``callback(i, x)`` is called after guided iteration ``i`` with the flat sample (a view of
         the working buffer: copy it to keep it; not with ``graph=True``).
         """

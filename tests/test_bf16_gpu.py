@@ -106,6 +106,31 @@ def test_conv3x3_bf16_residual_and_repeatable(cuda):
     assert _rel(y1, ref) < 3e-3
 
 
+@pytest.mark.parametrize("n,c,co,h", [(2, 320, 320, 32), (1, 128, 128, 64), (3, 64, 64, 8), (1, 1280, 1280, 4)])
+def test_upsample_conv_bf16_fwd_vjp(cuda, n, c, co, h):
+    """conv(upsample_nearest2x(x)) fused (sp_conv3x3_bf16_up) and its VJP (full-resolution input VJP
+    + sp_pool2x2_bf16) against fp32 torch on the same bf16 operands."""
+    from samplers_amd.networks import bf16
+    from samplers_amd.networks.layers import Conv3x3
+
+    torch.manual_seed(9)
+    conv = Conv3x3(c, co).to(BF).requires_grad_(False)
+    x = torch.randn(n, c, h, h).to(BF)
+    dy = torch.randn(n, co, 2 * h, 2 * h).to(BF)
+    g = copy.deepcopy(conv).to(cuda)
+    xr = x.to(cuda).requires_grad_(True)
+    assert bf16.upsample_conv_supported(g, xr)
+    with torch.enable_grad():
+        y = bf16.upsample_conv3x3(g, xr)
+    (dx,) = torch.autograd.grad(y, xr, dy.to(cuda))
+    xf = x.float().requires_grad_(True)
+    with torch.enable_grad():
+        ref = F.conv2d(F.interpolate(xf, scale_factor=2.0, mode="nearest"), conv.weight.float(),
+                       conv.bias.float(), padding=1)
+    (rdx,) = torch.autograd.grad(ref, xf, dy.float())
+    assert _rel(y, ref) < 3e-3 and _rel(dx, rdx) < 5e-3, (_rel(y, ref), _rel(dx, rdx))
+
+
 @pytest.mark.parametrize("c1,c2,hw,act,bias", [(320, 0, 64, True, True), (640, 640, 16, True, False),
                                                (128, 0, 128, False, False), (1280, 1280, 8, True, True),
                                                (512, 0, 32, True, False)])

@@ -116,3 +116,23 @@ def test_default_is_eager_at_the_shipped_threshold(cuda):
     s = DPSSampler(net)
     s(_problem("identity", cuda, b=1), num_sampling_steps=12, gamma=0.5, seed=3)
     assert s.execution == ("graph" if dps_mod.GRAPH_AUTO_MAX_BATCH >= 1 else "eager")
+
+
+def test_timestep_table_follows_replaced_parameters(cuda):
+    """the table over t of time embeddings (host timesteps) is keyed on the live
+    parameters, so load_state_dict(..., assign=True) after a forward rebuilds it: the table path
+    then equals the per-step path (a device timestep, which never uses the table)."""
+    from samplers_amd.networks import unet2d
+
+    cfg = unet2d.UNet2DConfig(sample_size=16, block_out_channels=(32, 32), attention_levels=(),
+                              layers_per_block=1)
+    m = unet2d.build_unet(cfg, seed=0, device=cuda)
+    x = torch.randn(1, 3, 16, 16, device=cuda)
+    with torch.no_grad():
+        m(x, 321)  # builds the table
+        state = {k: v.clone() * 1.5 for k, v in m.state_dict().items()}
+        m.load_state_dict(state, assign=True)
+        m.requires_grad_(False)
+        table = m(x, 321)
+        per_step = m(x, torch.tensor([321], device=cuda))
+    assert torch.allclose(table, per_step, rtol=1e-5, atol=1e-5)

@@ -255,3 +255,22 @@ def test_sd_from_pretrained_never_fetches_and_rejects_unsupported(tmp_path):
     sch.write_text(json.dumps(dict(raw, prediction_type="v_prediction")))
     with pytest.raises(NotImplementedError, match="prediction_type"):
         LatentDiffusionNetwork.from_pretrained(str(tmp_path))
+
+
+def test_sd_from_pretrained_without_null_embeds_refuses_empty_prompts(tmp_path):
+    """real weights must not be conditioned on the synthetic null context — without
+    ``null_prompt_embeds`` an empty prompt raises; prompt embeddings still work; a wrongly shaped
+    null embedding is refused with a clear message (2-d (77, d) is accepted)."""
+    from samplers_amd.networks.latent import LatentDiffusionNetwork, StableDiffusionCondition
+
+    _, ucfg = _tiny_sd_dir(tmp_path, False)
+    net = LatentDiffusionNetwork.from_pretrained(str(tmp_path))
+    net.set_sampling_parameters(10, batch_size=1)
+    with pytest.raises(ValueError, match="null_prompt_embeds"):
+        net.set_condition(StableDiffusionCondition())
+    pe = torch.randn(1, ucfg.context_tokens, 24)
+    net.set_condition(StableDiffusionCondition(prompt=None, prompt_embeds=pe, guidance_scale=1.0))
+    with pytest.raises(ValueError, match="CLIP embedding"):
+        LatentDiffusionNetwork.from_pretrained(str(tmp_path), null_prompt_embeds=torch.randn(1, 5, 24))
+    ok = LatentDiffusionNetwork.from_pretrained(str(tmp_path), null_prompt_embeds=pe[0])
+    assert torch.equal(ok.null_prompt_embeds, pe)
