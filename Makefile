@@ -26,7 +26,7 @@ debug: $(DLIB)
 build/sp_wino.o build/debug/sp_wino.o: EXTRA := -fno-slp-vectorize
 # the attention kernels keep their accumulators in VGPRs: in the AGPR form the compiler copied
 # every score / output block between the two register files around each MFMA
-build/sp_attention.o build/debug/sp_attention.o build/sp_attention6.o build/debug/sp_attention6.o: EXTRA := -mllvm -amdgpu-mfma-vgpr-form=1
+build/sp_attention.o build/debug/sp_attention.o build/sp_attention6.o build/debug/sp_attention6.o build/sp_bf16.o build/debug/sp_bf16.o: EXTRA := -mllvm -amdgpu-mfma-vgpr-form=1
 
 build/%.o: samplers_amd/csrc/%.hip samplers_amd/csrc/sp_common.h include/samplers_hip.h
 	@mkdir -p build

@@ -599,6 +599,13 @@ int sp_attention_bf16_supported(int64_t batch, int32_t heads, int64_t n, int64_t
 int sp_attention_bf16_fwd(const void* q, const void* k, const void* v, int64_t batch, int32_t heads, int64_t n,
                           int64_t m, int32_t d, int32_t rsq, int32_t rskv, int32_t kv_shared, int32_t ro, float scale,
                           void* out, float* lse, sp_stream_t stream);
+/* its VJP on the bf16 MFMAs (P, dS never in HBM): delta = caller's [batch heads][n] fp32 scratch;
+ * dq rows of stride rdq; dk / dv (self-attention only) rows of stride rdkv, or NULL. */
+int sp_attention_bf16_bwd_supported(int64_t batch, int32_t heads, int64_t n, int64_t m, int32_t d);
+int sp_attention_bf16_bwd(const void* q, const void* k, const void* v, const void* out, const void* dout,
+                          const float* lse, int64_t batch, int32_t heads, int64_t n, int64_t m, int32_t d,
+                          int32_t rsq, int32_t rskv, int32_t kv_shared, int32_t ro, int32_t rdq, int32_t rdkv,
+                          float scale, float* delta, void* dq, void* dk, void* dv, sp_stream_t stream);
 
 #ifdef __cplusplus
 }

@@ -245,6 +245,11 @@ SIGNATURES = {
                                              _I64, ctypes.c_int32, ctypes.c_int32, _P, _P, _P, _P, _P, _P, _I64,
                                              _P]),
     "sp_attention_bf16_supported": (ctypes.c_int, [_I64, ctypes.c_int32, _I64, _I64, ctypes.c_int32]),
+    "sp_attention_bf16_bwd_supported": (ctypes.c_int, [_I64, ctypes.c_int32, _I64, _I64, ctypes.c_int32]),
+    "sp_attention_bf16_bwd": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _I64, ctypes.c_int32, _I64, _I64,
+                                             ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
+                                             ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, _F, _P, _P, _P, _P,
+                                             _P]),
     "sp_attention_bf16_fwd": (ctypes.c_int, [_P, _P, _P, _I64, ctypes.c_int32, _I64, _I64, ctypes.c_int32,
                                              ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, _F,
                                              _P, _P, _P]),

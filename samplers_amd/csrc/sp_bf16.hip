@@ -513,80 +513,105 @@ __global__ __launch_bounds__(64) void k_gnb_final_bwd(const float* __restrict__ 
     }
 }
 
-// forward apply: z = act(x sc + sh) over the concatenated channels (one 16-byte vector per
-// thread-iteration; the (n, c) coefficients stay in L2)
+// forward apply: z = act(x sc + sh) over the concatenated channels.  Grid (chunks, batch) as the
+// stats pass: a thread owns one 8-channel column of the sample, keeps its (n, c) coefficients in
+// registers and walks the chunk's pixels (the block reads rows of C channels contiguously).
 template <bool ACT>
 __global__ __launch_bounds__(kBlock) void k_gnb_apply(const u16* __restrict__ x1, const u16* __restrict__ x2, int c1,
-                                                      int c2, const float* __restrict__ co, int64_t n, int64_t hw,
+                                                      int c2, const float* __restrict__ co, int64_t hw, int chunk_px,
                                                       u16* __restrict__ z) {
-    const int c = c1 + c2, cv = c / 8;
-    const int64_t total = n * hw * cv, nc = n * c;
-    for (int64_t v = (int64_t)blockIdx.x * kBlock + threadIdx.x; v < total; v += (int64_t)gridDim.x * kBlock) {
-        const int j = static_cast<int>(v % cv);
-        const int64_t pix = v / cv, nn = pix / hw, p = pix - nn * hw;
-        float f[8];
-        unpack8(gnb_ld(x1, x2, c1, c2, nn, hw, p, j), f);
-        const float* sc = co + nn * c + 8 * j;
-        const float* sh = co + nc + nn * c + 8 * j;
+    const int c = c1 + c2, cv = c / 8, nn = blockIdx.y, tid = threadIdx.x;
+    const int64_t nc = (int64_t)gridDim.y * c;
+    const int64_t p0 = (int64_t)blockIdx.x * chunk_px, p1 = std::min<int64_t>(hw, p0 + chunk_px);
+    for (int jb = 0; jb < cv; jb += kBlock) {
+        const int colw = std::min(cv - jb, kBlock), rows = kBlock / colw;
+        const int j = jb + tid % colw, row = tid / colw;
+        if (row >= rows) continue;
+        const float* sc = co + (int64_t)nn * c + 8 * j;
+        const float* sh = co + nc + (int64_t)nn * c + 8 * j;
         const float4 a0 = *reinterpret_cast<const float4*>(sc), a1 = *reinterpret_cast<const float4*>(sc + 4);
         const float4 b0 = *reinterpret_cast<const float4*>(sh), b1 = *reinterpret_cast<const float4*>(sh + 4);
         const float sa[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
         const float sb[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+        for (int64_t p = p0 + row; p < p1; p += rows) {
+            float f[8];
+            unpack8(gnb_ld(x1, x2, c1, c2, nn, hw, p, j), f);
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-            const float yv = fmaf(f[e], sa[e], sb[e]);
-            f[e] = ACT ? silu_f(yv) : yv;
+            for (int e = 0; e < 8; ++e) {
+                const float yv = fmaf(f[e], sa[e], sb[e]);
+                f[e] = ACT ? silu_f(yv) : yv;
+            }
+            *reinterpret_cast<bq_u4*>(z + ((int64_t)nn * hw + p) * c + 8 * j) = pack8(f);
         }
-        *reinterpret_cast<bq_u4*>(z + pix * c + 8 * j) = pack8(f);
     }
 }
 
-// VJP apply: dx = A dy' + B x + D (+ add1 / add2 / add1b), written to the parts' layouts
+__device__ __forceinline__ void ld8f(const float* p, float (&f)[8]) {
+    const float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
+    f[0] = a.x, f[1] = a.y, f[2] = a.z, f[3] = a.w, f[4] = b.x, f[5] = b.y, f[6] = b.z, f[7] = b.w;
+}
+
+// VJP apply: dx = A dy' + B x + D (+ add1 / add2 / add1b), written to the parts' layouts; grid
+// and column ownership as k_gnb_apply (the five (n, c) coefficient rows held in registers)
 template <bool ACT>
 __global__ __launch_bounds__(kBlock) void k_gnb_bwd_apply(const u16* __restrict__ dz, const u16* __restrict__ x1,
                                                           const u16* __restrict__ x2, int c1, int c2,
                                                           const float* __restrict__ co, const float* __restrict__ co2,
-                                                          int64_t n, int64_t hw, u16* __restrict__ dx1,
+                                                          int64_t hw, int chunk_px, u16* __restrict__ dx1,
                                                           u16* __restrict__ dx2, const u16* __restrict__ add1,
                                                           const u16* __restrict__ add2,
                                                           const u16* __restrict__ add1b) {
-    const int c = c1 + c2, cv = c / 8;
-    const int64_t total = n * hw * cv, nc = n * c;
-    for (int64_t v = (int64_t)blockIdx.x * kBlock + threadIdx.x; v < total; v += (int64_t)gridDim.x * kBlock) {
-        const int j = static_cast<int>(v % cv);
-        const int64_t pix = v / cv, nn = pix / hw, p = pix - nn * hw;
-        float f[8], d[8];
-        unpack8(gnb_ld(x1, x2, c1, c2, nn, hw, p, j), f);
-        unpack8(*reinterpret_cast<const bq_u4*>(dz + pix * c + 8 * j), d);
-        const int64_t ci = nn * c + 8 * j;
-        float o[8];
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-            float dd = d[e];
-            if constexpr (ACT) {
-                const float yv = fmaf(f[e], co[ci + e], co[nc + ci + e]);
-                const float sg = __builtin_amdgcn_rcpf(1.f + __expf(-yv));
-                dd *= sg * (1.f + yv * (1.f - sg));
-            }
-            o[e] = fmaf(co2[ci + e], dd, fmaf(co2[nc + ci + e], f[e], co2[2 * nc + ci + e]));
+    const int c = c1 + c2, cv = c / 8, nn = blockIdx.y, tid = threadIdx.x;
+    const int64_t nc = (int64_t)gridDim.y * c;
+    const int64_t p0 = (int64_t)blockIdx.x * chunk_px, p1 = std::min<int64_t>(hw, p0 + chunk_px);
+    for (int jb = 0; jb < cv; jb += kBlock) {
+        const int colw = std::min(cv - jb, kBlock), rows = kBlock / colw;
+        const int j = jb + tid % colw, row = tid / colw;
+        if (row >= rows) continue;
+        const int64_t ci = (int64_t)nn * c + 8 * j;
+        float ka[8], kb[8], kd[8], ksc[8], ksh[8];
+        ld8f(co2 + ci, ka);
+        ld8f(co2 + nc + ci, kb);
+        ld8f(co2 + 2 * nc + ci, kd);
+        if constexpr (ACT) {
+            ld8f(co + ci, ksc);
+            ld8f(co + nc + ci, ksh);
         }
         const int ch = 8 * j;
         const bool first = ch < c1;
-        const int64_t off = first ? (nn * hw + p) * c1 + ch : (nn * hw + p) * c2 + ch - c1;
-        const u16* a = first ? add1 : add2;
-        if (a) {
-            float t[8];
-            unpack8(*reinterpret_cast<const bq_u4*>(a + off), t);
+        const int cp = first ? c1 : c2, chp = first ? ch : ch - c1;
+        u16* __restrict__ dst = first ? dx1 : dx2;
+        const u16* __restrict__ a = first ? add1 : add2;
+        const u16* __restrict__ ab = first ? add1b : nullptr;
+        for (int64_t p = p0 + row; p < p1; p += rows) {
+            float f[8], d[8], o[8];
+            const int64_t off = ((int64_t)nn * hw + p) * cp + chp;
+            unpack8(*reinterpret_cast<const bq_u4*>((first ? x1 : x2) + off), f);
+            unpack8(*reinterpret_cast<const bq_u4*>(dz + ((int64_t)nn * hw + p) * c + ch), d);
 #pragma unroll
-            for (int e = 0; e < 8; ++e) o[e] += t[e];
-        }
-        if (first && add1b) {
-            float t[8];
-            unpack8(*reinterpret_cast<const bq_u4*>(add1b + off), t);
+            for (int e = 0; e < 8; ++e) {
+                float dd = d[e];
+                if constexpr (ACT) {
+                    const float yv = fmaf(f[e], ksc[e], ksh[e]);
+                    const float sg = __builtin_amdgcn_rcpf(1.f + __expf(-yv));
+                    dd *= sg * (1.f + yv * (1.f - sg));
+                }
+                o[e] = fmaf(ka[e], dd, fmaf(kb[e], f[e], kd[e]));
+            }
+            if (a) {
+                float t[8];
+                unpack8(*reinterpret_cast<const bq_u4*>(a + off), t);
 #pragma unroll
-            for (int e = 0; e < 8; ++e) o[e] += t[e];
+                for (int e = 0; e < 8; ++e) o[e] += t[e];
+            }
+            if (ab) {
+                float t[8];
+                unpack8(*reinterpret_cast<const bq_u4*>(ab + off), t);
+#pragma unroll
+                for (int e = 0; e < 8; ++e) o[e] += t[e];
+            }
+            *reinterpret_cast<bq_u4*>(dst + off) = pack8(o);
         }
-        *reinterpret_cast<bq_u4*>((first ? dx1 : dx2) + off) = pack8(o);
     }
 }
 
@@ -782,6 +807,313 @@ static void attnb_launch(const u16* q, const u16* k, const u16* v, int64_t batch
            rskv, kv_shared, ro, scale * AB_LOG2E, out, lse);
 }
 
+// ---------------------------------------------------------------------------------------------
+// Attention VJP on bf16 MFMAs (FlashAttention-2 recurrence, P never in HBM): delta = rowsum(dO o O),
+// then
+//   k_attnb_dq   per wave 32 queries: S^T = K Q^T, dP^T = V dO^T (Q^T, dO^T in registers), dS^T =
+//                P^T (dP^T - delta), dQ^T += K^T dS^T (K^T staged in LDS in the C layout's key order)
+//   k_attnb_dkv  per wave 32 keys: S = Q K^T, dP = dO V^T (K^T, V^T in registers), dS = P (dP -
+//                delta), dV^T += dO^T P and dK^T += Q^T dS (Q^T, dO^T staged in that order)
+// P and dS are rounded to bf16 as MFMA operands (as the forward's P); fp32 accumulation.
+// ---------------------------------------------------------------------------------------------
+template <int D>
+__global__ __launch_bounds__(kBlock) void k_attnb_delta(const u16* __restrict__ out, const u16* __restrict__ dout,
+                                                        int n, int heads, int ro, int64_t rows,
+                                                        float* __restrict__ delta) {
+    const int64_t rr = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (rr >= rows) return;
+    const int bh = static_cast<int>(rr / n), i = static_cast<int>(rr - (int64_t)bh * n);
+    const int b = bh / heads, hd = bh - b * heads;
+    const int64_t off = ((int64_t)b * n + i) * ro + hd * D;
+    float acc = 0.f;
+#pragma unroll
+    for (int j = 0; j < D / 8; ++j) {
+        float a[8], c[8];
+        unpack8(*reinterpret_cast<const bq_u4*>(out + off + 8 * j), a);
+        unpack8(*reinterpret_cast<const bq_u4*>(dout + off + 8 * j), c);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc = fmaf(a[e], c[e], acc);
+    }
+    delta[rr] = acc;
+}
+
+// a stage of SB rows (row pairs 2p, 2p + 1 x 8 d per unit) into registers; rows >= limit zero
+template <int D>
+__device__ __forceinline__ void ab_ld_pairs(const u16* __restrict__ src, int64_t rs, int base, int limit,
+                                            bq_u4 (&st)[AbGeo<D>::NVU][2]) {
+    using G = AbGeo<D>;
+#pragma unroll
+    for (int j = 0; j < G::NVU; ++j) {
+        const int u = threadIdx.x + j * kBlock;
+        if (u < G::SB / 2 * (D / 8)) {
+            const int p = u / (D / 8), d0 = 8 * (u - p * (D / 8));
+            const int r0 = base + 2 * p;
+            st[j][0] = r0 < limit ? *reinterpret_cast<const bq_u4*>(src + (int64_t)r0 * rs + d0) : bq_u4{0u, 0u, 0u, 0u};
+            st[j][1] = r0 + 1 < limit ? *reinterpret_cast<const bq_u4*>(src + (int64_t)(r0 + 1) * rs + d0)
+                                      : bq_u4{0u, 0u, 0u, 0u};
+        }
+    }
+}
+
+// natural image [SB][KROW]
+template <int D>
+__device__ __forceinline__ void ab_st_nat(u16* img, const bq_u4 (&st)[AbGeo<D>::NVU][2]) {
+    using G = AbGeo<D>;
+#pragma unroll
+    for (int j = 0; j < G::NVU; ++j) {
+        const int u = threadIdx.x + j * kBlock;
+        if (u < G::SB / 2 * (D / 8)) {
+            const int p = u / (D / 8), d0 = 8 * (u - p * (D / 8));
+            *reinterpret_cast<bq_u4*>(img + (2 * p) * G::KROW + d0) = st[j][0];
+            *reinterpret_cast<bq_u4*>(img + (2 * p + 1) * G::KROW + d0) = st[j][1];
+        }
+    }
+}
+
+// transposed image [32 DT][VROW]: row d, the stage's rows at their C-layout positions
+template <int D>
+__device__ __forceinline__ void ab_st_tr(u16* img, const bq_u4 (&st)[AbGeo<D>::NVU][2]) {
+    using G = AbGeo<D>;
+#pragma unroll
+    for (int j = 0; j < G::NVU; ++j) {
+        const int u = threadIdx.x + j * kBlock;
+        if (u < G::SB / 2 * (D / 8)) {
+            const int p = u / (D / 8), d0 = 8 * (u - p * (D / 8));
+            const int key = 2 * p, pos = (key & ~15) | ab_pos(key & 15);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const unsigned a = st[j][0][e], c = st[j][1][e];
+                *reinterpret_cast<unsigned*>(img + (d0 + 2 * e) * G::VROW + pos) = (a & 0xffffu) | (c << 16);
+                *reinterpret_cast<unsigned*>(img + (d0 + 2 * e + 1) * G::VROW + pos) = (a >> 16) | (c & 0xffff0000u);
+            }
+        }
+    }
+}
+
+// the B-operand fragments of 32 rows (lane row r) of a row-major [rows][D] operand, d padded to 16
+template <int D>
+__device__ __forceinline__ void ab_rowfrags(const u16* __restrict__ src, int64_t rs, int row, int limit, int hh,
+                                            bq_u4 (&f)[AbGeo<D>::DK]) {
+#pragma unroll
+    for (int s = 0; s < AbGeo<D>::DK; ++s) {
+        const int d0 = 16 * s + 8 * hh;
+        f[s] = (d0 + 8 <= D && row < limit) ? *reinterpret_cast<const bq_u4*>(src + (int64_t)row * rs + d0)
+                                            : bq_u4{0u, 0u, 0u, 0u};
+    }
+}
+
+template <int D>
+__device__ __forceinline__ void ab_zero_pad(u16* img) {
+    using G = AbGeo<D>;
+    if constexpr (G::DKP > D) {
+        for (int i = threadIdx.x; i < G::SB; i += kBlock)
+#pragma unroll
+            for (int cc = D; cc < G::DKP; cc += 2) *reinterpret_cast<unsigned*>(img + i * G::KROW + cc) = 0u;
+    }
+}
+
+// C-layout rows d of 32 columns -> bf16 row-major output: lane's column `row`, 4 d per store
+template <int D>
+__device__ __forceinline__ void ab_store_rows(u16* __restrict__ dst, int64_t rs, int row, int limit, int hh,
+                                              const bq_f16 (&acc)[AbGeo<D>::DT], float mul) {
+    if (row >= limit) return;
+    u16* o = dst + (int64_t)row * rs;
+#pragma unroll
+    for (int dt = 0; dt < AbGeo<D>::DT; ++dt)
+#pragma unroll
+        for (int g4 = 0; g4 < 4; ++g4) {
+            const int d0 = 32 * dt + 8 * g4 + 4 * hh;
+            if (d0 + 4 <= D)
+                *reinterpret_cast<bq_u2*>(o + d0) = bq_u2{pk2(acc[dt][4 * g4] * mul, acc[dt][4 * g4 + 1] * mul),
+                                                          pk2(acc[dt][4 * g4 + 2] * mul, acc[dt][4 * g4 + 3] * mul)};
+        }
+}
+
+template <int D>
+__global__ __launch_bounds__(kBlock) void k_attnb_dq(const u16* __restrict__ q, const u16* __restrict__ k,
+                                                     const u16* __restrict__ v, const u16* __restrict__ dout,
+                                                     const float* __restrict__ lse, const float* __restrict__ delta,
+                                                     int n, int m, int heads, int rsq, int rskv, int kv_shared,
+                                                     int ro, int rdq, float sl2, float scale,
+                                                     u16* __restrict__ dq) {
+    using G = AbGeo<D>;
+    __shared__ __attribute__((aligned(16))) u16 Kn[G::SB * G::KROW];
+    __shared__ __attribute__((aligned(16))) u16 Vn[G::SB * G::KROW];
+    __shared__ __attribute__((aligned(16))) u16 Kt[G::DT * 32 * G::VROW];
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, r = lane & 31, hh = lane >> 5;
+    const int bh = blockIdx.y, b = bh / heads, hd = bh - b * heads;
+    const int qq = blockIdx.x * AB_WB + wv * AB_QW + r;
+    const int64_t kvb = (kv_shared ? 0 : (int64_t)b * m * rskv) + hd * D;
+    ab_zero_pad<D>(Kn);
+    ab_zero_pad<D>(Vn);
+    bq_u4 qf[G::DK], of[G::DK];
+    ab_rowfrags<D>(q + (int64_t)b * n * rsq + hd * D, rsq, qq, n, hh, qf);
+    ab_rowfrags<D>(dout + (int64_t)b * n * ro + hd * D, ro, qq, n, hh, of);
+    const float ll = qq < n ? lse[(int64_t)bh * n + qq] * AB_LOG2E : 0.f;
+    const float dl = qq < n ? delta[(int64_t)bh * n + qq] : 0.f;
+    bq_f16 acc[G::DT];
+#pragma unroll
+    for (int dt = 0; dt < G::DT; ++dt) acc[dt] = bq_f16{};
+    const int nst = (m + G::SB - 1) / G::SB;
+    bq_u4 ks[G::NVU][2], vs[G::NVU][2];
+    ab_ld_pairs<D>(k + kvb, rskv, 0, m, ks);
+    ab_ld_pairs<D>(v + kvb, rskv, 0, m, vs);
+    for (int si = 0; si < nst; ++si) {
+        __syncthreads();
+        ab_st_nat<D>(Kn, ks);
+        ab_st_tr<D>(Kt, ks);
+        ab_st_nat<D>(Vn, vs);
+        __syncthreads();
+        if (si + 1 < nst) {
+            ab_ld_pairs<D>(k + kvb, rskv, (si + 1) * G::SB, m, ks);
+            ab_ld_pairs<D>(v + kvb, rskv, (si + 1) * G::SB, m, vs);
+        }
+        const int kbase = si * G::SB;
+#pragma unroll
+        for (int kb32 = 0; kb32 < G::SB / 32; ++kb32) {
+            if (kbase + kb32 * 32 >= m) break;
+            bq_f16 sv = bq_f16{}, dp = bq_f16{};
+#pragma unroll
+            for (int s2 = 0; s2 < G::DK; ++s2) {
+                const int o = (kb32 * 32 + r) * G::KROW + 16 * s2 + 8 * hh;
+                sv = bq_mfma(*reinterpret_cast<const bq_u4*>(Kn + o), qf[s2], sv);
+                dp = bq_mfma(*reinterpret_cast<const bq_u4*>(Vn + o), of[s2], dp);
+            }
+            float ds[16];
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                const int key = kbase + kb32 * 32 + (i & 3) + 8 * (i >> 2) + 4 * hh;
+                const float p = key < m ? __builtin_amdgcn_exp2f(fmaf(sv[i], sl2, -ll)) : 0.f;
+                ds[i] = p * (dp[i] - dl);
+            }
+#pragma unroll
+            for (int kk = 0; kk < 2; ++kk) {
+                const bq_u4 pf = {pk2(ds[8 * kk], ds[8 * kk + 1]), pk2(ds[8 * kk + 2], ds[8 * kk + 3]),
+                                  pk2(ds[8 * kk + 4], ds[8 * kk + 5]), pk2(ds[8 * kk + 6], ds[8 * kk + 7])};
+#pragma unroll
+                for (int dt = 0; dt < G::DT; ++dt) {
+                    const bq_u4 a = *reinterpret_cast<const bq_u4*>(Kt + (dt * 32 + r) * G::VROW + kb32 * 32 + kk * 16 + 8 * hh);
+                    acc[dt] = bq_mfma(a, pf, acc[dt]);
+                }
+            }
+        }
+    }
+    ab_store_rows<D>(dq + (int64_t)b * n * rdq + hd * D, rdq, qq, n, hh, acc, scale);
+}
+
+template <int D>
+__global__ __launch_bounds__(kBlock) void k_attnb_dkv(const u16* __restrict__ q, const u16* __restrict__ k,
+                                                      const u16* __restrict__ v, const u16* __restrict__ dout,
+                                                      const float* __restrict__ lse, const float* __restrict__ delta,
+                                                      int n, int heads, int rs, int ro, int rdkv, float sl2,
+                                                      float scale, u16* __restrict__ dk, u16* __restrict__ dv) {
+    using G = AbGeo<D>;
+    __shared__ __attribute__((aligned(16))) u16 Qn[G::SB * G::KROW];
+    __shared__ __attribute__((aligned(16))) u16 On[G::SB * G::KROW];
+    __shared__ __attribute__((aligned(16))) u16 Qt[G::DT * 32 * G::VROW];
+    __shared__ __attribute__((aligned(16))) u16 Ot[G::DT * 32 * G::VROW];
+    __shared__ __attribute__((aligned(16))) float Ls[G::SB], Dl[G::SB];
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, r = lane & 31, hh = lane >> 5;
+    const int bh = blockIdx.y, b = bh / heads, hd = bh - b * heads;
+    const int kk_ = blockIdx.x * AB_WB + wv * AB_QW + r;  // this lane's key
+    const int64_t base = (int64_t)b * n * rs + hd * D, obase = (int64_t)b * n * ro + hd * D;
+    ab_zero_pad<D>(Qn);
+    ab_zero_pad<D>(On);
+    bq_u4 kf[G::DK], vf[G::DK];
+    ab_rowfrags<D>(k + base, rs, kk_, n, hh, kf);
+    ab_rowfrags<D>(v + base, rs, kk_, n, hh, vf);
+    bq_f16 ak[G::DT], av[G::DT];
+#pragma unroll
+    for (int dt = 0; dt < G::DT; ++dt) ak[dt] = bq_f16{}, av[dt] = bq_f16{};
+    const int nst = (n + G::SB - 1) / G::SB;
+    bq_u4 qs[G::NVU][2], os[G::NVU][2];
+    float lv = 0.f;
+    auto ld = [&](int si) {
+        ab_ld_pairs<D>(q + base, rs, si * G::SB, n, qs);
+        ab_ld_pairs<D>(dout + obase, ro, si * G::SB, n, os);
+        const int qi = si * G::SB + (tid & (G::SB - 1));
+        if (tid < 2 * G::SB) {
+            if (tid < G::SB)
+                lv = qi < n ? lse[(int64_t)bh * n + qi] * AB_LOG2E : INFINITY;
+            else
+                lv = qi < n ? delta[(int64_t)bh * n + qi] : 0.f;
+        }
+    };
+    ld(0);
+    for (int si = 0; si < nst; ++si) {
+        __syncthreads();
+        ab_st_nat<D>(Qn, qs);
+        ab_st_tr<D>(Qt, qs);
+        ab_st_nat<D>(On, os);
+        ab_st_tr<D>(Ot, os);
+        if (tid < G::SB)
+            Ls[tid] = lv;
+        else if (tid < 2 * G::SB)
+            Dl[tid - G::SB] = lv;
+        __syncthreads();
+        if (si + 1 < nst) ld(si + 1);
+#pragma unroll
+        for (int ib32 = 0; ib32 < G::SB / 32; ++ib32) {
+            if (si * G::SB + ib32 * 32 >= n) break;
+            bq_f16 sv = bq_f16{}, dp = bq_f16{};
+#pragma unroll
+            for (int s2 = 0; s2 < G::DK; ++s2) {
+                const int o = (ib32 * 32 + r) * G::KROW + 16 * s2 + 8 * hh;
+                sv = bq_mfma(*reinterpret_cast<const bq_u4*>(Qn + o), kf[s2], sv);
+                dp = bq_mfma(*reinterpret_cast<const bq_u4*>(On + o), vf[s2], dp);
+            }
+            float p[16], ds[16];
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const int q0 = ib32 * 32 + 8 * g + 4 * hh;
+                const float4 l4 = *reinterpret_cast<const float4*>(Ls + q0);
+                const float4 d4 = *reinterpret_cast<const float4*>(Dl + q0);
+                const float la[4] = {l4.x, l4.y, l4.z, l4.w}, da[4] = {d4.x, d4.y, d4.z, d4.w};
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const int i = 4 * g + e;
+                    p[i] = __builtin_amdgcn_exp2f(fmaf(sv[i], sl2, -la[e]));
+                    ds[i] = p[i] * (dp[i] - da[e]);
+                }
+            }
+#pragma unroll
+            for (int kk = 0; kk < 2; ++kk) {
+                const bq_u4 pp = {pk2(p[8 * kk], p[8 * kk + 1]), pk2(p[8 * kk + 2], p[8 * kk + 3]),
+                                  pk2(p[8 * kk + 4], p[8 * kk + 5]), pk2(p[8 * kk + 6], p[8 * kk + 7])};
+                const bq_u4 pd = {pk2(ds[8 * kk], ds[8 * kk + 1]), pk2(ds[8 * kk + 2], ds[8 * kk + 3]),
+                                  pk2(ds[8 * kk + 4], ds[8 * kk + 5]), pk2(ds[8 * kk + 6], ds[8 * kk + 7])};
+#pragma unroll
+                for (int dt = 0; dt < G::DT; ++dt) {
+                    const int o = (dt * 32 + r) * G::VROW + ib32 * 32 + kk * 16 + 8 * hh;
+                    av[dt] = bq_mfma(*reinterpret_cast<const bq_u4*>(Ot + o), pp, av[dt]);
+                    ak[dt] = bq_mfma(*reinterpret_cast<const bq_u4*>(Qt + o), pd, ak[dt]);
+                }
+            }
+        }
+    }
+    ab_store_rows<D>(dk + (int64_t)b * n * rdkv + hd * D, rdkv, kk_, n, hh, ak, scale);
+    ab_store_rows<D>(dv + (int64_t)b * n * rdkv + hd * D, rdkv, kk_, n, hh, av, 1.f);
+}
+
+template <int D>
+static void attnb_bwd_launch(const u16* q, const u16* k, const u16* v, const u16* out, const u16* dout,
+                             const float* lse, int64_t batch, int heads, int64_t n, int64_t m, int rsq, int rskv,
+                             int kv_shared, int ro, int rdq, int rdkv, float scale, float* delta, u16* dq, u16* dk,
+                             u16* dv, hipStream_t s) {
+    const int64_t rows = batch * heads * n;
+    launch(0, k_attnb_delta<D>, dim3(static_cast<unsigned>((rows + kBlock - 1) / kBlock)), dim3(kBlock), s, out, dout,
+           static_cast<int>(n), heads, ro, rows, delta);
+    const float sl2 = scale * AB_LOG2E;
+    if (dq)
+        launch(0, k_attnb_dq<D>, dim3(static_cast<unsigned>((n + AB_WB - 1) / AB_WB), static_cast<unsigned>(batch * heads)),
+               dim3(kBlock), s, q, k, v, dout, lse, static_cast<const float*>(delta), static_cast<int>(n),
+               static_cast<int>(m), heads, rsq, rskv, kv_shared, ro, rdq, sl2, scale, dq);
+    if (dk)
+        launch(0, k_attnb_dkv<D>, dim3(static_cast<unsigned>((n + AB_WB - 1) / AB_WB), static_cast<unsigned>(batch * heads)),
+               dim3(kBlock), s, q, k, v, dout, lse, static_cast<const float*>(delta), static_cast<int>(n), heads, rsq,
+               ro, rdkv, sl2, scale, dk, dv);
+}
+
 }  // namespace sp
 
 using namespace sp;
@@ -886,13 +1218,13 @@ int sp_groupnorm_bf16_fwd(const void* x1, const void* x2, int32_t c1, int32_t c2
            static_cast<const float*>(nullptr), hw, g.chunk_px, part);
     launch(0, k_gnb_final_fwd, dim3(groups, static_cast<unsigned>(n)), dim3(64), s, a, b, c1, c2, chan_bias,
            static_cast<const float*>(part), g.chunks, hw, groups, eps, gamma, beta, stats, co);
-    const unsigned blocks = stream_blocks(n * hw * (c / 8));
+    const dim3 grid(g.chunks, static_cast<unsigned>(n));
     if (act)
-        launch(0, k_gnb_apply<true>, dim3(blocks), dim3(kBlock), s, a, b, c1, c2, static_cast<const float*>(co), n, hw,
+        launch(0, k_gnb_apply<true>, grid, dim3(kBlock), s, a, b, c1, c2, static_cast<const float*>(co), hw, g.chunk_px,
                static_cast<u16*>(z));
     else
-        launch(0, k_gnb_apply<false>, dim3(blocks), dim3(kBlock), s, a, b, c1, c2, static_cast<const float*>(co), n,
-               hw, static_cast<u16*>(z));
+        launch(0, k_gnb_apply<false>, grid, dim3(kBlock), s, a, b, c1, c2, static_cast<const float*>(co), hw,
+               g.chunk_px, static_cast<u16*>(z));
     return check_launch("sp_groupnorm_bf16_fwd");
 }
 
@@ -927,14 +1259,14 @@ int sp_groupnorm_bf16_bwd(const void* dz, const void* x1, const void* x2, int32_
                chan_bias, d, static_cast<const float*>(co), gamma, hw, g.chunk_px, part);
     launch(0, k_gnb_final_bwd, dim3(groups, static_cast<unsigned>(n)), dim3(64), s, static_cast<const float*>(part),
            g.chunks, hw, c, groups, stats, gamma, static_cast<const float*>(co), co2);
-    const unsigned blocks = stream_blocks(n * hw * (c / 8));
+    const dim3 grid(g.chunks, static_cast<unsigned>(n));
     if (act)
-        launch(0, k_gnb_bwd_apply<true>, dim3(blocks), dim3(kBlock), s, d, a, b, c1, c2, static_cast<const float*>(co),
-               static_cast<const float*>(co2), n, hw, static_cast<u16*>(dx1), static_cast<u16*>(dx2),
+        launch(0, k_gnb_bwd_apply<true>, grid, dim3(kBlock), s, d, a, b, c1, c2, static_cast<const float*>(co),
+               static_cast<const float*>(co2), hw, g.chunk_px, static_cast<u16*>(dx1), static_cast<u16*>(dx2),
                static_cast<const u16*>(add1), static_cast<const u16*>(add2), static_cast<const u16*>(add1b));
     else
-        launch(0, k_gnb_bwd_apply<false>, dim3(blocks), dim3(kBlock), s, d, a, b, c1, c2, static_cast<const float*>(co),
-               static_cast<const float*>(co2), n, hw, static_cast<u16*>(dx1), static_cast<u16*>(dx2),
+        launch(0, k_gnb_bwd_apply<false>, grid, dim3(kBlock), s, d, a, b, c1, c2, static_cast<const float*>(co),
+               static_cast<const float*>(co2), hw, g.chunk_px, static_cast<u16*>(dx1), static_cast<u16*>(dx2),
                static_cast<const u16*>(add1), static_cast<const u16*>(add2), static_cast<const u16*>(add1b));
     return check_launch("sp_groupnorm_bf16_bwd");
 }
@@ -968,6 +1300,35 @@ int sp_attention_bf16_fwd(const void* q, const void* k, const void* v, int64_t b
         default: attnb_launch<160>(qq, kk, vv, batch, heads, n, m, rsq, rskv, kv_shared, ro, scale, oo, lse, s); break;
     }
     return check_launch("sp_attention_bf16_fwd");
+}
+
+// VJP of sp_attention_bf16_fwd given its output and lse: delta [batch heads][n] fp32 (caller's
+// scratch); dq rows of stride rdq ([batch][n][rdq]); dk / dv (self-attention only: m == n, one K/V
+// per sample, rsq == rskv) rows of stride rdkv, or NULL (cross-attention: the context is constant).
+int sp_attention_bf16_bwd_supported(int64_t batch, int32_t heads, int64_t n, int64_t m, int32_t d) {
+    return sp_attention_bf16_supported(batch, heads, n, m, d) && (d == 40 || d == 64 || d == 80);
+}
+
+int sp_attention_bf16_bwd(const void* q, const void* k, const void* v, const void* out, const void* dout,
+                          const float* lse, int64_t batch, int32_t heads, int64_t n, int64_t m, int32_t d,
+                          int32_t rsq, int32_t rskv, int32_t kv_shared, int32_t ro, int32_t rdq, int32_t rdkv,
+                          float scale, float* delta, void* dq, void* dk, void* dv, sp_stream_t stream) {
+    if (!q || !k || !v || !out || !dout || !lse || !delta || !sp_attention_bf16_bwd_supported(batch, heads, n, m, d))
+        return SP_EINVAL;
+    if (rsq < heads * d || rskv < heads * d || ro < heads * d || rsq % 8 || rskv % 8 || ro % 8 || rdq % 4 || rdkv % 4)
+        return SP_EINVAL;
+    if ((dk || dv) && (!dk || !dv || m != n || kv_shared || rsq != rskv || rdkv < heads * d)) return SP_EINVAL;
+    if (dq && rdq < heads * d) return SP_EINVAL;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const u16 *qq = static_cast<const u16*>(q), *kk = static_cast<const u16*>(k), *vv = static_cast<const u16*>(v);
+    const u16 *oo = static_cast<const u16*>(out), *dd = static_cast<const u16*>(dout);
+    u16 *a = static_cast<u16*>(dq), *bb = static_cast<u16*>(dk), *c = static_cast<u16*>(dv);
+    switch (d) {
+        case 40: attnb_bwd_launch<40>(qq, kk, vv, oo, dd, lse, batch, heads, n, m, rsq, rskv, kv_shared, ro, rdq, rdkv, scale, delta, a, bb, c, s); break;
+        case 64: attnb_bwd_launch<64>(qq, kk, vv, oo, dd, lse, batch, heads, n, m, rsq, rskv, kv_shared, ro, rdq, rdkv, scale, delta, a, bb, c, s); break;
+        default: attnb_bwd_launch<80>(qq, kk, vv, oo, dd, lse, batch, heads, n, m, rsq, rskv, kv_shared, ro, rdq, rdkv, scale, delta, a, bb, c, s); break;
+    }
+    return check_launch("sp_attention_bf16_bwd");
 }
 
 }  // extern "C"

@@ -12,8 +12,9 @@ stable_diffusion.py:90-101``, ``ddpm.py:23-34``) and its PSLD driver runs SD 1.5
   accumulation, bias and residual in the epilogue);
 * GroupNorm(+time-embedding bias)(+SiLU) and its input VJP on ``sp_groupnorm_bf16_fwd/bwd``
   (fp32 statistics);
-* the SD UNet's self- and cross-attention forward on ``sp_attention_bf16_fwd`` (flash-style,
-  scores never in HBM); its VJP runs the exact-fp32 fused kernels on the inputs widened to fp32;
+* the SD UNet's self- and cross-attention on ``sp_attention_bf16_fwd`` / ``_bwd`` (flash-style,
+  scores never in HBM, either direction; head dim 160 — the 16² / 8² levels — takes the VJP on
+  the exact-fp32 fused kernels with the operands widened);
 * 1x1 convolutions and linears are bf16 GEMMs (hipBLASLt through ``F.linear``); LayerNorm,
   GEGLU and the d = 512 single-head attention (score matrix kept) are torch bf16 ops.
 
@@ -359,6 +360,16 @@ class _SelfAttnBf16Fn(torch.autograd.Function):
         c = c3 // 3
         heads = ctx.heads
         d = c // heads
+        if lib.sp_attention_bf16_bwd_supported(b, heads, n, n, d):  # the bf16 VJP kernels
+            do = dout.to(BF16).contiguous()
+            dqkv = torch.empty_like(qkv)
+            delta = torch.empty(b * heads, n, device=qkv.device, dtype=torch.float32)
+            base, dbase = _p(qkv, cl=False), _p(dqkv, cl=False)
+            _hip.check(lib.sp_attention_bf16_bwd(base, base + 2 * c, base + 4 * c, _p(out, cl=False),
+                                                 _p(do, cl=False), lse.data_ptr(), b, heads, n, n, d, c3, c3, 0, c,
+                                                 c3, c3, 1.0 / math.sqrt(d), delta.data_ptr(), dbase, dbase + 2 * c,
+                                                 dbase + 4 * c, _hip.stream_of(do)), "sp_attention_bf16_bwd")
+            return dqkv, None
         q32, o32, do32 = qkv.float(), out.float(), dout.float().contiguous()
         dqkv = torch.empty_like(q32)
         delta = torch.empty(b * heads, n, device=qkv.device, dtype=torch.float32)
@@ -393,6 +404,16 @@ class _CrossAttnBf16Fn(torch.autograd.Function):
         b, n, c = q.shape
         bc, m, _ = k.shape
         heads = ctx.heads
+        if lib.sp_attention_bf16_bwd_supported(b, heads, n, m, c // heads):  # the bf16 VJP kernels
+            do = dout.to(BF16).contiguous()
+            dq = torch.empty_like(q)
+            delta = torch.empty(b * heads, n, device=q.device, dtype=torch.float32)
+            _hip.check(lib.sp_attention_bf16_bwd(_p(q, cl=False), _p(k, cl=False), _p(v, cl=False),
+                                                 _p(out, cl=False), _p(do, cl=False), lse.data_ptr(), b, heads, n,
+                                                 m, c // heads, c, c, int(bc == 1), c, c, c,
+                                                 1.0 / math.sqrt(c // heads), delta.data_ptr(), _p(dq, cl=False),
+                                                 None, None, _hip.stream_of(do)), "sp_attention_bf16_bwd")
+            return dq, None, None, None
         q32, k32, v32, o32 = q.float(), k.float(), v.float(), out.float()
         do32 = dout.float().contiguous()
         dq = torch.empty_like(q32)
@@ -412,6 +433,8 @@ def cross_attention(q: Tensor, k: Tensor, v: Tensor, heads: int) -> Tensor:
     return _CrossAttnBf16Fn.apply(q, k, v, heads)
 
 
-def fp32_vjp_supported(b: int, heads: int, n: int, m: int, d: int) -> bool:
-    """The fp32 fused VJP kernels serve this shape (they carry the bf16 forward's VJP)."""
-    return bool(_hip.load_library().sp_attention_mh_supported(b, heads, n, m, d))
+def vjp_supported(b: int, heads: int, n: int, m: int, d: int) -> bool:
+    """A fused VJP serves this shape: the bf16 kernels (head dims 40 / 64 / 80), else the exact-fp32
+    ones on the operands widened to fp32 (head dim 160)."""
+    lib = _hip.load_library()
+    return bool(lib.sp_attention_bf16_bwd_supported(b, heads, n, m, d) or lib.sp_attention_mh_supported(b, heads, n, m, d))

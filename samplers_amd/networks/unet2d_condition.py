@@ -107,13 +107,13 @@ class Attention(nn.Module):
         b, n, c = x.shape
         d = c // self.heads
         if context is None:
-            if not (bf16.attention_supported(b, self.heads, n, n, d) and bf16.fp32_vjp_supported(b, self.heads, n, n, d)):
+            if not (bf16.attention_supported(b, self.heads, n, n, d) and bf16.vjp_supported(b, self.heads, n, n, d)):
                 return None
             qkv = torch.nn.functional.linear(x, self._qkv_weight().weight)
             return bf16.self_attention(qkv, self.heads)
         bc, m = context.shape[0], context.shape[1]
         if bc not in (1, b) or context.requires_grad or not (
-                bf16.attention_supported(b, self.heads, n, m, d) and bf16.fp32_vjp_supported(b, self.heads, n, m, d)):
+                bf16.attention_supported(b, self.heads, n, m, d) and bf16.vjp_supported(b, self.heads, n, m, d)):
             return None
         q, k, v = self.to_q(x), self.to_k(context), self.to_v(context)
         return bf16.cross_attention(q, k, v, self.heads)
