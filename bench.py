@@ -309,38 +309,52 @@ class _Heartbeat:
         return False
 
 
-def cpu_baseline(image: int, seconds: float) -> dict:
+def cpu_baseline(image: int, seconds: float, config: str = "inpaint") -> dict:
     """oracle/dps_loop.py (dps.py:91-122 semantics) on the host cores with the same UNet and
-    workload per sample.  The thread count is probed first at batch 1 (the CPU share this
+    workload per sample (the config's operator: 50 % random mask, 9x9 / sigma 3 blur or identity).  The thread count is probed first at batch 1 (the CPU share this
     process is given — OMP_NUM_THREADS / the cgroup quota — and multiples of it up to every
     core the process may run on), then batch 1 and batch 8 are timed on the best count for
     about `seconds` / 2 each; the best per-sample rate is reported."""
     with _Heartbeat("cpu baseline"):
-        return _cpu_baseline(image, seconds)
+        return _cpu_baseline(image, seconds, config)
 
 
-def _cpu_baseline(image: int, seconds: float) -> dict:
+def _cpu_apply_op(config: str, shape: tuple):
+    """(the config's forward operator A on the CPU, its description) for the oracle loop."""
+    if config == "blur":
+        from oracle import blur as oblur
+
+        k1d = oblur.taps(9, 3.0)
+        return (lambda v: oblur.blur(v, k1d).to(v.dtype)), "9x9 / sigma 3 Gaussian blur (reflect)"
+    if config == "identity":
+        return (lambda v: v), "identity operator"
+    from samplers_amd.operators import get_mask_random
+
+    mask = get_mask_random(shape, 0.5, seed=1)
+    kept = torch.nonzero(~mask.flatten()).squeeze(1)
+    return (lambda v: v.reshape(v.shape[0], -1)[:, kept]), "50% random mask"
+
+
+def _cpu_baseline(image: int, seconds: float, config: str = "inpaint") -> dict:
     from oracle import dps_loop
     from samplers_amd.networks.unet2d import build_unet
-    from samplers_amd.operators import get_mask_random
 
     host = host_cpu()
     share, cores = host["cpu_share"], host["affinity_cores"]
     candidates = sorted({min(cores, share * k) for k in (1, 2, 4)})
     shape = (3, image, image)
     unet = build_unet(seed=0)
-    mask = get_mask_random(shape, 0.5, seed=1)
-    kept = torch.nonzero(~mask.flatten()).squeeze(1)
+    apply_op, op_desc = _cpu_apply_op(config, shape)
     betas = torch.linspace(1e-4, 0.02, 1000, dtype=torch.float32)
     acp = torch.cat([torch.ones(1), torch.cumprod(1 - betas, 0)]).clip(1e-6, 1)
     ts = list(range(1000))
-    apply_op = lambda v: v.reshape(v.shape[0], -1)[:, kept]  # noqa: E731
     lp = dps_loop.gaussian_log_prob(0.05)
     def point(batch: int, nthreads: int, budget: float) -> dict:
         torch.set_num_threads(nthreads)
         gen = torch.Generator().manual_seed(1000)
         x_true = torch.rand((batch, *shape), generator=gen) * 2 - 1
-        y = apply_op(x_true) + 0.05 * torch.randn(batch, kept.numel(), generator=gen)
+        y0 = apply_op(x_true)
+        y = y0 + 0.05 * torch.randn(y0.shape, generator=gen)
         x = torch.randn((batch, *shape), generator=gen)
         noise = lambda i: torch.randn((batch, *shape), generator=gen)  # noqa: E731
         # one warm-up iteration, then as many as fit in the budget (at least 1)
@@ -360,7 +374,7 @@ def _cpu_baseline(image: int, seconds: float) -> dict:
 
     probe = [point(1, t, 0.0) for t in candidates]  # thread-count probe: one timed iteration
     nthreads = max(probe, key=lambda p: p["samples_per_s"])["threads"]
-    sweep = [point(b, nthreads, seconds / 2) for b in (1, 8)]
+    sweep = [point(b, nthreads, seconds / 2) for b in ((1, 8) if image <= 256 else (1, 2))]
     best = max(sweep, key=lambda p: p["samples_per_s"])
     return {
         "value": best["samples_per_s"],
@@ -373,9 +387,9 @@ def _cpu_baseline(image: int, seconds: float) -> dict:
         "cgroup_cpus": host["cgroup_cpus"],
         "thread_probe": probe,
         "sweep": sweep,
-        "sample": f"batch 1 and 8 on the best of {candidates} threads (probed at batch 1): "
+        "sample": f"batch {' and '.join(str(p['batch']) for p in sweep)} on the best of {candidates} threads (probed at batch 1): "
                   f"guided DPS iterations (t=999) of oracle/dps_loop.py at 3x{image}x{image}, "
-                  f"50% random mask, same random-init UNet, fp32, torch-CPU {torch.__version__}; "
+                  f"{op_desc}, same random-init UNet, fp32, torch-CPU {torch.__version__}; "
                   f"best = batch {best['batch']} on {best['threads']} threads, "
                   f"{best['iterations']} iterations",
     }
@@ -556,7 +570,7 @@ def main():
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         log("timing the CPU baseline ...")
-        result["cpu_baseline"] = cpu_baseline(args.image, args.cpu_seconds)
+        result["cpu_baseline"] = cpu_baseline(args.image, args.cpu_seconds, args.config)
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:

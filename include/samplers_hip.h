@@ -574,6 +574,11 @@ int64_t sp_conv3x3_bf16_packed_size(int32_t cin, int32_t cout);
  * W'[ci][co][2-ky][2-kx].  bias fp32 [cout] or NULL, res bf16 like y or NULL. */
 int sp_conv3x3_bf16(const void* x, const void* wp, const float* bias, const void* res, int64_t n, int32_t cin,
                     int32_t cout, int32_t h, int32_t w, void* y, sp_stream_t stream);
+/* split-K form for launches that leave CUs idle (the priors' 16x16 / 8x8 levels): the parts' fp32
+ * sums in ws (sp_conv3x3_bf16_workspace bytes, 0 = unsplit), reduced in a fixed order */
+int64_t sp_conv3x3_bf16_workspace(int64_t n, int32_t cin, int32_t cout, int32_t h, int32_t w);
+int sp_conv3x3_bf16_ws(const void* x, const void* wp, const float* bias, const void* res, int64_t n, int32_t cin,
+                       int32_t cout, int32_t h, int32_t w, void* y, void* ws, int64_t ws_bytes, sp_stream_t stream);
 /* y = conv3x3(upsample_nearest2x(x)) + bias (+ res) (diffusers' Upsample2D): x [n][h/2][w/2][cin],
  * y [n][h][w][cout] — the upsampled tensor is never written; its VJP is sp_conv3x3_bf16 with the
  * VJP pack at full resolution followed by sp_pool2x2_bf16. */

@@ -234,6 +234,9 @@ SIGNATURES = {
     "sp_conv3x3_bf16_packed_size": (_I64, [ctypes.c_int32, ctypes.c_int32]),
     "sp_conv3x3_bf16": (ctypes.c_int, [_P, _P, _P, _P, _I64, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
                                        ctypes.c_int32, _P, _P]),
+    "sp_conv3x3_bf16_workspace": (_I64, [_I64, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32]),
+    "sp_conv3x3_bf16_ws": (ctypes.c_int, [_P, _P, _P, _P, _I64, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
+                                          ctypes.c_int32, _P, _P, _I64, _P]),
     "sp_conv3x3_bf16_up": (ctypes.c_int, [_P, _P, _P, _P, _I64, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
                                           ctypes.c_int32, _P, _P]),
     "sp_pool2x2_bf16": (ctypes.c_int, [_P, _I64, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, _P, _P]),

@@ -87,17 +87,27 @@ struct CvGeo {
     static constexpr int LW = WROWS * RB;
     static constexpr int LP = PQ * RB;
     static constexpr int NW = (WROWS * 2 + kBlock - 1) / kBlock;  // 16-byte weight pieces per thread
-    static constexpr int NP = (PQ * 2 + kBlock - 1) / kBlock;     // 16-byte patch pieces per thread
+    static constexpr int PQP = PQ;
+    static constexpr int NP = (PQP * 2 + kBlock - 1) / kBlock;    // 16-byte patch pieces per thread
 };
+
+// 16-byte piece p of an LDS image of 32-byte rows (48-byte stride): row p / 2, chunk p % 2 —
+// consecutive lanes read the two halves of a pixel's 32 bytes (measured faster than writing one
+// chunk of 64 rows per instruction, which avoids the 2-way ds_write conflicts but doubles the
+// cache lines each global load instruction touches: -8 % on the 64x64 / 512x512 layers)
+__device__ __forceinline__ int cv_row(int p) { return p >> 1; }
+__device__ __forceinline__ int cv_chunk(int p) { return p & 1; }
 
 // UP: the input is the half-resolution tensor of diffusers' Upsample2D and the patch reads
 // pixel (h >> 1, w >> 1) of it for full-resolution pixel (h, w): conv(upsample_nearest2x(x))
 // without the upsampled tensor in HBM.
+// part != NULL (split-K, gridDim.z parts over the input-channel stages): part z of the
+// contraction is stored as fp32 to part[z][n h w][cout] without bias / residual (k_conv_reduce).
 template <int TC, bool UP>
 __global__ __launch_bounds__(kBlock, TC == 4 ? 1 : 2) void k_conv3x3_bf16(const u16* __restrict__ x, const u16* __restrict__ wp,
                                                          const float* __restrict__ bias, const u16* __restrict__ res,
                                                          int n, int cin, int cout, int h, int w,
-                                                         u16* __restrict__ y) {
+                                                         u16* __restrict__ y, float* __restrict__ part) {
     using G = CvGeo<TC>;
     __shared__ __attribute__((aligned(16))) char lds[G::LW + G::LP];
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, r = lane & 31, hh = lane >> 5;
@@ -121,8 +131,8 @@ __global__ __launch_bounds__(kBlock, TC == 4 ? 1 : 2) void k_conv3x3_bf16(const 
     for (int k = 0; k < G::NP; ++k) {
         const int i = tid + k * kBlock;
         poff[k] = -1;
-        if (i < 2 * G::PQ) {
-            const int q = i >> 1, half = i & 1;
+        if (i < 2 * G::PQP && cv_row(i) < G::PQ) {
+            const int q = cv_row(i), half = cv_chunk(i);
             const int prow = q / G::PW, pcol = q - prow * G::PW;
             const int seg = prow / (G::SR + 2), pr = prow - seg * (G::SR + 2);
             const int nn = n0 + seg, hi = h0 + pr - 1, wi = c0 + pcol - 1;
@@ -140,7 +150,7 @@ __global__ __launch_bounds__(kBlock, TC == 4 ? 1 : 2) void k_conv3x3_bf16(const 
 #pragma unroll
         for (int k = 0; k < G::NW; ++k) {
             const int i = tid + k * kBlock;
-            if (i < G::WROWS * 2) sw[k] = ws[i];
+            if (i < G::WROWS * 2) sw[k] = ws[2 * cv_row(i) + cv_chunk(i)];
         }
 #pragma unroll
         for (int k = 0; k < G::NP; ++k)
@@ -150,12 +160,13 @@ __global__ __launch_bounds__(kBlock, TC == 4 ? 1 : 2) void k_conv3x3_bf16(const 
 #pragma unroll
         for (int k = 0; k < G::NW; ++k) {
             const int i = tid + k * kBlock;
-            if (i < G::WROWS * 2) *reinterpret_cast<bq_u4*>(lds + (i >> 1) * G::RB + (i & 1) * 16) = sw[k];
+            if (i < G::WROWS * 2) *reinterpret_cast<bq_u4*>(lds + cv_row(i) * G::RB + cv_chunk(i) * 16) = sw[k];
         }
 #pragma unroll
         for (int k = 0; k < G::NP; ++k) {
             const int i = tid + k * kBlock;
-            if (i < 2 * G::PQ) *reinterpret_cast<bq_u4*>(lds + G::LW + (i >> 1) * G::RB + (i & 1) * 16) = spx[k];
+            if (i < 2 * G::PQP && cv_row(i) < G::PQ)
+                *reinterpret_cast<bq_u4*>(lds + G::LW + cv_row(i) * G::RB + cv_chunk(i) * 16) = spx[k];
         }
     };
 
@@ -173,26 +184,35 @@ __global__ __launch_bounds__(kBlock, TC == 4 ? 1 : 2) void k_conv3x3_bf16(const 
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[a][j] = bq_f16{};
 
-    gload(0);
-    for (int ks = 0; ks < nci; ++ks) {
+    const int kz = blockIdx.z, nz = gridDim.z;
+    const int ks0 = kz * nci / nz, ks1 = (kz + 1) * nci / nz;
+    gload(ks0);
+    for (int ks = ks0; ks < ks1; ++ks) {
         __syncthreads();  // the previous stage's fragment reads are done
         lstore();
         __syncthreads();
-        if (ks + 1 < nci) gload(ks + 1);
+        if (ks + 1 < ks1) gload(ks + 1);
         const char* __restrict__ wl = lds + r * G::RB + hh * 16;
         const char* __restrict__ pl = lds + G::LW;
+        // fragments of tap t + 1 are read while tap t's 8 MFMAs run (two register sets)
+        bq_u4 fa[2][2], fb[2][4];
+        auto frags = [&](int t, int slot) {
+            const int dy = t / 3, dx = t - 3 * (t / 3);
+            fa[slot][0] = *reinterpret_cast<const bq_u4*>(wl + (t * 64) * G::RB);
+            fa[slot][1] = *reinterpret_cast<const bq_u4*>(wl + (t * 64 + 32) * G::RB);
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                fb[slot][j] = *reinterpret_cast<const bq_u4*>(pl + qb[j] + (dy * G::PW + dx) * G::RB);
+        };
+        frags(0, 0);
 #pragma unroll
         for (int t = 0; t < 9; ++t) {
-            const int dy = t / 3, dx = t - 3 * (t / 3);
-            const bq_u4 a0 = *reinterpret_cast<const bq_u4*>(wl + (t * 64) * G::RB);
-            const bq_u4 a1 = *reinterpret_cast<const bq_u4*>(wl + (t * 64 + 32) * G::RB);
-            bq_u4 b[4];
-#pragma unroll
-            for (int j = 0; j < 4; ++j) b[j] = *reinterpret_cast<const bq_u4*>(pl + qb[j] + (dy * G::PW + dx) * G::RB);
+            if (t + 1 < 9) frags(t + 1, (t + 1) & 1);
+            const int sl = t & 1;
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
-                acc[0][j] = bq_mfma(a0, b[j], acc[0][j]);
-                acc[1][j] = bq_mfma(a1, b[j], acc[1][j]);
+                acc[0][j] = bq_mfma(fa[sl][0], fb[sl][j], acc[0][j]);
+                acc[1][j] = bq_mfma(fa[sl][1], fb[sl][j], acc[1][j]);
             }
         }
     }
@@ -206,6 +226,19 @@ __global__ __launch_bounds__(kBlock, TC == 4 ? 1 : 2) void k_conv3x3_bf16(const 
         if (nn >= n) continue;
         const int64_t obase = (((int64_t)nn * h + h0 + rr) * w + c0 + col) * cout;
         SP_DCHECK(h0 + rr < h && c0 + col < w);
+        if (part) {  // split-K partial (cout % 4 == 0): fp32, no bias / residual
+            float* pp = part + (int64_t)kz * ((int64_t)n * h * w * cout) + obase;
+#pragma unroll
+            for (int a = 0; a < 2; ++a)
+#pragma unroll
+                for (int g = 0; g < 4; ++g) {
+                    const int co = cb * 64 + 32 * a + 8 * g + 4 * hh;
+                    if (co + 4 <= cout)
+                        *reinterpret_cast<float4*>(pp + co) = make_float4(acc[a][j][4 * g], acc[a][j][4 * g + 1],
+                                                                          acc[a][j][4 * g + 2], acc[a][j][4 * g + 3]);
+                }
+            continue;
+        }
 #pragma unroll
         for (int a = 0; a < 2; ++a)
 #pragma unroll
@@ -245,19 +278,64 @@ static int conv_tc(int h, int w) {
     return 0;
 }
 
+// y = sum over the split-K parts (fixed order) + bias (+ res), 4 channels per thread-iteration
+__global__ __launch_bounds__(kBlock) void k_conv_reduce(const float* __restrict__ part, int parts, int64_t total,
+                                                        int cout, const float* __restrict__ bias,
+                                                        const u16* __restrict__ res, u16* __restrict__ y) {
+    for (int64_t v = (int64_t)blockIdx.x * kBlock + threadIdx.x; v < total / 4; v += (int64_t)gridDim.x * kBlock) {
+        const int64_t i = 4 * v;
+        float4 a = *reinterpret_cast<const float4*>(part + i);
+        for (int z = 1; z < parts; ++z) {
+            const float4 b = *reinterpret_cast<const float4*>(part + (int64_t)z * total + i);
+            a.x += b.x, a.y += b.y, a.z += b.z, a.w += b.w;
+        }
+        const int co = static_cast<int>(i % cout);
+        if (bias) a.x += bias[co], a.y += bias[co + 1], a.z += bias[co + 2], a.w += bias[co + 3];
+        if (res) {
+            const bq_u2 rv = *reinterpret_cast<const bq_u2*>(res + i);
+            a.x += bf_lo(rv.x), a.y += bf_hi(rv.x), a.z += bf_lo(rv.y), a.w += bf_hi(rv.y);
+        }
+        *reinterpret_cast<bq_u2*>(y + i) = bq_u2{pk2(a.x, a.y), pk2(a.z, a.w)};
+    }
+}
+
+template <int TC>
+static int64_t conv_tiles(int n, int h, int w) {
+    using G = CvGeo<TC>;
+    if constexpr (TC == 32)
+        return (int64_t)n * (h / G::SR) * (w / 32);
+    else
+        return (n + G::S - 1) / G::S;
+}
+
+// split-K parts for a launch whose workgroups leave CUs idle (fewer than two per CU): doubling
+// while each part keeps >= 8 input-channel stages and the grid stays under ~4 per CU
+static int conv_parts(int n, int cin, int cout, int h, int w) {
+    const int tc = conv_tc(h, w);
+    if (!tc || cout % 4) return 1;
+    const int64_t tiles = tc == 32 ? conv_tiles<32>(n, h, w) : tc == 16 ? conv_tiles<16>(n, h, w)
+                        : tc == 8 ? conv_tiles<8>(n, h, w) : conv_tiles<4>(n, h, w);
+    const int64_t wgs = tiles * ((cout + 63) / 64);
+    int parts = 1;
+    while (wgs * parts < 512 && (cin / 16) / (2 * parts) >= 8 && parts < 16) parts *= 2;
+    return parts;
+}
+
 template <int TC, bool UP>
 static void conv_bf16_launch(const u16* x, const u16* wp, const float* bias, const u16* res, int n, int cin,
-                             int cout, int h, int w, u16* y, hipStream_t s) {
+                             int cout, int h, int w, u16* y, hipStream_t s, float* part = nullptr, int parts = 1) {
     using G = CvGeo<TC>;
+    (void)sizeof(G);
     const int cbn = (cout + 63) / 64;
-    int64_t tiles;
-    if constexpr (TC == 32)
-        tiles = (int64_t)n * (h / G::SR) * (w / 32);
-    else
-        tiles = (n + G::S - 1) / G::S;
+    const int64_t tiles = conv_tiles<TC>(n, h, w);
     const double flops = 18.0 * n * (double)h * w * cin * cout;
-    launch_w(TK_CONV_BF16, flops, k_conv3x3_bf16<TC, UP>, dim3(cbn, static_cast<unsigned>(tiles)), dim3(kBlock), s, x,
-             wp, bias, res, n, cin, cout, h, w, y);
+    launch_w(TK_CONV_BF16, flops, k_conv3x3_bf16<TC, UP>, dim3(cbn, static_cast<unsigned>(tiles), parts), dim3(kBlock),
+             s, x, wp, bias, res, n, cin, cout, h, w, y, parts > 1 ? part : nullptr);
+    if (parts > 1) {
+        const int64_t total = (int64_t)n * h * w * cout;
+        launch(0, k_conv_reduce, dim3(stream_blocks(total / 8)), dim3(kBlock), s, static_cast<const float*>(part),
+               parts, total, cout, bias, res, y);
+    }
 }
 
 // Upsample2D's VJP after the full-resolution input VJP: dx[n][i][j][c] = sum of the 2 x 2 block
@@ -1135,7 +1213,8 @@ int64_t sp_conv3x3_bf16_packed_size(int32_t cin, int32_t cout) {
 // wp: packed as [co block of 64][ci block of 16][tap 3 ky + kx][64 co][16 ci] (rows past cout
 // zero); the input VJP is the same call with the pack of W'[ci][co][2-ky][2-kx].
 static int conv_bf16_call(const void* x, const void* wp, const float* bias, const void* res, int64_t n, int32_t cin,
-                          int32_t cout, int32_t h, int32_t w, void* y, sp_stream_t stream, bool up) {
+                          int32_t cout, int32_t h, int32_t w, void* y, sp_stream_t stream, bool up,
+                          void* ws = nullptr, int64_t ws_bytes = 0) {
     if (!x || !wp || !y || n <= 0 || !sp_conv3x3_bf16_supported(cin, cout, h, w)) return SP_EINVAL;
     if (up && (h % 2 || w % 2)) return SP_EINVAL;
     if (n * h * (int64_t)w * std::max(cin, cout) >= (int64_t(1) << 40) || n >= (int64_t(1) << 30)) return SP_EINVAL;
@@ -1154,13 +1233,32 @@ static int conv_bf16_call(const void* x, const void* wp, const float* bias, cons
         }
         return check_launch("sp_conv3x3_bf16_up");
     }
+    int parts = conv_parts(ni, cin, cout, h, w);
+    if (parts > 1 && (!ws || ws_bytes < 4 * parts * (int64_t)ni * h * w * cout)) parts = 1;
+    float* part = static_cast<float*>(ws);
     switch (conv_tc(h, w)) {
-        case 32: conv_bf16_launch<32, false>(xx, ww, bias, rr, ni, cin, cout, h, w, yy, s); break;
-        case 16: conv_bf16_launch<16, false>(xx, ww, bias, rr, ni, cin, cout, h, w, yy, s); break;
-        case 8: conv_bf16_launch<8, false>(xx, ww, bias, rr, ni, cin, cout, h, w, yy, s); break;
-        default: conv_bf16_launch<4, false>(xx, ww, bias, rr, ni, cin, cout, h, w, yy, s); break;
+        case 32: conv_bf16_launch<32, false>(xx, ww, bias, rr, ni, cin, cout, h, w, yy, s, part, parts); break;
+        case 16: conv_bf16_launch<16, false>(xx, ww, bias, rr, ni, cin, cout, h, w, yy, s, part, parts); break;
+        case 8: conv_bf16_launch<8, false>(xx, ww, bias, rr, ni, cin, cout, h, w, yy, s, part, parts); break;
+        default: conv_bf16_launch<4, false>(xx, ww, bias, rr, ni, cin, cout, h, w, yy, s, part, parts); break;
     }
     return check_launch("sp_conv3x3_bf16");
+}
+
+// bytes of the split-K workspace sp_conv3x3_bf16_ws uses for this shape (0: the launch fills the
+// chip unsplit): parts x n h w cout fp32
+int64_t sp_conv3x3_bf16_workspace(int64_t n, int32_t cin, int32_t cout, int32_t h, int32_t w) {
+    if (n <= 0 || n >= (int64_t(1) << 30) || !sp_conv3x3_bf16_supported(cin, cout, h, w)) return 0;
+    const int parts = conv_parts(static_cast<int>(n), cin, cout, h, w);
+    return parts > 1 ? 4 * parts * n * h * (int64_t)w * cout : 0;
+}
+
+// sp_conv3x3_bf16 with split-K over the input channels where the workgroups would leave CUs idle:
+// the parts' fp32 sums go to ws (sp_conv3x3_bf16_workspace bytes) and a fixed-order reduce adds
+// them with the bias / residual (deterministic); ws = NULL or short: unsplit
+int sp_conv3x3_bf16_ws(const void* x, const void* wp, const float* bias, const void* res, int64_t n, int32_t cin,
+                       int32_t cout, int32_t h, int32_t w, void* y, void* ws, int64_t ws_bytes, sp_stream_t stream) {
+    return conv_bf16_call(x, wp, bias, res, n, cin, cout, h, w, y, stream, false, ws, ws_bytes);
 }
 
 int sp_conv3x3_bf16(const void* x, const void* wp, const float* bias, const void* res, int64_t n, int32_t cin,

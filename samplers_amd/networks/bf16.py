@@ -120,11 +120,18 @@ def _pad_channels(x: Tensor, c: int) -> Tensor:
 
 
 def _conv_launch(x: Tensor, pack: Tensor, bias: Tensor | None, res: Tensor | None, cout: int) -> Tensor:
+    from ..runtime import split_k_enabled
+    from .layers import _query
+
     lib = _hip.load_library()
     n, cin, h, w = x.shape
     y = torch.empty(n, cout, h, w, device=x.device, dtype=BF16, memory_format=CL)
-    _hip.check(lib.sp_conv3x3_bf16(_p(x), _p(pack, cl=False), None if bias is None else bias.data_ptr(), _p(res), n,
-                                   cin, cout, h, w, _p(y), _hip.stream_of(x)), "sp_conv3x3_bf16")
+    # split-K where the tiles leave CUs idle (torch's caching allocator on the launch stream)
+    nb = _query("sp_conv3x3_bf16_workspace", n, cin, cout, h, w) if split_k_enabled() else 0
+    ws = torch.empty(max(nb // 4, 1), device=x.device, dtype=torch.float32)
+    _hip.check(lib.sp_conv3x3_bf16_ws(_p(x), _p(pack, cl=False), None if bias is None else bias.data_ptr(), _p(res),
+                                      n, cin, cout, h, w, _p(y), ws.data_ptr() if nb else None, nb,
+                                      _hip.stream_of(x)), "sp_conv3x3_bf16_ws")
     return y
 
 

@@ -91,6 +91,32 @@ def test_conv3x3_bf16_fwd_vjp_matches_fp32(cuda, shape, parity_record):
     assert e < 3e-3 and ed < 5e-3, (e, ed)
 
 
+def test_conv3x3_bf16_split_k_equals_unsplit_within_rounding(cuda):
+    """The 8x8 / 16x16 levels split K (sp_conv3x3_bf16_workspace > 0): the fixed-order reduce is
+    repeatable and agrees with the unsplit launch to the bf16 rounding of the output."""
+    from samplers_amd import _hip
+    from samplers_amd.networks import bf16
+    from samplers_amd.networks.layers import Conv3x3
+
+    lib = _hip.load_library()
+    torch.manual_seed(11)
+    n, c, h = 32, 1280, 8
+    assert lib.sp_conv3x3_bf16_workspace(n, c, c, h, h) > 0
+    conv = Conv3x3(c, c).to(device=cuda, dtype=BF).requires_grad_(False)
+    x = torch.randn(n, c, h, h, device=cuda).to(BF).contiguous(memory_format=torch.channels_last)
+    res = torch.randn(n, c, h, h, device=cuda).to(BF).contiguous(memory_format=torch.channels_last)
+    y1 = bf16.conv3x3(conv, x, res=res)
+    y2 = bf16.conv3x3(conv, x, res=res)
+    assert torch.equal(y1, y2)
+    pk = bf16.conv_pack(conv, False)
+    y0 = torch.empty_like(y1)
+    b = conv.bias.float().contiguous()
+    _hip.check(lib.sp_conv3x3_bf16(x.data_ptr(), pk.data_ptr(), b.data_ptr(), res.data_ptr(), n, c, c, h, h,
+                                   y0.data_ptr(), _hip.stream_of(x)), "unsplit")
+    ref = F.conv2d(x.float(), conv.weight.float(), conv.bias.float(), padding=1) + res.float()
+    assert _rel(y1, ref) < 3e-3 and _rel(y0, ref) < 3e-3 and _rel(y1, y0) < 3e-3
+
+
 def test_conv3x3_bf16_residual_and_repeatable(cuda):
     from samplers_amd.networks import bf16
     from samplers_amd.networks.layers import Conv3x3

@@ -26,6 +26,8 @@ for step in "$@"; do
         psldbf16) run psld_bf16 900 python -u tools/bench_psld.py --dtype bf16 --steps 3 --warmup 2 --cpu-baseline ;;
         psldbf16q) run psld_bf16 600 python -u tools/bench_psld.py --dtype bf16 --steps 3 --warmup 2 ;;
         psldbf16prof) run psld_bf16_prof 900 rocprofv3 --kernel-trace --stats -d "$OUT/prof_psld_bf16" -o run -- python -u tools/bench_psld.py --dtype bf16 --steps 2 --warmup 1 ;;
+        convbf16) run conv_bf16 300 python -u tools/bench_conv_bf16.py --miopen ;;
+        convbf16sq) FILTER=k_conv3x3_bf16 NAME=convbf16 run conv_bf16_sq 600 tools/sq_pmc.sh tools/bench_conv_bf16.py --reps 3 --shapes sd ;;
         gputests) run gpu_tests 1100 python -u -m pytest tests -m gpu -q --timeout 400 --timeout-method thread ;;
         *) echo "unknown step $step"; exit 2 ;;
     esac
