@@ -711,7 +711,6 @@ constexpr float AB_LN2 = 0.6931471805599453f;
 constexpr int AB_QW = 32, AB_WB = 4 * AB_QW;
 constexpr float AB_LAZY = 8.f;
 
-__device__ __forceinline__ int ab_pos(int k) { return (k & ~12) | ((k & 4) << 1) | ((k & 8) >> 1); }
 
 template <int D>
 struct AbGeo {
@@ -721,10 +720,65 @@ struct AbGeo {
     static constexpr int DT = (D + 31) / 32;
     static constexpr int SB = 64;
     static constexpr int KROW = DKP + 8;   // bf16 per K row in LDS
-    static constexpr int VROW = SB + 8;    // bf16 per V^T row
-    static constexpr int NKU = (SB * (D / 8) + kBlock - 1) / kBlock;          // K 16-byte pieces per thread
+    static constexpr int IMG = SB * KROW + 32 * DT;  // a natural image + the columns a last-row tr read reaches
     static constexpr int NVU = (SB / 2 * (D / 8) + kBlock - 1) / kBlock;      // V (2 keys x 8 d) units
 };
+
+// a stage of SB rows (row pairs 2p, 2p + 1 x 8 d per unit) into registers.  Rows >= limit read
+// row limit - 1 instead (unconditional loads: a select on a loaded value, or a zero written into
+// a load's destination, makes the compiler wait for the whole stage's loads at once); the
+// kernels give such rows no weight (keys past m: P = 0; queries past n: lse = +inf, delta = 0)
+template <int D>
+__device__ __forceinline__ void ab_ld_pairs(const u16* __restrict__ src, int64_t rs, int base, int limit,
+                                            bq_u4 (&st)[AbGeo<D>::NVU][2]) {
+    using G = AbGeo<D>;
+#pragma unroll
+    for (int j = 0; j < G::NVU; ++j) {
+        const int u = threadIdx.x + j * kBlock;
+        if (u < G::SB / 2 * (D / 8)) {
+            const int p = u / (D / 8), d0 = 8 * (u - p * (D / 8));
+            const int r0 = min(base + 2 * p, limit - 1), r1 = min(base + 2 * p + 1, limit - 1);
+            st[j][0] = *reinterpret_cast<const bq_u4*>(src + (int64_t)r0 * rs + d0);
+            st[j][1] = *reinterpret_cast<const bq_u4*>(src + (int64_t)r1 * rs + d0);
+        }
+    }
+}
+
+// natural image [SB][KROW]
+template <int D>
+__device__ __forceinline__ void ab_st_nat(u16* img, const bq_u4 (&st)[AbGeo<D>::NVU][2]) {
+    using G = AbGeo<D>;
+#pragma unroll
+    for (int j = 0; j < G::NVU; ++j) {
+        const int u = threadIdx.x + j * kBlock;
+        if (u < G::SB / 2 * (D / 8)) {
+            const int p = u / (D / 8), d0 = 8 * (u - p * (D / 8));
+            *reinterpret_cast<bq_u4*>(img + (2 * p) * G::KROW + d0) = st[j][0];
+            *reinterpret_cast<bq_u4*>(img + (2 * p + 1) * G::KROW + d0) = st[j][1];
+        }
+    }
+}
+
+typedef short ab_s4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) ab_s4 ab_lds_s4;
+
+// The A fragment of a transposed operand (rows d = 32 dt .. +31, K = 16 rows of a natural
+// [rows][KROW] image in the C layout's order: element j of lane half h is row
+// row0 + 8 (j >> 2) + 4 h + (j & 3)) read straight from the natural image with two
+// ds_read_b64_tr_b16 (T10: lane 4q + p of a 16-lane group gives the address of row q, columns
+// 4p .. 4p + 3, and receives column `lane % 16` of the 4 rows) — no transposed copy in LDS.
+// trb = img + (4 h + q) KROW + 16 g + 4 p for lane (h, g, q, p); off = row0 KROW + 32 dt.
+template <int KROW>
+__device__ __forceinline__ bq_u4 ab_tr(const u16* trb, int off) {
+    const ab_s4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((ab_lds_s4*)(trb + off));
+    const ab_s4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((ab_lds_s4*)(trb + off + 8 * KROW));
+    return bq_u4{__builtin_bit_cast(bq_u2, lo)[0], __builtin_bit_cast(bq_u2, lo)[1], __builtin_bit_cast(bq_u2, hi)[0],
+                 __builtin_bit_cast(bq_u2, hi)[1]};
+}
+
+__device__ __forceinline__ int ab_trlane(int lane, int krow) {
+    return (4 * (lane >> 5) + ((lane >> 2) & 3)) * krow + 16 * ((lane >> 4) & 1) + 4 * (lane & 3);
+}
 
 template <int D>
 __global__ __launch_bounds__(kBlock) void k_attnb_fwd(const u16* __restrict__ q, const u16* __restrict__ k,
@@ -732,8 +786,8 @@ __global__ __launch_bounds__(kBlock) void k_attnb_fwd(const u16* __restrict__ q,
                                                       int rsq, int rskv, int kv_shared, int ro, float sl2,
                                                       u16* __restrict__ out, float* __restrict__ lse) {
     using G = AbGeo<D>;
-    __shared__ __attribute__((aligned(16))) u16 Ks[G::SB * G::KROW];
-    __shared__ __attribute__((aligned(16))) u16 Vs[G::DT * 32 * G::VROW];
+    __shared__ __attribute__((aligned(16))) u16 Ks[G::IMG];
+    __shared__ __attribute__((aligned(16))) u16 Vs[G::IMG];
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, r = lane & 31, hh = lane >> 5;
     const int bh = blockIdx.y, b = bh / heads, hd = bh - b * heads;
     const int q0 = blockIdx.x * AB_WB + wv * AB_QW;
@@ -760,62 +814,19 @@ __global__ __launch_bounds__(kBlock) void k_attnb_fwd(const u16* __restrict__ q,
     float mx = -INFINITY, l = 0.f;
 
     const int nst = (m + G::SB - 1) / G::SB;
-    bq_u4 kr[G::NKU], vr[G::NVU][2];
-    auto load_stage = [&](int si) {
-        const int kbase = si * G::SB;
-#pragma unroll
-        for (int j = 0; j < G::NKU; ++j) {
-            const int i = tid + j * kBlock;
-            if (i < G::SB * (D / 8)) {
-                const int row = i / (D / 8), col = 8 * (i - row * (D / 8));
-                kr[j] = kbase + row < m ? *reinterpret_cast<const bq_u4*>(k + kvb + (int64_t)(kbase + row) * rskv + col)
-                                        : bq_u4{0u, 0u, 0u, 0u};
-            }
-        }
-#pragma unroll
-        for (int j = 0; j < G::NVU; ++j) {
-            const int u = tid + j * kBlock;
-            if (u < G::SB / 2 * (D / 8)) {
-                const int p = u / (D / 8), d0 = 8 * (u - p * (D / 8));
-                const int k0 = kbase + 2 * p;
-                vr[j][0] = k0 < m ? *reinterpret_cast<const bq_u4*>(v + kvb + (int64_t)k0 * rskv + d0)
-                                  : bq_u4{0u, 0u, 0u, 0u};
-                vr[j][1] = k0 + 1 < m ? *reinterpret_cast<const bq_u4*>(v + kvb + (int64_t)(k0 + 1) * rskv + d0)
-                                      : bq_u4{0u, 0u, 0u, 0u};
-            }
-        }
-    };
-    auto store_stage = [&]() {
-#pragma unroll
-        for (int j = 0; j < G::NKU; ++j) {
-            const int i = tid + j * kBlock;
-            if (i < G::SB * (D / 8)) {
-                const int row = i / (D / 8), col = 8 * (i - row * (D / 8));
-                *reinterpret_cast<bq_u4*>(Ks + row * G::KROW + col) = kr[j];
-            }
-        }
-#pragma unroll
-        for (int j = 0; j < G::NVU; ++j) {
-            const int u = tid + j * kBlock;
-            if (u < G::SB / 2 * (D / 8)) {
-                const int p = u / (D / 8), d0 = 8 * (u - p * (D / 8));
-                const int key = 2 * p, pos = (key & ~15) | ab_pos(key & 15);  // keys 2p, 2p + 1 adjacent
-#pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    const unsigned a = vr[j][0][e], c = vr[j][1][e];
-                    // d0 + 2e: (key 2p, key 2p + 1) low halves; d0 + 2e + 1: high halves
-                    *reinterpret_cast<unsigned*>(Vs + (d0 + 2 * e) * G::VROW + pos) = (a & 0xffffu) | (c << 16);
-                    *reinterpret_cast<unsigned*>(Vs + (d0 + 2 * e + 1) * G::VROW + pos) = (a >> 16) | (c & 0xffff0000u);
-                }
-            }
-        }
-    };
-    load_stage(0);
+    bq_u4 ks[G::NVU][2], vs[G::NVU][2];
+    const u16* trb = Vs + ab_trlane(lane, G::KROW);
+    ab_ld_pairs<D>(k + kvb, rskv, 0, m, ks);
+    ab_ld_pairs<D>(v + kvb, rskv, 0, m, vs);
     for (int si = 0; si < nst; ++si) {
         __syncthreads();
-        store_stage();
+        ab_st_nat<D>(Ks, ks);
+        ab_st_nat<D>(Vs, vs);
         __syncthreads();
-        if (si + 1 < nst) load_stage(si + 1);
+        if (si + 1 < nst) {
+            ab_ld_pairs<D>(k + kvb, rskv, (si + 1) * G::SB, m, ks);
+            ab_ld_pairs<D>(v + kvb, rskv, (si + 1) * G::SB, m, vs);
+        }
         const int kbase = si * G::SB;
 #pragma unroll
         for (int kb32 = 0; kb32 < G::SB / 32; ++kb32) {
@@ -856,7 +867,7 @@ __global__ __launch_bounds__(kBlock) void k_attnb_fwd(const u16* __restrict__ q,
             for (int dt = 0; dt < G::DT; ++dt)
 #pragma unroll
                 for (int kk = 0; kk < 2; ++kk) {
-                    const bq_u4 vf = *reinterpret_cast<const bq_u4*>(Vs + (dt * 32 + r) * G::VROW + kb32 * 32 + kk * 16 + 8 * hh);
+                    const bq_u4 vf = ab_tr<G::KROW>(trb, (kb32 * 32 + kk * 16) * G::KROW + 32 * dt);
                     o[dt] = bq_mfma(vf, pf[kk], o[dt]);
                 }
         }
@@ -915,59 +926,6 @@ __global__ __launch_bounds__(kBlock) void k_attnb_delta(const u16* __restrict__ 
     delta[rr] = acc;
 }
 
-// a stage of SB rows (row pairs 2p, 2p + 1 x 8 d per unit) into registers; rows >= limit zero
-template <int D>
-__device__ __forceinline__ void ab_ld_pairs(const u16* __restrict__ src, int64_t rs, int base, int limit,
-                                            bq_u4 (&st)[AbGeo<D>::NVU][2]) {
-    using G = AbGeo<D>;
-#pragma unroll
-    for (int j = 0; j < G::NVU; ++j) {
-        const int u = threadIdx.x + j * kBlock;
-        if (u < G::SB / 2 * (D / 8)) {
-            const int p = u / (D / 8), d0 = 8 * (u - p * (D / 8));
-            const int r0 = base + 2 * p;
-            st[j][0] = r0 < limit ? *reinterpret_cast<const bq_u4*>(src + (int64_t)r0 * rs + d0) : bq_u4{0u, 0u, 0u, 0u};
-            st[j][1] = r0 + 1 < limit ? *reinterpret_cast<const bq_u4*>(src + (int64_t)(r0 + 1) * rs + d0)
-                                      : bq_u4{0u, 0u, 0u, 0u};
-        }
-    }
-}
-
-// natural image [SB][KROW]
-template <int D>
-__device__ __forceinline__ void ab_st_nat(u16* img, const bq_u4 (&st)[AbGeo<D>::NVU][2]) {
-    using G = AbGeo<D>;
-#pragma unroll
-    for (int j = 0; j < G::NVU; ++j) {
-        const int u = threadIdx.x + j * kBlock;
-        if (u < G::SB / 2 * (D / 8)) {
-            const int p = u / (D / 8), d0 = 8 * (u - p * (D / 8));
-            *reinterpret_cast<bq_u4*>(img + (2 * p) * G::KROW + d0) = st[j][0];
-            *reinterpret_cast<bq_u4*>(img + (2 * p + 1) * G::KROW + d0) = st[j][1];
-        }
-    }
-}
-
-// transposed image [32 DT][VROW]: row d, the stage's rows at their C-layout positions
-template <int D>
-__device__ __forceinline__ void ab_st_tr(u16* img, const bq_u4 (&st)[AbGeo<D>::NVU][2]) {
-    using G = AbGeo<D>;
-#pragma unroll
-    for (int j = 0; j < G::NVU; ++j) {
-        const int u = threadIdx.x + j * kBlock;
-        if (u < G::SB / 2 * (D / 8)) {
-            const int p = u / (D / 8), d0 = 8 * (u - p * (D / 8));
-            const int key = 2 * p, pos = (key & ~15) | ab_pos(key & 15);
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                const unsigned a = st[j][0][e], c = st[j][1][e];
-                *reinterpret_cast<unsigned*>(img + (d0 + 2 * e) * G::VROW + pos) = (a & 0xffffu) | (c << 16);
-                *reinterpret_cast<unsigned*>(img + (d0 + 2 * e + 1) * G::VROW + pos) = (a >> 16) | (c & 0xffff0000u);
-            }
-        }
-    }
-}
-
 // the B-operand fragments of 32 rows (lane row r) of a row-major [rows][D] operand, d padded to 16
 template <int D>
 __device__ __forceinline__ void ab_rowfrags(const u16* __restrict__ src, int64_t rs, int row, int limit, int hh,
@@ -1015,15 +973,15 @@ __global__ __launch_bounds__(kBlock) void k_attnb_dq(const u16* __restrict__ q, 
                                                      int ro, int rdq, float sl2, float scale,
                                                      u16* __restrict__ dq) {
     using G = AbGeo<D>;
-    __shared__ __attribute__((aligned(16))) u16 Kn[G::SB * G::KROW];
-    __shared__ __attribute__((aligned(16))) u16 Vn[G::SB * G::KROW];
-    __shared__ __attribute__((aligned(16))) u16 Kt[G::DT * 32 * G::VROW];
+    __shared__ __attribute__((aligned(16))) u16 Kn[G::IMG];
+    __shared__ __attribute__((aligned(16))) u16 Vn[G::IMG];
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, r = lane & 31, hh = lane >> 5;
     const int bh = blockIdx.y, b = bh / heads, hd = bh - b * heads;
     const int qq = blockIdx.x * AB_WB + wv * AB_QW + r;
     const int64_t kvb = (kv_shared ? 0 : (int64_t)b * m * rskv) + hd * D;
     ab_zero_pad<D>(Kn);
     ab_zero_pad<D>(Vn);
+    const u16* trk = Kn + ab_trlane(lane, G::KROW);
     bq_u4 qf[G::DK], of[G::DK];
     ab_rowfrags<D>(q + (int64_t)b * n * rsq + hd * D, rsq, qq, n, hh, qf);
     ab_rowfrags<D>(dout + (int64_t)b * n * ro + hd * D, ro, qq, n, hh, of);
@@ -1039,7 +997,6 @@ __global__ __launch_bounds__(kBlock) void k_attnb_dq(const u16* __restrict__ q, 
     for (int si = 0; si < nst; ++si) {
         __syncthreads();
         ab_st_nat<D>(Kn, ks);
-        ab_st_tr<D>(Kt, ks);
         ab_st_nat<D>(Vn, vs);
         __syncthreads();
         if (si + 1 < nst) {
@@ -1070,7 +1027,7 @@ __global__ __launch_bounds__(kBlock) void k_attnb_dq(const u16* __restrict__ q, 
                                   pk2(ds[8 * kk + 4], ds[8 * kk + 5]), pk2(ds[8 * kk + 6], ds[8 * kk + 7])};
 #pragma unroll
                 for (int dt = 0; dt < G::DT; ++dt) {
-                    const bq_u4 a = *reinterpret_cast<const bq_u4*>(Kt + (dt * 32 + r) * G::VROW + kb32 * 32 + kk * 16 + 8 * hh);
+                    const bq_u4 a = ab_tr<G::KROW>(trk, (kb32 * 32 + kk * 16) * G::KROW + 32 * dt);
                     acc[dt] = bq_mfma(a, pf, acc[dt]);
                 }
             }
@@ -1086,10 +1043,8 @@ __global__ __launch_bounds__(kBlock) void k_attnb_dkv(const u16* __restrict__ q,
                                                       int n, int heads, int rs, int ro, int rdkv, float sl2,
                                                       float scale, u16* __restrict__ dk, u16* __restrict__ dv) {
     using G = AbGeo<D>;
-    __shared__ __attribute__((aligned(16))) u16 Qn[G::SB * G::KROW];
-    __shared__ __attribute__((aligned(16))) u16 On[G::SB * G::KROW];
-    __shared__ __attribute__((aligned(16))) u16 Qt[G::DT * 32 * G::VROW];
-    __shared__ __attribute__((aligned(16))) u16 Ot[G::DT * 32 * G::VROW];
+    __shared__ __attribute__((aligned(16))) u16 Qn[G::IMG];
+    __shared__ __attribute__((aligned(16))) u16 On[G::IMG];
     __shared__ __attribute__((aligned(16))) float Ls[G::SB], Dl[G::SB];
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, r = lane & 31, hh = lane >> 5;
     const int bh = blockIdx.y, b = bh / heads, hd = bh - b * heads;
@@ -1097,6 +1052,8 @@ __global__ __launch_bounds__(kBlock) void k_attnb_dkv(const u16* __restrict__ q,
     const int64_t base = (int64_t)b * n * rs + hd * D, obase = (int64_t)b * n * ro + hd * D;
     ab_zero_pad<D>(Qn);
     ab_zero_pad<D>(On);
+    const u16* trq = Qn + ab_trlane(lane, G::KROW);
+    const u16* tro = On + ab_trlane(lane, G::KROW);
     bq_u4 kf[G::DK], vf[G::DK];
     ab_rowfrags<D>(k + base, rs, kk_, n, hh, kf);
     ab_rowfrags<D>(v + base, rs, kk_, n, hh, vf);
@@ -1105,29 +1062,28 @@ __global__ __launch_bounds__(kBlock) void k_attnb_dkv(const u16* __restrict__ q,
     for (int dt = 0; dt < G::DT; ++dt) ak[dt] = bq_f16{}, av[dt] = bq_f16{};
     const int nst = (n + G::SB - 1) / G::SB;
     bq_u4 qs[G::NVU][2], os[G::NVU][2];
+    // the row constants of the next stage: a plain load in flight beside the Q / dO rows (any
+    // arithmetic on it here would make the compiler wait for every load of the stage at once);
+    // scaled and masked when stored
     float lv = 0.f;
     auto ld = [&](int si) {
         ab_ld_pairs<D>(q + base, rs, si * G::SB, n, qs);
         ab_ld_pairs<D>(dout + obase, ro, si * G::SB, n, os);
-        const int qi = si * G::SB + (tid & (G::SB - 1));
-        if (tid < 2 * G::SB) {
-            if (tid < G::SB)
-                lv = qi < n ? lse[(int64_t)bh * n + qi] * AB_LOG2E : INFINITY;
-            else
-                lv = qi < n ? delta[(int64_t)bh * n + qi] : 0.f;
-        }
+        const int qi = min(si * G::SB + (tid & (G::SB - 1)), n - 1);
+        lv = ((tid & G::SB) ? delta : lse)[(int64_t)bh * n + qi];  // every thread: no branch
     };
     ld(0);
     for (int si = 0; si < nst; ++si) {
         __syncthreads();
         ab_st_nat<D>(Qn, qs);
-        ab_st_tr<D>(Qt, qs);
         ab_st_nat<D>(On, os);
-        ab_st_tr<D>(Ot, os);
-        if (tid < G::SB)
-            Ls[tid] = lv;
-        else if (tid < 2 * G::SB)
-            Dl[tid - G::SB] = lv;
+        {
+            const bool in = si * G::SB + (tid & (G::SB - 1)) < n;
+            if (tid < G::SB)
+                Ls[tid] = in ? lv * AB_LOG2E : INFINITY;
+            else if (tid < 2 * G::SB)
+                Dl[tid - G::SB] = in ? lv : 0.f;
+        }
         __syncthreads();
         if (si + 1 < nst) ld(si + 1);
 #pragma unroll
@@ -1162,9 +1118,9 @@ __global__ __launch_bounds__(kBlock) void k_attnb_dkv(const u16* __restrict__ q,
                                   pk2(ds[8 * kk + 4], ds[8 * kk + 5]), pk2(ds[8 * kk + 6], ds[8 * kk + 7])};
 #pragma unroll
                 for (int dt = 0; dt < G::DT; ++dt) {
-                    const int o = (dt * 32 + r) * G::VROW + ib32 * 32 + kk * 16 + 8 * hh;
-                    av[dt] = bq_mfma(*reinterpret_cast<const bq_u4*>(Ot + o), pp, av[dt]);
-                    ak[dt] = bq_mfma(*reinterpret_cast<const bq_u4*>(Qt + o), pd, ak[dt]);
+                    const int o = (ib32 * 32 + kk * 16) * G::KROW + 32 * dt;
+                    av[dt] = bq_mfma(ab_tr<G::KROW>(tro, o), pp, av[dt]);
+                    ak[dt] = bq_mfma(ab_tr<G::KROW>(trq, o), pd, ak[dt]);
                 }
             }
         }
