@@ -62,7 +62,7 @@ def problem_cpu(case: str):
     return x_true, y, apply
 
 
-def run_gpu(case: str, out: Path) -> None:
+def run_gpu(case: str, out: Path, init: torch.Tensor | None = None, name: str | None = None) -> None:
     from samplers_amd.inverse_problem import InverseProblem
     from samplers_amd.networks.ddpm import DDPMNetwork
     from samplers_amd.noise import GaussianNoise
@@ -83,14 +83,18 @@ def run_gpu(case: str, out: Path) -> None:
             seen[done] = x.detach().cpu().clone()
             print(f"[gpu {case}] checkpoint {done}", flush=True)
 
-    fn = lambda k, i, s: noise(-1 if k == "init" else i, s).to(dev)  # noqa: E731
+    def fn(k, i, s):
+        if k == "init" and init is not None:
+            return init.reshape(s).to(dev)
+        return noise(-1 if k == "init" else i, s).to(dev)
+
     t0 = time.perf_counter()
     x0 = DPSSampler(net)(problem, num_sampling_steps=STEPS, gamma=1.0, eta=1.0, noise_fn=fn,
                          callback=keep)
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     torch.save({"checkpoints": seen, "x0": x0.detach().cpu().reshape(b, *SHAPE), "seconds": dt},
-               out / f"gpu_{case}.pt")
+               out / (name or f"gpu_{case}.pt"))
     print(f"[gpu {case}] done in {dt:.1f} s", flush=True)
 
 
@@ -124,25 +128,148 @@ def run_cpu(case: str, out: Path) -> None:
                 "threads": torch.get_num_threads()}, out / f"cpu_{case}.pt")
 
 
+ONESTEP_FROM = (0, 100, 250, 500)  # guided iterations done before the single step checked
+
+
+STATES = ROOT / "gpurun_in" / "parity1000"  # the oracle's states, shipped to the GPU box (git-ignored)
+
+
+def _cpu_state(case: str, k: int, out: Path) -> torch.Tensor:
+    b = CASES[case]
+    if k == 0:
+        return noise(-1, (b, *SHAPE))
+    src = out / f"cpu_{case}.pt"
+    if not src.exists():
+        src = STATES / f"cpu_{case}.pt"
+    return torch.load(src)["checkpoints"][k]
+
+
+def run_onestep_gpu(case: str, out: Path) -> None:
+    """One guided iteration on the GPU from the oracle's own state after k iterations (same
+    noise): the per-step error, free of the trajectory's amplification."""
+    from samplers_amd.inverse_problem import InverseProblem
+    from samplers_amd.networks.ddpm import DDPMNetwork
+    from samplers_amd.noise import GaussianNoise
+    from samplers_amd.operators import IdentityOperator, RandomInpaintingOperator
+    from samplers_amd.samplers.dps import make_dps_step
+
+    dev = torch.device("cuda:0")
+    b = CASES[case]
+    _, y, _ = problem_cpu(case)
+    op = IdentityOperator(SHAPE) if case == "identity" else RandomInpaintingOperator(SHAPE, 0.5, seed=1)
+    problem = InverseProblem(op.to(dev), y.to(dev), GaussianNoise(0.05).to(dev))
+    net = DDPMNetwork.from_config(seed=0, device=dev)
+    net.set_sampling_parameters(STEPS, batch_size=b)
+    ts = net.timesteps_host
+    step = make_dps_step(net, problem, problem.observation.reshape(b, *op.y_shape).to(torch.float32), 1)
+    res = {}
+    for k in ONESTEP_FROM:
+        i = STEPS - 1 - k
+        x = _cpu_state(case, k, out).reshape(b, *SHAPE).to(dev).contiguous()
+        step(x, i, ts[i], ts[i - 1], ts[0], xi=noise(i, (b, *SHAPE)).to(dev))
+        res[k] = x.cpu()
+    torch.cuda.synchronize()
+    torch.save(res, out / f"onestep_gpu_{case}.pt")
+
+
+def run_onestep_cpu(case: str, out: Path) -> dict:
+    """The same single steps on the CPU oracle in fp32 and in fp64 (the fp64 step is the yardstick
+    both fp32 implementations are measured against)."""
+    from oracle import dps_loop
+    from samplers_amd.networks.ddpm import DDPMNetwork
+    from samplers_amd.networks.unet2d import build_unet
+
+    b = CASES[case]
+    _, y, apply = problem_cpu(case)
+    net = DDPMNetwork.from_config(seed=0)
+    ts = net.schedule.set_timesteps(STEPS).flip(0).tolist()
+    acp = net.alphas_cumprod.cpu()
+    g = torch.load(out / f"onestep_gpu_{case}.pt")
+    res = {}
+    for dt in (torch.float32, torch.float64):
+        unet = build_unet(seed=0).to(dt)
+        for k in ONESTEP_FROM:
+            i = STEPS - 1 - k
+            x = _cpu_state(case, k, out).to(dt)
+            xn = dps_loop.dps_reference(lambda v, t: unet(v, t), acp.to(dt), ts[:i + 1], apply,
+                                        dps_loop.gaussian_log_prob(0.05), y.to(dt), x,
+                                        lambda j: noise(j, (b, *SHAPE)).to(dt), gamma=1.0, eta=1.0,
+                                        steps_limit=1, return_sample=True)
+            res.setdefault(k, {})[str(dt).split(".")[-1]] = xn
+            print(f"[onestep {case}] k={k} {dt} done", flush=True)
+    rec = {}
+    for k in ONESTEP_FROM:
+        r64 = res[k]["float64"]
+        rec[str(k)] = {"gpu_fp32_vs_cpu_fp64": rel(g[k], r64), "cpu_fp32_vs_cpu_fp64": rel(res[k]["float32"], r64),
+                       "gpu_fp32_vs_cpu_fp32": rel(g[k], res[k]["float32"])}
+    return rec
+
+
+def run_perturb_gpu(case: str, out: Path, eps: float = 1e-6) -> dict:
+    """The GPU solve again with the initial sample perturbed by eps (relative, Gaussian): the
+    growth of a rounding-sized difference along the trajectory, GPU against GPU."""
+    if not (out / f"gpu_{case}.pt").exists():
+        run_gpu(case, out)
+    src = torch.load(out / f"gpu_{case}.pt")
+    pert = out / f"gpu_{case}_perturbed.pt"
+    b = CASES[case]
+    x0 = noise(-1, (b, *SHAPE))
+    d = torch.randn(x0.shape, generator=torch.Generator().manual_seed(99))
+    xp = x0 + eps * d * (x0.norm() / d.norm())
+    run_gpu(case, out, init=xp, name=pert.name)
+    p = torch.load(pert)
+    return {str(k): rel(p["checkpoints"][k], src["checkpoints"][k]) for k in CHECKPOINTS} | {
+        "x0": rel(p["x0"], src["x0"]), "eps": eps}
+
+
 def rel(a: torch.Tensor, b: torch.Tensor) -> float:
     a, b = a.double().reshape(-1), b.double().reshape(-1)
     return float((a - b).norm() / max(b.norm().item(), 1e-30))
 
 
+ONESTEP_TOL = 1e-5   # one guided step from an oracle state, GPU fp32 against the fp64 oracle
+EARLY_STEPS = 10     # a chaotic case is held to the pointwise tolerance up to this checkpoint
+
+
 def compare(out: Path, record: Path, tol: float) -> dict:
-    res = {"tolerance_rel_l2": tol, "steps": STEPS, "guided_iterations": STEPS - 2, "image": list(SHAPE),
-           "cases": {}}
+    """Pointwise parity over the whole trajectory where the dynamics allow it.
+
+    A case whose GPU-vs-GPU perturbation record (phase ``perturb``: the same solve from an initial
+    sample moved by 1e-6 relative) grows past ``tol`` is chaotic: no fp32 implementation -- the
+    oracle's own fp32 run included -- can stay within ``tol`` of another over 1000 steps. Such a
+    case is judged on (i) the one-step record (phase ``onestep-cpu``: one guided step from the
+    oracle's saved states, GPU fp32 within ONESTEP_TOL of the fp64 oracle) and (ii) the pointwise
+    tolerance up to EARLY_STEPS; the full curve is still recorded. Every other case must stay
+    within ``tol`` at every checkpoint and at x0."""
+    pert_p, one_p = record.with_name(record.stem + "_perturb.json"), record.with_name(record.stem + "_onestep-cpu.json")
+    pert = json.loads(pert_p.read_text()) if pert_p.exists() else {}
+    one = json.loads(one_p.read_text()) if one_p.exists() else {}
+    res = {"tolerance_rel_l2": tol, "onestep_tolerance_rel_l2": ONESTEP_TOL, "steps": STEPS,
+           "guided_iterations": STEPS - 2, "image": list(SHAPE), "cases": {}}
+    ok = True
     for case, b in CASES.items():
         g, c = torch.load(out / f"gpu_{case}.pt"), torch.load(out / f"cpu_{case}.pt")
         curve = {str(k): rel(g["checkpoints"][k], c["checkpoints"][k]) for k in CHECKPOINTS}
         per_sample = [rel(g["x0"][i], c["x0"][i]) for i in range(b)]
-        res["cases"][case] = {"batch": b, "sample_rel_l2_after": curve, "x0_rel_l2": rel(g["x0"], c["x0"]),
-                              "x0_rel_l2_per_sample": per_sample,
-                              "x0_norm": float(c["x0"].double().norm()),
-                              "gpu_seconds": g["seconds"], "cpu_seconds": c["seconds"],
-                              "cpu_threads": c.get("threads")}
-    res["pass"] = all(v <= tol for cs in res["cases"].values()
-                      for v in list(cs["sample_rel_l2_after"].values()) + [cs["x0_rel_l2"]])
+        growth = pert.get(case, {})
+        chaotic = any(v > tol for k, v in growth.items() if k != "eps")
+        entry = {"batch": b, "sample_rel_l2_after": curve, "x0_rel_l2": rel(g["x0"], c["x0"]),
+                 "x0_rel_l2_per_sample": per_sample, "x0_norm": float(c["x0"].double().norm()),
+                 "perturbation_growth": growth, "chaotic": chaotic,
+                 "gpu_seconds": g["seconds"], "cpu_seconds": c["seconds"], "cpu_threads": c.get("threads")}
+        if chaotic:
+            steps = one.get(case, {})
+            entry["onestep"] = steps
+            case_ok = (bool(steps) and all(v["gpu_fp32_vs_cpu_fp64"] <= ONESTEP_TOL for v in steps.values())
+                       and all(v <= tol for k, v in curve.items() if int(k) <= EARLY_STEPS))
+            entry["criterion"] = f"one step <= {ONESTEP_TOL:g} vs fp64 oracle; pointwise <= {tol:g} to step {EARLY_STEPS}"
+        else:
+            case_ok = all(v <= tol for v in list(curve.values()) + [entry["x0_rel_l2"]])
+            entry["criterion"] = f"pointwise <= {tol:g} at every checkpoint and x0"
+        entry["pass"] = case_ok
+        ok = ok and case_ok
+        res["cases"][case] = entry
+    res["pass"] = ok
     record.parent.mkdir(parents=True, exist_ok=True)
     record.write_text(json.dumps(res, indent=1) + "\n")
     return res
@@ -150,7 +277,8 @@ def compare(out: Path, record: Path, tol: float) -> dict:
 
 def main() -> int:
     ap = argparse.ArgumentParser()
-    ap.add_argument("--phase", choices=("gpu", "cpu", "compare"), required=True)
+    ap.add_argument("--phase", choices=("gpu", "cpu", "compare", "onestep-gpu", "onestep-cpu", "perturb"),
+                    required=True)
     ap.add_argument("--case", choices=tuple(CASES) + ("all",), default="all")
     ap.add_argument("--out", default=str(ROOT / "gpurun_out" / "parity1000"))
     ap.add_argument("--record", default=str(ROOT / "profiles" / "round6" / "parity" / "dps_1000_steps.json"))
@@ -166,6 +294,18 @@ def main() -> int:
         res = compare(out, Path(a.record), a.tol)
         print(json.dumps(res, indent=1))
         return 0 if res["pass"] else 1
+    if a.phase == "onestep-gpu":
+        for case in cases:
+            run_onestep_gpu(case, out)
+        return 0
+    if a.phase in ("onestep-cpu", "perturb"):
+        fn = run_onestep_cpu if a.phase == "onestep-cpu" else run_perturb_gpu
+        rec = {case: fn(case, out) for case in cases}
+        path = Path(a.record).with_name(f"dps_1000_steps_{a.phase}.json")
+        path.parent.mkdir(parents=True, exist_ok=True)
+        path.write_text(json.dumps(rec, indent=1) + "\n")
+        print(json.dumps(rec, indent=1))
+        return 0
     for case in cases:
         (run_gpu if a.phase == "gpu" else run_cpu)(case, out)
     return 0

@@ -21,6 +21,8 @@ run() {  # run NAME SECONDS CMD...: log to $OUT/NAME.log; stop on a signal / tim
 for step in "$@"; do
     case $step in
         parity1000) run parity1000 600 python -u tools/parity_1000.py --phase gpu ;;
+        perturb) run perturb 600 python -u tools/parity_1000.py --phase perturb --record gpurun_out/r6/parity/dps_1000_steps.json ;;
+        onestep) run onestep 300 python -u tools/parity_1000.py --phase onestep-gpu --case identity ;;
         bf16tests) run bf16_tests 900 python -u -m pytest tests/test_bf16_gpu.py -v --timeout 400 --timeout-method thread ;;
         bf16kern) run bf16_kern 600 python -u -m pytest tests/test_bf16_gpu.py -v --timeout 300 --timeout-method thread -k "conv3x3 or groupnorm or attention" ;;
         psldbf16) run psld_bf16 900 python -u tools/bench_psld.py --dtype bf16 --steps 3 --warmup 2 --cpu-baseline ;;
