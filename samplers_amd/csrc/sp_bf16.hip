@@ -36,6 +36,11 @@ typedef unsigned bq_u2 __attribute__((ext_vector_type(2)));
 typedef __bf16 bq_bf8 __attribute__((ext_vector_type(8)));
 typedef unsigned short u16;
 
+#ifndef SP_CONV_ROW_REUSE
+#define SP_CONV_ROW_REUSE 1  // TC = 32 conv: B fragments shared by the taps of one column shift
+#endif
+constexpr bool kConvRowReuse = SP_CONV_ROW_REUSE != 0;
+
 __device__ __forceinline__ bq_f16 bq_mfma(bq_u4 a, bq_u4 b, bq_f16 c) {
     return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bq_bf8, a), __builtin_bit_cast(bq_bf8, b), c,
                                                    0, 0, 0);
@@ -194,6 +199,39 @@ __global__ __launch_bounds__(kBlock, TC == 4 ? 1 : 2) void k_conv3x3_bf16(const 
         if (ks + 1 < ks1) gload(ks + 1);
         const char* __restrict__ wl = lds + r * G::RB + hh * 16;
         const char* __restrict__ pl = lds + G::LW;
+        if constexpr (TC == 32 && kConvRowReuse) {
+            // TC = 32: the wave's pixel tile j is image row 4 wv + j, so tap (dy, dx) of tile j
+            // reads the B fragment of patch row j + dy, column shift dx — the fragment tile
+            // j + 1 reads at tap (dy - 1, dx).  Taps run dx-major: per dx, patch rows 0..5 of
+            // the wave (6 B fragments) serve all 12 (dy, j) pairs, so a stage reads 18 + 18
+            // fragments instead of 18 + 36.  Each tap's new fragments (2 A, and 4 B at dy = 0 /
+            // 1 B at dy = 1, 2) are read while the previous tap's 8 MFMAs run.
+            const char* __restrict__ bl = pl + ((4 * wv) * G::PW + r) * G::RB + hh * 16;
+            bq_u4 fa[9][2], fb[3][6];
+            auto lda = [&](int s) {
+                const int dx = s / 3, dy = s - 3 * dx, t = 3 * dy + dx;
+                fa[s][0] = *reinterpret_cast<const bq_u4*>(wl + (t * 64) * G::RB);
+                fa[s][1] = *reinterpret_cast<const bq_u4*>(wl + (t * 64 + 32) * G::RB);
+                if (dy == 0) {
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) fb[dx][i] = *reinterpret_cast<const bq_u4*>(bl + (i * G::PW + dx) * G::RB);
+                } else {
+                    fb[dx][dy + 3] = *reinterpret_cast<const bq_u4*>(bl + ((dy + 3) * G::PW + dx) * G::RB);
+                }
+            };
+            lda(0);
+#pragma unroll
+            for (int s = 0; s < 9; ++s) {
+                if (s + 1 < 9) lda(s + 1);
+                const int dx = s / 3, dy = s - 3 * dx;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    acc[0][j] = bq_mfma(fa[s][0], fb[dx][j + dy], acc[0][j]);
+                    acc[1][j] = bq_mfma(fa[s][1], fb[dx][j + dy], acc[1][j]);
+                }
+            }
+            continue;
+        }
         // fragments of tap t + 1 are read while tap t's 8 MFMAs run (two register sets)
         bq_u4 fa[2][2], fb[2][4];
         auto frags = [&](int t, int slot) {

@@ -227,6 +227,10 @@ __device__ __forceinline__ void g6_raw_x_tm(const unsigned char* raw, int pq, in
 }
 
 struct G6Pos { int n, p0, cb, kh; };
+#ifndef G6_DESC
+#define G6_DESC 0  // 1: per-tile X load descriptors advanced per k-step (round-6 A/B; else formed per load)
+#endif
+struct XDesc { int so, rem; };
 // SPLIT: the split-K kernels (a compile-time variant: the unsplit ones keep their registers)
 template <bool SPLIT>
 __device__ __forceinline__ G6Pos g6_pos(const G6Geom& g, int t) {
@@ -420,6 +424,25 @@ __device__ __forceinline__ void g6_body(const G6Geom& g, G6XSlot* xraw, G6WSlot*
         }
         return false;
     };
+#if G6_DESC
+    // Per-tile load descriptors of the X stream (NCHW X): this wave's load i reads channel
+    // 16 ks + G6_XP wv + i at k-step ks, an arithmetic progression — so its buffer resource and
+    // byte offset are formed once per tile and then advanced by one k-step's channel stride
+    // (one scalar add); `rem` = c1 - channel detects the one step at which the progression
+    // crosses from x1 into x2 (c1 % 8 == 0 only: a k-step may straddle the parts).
+    XDesc xd[G6_XP];
+    auto xdesc_init = [&]() {
+        const int ks = SPLIT ? cx.ps.kh * kper : 0;
+#pragma unroll
+        for (int i = 0; i < G6_XP; ++i) {
+            const int c = ks * G6_KC + G6_XP * wv + i;
+            const bool second = c >= g.c1;
+            xd[i].so = ((second ? c - g.c1 : c) * g.hw + cx.ps.p0) * 4;
+            xd[i].rem = g.c1 - c;
+        }
+    };
+    if constexpr (!LTM) xdesc_init();
+#endif
     auto dma_x = [&]() {
         if (cx.j < J) {
             const unsigned sl = xraw_lds + cx.slot * (G6_KC * G6_PX * 4);
@@ -429,13 +452,40 @@ __device__ __forceinline__ void g6_body(const G6Geom& g, G6XSlot* xraw, G6WSlot*
             g6_lds_dma(wrs, sl + (2 * wv) * 1024, lane * 16, 0);
             g6_lds_dma(wrs, sl + (2 * wv + 1) * 1024, lane * 16, 1024);
 #else
-            if constexpr (LTM) g6_dma_x_tm(g, cx.ps.n * g.hw + cx.ps.p0, ks, wv, lane, sl);
-            else g6_dma_x(g, xb1, xb2, cx.ps.p0, ks, wv, lane, sl);
+            if constexpr (LTM) {
+                g6_dma_x_tm(g, cx.ps.n * g.hw + cx.ps.p0, ks, wv, lane, sl);
+            } else {
+#if G6_DESC
+                (void)ks;
+#pragma unroll
+                for (int i = 0; i < G6_XP; ++i) {
+                    const bool second = xd[i].rem <= 0;
+                    const auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(second ? xb2 : xb1), (short)0,
+                                                                      (second ? g.c2 : g.c1) * g.hw * 4, 0x00020000);
+                    g6_lds_dma(rs, sl + (G6_XP * wv + i) * 1024, lane * 16, xd[i].so);
+                }
+#else
+                g6_dma_x(g, xb1, xb2, cx.ps.p0, ks, wv, lane, sl);
+#endif
+            }
 #endif
         }
         if (advance(cx, G6_NX) && !LTM) {
             xb1 = g.x1 + (int64_t)cx.ps.n * g.c1 * g.hw;
             xb2 = g.x2 + (int64_t)cx.ps.n * g.c2 * g.hw;
+#if G6_DESC
+            xdesc_init();
+        } else if (!LTM) {
+#pragma unroll
+            for (int i = 0; i < G6_XP; ++i) {
+                xd[i].rem -= G6_KC;
+                if (xd[i].rem > 0 || xd[i].rem <= -G6_KC) {
+                    xd[i].so += G6_KC * g.hw * 4;
+                } else {  // this step's channel is the first of x2 in the progression
+                    xd[i].so = (-xd[i].rem * g.hw + cx.ps.p0) * 4;
+                }
+            }
+#endif
         }
     };
     auto dma_w = [&]() {

@@ -15,7 +15,7 @@ for src in $(make -s -p -n 2>/dev/null | sed -n 's/^SRC := //p'); do
   # the Makefile's per-file flags
   extra=""; case "$(basename $src)" in
     sp_wino.hip) extra="-fno-slp-vectorize" ;;
-    sp_attention.hip|sp_attention6.hip) extra="-mllvm -amdgpu-mfma-vgpr-form=1" ;;
+    sp_attention.hip|sp_attention6.hip|sp_bf16.hip) extra="-mllvm -amdgpu-mfma-vgpr-form=1" ;;
   esac
   /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wall -Wno-unused-result $extra $flags -c $src -o $o &
   objs+=($o)

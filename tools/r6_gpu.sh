@@ -28,6 +28,14 @@ for step in "$@"; do
         psldbf16) run psld_bf16 900 python -u tools/bench_psld.py --dtype bf16 --steps 3 --warmup 2 --cpu-baseline ;;
         psldbf16q) run psld_bf16 600 python -u tools/bench_psld.py --dtype bf16 --steps 3 --warmup 2 ;;
         psldbf16prof) run psld_bf16_prof 900 rocprofv3 --kernel-trace --stats -d "$OUT/prof_psld_bf16" -o run -- python -u tools/bench_psld.py --dtype bf16 --steps 2 --warmup 1 ;;
+        convab) run conv_ab_base 300 env SAMPLERS_HIP_LIB=samplers_amd/lib/variants/lib_${BASE:-norr}.so python -u tools/bench_conv_bf16.py
+                run conv_ab_new 300 python -u tools/bench_conv_bf16.py ;;
+        psldab) run psld_ab_base 600 env SAMPLERS_HIP_LIB=samplers_amd/lib/variants/lib_${BASE:-norr}.so python -u tools/bench_psld.py --dtype bf16 --steps 3 --warmup 2
+                run psld_ab_new 600 python -u tools/bench_psld.py --dtype bf16 --steps 3 --warmup 2 ;;
+        x6ab) run x6_desc_tests 300 env SAMPLERS_HIP_LIB=samplers_amd/lib/variants/lib_desc.so python -u -m pytest tests/test_gemm_x6_gpu.py -x -q --timeout 200 --timeout-method thread
+              run x6_base 300 python -u tools/bench_gemm_x6.py
+              run x6_desc 300 env SAMPLERS_HIP_LIB=samplers_amd/lib/variants/lib_desc.so python -u tools/bench_gemm_x6.py
+              run x6_base2 300 python -u tools/bench_gemm_x6.py ;;
         convbf16) run conv_bf16 300 python -u tools/bench_conv_bf16.py --miopen ;;
         convbf16sq) FILTER=k_conv3x3_bf16 NAME=convbf16 run conv_bf16_sq 600 tools/sq_pmc.sh tools/bench_conv_bf16.py --reps 3 --shapes sd ;;
         gputests) run gpu_tests 1100 python -u -m pytest tests -m gpu -q --timeout 400 --timeout-method thread ;;
