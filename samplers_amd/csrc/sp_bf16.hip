@@ -534,7 +534,17 @@ __device__ __forceinline__ double wave_sum_d(double v) {
 }
 
 // forward finalize: one wave per (n, group).  stats = [mean | rstd] (n*groups each);
-// co = [sc | sh] (n*c each): y = x sc + sh.
+// co = [sc | sh] (n*c each): y = x sc + sh.  The group's (chunk, channel) partials are spread
+// over the wave's lanes (pair i = lane, lane + 64, ...: channel i % cpg of chunk i / cpg, so a
+// row of partials is read by consecutive lanes), each lane sums its pairs in a fixed order in
+// fp64, and the wave meets in a fixed butterfly — a handful of loads per lane instead of a
+// chain of `chunks` dependent loads on cpg lanes (4 of 64 at 128 channels / 32 groups).
+__device__ __forceinline__ float gnb_shift(const u16* __restrict__ x1, const u16* __restrict__ x2, int c1, int c2,
+                                           const float* __restrict__ cbias, int64_t nn, int64_t hw, int c, int ch) {
+    const float cbv = cbias ? cbias[nn * c + ch] : 0.f;
+    return (ch < c1 ? bf1(x1[nn * hw * c1 + ch]) : bf1(x2[nn * hw * c2 + ch - c1])) + cbv;
+}
+
 __global__ __launch_bounds__(64) void k_gnb_final_fwd(const u16* __restrict__ x1, const u16* __restrict__ x2, int c1,
                                                       int c2, const float* __restrict__ cbias,
                                                       const float* __restrict__ part, int chunks, int64_t hw,
@@ -543,30 +553,29 @@ __global__ __launch_bounds__(64) void k_gnb_final_fwd(const u16* __restrict__ x1
                                                       float* __restrict__ co) {
     const int c = c1 + c2, cpg = c / groups, g = blockIdx.x, nn = blockIdx.y, lane = threadIdx.x;
     const int64_t ng = (int64_t)gridDim.y * groups;
-    double sa = 0.0, sx = 0.0;
-    // pass 1: group sum of x~ (shift s_c re-read from the sample's first pixel)
-    for (int cc = lane; cc < cpg; cc += 64) {
-        const int ch = g * cpg + cc;
-        const float cbv = cbias ? cbias[(int64_t)nn * c + ch] : 0.f;
-        const float s = (ch < c1 ? bf1(x1[(int64_t)nn * hw * c1 + ch]) : bf1(x2[(int64_t)nn * hw * c2 + ch - c1])) + cbv;
-        double a = 0.0;
-        for (int k = 0; k < chunks; ++k) a += part[(((int64_t)nn * chunks + k) * 2) * c + ch];
-        sa += a + (double)hw * s;
+    const int pairs = cpg * chunks;
+    const float* __restrict__ pb = part + (int64_t)nn * chunks * 2 * c + g * cpg;  // chunk 0, first channel
+    // pass 1: group sum of x~ = sum of the shifted partials + hw * shift per channel
+    double sa = 0.0;
+    for (int i = lane; i < pairs; i += 64) {
+        const int k = i / cpg, cc = i - k * cpg;
+        sa += pb[(int64_t)k * 2 * c + cc];
     }
+    for (int cc = lane; cc < cpg; cc += 64)
+        sa += (double)hw * gnb_shift(x1, x2, c1, c2, cbias, nn, hw, c, g * cpg + cc);
     const double cnt = (double)hw * cpg;
     const double mean = wave_sum_d(sa) / cnt;
+    // pass 2: sum (x~ - mean)^2 = sum_c [S2_c + 2 dm_c S1_c + hw dm_c^2], dm_c = shift_c - mean
+    double sx = 0.0;
+    for (int i = lane; i < pairs; i += 64) {
+        const int k = i / cpg, cc = i - k * cpg;
+        const float* pp = pb + (int64_t)k * 2 * c + cc;
+        const double dm = (double)gnb_shift(x1, x2, c1, c2, cbias, nn, hw, c, g * cpg + cc) - mean;
+        sx += pp[c] + 2.0 * dm * pp[0];
+    }
     for (int cc = lane; cc < cpg; cc += 64) {
-        const int ch = g * cpg + cc;
-        const float cbv = cbias ? cbias[(int64_t)nn * c + ch] : 0.f;
-        const float s = (ch < c1 ? bf1(x1[(int64_t)nn * hw * c1 + ch]) : bf1(x2[(int64_t)nn * hw * c2 + ch - c1])) + cbv;
-        double a = 0.0, b = 0.0;
-        for (int k = 0; k < chunks; ++k) {
-            const float* pp = part + (((int64_t)nn * chunks + k) * 2) * c + ch;
-            a += pp[0];
-            b += pp[c];
-        }
-        const double dm = (double)s - mean;
-        sx += b + 2.0 * dm * a + (double)hw * dm * dm;
+        const double dm = (double)gnb_shift(x1, x2, c1, c2, cbias, nn, hw, c, g * cpg + cc) - mean;
+        sx += (double)hw * dm * dm;
     }
     const double var = std::max(0.0, wave_sum_d(sx) / cnt);
     const float rstd = (float)(1.0 / sqrt(var + (double)eps));
@@ -607,14 +616,14 @@ __global__ __launch_bounds__(64) void k_gnb_final_bwd(const float* __restrict__ 
                                                       const float* __restrict__ gamma, const float* __restrict__ co,
                                                       float* __restrict__ co2) {
     const int cpg = c / groups, g = blockIdx.x, nn = blockIdx.y, lane = threadIdx.x, n = gridDim.y;
-    double s1 = 0.0, s2 = 0.0;
-    for (int cc = lane; cc < cpg; cc += 64) {
-        const int ch = g * cpg + cc;
-        for (int k = 0; k < chunks; ++k) {
-            const float* pp = part + (((int64_t)nn * chunks + k) * 2) * c + ch;
-            s1 += pp[0];
-            s2 += pp[c];
-        }
+    const int pairs = cpg * chunks;
+    const float* __restrict__ pb = part + (int64_t)nn * chunks * 2 * c + g * cpg;
+    double s1 = 0.0, s2 = 0.0;  // (chunk, channel) pairs spread over the lanes as k_gnb_final_fwd
+    for (int i = lane; i < pairs; i += 64) {
+        const int k = i / cpg, cc = i - k * cpg;
+        const float* pp = pb + (int64_t)k * 2 * c + cc;
+        s1 += pp[0];
+        s2 += pp[c];
     }
     const double cnt = (double)hw * cpg;
     const float m1 = (float)(wave_sum_d(s1) / cnt), m2 = (float)(wave_sum_d(s2) / cnt);

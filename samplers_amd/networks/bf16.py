@@ -269,22 +269,49 @@ def _gn_ws(lib, n: int, c: int, hw: int, device) -> tuple[Tensor, int]:
     return torch.empty(nb, device=device, dtype=torch.uint8), nb
 
 
+def _gn_fwd_raw(norm: nn.GroupNorm, x1: Tensor, x2: Tensor | None, cb: Tensor | None) -> tuple[Tensor, Tensor]:
+    """(z, stats) of ``sp_groupnorm_bf16_fwd`` over cat(x1, x2) (+ cb) read in place."""
+    lib = _hip.load_library()
+    n, c1, h, w = x1.shape
+    c2 = 0 if x2 is None else x2.shape[1]
+    c, hw, g = c1 + c2, h * w, norm.num_groups
+    gamma, beta = _gn_params(norm)
+    z = torch.empty(n, c, h, w, device=x1.device, dtype=BF16, memory_format=CL)
+    stats = torch.empty(2, n * g, device=x1.device, dtype=torch.float32)
+    ws, nb = _gn_ws(lib, n, c, hw, x1.device)
+    _hip.check(lib.sp_groupnorm_bf16_fwd(_p(x1), _p(x2), c1, c2, None if cb is None else cb.data_ptr(),
+                                         None if gamma is None else gamma.data_ptr(),
+                                         None if beta is None else beta.data_ptr(), n, hw, g, float(norm.eps),
+                                         int(norm.act), _p(z), stats.data_ptr(), ws.data_ptr(), nb,
+                                         _hip.stream_of(x1)), "sp_groupnorm_bf16_fwd")
+    return z, stats
+
+
+def _gn_bwd_raw(norm: nn.GroupNorm, dz: Tensor, x1: Tensor, x2: Tensor | None, cb: Tensor | None, stats: Tensor,
+                add1: Tensor | None = None, add2: Tensor | None = None, out1: Tensor | None = None,
+                out2: Tensor | None = None) -> tuple[Tensor, Tensor | None]:
+    """Input VJP of ``_gn_fwd_raw`` into the parts' layouts, + the addends (channels-last, shaped
+    like the parts) added in the kernel; ``out1`` / ``out2`` may be the addends (in place)."""
+    lib = _hip.load_library()
+    n, c1, h, w = x1.shape
+    c2 = 0 if x2 is None else x2.shape[1]
+    gamma, beta = _gn_params(norm)
+    dz = nhwc(dz.to(BF16))
+    dx1 = torch.empty_like(x1, memory_format=CL) if out1 is None else out1
+    dx2 = None if x2 is None else (torch.empty_like(x2, memory_format=CL) if out2 is None else out2)
+    ws, nb = _gn_ws(lib, n, c1 + c2, h * w, x1.device)
+    _hip.check(lib.sp_groupnorm_bf16_bwd(_p(dz), _p(x1), _p(x2), c1, c2, None if cb is None else cb.data_ptr(),
+                                         None if gamma is None else gamma.data_ptr(),
+                                         None if beta is None else beta.data_ptr(), stats.data_ptr(), n, h * w,
+                                         norm.num_groups, int(norm.act), _p(dx1), _p(dx2), _p(add1), _p(add2), None,
+                                         ws.data_ptr(), nb, _hip.stream_of(dz)), "sp_groupnorm_bf16_bwd")
+    return dx1, dx2
+
+
 class _GroupNormBf16Fn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x1, x2, norm, cb):
-        lib = _hip.load_library()
-        n, c1, h, w = x1.shape
-        c2 = 0 if x2 is None else x2.shape[1]
-        c, hw, g = c1 + c2, h * w, norm.num_groups
-        gamma, beta = _gn_params(norm)
-        z = torch.empty(n, c, h, w, device=x1.device, dtype=BF16, memory_format=CL)
-        stats = torch.empty(2, n * g, device=x1.device, dtype=torch.float32)
-        ws, nb = _gn_ws(lib, n, c, hw, x1.device)
-        _hip.check(lib.sp_groupnorm_bf16_fwd(_p(x1), _p(x2), c1, c2, None if cb is None else cb.data_ptr(),
-                                             None if gamma is None else gamma.data_ptr(),
-                                             None if beta is None else beta.data_ptr(), n, hw, g, float(norm.eps),
-                                             int(norm.act), _p(z), stats.data_ptr(), ws.data_ptr(), nb,
-                                             _hip.stream_of(x1)), "sp_groupnorm_bf16_fwd")
+        z, stats = _gn_fwd_raw(norm, x1, x2, cb)
         ctx.save_for_backward(x1, x2, cb, stats)
         ctx.norm = norm
         return z
@@ -292,20 +319,7 @@ class _GroupNormBf16Fn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dz):
         x1, x2, cb, stats = ctx.saved_tensors
-        norm = ctx.norm
-        lib = _hip.load_library()
-        n, c1, h, w = x1.shape
-        c2 = 0 if x2 is None else x2.shape[1]
-        gamma, beta = _gn_params(norm)
-        dz = nhwc(dz.to(BF16))
-        dx1 = torch.empty_like(x1, memory_format=CL)
-        dx2 = None if x2 is None else torch.empty_like(x2, memory_format=CL)
-        ws, nb = _gn_ws(lib, n, c1 + c2, h * w, x1.device)
-        _hip.check(lib.sp_groupnorm_bf16_bwd(_p(dz), _p(x1), _p(x2), c1, c2, None if cb is None else cb.data_ptr(),
-                                             None if gamma is None else gamma.data_ptr(),
-                                             None if beta is None else beta.data_ptr(), stats.data_ptr(), n, h * w,
-                                             norm.num_groups, int(norm.act), _p(dx1), _p(dx2), None, None, None,
-                                             ws.data_ptr(), nb, _hip.stream_of(dz)), "sp_groupnorm_bf16_bwd")
+        dx1, dx2 = _gn_bwd_raw(ctx.norm, dz, x1, x2, cb, stats)
         return dx1, dx2, None, None
 
 
@@ -320,6 +334,117 @@ def group_norm(norm: nn.GroupNorm, x1: Tensor, x2: Tensor | None = None, chan_bi
     parts read in place."""
     cb = None if chan_bias is None else chan_bias.detach().to(torch.float32).reshape(x1.shape[0], -1).contiguous()
     return _GroupNormBf16Fn.apply(nhwc(x1), None if x2 is None else nhwc(x2), norm, cb)
+
+
+# ---------------------------------------------------------------------------------------------
+# ResnetBlock2D as one autograd function
+# ---------------------------------------------------------------------------------------------
+
+def _rows(t: Tensor) -> Tensor:
+    """A channels-last (n, c, h, w) tensor as its [n h w][c] pixel rows (a view)."""
+    return t.permute(0, 2, 3, 1).reshape(-1, t.shape[1])
+
+
+def _shortcut_w(block: nn.Module, c1: int) -> tuple[Tensor, Tensor]:
+    """conv_shortcut's [cout][cin] weight split at c1 (x's channels | the skip's), contiguous."""
+    w = block.conv_shortcut.weight
+    return _cached(block.conv_shortcut, f"split{c1}", _wkey(w),
+                   lambda: tuple(t.contiguous() for t in w.detach().reshape(w.shape[0], -1).split(
+                       [c1, w.shape[1] - c1], dim=1)))
+
+
+class _ResnetBlockBf16Fn(torch.autograd.Function):
+    """A whole ResnetBlock2D at bf16 (the structure of unet2d._ResnetBlockFn):
+
+    fwd  z1 = silu(GN1(cat(x1, x2)))   both parts read in place
+         h1 = conv1(z1)
+         z2 = silu(GN2(h1 + tb))
+         out = conv2(z2) + shortcut(x)   the shortcut added in conv2's epilogue; a 1x1 shortcut
+                                         over cat(x1, x2) is two GEMMs over the parts' rows (no cat)
+    bwd  dx = GN1^T(conv1^T(GN2^T(conv2^T dout))) + shortcut^T dout, the shortcut's gradient
+         added by GN1's VJP kernel into the parts' gradients (no autograd accumulation add).
+    Saves x1, x2, h1 and the GroupNorm statistics (weights are frozen: no z1 / z2)."""
+
+    @staticmethod
+    def forward(ctx, block, tb, x1, x2):
+        cout = block.conv2.weight.shape[0]
+        z1, st1 = _gn_fwd_raw(block.norm1, x1, x2, None)
+        h1 = _conv_launch(z1, conv_pack(block.conv1, False), _bias_f32(block.conv1, block.conv1.bias), None,
+                          block.conv1.weight.shape[0])
+        del z1
+        z2, st2 = _gn_fwd_raw(block.norm2, h1, None, tb)
+        if block.conv_shortcut is None:
+            short = x1
+        else:
+            c1 = x1.shape[1]
+            w1, w2 = _shortcut_w(block, c1)
+            n, _, h, w = x1.shape
+            b = block.conv_shortcut.bias
+            r = (torch.addmm(b, _rows(x1), w1.t()) if b is not None else _rows(x1) @ w1.t())
+            if x2 is not None:
+                r.addmm_(_rows(x2), w2.t())
+            short = r.reshape(n, h, w, cout).permute(0, 3, 1, 2)
+        out = _conv_launch(z2, conv_pack(block.conv2, False), _bias_f32(block.conv2, block.conv2.bias), short, cout)
+        ctx.block = block
+        ctx.save_for_backward(x1, x2, h1, tb, st1, st2)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        x1, x2, h1, tb, st1, st2 = ctx.saved_tensors
+        blk = ctx.block
+        dout = nhwc(dout.to(BF16))
+        cout = blk.conv2.weight.shape[0]
+        dz2 = _conv_launch(_pad_channels(dout, _ceil(cout, 16)), conv_pack(blk.conv2, True), None, None, cout)
+        dh1, _ = _gn_bwd_raw(blk.norm2, dz2, h1, None, tb, st2)
+        del dz2
+        cmid = blk.conv1.weight.shape[0]
+        dz1 = _conv_launch(_pad_channels(dh1, _ceil(cmid, 16)), conv_pack(blk.conv1, True), None, None,
+                           blk.conv1.weight.shape[1])
+        del dh1
+        if blk.conv_shortcut is None:  # identity shortcut: dx1 = GN1^T dz1 + dout
+            dx1, dx2 = _gn_bwd_raw(blk.norm1, dz1, x1, x2, None, st1, add1=dout)
+        else:  # s = shortcut^T dout per part (pixel rows), then += GN1^T dz1 in place
+            c1 = x1.shape[1]
+            w1, w2 = _shortcut_w(blk, c1)
+            n, _, h, w = x1.shape
+            d = _rows(dout)
+            s1 = (d @ w1).reshape(n, h, w, c1).permute(0, 3, 1, 2)
+            s2 = None if x2 is None else (d @ w2).reshape(n, h, w, x2.shape[1]).permute(0, 3, 1, 2)
+            dx1, dx2 = _gn_bwd_raw(blk.norm1, dz1, x1, x2, None, st1, add1=s1, add2=s2, out1=s1, out2=s2)
+        return None, None, dx1, dx2
+
+
+def resnet_block_supported(block: nn.Module, x: Tensor, skip: Tensor | None) -> bool:
+    """Whether ``resnet_block`` serves the block: bf16 device tensors, frozen weights, both 3x3
+    convolutions and both norms on the bf16 kernels, channel counts in whole 16-blocks
+    (``SAMPLERS_AMD_BF16_RESNET=0``: module by module, for A/B measurements)."""
+    import os
+
+    if os.environ.get("SAMPLERS_AMD_BF16_RESNET", "1") == "0":
+        return False
+    if not is_bf16_device(x) or x.dim() != 4 or (skip is not None and not is_bf16_device(skip)):
+        return False
+    c2 = 0 if skip is None else skip.shape[1]
+    cin, cout = x.shape[1] + c2, block.conv2.weight.shape[0]
+    if cin % 16 or cout % 16 or block.conv1.weight.shape[1] != cin or block.conv1.weight.shape[0] != cout:
+        return False
+    if block.conv_shortcut is None and skip is not None:  # an identity shortcut of cat(x, skip)
+        return False
+    if any(p.requires_grad for p in block.parameters()):
+        return False
+    lib = _hip.load_library()
+    n, _, h, w = x.shape
+    return bool(lib.sp_groupnorm_bf16_supported(x.shape[1], c2, block.norm1.num_groups)
+                and lib.sp_groupnorm_bf16_supported(cout, 0, block.norm2.num_groups)
+                and lib.sp_conv3x3_bf16_supported(cin, cout, h, w) and lib.sp_conv3x3_bf16_supported(cout, cout, h, w))
+
+
+def resnet_block(block: nn.Module, x: Tensor, skip: Tensor | None, tb: Tensor | None) -> Tensor:
+    """``block(x, temb, skip)`` at bf16 as ``_ResnetBlockBf16Fn`` (``tb``: the block's
+    time-embedding projection, [n, cout], or None)."""
+    cb = None if tb is None else tb.detach().to(torch.float32).reshape(x.shape[0], -1).contiguous()
+    return _ResnetBlockBf16Fn.apply(block, cb, nhwc(x), None if skip is None else nhwc(skip))
 
 
 # ---------------------------------------------------------------------------------------------

@@ -360,12 +360,16 @@ class ResnetBlock2D(nn.Module):
                       box_out: SkipGrad | None) -> Tensor:
         """The block at bf16 on the NHWC kernels (networks/bf16.py): GN1 over cat(x, skip) read in
         place, conv1, GN2 with the time-embedding bias, conv2 with the shortcut added in its
-        epilogue; autograd sums the skip gradients (the SkipGrad hand-offs are fp32-only)."""
+        epilogue — as one autograd function (``bf16.resnet_block``) where the kernels serve the
+        shapes, module by module otherwise; autograd sums the skip gradients (the SkipGrad
+        hand-offs are fp32-only)."""
         from . import bf16
 
         for box in (box_in, box_out):
             if box is not None:
                 box.enabled = False
+        if bf16.resnet_block_supported(self, x, skip):
+            return bf16.resnet_block(self, x, skip, tb)
         c2 = 0 if skip is None else skip.shape[1]
         if bf16.group_norm_supported(self.norm1, x, c2):
             z1 = bf16.group_norm(self.norm1, x, skip)

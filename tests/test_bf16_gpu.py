@@ -54,9 +54,11 @@ def _kernel_names(fn) -> set[str]:
 
 
 def _no_miopen_conv(names: set[str]) -> None:
+    """No MIOpen / torch convolution kernel ran (this project's sp:: kernels — the conv tile and its
+    split-K reduce — are the only convolution code allowed)."""
     bad = {n for n in names if ("conv" in n.lower() or "miopen" in n.lower() or "igemm" in n.lower())
-           and "k_conv3x3_bf16" not in n}
-    assert not bad, f"convolutions outside sp::k_conv3x3_bf16: {sorted(bad)[:5]}"
+           and not n.startswith("sp::") and "void sp::" not in n}
+    assert not bad, f"convolutions outside this project's kernels: {sorted(bad)[:5]}"
 
 
 # ---- kernels ------------------------------------------------------------------------------------

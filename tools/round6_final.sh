@@ -4,7 +4,8 @@
 # record carries its CPU baseline (the oracle on the box's host cores, same workload).
 #   PART=benches   DPS bench records: headline inpaint, blur, identity B = 1 (eager and hipGraph),
 #                  512² at B = 16
-#   PART=latent    PSLD fp32 / bf16 (with and without CFG) and ReSample with their CPU baselines
+#   PART=latent    PSLD fp32 / bf16 (with and without CFG) with their CPU baselines
+#   PART=resample  ReSample pieces + the whole-call projection with its CPU baseline
 #   PART=dist      2- / 8-rank self-launch rehearsals over gloo and a whole 1000-step B = 1 call
 #   PART=profiles  rocprofv3 kernel statistics of the DPS (B = 64, B = 1) and PSLD fp32 / bf16 benches
 set -o pipefail
@@ -25,6 +26,7 @@ elif [ "$PART" = latent ]; then
   step 400 bench_psld_bf16.log python -u tools/bench_psld.py --dtype bf16 --cpu-baseline
   step 400 bench_psld_cfg.log python -u tools/bench_psld.py --cfg --cpu-baseline
   step 400 bench_psld_bf16_cfg.log python -u tools/bench_psld.py --dtype bf16 --cfg --cpu-baseline
+elif [ "$PART" = resample ]; then
   step 1100 bench_resample.log python -u tools/bench_resample.py --cpu-baseline --pixel-iters 2000 --latent-iters 200 --heartbeat $O/rs_heartbeat.log
 elif [ "$PART" = dist ]; then
   step 300 bench_call_b1.log python -u tools/bench_call.py --batch 1 --steps 1000
