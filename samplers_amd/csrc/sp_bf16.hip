@@ -36,10 +36,6 @@ typedef unsigned bq_u2 __attribute__((ext_vector_type(2)));
 typedef __bf16 bq_bf8 __attribute__((ext_vector_type(8)));
 typedef unsigned short u16;
 
-#ifndef SP_CONV_ROW_REUSE
-#define SP_CONV_ROW_REUSE 1  // TC = 32 conv: B fragments shared by the taps of one column shift
-#endif
-constexpr bool kConvRowReuse = SP_CONV_ROW_REUSE != 0;
 
 __device__ __forceinline__ bq_f16 bq_mfma(bq_u4 a, bq_u4 b, bq_f16 c) {
     return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bq_bf8, a), __builtin_bit_cast(bq_bf8, b), c,
@@ -87,10 +83,16 @@ struct CvGeo {
     static constexpr int PW = TC + 2;                 // patch columns
     static constexpr int PH = S * (SR + 2);           // patch rows
     static constexpr int PQ = PH * PW;                // patch pixels
-    static constexpr int RB = 48;                     // LDS bytes per row
+    // TC = 32: 32-byte rows with the two 16-byte halves swapped on every other group of 8 rows
+    // (weights) / 8 columns (patch) — conflict-free for the fragment reads — and two stage
+    // buffers; else 48-byte rows (32 bytes + 16 pad), one buffer
+    static constexpr bool DB = TC == 32;
+    static constexpr int RB = DB ? 32 : 48;           // LDS bytes per row
     static constexpr int WROWS = 9 * 64;              // weight rows per stage
     static constexpr int LW = WROWS * RB;
     static constexpr int LP = PQ * RB;
+    static constexpr int BUF = LW + LP;               // one stage
+    static constexpr int LDS = DB ? 2 * BUF : BUF;
     static constexpr int NW = (WROWS * 2 + kBlock - 1) / kBlock;  // 16-byte weight pieces per thread
     static constexpr int PQP = PQ;
     static constexpr int NP = (PQP * 2 + kBlock - 1) / kBlock;    // 16-byte patch pieces per thread
@@ -114,7 +116,7 @@ __global__ __launch_bounds__(kBlock, TC == 4 ? 1 : 2) void k_conv3x3_bf16(const 
                                                          int n, int cin, int cout, int h, int w,
                                                          u16* __restrict__ y, float* __restrict__ part) {
     using G = CvGeo<TC>;
-    __shared__ __attribute__((aligned(16))) char lds[G::LW + G::LP];
+    __shared__ __attribute__((aligned(16))) char lds[G::LDS];
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, r = lane & 31, hh = lane >> 5;
     const int cb = blockIdx.x, pt = blockIdx.y;
     int n0, h0, c0;
@@ -191,32 +193,50 @@ __global__ __launch_bounds__(kBlock, TC == 4 ? 1 : 2) void k_conv3x3_bf16(const 
 
     const int kz = blockIdx.z, nz = gridDim.z;
     const int ks0 = kz * nci / nz, ks1 = (kz + 1) * nci / nz;
-    gload(ks0);
-    for (int ks = ks0; ks < ks1; ++ks) {
-        __syncthreads();  // the previous stage's fragment reads are done
-        lstore();
-        __syncthreads();
-        if (ks + 1 < ks1) gload(ks + 1);
-        const char* __restrict__ wl = lds + r * G::RB + hh * 16;
-        const char* __restrict__ pl = lds + G::LW;
-        if constexpr (TC == 32 && kConvRowReuse) {
-            // TC = 32: the wave's pixel tile j is image row 4 wv + j, so tap (dy, dx) of tile j
-            // reads the B fragment of patch row j + dy, column shift dx — the fragment tile
-            // j + 1 reads at tap (dy - 1, dx).  Taps run dx-major: per dx, patch rows 0..5 of
-            // the wave (6 B fragments) serve all 12 (dy, j) pairs, so a stage reads 18 + 18
-            // fragments instead of 18 + 36.  Each tap's new fragments (2 A, and 4 B at dy = 0 /
-            // 1 B at dy = 1, 2) are read while the previous tap's 8 MFMAs run.
-            const char* __restrict__ bl = pl + ((4 * wv) * G::PW + r) * G::RB + hh * 16;
+    if constexpr (G::DB) {
+        // Two stage buffers, one barrier per stage: stage s + 1 (in registers since stage s - 1)
+        // is written to the other buffer and stage s + 2's global loads are issued before stage
+        // s's MFMAs; the barrier after them both publishes stage s + 1 and frees stage s's buffer.
+        // Swizzle: weight row wr keeps its 16-byte half c at (c ^ (wr >> 3 & 1)); patch pixel q
+        // (column q % PW) at (c ^ (q % PW >> 3 & 1)) — the 16-lane groups of a ds_read_b128 then
+        // read 16 distinct 16-byte slots of the 256-byte bank row for any column offset.
+        auto lstore_db = [&](int b) {
+            char* __restrict__ base = lds + b * G::BUF;
+#pragma unroll
+            for (int k = 0; k < G::NW; ++k) {
+                const int i = tid + k * kBlock;
+                if (i < G::WROWS * 2) {
+                    const int wr = cv_row(i);
+                    *reinterpret_cast<bq_u4*>(base + wr * 32 + ((cv_chunk(i) ^ ((wr >> 3) & 1)) << 4)) = sw[k];
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < G::NP; ++k) {
+                const int i = tid + k * kBlock;
+                if (i < 2 * G::PQP && cv_row(i) < G::PQ) {
+                    const int q = cv_row(i), col = q % G::PW;
+                    *reinterpret_cast<bq_u4*>(base + G::LW + q * 32 + ((cv_chunk(i) ^ ((col >> 3) & 1)) << 4)) = spx[k];
+                }
+            }
+        };
+        // per-lane fragment offsets: A row 64 t + 32 a + r (its swizzle bit is r's); B pixel
+        // (4 wv + i) PW + r + dx, column r + dx
+        const int wl_lane = r * 32 + ((hh ^ ((r >> 3) & 1)) << 4);
+        int bl_lane[3];
+#pragma unroll
+        for (int dx = 0; dx < 3; ++dx) bl_lane[dx] = G::LW + (4 * wv * G::PW + r + dx) * 32 + ((hh ^ (((r + dx) >> 3) & 1)) << 4);
+        auto compute = [&](int b) {
+            const char* __restrict__ base = lds + b * G::BUF;
             bq_u4 fa[9][2], fb[3][6];
             auto lda = [&](int s) {
                 const int dx = s / 3, dy = s - 3 * dx, t = 3 * dy + dx;
-                fa[s][0] = *reinterpret_cast<const bq_u4*>(wl + (t * 64) * G::RB);
-                fa[s][1] = *reinterpret_cast<const bq_u4*>(wl + (t * 64 + 32) * G::RB);
+                fa[s][0] = *reinterpret_cast<const bq_u4*>(base + wl_lane + (t * 64) * 32);
+                fa[s][1] = *reinterpret_cast<const bq_u4*>(base + wl_lane + (t * 64 + 32) * 32);
                 if (dy == 0) {
 #pragma unroll
-                    for (int i = 0; i < 4; ++i) fb[dx][i] = *reinterpret_cast<const bq_u4*>(bl + (i * G::PW + dx) * G::RB);
+                    for (int i = 0; i < 4; ++i) fb[dx][i] = *reinterpret_cast<const bq_u4*>(base + bl_lane[dx] + i * G::PW * 32);
                 } else {
-                    fb[dx][dy + 3] = *reinterpret_cast<const bq_u4*>(bl + ((dy + 3) * G::PW + dx) * G::RB);
+                    fb[dx][dy + 3] = *reinterpret_cast<const bq_u4*>(base + bl_lane[dx] + (dy + 3) * G::PW * 32);
                 }
             };
             lda(0);
@@ -229,28 +249,67 @@ __global__ __launch_bounds__(kBlock, TC == 4 ? 1 : 2) void k_conv3x3_bf16(const 
                     acc[0][j] = bq_mfma(fa[s][0], fb[dx][j + dy], acc[0][j]);
                     acc[1][j] = bq_mfma(fa[s][1], fb[dx][j + dy], acc[1][j]);
                 }
+                // issue order pinned: tap s + 1's fragment reads, then tap s's 8 MFMAs (left to
+                // itself the scheduler sinks each read to just before its first use, so every
+                // tap waited for its LDS latency behind a single MFMA: MFMA busy 0.52)
+                if (s + 1 < 9) {
+                    const int dx1 = (s + 1) / 3, dy1 = (s + 1) - 3 * dx1;
+                    if (dy1 == 0) __builtin_amdgcn_sched_group_barrier(0x100, 6, 0);
+                    else __builtin_amdgcn_sched_group_barrier(0x100, 3, 0);
+                }
+                __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);
+                __builtin_amdgcn_sched_barrier(0);
             }
-            continue;
-        }
-        // fragments of tap t + 1 are read while tap t's 8 MFMAs run (two register sets)
-        bq_u4 fa[2][2], fb[2][4];
-        auto frags = [&](int t, int slot) {
-            const int dy = t / 3, dx = t - 3 * (t / 3);
-            fa[slot][0] = *reinterpret_cast<const bq_u4*>(wl + (t * 64) * G::RB);
-            fa[slot][1] = *reinterpret_cast<const bq_u4*>(wl + (t * 64 + 32) * G::RB);
-#pragma unroll
-            for (int j = 0; j < 4; ++j)
-                fb[slot][j] = *reinterpret_cast<const bq_u4*>(pl + qb[j] + (dy * G::PW + dx) * G::RB);
         };
-        frags(0, 0);
+        const int nst = ks1 - ks0;
+        gload(ks0);
+        lstore_db(0);
+        if (nst > 1) gload(ks0 + 1);
+        __syncthreads();
+        for (int s = 0; s < nst; ++s) {
+            const int b = s & 1;
+            if (s + 1 < nst) lstore_db(b ^ 1);
+            if (s + 2 < nst) gload(ks0 + s + 2);
+            __builtin_amdgcn_sched_barrier(0);
+            compute(b);
+            __syncthreads();
+        }
+    } else {
+        gload(ks0);
+        for (int ks = ks0; ks < ks1; ++ks) {
+            __syncthreads();  // the previous stage's fragment reads are done
+            lstore();
+            __syncthreads();
+            if (ks + 1 < ks1) gload(ks + 1);
+            const char* __restrict__ wl = lds + r * G::RB + hh * 16;
+            const char* __restrict__ pl = lds + G::LW;
+            // fragments of tap t + 1 are read while tap t's 8 MFMAs run (two register sets)
+            bq_u4 fa[2][2], fb[2][4];
+            auto frags = [&](int t, int slot) {
+                const int dy = t / 3, dx = t - 3 * (t / 3);
+                fa[slot][0] = *reinterpret_cast<const bq_u4*>(wl + (t * 64) * G::RB);
+                fa[slot][1] = *reinterpret_cast<const bq_u4*>(wl + (t * 64 + 32) * G::RB);
 #pragma unroll
-        for (int t = 0; t < 9; ++t) {
-            if (t + 1 < 9) frags(t + 1, (t + 1) & 1);
-            const int sl = t & 1;
+                for (int j = 0; j < 4; ++j)
+                    fb[slot][j] = *reinterpret_cast<const bq_u4*>(pl + qb[j] + (dy * G::PW + dx) * G::RB);
+            };
+            frags(0, 0);
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                acc[0][j] = bq_mfma(fa[sl][0], fb[sl][j], acc[0][j]);
-                acc[1][j] = bq_mfma(fa[sl][1], fb[sl][j], acc[1][j]);
+            for (int t = 0; t < 9; ++t) {
+                if (t + 1 < 9) frags(t + 1, (t + 1) & 1);
+                const int sl = t & 1;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    acc[0][j] = bq_mfma(fa[sl][0], fb[sl][j], acc[0][j]);
+                    acc[1][j] = bq_mfma(fa[sl][1], fb[sl][j], acc[1][j]);
+                }
+                // tap t + 1's 6 reads, then tap t's 8 MFMAs (as the TC = 32 loop; TC = 8 holds
+                // 7 staged patch pieces per thread and would spill with both register sets live)
+                if constexpr (TC != 8) {
+                    if (t + 1 < 9) __builtin_amdgcn_sched_group_barrier(0x100, 6, 0);
+                    __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);
+                    __builtin_amdgcn_sched_barrier(0);
+                }
             }
         }
     }
