@@ -472,6 +472,9 @@ __global__ __launch_bounds__(kBlock) void k_pool2x2_bf16(const u16* __restrict__
 // (y = x sc + sh); VJP -> the per-(n, c) coefficients of dx = A dy' + B x + D.
 // ---------------------------------------------------------------------------------------------
 constexpr int GNB_TARGET_BLOCKS = 2048;
+#ifndef GNB_U
+#define GNB_U 4  // pixels whose loads a thread keeps in flight in the streaming GroupNorm loops
+#endif
 
 struct GnbGeo {
     int cv, rows, chunks, chunk_px;
@@ -537,10 +540,12 @@ __global__ __launch_bounds__(kBlock) void k_gnb_stats(const u16* __restrict__ x1
                     gm[e] = gamma[8 * j + e];
                 }
             }
-            for (int64_t p = p0 + row; p < p1; p += rows_here) {
+            // one pixel's contribution, from its loaded vectors (x; dz for the VJP)
+            auto acc1 = [&](bq_u4 xv, bq_u4 dzv) {
                 float f[8];
-                unpack8(gnb_ld(x1, x2, c1, c2, nn, hw, p, j), f);
+                unpack8(xv, f);
                 if constexpr (MODE == 0) {
+                    (void)dzv;
 #pragma unroll
                     for (int e = 0; e < 8; ++e) {
                         const float d = f[e] + cbv[e] - sh[e];
@@ -549,7 +554,7 @@ __global__ __launch_bounds__(kBlock) void k_gnb_stats(const u16* __restrict__ x1
                     }
                 } else {
                     float dv[8];
-                    unpack8(*reinterpret_cast<const bq_u4*>(dz + ((int64_t)nn * hw + p) * c + 8 * j), dv);
+                    unpack8(dzv, dv);
 #pragma unroll
                     for (int e = 0; e < 8; ++e) {
                         const float yv = fmaf(f[e], k0[e], k1[e]);
@@ -564,7 +569,25 @@ __global__ __launch_bounds__(kBlock) void k_gnb_stats(const u16* __restrict__ x1
                         s2[e] = fmaf(g, xh, s2[e]);
                     }
                 }
+            };
+            auto ldz = [&](int64_t p) {
+                if constexpr (MODE == 1) return *reinterpret_cast<const bq_u4*>(dz + ((int64_t)nn * hw + p) * c + 8 * j);
+                else return bq_u4{0u, 0u, 0u, 0u};
+            };
+            // GNB_U pixels' loads in flight per thread, then their sums in pixel order (the same
+            // order as one pixel at a time: bit-identical partials)
+            int64_t p = p0 + row;
+            for (; p + (GNB_U - 1) * rows_here < p1; p += GNB_U * rows_here) {
+                bq_u4 xv[GNB_U], dzv[GNB_U];
+#pragma unroll
+                for (int u = 0; u < GNB_U; ++u) {
+                    xv[u] = gnb_ld(x1, x2, c1, c2, nn, hw, p + u * rows_here, j);
+                    dzv[u] = ldz(p + u * rows_here);
+                }
+#pragma unroll
+                for (int u = 0; u < GNB_U; ++u) acc1(xv[u], dzv[u]);
             }
+            for (; p < p1; p += rows_here) acc1(gnb_ld(x1, x2, c1, c2, nn, hw, p, j), ldz(p));
         }
         __syncthreads();
 #pragma unroll
@@ -717,16 +740,25 @@ __global__ __launch_bounds__(kBlock) void k_gnb_apply(const u16* __restrict__ x1
         const float4 b0 = *reinterpret_cast<const float4*>(sh), b1 = *reinterpret_cast<const float4*>(sh + 4);
         const float sa[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
         const float sb[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
-        for (int64_t p = p0 + row; p < p1; p += rows) {
+        auto one = [&](bq_u4 xv, int64_t p) {
             float f[8];
-            unpack8(gnb_ld(x1, x2, c1, c2, nn, hw, p, j), f);
+            unpack8(xv, f);
 #pragma unroll
             for (int e = 0; e < 8; ++e) {
                 const float yv = fmaf(f[e], sa[e], sb[e]);
                 f[e] = ACT ? silu_f(yv) : yv;
             }
             *reinterpret_cast<bq_u4*>(z + ((int64_t)nn * hw + p) * c + 8 * j) = pack8(f);
+        };
+        int64_t p = p0 + row;
+        for (; p + (GNB_U - 1) * rows < p1; p += GNB_U * rows) {  // GNB_U pixels' loads in flight
+            bq_u4 xv[GNB_U];
+#pragma unroll
+            for (int u = 0; u < GNB_U; ++u) xv[u] = gnb_ld(x1, x2, c1, c2, nn, hw, p + u * rows, j);
+#pragma unroll
+            for (int u = 0; u < GNB_U; ++u) one(xv[u], p + u * rows);
         }
+        for (; p < p1; p += rows) one(gnb_ld(x1, x2, c1, c2, nn, hw, p, j), p);
     }
 }
 
@@ -767,11 +799,12 @@ __global__ __launch_bounds__(kBlock) void k_gnb_bwd_apply(const u16* __restrict_
         u16* __restrict__ dst = first ? dx1 : dx2;
         const u16* __restrict__ a = first ? add1 : add2;
         const u16* __restrict__ ab = first ? add1b : nullptr;
-        for (int64_t p = p0 + row; p < p1; p += rows) {
+        const u16* __restrict__ xs = first ? x1 : x2;
+        // one pixel from its loaded vectors (x, dy', and the addends or zeros)
+        auto one = [&](bq_u4 xv, bq_u4 dv, bq_u4 av, bq_u4 bv, int64_t off) {
             float f[8], d[8], o[8];
-            const int64_t off = ((int64_t)nn * hw + p) * cp + chp;
-            unpack8(*reinterpret_cast<const bq_u4*>((first ? x1 : x2) + off), f);
-            unpack8(*reinterpret_cast<const bq_u4*>(dz + ((int64_t)nn * hw + p) * c + ch), d);
+            unpack8(xv, f);
+            unpack8(dv, d);
 #pragma unroll
             for (int e = 0; e < 8; ++e) {
                 float dd = d[e];
@@ -784,17 +817,40 @@ __global__ __launch_bounds__(kBlock) void k_gnb_bwd_apply(const u16* __restrict_
             }
             if (a) {
                 float t[8];
-                unpack8(*reinterpret_cast<const bq_u4*>(a + off), t);
+                unpack8(av, t);
 #pragma unroll
                 for (int e = 0; e < 8; ++e) o[e] += t[e];
             }
             if (ab) {
                 float t[8];
-                unpack8(*reinterpret_cast<const bq_u4*>(ab + off), t);
+                unpack8(bv, t);
 #pragma unroll
                 for (int e = 0; e < 8; ++e) o[e] += t[e];
             }
             *reinterpret_cast<bq_u4*>(dst + off) = pack8(o);
+        };
+        const bq_u4 zero4 = {0u, 0u, 0u, 0u};
+        auto ld = [&](const u16* __restrict__ src, int64_t off) {
+            return src ? *reinterpret_cast<const bq_u4*>(src + off) : zero4;
+        };
+        int64_t p = p0 + row;
+        for (; p + (GNB_U - 1) * rows < p1; p += GNB_U * rows) {  // GNB_U pixels' loads in flight
+            bq_u4 xv[GNB_U], dv[GNB_U], av[GNB_U], bv[GNB_U];
+#pragma unroll
+            for (int u = 0; u < GNB_U; ++u) {
+                const int64_t pp = p + u * rows, off = ((int64_t)nn * hw + pp) * cp + chp;
+                xv[u] = *reinterpret_cast<const bq_u4*>(xs + off);
+                dv[u] = *reinterpret_cast<const bq_u4*>(dz + ((int64_t)nn * hw + pp) * c + ch);
+                av[u] = ld(a, off);
+                bv[u] = ld(ab, off);
+            }
+#pragma unroll
+            for (int u = 0; u < GNB_U; ++u) one(xv[u], dv[u], av[u], bv[u], ((int64_t)nn * hw + p + u * rows) * cp + chp);
+        }
+        for (; p < p1; p += rows) {
+            const int64_t off = ((int64_t)nn * hw + p) * cp + chp;
+            one(*reinterpret_cast<const bq_u4*>(xs + off),
+                *reinterpret_cast<const bq_u4*>(dz + ((int64_t)nn * hw + p) * c + ch), ld(a, off), ld(ab, off), off);
         }
     }
 }
