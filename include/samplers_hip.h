@@ -586,6 +586,12 @@ int sp_conv3x3_bf16_up(const void* x, const void* wp, const float* bias, const v
                        int32_t cout, int32_t h, int32_t w, void* y, sp_stream_t stream);
 /* dx[n][h/2][w/2][c] = 2x2 block sums of dz[n][h][w][c], NHWC bf16 (c % 8 == 0) */
 int sp_pool2x2_bf16(const void* dz, int64_t n, int32_t c, int32_t h, int32_t w, void* dx, sp_stream_t stream);
+/* GEGLU at bf16 (diffusers GEGLU after its projection, the SD 1.5 transformers' feed-forward,
+ * reached from stable_diffusion.py:306-313): h = [a | gate] [rows][2f] -> y = a * gelu(gate)
+ * [rows][f] (exact erf GELU, fp32 arithmetic); VJP dh = [dy gelu(gate) | dy a gelu'(gate)] as one
+ * [rows][2f] buffer.  f % 8 == 0; bf16 throughout. */
+int sp_geglu_bf16_fwd(const void* h, int64_t rows, int32_t f, void* y, sp_stream_t stream);
+int sp_geglu_bf16_bwd(const void* h, const void* dy, int64_t rows, int32_t f, void* dh, sp_stream_t stream);
 int sp_groupnorm_bf16_supported(int32_t c1, int32_t c2, int32_t groups);
 int64_t sp_groupnorm_bf16_workspace(int64_t n, int32_t c, int64_t hw);
 /* z = act(GroupNorm(cat(x1, x2) + chan_bias) * gamma + beta) over NHWC bf16 parts (channel

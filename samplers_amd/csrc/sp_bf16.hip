@@ -860,6 +860,58 @@ static unsigned stream_blocks(int64_t vectors) {
 }
 
 // ---------------------------------------------------------------------------------------------
+// GEGLU of the SD 1.5 transformers' feed-forward at bf16: h = [a | gate] ([T][2F], the
+// projection's output), y = a * gelu(gate) ([T][F]; exact erf GELU, fp32 arithmetic, one
+// rounding); VJP dh = [dy * gelu(gate) | dy * a * gelu'(gate)] written as one [T][2F] buffer (the
+// projection's cotangent: no chunk-gradient concatenation).  8 features per thread-iteration.
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ float bq_gelu(float g) { return 0.5f * g * (1.f + erff(g * 0.70710678118654752f)); }
+__device__ __forceinline__ float bq_gelu_grad(float g) {
+    const float cdf = 0.5f * (1.f + erff(g * 0.70710678118654752f));
+    return cdf + g * (expf(-0.5f * g * g) * 0.39894228040143268f);
+}
+
+__global__ __launch_bounds__(kBlock) void k_geglu_bf16_fwd(const u16* __restrict__ h, int64_t rows, int f,
+                                                           u16* __restrict__ y) {
+    const int f8 = f >> 3;
+    const int64_t n8 = rows * f8;
+    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n8; i += (int64_t)gridDim.x * kBlock) {
+        const int64_t r = i / f8;
+        const int j = static_cast<int>(i - r * f8);
+        const bq_u4* hr = reinterpret_cast<const bq_u4*>(h + r * 2 * f);
+        float a[8], g[8];
+        unpack8(hr[j], a);
+        unpack8(hr[f8 + j], g);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) a[e] *= bq_gelu(g[e]);
+        reinterpret_cast<bq_u4*>(y)[i] = pack8(a);
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_geglu_bf16_bwd(const u16* __restrict__ h, const u16* __restrict__ dy,
+                                                           int64_t rows, int f, u16* __restrict__ dh) {
+    const int f8 = f >> 3;
+    const int64_t n8 = rows * f8;
+    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n8; i += (int64_t)gridDim.x * kBlock) {
+        const int64_t r = i / f8;
+        const int j = static_cast<int>(i - r * f8);
+        const bq_u4* hr = reinterpret_cast<const bq_u4*>(h + r * 2 * f);
+        float a[8], g[8], d[8], da[8], dg[8];
+        unpack8(hr[j], a);
+        unpack8(hr[f8 + j], g);
+        unpack8(reinterpret_cast<const bq_u4*>(dy)[i], d);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            da[e] = d[e] * bq_gelu(g[e]);
+            dg[e] = d[e] * a[e] * bq_gelu_grad(g[e]);
+        }
+        bq_u4* o = reinterpret_cast<bq_u4*>(dh + r * 2 * f);
+        o[j] = pack8(da);
+        o[f8 + j] = pack8(dg);
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
 // Multi-head attention on bf16 q / k / v (the SD 1.5 UNet's attn1 / attn2 at the reference's
 // bf16): the structure of k_attn6_fwd (sp_attention6.hip) with one bf16 term per operand.
 // Per wave 32 queries; per 32-key block S^T = K Q^T (K rows from LDS as A, Q^T in registers as
@@ -1398,6 +1450,28 @@ int sp_pool2x2_bf16(const void* dz, int64_t n, int32_t c, int32_t h, int32_t w, 
     launch(0, k_pool2x2_bf16, dim3(stream_blocks(vec)), dim3(kBlock), s, static_cast<const u16*>(dz), n, c, h / 2,
            w / 2, static_cast<u16*>(dx));
     return check_launch("sp_pool2x2_bf16");
+}
+
+// ---- GEGLU ---------------------------------------------------------------------------------
+
+int sp_geglu_bf16_fwd(const void* h, int64_t rows, int32_t f, void* y, sp_stream_t stream) {
+    if (rows < 0 || f <= 0 || f % 8) return SP_EINVAL;
+    if (rows == 0) return SP_OK;
+    if (!h || !y) return SP_EINVAL;
+    const int64_t vec = rows * (f / 8);
+    launch(0, k_geglu_bf16_fwd, dim3(stream_blocks(vec)), dim3(kBlock), static_cast<hipStream_t>(stream),
+           static_cast<const u16*>(h), rows, static_cast<int>(f), static_cast<u16*>(y));
+    return check_launch("sp_geglu_bf16_fwd");
+}
+
+int sp_geglu_bf16_bwd(const void* h, const void* dy, int64_t rows, int32_t f, void* dh, sp_stream_t stream) {
+    if (rows < 0 || f <= 0 || f % 8) return SP_EINVAL;
+    if (rows == 0) return SP_OK;
+    if (!h || !dy || !dh || dh == h) return SP_EINVAL;
+    const int64_t vec = rows * (f / 8);
+    launch(0, k_geglu_bf16_bwd, dim3(stream_blocks(vec)), dim3(kBlock), static_cast<hipStream_t>(stream),
+           static_cast<const u16*>(h), static_cast<const u16*>(dy), rows, static_cast<int>(f), static_cast<u16*>(dh));
+    return check_launch("sp_geglu_bf16_bwd");
 }
 
 // ---- GroupNorm ------------------------------------------------------------------------------

@@ -15,8 +15,9 @@ stable_diffusion.py:90-101``, ``ddpm.py:23-34``) and its PSLD driver runs SD 1.5
 * the SD UNet's self- and cross-attention on ``sp_attention_bf16_fwd`` / ``_bwd`` (flash-style,
   scores never in HBM, either direction; head dim 160 — the 16² / 8² levels — takes the VJP on
   the exact-fp32 fused kernels with the operands widened);
-* 1x1 convolutions and linears are bf16 GEMMs (hipBLASLt through ``F.linear``); LayerNorm,
-  GEGLU and the d = 512 single-head attention (score matrix kept) are torch bf16 ops.
+* the transformers' GEGLU gate and its VJP on ``sp_geglu_bf16_fwd`` / ``_bwd``;
+* 1x1 convolutions and linears are bf16 GEMMs (hipBLASLt through ``F.linear``); LayerNorm and the
+  d = 512 single-head attention (score matrix kept) are torch bf16 ops.
 
 Semantics follow PyTorch's bf16 modules (fp32 accumulation / statistics, one rounding to bf16
 per layer output), which is what the reference computes in bf16.  Every entry here raises
@@ -334,6 +335,48 @@ def group_norm(norm: nn.GroupNorm, x1: Tensor, x2: Tensor | None = None, chan_bi
     parts read in place."""
     cb = None if chan_bias is None else chan_bias.detach().to(torch.float32).reshape(x1.shape[0], -1).contiguous()
     return _GroupNormBf16Fn.apply(nhwc(x1), None if x2 is None else nhwc(x2), norm, cb)
+
+
+# ---------------------------------------------------------------------------------------------
+# GEGLU (the SD 1.5 transformers' feed-forward gate)
+# ---------------------------------------------------------------------------------------------
+
+class _GegluBf16Fn(torch.autograd.Function):
+    """``a * gelu(gate)`` with ``a, gate = h.chunk(2, -1)`` on ``sp_geglu_bf16_fwd``; the VJP writes
+    the projection's whole cotangent [T][2F] (``sp_geglu_bf16_bwd``: no chunk-gradient concat)."""
+
+    @staticmethod
+    def forward(ctx, h):
+        lib = _hip.load_library()
+        f = h.shape[-1] // 2
+        h2 = h.reshape(-1, 2 * f).contiguous()
+        y = torch.empty(h2.shape[0], f, device=h.device, dtype=BF16)
+        _hip.check(lib.sp_geglu_bf16_fwd(_p(h2), h2.shape[0], f, _p(y), _hip.stream_of(h2)), "sp_geglu_bf16_fwd")
+        ctx.save_for_backward(h2)
+        ctx.shape = h.shape
+        return y.reshape(*h.shape[:-1], f)
+
+    @staticmethod
+    def backward(ctx, dy):
+        (h2,) = ctx.saved_tensors
+        lib = _hip.load_library()
+        rows, f2 = h2.shape
+        d2 = dy.to(BF16).reshape(rows, f2 // 2).contiguous()
+        dh = torch.empty_like(h2)
+        _hip.check(lib.sp_geglu_bf16_bwd(_p(h2), _p(d2), rows, f2 // 2, _p(dh), _hip.stream_of(d2)),
+                   "sp_geglu_bf16_bwd")
+        return dh.reshape(ctx.shape)
+
+
+def geglu_supported(h: Tensor) -> bool:
+    """bf16 device rows of whole 16-feature blocks (``SAMPLERS_AMD_BF16_GEGLU=0``: torch, for A/B)."""
+    import os
+
+    return is_bf16_device(h) and h.shape[-1] % 16 == 0 and os.environ.get("SAMPLERS_AMD_BF16_GEGLU", "1") != "0"
+
+
+def geglu(h: Tensor) -> Tensor:
+    return _GegluBf16Fn.apply(h)
 
 
 # ---------------------------------------------------------------------------------------------

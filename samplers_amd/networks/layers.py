@@ -1050,10 +1050,14 @@ class _GegluFn(torch.autograd.Function):
 
 def geglu(h: Tensor) -> Tensor:
     """``a * gelu(gate)`` with ``a, gate = h.chunk(2, -1)`` (diffusers GEGLU after its
-    projection): one HIP pass each way on CUDA fp32, torch otherwise."""
+    projection): one HIP pass each way on CUDA fp32 and bf16, torch otherwise."""
     f = h.shape[-1] // 2
     if (h.is_cuda and h.dtype == torch.float32 and h.shape[-1] % 8 == 0
             and (h.numel() // 2) < 2**31):
         return _GegluFn.apply(h)
+    if h.is_cuda and h.dtype == torch.bfloat16:
+        from . import bf16
+        if bf16.geglu_supported(h):
+            return bf16.geglu(h)
     a, gate = h.chunk(2, dim=-1)
     return a * F.gelu(gate)

@@ -256,6 +256,31 @@ def test_attention_bf16_cross_77_context(cuda):
     assert _rel(o, ref) < 1e-2 and _rel(dq, rq) < 1e-2
 
 
+def test_geglu_bf16_fwd_vjp(cuda, parity_record):
+    """sp_geglu_bf16_fwd / _bwd vs the fp32 torch GEGLU of the same bf16 inputs (one rounding of
+    the result each way), and the kernel runs instead of torch's gelu / cat."""
+    from samplers_amd.networks.layers import geglu
+
+    gen = torch.Generator().manual_seed(31)
+    h = torch.randn(2, 77, 2 * 1280, generator=gen).to(BF)
+    dy = torch.randn(2, 77, 1280, generator=gen).to(BF)
+    hg = h.to(cuda).requires_grad_(True)
+    with torch.enable_grad():
+        y = geglu(hg)
+    (dh,) = torch.autograd.grad(y, hg, dy.to(cuda))
+    hf = h.float().requires_grad_(True)
+    with torch.enable_grad():
+        a, g = hf.chunk(2, dim=-1)
+        ref = a * torch.nn.functional.gelu(g)
+    (rh,) = torch.autograd.grad(ref, hf, dy.float())
+    e1, e2 = _rel(y, ref), _rel(dh, rh)
+    parity_record("geglu_bf16_rel_l2", e1, 4e-3)
+    parity_record("geglu_bf16_vjp_rel_l2", e2, 4e-3)
+    assert y.dtype == BF and dh.dtype == BF and e1 < 4e-3 and e2 < 4e-3, (e1, e2)
+    names = _kernel_names(lambda: geglu(h.to(cuda)))
+    assert any("k_geglu_bf16_fwd" in s for s in names) and not any("Gelu" in s for s in names)
+
+
 # ---- whole priors -----------------------------------------------------------------------------
 
 def _fwd_vjp(fn, x, cot):
