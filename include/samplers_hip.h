@@ -586,6 +586,14 @@ int sp_conv3x3_bf16_up(const void* x, const void* wp, const float* bias, const v
                        int32_t cout, int32_t h, int32_t w, void* y, sp_stream_t stream);
 /* dx[n][h/2][w/2][c] = 2x2 block sums of dz[n][h][w][c], NHWC bf16 (c % 8 == 0) */
 int sp_pool2x2_bf16(const void* dz, int64_t n, int32_t c, int32_t h, int32_t w, void* dx, sp_stream_t stream);
+/* LayerNorm over bf16 token rows [rows][c] (BasicTransformerBlock's norm1-3 at bf16), fp32 weight /
+ * bias / statistics (mean, rstd per row, for the VJP); the VJP (frozen weights) adds `add` (bf16,
+ * nullable: the residual branch's gradient of the same tensor).  c % 8 == 0, c <= 2048. */
+int sp_layernorm_bf16_supported(int64_t rows, int32_t c);
+int sp_layernorm_bf16_fwd(const void* x, const float* w, const float* b, int64_t rows, int32_t c, float eps, void* y,
+                          float* mean, float* rstd, sp_stream_t stream);
+int sp_layernorm_bf16_bwd(const void* dy, const void* x, const float* w, const float* mean, const float* rstd,
+                          const void* add, int64_t rows, int32_t c, void* dx, sp_stream_t stream);
 /* GEGLU at bf16 (diffusers GEGLU after its projection, the SD 1.5 transformers' feed-forward,
  * reached from stable_diffusion.py:306-313): h = [a | gate] [rows][2f] -> y = a * gelu(gate)
  * [rows][f] (exact erf GELU, fp32 arithmetic); VJP dh = [dy gelu(gate) | dy a gelu'(gate)] as one

@@ -240,6 +240,9 @@ SIGNATURES = {
     "sp_conv3x3_bf16_up": (ctypes.c_int, [_P, _P, _P, _P, _I64, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
                                           ctypes.c_int32, _P, _P]),
     "sp_pool2x2_bf16": (ctypes.c_int, [_P, _I64, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, _P, _P]),
+    "sp_layernorm_bf16_supported": (ctypes.c_int, [_I64, ctypes.c_int32]),
+    "sp_layernorm_bf16_fwd": (ctypes.c_int, [_P, _P, _P, _I64, ctypes.c_int32, ctypes.c_float, _P, _P, _P, _P]),
+    "sp_layernorm_bf16_bwd": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, _I64, ctypes.c_int32, _P, _P]),
     "sp_geglu_bf16_fwd": (ctypes.c_int, [_P, _I64, ctypes.c_int32, _P, _P]),
     "sp_geglu_bf16_bwd": (ctypes.c_int, [_P, _P, _I64, ctypes.c_int32, _P, _P]),
     "sp_groupnorm_bf16_supported": (ctypes.c_int, [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32]),

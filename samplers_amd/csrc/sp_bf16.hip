@@ -912,6 +912,115 @@ __global__ __launch_bounds__(kBlock) void k_geglu_bf16_bwd(const u16* __restrict
 }
 
 // ---------------------------------------------------------------------------------------------
+// LayerNorm of the SD 1.5 transformer blocks at bf16 (token rows [T][C], C = 320 / 640 / 1280):
+// one wave per row held in registers (lane l: 8-channel vectors l, l + 64, ...), fp32 statistics
+// (two wave reductions), fp32 weight / bias; the VJP (frozen weights) adds the residual branch's
+// gradient of the same tensor (`add`, the linear that consumed the residual hands it over), so
+// x + f(norm(x)) costs no autograd add.
+// ---------------------------------------------------------------------------------------------
+constexpr int LNB_ROWS = kBlock / 64;
+
+template <int NV>
+__device__ __forceinline__ void lnb_load(const u16* __restrict__ row, int c8, int lane, float (&v)[NV][8]) {
+#pragma unroll
+    for (int j = 0; j < NV; ++j) {
+        const int i = lane + 64 * j;
+        const bq_u4 q = i < c8 ? reinterpret_cast<const bq_u4*>(row)[i] : bq_u4{0u, 0u, 0u, 0u};
+        unpack8(q, v[j]);
+    }
+}
+
+template <int NV>
+__global__ __launch_bounds__(kBlock) void k_layernorm_bf16_fwd(const u16* __restrict__ x, const float* __restrict__ w,
+                                                               const float* __restrict__ b, int64_t rows, int c,
+                                                               float eps, u16* __restrict__ y,
+                                                               float* __restrict__ mean, float* __restrict__ rstd) {
+    const int lane = threadIdx.x & 63;
+    const int64_t r = (int64_t)blockIdx.x * LNB_ROWS + (threadIdx.x >> 6);
+    if (r >= rows) return;
+    const int c8 = c >> 3;
+    float v[NV][8];
+    lnb_load<NV>(x + r * c, c8, lane, v);
+    float s = 0.f;
+#pragma unroll
+    for (int j = 0; j < NV; ++j)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) s += v[j][e];
+    const float mu = wave_sum(s) / static_cast<float>(c);
+    float q = 0.f;
+#pragma unroll
+    for (int j = 0; j < NV; ++j)
+        if (lane + 64 * j < c8)
+#pragma unroll
+            for (int e = 0; e < 8; ++e) q = fmaf(v[j][e] - mu, v[j][e] - mu, q);
+    const float rs = 1.f / sqrtf(wave_sum(q) / static_cast<float>(c) + eps);
+#pragma unroll
+    for (int j = 0; j < NV; ++j) {
+        const int i = lane + 64 * j;
+        if (i < c8) {
+            float o[8], g[8], bb[8];
+            ld8f(w + 8 * i, g);
+            ld8f(b + 8 * i, bb);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) o[e] = fmaf((v[j][e] - mu) * rs, g[e], bb[e]);
+            reinterpret_cast<bq_u4*>(y + r * c)[i] = pack8(o);
+        }
+    }
+    if (lane == 0) mean[r] = mu, rstd[r] = rs;
+}
+
+template <int NV>
+__global__ __launch_bounds__(kBlock) void k_layernorm_bf16_bwd(const u16* __restrict__ dy, const u16* __restrict__ x,
+                                                               const float* __restrict__ w,
+                                                               const float* __restrict__ mean,
+                                                               const float* __restrict__ rstd,
+                                                               const u16* __restrict__ add, int64_t rows, int c,
+                                                               u16* __restrict__ dx) {
+    const int lane = threadIdx.x & 63;
+    const int64_t r = (int64_t)blockIdx.x * LNB_ROWS + (threadIdx.x >> 6);
+    if (r >= rows) return;
+    const int c8 = c >> 3;
+    const float mu = mean[r], rs = rstd[r];
+    float g[NV][8], h[NV][8];
+    lnb_load<NV>(dy + r * c, c8, lane, g);
+    lnb_load<NV>(x + r * c, c8, lane, h);
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int j = 0; j < NV; ++j) {
+        const int i = lane + 64 * j;
+        if (i < c8) {
+            float ww[8];
+            ld8f(w + 8 * i, ww);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                g[j][e] *= ww[e];
+                h[j][e] = (h[j][e] - mu) * rs;
+                s1 = fmaf(g[j][e], h[j][e], s1);
+                s2 += g[j][e];
+            }
+        }
+    }
+    const float inv_c = 1.f / static_cast<float>(c);
+    const float m1 = wave_sum(s1) * inv_c, m2 = wave_sum(s2) * inv_c;
+#pragma unroll
+    for (int j = 0; j < NV; ++j) {
+        const int i = lane + 64 * j;
+        if (i < c8) {
+            float o[8];
+#pragma unroll
+            for (int e = 0; e < 8; ++e) o[e] = rs * (g[j][e] - m2 - h[j][e] * m1);
+            if (add) {
+                float a[8];
+                unpack8(reinterpret_cast<const bq_u4*>(add + r * c)[i], a);
+#pragma unroll
+                for (int e = 0; e < 8; ++e) o[e] += a[e];
+            }
+            reinterpret_cast<bq_u4*>(dx + r * c)[i] = pack8(o);
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
 // Multi-head attention on bf16 q / k / v (the SD 1.5 UNet's attn1 / attn2 at the reference's
 // bf16): the structure of k_attn6_fwd (sp_attention6.hip) with one bf16 term per operand.
 // Per wave 32 queries; per 32-key block S^T = K Q^T (K rows from LDS as A, Q^T in registers as
@@ -1450,6 +1559,44 @@ int sp_pool2x2_bf16(const void* dz, int64_t n, int32_t c, int32_t h, int32_t w, 
     launch(0, k_pool2x2_bf16, dim3(stream_blocks(vec)), dim3(kBlock), s, static_cast<const u16*>(dz), n, c, h / 2,
            w / 2, static_cast<u16*>(dx));
     return check_launch("sp_pool2x2_bf16");
+}
+
+// ---- LayerNorm -----------------------------------------------------------------------------
+
+int sp_layernorm_bf16_supported(int64_t rows, int32_t c) { return rows >= 0 && c > 0 && c % 8 == 0 && c <= 8 * 64 * 4; }
+
+int sp_layernorm_bf16_fwd(const void* x, const float* w, const float* b, int64_t rows, int32_t c, float eps, void* y,
+                          float* mean, float* rstd, sp_stream_t stream) {
+    if (!sp_layernorm_bf16_supported(rows, c)) return SP_EINVAL;
+    if (rows == 0) return SP_OK;
+    if (!x || !w || !b || !y || !mean || !rstd) return SP_EINVAL;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const dim3 grid(static_cast<unsigned>((rows + LNB_ROWS - 1) / LNB_ROWS));
+    const int nv = (c / 8 + 63) / 64;
+    const u16* xx = static_cast<const u16*>(x);
+    u16* yy = static_cast<u16*>(y);
+    if (nv == 1) launch(0, k_layernorm_bf16_fwd<1>, grid, dim3(kBlock), s, xx, w, b, rows, static_cast<int>(c), eps, yy, mean, rstd);
+    else if (nv == 2) launch(0, k_layernorm_bf16_fwd<2>, grid, dim3(kBlock), s, xx, w, b, rows, static_cast<int>(c), eps, yy, mean, rstd);
+    else if (nv == 3) launch(0, k_layernorm_bf16_fwd<3>, grid, dim3(kBlock), s, xx, w, b, rows, static_cast<int>(c), eps, yy, mean, rstd);
+    else launch(0, k_layernorm_bf16_fwd<4>, grid, dim3(kBlock), s, xx, w, b, rows, static_cast<int>(c), eps, yy, mean, rstd);
+    return check_launch("sp_layernorm_bf16_fwd");
+}
+
+int sp_layernorm_bf16_bwd(const void* dy, const void* x, const float* w, const float* mean, const float* rstd,
+                          const void* add, int64_t rows, int32_t c, void* dx, sp_stream_t stream) {
+    if (!sp_layernorm_bf16_supported(rows, c)) return SP_EINVAL;
+    if (rows == 0) return SP_OK;
+    if (!dy || !x || !w || !mean || !rstd || !dx) return SP_EINVAL;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const dim3 grid(static_cast<unsigned>((rows + LNB_ROWS - 1) / LNB_ROWS));
+    const int nv = (c / 8 + 63) / 64;
+    const u16 *d = static_cast<const u16*>(dy), *xx = static_cast<const u16*>(x), *a = static_cast<const u16*>(add);
+    u16* o = static_cast<u16*>(dx);
+    if (nv == 1) launch(0, k_layernorm_bf16_bwd<1>, grid, dim3(kBlock), s, d, xx, w, mean, rstd, a, rows, static_cast<int>(c), o);
+    else if (nv == 2) launch(0, k_layernorm_bf16_bwd<2>, grid, dim3(kBlock), s, d, xx, w, mean, rstd, a, rows, static_cast<int>(c), o);
+    else if (nv == 3) launch(0, k_layernorm_bf16_bwd<3>, grid, dim3(kBlock), s, d, xx, w, mean, rstd, a, rows, static_cast<int>(c), o);
+    else launch(0, k_layernorm_bf16_bwd<4>, grid, dim3(kBlock), s, d, xx, w, mean, rstd, a, rows, static_cast<int>(c), o);
+    return check_launch("sp_layernorm_bf16_bwd");
 }
 
 // ---- GEGLU ---------------------------------------------------------------------------------

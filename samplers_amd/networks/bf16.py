@@ -15,9 +15,11 @@ stable_diffusion.py:90-101``, ``ddpm.py:23-34``) and its PSLD driver runs SD 1.5
 * the SD UNet's self- and cross-attention on ``sp_attention_bf16_fwd`` / ``_bwd`` (flash-style,
   scores never in HBM, either direction; head dim 160 — the 16² / 8² levels — takes the VJP on
   the exact-fp32 fused kernels with the operands widened);
-* the transformers' GEGLU gate and its VJP on ``sp_geglu_bf16_fwd`` / ``_bwd``;
-* 1x1 convolutions and linears are bf16 GEMMs (hipBLASLt through ``F.linear``); LayerNorm and the
-  d = 512 single-head attention (score matrix kept) are torch bf16 ops.
+* the transformers' GEGLU gate and LayerNorm, forward and VJP, on ``sp_geglu_bf16_*`` /
+  ``sp_layernorm_bf16_*`` (the LayerNorm VJP adds the residual branch's gradient handed over by the
+  residual linear: no autograd accumulation adds in x + f(norm(x)));
+* 1x1 convolutions and linears are bf16 GEMMs (hipBLASLt through ``F.linear``); the d = 512
+  single-head attention (score matrix kept) is torch bf16 ops.
 
 Semantics follow PyTorch's bf16 modules (fp32 accumulation / statistics, one rounding to bf16
 per layer output), which is what the reference computes in bf16.  Every entry here raises
@@ -335,6 +337,86 @@ def group_norm(norm: nn.GroupNorm, x1: Tensor, x2: Tensor | None = None, chan_bi
     parts read in place."""
     cb = None if chan_bias is None else chan_bias.detach().to(torch.float32).reshape(x1.shape[0], -1).contiguous()
     return _GroupNormBf16Fn.apply(nhwc(x1), None if x2 is None else nhwc(x2), norm, cb)
+
+
+# ---------------------------------------------------------------------------------------------
+# LayerNorm and the residual linears around it (x + f(norm(x)) of the transformer blocks)
+# ---------------------------------------------------------------------------------------------
+
+class _LayerNormBf16Fn(torch.autograd.Function):
+    """``module(x)`` on ``sp_layernorm_bf16_fwd``; the VJP adds the residual branch's gradient of
+    ``x`` when the linear that consumed the residual handed it over (``box``, layers.SkipGrad)."""
+
+    @staticmethod
+    def forward(ctx, x, module, box):
+        lib = _hip.load_library()
+        c = x.shape[-1]
+        x2 = x.reshape(-1, c).contiguous()
+        rows = x2.shape[0]
+        w = _cached(module, "ln_w", _wkey(module.weight), lambda: _f32(module.weight))
+        b = _cached(module, "ln_b", _wkey(module.bias), lambda: _f32(module.bias))
+        y = torch.empty_like(x2)
+        stats = torch.empty(2, rows, device=x.device, dtype=torch.float32)
+        _hip.check(lib.sp_layernorm_bf16_fwd(_p(x2), w.data_ptr(), b.data_ptr(), rows, c, float(module.eps), _p(y),
+                                             stats[0].data_ptr(), stats[1].data_ptr(), _hip.stream_of(x2)),
+                   "sp_layernorm_bf16_fwd")
+        ctx.save_for_backward(x2, w, stats)
+        ctx.box, ctx.shape = box, x.shape
+        return y.reshape(x.shape)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, w, stats = ctx.saved_tensors
+        lib = _hip.load_library()
+        rows, c = x2.shape
+        d2 = dy.to(BF16).reshape(rows, c).contiguous()
+        add = ctx.box.take() if ctx.box is not None else None
+        if add is not None:
+            add = add.to(BF16).reshape(rows, c).contiguous()
+        dx = torch.empty_like(x2)
+        _hip.check(lib.sp_layernorm_bf16_bwd(_p(d2), _p(x2), w.data_ptr(), stats[0].data_ptr(), stats[1].data_ptr(),
+                                             _p(add), rows, c, _p(dx), _hip.stream_of(d2)), "sp_layernorm_bf16_bwd")
+        return dx.reshape(ctx.shape), None, None
+
+
+def layer_norm_supported(module: nn.Module, x: Tensor) -> bool:
+    """bf16 device rows, frozen affine LayerNorm over the last dim (``SAMPLERS_AMD_BF16_LN=0``:
+    torch, for A/B)."""
+    import os
+
+    c = x.shape[-1]
+    return (is_bf16_device(x) and os.environ.get("SAMPLERS_AMD_BF16_LN", "1") != "0" and module.weight is not None and module.bias is not None
+            and not module.weight.requires_grad and tuple(module.normalized_shape) == (c,)
+            and bool(_hip.load_library().sp_layernorm_bf16_supported(x.numel() // max(c, 1), c)))
+
+
+def layer_norm(x: Tensor, module: nn.Module, box=None) -> Tensor:
+    return _LayerNormBf16Fn.apply(x, module, box)
+
+
+class _LinearResBf16Fn(torch.autograd.Function):
+    """``F.linear(x, w2d, bias) + res`` (hipBLASLt bf16 GEMM, the residual added to its output);
+    input VJP dx = dy W, and the residual's gradient dy handed to ``box`` (the LayerNorm VJP that
+    adds it) instead of autograd's accumulation add."""
+
+    @staticmethod
+    def forward(ctx, x, w2d, bias, res, box):
+        y = F.linear(x, w2d, bias)
+        y += res
+        ctx.w2d, ctx.box = w2d, box
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        dx = torch.matmul(dy, ctx.w2d)
+        dres = dy
+        if ctx.box is not None and ctx.box.enabled:
+            ctx.box.grad, dres = dy, None
+        return dx, None, None, dres, None
+
+
+def linear_res(x: Tensor, w2d: Tensor, bias: Tensor | None, res: Tensor, box=None) -> Tensor:
+    return _LinearResBf16Fn.apply(x, w2d.detach(), None if bias is None else bias.detach(), res, box)
 
 
 # ---------------------------------------------------------------------------------------------

@@ -815,6 +815,10 @@ def linear(x: Tensor, module: nn.Module, w2d: Tensor | None = None, bias: Tensor
             and (res is None or (res.dtype == torch.float32 and res.numel() == t * m))):
         if _query("sp_linear_x6_supported", t, k, m) and x6_enough_tiles(t, m):
             return _LinearX6Fn.apply(x, w2d, bias, module, w2d, res, box)
+    if (res is not None and x.is_cuda and x.dtype == torch.bfloat16 and res.dtype == torch.bfloat16
+            and not w2d.requires_grad and (bias is None or not bias.requires_grad) and res.shape[-1] == m):
+        from . import bf16
+        return bf16.linear_res(x, w2d, bias, res, box)
     if box is not None:
         box.enabled = False
     y = F.linear(x, w2d, bias)
@@ -1011,6 +1015,10 @@ def layer_norm(x: Tensor, module: nn.LayerNorm, box: SkipGrad | None = None) -> 
         if lib.sp_layernorm_supported(x.numel() // c, c):
             return _LayerNormFn.apply(x, module.weight.detach().contiguous(),
                                       module.bias.detach().contiguous(), module.eps, box)
+    if x.is_cuda and x.dtype == torch.bfloat16:
+        from . import bf16
+        if bf16.layer_norm_supported(module, x):
+            return bf16.layer_norm(x, module, box)
     if box is not None:
         box.enabled = False
     return F.layer_norm(x, module.normalized_shape, module.weight, module.bias, module.eps)
