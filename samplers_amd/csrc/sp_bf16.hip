@@ -37,9 +37,22 @@ typedef __bf16 bq_bf8 __attribute__((ext_vector_type(8)));
 typedef unsigned short u16;
 
 
+#ifndef BQ_EXP
+#define BQ_EXP 0  // diagnostics only: 7 = each 32x32x16 MFMA replaced by two 16x16x32 ones on the same
+                  // operands (the same MACs, wrong results): the clock the chip holds per MFMA shape
+#endif
 __device__ __forceinline__ bq_f16 bq_mfma(bq_u4 a, bq_u4 b, bq_f16 c) {
+#if BQ_EXP == 7
+    typedef float bq_f4 __attribute__((ext_vector_type(4)));
+    bq_f4 c0 = {c[0], c[1], c[2], c[3]}, c1 = {c[4], c[5], c[6], c[7]};
+    c0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bq_bf8, a), __builtin_bit_cast(bq_bf8, b), c0, 0, 0, 0);
+    c1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bq_bf8, b), __builtin_bit_cast(bq_bf8, a), c1, 0, 0, 0);
+    c[0] = c0[0], c[1] = c0[1], c[2] = c0[2], c[3] = c0[3], c[4] = c1[0], c[5] = c1[1], c[6] = c1[2], c[7] = c1[3];
+    return c;
+#else
     return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bq_bf8, a), __builtin_bit_cast(bq_bf8, b), c,
                                                    0, 0, 0);
+#endif
 }
 
 __device__ __forceinline__ float bf_lo(unsigned u) { return __uint_as_float(u << 16); }
