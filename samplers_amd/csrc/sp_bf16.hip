@@ -37,9 +37,16 @@ typedef __bf16 bq_bf8 __attribute__((ext_vector_type(8)));
 typedef unsigned short u16;
 
 
+#ifndef SP_CONV_XCD
+#define SP_CONV_XCD 1  // XCD-aware workgroup order of the bf16 conv tile (k_conv3x3_bf16)
+#endif
+constexpr bool kConvXcdRemap = SP_CONV_XCD != 0;
 #ifndef BQ_EXP
 #define BQ_EXP 0  // diagnostics only: 7 = each 32x32x16 MFMA replaced by two 16x16x32 ones on the same
-                  // operands (the same MACs, wrong results): the clock the chip holds per MFMA shape
+                  // operands (the same MACs, wrong results): the clock the chip holds per MFMA shape;
+                  // 8 = the TC = 32 conv's fragment reads after tap 0 removed (wrong results);
+                  // 9 = its global loads after the first two stages removed (wrong results);
+                  // 10 = every patch load from one cached line (weights as usual; wrong results)
 #endif
 __device__ __forceinline__ bq_f16 bq_mfma(bq_u4 a, bq_u4 b, bq_f16 c) {
 #if BQ_EXP == 7
@@ -131,7 +138,17 @@ __global__ __launch_bounds__(kBlock, TC == 4 ? 1 : 2) void k_conv3x3_bf16(const 
     using G = CvGeo<TC>;
     __shared__ __attribute__((aligned(16))) char lds[G::LDS];
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, r = lane & 31, hh = lane >> 5;
-    const int cb = blockIdx.x, pt = blockIdx.y;
+    // XCD-aware order: the hardware deals workgroups to the 8 XCDs round-robin by dispatch order,
+    // which would put the output-channel blocks of one pixel tile (consecutive ids, cb fastest)
+    // on 8 different L2s, each fetching the same patch; remapped, XCD x runs ids x T/8 ..
+    // (x + 1) T/8 - 1 in order, so a tile's channel blocks and its neighbours share one L2
+    int cb = blockIdx.x, pt = blockIdx.y;
+    if (kConvXcdRemap) {  // (the blur kernels' mapping: XCD x gets ceil / floor(nb / 8) ids)
+        const unsigned nb = gridDim.x * gridDim.y, lin = blockIdx.x + gridDim.x * blockIdx.y;
+        const unsigned q8 = nb / 8, r8 = nb % 8, xcd = lin % 8, loc = lin / 8;
+        const unsigned l2 = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + loc;
+        cb = static_cast<int>(l2 % gridDim.x), pt = static_cast<int>(l2 / gridDim.x);
+    }
     int n0, h0, c0;
     if constexpr (TC == 32) {
         const int strips = w >> 5, rowblk = h / G::SR;
@@ -174,7 +191,11 @@ __global__ __launch_bounds__(kBlock, TC == 4 ? 1 : 2) void k_conv3x3_bf16(const 
         }
 #pragma unroll
         for (int k = 0; k < G::NP; ++k)
+#if BQ_EXP == 10  // diagnostics (wrong results): every patch piece from one cached 32-byte line per stage
+            spx[k] = poff[k] >= 0 ? *reinterpret_cast<const bq_u4*>(x + (tid & 1) * 8 + ks * 16) : bq_u4{0u, 0u, 0u, 0u};
+#else
             spx[k] = poff[k] >= 0 ? *reinterpret_cast<const bq_u4*>(x + poff[k] + ks * 16) : bq_u4{0u, 0u, 0u, 0u};
+#endif
     };
     auto lstore = [&]() {
 #pragma unroll
@@ -255,7 +276,19 @@ __global__ __launch_bounds__(kBlock, TC == 4 ? 1 : 2) void k_conv3x3_bf16(const 
             lda(0);
 #pragma unroll
             for (int s = 0; s < 9; ++s) {
+#if BQ_EXP == 8  // diagnostics (wrong results): tap 0's fragments for every tap, no further LDS reads
+                if (s + 1 < 9) {
+                    const int dx1 = (s + 1) / 3, dy1 = (s + 1) - 3 * dx1;
+                    fa[s + 1][0] = fa[0][0], fa[s + 1][1] = fa[0][1];
+                    if (dy1 == 0) {
+                        for (int i = 0; i < 4; ++i) fb[dx1][i] = fb[0][i];
+                    } else {
+                        fb[dx1][dy1 + 3] = fb[0][dy1 - 1];
+                    }
+                }
+#else
                 if (s + 1 < 9) lda(s + 1);
+#endif
                 const int dx = s / 3, dy = s - 3 * dx;
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
@@ -282,7 +315,11 @@ __global__ __launch_bounds__(kBlock, TC == 4 ? 1 : 2) void k_conv3x3_bf16(const 
         for (int s = 0; s < nst; ++s) {
             const int b = s & 1;
             if (s + 1 < nst) lstore_db(b ^ 1);
+#if BQ_EXP == 9  // diagnostics (wrong results): no global loads after the prologue's two stages
+            (void)b;
+#else
             if (s + 2 < nst) gload(ks0 + s + 2);
+#endif
             __builtin_amdgcn_sched_barrier(0);
             compute(b);
             __syncthreads();

@@ -46,6 +46,12 @@ for step in "$@"; do
               run psld_ln_on 600 python -u tools/bench_psld.py --dtype bf16 --steps 3 --warmup 2 ;;
         convexp7) run conv_exp7 300 env SAMPLERS_HIP_LIB=samplers_amd/lib/variants/lib_exp7.so python -u tools/bench_conv_bf16.py
                   run conv_base7 300 python -u tools/bench_conv_bf16.py ;;
+        convexp8) run conv_exp8 300 env SAMPLERS_HIP_LIB=samplers_amd/lib/variants/lib_exp8.so python -u tools/bench_conv_bf16.py
+                  run conv_base8 300 python -u tools/bench_conv_bf16.py ;;
+        convexp9) run conv_exp9 300 env SAMPLERS_HIP_LIB=samplers_amd/lib/variants/lib_exp9.so python -u tools/bench_conv_bf16.py
+                  run conv_base9 300 python -u tools/bench_conv_bf16.py ;;
+        convexp10) run conv_exp10 300 env SAMPLERS_HIP_LIB=samplers_amd/lib/variants/lib_exp10.so python -u tools/bench_conv_bf16.py
+                   run conv_base10 300 python -u tools/bench_conv_bf16.py ;;
         convbf16) run conv_bf16 300 python -u tools/bench_conv_bf16.py --miopen ;;
         convbf16sq) FILTER=k_conv3x3_bf16 NAME=convbf16 run conv_bf16_sq 600 tools/sq_pmc.sh tools/bench_conv_bf16.py --reps 3 --shapes sd ;;
         gputests) run gpu_tests 1100 python -u -m pytest tests -m gpu -q --timeout 400 --timeout-method thread ;;
