@@ -612,6 +612,25 @@ int sp_groupnorm_bf16_bwd(const void* dz, const void* x1, const void* x2, int32_
                           const float* chan_bias, const float* gamma, const float* beta, const float* stats,
                           int64_t n, int64_t hw, int32_t groups, int32_t act, void* dx1, void* dx2, const void* add1,
                           const void* add2, const void* add1b, void* ws, int64_t ws_bytes, sp_stream_t stream);
+/* The same with a chosen layout for z (z_layout 1: channel-blocked [n][c/16][hw][16], c % 16 == 0:
+ * the conv tile's preferred input, sp_conv3x3_bf16_ex) / for dx1 (dx_layout 1: one part, c1 % 16 == 0;
+ * the addends stay NHWC). */
+int sp_groupnorm_bf16_fwd_ex(const void* x1, const void* x2, int32_t c1, int32_t c2, const float* chan_bias,
+                             const float* gamma, const float* beta, int64_t n, int64_t hw, int32_t groups, float eps,
+                             int32_t act, void* z, int32_t z_layout, float* stats, void* ws, int64_t ws_bytes,
+                             sp_stream_t stream);
+int sp_groupnorm_bf16_bwd_ex(const void* dz, const void* x1, const void* x2, int32_t c1, int32_t c2,
+                             const float* chan_bias, const float* gamma, const float* beta, const float* stats,
+                             int64_t n, int64_t hw, int32_t groups, int32_t act, void* dx1, void* dx2, int32_t dx_layout,
+                             const void* add1, const void* add2, const void* add1b, void* ws, int64_t ws_bytes,
+                             sp_stream_t stream);
+/* sp_conv3x3_bf16_ws with the input in a chosen layout (in_layout 0 NHWC, 1 channel-blocked
+ * [n][cin/16][h][w][16]: every 16-channel stage reads whole cache lines); in_layout 1 needs
+ * sp_conv3x3_bf16_blk_supported (w % 32 == 0, h % 16 == 0).  The output stays NHWC. */
+int sp_conv3x3_bf16_blk_supported(int32_t cin, int32_t cout, int32_t h, int32_t w);
+int sp_conv3x3_bf16_ex(const void* x, int32_t in_layout, const void* wp, const float* bias, const void* res, int64_t n,
+                       int32_t cin, int32_t cout, int32_t h, int32_t w, void* y, void* ws, int64_t ws_bytes,
+                       sp_stream_t stream);
 int sp_attention_bf16_supported(int64_t batch, int32_t heads, int64_t n, int64_t m, int32_t d);
 /* multi-head softmax(q k^T scale) v on bf16 token rows (self: m = n; cross: kv_shared = 1 for
  * one context row for the whole batch); lse [batch heads][n] fp32 for the VJP. */

@@ -130,7 +130,7 @@ __device__ __forceinline__ int cv_chunk(int p) { return p & 1; }
 // without the upsampled tensor in HBM.
 // part != NULL (split-K, gridDim.z parts over the input-channel stages): part z of the
 // contraction is stored as fp32 to part[z][n h w][cout] without bias / residual (k_conv_reduce).
-template <int TC, bool UP>
+template <int TC, bool UP, bool BLK = false>
 __global__ __launch_bounds__(kBlock, TC == 4 ? 1 : 2) void k_conv3x3_bf16(const u16* __restrict__ x, const u16* __restrict__ wp,
                                                          const float* __restrict__ bias, const u16* __restrict__ res,
                                                          int n, int cin, int cout, int h, int w,
@@ -176,12 +176,15 @@ __global__ __launch_bounds__(kBlock, TC == 4 ? 1 : 2) void k_conv3x3_bf16(const 
             if (nn < n && (unsigned)hi < (unsigned)h && (unsigned)wi < (unsigned)w) {
                 if constexpr (UP)
                     poff[k] = (((int64_t)nn * (h >> 1) + (hi >> 1)) * (w >> 1) + (wi >> 1)) * cin + half * 8;
+                else if constexpr (BLK)  // [n][cin / 16][h][w][16]: stage ks is plane ks of the sample
+                    poff[k] = ((int64_t)nn * (cin >> 4) * h * w + (int64_t)hi * w + wi) * 16 + half * 8;
                 else
                     poff[k] = (((int64_t)nn * h + hi) * w + wi) * cin + half * 8;
             }
         }
     }
     bq_u4 sw[G::NW], spx[G::NP];
+    const int64_t kstride = BLK ? (int64_t)h * w * 16 : 16;  // elements between stages' pieces
     auto gload = [&](int ks) {
         const bq_u4* __restrict__ ws = wsrc + (int64_t)ks * (9 * 64 * 2);
 #pragma unroll
@@ -194,7 +197,7 @@ __global__ __launch_bounds__(kBlock, TC == 4 ? 1 : 2) void k_conv3x3_bf16(const 
 #if BQ_EXP == 10  // diagnostics (wrong results): every patch piece from one cached 32-byte line per stage
             spx[k] = poff[k] >= 0 ? *reinterpret_cast<const bq_u4*>(x + (tid & 1) * 8 + ks * 16) : bq_u4{0u, 0u, 0u, 0u};
 #else
-            spx[k] = poff[k] >= 0 ? *reinterpret_cast<const bq_u4*>(x + poff[k] + ks * 16) : bq_u4{0u, 0u, 0u, 0u};
+            spx[k] = poff[k] >= 0 ? *reinterpret_cast<const bq_u4*>(x + poff[k] + ks * kstride) : bq_u4{0u, 0u, 0u, 0u};
 #endif
     };
     auto lstore = [&]() {
@@ -468,7 +471,7 @@ static int conv_parts(int n, int cin, int cout, int h, int w) {
     return parts;
 }
 
-template <int TC, bool UP>
+template <int TC, bool UP, bool BLK = false>
 static void conv_bf16_launch(const u16* x, const u16* wp, const float* bias, const u16* res, int n, int cin,
                              int cout, int h, int w, u16* y, hipStream_t s, float* part = nullptr, int parts = 1) {
     using G = CvGeo<TC>;
@@ -476,7 +479,7 @@ static void conv_bf16_launch(const u16* x, const u16* wp, const float* bias, con
     const int cbn = (cout + 63) / 64;
     const int64_t tiles = conv_tiles<TC>(n, h, w);
     const double flops = 18.0 * n * (double)h * w * cin * cout;
-    launch_w(TK_CONV_BF16, flops, k_conv3x3_bf16<TC, UP>, dim3(cbn, static_cast<unsigned>(tiles), parts), dim3(kBlock),
+    launch_w(TK_CONV_BF16, flops, k_conv3x3_bf16<TC, UP, BLK>, dim3(cbn, static_cast<unsigned>(tiles), parts), dim3(kBlock),
              s, x, wp, bias, res, n, cin, cout, h, w, y, parts > 1 ? part : nullptr);
     if (parts > 1) {
         const int64_t total = (int64_t)n * h * w * cout;
@@ -776,7 +779,7 @@ __global__ __launch_bounds__(64) void k_gnb_final_bwd(const float* __restrict__ 
 template <bool ACT>
 __global__ __launch_bounds__(kBlock) void k_gnb_apply(const u16* __restrict__ x1, const u16* __restrict__ x2, int c1,
                                                       int c2, const float* __restrict__ co, int64_t hw, int chunk_px,
-                                                      u16* __restrict__ z) {
+                                                      u16* __restrict__ z, int blk) {
     const int c = c1 + c2, cv = c / 8, nn = blockIdx.y, tid = threadIdx.x;
     const int64_t nc = (int64_t)gridDim.y * c;
     const int64_t p0 = (int64_t)blockIdx.x * chunk_px, p1 = std::min<int64_t>(hw, p0 + chunk_px);
@@ -798,7 +801,10 @@ __global__ __launch_bounds__(kBlock) void k_gnb_apply(const u16* __restrict__ x1
                 const float yv = fmaf(f[e], sa[e], sb[e]);
                 f[e] = ACT ? silu_f(yv) : yv;
             }
-            *reinterpret_cast<bq_u4*>(z + ((int64_t)nn * hw + p) * c + 8 * j) = pack8(f);
+            // blk: z in the channel-blocked layout [n][c / 16][hw][16] the conv tile reads best
+            const int64_t zo = blk ? (((int64_t)nn * (c >> 4) + (j >> 1)) * hw + p) * 16 + 8 * (j & 1)
+                                   : ((int64_t)nn * hw + p) * c + 8 * j;
+            *reinterpret_cast<bq_u4*>(z + zo) = pack8(f);
         };
         int64_t p = p0 + row;
         for (; p + (GNB_U - 1) * rows < p1; p += GNB_U * rows) {  // GNB_U pixels' loads in flight
@@ -826,7 +832,7 @@ __global__ __launch_bounds__(kBlock) void k_gnb_bwd_apply(const u16* __restrict_
                                                           int64_t hw, int chunk_px, u16* __restrict__ dx1,
                                                           u16* __restrict__ dx2, const u16* __restrict__ add1,
                                                           const u16* __restrict__ add2,
-                                                          const u16* __restrict__ add1b) {
+                                                          const u16* __restrict__ add1b, int blk) {
     const int c = c1 + c2, cv = c / 8, nn = blockIdx.y, tid = threadIdx.x;
     const int64_t nc = (int64_t)gridDim.y * c;
     const int64_t p0 = (int64_t)blockIdx.x * chunk_px, p1 = std::min<int64_t>(hw, p0 + chunk_px);
@@ -851,7 +857,7 @@ __global__ __launch_bounds__(kBlock) void k_gnb_bwd_apply(const u16* __restrict_
         const u16* __restrict__ ab = first ? add1b : nullptr;
         const u16* __restrict__ xs = first ? x1 : x2;
         // one pixel from its loaded vectors (x, dy', and the addends or zeros)
-        auto one = [&](bq_u4 xv, bq_u4 dv, bq_u4 av, bq_u4 bv, int64_t off) {
+        auto one = [&](bq_u4 xv, bq_u4 dv, bq_u4 av, bq_u4 bv, int64_t off, int64_t p) {
             float f[8], d[8], o[8];
             unpack8(xv, f);
             unpack8(dv, d);
@@ -877,7 +883,9 @@ __global__ __launch_bounds__(kBlock) void k_gnb_bwd_apply(const u16* __restrict_
 #pragma unroll
                 for (int e = 0; e < 8; ++e) o[e] += t[e];
             }
-            *reinterpret_cast<bq_u4*>(dst + off) = pack8(o);
+            // blk (one part): dx in the channel-blocked layout [n][c / 16][hw][16]
+            const int64_t oo = blk ? (((int64_t)nn * (cp >> 4) + (chp >> 4)) * hw + p) * 16 + (chp & 15) : off;
+            *reinterpret_cast<bq_u4*>(dst + oo) = pack8(o);
         };
         const bq_u4 zero4 = {0u, 0u, 0u, 0u};
         auto ld = [&](const u16* __restrict__ src, int64_t off) {
@@ -895,12 +903,13 @@ __global__ __launch_bounds__(kBlock) void k_gnb_bwd_apply(const u16* __restrict_
                 bv[u] = ld(ab, off);
             }
 #pragma unroll
-            for (int u = 0; u < GNB_U; ++u) one(xv[u], dv[u], av[u], bv[u], ((int64_t)nn * hw + p + u * rows) * cp + chp);
+            for (int u = 0; u < GNB_U; ++u)
+                one(xv[u], dv[u], av[u], bv[u], ((int64_t)nn * hw + p + u * rows) * cp + chp, p + u * rows);
         }
         for (; p < p1; p += rows) {
             const int64_t off = ((int64_t)nn * hw + p) * cp + chp;
             one(*reinterpret_cast<const bq_u4*>(xs + off),
-                *reinterpret_cast<const bq_u4*>(dz + ((int64_t)nn * hw + p) * c + ch), ld(a, off), ld(ab, off), off);
+                *reinterpret_cast<const bq_u4*>(dz + ((int64_t)nn * hw + p) * c + ch), ld(a, off), ld(ab, off), off, p);
         }
     }
 }
@@ -1543,8 +1552,9 @@ int64_t sp_conv3x3_bf16_packed_size(int32_t cin, int32_t cout) {
 // zero); the input VJP is the same call with the pack of W'[ci][co][2-ky][2-kx].
 static int conv_bf16_call(const void* x, const void* wp, const float* bias, const void* res, int64_t n, int32_t cin,
                           int32_t cout, int32_t h, int32_t w, void* y, sp_stream_t stream, bool up,
-                          void* ws = nullptr, int64_t ws_bytes = 0) {
+                          void* ws = nullptr, int64_t ws_bytes = 0, int blk = 0) {
     if (!x || !wp || !y || n <= 0 || !sp_conv3x3_bf16_supported(cin, cout, h, w)) return SP_EINVAL;
+    if (blk && (up || conv_tc(h, w) != 32)) return SP_EINVAL;
     if (up && (h % 2 || w % 2)) return SP_EINVAL;
     if (n * h * (int64_t)w * std::max(cin, cout) >= (int64_t(1) << 40) || n >= (int64_t(1) << 30)) return SP_EINVAL;
     hipStream_t s = static_cast<hipStream_t>(stream);
@@ -1565,6 +1575,10 @@ static int conv_bf16_call(const void* x, const void* wp, const float* bias, cons
     int parts = conv_parts(ni, cin, cout, h, w);
     if (parts > 1 && (!ws || ws_bytes < 4 * parts * (int64_t)ni * h * w * cout)) parts = 1;
     float* part = static_cast<float*>(ws);
+    if (blk) {
+        conv_bf16_launch<32, false, true>(xx, ww, bias, rr, ni, cin, cout, h, w, yy, s, part, parts);
+        return check_launch("sp_conv3x3_bf16_ex");
+    }
     switch (conv_tc(h, w)) {
         case 32: conv_bf16_launch<32, false>(xx, ww, bias, rr, ni, cin, cout, h, w, yy, s, part, parts); break;
         case 16: conv_bf16_launch<16, false>(xx, ww, bias, rr, ni, cin, cout, h, w, yy, s, part, parts); break;
@@ -1588,6 +1602,20 @@ int64_t sp_conv3x3_bf16_workspace(int64_t n, int32_t cin, int32_t cout, int32_t 
 int sp_conv3x3_bf16_ws(const void* x, const void* wp, const float* bias, const void* res, int64_t n, int32_t cin,
                        int32_t cout, int32_t h, int32_t w, void* y, void* ws, int64_t ws_bytes, sp_stream_t stream) {
     return conv_bf16_call(x, wp, bias, res, n, cin, cout, h, w, y, stream, false, ws, ws_bytes);
+}
+
+// sp_conv3x3_bf16_ws with the input in a chosen layout: in_layout 0 = NHWC, 1 = channel-blocked
+// [n][cin / 16][h][w][16] (each 16-channel stage of the tile reads whole lines; TC = 32 shapes only:
+// sp_conv3x3_bf16_blk_supported).  The output stays NHWC.
+int sp_conv3x3_bf16_blk_supported(int32_t cin, int32_t cout, int32_t h, int32_t w) {
+    return sp_conv3x3_bf16_supported(cin, cout, h, w) && conv_tc(h, w) == 32;
+}
+
+int sp_conv3x3_bf16_ex(const void* x, int32_t in_layout, const void* wp, const float* bias, const void* res, int64_t n,
+                       int32_t cin, int32_t cout, int32_t h, int32_t w, void* y, void* ws, int64_t ws_bytes,
+                       sp_stream_t stream) {
+    if (in_layout != 0 && in_layout != 1) return SP_EINVAL;
+    return conv_bf16_call(x, wp, bias, res, n, cin, cout, h, w, y, stream, false, ws, ws_bytes, in_layout);
 }
 
 int sp_conv3x3_bf16(const void* x, const void* wp, const float* bias, const void* res, int64_t n, int32_t cin,
@@ -1689,8 +1717,19 @@ int64_t sp_groupnorm_bf16_workspace(int64_t n, int32_t c, int64_t hw) {
 int sp_groupnorm_bf16_fwd(const void* x1, const void* x2, int32_t c1, int32_t c2, const float* chan_bias,
                           const float* gamma, const float* beta, int64_t n, int64_t hw, int32_t groups, float eps,
                           int32_t act, void* z, float* stats, void* ws, int64_t ws_bytes, sp_stream_t stream) {
+    return sp_groupnorm_bf16_fwd_ex(x1, x2, c1, c2, chan_bias, gamma, beta, n, hw, groups, eps, act, z, 0, stats, ws,
+                                    ws_bytes, stream);
+}
+
+// z_layout 1: z in the channel-blocked layout [n][c / 16][hw][16] (c % 16 == 0), the conv tile's
+// preferred input (sp_conv3x3_bf16_ex)
+int sp_groupnorm_bf16_fwd_ex(const void* x1, const void* x2, int32_t c1, int32_t c2, const float* chan_bias,
+                             const float* gamma, const float* beta, int64_t n, int64_t hw, int32_t groups, float eps,
+                             int32_t act, void* z, int32_t z_layout, float* stats, void* ws, int64_t ws_bytes,
+                             sp_stream_t stream) {
     if (!x1 || (c2 && !x2) || !z || !stats || !ws || n <= 0 || hw <= 0 || !sp_groupnorm_bf16_supported(c1, c2, groups))
         return SP_EINVAL;
+    if (z_layout != 0 && (z_layout != 1 || (c1 + c2) % 16)) return SP_EINVAL;
     const int c = c1 + c2;
     if (ws_bytes < sp_groupnorm_bf16_workspace(n, c, hw) || n * hw * c >= (int64_t(1) << 40) || n > 65535)
         return SP_EINVAL;
@@ -1708,10 +1747,10 @@ int sp_groupnorm_bf16_fwd(const void* x1, const void* x2, int32_t c1, int32_t c2
     const dim3 grid(g.chunks, static_cast<unsigned>(n));
     if (act)
         launch(0, k_gnb_apply<true>, grid, dim3(kBlock), s, a, b, c1, c2, static_cast<const float*>(co), hw, g.chunk_px,
-               static_cast<u16*>(z));
+               static_cast<u16*>(z), static_cast<int>(z_layout));
     else
         launch(0, k_gnb_apply<false>, grid, dim3(kBlock), s, a, b, c1, c2, static_cast<const float*>(co), hw,
-               g.chunk_px, static_cast<u16*>(z));
+               g.chunk_px, static_cast<u16*>(z), static_cast<int>(z_layout));
     return check_launch("sp_groupnorm_bf16_fwd");
 }
 
@@ -1721,9 +1760,21 @@ int sp_groupnorm_bf16_bwd(const void* dz, const void* x1, const void* x2, int32_
                           const float* chan_bias, const float* gamma, const float* beta, const float* stats,
                           int64_t n, int64_t hw, int32_t groups, int32_t act, void* dx1, void* dx2, const void* add1,
                           const void* add2, const void* add1b, void* ws, int64_t ws_bytes, sp_stream_t stream) {
+    return sp_groupnorm_bf16_bwd_ex(dz, x1, x2, c1, c2, chan_bias, gamma, beta, stats, n, hw, groups, act, dx1, dx2,
+                                    0, add1, add2, add1b, ws, ws_bytes, stream);
+}
+
+// dx_layout 1 (one part, c2 == 0, c1 % 16 == 0): dx1 in the channel-blocked layout [n][c / 16][hw][16]
+// (the addends stay NHWC)
+int sp_groupnorm_bf16_bwd_ex(const void* dz, const void* x1, const void* x2, int32_t c1, int32_t c2,
+                             const float* chan_bias, const float* gamma, const float* beta, const float* stats,
+                             int64_t n, int64_t hw, int32_t groups, int32_t act, void* dx1, void* dx2, int32_t dx_layout,
+                             const void* add1, const void* add2, const void* add1b, void* ws, int64_t ws_bytes,
+                             sp_stream_t stream) {
     if (!dz || !x1 || (c2 && (!x2 || !dx2)) || !dx1 || !stats || !ws || n <= 0 || hw <= 0 ||
         !sp_groupnorm_bf16_supported(c1, c2, groups))
         return SP_EINVAL;
+    if (dx_layout != 0 && (dx_layout != 1 || c2 || c1 % 16)) return SP_EINVAL;
     const int c = c1 + c2;
     if (ws_bytes < sp_groupnorm_bf16_workspace(n, c, hw) || n * hw * c >= (int64_t(1) << 40) || n > 65535)
         return SP_EINVAL;
@@ -1750,11 +1801,13 @@ int sp_groupnorm_bf16_bwd(const void* dz, const void* x1, const void* x2, int32_
     if (act)
         launch(0, k_gnb_bwd_apply<true>, grid, dim3(kBlock), s, d, a, b, c1, c2, static_cast<const float*>(co),
                static_cast<const float*>(co2), hw, g.chunk_px, static_cast<u16*>(dx1), static_cast<u16*>(dx2),
-               static_cast<const u16*>(add1), static_cast<const u16*>(add2), static_cast<const u16*>(add1b));
+               static_cast<const u16*>(add1), static_cast<const u16*>(add2), static_cast<const u16*>(add1b),
+               static_cast<int>(dx_layout));
     else
         launch(0, k_gnb_bwd_apply<false>, grid, dim3(kBlock), s, d, a, b, c1, c2, static_cast<const float*>(co),
                static_cast<const float*>(co2), hw, g.chunk_px, static_cast<u16*>(dx1), static_cast<u16*>(dx2),
-               static_cast<const u16*>(add1), static_cast<const u16*>(add2), static_cast<const u16*>(add1b));
+               static_cast<const u16*>(add1), static_cast<const u16*>(add2), static_cast<const u16*>(add1b),
+               static_cast<int>(dx_layout));
     return check_launch("sp_groupnorm_bf16_bwd");
 }
 

@@ -122,20 +122,33 @@ def _pad_channels(x: Tensor, c: int) -> Tensor:
     return out
 
 
-def _conv_launch(x: Tensor, pack: Tensor, bias: Tensor | None, res: Tensor | None, cout: int) -> Tensor:
+def _conv_launch(x: Tensor, pack: Tensor, bias: Tensor | None, res: Tensor | None, cout: int,
+                 shape: tuple | None = None) -> Tensor:
+    """conv3x3 on the bf16 tile; ``shape`` given: x is a flat buffer in the channel-blocked layout
+    [n][cin / 16][h][w][16] of that (n, cin, h, w) (``blocked_ok``), else a channels-last tensor."""
     from ..runtime import split_k_enabled
     from .layers import _query
 
     lib = _hip.load_library()
-    n, cin, h, w = x.shape
+    n, cin, h, w = x.shape if shape is None else shape
     y = torch.empty(n, cout, h, w, device=x.device, dtype=BF16, memory_format=CL)
     # split-K where the tiles leave CUs idle (torch's caching allocator on the launch stream)
     nb = _query("sp_conv3x3_bf16_workspace", n, cin, cout, h, w) if split_k_enabled() else 0
     ws = torch.empty(max(nb // 4, 1), device=x.device, dtype=torch.float32)
-    _hip.check(lib.sp_conv3x3_bf16_ws(_p(x), _p(pack, cl=False), None if bias is None else bias.data_ptr(), _p(res),
-                                      n, cin, cout, h, w, _p(y), ws.data_ptr() if nb else None, nb,
-                                      _hip.stream_of(x)), "sp_conv3x3_bf16_ws")
+    _hip.check(lib.sp_conv3x3_bf16_ex(_p(x, cl=shape is None), 0 if shape is None else 1, _p(pack, cl=False),
+                                      None if bias is None else bias.data_ptr(), _p(res), n, cin, cout, h, w, _p(y),
+                                      ws.data_ptr() if nb else None, nb, _hip.stream_of(x)), "sp_conv3x3_bf16_ex")
     return y
+
+
+def blocked_ok(cin: int, cout: int, h: int, w: int) -> bool:
+    """Whether a conv's input can be handed over channel-blocked ([n][cin/16][h][w][16]: each 16-channel
+    stage of the tile then reads whole cache lines instead of 32 bytes of every pixel's row);
+    ``SAMPLERS_AMD_BF16_BLOCKED=0`` keeps NHWC (A/B)."""
+    import os
+
+    return (cin % 16 == 0 and os.environ.get("SAMPLERS_AMD_BF16_BLOCKED", "1") != "0"
+            and bool(_hip.load_library().sp_conv3x3_bf16_blk_supported(cin, cout, h, w)))
 
 
 class _ConvBf16Fn(torch.autograd.Function):
@@ -272,42 +285,52 @@ def _gn_ws(lib, n: int, c: int, hw: int, device) -> tuple[Tensor, int]:
     return torch.empty(nb, device=device, dtype=torch.uint8), nb
 
 
-def _gn_fwd_raw(norm: nn.GroupNorm, x1: Tensor, x2: Tensor | None, cb: Tensor | None) -> tuple[Tensor, Tensor]:
-    """(z, stats) of ``sp_groupnorm_bf16_fwd`` over cat(x1, x2) (+ cb) read in place."""
+def _gn_fwd_raw(norm: nn.GroupNorm, x1: Tensor, x2: Tensor | None, cb: Tensor | None,
+                blocked: bool = False) -> tuple[Tensor, Tensor]:
+    """(z, stats) of ``sp_groupnorm_bf16_fwd_ex`` over cat(x1, x2) (+ cb) read in place; ``blocked``:
+    z as a flat buffer in the channel-blocked layout a conv tile reads (``_conv_launch(shape=)``)."""
     lib = _hip.load_library()
     n, c1, h, w = x1.shape
     c2 = 0 if x2 is None else x2.shape[1]
     c, hw, g = c1 + c2, h * w, norm.num_groups
     gamma, beta = _gn_params(norm)
-    z = torch.empty(n, c, h, w, device=x1.device, dtype=BF16, memory_format=CL)
+    if blocked:
+        z = torch.empty(n * c * hw, device=x1.device, dtype=BF16)
+    else:
+        z = torch.empty(n, c, h, w, device=x1.device, dtype=BF16, memory_format=CL)
     stats = torch.empty(2, n * g, device=x1.device, dtype=torch.float32)
     ws, nb = _gn_ws(lib, n, c, hw, x1.device)
-    _hip.check(lib.sp_groupnorm_bf16_fwd(_p(x1), _p(x2), c1, c2, None if cb is None else cb.data_ptr(),
-                                         None if gamma is None else gamma.data_ptr(),
-                                         None if beta is None else beta.data_ptr(), n, hw, g, float(norm.eps),
-                                         int(norm.act), _p(z), stats.data_ptr(), ws.data_ptr(), nb,
-                                         _hip.stream_of(x1)), "sp_groupnorm_bf16_fwd")
+    _hip.check(lib.sp_groupnorm_bf16_fwd_ex(_p(x1), _p(x2), c1, c2, None if cb is None else cb.data_ptr(),
+                                            None if gamma is None else gamma.data_ptr(),
+                                            None if beta is None else beta.data_ptr(), n, hw, g, float(norm.eps),
+                                            int(norm.act), _p(z, cl=not blocked), int(blocked), stats.data_ptr(),
+                                            ws.data_ptr(), nb, _hip.stream_of(x1)), "sp_groupnorm_bf16_fwd_ex")
     return z, stats
 
 
 def _gn_bwd_raw(norm: nn.GroupNorm, dz: Tensor, x1: Tensor, x2: Tensor | None, cb: Tensor | None, stats: Tensor,
                 add1: Tensor | None = None, add2: Tensor | None = None, out1: Tensor | None = None,
-                out2: Tensor | None = None) -> tuple[Tensor, Tensor | None]:
+                out2: Tensor | None = None, blocked: bool = False) -> tuple[Tensor, Tensor | None]:
     """Input VJP of ``_gn_fwd_raw`` into the parts' layouts, + the addends (channels-last, shaped
-    like the parts) added in the kernel; ``out1`` / ``out2`` may be the addends (in place)."""
+    like the parts) added in the kernel; ``out1`` / ``out2`` may be the addends (in place);
+    ``blocked`` (one part): dx1 as a flat channel-blocked buffer for the next conv VJP."""
     lib = _hip.load_library()
     n, c1, h, w = x1.shape
     c2 = 0 if x2 is None else x2.shape[1]
     gamma, beta = _gn_params(norm)
     dz = nhwc(dz.to(BF16))
-    dx1 = torch.empty_like(x1, memory_format=CL) if out1 is None else out1
+    if blocked:
+        dx1 = torch.empty(n * c1 * h * w, device=x1.device, dtype=BF16)
+    else:
+        dx1 = torch.empty_like(x1, memory_format=CL) if out1 is None else out1
     dx2 = None if x2 is None else (torch.empty_like(x2, memory_format=CL) if out2 is None else out2)
     ws, nb = _gn_ws(lib, n, c1 + c2, h * w, x1.device)
-    _hip.check(lib.sp_groupnorm_bf16_bwd(_p(dz), _p(x1), _p(x2), c1, c2, None if cb is None else cb.data_ptr(),
-                                         None if gamma is None else gamma.data_ptr(),
-                                         None if beta is None else beta.data_ptr(), stats.data_ptr(), n, h * w,
-                                         norm.num_groups, int(norm.act), _p(dx1), _p(dx2), _p(add1), _p(add2), None,
-                                         ws.data_ptr(), nb, _hip.stream_of(dz)), "sp_groupnorm_bf16_bwd")
+    _hip.check(lib.sp_groupnorm_bf16_bwd_ex(_p(dz), _p(x1), _p(x2), c1, c2, None if cb is None else cb.data_ptr(),
+                                            None if gamma is None else gamma.data_ptr(),
+                                            None if beta is None else beta.data_ptr(), stats.data_ptr(), n, h * w,
+                                            norm.num_groups, int(norm.act), _p(dx1, cl=not blocked), _p(dx2),
+                                            int(blocked), _p(add1), _p(add2), None, ws.data_ptr(), nb,
+                                            _hip.stream_of(dz)), "sp_groupnorm_bf16_bwd_ex")
     return dx1, dx2
 
 
@@ -493,11 +516,15 @@ class _ResnetBlockBf16Fn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, block, tb, x1, x2):
         cout = block.conv2.weight.shape[0]
-        z1, st1 = _gn_fwd_raw(block.norm1, x1, x2, None)
+        n, c1, hh, ww = x1.shape
+        cin = c1 + (0 if x2 is None else x2.shape[1])
+        # the GroupNorm outputs feed only the convs: handed over channel-blocked where the tile takes it
+        b1, b2 = blocked_ok(cin, cout, hh, ww), blocked_ok(cout, cout, hh, ww)
+        z1, st1 = _gn_fwd_raw(block.norm1, x1, x2, None, blocked=b1)
         h1 = _conv_launch(z1, conv_pack(block.conv1, False), _bias_f32(block.conv1, block.conv1.bias), None,
-                          block.conv1.weight.shape[0])
+                          block.conv1.weight.shape[0], shape=(n, cin, hh, ww) if b1 else None)
         del z1
-        z2, st2 = _gn_fwd_raw(block.norm2, h1, None, tb)
+        z2, st2 = _gn_fwd_raw(block.norm2, h1, None, tb, blocked=b2)
         if block.conv_shortcut is None:
             short = x1
         else:
@@ -509,7 +536,8 @@ class _ResnetBlockBf16Fn(torch.autograd.Function):
             if x2 is not None:
                 r.addmm_(_rows(x2), w2.t())
             short = r.reshape(n, h, w, cout).permute(0, 3, 1, 2)
-        out = _conv_launch(z2, conv_pack(block.conv2, False), _bias_f32(block.conv2, block.conv2.bias), short, cout)
+        out = _conv_launch(z2, conv_pack(block.conv2, False), _bias_f32(block.conv2, block.conv2.bias), short, cout,
+                           shape=(n, cout, hh, ww) if b2 else None)
         ctx.block = block
         ctx.save_for_backward(x1, x2, h1, tb, st1, st2)
         return out
@@ -521,11 +549,17 @@ class _ResnetBlockBf16Fn(torch.autograd.Function):
         dout = nhwc(dout.to(BF16))
         cout = blk.conv2.weight.shape[0]
         dz2 = _conv_launch(_pad_channels(dout, _ceil(cout, 16)), conv_pack(blk.conv2, True), None, None, cout)
-        dh1, _ = _gn_bwd_raw(blk.norm2, dz2, h1, None, tb, st2)
-        del dz2
         cmid = blk.conv1.weight.shape[0]
-        dz1 = _conv_launch(_pad_channels(dh1, _ceil(cmid, 16)), conv_pack(blk.conv1, True), None, None,
-                           blk.conv1.weight.shape[1])
+        cin = blk.conv1.weight.shape[1]
+        n, _, hh, ww = h1.shape
+        # dh1 feeds only conv1's VJP: channel-blocked where the tile takes it
+        bl = cmid % 16 == 0 and blocked_ok(cmid, cin, hh, ww)
+        dh1, _ = _gn_bwd_raw(blk.norm2, dz2, h1, None, tb, st2, blocked=bl)
+        del dz2
+        if bl:
+            dz1 = _conv_launch(dh1, conv_pack(blk.conv1, True), None, None, cin, shape=(n, cmid, hh, ww))
+        else:
+            dz1 = _conv_launch(_pad_channels(dh1, _ceil(cmid, 16)), conv_pack(blk.conv1, True), None, None, cin)
         del dh1
         if blk.conv_shortcut is None:  # identity shortcut: dx1 = GN1^T dz1 + dout
             dx1, dx2 = _gn_bwd_raw(blk.norm1, dz1, x1, x2, None, st1, add1=dout)

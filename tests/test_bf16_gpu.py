@@ -355,6 +355,73 @@ def test_transformer_block_bf16_residual_handoff(cuda, parity_record):
     assert sum("CUDAFunctor_add" in s for s in names) <= 3, [s for s in names if "add" in s.lower()]
 
 
+def _blocked(t):
+    """(n, c, h, w) -> flat [n][c / 16][h][w][16] (the conv tile's channel-blocked input layout)."""
+    n, c, h, w = t.shape
+    return t.permute(0, 2, 3, 1).reshape(n, h, w, c // 16, 16).permute(0, 3, 1, 2, 4).contiguous().reshape(-1)
+
+
+@pytest.mark.parametrize("shape", [(2, 64, 128, 32, 64), (1, 320, 320, 64, 64), (3, 32, 64, 16, 32)])
+def test_conv3x3_bf16_blocked_input_bitwise(cuda, shape):
+    """sp_conv3x3_bf16_ex with the channel-blocked input equals the NHWC call bit for bit (same
+    data, same summation order), split-K included."""
+    from samplers_amd.networks import bf16
+
+    n, ci, co, h, w = shape
+    gen = torch.Generator().manual_seed(ci + co)
+    conv = torch.nn.Conv2d(ci, co, 3, padding=1).to(BF).requires_grad_(False).to(cuda)
+    x = torch.randn(n, ci, h, w, generator=gen).to(BF).to(cuda).contiguous(memory_format=torch.channels_last)
+    pk, b = bf16.conv_pack(conv, False), bf16._bias_f32(conv, conv.bias)
+    assert bf16.blocked_ok(ci, co, h, w)
+    y0 = bf16._conv_launch(x, pk, b, None, co)
+    y1 = bf16._conv_launch(_blocked(x), pk, b, None, co, shape=(n, ci, h, w))
+    assert torch.equal(y0, y1)
+
+
+def test_groupnorm_bf16_blocked_outputs_bitwise(cuda):
+    """GroupNorm forward / VJP writing the channel-blocked layout equal the NHWC results bit for bit."""
+    from samplers_amd.networks import bf16
+    from samplers_amd.networks.layers import GroupNormAct
+
+    gen = torch.Generator().manual_seed(3)
+    norm = GroupNormAct(32, 128, eps=1e-6, act=True).to(cuda, BF).requires_grad_(False)
+    x = torch.randn(2, 128, 32, 32, generator=gen).to(BF).to(cuda).contiguous(memory_format=torch.channels_last)
+    dz = torch.randn(2, 128, 32, 32, generator=gen).to(BF).to(cuda).contiguous(memory_format=torch.channels_last)
+    z0, st = bf16._gn_fwd_raw(norm, x, None, None)
+    z1, _ = bf16._gn_fwd_raw(norm, x, None, None, blocked=True)
+    assert torch.equal(_blocked(z0), z1)
+    d0, _ = bf16._gn_bwd_raw(norm, dz, x, None, None, st)
+    d1, _ = bf16._gn_bwd_raw(norm, dz, x, None, None, st, blocked=True)
+    assert torch.equal(_blocked(d0), d1)
+
+
+def test_resnet_block_bf16_blocked_equals_nhwc(cuda, monkeypatch):
+    """The fused bf16 ResnetBlock with channel-blocked GroupNorm -> conv hand-offs equals the NHWC
+    hand-offs bit for bit, forward and input VJP (skip input and 1x1 shortcut included)."""
+    from samplers_amd.networks.unet2d import ResnetBlock2D
+
+    torch.manual_seed(1)
+    blk = ResnetBlock2D(128 + 64, 128, 64, 32, 1e-5).to(cuda, BF).requires_grad_(False)
+    gen = torch.Generator().manual_seed(2)
+    x = torch.randn(2, 128, 32, 64, generator=gen).to(BF).to(cuda)
+    skip = torch.randn(2, 64, 32, 64, generator=gen).to(BF).to(cuda)
+    temb = torch.randn(2, 64, generator=gen).to(BF).to(cuda)
+    cot = torch.randn(2, 128, 32, 64, generator=gen).to(BF).to(cuda)
+
+    def run():
+        xr, sr = x.clone().requires_grad_(True), skip.clone().requires_grad_(True)
+        with torch.enable_grad():
+            out = blk(xr, temb, skip=sr)
+        gx, gs = torch.autograd.grad(out, (xr, sr), cot)
+        return out, gx, gs
+
+    a = run()
+    monkeypatch.setenv("SAMPLERS_AMD_BF16_BLOCKED", "0")
+    b = run()
+    for u, v in zip(a, b):
+        assert torch.equal(u, v)
+
+
 # ---- whole priors -----------------------------------------------------------------------------
 
 def _fwd_vjp(fn, x, cot):
