@@ -52,6 +52,8 @@ for step in "$@"; do
                   run conv_base9 300 python -u tools/bench_conv_bf16.py ;;
         convexp10) run conv_exp10 300 env SAMPLERS_HIP_LIB=samplers_amd/lib/variants/lib_exp10.so python -u tools/bench_conv_bf16.py
                    run conv_base10 300 python -u tools/bench_conv_bf16.py ;;
+        blkab) run psld_blk_off 600 env SAMPLERS_AMD_BF16_BLOCKED=0 python -u tools/bench_psld.py --dtype bf16 --steps 3 --warmup 2
+               run psld_blk_on 600 python -u tools/bench_psld.py --dtype bf16 --steps 3 --warmup 2 ;;
         convbf16) run conv_bf16 300 python -u tools/bench_conv_bf16.py --miopen ;;
         convbf16sq) FILTER=k_conv3x3_bf16 NAME=convbf16 run conv_bf16_sq 600 tools/sq_pmc.sh tools/bench_conv_bf16.py --reps 3 --shapes sd ;;
         gputests) run gpu_tests 1100 python -u -m pytest tests -m gpu -q --timeout 400 --timeout-method thread ;;
