@@ -81,6 +81,9 @@ def parse():
     p.add_argument("--graph", action="store_true",
                    help="replay one hipGraph-captured step (samplers/graph.py); kernel times and "
                         "the roofline then come from the eager warmup steps")
+    p.add_argument("--dtype", choices=("fp32", "bf16"), default="fp32",
+                   help="the prior's dtype (fp32: the headline, the reference's run_dps.py:14; bf16: the "
+                        "reference's bf16 precision on the bf16 NHWC kernels, behind the fp32 sampler loop)")
     p.add_argument("--cpu-seconds", type=float, default=15.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
     return p.parse_args()
@@ -189,7 +192,7 @@ def measure_gather(x: torch.Tensor, reps: int = 3) -> dict:
                 gathered_shape=list(full.shape), own_slice_checked=True)
 
 
-def build_workload(config: str, batch: int, image: int, rank: int, device):
+def build_workload(config: str, batch: int, image: int, rank: int, device, dtype=torch.float32):
     from samplers_amd.inverse_problem import InverseProblem
     from samplers_amd.networks.ddpm import DDPMNetwork
     from samplers_amd.noise import GaussianNoise
@@ -208,7 +211,7 @@ def build_workload(config: str, batch: int, image: int, rank: int, device):
     x_true = torch.rand((batch, *shape), generator=gen) * 2 - 1
     y_clean = op.apply(x_true.to(device))  # HIP operator
     y = y_clean + (0.05 * torch.randn(tuple(y_clean.shape), generator=gen)).to(device)
-    net = DDPMNetwork.from_config(seed=0, device=device, torch_dtype=torch.float32)
+    net = DDPMNetwork.from_config(seed=0, device=device, torch_dtype=dtype)
     net.set_sampling_parameters(1000, batch_size=batch)
     return InverseProblem(op, y, noise), net, shape
 
@@ -309,14 +312,14 @@ class _Heartbeat:
         return False
 
 
-def cpu_baseline(image: int, seconds: float, config: str = "inpaint") -> dict:
+def cpu_baseline(image: int, seconds: float, config: str = "inpaint", dtype=torch.float32) -> dict:
     """oracle/dps_loop.py (dps.py:91-122 semantics) on the host cores with the same UNet and
     workload per sample (the config's operator: 50 % random mask, 9x9 / sigma 3 blur or identity).  The thread count is probed first at batch 1 (the CPU share this
     process is given — OMP_NUM_THREADS / the cgroup quota — and multiples of it up to every
     core the process may run on), then batch 1 and batch 8 are timed on the best count for
     about `seconds` / 2 each; the best per-sample rate is reported."""
     with _Heartbeat("cpu baseline"):
-        return _cpu_baseline(image, seconds, config)
+        return _cpu_baseline(image, seconds, config, dtype)
 
 
 def _cpu_apply_op(config: str, shape: tuple):
@@ -335,7 +338,7 @@ def _cpu_apply_op(config: str, shape: tuple):
     return (lambda v: v.reshape(v.shape[0], -1)[:, kept]), "50% random mask"
 
 
-def _cpu_baseline(image: int, seconds: float, config: str = "inpaint") -> dict:
+def _cpu_baseline(image: int, seconds: float, config: str = "inpaint", dtype=torch.float32) -> dict:
     from oracle import dps_loop
     from samplers_amd.networks.unet2d import build_unet
 
@@ -343,7 +346,8 @@ def _cpu_baseline(image: int, seconds: float, config: str = "inpaint") -> dict:
     share, cores = host["cpu_share"], host["affinity_cores"]
     candidates = sorted({min(cores, share * k) for k in (1, 2, 4)})
     shape = (3, image, image)
-    unet = build_unet(seed=0)
+    unet = build_unet(seed=0).to(dtype)  # bf16: the same UNet's CPU copy behind the fp32 loop
+    eps = (lambda v, t: unet(v, t)) if dtype == torch.float32 else (lambda v, t: unet(v.to(dtype), t).float())
     apply_op, op_desc = _cpu_apply_op(config, shape)
     betas = torch.linspace(1e-4, 0.02, 1000, dtype=torch.float32)
     acp = torch.cat([torch.ones(1), torch.cumprod(1 - betas, 0)]).clip(1e-6, 1)
@@ -358,11 +362,11 @@ def _cpu_baseline(image: int, seconds: float, config: str = "inpaint") -> dict:
         x = torch.randn((batch, *shape), generator=gen)
         noise = lambda i: torch.randn((batch, *shape), generator=gen)  # noqa: E731
         # one warm-up iteration, then as many as fit in the budget (at least 1)
-        x = dps_loop.dps_reference(lambda v, t: unet(v, t), acp, ts, apply_op, lp, y, x, noise,
+        x = dps_loop.dps_reference(eps, acp, ts, apply_op, lp, y, x, noise,
                                    gamma=1.0, eta=1.0, steps_limit=1, return_sample=True)
         done, t0 = 0, time.perf_counter()
         while done < 1 or time.perf_counter() - t0 < budget:
-            x = dps_loop.dps_reference(lambda v, t: unet(v, t), acp, ts, apply_op, lp, y, x,
+            x = dps_loop.dps_reference(eps, acp, ts, apply_op, lp, y, x,
                                        noise, gamma=1.0, eta=1.0, steps_limit=1,
                                        return_sample=True)
             done += 1
@@ -389,7 +393,8 @@ def _cpu_baseline(image: int, seconds: float, config: str = "inpaint") -> dict:
         "sweep": sweep,
         "sample": f"batch {' and '.join(str(p['batch']) for p in sweep)} on the best of {candidates} threads (probed at batch 1): "
                   f"guided DPS iterations (t=999) of oracle/dps_loop.py at 3x{image}x{image}, "
-                  f"{op_desc}, same random-init UNet, fp32, torch-CPU {torch.__version__}; "
+                  f"{op_desc}, same random-init UNet, "
+                  f"{'bf16 UNet behind the fp32 loop' if dtype == torch.bfloat16 else 'fp32'}, torch-CPU {torch.__version__}; "
                   f"best = batch {best['batch']} on {best['threads']} threads, "
                   f"{best['iterations']} iterations",
     }
@@ -408,12 +413,16 @@ def main():
     from samplers_amd.samplers.dps import FusedDPSStep, KernelTimer
 
     _hip.load_library()
-    problem, net, shape = build_workload(args.config, args.batch, args.image, rank, device)
+    bf = args.dtype == "bf16"
+    problem, net, shape = build_workload(args.config, args.batch, args.image, rank, device,
+                                         torch.bfloat16 if bf else torch.float32)
     n = int(np.prod(shape))
     m = int(problem.operator.hip_descriptor().m)
     index_bytes = 12 * ((n + 63) // 64) if args.config == "inpaint" else 0
     timer = KernelTimer()
-    step = FusedDPSStep(net, problem, problem.observation, 1, gamma=1.0, eta=1.0,
+    from samplers_amd.networks.base import fp32_view
+
+    step = FusedDPSStep(fp32_view(net), problem, problem.observation, 1, gamma=1.0, eta=1.0,
                         micro_batch=args.micro_batch or None, timer=timer, reuse_v=args.reuse_v)
     from samplers_amd.samplers.dps import initial_sample
 
@@ -506,17 +515,19 @@ def main():
         guidance_roofline["minimal_bytes_per_launch"] = min_bytes
         guidance_roofline["frac_minimal"] = round(min_bytes / rl[g_dom]["avg_ms"] / 1e6
                                                   / HBM_PEAK_GBS, 4)
-    conv = conv_summary(kern)
+    conv = conv_summary(kern, ("conv3x3_bf16",)) if bf else conv_summary(kern)
+    peak = MFMA_BF16_PEAK_TFLOPS if bf else MFMA_F32_PEAK_TFLOPS
     if conv and conv["ms"] > sum(rl[k]["avg_ms"] * kern[k]["count"] for k in rl):
-        # the prior's fp32-MFMA convolution tile dominates the step
-        c_rec = pmc.get(f"conv3x3_tiles@B{args.batch}_{args.image}{tag}")
+        # the prior's MFMA convolution tile dominates the step
+        c_rec = None if bf else pmc.get(f"conv3x3_tiles@B{args.batch}_{args.image}{tag}")
         roofline = {
             "kernel": "3x3 conv tiles (" + " + ".join(conv["kernels"]) + ")", "bound": "mfma",
-            "achieved": round(conv["tflops"], 2), "peak": MFMA_F32_PEAK_TFLOPS, "unit": "TFLOP/s",
-            "frac": round(conv["tflops"] / MFMA_F32_PEAK_TFLOPS, 4),
+            "achieved": round(conv["tflops"], 2), "peak": peak, "unit": "TFLOP/s",
+            "frac": round(conv["tflops"] / peak, 4),
             "traffic": c_rec["hbm_bytes_per_launch"] if c_rec else None,
             "algorithmic_flops_per_launch": conv["flops"] / conv["count"],
-            "flops_basis": "executed MFMA FLOPs (Winograd: 8*N*Cin*Cout*H*W, direct: 18*...)",
+            "flops_basis": ("bf16 implicit GEMM: 18*N*Cin*Cout*H*W per launch, dense bf16 MFMA peak" if bf else
+                            "executed MFMA FLOPs (Winograd: 8*N*Cin*Cout*H*W, direct: 18*...)"),
             "effective_tflops": round(conv["effective_tflops"], 2),
             "avg_launch_ms": round(conv["ms"] / conv["count"], 4),
             "launches_per_step": conv["count"] / kern_steps,
@@ -538,13 +549,17 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "f32",
-        "arithmetic": {
+        "dtype": "bf16" if bf else "f32",
+        "arithmetic": ({
+            "guidance, bridge update, sample": "fp32",
+            "prior (UNet forward + input VJP)": "bf16 activations / weights on the bf16 NHWC kernels (conv, "
+                                                "GroupNorm, attention), fp32 accumulation and statistics"}
+            if bf else {
             "guidance, GroupNorm, 3x3 convs (Winograd / direct / stride-2), attention": "fp32 (fp32 MFMA, fp32 VALU)",
             "1x1 shortcuts, attention / transformer linears":
                 "fp32 operands on bf16 MFMAs: exact three-term splits, six partial products, fp32 "
                 "accumulation (relative L2 error 1.1e-7 vs fp64, hipBLASLt fp32 2.0e-7; "
-                "SAMPLERS_AMD_SHORTCUT=torch / SAMPLERS_AMD_LINEAR=torch select hipBLASLt fp32)"},
+                "SAMPLERS_AMD_SHORTCUT=torch / SAMPLERS_AMD_LINEAR=torch select hipBLASLt fp32)"}),
         "data": "synthetic (seeded U(-1,1) images, sigma=0.05 Gaussian noise; "
                 "random-init ddpm-celebahq-256 UNet architecture)",
         "config": {"workload": f"{CONFIGS[args.config]}, 3x{args.image}x{args.image}, "
@@ -570,7 +585,8 @@ def main():
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         log("timing the CPU baseline ...")
-        result["cpu_baseline"] = cpu_baseline(args.image, args.cpu_seconds, args.config)
+        result["cpu_baseline"] = cpu_baseline(args.image, args.cpu_seconds, args.config,
+                                              torch.bfloat16 if bf else torch.float32)
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:
