@@ -31,7 +31,7 @@ def main():
     p.add_argument("--steps", type=int, default=1000)
     p.add_argument("--image", type=int, default=256)
     p.add_argument("--config", choices=("identity", "inpaint", "blur"), default="identity")
-    p.add_argument("--modes", default="default,eager", help="default (graph=None) and / or eager")
+    p.add_argument("--modes", default="default,eager", help="default (graph=None), eager and / or graph (forced replay)")
     p.add_argument("--warm-steps", type=int, default=0, help="steps of the untimed call (0: --steps)")
     args = p.parse_args()
     # a long call (configs[1]: ~5 min) prints nothing until it ends: report progress every 30 s
@@ -64,7 +64,7 @@ def main():
     rec = {"workload": f"DPS + {args.config} + GaussianNoise(0.05), 3x{args.image}², batch {args.batch}, "
                        f"{args.steps}-step schedule ({args.steps - 2} guided iterations), "
                        "ddpm-celebahq-256 architecture (random init)"}
-    modes = {"default": {}, "eager": {"graph": False}}
+    modes = {"default": {}, "eager": {"graph": False}, "graph": {"graph": True}}
     for label in args.modes.split(","):
         kw = modes[label]
         sampler(prob, num_sampling_steps=args.warm_steps or args.steps, seed=1, **kw)  # warm
