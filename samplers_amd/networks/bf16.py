@@ -310,9 +310,11 @@ def _gn_fwd_raw(norm: nn.GroupNorm, x1: Tensor, x2: Tensor | None, cb: Tensor | 
 
 def _gn_bwd_raw(norm: nn.GroupNorm, dz: Tensor, x1: Tensor, x2: Tensor | None, cb: Tensor | None, stats: Tensor,
                 add1: Tensor | None = None, add2: Tensor | None = None, out1: Tensor | None = None,
-                out2: Tensor | None = None, blocked: bool = False) -> tuple[Tensor, Tensor | None]:
+                out2: Tensor | None = None, blocked: bool = False,
+                add1b: Tensor | None = None) -> tuple[Tensor, Tensor | None]:
     """Input VJP of ``_gn_fwd_raw`` into the parts' layouts, + the addends (channels-last, shaped
     like the parts) added in the kernel; ``out1`` / ``out2`` may be the addends (in place);
+    ``add1b``: a second addend of dx1 (a skip tensor's up-block gradient, layers.SkipGrad);
     ``blocked`` (one part): dx1 as a flat channel-blocked buffer for the next conv VJP."""
     lib = _hip.load_library()
     n, c1, h, w = x1.shape
@@ -329,7 +331,7 @@ def _gn_bwd_raw(norm: nn.GroupNorm, dz: Tensor, x1: Tensor, x2: Tensor | None, c
                                             None if gamma is None else gamma.data_ptr(),
                                             None if beta is None else beta.data_ptr(), stats.data_ptr(), n, h * w,
                                             norm.num_groups, int(norm.act), _p(dx1, cl=not blocked), _p(dx2),
-                                            int(blocked), _p(add1), _p(add2), None, ws.data_ptr(), nb,
+                                            int(blocked), _p(add1), _p(add2), _p(add1b), ws.data_ptr(), nb,
                                             _hip.stream_of(dz)), "sp_groupnorm_bf16_bwd_ex")
     return dx1, dx2
 
@@ -511,10 +513,13 @@ class _ResnetBlockBf16Fn(torch.autograd.Function):
                                          over cat(x1, x2) is two GEMMs over the parts' rows (no cat)
     bwd  dx = GN1^T(conv1^T(GN2^T(conv2^T dout))) + shortcut^T dout, the shortcut's gradient
          added by GN1's VJP kernel into the parts' gradients (no autograd accumulation add).
+    Skip tensors (layers.SkipGrad, as unet2d._ResnetBlockFn): ``box_out`` receives dx2 (the
+    up-block's gradient of its skip part) instead of autograd; ``box_in`` (x1 is a skip tensor)
+    delivers that gradient, added by GN1's VJP kernel (its add1b) — no accumulation add.
     Saves x1, x2, h1 and the GroupNorm statistics (weights are frozen: no z1 / z2)."""
 
     @staticmethod
-    def forward(ctx, block, tb, x1, x2):
+    def forward(ctx, block, tb, x1, x2, box_in=None, box_out=None):
         cout = block.conv2.weight.shape[0]
         n, c1, hh, ww = x1.shape
         cin = c1 + (0 if x2 is None else x2.shape[1])
@@ -539,6 +544,7 @@ class _ResnetBlockBf16Fn(torch.autograd.Function):
         out = _conv_launch(z2, conv_pack(block.conv2, False), _bias_f32(block.conv2, block.conv2.bias), short, cout,
                            shape=(n, cout, hh, ww) if b2 else None)
         ctx.block = block
+        ctx.box_in, ctx.box_out = box_in, box_out
         ctx.save_for_backward(x1, x2, h1, tb, st1, st2)
         return out
 
@@ -561,8 +567,11 @@ class _ResnetBlockBf16Fn(torch.autograd.Function):
         else:
             dz1 = _conv_launch(_pad_channels(dh1, _ceil(cmid, 16)), conv_pack(blk.conv1, True), None, None, cin)
         del dh1
-        if blk.conv_shortcut is None:  # identity shortcut: dx1 = GN1^T dz1 + dout
-            dx1, dx2 = _gn_bwd_raw(blk.norm1, dz1, x1, x2, None, st1, add1=dout)
+        extra = ctx.box_in.take() if ctx.box_in is not None else None
+        if extra is not None:
+            extra = nhwc(extra.to(BF16))
+        if blk.conv_shortcut is None:  # identity shortcut: dx1 = GN1^T dz1 + dout (+ skip grad)
+            dx1, dx2 = _gn_bwd_raw(blk.norm1, dz1, x1, x2, None, st1, add1=dout, add1b=extra)
         else:  # s = shortcut^T dout per part (pixel rows), then += GN1^T dz1 in place
             c1 = x1.shape[1]
             w1, w2 = _shortcut_w(blk, c1)
@@ -570,8 +579,11 @@ class _ResnetBlockBf16Fn(torch.autograd.Function):
             d = _rows(dout)
             s1 = (d @ w1).reshape(n, h, w, c1).permute(0, 3, 1, 2)
             s2 = None if x2 is None else (d @ w2).reshape(n, h, w, x2.shape[1]).permute(0, 3, 1, 2)
-            dx1, dx2 = _gn_bwd_raw(blk.norm1, dz1, x1, x2, None, st1, add1=s1, add2=s2, out1=s1, out2=s2)
-        return None, None, dx1, dx2
+            dx1, dx2 = _gn_bwd_raw(blk.norm1, dz1, x1, x2, None, st1, add1=s1, add2=s2, out1=s1, out2=s2,
+                                   add1b=extra)
+        if ctx.box_out is not None:  # x2 (a skip): its down-path consumer adds this gradient
+            ctx.box_out.grad, dx2 = dx2, None
+        return None, None, dx1, dx2, None, None
 
 
 def resnet_block_supported(block: nn.Module, x: Tensor, skip: Tensor | None) -> bool:
@@ -599,11 +611,14 @@ def resnet_block_supported(block: nn.Module, x: Tensor, skip: Tensor | None) -> 
                 and lib.sp_conv3x3_bf16_supported(cin, cout, h, w) and lib.sp_conv3x3_bf16_supported(cout, cout, h, w))
 
 
-def resnet_block(block: nn.Module, x: Tensor, skip: Tensor | None, tb: Tensor | None) -> Tensor:
+def resnet_block(block: nn.Module, x: Tensor, skip: Tensor | None, tb: Tensor | None, box_in=None,
+                 box_out=None) -> Tensor:
     """``block(x, temb, skip)`` at bf16 as ``_ResnetBlockBf16Fn`` (``tb``: the block's
-    time-embedding projection, [n, cout], or None)."""
+    time-embedding projection, [n, cout], or None; ``box_in`` / ``box_out``: enabled SkipGrad
+    mailboxes of x / skip, or None)."""
     cb = None if tb is None else tb.detach().to(torch.float32).reshape(x.shape[0], -1).contiguous()
-    return _ResnetBlockBf16Fn.apply(block, cb, nhwc(x), None if skip is None else nhwc(skip))
+    return _ResnetBlockBf16Fn.apply(block, cb, nhwc(x), None if skip is None else nhwc(skip), box_in,
+                                    None if skip is None else box_out)
 
 
 # ---------------------------------------------------------------------------------------------

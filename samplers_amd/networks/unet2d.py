@@ -361,15 +361,18 @@ class ResnetBlock2D(nn.Module):
         """The block at bf16 on the NHWC kernels (networks/bf16.py): GN1 over cat(x, skip) read in
         place, conv1, GN2 with the time-embedding bias, conv2 with the shortcut added in its
         epilogue — as one autograd function (``bf16.resnet_block``) where the kernels serve the
-        shapes, module by module otherwise; autograd sums the skip gradients (the SkipGrad
-        hand-offs are fp32-only)."""
+        shapes, module by module otherwise.  Skip gradients: handed over through the SkipGrad
+        mailboxes where both consumers are fused blocks (added in GN1's VJP kernel), else
+        summed by autograd (the box disabled in the forward pass)."""
         from . import bf16
 
+        if bf16.resnet_block_supported(self, x, skip):
+            box_in = box_in if box_in is not None and box_in.enabled else None
+            box_out = box_out if box_out is not None and box_out.enabled and skip is not None else None
+            return bf16.resnet_block(self, x, skip, tb, box_in, box_out)
         for box in (box_in, box_out):
             if box is not None:
                 box.enabled = False
-        if bf16.resnet_block_supported(self, x, skip):
-            return bf16.resnet_block(self, x, skip, tb)
         c2 = 0 if skip is None else skip.shape[1]
         if bf16.group_norm_supported(self.norm1, x, c2):
             z1 = bf16.group_norm(self.norm1, x, skip)
@@ -738,7 +741,10 @@ class UNet2DModel(nn.Module):
         # every skip tensor has two consumers (the next down-path layer and an up-block
         # resnet); with grad on the device their gradients meet inside the down-path
         # consumer's VJP kernel (SkipGrad) instead of an autograd accumulation add
-        mail = torch.is_grad_enabled() and sample.is_cuda
+        # (SAMPLERS_AMD_SKIPGRAD=0: autograd sums them, for A/B measurements and tests)
+        import os
+
+        mail = torch.is_grad_enabled() and sample.is_cuda and os.environ.get("SAMPLERS_AMD_SKIPGRAD", "1") != "0"
         new_box = (lambda: SkipGrad()) if mail else (lambda: None)  # noqa: E731
         h = self.conv_in(sample)
         skips, boxes = [h], [new_box()]

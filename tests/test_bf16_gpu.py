@@ -496,6 +496,39 @@ def test_celebahq_unet_bf16_fwd_vjp(cuda, parity_record):
             parity_record, 1e-1)
 
 
+def test_celebahq_unet_bf16_skip_grad_handoff(cuda, monkeypatch, parity_record):
+    """The bf16 UNet's skip-tensor gradients handed from the up-block to the down-path ResnetBlock's
+    GroupNorm VJP kernel (layers.SkipGrad) equal autograd's accumulation adds within one bf16
+    rounding of the summed gradient, with fewer full-size add kernels in the step."""
+    from torch.profiler import ProfilerActivity, profile
+
+    from samplers_amd.networks.unet2d import build_unet
+
+    gpu = build_unet(seed=0).to(cuda, BF).requires_grad_(False)
+    gen = torch.Generator().manual_seed(9)
+    x = torch.randn(2, 3, 256, 256, generator=gen).to(cuda, BF)
+    cot = torch.randn(2, 3, 256, 256, generator=gen).to(cuda, BF)
+
+    def run():
+        xr = x.clone().requires_grad_(True)
+        with profile(activities=[ProfilerActivity.CUDA]) as prof:
+            with torch.enable_grad():
+                out = gpu(xr, 500)
+            (g,) = torch.autograd.grad(out, xr, cot)
+            torch.cuda.synchronize()
+        adds = sum("CUDAFunctor_add" in e.name for e in prof.events() if e.device_type.name == "CUDA")
+        return out.float().cpu(), g.float().cpu(), adds
+
+    oa, ga, adds_box = run()
+    monkeypatch.setenv("SAMPLERS_AMD_SKIPGRAD", "0")
+    ob, gb, adds_autograd = run()
+    assert torch.equal(oa, ob)
+    e = _rel(ga, gb)
+    parity_record("celebahq_unet_bf16_skipgrad_vs_autograd_vjp", e, 1e-2)
+    assert e < 1e-2, e
+    assert adds_box + 10 <= adds_autograd, (adds_box, adds_autograd)
+
+
 def test_psld_bf16_sd15_matches_oracle(cuda, parity_record):
     """PSLDSampler with LatentDiffusionNetwork.from_config(torch_dtype=bf16): 3 guided iterations +
     the final decode at 3x256², B = 2, centre inpainting, vs oracle/latent_loops.py with the same
