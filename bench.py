@@ -526,7 +526,7 @@ def main():
             "frac": round(conv["tflops"] / peak, 4),
             "traffic": c_rec["hbm_bytes_per_launch"] if c_rec else None,
             "algorithmic_flops_per_launch": conv["flops"] / conv["count"],
-            "flops_basis": ("bf16 implicit GEMM: 18*N*Cin*Cout*H*W per launch, dense bf16 MFMA peak" if bf else
+            "flops_basis": ("bf16 implicit GEMM: 18*N*Cin*Cout*H*W (+ 2*N*Cs*Cout*H*W where a 1x1 shortcut is fused) per launch, dense bf16 MFMA peak" if bf else
                             "executed MFMA FLOPs (Winograd: 8*N*Cin*Cout*H*W, direct: 18*...)"),
             "effective_tflops": round(conv["effective_tflops"], 2),
             "avg_launch_ms": round(conv["ms"] / conv["count"], 4),

@@ -631,6 +631,18 @@ int sp_conv3x3_bf16_blk_supported(int32_t cin, int32_t cout, int32_t h, int32_t 
 int sp_conv3x3_bf16_ex(const void* x, int32_t in_layout, const void* wp, const float* bias, const void* res, int64_t n,
                        int32_t cin, int32_t cout, int32_t h, int32_t w, void* y, void* ws, int64_t ws_bytes,
                        sp_stream_t stream);
+/* y = conv3x3(x) + conv1x1(cat(xs1, xs2)) + bias: a ResnetBlock's conv2 with its conv_shortcut
+ * summed as (cs1 + cs2) / 16 further stages of the same contraction (no shortcut tensor, no
+ * residual read).  wsp: [ceil(cout/64)][cs/16][64 co][16 ci] bf16 (rows past cout zero,
+ * sp_conv3x3_bf16_sc_packed_size elements); bias: conv2's + the shortcut's; x in in_layout as
+ * sp_conv3x3_bf16_ex; xs1 / xs2 NHWC.  Replaces the shortcut GEMM + residual epilogue of
+ * diffusers' ResnetBlock2D (reference: samplers/networks/diffusers/ddpm.py:40-43 prior call). */
+int sp_conv3x3_bf16_sc_supported(int32_t cin, int32_t cout, int32_t cs1, int32_t cs2, int32_t h, int32_t w);
+int64_t sp_conv3x3_bf16_sc_packed_size(int32_t cs, int32_t cout);
+int64_t sp_conv3x3_bf16_sc_workspace(int64_t n, int32_t cin, int32_t cs, int32_t cout, int32_t h, int32_t w);
+int sp_conv3x3_bf16_sc(const void* x, int32_t in_layout, const void* wp, const float* bias, const void* xs1,
+                       const void* xs2, int32_t cs1, int32_t cs2, const void* wsp, int64_t n, int32_t cin,
+                       int32_t cout, int32_t h, int32_t w, void* y, void* ws, int64_t ws_bytes, sp_stream_t stream);
 int sp_attention_bf16_supported(int64_t batch, int32_t heads, int64_t n, int64_t m, int32_t d);
 /* multi-head softmax(q k^T scale) v on bf16 token rows (self: m = n; cross: kv_shared = 1 for
  * one context row for the whole batch); lse [batch heads][n] fp32 for the VJP. */

@@ -93,6 +93,15 @@ __device__ __forceinline__ float silu_f(float y) { return y * __builtin_amdgcn_r
 // pixel), 9 taps x 8 MFMAs per wave per stage; the next stage's global loads are issued into
 // registers before the current stage's MFMAs.
 // ---------------------------------------------------------------------------------------------
+// threadIdx.x re-read opaque to the compiler: the shortcut stages' per-thread addresses are then
+// formed inside their loop instead of being hoisted ahead of the 3x3 loop (where they were live
+// across it: the kernel spilled ~200 VGPRs)
+__device__ __forceinline__ int cv_tid() {
+    int t = threadIdx.x;
+    asm volatile("" : "+v"(t));
+    return t;
+}
+
 template <int TC>
 struct CvGeo {
     static_assert(TC == 32 || TC == 16 || TC == 8 || TC == 4, "tile width");
@@ -130,11 +139,19 @@ __device__ __forceinline__ int cv_chunk(int p) { return p & 1; }
 // without the upsampled tensor in HBM.
 // part != NULL (split-K, gridDim.z parts over the input-channel stages): part z of the
 // contraction is stored as fp32 to part[z][n h w][cout] without bias / residual (k_conv_reduce).
-template <int TC, bool UP, bool BLK = false>
+// SC (TC = 32): a 1x1 convolution of cat(xs1, xs2) (cs1 + cs2 channels, NHWC, the ResnetBlock's
+// conv_shortcut) is summed into the same accumulators as (cs1 + cs2) / 16 further stages of the
+// contraction — weights wsp [co block of 64][cs / 16][64 co][16 ci], the stage's 512 pixels
+// written to the patch centre and read by the centre tap only (8 MFMAs per wave) — so the
+// shortcut's output is never written to HBM nor read back as a residual.
+template <int TC, bool UP, bool BLK = false, bool SC = false>
 __global__ __launch_bounds__(kBlock, TC == 4 ? 1 : 2) void k_conv3x3_bf16(const u16* __restrict__ x, const u16* __restrict__ wp,
                                                          const float* __restrict__ bias, const u16* __restrict__ res,
                                                          int n, int cin, int cout, int h, int w,
-                                                         u16* __restrict__ y, float* __restrict__ part) {
+                                                         u16* __restrict__ y, float* __restrict__ part,
+                                                         const u16* __restrict__ xs1, const u16* __restrict__ xs2,
+                                                         int cs1, int cs2, const u16* __restrict__ wsp) {
+    static_assert(!SC || (TC == 32 && !UP), "shortcut stages: TC = 32 tiles");
     using G = CvGeo<TC>;
     __shared__ __attribute__((aligned(16))) char lds[G::LDS];
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, r = lane & 31, hh = lane >> 5;
@@ -159,7 +176,7 @@ __global__ __launch_bounds__(kBlock, TC == 4 ? 1 : 2) void k_conv3x3_bf16(const 
     } else {
         c0 = 0, h0 = 0, n0 = pt * G::S;
     }
-    const int nci = cin >> 4;
+    const int nci = cin >> 4, nsc = SC ? (cs1 + cs2) >> 4 : 0;
     const bq_u4* __restrict__ wsrc = reinterpret_cast<const bq_u4*>(wp + (int64_t)cb * nci * (9 * 64 * 16));
 
     // per-thread patch pieces: global element offset (channel 0 of the stage) or -1 (halo / past the batch)
@@ -185,6 +202,21 @@ __global__ __launch_bounds__(kBlock, TC == 4 ? 1 : 2) void k_conv3x3_bf16(const 
     }
     bq_u4 sw[G::NW], spx[G::NP];
     const int64_t kstride = BLK ? (int64_t)h * w * 16 : 16;  // elements between stages' pieces
+    // shortcut stage k1: the 64 x 16 weights (threads < 128, one piece each) and the tile's 512
+    // pixels x 16 channels of cat(xs1, xs2) (4 pieces per thread; TC = 32 tiles lie inside the image)
+    auto gload_sc = [&](int k1) {
+        const int tid = cv_tid();
+        if (tid < 128) sw[0] = reinterpret_cast<const bq_u4*>(wsp)[((int64_t)cb * nsc + k1) * 128 + tid];
+        // piece k of thread tid: pixel (tid / 2) + 128 k = row (tid / 64) + 4 k, column (tid / 2) % 32
+        const bool first = k1 * 16 < cs1;
+        const int64_t cstr = first ? cs1 : cs2;
+        const int q0 = tid >> 1;
+        const u16* __restrict__ src = (first ? xs1 + k1 * 16 : xs2 + (k1 * 16 - cs1)) + (tid & 1) * 8 +
+                                      (((int64_t)n0 * h + h0 + (q0 >> 5)) * w + c0 + (q0 & 31)) * cstr;
+        const int64_t kstep = 4 * (int64_t)w * cstr;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) spx[k] = *reinterpret_cast<const bq_u4*>(src + k * kstep);
+    };
     auto gload = [&](int ks) {
         const bq_u4* __restrict__ ws = wsrc + (int64_t)ks * (9 * 64 * 2);
 #pragma unroll
@@ -228,8 +260,8 @@ __global__ __launch_bounds__(kBlock, TC == 4 ? 1 : 2) void k_conv3x3_bf16(const 
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[a][j] = bq_f16{};
 
-    const int kz = blockIdx.z, nz = gridDim.z;
-    const int ks0 = kz * nci / nz, ks1 = (kz + 1) * nci / nz;
+    const int kz = blockIdx.z, nz = gridDim.z, ntot = nci + nsc;
+    const int ks0 = kz * ntot / nz, ks1 = (kz + 1) * ntot / nz;
     if constexpr (G::DB) {
         // Two stage buffers, one barrier per stage: stage s + 1 (in registers since stage s - 1)
         // is written to the other buffer and stage s + 2's global loads are issued before stage
@@ -237,6 +269,19 @@ __global__ __launch_bounds__(kBlock, TC == 4 ? 1 : 2) void k_conv3x3_bf16(const 
         // Swizzle: weight row wr keeps its 16-byte half c at (c ^ (wr >> 3 & 1)); patch pixel q
         // (column q % PW) at (c ^ (q % PW >> 3 & 1)) — the 16-lane groups of a ds_read_b128 then
         // read 16 distinct 16-byte slots of the 256-byte bank row for any column offset.
+        auto lstore_sc = [&](int b) {  // the shortcut stage: weights as tap 0, pixels at the patch centre
+            const int tid = cv_tid();
+            char* __restrict__ base = lds + b * G::BUF;
+            if (tid < 128) {
+                const int wr = tid >> 1;
+                *reinterpret_cast<bq_u4*>(base + wr * 32 + (((tid & 1) ^ ((wr >> 3) & 1)) << 4)) = sw[0];
+            }
+            const int q0 = tid >> 1, pcol = (q0 & 31) + 1;
+            char* __restrict__ pp = base + G::LW + (((q0 >> 5) + 1) * G::PW + pcol) * 32 +
+                                    (((tid & 1) ^ ((pcol >> 3) & 1)) << 4);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) *reinterpret_cast<bq_u4*>(pp + k * 4 * G::PW * 32) = spx[k];
+        };
         auto lstore_db = [&](int b) {
             char* __restrict__ base = lds + b * G::BUF;
 #pragma unroll
@@ -310,23 +355,50 @@ __global__ __launch_bounds__(kBlock, TC == 4 ? 1 : 2) void k_conv3x3_bf16(const 
                 __builtin_amdgcn_sched_barrier(0);
             }
         };
-        const int nst = ks1 - ks0;
-        gload(ks0);
-        lstore_db(0);
-        if (nst > 1) gload(ks0 + 1);
-        __syncthreads();
-        for (int s = 0; s < nst; ++s) {
-            const int b = s & 1;
-            if (s + 1 < nst) lstore_db(b ^ 1);
-#if BQ_EXP == 9  // diagnostics (wrong results): no global loads after the prologue's two stages
-            (void)b;
-#else
-            if (s + 2 < nst) gload(ks0 + s + 2);
-#endif
-            __builtin_amdgcn_sched_barrier(0);
-            compute(b);
+        // the shortcut stage's centre-tap MFMAs (fragments as compute's tap (1, 1))
+        auto compute_sc = [&](int b) {
+            const int t = cv_tid(), ln = t & 63, rr = ln & 31, h2 = ln >> 5, wq = t >> 6;
+            const char* __restrict__ base = lds + b * G::BUF;
+            const int wl = rr * 32 + ((h2 ^ ((rr >> 3) & 1)) << 4);
+            const int bl = G::LW + (4 * wq * G::PW + rr + 1) * 32 + ((h2 ^ (((rr + 1) >> 3) & 1)) << 4);
+            const bq_u4 a0 = *reinterpret_cast<const bq_u4*>(base + wl);
+            const bq_u4 a1 = *reinterpret_cast<const bq_u4*>(base + wl + 32 * 32);
+            bq_u4 f[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) f[j] = *reinterpret_cast<const bq_u4*>(base + bl + (j + 1) * G::PW * 32);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                acc[0][j] = bq_mfma(a0, f[j], acc[0][j]);
+                acc[1][j] = bq_mfma(a1, f[j], acc[1][j]);
+            }
+        };
+        // stages kb .. ke - 1 through the two buffers (gl: global loads of a stage into registers,
+        // st: registers -> LDS buffer, cp: the buffer's MFMAs); the shortcut's stages (part z's
+        // share of stages nci ..) in a loop of their own ahead of the 3x3 stages (one loop over
+        // both kinds, or the shortcut's loop second, spilled ~200 VGPRs)
+        auto pipeline = [&](int kb, int ke, auto&& gl, auto&& st, auto&& cp) {
+            const int nst = ke - kb;
+            if (nst <= 0) return;
+            gl(kb);
+            st(0);
+            if (nst > 1) gl(kb + 1);
             __syncthreads();
-        }
+            for (int s = 0; s < nst; ++s) {
+                const int b = s & 1;
+                if (s + 1 < nst) st(b ^ 1);
+#if BQ_EXP == 9  // diagnostics (wrong results): no global loads after the prologue's two stages
+                (void)b;
+#else
+                if (s + 2 < nst) gl(kb + s + 2);
+#endif
+                __builtin_amdgcn_sched_barrier(0);
+                cp(b);
+                __syncthreads();
+            }
+        };
+        if constexpr (SC)
+            pipeline(ks0 > nci ? ks0 - nci : 0, ks1 - nci, gload_sc, lstore_sc, compute_sc);
+        pipeline(ks0, ks1 < nci ? ks1 : nci, gload, lstore_db, compute);
     } else {
         gload(ks0);
         for (int ks = ks0; ks < ks1; ++ks) {
@@ -471,16 +543,27 @@ static int conv_parts(int n, int cin, int cout, int h, int w) {
     return parts;
 }
 
-template <int TC, bool UP, bool BLK = false>
+// the shortcut operands of an SC launch (wsp == nullptr: none)
+struct ConvSc {
+    const u16* xs1 = nullptr;
+    const u16* xs2 = nullptr;
+    int cs1 = 0, cs2 = 0;
+    const u16* wsp = nullptr;
+};
+
+template <int TC, bool UP, bool BLK = false, bool SC = false>
 static void conv_bf16_launch(const u16* x, const u16* wp, const float* bias, const u16* res, int n, int cin,
-                             int cout, int h, int w, u16* y, hipStream_t s, float* part = nullptr, int parts = 1) {
+                             int cout, int h, int w, u16* y, hipStream_t s, float* part = nullptr, int parts = 1,
+                             const ConvSc& sc = ConvSc{}) {
     using G = CvGeo<TC>;
     (void)sizeof(G);
     const int cbn = (cout + 63) / 64;
     const int64_t tiles = conv_tiles<TC>(n, h, w);
-    const double flops = 18.0 * n * (double)h * w * cin * cout;
-    launch_w(TK_CONV_BF16, flops, k_conv3x3_bf16<TC, UP, BLK>, dim3(cbn, static_cast<unsigned>(tiles), parts), dim3(kBlock),
-             s, x, wp, bias, res, n, cin, cout, h, w, y, parts > 1 ? part : nullptr);
+    // (+ the shortcut stages' 1x1 contraction)
+    const double flops = 18.0 * n * (double)h * w * cin * cout + 2.0 * n * (double)h * w * (sc.cs1 + sc.cs2) * cout;
+    launch_w(TK_CONV_BF16, flops, k_conv3x3_bf16<TC, UP, BLK, SC>, dim3(cbn, static_cast<unsigned>(tiles), parts),
+             dim3(kBlock), s, x, wp, bias, res, n, cin, cout, h, w, y, parts > 1 ? part : nullptr, sc.xs1, sc.xs2,
+             sc.cs1, sc.cs2, sc.wsp);
     if (parts > 1) {
         const int64_t total = (int64_t)n * h * w * cout;
         launch(0, k_conv_reduce, dim3(stream_blocks(total / 8)), dim3(kBlock), s, static_cast<const float*>(part),
@@ -1552,9 +1635,13 @@ int64_t sp_conv3x3_bf16_packed_size(int32_t cin, int32_t cout) {
 // zero); the input VJP is the same call with the pack of W'[ci][co][2-ky][2-kx].
 static int conv_bf16_call(const void* x, const void* wp, const float* bias, const void* res, int64_t n, int32_t cin,
                           int32_t cout, int32_t h, int32_t w, void* y, sp_stream_t stream, bool up,
-                          void* ws = nullptr, int64_t ws_bytes = 0, int blk = 0) {
+                          void* ws = nullptr, int64_t ws_bytes = 0, int blk = 0, const ConvSc& sc = ConvSc{}) {
     if (!x || !wp || !y || n <= 0 || !sp_conv3x3_bf16_supported(cin, cout, h, w)) return SP_EINVAL;
     if (blk && (up || conv_tc(h, w) != 32)) return SP_EINVAL;
+    const int cs = sc.cs1 + sc.cs2;
+    if (sc.wsp && (up || res || conv_tc(h, w) != 32 || !sc.xs1 || sc.cs1 <= 0 || sc.cs1 % 16 || sc.cs2 < 0 ||
+                   sc.cs2 % 16 || (sc.cs2 && !sc.xs2) || n * h * (int64_t)w * cs >= (int64_t(1) << 40)))
+        return SP_EINVAL;
     if (up && (h % 2 || w % 2)) return SP_EINVAL;
     if (n * h * (int64_t)w * std::max(cin, cout) >= (int64_t(1) << 40) || n >= (int64_t(1) << 30)) return SP_EINVAL;
     hipStream_t s = static_cast<hipStream_t>(stream);
@@ -1572,9 +1659,14 @@ static int conv_bf16_call(const void* x, const void* wp, const float* bias, cons
         }
         return check_launch("sp_conv3x3_bf16_up");
     }
-    int parts = conv_parts(ni, cin, cout, h, w);
+    int parts = conv_parts(ni, cin + (sc.wsp ? cs : 0), cout, h, w);
     if (parts > 1 && (!ws || ws_bytes < 4 * parts * (int64_t)ni * h * w * cout)) parts = 1;
     float* part = static_cast<float*>(ws);
+    if (sc.wsp) {
+        if (blk) conv_bf16_launch<32, false, true, true>(xx, ww, bias, rr, ni, cin, cout, h, w, yy, s, part, parts, sc);
+        else conv_bf16_launch<32, false, false, true>(xx, ww, bias, rr, ni, cin, cout, h, w, yy, s, part, parts, sc);
+        return check_launch("sp_conv3x3_bf16_sc");
+    }
     if (blk) {
         conv_bf16_launch<32, false, true>(xx, ww, bias, rr, ni, cin, cout, h, w, yy, s, part, parts);
         return check_launch("sp_conv3x3_bf16_ex");
@@ -1616,6 +1708,35 @@ int sp_conv3x3_bf16_ex(const void* x, int32_t in_layout, const void* wp, const f
                        sp_stream_t stream) {
     if (in_layout != 0 && in_layout != 1) return SP_EINVAL;
     return conv_bf16_call(x, wp, bias, res, n, cin, cout, h, w, y, stream, false, ws, ws_bytes, in_layout);
+}
+
+// y = conv3x3(x) + conv1x1(cat(xs1, xs2)) + bias: the ResnetBlock's conv2 with its conv_shortcut summed
+// as further stages of the same contraction (no shortcut tensor, no residual read).  wsp: the 1x1
+// weights packed as [co block of 64][cs / 16][64 co][16 ci] (sp_conv3x3_bf16_sc_packed_size
+// elements, rows past cout zero); bias: conv2's + the shortcut's.  TC = 32 shapes
+// (sp_conv3x3_bf16_sc_supported); split-K over all stages (sp_conv3x3_bf16_sc_workspace).
+int sp_conv3x3_bf16_sc_supported(int32_t cin, int32_t cout, int32_t cs1, int32_t cs2, int32_t h, int32_t w) {
+    return sp_conv3x3_bf16_supported(cin, cout, h, w) && conv_tc(h, w) == 32 && cs1 > 0 && cs1 % 16 == 0 &&
+           cs2 >= 0 && cs2 % 16 == 0;
+}
+
+int64_t sp_conv3x3_bf16_sc_packed_size(int32_t cs, int32_t cout) { return (int64_t)((cout + 63) / 64) * 64 * cs; }
+
+int64_t sp_conv3x3_bf16_sc_workspace(int64_t n, int32_t cin, int32_t cs, int32_t cout, int32_t h, int32_t w) {
+    if (n <= 0 || n >= (int64_t(1) << 30) || cs < 0 || !sp_conv3x3_bf16_supported(cin, cout, h, w)) return 0;
+    const int parts = conv_parts(static_cast<int>(n), cin + cs, cout, h, w);
+    return parts > 1 ? 4 * parts * n * h * (int64_t)w * cout : 0;
+}
+
+int sp_conv3x3_bf16_sc(const void* x, int32_t in_layout, const void* wp, const float* bias, const void* xs1,
+                       const void* xs2, int32_t cs1, int32_t cs2, const void* wsp, int64_t n, int32_t cin, int32_t cout,
+                       int32_t h, int32_t w, void* y, void* ws, int64_t ws_bytes, sp_stream_t stream) {
+    if ((in_layout != 0 && in_layout != 1) || !wsp || !sp_conv3x3_bf16_sc_supported(cin, cout, cs1, cs2, h, w))
+        return SP_EINVAL;
+    ConvSc sc;
+    sc.xs1 = static_cast<const u16*>(xs1), sc.xs2 = static_cast<const u16*>(xs2);
+    sc.cs1 = cs1, sc.cs2 = cs2, sc.wsp = static_cast<const u16*>(wsp);
+    return conv_bf16_call(x, wp, bias, nullptr, n, cin, cout, h, w, y, stream, false, ws, ws_bytes, in_layout, sc);
 }
 
 int sp_conv3x3_bf16(const void* x, const void* wp, const float* bias, const void* res, int64_t n, int32_t cin,

@@ -141,6 +141,60 @@ def _conv_launch(x: Tensor, pack: Tensor, bias: Tensor | None, res: Tensor | Non
     return y
 
 
+def shortcut_pack(block: nn.Module) -> Tensor:
+    """conv_shortcut's [cout][cs] weights as sp_conv3x3_bf16_sc reads them: [co block of 64][cs / 16]
+    [64 co][16 ci] bf16, rows past cout zero."""
+    w = block.conv_shortcut.weight
+
+    def build():
+        co, cs = w.shape[0], w.shape[1]
+        cop = _ceil(co, 64)
+        wp = torch.zeros(cop, cs, device=w.device, dtype=torch.float32)
+        wp[:co] = w.detach().reshape(co, cs).float()
+        return wp.reshape(cop // 64, 64, cs // 16, 16).permute(0, 2, 1, 3).contiguous().to(BF16)
+
+    return _cached(block.conv_shortcut, "scpack", _wkey(w), build)
+
+
+def _sc_bias(block: nn.Module) -> Tensor | None:
+    """conv2's bias + conv_shortcut's (fp32): the bias of the fused conv2 + shortcut launch."""
+    b2, bs = block.conv2.bias, block.conv_shortcut.bias
+    if b2 is None and bs is None:
+        return None
+    return _cached(block.conv_shortcut, "scbias", _wkey(b2, bs),
+                   lambda: ((b2.detach().float() if b2 is not None else 0) + (bs.detach().float() if bs is not None else 0)).contiguous())
+
+
+def sc_ok(cout: int, c1: int, c2: int, h: int, w: int) -> bool:
+    """Whether conv2 + the 1x1 shortcut run as one sp_conv3x3_bf16_sc launch
+    (``SAMPLERS_AMD_BF16_SC=0``: shortcut GEMMs + residual epilogue, for A/B)."""
+    import os
+
+    from .layers import _query
+
+    return (os.environ.get("SAMPLERS_AMD_BF16_SC", "1") != "0"
+            and bool(_query("sp_conv3x3_bf16_sc_supported", cout, cout, c1, c2, h, w)))
+
+
+def _conv_sc_launch(z: Tensor, pack: Tensor, bias: Tensor | None, x1: Tensor, x2: Tensor | None, wsp: Tensor, cout: int,
+                    shape: tuple | None = None) -> Tensor:
+    """conv3x3(z) + conv1x1(cat(x1, x2)) + bias on sp_conv3x3_bf16_sc (``shape``: z flat channel-blocked)."""
+    from ..runtime import split_k_enabled
+    from .layers import _query
+
+    lib = _hip.load_library()
+    n, cin, h, w = z.shape if shape is None else shape
+    c1, c2 = x1.shape[1], (0 if x2 is None else x2.shape[1])
+    y = torch.empty(n, cout, h, w, device=x1.device, dtype=BF16, memory_format=CL)
+    nb = _query("sp_conv3x3_bf16_sc_workspace", n, cin, c1 + c2, cout, h, w) if split_k_enabled() else 0
+    ws = torch.empty(max(nb // 4, 1), device=x1.device, dtype=torch.float32)
+    _hip.check(lib.sp_conv3x3_bf16_sc(_p(z, cl=shape is None), 0 if shape is None else 1, _p(pack, cl=False),
+                                      None if bias is None else bias.data_ptr(), _p(x1), _p(x2), c1, c2,
+                                      _p(wsp, cl=False), n, cin, cout, h, w, _p(y), ws.data_ptr() if nb else None, nb,
+                                      _hip.stream_of(x1)), "sp_conv3x3_bf16_sc")
+    return y
+
+
 def blocked_ok(cin: int, cout: int, h: int, w: int) -> bool:
     """Whether a conv's input can be handed over channel-blocked ([n][cin/16][h][w][16]: each 16-channel
     stage of the tile then reads whole cache lines instead of 32 bytes of every pixel's row);
@@ -509,8 +563,10 @@ class _ResnetBlockBf16Fn(torch.autograd.Function):
     fwd  z1 = silu(GN1(cat(x1, x2)))   both parts read in place
          h1 = conv1(z1)
          z2 = silu(GN2(h1 + tb))
-         out = conv2(z2) + shortcut(x)   the shortcut added in conv2's epilogue; a 1x1 shortcut
-                                         over cat(x1, x2) is two GEMMs over the parts' rows (no cat)
+         out = conv2(z2) + shortcut(x)   an identity shortcut added in conv2's epilogue; a 1x1
+                                         shortcut over cat(x1, x2) summed into conv2's own
+                                         contraction (sp_conv3x3_bf16_sc: its stages read the
+                                         parts in place), else two GEMMs over the parts' rows
     bwd  dx = GN1^T(conv1^T(GN2^T(conv2^T dout))) + shortcut^T dout, the shortcut's gradient
          added by GN1's VJP kernel into the parts' gradients (no autograd accumulation add).
     Skip tensors (layers.SkipGrad, as unet2d._ResnetBlockFn): ``box_out`` receives dx2 (the
@@ -530,6 +586,15 @@ class _ResnetBlockBf16Fn(torch.autograd.Function):
                           block.conv1.weight.shape[0], shape=(n, cin, hh, ww) if b1 else None)
         del z1
         z2, st2 = _gn_fwd_raw(block.norm2, h1, None, tb, blocked=b2)
+        c2 = 0 if x2 is None else x2.shape[1]
+        if block.conv_shortcut is not None and sc_ok(cout, x1.shape[1], c2, hh, ww):
+            # conv2 + the 1x1 shortcut as one contraction: no shortcut tensor, no residual read
+            out = _conv_sc_launch(z2, conv_pack(block.conv2, False), _sc_bias(block), x1, x2, shortcut_pack(block),
+                                  cout, shape=(n, cout, hh, ww) if b2 else None)
+            ctx.block = block
+            ctx.box_in, ctx.box_out = box_in, box_out
+            ctx.save_for_backward(x1, x2, h1, tb, st1, st2)
+            return out
         if block.conv_shortcut is None:
             short = x1
         else:
