@@ -643,6 +643,20 @@ int64_t sp_conv3x3_bf16_sc_workspace(int64_t n, int32_t cin, int32_t cs, int32_t
 int sp_conv3x3_bf16_sc(const void* x, int32_t in_layout, const void* wp, const float* bias, const void* xs1,
                        const void* xs2, int32_t cs1, int32_t cs2, const void* wsp, int64_t n, int32_t cin,
                        int32_t cout, int32_t h, int32_t w, void* y, void* ws, int64_t ws_bytes, sp_stream_t stream);
+/* dz = the 3x3 conv input VJP of dy (flipped / transposed pack wp; dy in in_layout as
+ * sp_conv3x3_bf16_ex), then dx1 / dx2 = the input VJP of sp_groupnorm_bf16_fwd over cat(x1, x2)
+ * (c1 + c2 = cout) at dz (+ add1 / add2 / add1b; dx_layout as sp_groupnorm_bf16_bwd_ex): the
+ * ResnetBlock VJP's conv2^T -> GN2^T and conv1^T -> GN1^T pairs, with the GroupNorm VJP's sums
+ * taken in the conv's epilogue per 512-pixel tile (no pass re-reading dz and x).  dz: caller
+ * buffer [n][h][w][cout]; ws: sp_conv3x3_bf16_gnvjp_workspace bytes.  TC = 32 unsplit shapes. */
+int sp_conv3x3_bf16_gnvjp_supported(int64_t n, int32_t cin, int32_t cout, int32_t h, int32_t w, int32_t c1,
+                                    int32_t groups);
+int64_t sp_conv3x3_bf16_gnvjp_workspace(int64_t n, int32_t cout, int32_t h, int32_t w);
+int sp_conv3x3_bf16_gnvjp(const void* dy, int32_t in_layout, const void* wp, int64_t n, int32_t cin, int32_t cout,
+                          int32_t h, int32_t w, void* dz, const void* x1, const void* x2, int32_t c1,
+                          const float* chan_bias, const float* gamma, const float* beta, const float* stats,
+                          int32_t groups, int32_t act, void* dx1, void* dx2, int32_t dx_layout, const void* add1,
+                          const void* add2, const void* add1b, void* ws, int64_t ws_bytes, sp_stream_t stream);
 int sp_attention_bf16_supported(int64_t batch, int32_t heads, int64_t n, int64_t m, int32_t d);
 /* multi-head softmax(q k^T scale) v on bf16 token rows (self: m = n; cross: kv_shared = 1 for
  * one context row for the whole batch); lse [batch heads][n] fp32 for the VJP. */

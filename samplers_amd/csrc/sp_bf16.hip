@@ -144,14 +144,30 @@ __device__ __forceinline__ int cv_chunk(int p) { return p & 1; }
 // contraction — weights wsp [co block of 64][cs / 16][64 co][16 ci], the stage's 512 pixels
 // written to the patch centre and read by the centre tap only (8 MFMAs per wave) — so the
 // shortcut's output is never written to HBM nor read back as a residual.
-template <int TC, bool UP, bool BLK = false, bool SC = false>
+// GS (TC = 32, unsplit): the output y is the cotangent dz of a GroupNorm(+SiLU) over cat(gx1, gx2)
+// (gc1 + gc2 = cout channels, NHWC) and the epilogue also emits that GroupNorm VJP's per-(tile,
+// channel) sums sum(g), sum(g xhat) (g = dz act'(y) gamma) over the tile's 512 pixels, from dz as
+// stored (bf16) and the per-(n, c) coefficients gco = [sc | sh | xs | xo] (k_gnb_coefs): gpart
+// [n][tile][2][cout], tile = the tile's index within its sample — the layout k_gnb_final_bwd
+// reads, so the separate sums pass (x and dz read again) is not run.
+struct ConvGn {
+    const u16* x1;
+    const u16* x2;
+    int c1, act;
+    const float* co;
+    const float* gamma;
+    float* part;
+};
+
+template <int TC, bool UP, bool BLK = false, bool SC = false, bool GS = false>
 __global__ __launch_bounds__(kBlock, TC == 4 ? 1 : 2) void k_conv3x3_bf16(const u16* __restrict__ x, const u16* __restrict__ wp,
                                                          const float* __restrict__ bias, const u16* __restrict__ res,
                                                          int n, int cin, int cout, int h, int w,
                                                          u16* __restrict__ y, float* __restrict__ part,
                                                          const u16* __restrict__ xs1, const u16* __restrict__ xs2,
-                                                         int cs1, int cs2, const u16* __restrict__ wsp) {
+                                                         int cs1, int cs2, const u16* __restrict__ wsp, ConvGn gn) {
     static_assert(!SC || (TC == 32 && !UP), "shortcut stages: TC = 32 tiles");
+    static_assert(!GS || (TC == 32 && !UP && !SC), "GroupNorm VJP sums: TC = 32 tiles");
     using G = CvGeo<TC>;
     __shared__ __attribute__((aligned(16))) char lds[G::LDS];
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, r = lane & 31, hh = lane >> 5;
@@ -440,6 +456,103 @@ __global__ __launch_bounds__(kBlock, TC == 4 ? 1 : 2) void k_conv3x3_bf16(const 
     }
 
     // epilogue: lane (pixel r of tile j) holds channels 64 cb + 32 a + 8 g + 4 hh + e in register 4 g + e
+    if constexpr (GS) {
+        // dz stored, and per lane the sums over its 4 pixels (j) of each of its 32 channels: V[2 i + s],
+        // i = (a 4 + g) 4 + e, s = 0: sum g, 1: sum g xhat
+        const int64_t nc = (int64_t)n * cout;
+        const int c2 = cout - gn.c1;
+        // restrict-qualified: the x / coefficient loads may then be issued ahead of the dz stores
+        // (unqualified, every load waited for the store before it)
+        const u16* __restrict__ gx1 = gn.x1;
+        const u16* __restrict__ gx2 = gn.x2;
+        const float* __restrict__ gco = gn.co;
+        const float* __restrict__ ggm = gn.gamma;
+        float V[64];
+#pragma unroll
+        for (int a = 0; a < 2; ++a)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const int co = cb * 64 + 32 * a + 8 * g + 4 * hh;
+                const bool live = co < cout;  // cout % 16 == 0: a lane's 4 channels are all in or all out
+                const int cl = live ? co : 0;
+                const float4 k0 = *reinterpret_cast<const float4*>(gco + (int64_t)n0 * cout + cl);
+                const float4 k1 = *reinterpret_cast<const float4*>(gco + nc + (int64_t)n0 * cout + cl);
+                const float4 k2 = *reinterpret_cast<const float4*>(gco + 2 * nc + (int64_t)n0 * cout + cl);
+                const float4 k3 = *reinterpret_cast<const float4*>(gco + 3 * nc + (int64_t)n0 * cout + cl);
+                const float4 gm4 = ggm ? *reinterpret_cast<const float4*>(ggm + cl) : make_float4(1.f, 1.f, 1.f, 1.f);
+                const float K0[4] = {k0.x, k0.y, k0.z, k0.w}, K1[4] = {k1.x, k1.y, k1.z, k1.w};
+                const float K2[4] = {k2.x, k2.y, k2.z, k2.w}, K3[4] = {k3.x, k3.y, k3.z, k3.w};
+                const float GM[4] = {gm4.x, gm4.y, gm4.z, gm4.w};
+                float s1[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f};
+                bq_u2 xq[4];  // the 4 pixels' x, loaded before any of their arithmetic
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int64_t pix = ((int64_t)n0 * h + h0 + 4 * wv + j) * w + c0 + r;
+                    xq[j] = !live ? bq_u2{0u, 0u}
+                          : co < gn.c1 ? *reinterpret_cast<const bq_u2*>(gx1 + pix * gn.c1 + co)
+                                       : *reinterpret_cast<const bq_u2*>(gx2 + pix * c2 + (co - gn.c1));
+                }
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int64_t pix = ((int64_t)n0 * h + h0 + 4 * wv + j) * w + c0 + r;
+                    float v[4];
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) v[e] = acc[a][j][4 * g + e];
+                    if (!live) continue;
+                    if (bias) {
+                        const float4 bb = *reinterpret_cast<const float4*>(bias + co);
+                        v[0] += bb.x, v[1] += bb.y, v[2] += bb.z, v[3] += bb.w;
+                    }
+                    const bq_u2 dzv{pk2(v[0], v[1]), pk2(v[2], v[3])};
+                    *reinterpret_cast<bq_u2*>(y + pix * cout + co) = dzv;
+                    const bq_u2 xv = xq[j];
+                    const float xf[4] = {bf_lo(xv.x), bf_hi(xv.x), bf_lo(xv.y), bf_hi(xv.y)};
+                    const float df[4] = {bf_lo(dzv.x), bf_hi(dzv.x), bf_lo(dzv.y), bf_hi(dzv.y)};
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {  // the terms of k_gnb_stats<1, ACT>
+                        const float yv = fmaf(xf[e], K0[e], K1[e]);
+                        float d = df[e];
+                        if (gn.act) {
+                            const float sg = __builtin_amdgcn_rcpf(1.f + __expf(-yv));
+                            d *= sg * (1.f + yv * (1.f - sg));
+                        }
+                        const float gg = d * GM[e];
+                        s1[e] += gg;
+                        s2[e] = fmaf(gg, fmaf(xf[e], K2[e], K3[e]), s2[e]);
+                    }
+                }
+#pragma unroll
+                for (int e = 0; e < 4; ++e) V[2 * ((a * 4 + g) * 4 + e)] = s1[e], V[2 * ((a * 4 + g) * 4 + e) + 1] = s2[e];
+            }
+        // sum over the 32 lanes of each half-wave (its 32 pixels of each tile row) by halving
+        // exchanges: after the step with mask m a lane keeps the half of its values selected by
+        // its lane bit m; lane r ends with V[2 r], V[2 r + 1] = value index r's two sums
+#pragma unroll
+        for (int m = 16, L = 64; m >= 1; m >>= 1, L >>= 1) {
+            const bool up = (r & m) != 0;
+#pragma unroll
+            for (int k = 0; k < L / 2; ++k) {
+                const float keep = up ? V[L / 2 + k] : V[k], give = up ? V[k] : V[L / 2 + k];
+                V[k] = keep + __shfl_xor(give, m, 64);
+            }
+        }
+        __syncthreads();  // the stage buffers are free: the wave totals meet in LDS
+        float* red = reinterpret_cast<float*>(lds);  // [wave][stat][64 local channels]
+        {
+            const int i = r, a = i >> 4, g = (i >> 2) & 3, e = i & 3, cl = 32 * a + 8 * g + 4 * hh + e;
+            red[(wv * 2 + 0) * 64 + cl] = V[0];
+            red[(wv * 2 + 1) * 64 + cl] = V[1];
+        }
+        __syncthreads();
+        if (tid < 128) {
+            const int st = tid >> 6, cl = tid & 63, co = cb * 64 + cl;
+            const float t = ((red[(0 * 2 + st) * 64 + cl] + red[(1 * 2 + st) * 64 + cl]) + red[(2 * 2 + st) * 64 + cl]) +
+                            red[(3 * 2 + st) * 64 + cl];
+            const int tiles = (h / G::SR) * (w >> 5), tile = (h0 / G::SR) * (w >> 5) + (c0 >> 5);
+            if (co < cout) gn.part[(((int64_t)n0 * tiles + tile) * 2 + st) * cout + co] = t;
+        }
+        return;
+    }
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
         const int p = 128 * wv + 32 * j + r, vr = p / TC, col = p - vr * TC;
@@ -551,19 +664,19 @@ struct ConvSc {
     const u16* wsp = nullptr;
 };
 
-template <int TC, bool UP, bool BLK = false, bool SC = false>
+template <int TC, bool UP, bool BLK = false, bool SC = false, bool GS = false>
 static void conv_bf16_launch(const u16* x, const u16* wp, const float* bias, const u16* res, int n, int cin,
                              int cout, int h, int w, u16* y, hipStream_t s, float* part = nullptr, int parts = 1,
-                             const ConvSc& sc = ConvSc{}) {
+                             const ConvSc& sc = ConvSc{}, const ConvGn& gn = ConvGn{}) {
     using G = CvGeo<TC>;
     (void)sizeof(G);
     const int cbn = (cout + 63) / 64;
     const int64_t tiles = conv_tiles<TC>(n, h, w);
     // (+ the shortcut stages' 1x1 contraction)
     const double flops = 18.0 * n * (double)h * w * cin * cout + 2.0 * n * (double)h * w * (sc.cs1 + sc.cs2) * cout;
-    launch_w(TK_CONV_BF16, flops, k_conv3x3_bf16<TC, UP, BLK, SC>, dim3(cbn, static_cast<unsigned>(tiles), parts),
+    launch_w(TK_CONV_BF16, flops, k_conv3x3_bf16<TC, UP, BLK, SC, GS>, dim3(cbn, static_cast<unsigned>(tiles), parts),
              dim3(kBlock), s, x, wp, bias, res, n, cin, cout, h, w, y, parts > 1 ? part : nullptr, sc.xs1, sc.xs2,
-             sc.cs1, sc.cs2, sc.wsp);
+             sc.cs1, sc.cs2, sc.wsp, gn);
     if (parts > 1) {
         const int64_t total = (int64_t)n * h * w * cout;
         launch(0, k_conv_reduce, dim3(stream_blocks(total / 8)), dim3(kBlock), s, static_cast<const float*>(part),
@@ -1930,6 +2043,80 @@ int sp_groupnorm_bf16_bwd_ex(const void* dz, const void* x1, const void* x2, int
                static_cast<const u16*>(add1), static_cast<const u16*>(add2), static_cast<const u16*>(add1b),
                static_cast<int>(dx_layout));
     return check_launch("sp_groupnorm_bf16_bwd");
+}
+
+// ---- conv input VJP + the GroupNorm VJP it feeds, with the GroupNorm sums from the conv epilogue ----
+
+static int64_t gnv_tiles(int32_t h, int32_t w) { return (int64_t)(h / 16) * (w / 32); }
+
+int sp_conv3x3_bf16_gnvjp_supported(int64_t n, int32_t cin, int32_t cout, int32_t h, int32_t w, int32_t c1,
+                                    int32_t groups) {
+    return n > 0 && n <= 65535 && sp_conv3x3_bf16_supported(cin, cout, h, w) && conv_tc(h, w) == 32 &&
+           cout % 16 == 0 && c1 > 0 && c1 % 16 == 0 && c1 <= cout &&
+           sp_groupnorm_bf16_supported(c1, cout - c1, groups) &&
+           conv_parts(static_cast<int>(n), cin, cout, h, w) == 1 &&
+           n * h * (int64_t)w * std::max(cin, cout) < (int64_t(1) << 40);
+}
+
+// workspace bytes (fp32): per-tile sums [n][tiles][2][cout] + coefficients [4][n][cout] + [3][n][cout]
+int64_t sp_conv3x3_bf16_gnvjp_workspace(int64_t n, int32_t cout, int32_t h, int32_t w) {
+    return 4 * (n * gnv_tiles(h, w) * 2 * (int64_t)cout + 7 * n * (int64_t)cout);
+}
+
+// dz = conv3x3 input VJP of dy (the conv's flipped / transposed weight pack wp, dy in in_layout as
+// sp_conv3x3_bf16_ex, cin = dy's channels, cout = dz's), then dx1 / dx2 = the input VJP of
+// sp_groupnorm_bf16_fwd over cat(x1, x2) (c1 + c2 = cout channels) at dz, + the addends — as
+// sp_conv3x3_bf16_ex followed by sp_groupnorm_bf16_bwd_ex, except that the GroupNorm VJP's sums
+// come from the conv's epilogue (per 512-pixel tile, fixed order) instead of a pass that reads dz
+// and x again.  dz: a caller buffer [n][h][w][cout] (written, then read by the apply pass).
+int sp_conv3x3_bf16_gnvjp(const void* dy, int32_t in_layout, const void* wp, int64_t n, int32_t cin, int32_t cout,
+                          int32_t h, int32_t w, void* dz, const void* x1, const void* x2, int32_t c1,
+                          const float* chan_bias, const float* gamma, const float* beta, const float* stats,
+                          int32_t groups, int32_t act, void* dx1, void* dx2, int32_t dx_layout, const void* add1,
+                          const void* add2, const void* add1b, void* ws, int64_t ws_bytes, sp_stream_t stream) {
+    if (!dy || !wp || !dz || !x1 || !stats || !dx1 || !ws || (in_layout != 0 && in_layout != 1) ||
+        !sp_conv3x3_bf16_gnvjp_supported(n, cin, cout, h, w, c1, groups))
+        return SP_EINVAL;
+    const int c2 = cout - c1;
+    if ((c2 && (!x2 || !dx2)) || (dx_layout != 0 && (dx_layout != 1 || c2)) ||
+        ws_bytes < sp_conv3x3_bf16_gnvjp_workspace(n, cout, h, w))
+        return SP_EINVAL;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const int64_t hw = (int64_t)h * w, nc = n * (int64_t)cout;
+    const int tiles = static_cast<int>(gnv_tiles(h, w));
+    float* part = static_cast<float*>(ws);
+    float* co = part + n * tiles * 2 * (int64_t)cout;
+    float* co2 = co + 4 * nc;
+    const u16* a = static_cast<const u16*>(x1);
+    const u16* b = static_cast<const u16*>(x2);
+    const u16* d = static_cast<const u16*>(dz);
+    launch(0, k_gnb_coefs, dim3(static_cast<unsigned>((nc + kBlock - 1) / kBlock)), dim3(kBlock), s, stats, chan_bias,
+           gamma, beta, static_cast<int>(n), static_cast<int>(cout), groups, co);
+    ConvGn gn{a, b, c1, act ? 1 : 0, co, gamma, part};
+    const int ni = static_cast<int>(n);
+    if (in_layout)
+        conv_bf16_launch<32, false, true, false, true>(static_cast<const u16*>(dy), static_cast<const u16*>(wp), nullptr,
+                                                       nullptr, ni, cin, cout, h, w, static_cast<u16*>(dz), s, nullptr,
+                                                       1, ConvSc{}, gn);
+    else
+        conv_bf16_launch<32, false, false, false, true>(static_cast<const u16*>(dy), static_cast<const u16*>(wp),
+                                                        nullptr, nullptr, ni, cin, cout, h, w, static_cast<u16*>(dz), s,
+                                                        nullptr, 1, ConvSc{}, gn);
+    launch(0, k_gnb_final_bwd, dim3(groups, static_cast<unsigned>(n)), dim3(64), s, static_cast<const float*>(part),
+           tiles, hw, static_cast<int>(cout), groups, stats, gamma, static_cast<const float*>(co), co2);
+    const GnbGeo g = gnb_geo(n, cout, hw);
+    const dim3 grid(g.chunks, static_cast<unsigned>(n));
+    if (act)
+        launch(0, k_gnb_bwd_apply<true>, grid, dim3(kBlock), s, d, a, b, c1, c2, static_cast<const float*>(co),
+               static_cast<const float*>(co2), hw, g.chunk_px, static_cast<u16*>(dx1), static_cast<u16*>(dx2),
+               static_cast<const u16*>(add1), static_cast<const u16*>(add2), static_cast<const u16*>(add1b),
+               static_cast<int>(dx_layout));
+    else
+        launch(0, k_gnb_bwd_apply<false>, grid, dim3(kBlock), s, d, a, b, c1, c2, static_cast<const float*>(co),
+               static_cast<const float*>(co2), hw, g.chunk_px, static_cast<u16*>(dx1), static_cast<u16*>(dx2),
+               static_cast<const u16*>(add1), static_cast<const u16*>(add2), static_cast<const u16*>(add1b),
+               static_cast<int>(dx_layout));
+    return check_launch("sp_conv3x3_bf16_gnvjp");
 }
 
 // ---- attention ------------------------------------------------------------------------------

@@ -390,6 +390,52 @@ def _gn_bwd_raw(norm: nn.GroupNorm, dz: Tensor, x1: Tensor, x2: Tensor | None, c
     return dx1, dx2
 
 
+def gnvjp_ok(n: int, cin: int, cout: int, h: int, w: int, c1: int, groups: int) -> bool:
+    """Whether a conv input VJP (cin cotangent channels -> cout) and the GroupNorm VJP it feeds run as
+    ``sp_conv3x3_bf16_gnvjp`` (the GroupNorm sums from the conv's epilogue).  Off by default
+    (``SAMPLERS_AMD_BF16_GNVJP=1`` turns it on): measured 10 % slower per DPS bf16 step — the
+    epilogue's SiLU-derivative terms (an exp and a reciprocal per output element, per lane 128 of
+    them) cost the conv tile more than the sums pass's HBM reads (profiles/round6/bf16/gn_sums_epilogue_ab/)."""
+    import os
+
+    from .layers import _query
+
+    return (os.environ.get("SAMPLERS_AMD_BF16_GNVJP", "0") == "1"
+            and bool(_query("sp_conv3x3_bf16_gnvjp_supported", n, cin, cout, h, w, c1, groups)))
+
+
+def _conv_gn_vjp(dy: Tensor, pack: Tensor, cin: int, norm: nn.GroupNorm, x1: Tensor, x2: Tensor | None,
+                 cb: Tensor | None, stats: Tensor, dy_blocked: bool = False, add1: Tensor | None = None,
+                 add2: Tensor | None = None, out1: Tensor | None = None, out2: Tensor | None = None,
+                 add1b: Tensor | None = None, blocked: bool = False) -> tuple[Tensor, Tensor | None]:
+    """GN^T(conv^T dy) (+ addends) on ``sp_conv3x3_bf16_gnvjp``: ``dy`` channels-last (or flat
+    channel-blocked with ``dy_blocked``) with ``cin`` channels; the GroupNorm over cat(x1, x2) with
+    ``stats``; outputs as ``_gn_bwd_raw``."""
+    from .layers import _query
+
+    lib = _hip.load_library()
+    n, c1, h, w = x1.shape
+    c2 = 0 if x2 is None else x2.shape[1]
+    cout = c1 + c2
+    gamma, beta = _gn_params(norm)
+    dz = torch.empty(n, cout, h, w, device=x1.device, dtype=BF16, memory_format=CL)
+    if blocked:
+        dx1 = torch.empty(n * c1 * h * w, device=x1.device, dtype=BF16)
+    else:
+        dx1 = torch.empty_like(x1, memory_format=CL) if out1 is None else out1
+    dx2 = None if x2 is None else (torch.empty_like(x2, memory_format=CL) if out2 is None else out2)
+    nb = _query("sp_conv3x3_bf16_gnvjp_workspace", n, cout, h, w)
+    ws = torch.empty(nb, device=x1.device, dtype=torch.uint8)
+    _hip.check(lib.sp_conv3x3_bf16_gnvjp(_p(dy, cl=not dy_blocked), int(dy_blocked), _p(pack, cl=False), n, cin, cout,
+                                         h, w, _p(dz), _p(x1), _p(x2), c1, None if cb is None else cb.data_ptr(),
+                                         None if gamma is None else gamma.data_ptr(),
+                                         None if beta is None else beta.data_ptr(), stats.data_ptr(), norm.num_groups,
+                                         int(norm.act), _p(dx1, cl=not blocked), _p(dx2), int(blocked), _p(add1),
+                                         _p(add2), _p(add1b), ws.data_ptr(), nb, _hip.stream_of(x1)),
+               "sp_conv3x3_bf16_gnvjp")
+    return dx1, dx2
+
+
 class _GroupNormBf16Fn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x1, x2, norm, cb):
@@ -619,33 +665,42 @@ class _ResnetBlockBf16Fn(torch.autograd.Function):
         blk = ctx.block
         dout = nhwc(dout.to(BF16))
         cout = blk.conv2.weight.shape[0]
-        dz2 = _conv_launch(_pad_channels(dout, _ceil(cout, 16)), conv_pack(blk.conv2, True), None, None, cout)
         cmid = blk.conv1.weight.shape[0]
         cin = blk.conv1.weight.shape[1]
         n, _, hh, ww = h1.shape
+        c1 = x1.shape[1]
         # dh1 feeds only conv1's VJP: channel-blocked where the tile takes it
         bl = cmid % 16 == 0 and blocked_ok(cmid, cin, hh, ww)
-        dh1, _ = _gn_bwd_raw(blk.norm2, dz2, h1, None, tb, st2, blocked=bl)
-        del dz2
-        if bl:
-            dz1 = _conv_launch(dh1, conv_pack(blk.conv1, True), None, None, cin, shape=(n, cmid, hh, ww))
+        dpad = _pad_channels(dout, _ceil(cout, 16))
+        if gnvjp_ok(n, dpad.shape[1], cmid, hh, ww, cmid, blk.norm2.num_groups):  # GN2 sums from conv2^T's epilogue
+            dh1, _ = _conv_gn_vjp(dpad, conv_pack(blk.conv2, True), dpad.shape[1], blk.norm2, h1, None, tb, st2,
+                                  blocked=bl)
         else:
-            dz1 = _conv_launch(_pad_channels(dh1, _ceil(cmid, 16)), conv_pack(blk.conv1, True), None, None, cin)
-        del dh1
+            dz2 = _conv_launch(dpad, conv_pack(blk.conv2, True), None, None, cmid)
+            dh1, _ = _gn_bwd_raw(blk.norm2, dz2, h1, None, tb, st2, blocked=bl)
+            del dz2
+        del dpad
         extra = ctx.box_in.take() if ctx.box_in is not None else None
         if extra is not None:
             extra = nhwc(extra.to(BF16))
         if blk.conv_shortcut is None:  # identity shortcut: dx1 = GN1^T dz1 + dout (+ skip grad)
-            dx1, dx2 = _gn_bwd_raw(blk.norm1, dz1, x1, x2, None, st1, add1=dout, add1b=extra)
+            adds = dict(add1=dout, add1b=extra)
         else:  # s = shortcut^T dout per part (pixel rows), then += GN1^T dz1 in place
-            c1 = x1.shape[1]
             w1, w2 = _shortcut_w(blk, c1)
-            n, _, h, w = x1.shape
             d = _rows(dout)
-            s1 = (d @ w1).reshape(n, h, w, c1).permute(0, 3, 1, 2)
-            s2 = None if x2 is None else (d @ w2).reshape(n, h, w, x2.shape[1]).permute(0, 3, 1, 2)
-            dx1, dx2 = _gn_bwd_raw(blk.norm1, dz1, x1, x2, None, st1, add1=s1, add2=s2, out1=s1, out2=s2,
-                                   add1b=extra)
+            s1 = (d @ w1).reshape(n, hh, ww, c1).permute(0, 3, 1, 2)
+            s2 = None if x2 is None else (d @ w2).reshape(n, hh, ww, x2.shape[1]).permute(0, 3, 1, 2)
+            adds = dict(add1=s1, add2=s2, out1=s1, out2=s2, add1b=extra)
+        if cmid % 16 == 0 and gnvjp_ok(n, cmid, cin, hh, ww, c1, blk.norm1.num_groups):  # GN1 sums: conv1^T's epilogue
+            dx1, dx2 = _conv_gn_vjp(dh1, conv_pack(blk.conv1, True), cmid, blk.norm1, x1, x2, None, st1,
+                                    dy_blocked=bl, **adds)
+        else:
+            if bl:
+                dz1 = _conv_launch(dh1, conv_pack(blk.conv1, True), None, None, cin, shape=(n, cmid, hh, ww))
+            else:
+                dz1 = _conv_launch(_pad_channels(dh1, _ceil(cmid, 16)), conv_pack(blk.conv1, True), None, None, cin)
+            dx1, dx2 = _gn_bwd_raw(blk.norm1, dz1, x1, x2, None, st1, **adds)
+        del dh1
         if ctx.box_out is not None:  # x2 (a skip): its down-path consumer adds this gradient
             ctx.box_out.grad, dx2 = dx2, None
         return None, None, dx1, dx2, None, None

@@ -442,7 +442,7 @@ def test_resnet_block_bf16_shortcut_in_conv2(cuda, monkeypatch, parity_record, n
         return blk(x.to(cuda, BF), temb.to(cuda, BF), skip=None if skip is None else skip.to(cuda, BF)).float().cpu()
 
     names = _kernel_names(gpu_out)
-    assert any("k_conv3x3_bf16<32, false, true, true>" in s or "k_conv3x3_bf16<32, false, false, true>" in s
+    assert any("k_conv3x3_bf16<32, false, true, true," in s or "k_conv3x3_bf16<32, false, false, true," in s
                for s in names), sorted(s for s in names if "conv" in s)
     a = gpu_out()
     monkeypatch.setenv("SAMPLERS_AMD_BF16_SC", "0")
@@ -452,6 +452,52 @@ def test_resnet_block_bf16_shortcut_in_conv2(cuda, monkeypatch, parity_record, n
     parity_record("resnet_bf16_sc_vs_gemm_shortcut", e_ab, 1e-2, shape=[n, c1, c2, cout, h, w])
     parity_record("resnet_bf16_sc_vs_fp32", e_a, 1.2 * e_b + 1e-3, shape=[n, c1, c2, cout, h, w], gemm_vs_fp32=e_b)
     assert e_ab < 1e-2 and e_a <= 1.2 * e_b + 1e-3, (e_ab, e_a, e_b)
+
+
+@pytest.mark.parametrize("n,c1,c2,cout,h,w,blocked", [(2, 128, 64, 128, 32, 64, "1"), (2, 128, 0, 128, 32, 32, "0"),
+                                                      (1, 64, 64, 64, 64, 64, "1")])
+def test_resnet_block_bf16_groupnorm_sums_from_conv_epilogue(cuda, monkeypatch, parity_record, n, c1, c2, cout, h, w,
+                                                             blocked):
+    """The block's VJP with both GroupNorm VJPs' sums taken in the preceding conv VJP's epilogue
+    (sp_conv3x3_bf16_gnvjp, opt-in: per-tile partials, no sums pass) against the conv VJP + two-pass
+    GroupNorm VJP (SAMPLERS_AMD_BF16_GNVJP=0) — the same terms summed in another fixed order — and
+    the block in fp32 on the CPU."""
+    from samplers_amd.networks.unet2d import ResnetBlock2D
+
+    monkeypatch.setenv("SAMPLERS_AMD_BF16_BLOCKED", blocked)
+    monkeypatch.setenv("SAMPLERS_AMD_BF16_GNVJP", "1")  # off by default (slower, see bf16.gnvjp_ok)
+    torch.manual_seed(5)
+    ref = ResnetBlock2D(c1 + c2, cout, 64, 32, 1e-5).requires_grad_(False)
+    blk = copy.deepcopy(ref).to(cuda, BF)
+    gen = torch.Generator().manual_seed(6)
+    x = torch.randn(n, c1, h, w, generator=gen)
+    skip = torch.randn(n, c2, h, w, generator=gen) if c2 else None
+    temb = torch.randn(n, 64, generator=gen)
+    cot = torch.randn(n, cout, h, w, generator=gen)
+
+    def run(mod, dev, dt):
+        xr = x.to(dev, dt).requires_grad_(True)
+        sr = None if skip is None else skip.to(dev, dt).requires_grad_(True)
+        with torch.enable_grad():
+            out = mod(xr, temb.to(dev, dt), skip=sr)
+        gs = torch.autograd.grad(out, (xr,) if sr is None else (xr, sr), cot.to(dev, dt))
+        return torch.cat([g.float().cpu().reshape(-1) for g in gs])
+
+    def gpu_vjp():
+        return run(blk, cuda, BF)
+
+    names = _kernel_names(gpu_vjp)
+    assert any("k_conv3x3_bf16<32, false" in s and ", true>" in s and "true, true>" not in s for s in names)
+    assert not any("k_gnb_stats<1" in s for s in names), "the GroupNorm VJP sums pass still ran"
+    a = gpu_vjp()
+    monkeypatch.setenv("SAMPLERS_AMD_BF16_GNVJP", "0")
+    b = gpu_vjp()
+    r = run(ref, "cpu", torch.float32)
+    e_ab, e_a, e_b = _rel(a, b), _rel(a, r), _rel(b, r)
+    tag = [n, c1, c2, cout, h, w, blocked]
+    parity_record("resnet_bf16_gn_sums_epilogue_vs_two_pass_vjp", e_ab, 5e-3, shape=tag)
+    parity_record("resnet_bf16_gn_sums_epilogue_vjp_vs_fp32", e_a, 1.2 * e_b + 1e-3, shape=tag, two_pass_vs_fp32=e_b)
+    assert e_ab < 5e-3 and e_a <= 1.2 * e_b + 1e-3, (e_ab, e_a, e_b)
 
 
 # ---- whole priors -----------------------------------------------------------------------------
