@@ -657,6 +657,17 @@ int sp_conv3x3_bf16_gnvjp(const void* dy, int32_t in_layout, const void* wp, int
                           const float* chan_bias, const float* gamma, const float* beta, const float* stats,
                           int32_t groups, int32_t act, void* dx1, void* dx2, int32_t dx_layout, const void* add1,
                           const void* add2, const void* add1b, void* ws, int64_t ws_bytes, sp_stream_t stream);
+/* y = conv3x3(x) + bias (+ res) (as sp_conv3x3_bf16_ex), then z = act(GroupNorm(y + chan_bias))
+ * (as sp_groupnorm_bf16_fwd_ex: gamma / beta, z_layout, stats [mean | rstd]) — the ResnetBlock's
+ * conv1 -> GN2 pair, with the GroupNorm moments taken in the conv's epilogue per 512-pixel tile
+ * (shifted by the tile's first pixel; no statistics pass re-reading y).  ws:
+ * sp_conv3x3_bf16_gn_workspace bytes.  TC = 32 unsplit shapes. */
+int sp_conv3x3_bf16_gn_supported(int64_t n, int32_t cin, int32_t cout, int32_t h, int32_t w, int32_t groups);
+int64_t sp_conv3x3_bf16_gn_workspace(int64_t n, int32_t cout, int32_t h, int32_t w);
+int sp_conv3x3_bf16_gn(const void* x, int32_t in_layout, const void* wp, const float* bias, const void* res,
+                       int64_t n, int32_t cin, int32_t cout, int32_t h, int32_t w, void* y, const float* chan_bias,
+                       const float* gamma, const float* beta, int32_t groups, float eps, int32_t act, void* z,
+                       int32_t z_layout, float* stats, void* ws, int64_t ws_bytes, sp_stream_t stream);
 int sp_attention_bf16_supported(int64_t batch, int32_t heads, int64_t n, int64_t m, int32_t d);
 /* multi-head softmax(q k^T scale) v on bf16 token rows (self: m = n; cross: kv_shared = 1 for
  * one context row for the whole batch); lse [batch heads][n] fp32 for the VJP. */

@@ -262,6 +262,10 @@ SIGNATURES = {
     "sp_conv3x3_bf16_gnvjp_workspace": (_I64, [_I64, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32]),
     "sp_conv3x3_bf16_gnvjp": (ctypes.c_int, [_P, ctypes.c_int32, _P, _I64, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, _P, _P, _P, ctypes.c_int32, _P, _P, _P, _P,
                                              ctypes.c_int32, ctypes.c_int32, _P, _P, ctypes.c_int32, _P, _P, _P, _P, _I64, _P]),
+    "sp_conv3x3_bf16_gn_supported": (ctypes.c_int, [_I64] + [ctypes.c_int32] * 5),
+    "sp_conv3x3_bf16_gn_workspace": (_I64, [_I64, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32]),
+    "sp_conv3x3_bf16_gn": (ctypes.c_int, [_P, ctypes.c_int32, _P, _P, _P, _I64, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, _P, _P, _P, _P, ctypes.c_int32,
+                                          ctypes.c_float, ctypes.c_int32, _P, ctypes.c_int32, _P, _P, _I64, _P]),
     "sp_geglu_bf16_fwd": (ctypes.c_int, [_P, _I64, ctypes.c_int32, _P, _P]),
     "sp_geglu_bf16_bwd": (ctypes.c_int, [_P, _P, _I64, ctypes.c_int32, _P, _P]),
     "sp_groupnorm_bf16_supported": (ctypes.c_int, [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32]),

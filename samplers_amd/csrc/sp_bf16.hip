@@ -150,6 +150,10 @@ __device__ __forceinline__ int cv_chunk(int p) { return p & 1; }
 // stored (bf16) and the per-(n, c) coefficients gco = [sc | sh | xs | xo] (k_gnb_coefs): gpart
 // [n][tile][2][cout], tile = the tile's index within its sample — the layout k_gnb_final_bwd
 // reads, so the separate sums pass (x and dz read again) is not run.
+// FS (TC = 32, unsplit): the output y feeds a GroupNorm over y + cb (cb = gn.co: per-(n, c) fp32
+// or NULL) and the epilogue emits its per-(tile, channel) shifted moments from y as stored:
+// gpart [n][tile][3][cout] = sum(d), sum(d^2), K with d = y + cb - K and K the tile's first pixel's
+// y + cb (k_gnb_final_fwd_tiles) — the forward statistics pass is not run.
 struct ConvGn {
     const u16* x1;
     const u16* x2;
@@ -159,7 +163,7 @@ struct ConvGn {
     float* part;
 };
 
-template <int TC, bool UP, bool BLK = false, bool SC = false, bool GS = false>
+template <int TC, bool UP, bool BLK = false, bool SC = false, bool GS = false, bool FS = false>
 __global__ __launch_bounds__(kBlock, TC == 4 ? 1 : 2) void k_conv3x3_bf16(const u16* __restrict__ x, const u16* __restrict__ wp,
                                                          const float* __restrict__ bias, const u16* __restrict__ res,
                                                          int n, int cin, int cout, int h, int w,
@@ -168,6 +172,7 @@ __global__ __launch_bounds__(kBlock, TC == 4 ? 1 : 2) void k_conv3x3_bf16(const 
                                                          int cs1, int cs2, const u16* __restrict__ wsp, ConvGn gn) {
     static_assert(!SC || (TC == 32 && !UP), "shortcut stages: TC = 32 tiles");
     static_assert(!GS || (TC == 32 && !UP && !SC), "GroupNorm VJP sums: TC = 32 tiles");
+    static_assert(!FS || (TC == 32 && !UP && !GS), "GroupNorm moments: TC = 32 tiles");
     using G = CvGeo<TC>;
     __shared__ __attribute__((aligned(16))) char lds[G::LDS];
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, r = lane & 31, hh = lane >> 5;
@@ -456,6 +461,95 @@ __global__ __launch_bounds__(kBlock, TC == 4 ? 1 : 2) void k_conv3x3_bf16(const 
     }
 
     // epilogue: lane (pixel r of tile j) holds channels 64 cb + 32 a + 8 g + 4 hh + e in register 4 g + e
+    if constexpr (FS) {
+        const float* __restrict__ cbp = gn.co;
+        // the tile's first pixel (wave 0, j = 0, r = 0: lanes 0 / 32) as stored + cb: the shifts K
+        float* kb = reinterpret_cast<float*>(lds) + 512;  // [64 local channels]
+        if (wv == 0 && r == 0) {
+#pragma unroll
+            for (int a = 0; a < 2; ++a)
+#pragma unroll
+                for (int g = 0; g < 4; ++g) {
+                    const int cl = 32 * a + 8 * g + 4 * hh, co = cb * 64 + cl;
+                    if (co >= cout) continue;
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        float t = acc[a][0][4 * g + e];
+                        if (bias) t += bias[co + e];
+                        if (res) t += bf1(res[(((int64_t)n0 * h + h0) * w + c0) * cout + co + e]);
+                        kb[cl + e] = bf1(f2bf(t)) + (cbp ? cbp[(int64_t)n0 * cout + co + e] : 0.f);
+                    }
+                }
+        }
+        __syncthreads();
+        float V[64];
+#pragma unroll
+        for (int a = 0; a < 2; ++a)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const int cl = 32 * a + 8 * g + 4 * hh, co = cb * 64 + cl;
+                const bool live = co < cout;  // cout % 16 == 0
+                float K[4], C[4] = {0.f, 0.f, 0.f, 0.f}, s1[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                for (int e = 0; e < 4; ++e) K[e] = live ? kb[cl + e] : 0.f;
+                if (live && cbp) {
+                    const float4 c4 = *reinterpret_cast<const float4*>(cbp + (int64_t)n0 * cout + co);
+                    C[0] = c4.x, C[1] = c4.y, C[2] = c4.z, C[3] = c4.w;
+                }
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    if (!live) continue;
+                    const int64_t obase = (((int64_t)n0 * h + h0 + 4 * wv + j) * w + c0 + r) * cout;
+                    float v[4];
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) v[e] = acc[a][j][4 * g + e];
+                    if (bias) {
+                        const float4 bb = *reinterpret_cast<const float4*>(bias + co);
+                        v[0] += bb.x, v[1] += bb.y, v[2] += bb.z, v[3] += bb.w;
+                    }
+                    if (res) {
+                        const bq_u2 rv = *reinterpret_cast<const bq_u2*>(res + obase + co);
+                        v[0] += bf_lo(rv.x), v[1] += bf_hi(rv.x), v[2] += bf_lo(rv.y), v[3] += bf_hi(rv.y);
+                    }
+                    const bq_u2 yv{pk2(v[0], v[1]), pk2(v[2], v[3])};
+                    *reinterpret_cast<bq_u2*>(y + obase + co) = yv;
+                    const float yf[4] = {bf_lo(yv.x), bf_hi(yv.x), bf_lo(yv.y), bf_hi(yv.y)};
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {  // the terms of k_gnb_stats<0, _> with the tile's shift
+                        const float d = yf[e] + C[e] - K[e];
+                        s1[e] += d;
+                        s2[e] = fmaf(d, d, s2[e]);
+                    }
+                }
+#pragma unroll
+                for (int e = 0; e < 4; ++e) V[2 * ((a * 4 + g) * 4 + e)] = s1[e], V[2 * ((a * 4 + g) * 4 + e) + 1] = s2[e];
+            }
+#pragma unroll
+        for (int m = 16, L = 64; m >= 1; m >>= 1, L >>= 1) {  // halving exchanges, as the GS epilogue
+            const bool up = (r & m) != 0;
+#pragma unroll
+            for (int k = 0; k < L / 2; ++k) {
+                const float keep = up ? V[L / 2 + k] : V[k], give = up ? V[k] : V[L / 2 + k];
+                V[k] = keep + __shfl_xor(give, m, 64);
+            }
+        }
+        float* red = reinterpret_cast<float*>(lds);  // [wave][stat][64 local channels] (kb lies past it)
+        {
+            const int i = r, a = i >> 4, g = (i >> 2) & 3, e = i & 3, cl = 32 * a + 8 * g + 4 * hh + e;
+            red[(wv * 2 + 0) * 64 + cl] = V[0];
+            red[(wv * 2 + 1) * 64 + cl] = V[1];
+        }
+        __syncthreads();
+        if (tid < 192) {
+            const int st = tid >> 6, cl = tid & 63, co = cb * 64 + cl;
+            const float t = st == 2 ? kb[cl]
+                                    : ((red[(0 * 2 + st) * 64 + cl] + red[(1 * 2 + st) * 64 + cl]) +
+                                       red[(2 * 2 + st) * 64 + cl]) + red[(3 * 2 + st) * 64 + cl];
+            const int tiles = (h / G::SR) * (w >> 5), tile = (h0 / G::SR) * (w >> 5) + (c0 >> 5);
+            if (co < cout) gn.part[(((int64_t)n0 * tiles + tile) * 3 + st) * cout + co] = t;
+        }
+        return;
+    }
     if constexpr (GS) {
         // dz stored, and per lane the sums over its 4 pixels (j) of each of its 32 channels: V[2 i + s],
         // i = (a 4 + g) 4 + e, s = 0: sum g, 1: sum g xhat
@@ -664,7 +758,7 @@ struct ConvSc {
     const u16* wsp = nullptr;
 };
 
-template <int TC, bool UP, bool BLK = false, bool SC = false, bool GS = false>
+template <int TC, bool UP, bool BLK = false, bool SC = false, bool GS = false, bool FS = false>
 static void conv_bf16_launch(const u16* x, const u16* wp, const float* bias, const u16* res, int n, int cin,
                              int cout, int h, int w, u16* y, hipStream_t s, float* part = nullptr, int parts = 1,
                              const ConvSc& sc = ConvSc{}, const ConvGn& gn = ConvGn{}) {
@@ -674,7 +768,7 @@ static void conv_bf16_launch(const u16* x, const u16* wp, const float* bias, con
     const int64_t tiles = conv_tiles<TC>(n, h, w);
     // (+ the shortcut stages' 1x1 contraction)
     const double flops = 18.0 * n * (double)h * w * cin * cout + 2.0 * n * (double)h * w * (sc.cs1 + sc.cs2) * cout;
-    launch_w(TK_CONV_BF16, flops, k_conv3x3_bf16<TC, UP, BLK, SC, GS>, dim3(cbn, static_cast<unsigned>(tiles), parts),
+    launch_w(TK_CONV_BF16, flops, k_conv3x3_bf16<TC, UP, BLK, SC, GS, FS>, dim3(cbn, static_cast<unsigned>(tiles), parts),
              dim3(kBlock), s, x, wp, bias, res, n, cin, cout, h, w, y, parts > 1 ? part : nullptr, sc.xs1, sc.xs2,
              sc.cs1, sc.cs2, sc.wsp, gn);
     if (parts > 1) {
@@ -907,6 +1001,49 @@ __global__ __launch_bounds__(64) void k_gnb_final_fwd(const u16* __restrict__ x1
     for (int cc = lane; cc < cpg; cc += 64) {
         const double dm = (double)gnb_shift(x1, x2, c1, c2, cbias, nn, hw, c, g * cpg + cc) - mean;
         sx += (double)hw * dm * dm;
+    }
+    const double var = std::max(0.0, wave_sum_d(sx) / cnt);
+    const float rstd = (float)(1.0 / sqrt(var + (double)eps));
+    const float meanf = (float)mean;
+    if (lane == 0) stats[(int64_t)nn * groups + g] = meanf, stats[ng + (int64_t)nn * groups + g] = rstd;
+    const int64_t nc = (int64_t)gridDim.y * c;
+    for (int cc = lane; cc < cpg; cc += 64) {
+        const int ch = g * cpg + cc;
+        const float cbv = cbias ? cbias[(int64_t)nn * c + ch] : 0.f;
+        const float sc = rstd * (gamma ? gamma[ch] : 1.f);
+        co[(int64_t)nn * c + ch] = sc;
+        co[nc + (int64_t)nn * c + ch] = (beta ? beta[ch] : 0.f) + (cbv - meanf) * sc;
+    }
+}
+
+// forward finalize from per-tile shifted moments (the FS conv epilogue): part [n][tile][3][c] =
+// sum(d), sum(d^2), K (d = x~ - K over the tile's P pixels); per group in fp64: the mean from
+// sum(d) + P K, then sum (x~ - mean)^2 = sum over (tile, channel) of S2 + 2 (K - mean) S1 + P (K - mean)^2.
+// Outputs as k_gnb_final_fwd.
+__global__ __launch_bounds__(64) void k_gnb_final_fwd_tiles(const float* __restrict__ part, int tiles, int64_t px,
+                                                            int64_t hw, int c, int groups, float eps,
+                                                            const float* __restrict__ cbias,
+                                                            const float* __restrict__ gamma,
+                                                            const float* __restrict__ beta, float* __restrict__ stats,
+                                                            float* __restrict__ co) {
+    const int cpg = c / groups, g = blockIdx.x, nn = blockIdx.y, lane = threadIdx.x;
+    const int64_t ng = (int64_t)gridDim.y * groups;
+    const int pairs = cpg * tiles;
+    const float* __restrict__ pb = part + (int64_t)nn * tiles * 3 * c + g * cpg;
+    double sa = 0.0;
+    for (int i = lane; i < pairs; i += 64) {
+        const int k = i / cpg, cc = i - k * cpg;
+        const float* pp = pb + (int64_t)k * 3 * c + cc;
+        sa += (double)pp[0] + (double)px * pp[2 * c];
+    }
+    const double cnt = (double)hw * cpg;
+    const double mean = wave_sum_d(sa) / cnt;
+    double sx = 0.0;
+    for (int i = lane; i < pairs; i += 64) {
+        const int k = i / cpg, cc = i - k * cpg;
+        const float* pp = pb + (int64_t)k * 3 * c + cc;
+        const double dm = (double)pp[2 * c] - mean;
+        sx += (double)pp[c] + 2.0 * dm * pp[0] + (double)px * dm * dm;
     }
     const double var = std::max(0.0, wave_sum_d(sx) / cnt);
     const float rstd = (float)(1.0 / sqrt(var + (double)eps));
@@ -2117,6 +2254,62 @@ int sp_conv3x3_bf16_gnvjp(const void* dy, int32_t in_layout, const void* wp, int
                static_cast<const u16*>(add1), static_cast<const u16*>(add2), static_cast<const u16*>(add1b),
                static_cast<int>(dx_layout));
     return check_launch("sp_conv3x3_bf16_gnvjp");
+}
+
+// y = conv3x3(x) + bias (+ res) as sp_conv3x3_bf16_ex, then z = act(GroupNorm(y + chan_bias) gamma + beta)
+// as sp_groupnorm_bf16_fwd_ex (z_layout, stats [mean | rstd]) — with the GroupNorm's moments taken in
+// the conv's epilogue per 512-pixel tile, shifted by the tile's first pixel (no pass re-reading y).
+int sp_conv3x3_bf16_gn_supported(int64_t n, int32_t cin, int32_t cout, int32_t h, int32_t w, int32_t groups) {
+    return n > 0 && n <= 65535 && sp_conv3x3_bf16_supported(cin, cout, h, w) && conv_tc(h, w) == 32 &&
+           cout % 16 == 0 && sp_groupnorm_bf16_supported(cout, 0, groups) &&
+           conv_parts(static_cast<int>(n), cin, cout, h, w) == 1 &&
+           n * h * (int64_t)w * std::max(cin, cout) < (int64_t(1) << 40);
+}
+
+// workspace bytes (fp32): per-tile moments [n][tiles][3][cout] + coefficients [2][n][cout]
+int64_t sp_conv3x3_bf16_gn_workspace(int64_t n, int32_t cout, int32_t h, int32_t w) {
+    return 4 * (n * gnv_tiles(h, w) * 3 * (int64_t)cout + 2 * n * (int64_t)cout);
+}
+
+int sp_conv3x3_bf16_gn(const void* x, int32_t in_layout, const void* wp, const float* bias, const void* res,
+                       int64_t n, int32_t cin, int32_t cout, int32_t h, int32_t w, void* y, const float* chan_bias,
+                       const float* gamma, const float* beta, int32_t groups, float eps, int32_t act, void* z,
+                       int32_t z_layout, float* stats, void* ws, int64_t ws_bytes, sp_stream_t stream) {
+    if (!x || !wp || !y || !z || !stats || !ws || (in_layout != 0 && in_layout != 1) || (z_layout != 0 && z_layout != 1) ||
+        !sp_conv3x3_bf16_gn_supported(n, cin, cout, h, w, groups) || ws_bytes < sp_conv3x3_bf16_gn_workspace(n, cout, h, w))
+        return SP_EINVAL;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const int64_t hw = (int64_t)h * w, nc = n * (int64_t)cout;
+    const int tiles = static_cast<int>(gnv_tiles(h, w));
+    float* part = static_cast<float*>(ws);
+    float* co = part + n * tiles * 3 * (int64_t)cout;
+    ConvGn gn{nullptr, nullptr, cout, act ? 1 : 0, chan_bias, gamma, part};
+    const int ni = static_cast<int>(n);
+    const u16* xx = static_cast<const u16*>(x);
+    const u16* ww = static_cast<const u16*>(wp);
+    const u16* rr = static_cast<const u16*>(res);
+    u16* yy = static_cast<u16*>(y);
+    if (in_layout)
+        conv_bf16_launch<32, false, true, false, false, true>(xx, ww, bias, rr, ni, cin, cout, h, w, yy, s, nullptr, 1,
+                                                              ConvSc{}, gn);
+    else
+        conv_bf16_launch<32, false, false, false, false, true>(xx, ww, bias, rr, ni, cin, cout, h, w, yy, s, nullptr, 1,
+                                                               ConvSc{}, gn);
+    launch(0, k_gnb_final_fwd_tiles, dim3(groups, static_cast<unsigned>(n)), dim3(64), s,
+           static_cast<const float*>(part), tiles, static_cast<int64_t>(512), hw, static_cast<int>(cout), groups, eps,
+           chan_bias, gamma, beta, stats, co);
+    (void)nc;
+    const GnbGeo g = gnb_geo(n, cout, hw);
+    const dim3 grid(g.chunks, static_cast<unsigned>(n));
+    if (act)
+        launch(0, k_gnb_apply<true>, grid, dim3(kBlock), s, static_cast<const u16*>(yy), static_cast<const u16*>(nullptr),
+               static_cast<int>(cout), 0, static_cast<const float*>(co), hw, g.chunk_px, static_cast<u16*>(z),
+               static_cast<int>(z_layout));
+    else
+        launch(0, k_gnb_apply<false>, grid, dim3(kBlock), s, static_cast<const u16*>(yy), static_cast<const u16*>(nullptr),
+               static_cast<int>(cout), 0, static_cast<const float*>(co), hw, g.chunk_px, static_cast<u16*>(z),
+               static_cast<int>(z_layout));
+    return check_launch("sp_conv3x3_bf16_gn");
 }
 
 // ---- attention ------------------------------------------------------------------------------

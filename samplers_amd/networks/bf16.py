@@ -436,6 +436,47 @@ def _conv_gn_vjp(dy: Tensor, pack: Tensor, cin: int, norm: nn.GroupNorm, x1: Ten
     return dx1, dx2
 
 
+def gnfwd_ok(n: int, cin: int, cout: int, h: int, w: int, groups: int) -> bool:
+    """Whether a conv and the GroupNorm over its output run as ``sp_conv3x3_bf16_gn`` (the moments
+    from the conv's epilogue).  Off by default (``SAMPLERS_AMD_BF16_GNFWD=1`` turns it on): measured
+    1.7 % slower per DPS bf16 step — the epilogue's reduction (shuffles, two more barriers) costs the
+    conv tile more than the statistics pass's read (profiles/round6/bf16/gn_sums_epilogue_ab/)."""
+    import os
+
+    from .layers import _query
+
+    return (os.environ.get("SAMPLERS_AMD_BF16_GNFWD", "0") == "1"
+            and bool(_query("sp_conv3x3_bf16_gn_supported", n, cin, cout, h, w, groups)))
+
+
+def _conv_gn(x: Tensor, pack: Tensor, bias: Tensor | None, cout: int, norm: nn.GroupNorm, cb: Tensor | None,
+             shape: tuple | None = None, blocked: bool = False) -> tuple[Tensor, Tensor, Tensor]:
+    """(y, z, stats): y = conv3x3(x) + bias, z = act(GN(y + cb)) on ``sp_conv3x3_bf16_gn`` (``shape``:
+    x flat channel-blocked as ``_conv_launch``; ``blocked``: z flat channel-blocked as ``_gn_fwd_raw``)."""
+    from .layers import _query
+
+    lib = _hip.load_library()
+    n, cin, h, w = x.shape if shape is None else shape
+    g = norm.num_groups
+    gamma, beta = _gn_params(norm)
+    y = torch.empty(n, cout, h, w, device=x.device, dtype=BF16, memory_format=CL)
+    if blocked:
+        z = torch.empty(n * cout * h * w, device=x.device, dtype=BF16)
+    else:
+        z = torch.empty(n, cout, h, w, device=x.device, dtype=BF16, memory_format=CL)
+    stats = torch.empty(2, n * g, device=x.device, dtype=torch.float32)
+    nb = _query("sp_conv3x3_bf16_gn_workspace", n, cout, h, w)
+    ws = torch.empty(nb, device=x.device, dtype=torch.uint8)
+    _hip.check(lib.sp_conv3x3_bf16_gn(_p(x, cl=shape is None), 0 if shape is None else 1, _p(pack, cl=False),
+                                      None if bias is None else bias.data_ptr(), None, n, cin, cout, h, w, _p(y),
+                                      None if cb is None else cb.data_ptr(),
+                                      None if gamma is None else gamma.data_ptr(),
+                                      None if beta is None else beta.data_ptr(), g, float(norm.eps), int(norm.act),
+                                      _p(z, cl=not blocked), int(blocked), stats.data_ptr(), ws.data_ptr(), nb,
+                                      _hip.stream_of(x)), "sp_conv3x3_bf16_gn")
+    return y, z, stats
+
+
 class _GroupNormBf16Fn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x1, x2, norm, cb):
@@ -628,10 +669,16 @@ class _ResnetBlockBf16Fn(torch.autograd.Function):
         # the GroupNorm outputs feed only the convs: handed over channel-blocked where the tile takes it
         b1, b2 = blocked_ok(cin, cout, hh, ww), blocked_ok(cout, cout, hh, ww)
         z1, st1 = _gn_fwd_raw(block.norm1, x1, x2, None, blocked=b1)
-        h1 = _conv_launch(z1, conv_pack(block.conv1, False), _bias_f32(block.conv1, block.conv1.bias), None,
-                          block.conv1.weight.shape[0], shape=(n, cin, hh, ww) if b1 else None)
-        del z1
-        z2, st2 = _gn_fwd_raw(block.norm2, h1, None, tb, blocked=b2)
+        cmid = block.conv1.weight.shape[0]
+        if gnfwd_ok(n, cin, cmid, hh, ww, block.norm2.num_groups):  # GN2's moments from conv1's epilogue
+            h1, z2, st2 = _conv_gn(z1, conv_pack(block.conv1, False), _bias_f32(block.conv1, block.conv1.bias), cmid,
+                                   block.norm2, tb, shape=(n, cin, hh, ww) if b1 else None, blocked=b2)
+            del z1
+        else:
+            h1 = _conv_launch(z1, conv_pack(block.conv1, False), _bias_f32(block.conv1, block.conv1.bias), None,
+                              cmid, shape=(n, cin, hh, ww) if b1 else None)
+            del z1
+            z2, st2 = _gn_fwd_raw(block.norm2, h1, None, tb, blocked=b2)
         c2 = 0 if x2 is None else x2.shape[1]
         if block.conv_shortcut is not None and sc_ok(cout, x1.shape[1], c2, hh, ww):
             # conv2 + the 1x1 shortcut as one contraction: no shortcut tensor, no residual read

@@ -487,7 +487,7 @@ def test_resnet_block_bf16_groupnorm_sums_from_conv_epilogue(cuda, monkeypatch, 
         return run(blk, cuda, BF)
 
     names = _kernel_names(gpu_vjp)
-    assert any("k_conv3x3_bf16<32, false" in s and ", true>" in s and "true, true>" not in s for s in names)
+    assert any("k_conv3x3_bf16<32, false" in s and "false, true, false>" in s for s in names)  # GS, not SC / FS
     assert not any("k_gnb_stats<1" in s for s in names), "the GroupNorm VJP sums pass still ran"
     a = gpu_vjp()
     monkeypatch.setenv("SAMPLERS_AMD_BF16_GNVJP", "0")
@@ -498,6 +498,49 @@ def test_resnet_block_bf16_groupnorm_sums_from_conv_epilogue(cuda, monkeypatch, 
     parity_record("resnet_bf16_gn_sums_epilogue_vs_two_pass_vjp", e_ab, 5e-3, shape=tag)
     parity_record("resnet_bf16_gn_sums_epilogue_vjp_vs_fp32", e_a, 1.2 * e_b + 1e-3, shape=tag, two_pass_vs_fp32=e_b)
     assert e_ab < 5e-3 and e_a <= 1.2 * e_b + 1e-3, (e_ab, e_a, e_b)
+
+
+@pytest.mark.parametrize("n,c1,c2,cout,h,w,blocked", [(2, 128, 64, 128, 32, 64, "1"), (2, 128, 0, 128, 32, 32, "0"),
+                                                      (1, 64, 64, 256, 64, 64, "1")])
+def test_resnet_block_bf16_groupnorm_moments_from_conv_epilogue(cuda, monkeypatch, parity_record, n, c1, c2, cout, h,
+                                                                w, blocked):
+    """GN2's moments taken in conv1's epilogue (sp_conv3x3_bf16_gn, opt-in: per-tile moments shifted by the
+    tile's first pixel, combined in fp64) against conv1 + the two-pass GroupNorm
+    (SAMPLERS_AMD_BF16_GNFWD=0) and the block in fp32 on the CPU, forward and input VJP."""
+    from samplers_amd.networks.unet2d import ResnetBlock2D
+
+    monkeypatch.setenv("SAMPLERS_AMD_BF16_BLOCKED", blocked)
+    monkeypatch.setenv("SAMPLERS_AMD_BF16_GNFWD", "1")  # off by default (slower, see bf16.gnfwd_ok)
+    torch.manual_seed(7)
+    ref = ResnetBlock2D(c1 + c2, cout, 64, 32, 1e-5).requires_grad_(False)
+    blk = copy.deepcopy(ref).to(cuda, BF)
+    gen = torch.Generator().manual_seed(8)
+    x = torch.randn(n, c1, h, w, generator=gen) + 0.5  # a mean offset: the moments' shift matters
+    skip = torch.randn(n, c2, h, w, generator=gen) if c2 else None
+    temb = torch.randn(n, 64, generator=gen)
+    cot = torch.randn(n, cout, h, w, generator=gen)
+
+    def run(mod, dev, dt):
+        xr = x.to(dev, dt).requires_grad_(True)
+        sr = None if skip is None else skip.to(dev, dt).requires_grad_(True)
+        with torch.enable_grad():
+            out = mod(xr, temb.to(dev, dt), skip=sr)
+        gs = torch.autograd.grad(out, (xr,) if sr is None else (xr, sr), cot.to(dev, dt))
+        return out.float().cpu(), torch.cat([g.float().cpu().reshape(-1) for g in gs])
+
+    names = _kernel_names(lambda: run(blk, cuda, BF))
+    assert any("k_conv3x3_bf16<32, false" in s and "false, false, true>" in s for s in names)  # FS
+    oa, ga = run(blk, cuda, BF)
+    monkeypatch.setenv("SAMPLERS_AMD_BF16_GNFWD", "0")
+    ob, gb = run(blk, cuda, BF)
+    orf, grf = run(ref, "cpu", torch.float32)
+    tag = [n, c1, c2, cout, h, w, blocked]
+    for what, a, b, r in (("out", oa, ob, orf), ("vjp", ga, gb, grf)):
+        e_ab, e_a, e_b = _rel(a, b), _rel(a, r), _rel(b, r)
+        parity_record(f"resnet_bf16_gn_moments_epilogue_vs_two_pass_{what}", e_ab, 5e-3, shape=tag)
+        parity_record(f"resnet_bf16_gn_moments_epilogue_{what}_vs_fp32", e_a, 1.2 * e_b + 1e-3, shape=tag,
+                      two_pass_vs_fp32=e_b)
+        assert e_ab < 5e-3 and e_a <= 1.2 * e_b + 1e-3, (what, e_ab, e_a, e_b)
 
 
 # ---- whole priors -----------------------------------------------------------------------------

@@ -32,6 +32,7 @@ elif [ "$PART" = bf16 ]; then
   step 400 bench_psld_bf16_cfg.log python -u tools/bench_psld.py --dtype bf16 --cfg --cpu-baseline
   cd /tmp && export TMPDIR=/tmp
   step 300 rocprof_psld_bf16.log rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_psld_bf16 -o run -- python3 $R/tools/bench_psld.py --dtype bf16 --steps 3 --warmup 1
+  step 300 rocprof_dps_bf16.log rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_dps_bf16 -o run -- python3 $R/bench.py --dtype bf16 --no-cpu-baseline
   cd $R
   step 400 bench_dps_bf16.log python -u bench.py --dtype bf16
   step 400 bench_psld_bf16_gloo2.log env SAMPLERS_AMD_DIST_BACKEND=gloo python -u tools/bench_psld.py --gpus 2 --dtype bf16 --batch 8 --steps 2 --warmup 1
