@@ -6,6 +6,7 @@
 #                  512² at B = 16
 #   PART=latent    PSLD fp32 / bf16 (with and without CFG) with their CPU baselines
 #   PART=bf16      PSLD bf16 (with / without CFG) and its rocprofv3 statistics again (the bf16 tiles' late changes)
+#   PART=bf16a     DPS bf16 record + rocprofv3 statistics of DPS bf16 and PSLD bf16; PART=bf16b: PSLD bf16 records
 #   PART=resample  ReSample pieces + the whole-call projection with its CPU baseline
 #   PART=dist      2- / 8-rank self-launch rehearsals over gloo and a whole 1000-step B = 1 call
 #   PART=profiles  rocprofv3 kernel statistics of the DPS (B = 64, B = 1) and PSLD fp32 / bf16 benches
@@ -36,6 +37,14 @@ elif [ "$PART" = bf16 ]; then
   cd $R
   step 400 bench_dps_bf16.log python -u bench.py --dtype bf16
   step 400 bench_psld_bf16_gloo2.log env SAMPLERS_AMD_DIST_BACKEND=gloo python -u tools/bench_psld.py --gpus 2 --dtype bf16 --batch 8 --steps 2 --warmup 1
+elif [ "$PART" = bf16a ]; then
+  step 400 bench_dps_bf16.log python -u bench.py --dtype bf16
+  cd /tmp && export TMPDIR=/tmp
+  step 300 rocprof_dps_bf16.log rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_dps_bf16 -o run -- python3 $R/bench.py --dtype bf16 --no-cpu-baseline
+  step 300 rocprof_psld_bf16.log rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_psld_bf16 -o run -- python3 $R/tools/bench_psld.py --dtype bf16 --steps 3 --warmup 1
+elif [ "$PART" = bf16b ]; then
+  step 400 bench_psld_bf16.log python -u tools/bench_psld.py --dtype bf16 --cpu-baseline
+  step 400 bench_psld_bf16_cfg.log python -u tools/bench_psld.py --dtype bf16 --cfg --cpu-baseline
 elif [ "$PART" = resample ]; then
   step 1100 bench_resample.log python -u tools/bench_resample.py --cpu-baseline --pixel-iters 2000 --latent-iters 200 --heartbeat $O/rs_heartbeat.log
 elif [ "$PART" = dist ]; then
