@@ -93,6 +93,10 @@ __device__ __forceinline__ float silu_f(float y) { return y * __builtin_amdgcn_r
 // pixel), 9 taps x 8 MFMAs per wave per stage; the next stage's global loads are issued into
 // registers before the current stage's MFMAs.
 // ---------------------------------------------------------------------------------------------
+#ifndef SP_CONV_PRIO
+#define SP_CONV_PRIO 0  // wave priority around the TC = 32 pipeline's phases (A/B knob, 0 = none)
+#endif
+
 // threadIdx.x re-read opaque to the compiler: the shortcut stages' per-thread addresses are then
 // formed inside their loop instead of being hoisted ahead of the 3x3 loop (where they were live
 // across it: the kernel spilled ~200 VGPRs)
@@ -406,6 +410,9 @@ __global__ __launch_bounds__(kBlock, TC == 4 ? 1 : 2) void k_conv3x3_bf16(const 
             __syncthreads();
             for (int s = 0; s < nst; ++s) {
                 const int b = s & 1;
+#if SP_CONV_PRIO == 1  // A/B knob: the stage hand-off and next loads issued at raised priority
+                __builtin_amdgcn_s_setprio(2);
+#endif
                 if (s + 1 < nst) st(b ^ 1);
 #if BQ_EXP == 9  // diagnostics (wrong results): no global loads after the prologue's two stages
                 (void)b;
@@ -413,7 +420,15 @@ __global__ __launch_bounds__(kBlock, TC == 4 ? 1 : 2) void k_conv3x3_bf16(const 
                 if (s + 2 < nst) gl(kb + s + 2);
 #endif
                 __builtin_amdgcn_sched_barrier(0);
+#if SP_CONV_PRIO == 1
+                __builtin_amdgcn_s_setprio(0);
+#elif SP_CONV_PRIO == 2  // A/B knob: the MFMA phase at raised priority
+                __builtin_amdgcn_s_setprio(2);
+#endif
                 cp(b);
+#if SP_CONV_PRIO == 2
+                __builtin_amdgcn_s_setprio(0);
+#endif
                 __syncthreads();
             }
         };
