@@ -838,6 +838,16 @@ struct GnbGeo {
     int cv, rows, chunks, chunk_px;
 };
 
+// non-temporal GroupNorm streams for tensors of at least SP_GNB_NT_MB MB (0 = always, negative =
+// never: the default — at 256 MB the microbenchmark's large shapes gain 5-9 % but the PSLD bf16 step
+// lost 2 %, profiles/round6/bf16/gn_nt_ab/)
+#ifndef SP_GNB_NT_MB
+#define SP_GNB_NT_MB -1
+#endif
+static bool gnb_nt(int64_t n, int c, int64_t hw) {
+    return SP_GNB_NT_MB >= 0 && 2 * n * hw * (int64_t)c >= (int64_t)SP_GNB_NT_MB * (1 << 20);
+}
+
 static GnbGeo gnb_geo(int64_t n, int c, int64_t hw) {
     GnbGeo g;
     g.cv = c / 8;
@@ -851,17 +861,35 @@ static GnbGeo gnb_geo(int64_t n, int c, int64_t hw) {
     return g;
 }
 
+// GroupNorm streams: NT = non-temporal cache policy on the loads and stores, chosen per call by the
+// tensor's size (gnb_nt: an A/B knob, off by default; below the 256 MB last-level cache the second
+// pass's re-read hits that cache and NT loses — measured, profiles/round6/bf16/gn_nt_ab/)
+template <bool NT>
+__device__ __forceinline__ bq_u4 gnb_load(const u16* p) {
+    if constexpr (NT) return __builtin_nontemporal_load(reinterpret_cast<const bq_u4*>(p));
+    return *reinterpret_cast<const bq_u4*>(p);
+}
+#ifndef SP_GNB_NT_STORE
+#define SP_GNB_NT_STORE 1  // the NT policy on the stores too (A/B knob)
+#endif
+template <bool NT>
+__device__ __forceinline__ void gnb_store(u16* p, bq_u4 v) {
+    if constexpr (NT && SP_GNB_NT_STORE) __builtin_nontemporal_store(v, reinterpret_cast<bq_u4*>(p));
+    else *reinterpret_cast<bq_u4*>(p) = v;
+}
+
 // one 16-byte vector (8 channels, column j) of pixel p of sample nn, from the part that holds it
+template <bool NT = false>
 __device__ __forceinline__ bq_u4 gnb_ld(const u16* __restrict__ x1, const u16* __restrict__ x2, int c1, int c2,
                                         int64_t nn, int64_t hw, int64_t p, int j) {
     const int ch = 8 * j;
-    if (ch < c1) return *reinterpret_cast<const bq_u4*>(x1 + ((nn * hw + p) * c1 + ch));
-    return *reinterpret_cast<const bq_u4*>(x2 + ((nn * hw + p) * c2 + ch - c1));
+    if (ch < c1) return gnb_load<NT>(x1 + ((nn * hw + p) * c1 + ch));
+    return gnb_load<NT>(x2 + ((nn * hw + p) * c2 + ch - c1));
 }
 
 // MODE 0: forward shifted sums; MODE 1: VJP sums (g, g xhat) given per-(n,c) coefs
 // co = [sc | sh | xs | xo] (each n x c fp32) and gamma (c fp32)
-template <int MODE, bool ACT>
+template <int MODE, bool ACT, bool NT = false>
 __global__ __launch_bounds__(kBlock) void k_gnb_stats(const u16* __restrict__ x1, const u16* __restrict__ x2, int c1,
                                                       int c2, const float* __restrict__ cbias,
                                                       const u16* __restrict__ dz, const float* __restrict__ co,
@@ -929,7 +957,7 @@ __global__ __launch_bounds__(kBlock) void k_gnb_stats(const u16* __restrict__ x1
                 }
             };
             auto ldz = [&](int64_t p) {
-                if constexpr (MODE == 1) return *reinterpret_cast<const bq_u4*>(dz + ((int64_t)nn * hw + p) * c + 8 * j);
+                if constexpr (MODE == 1) return gnb_load<NT>(dz + ((int64_t)nn * hw + p) * c + 8 * j);
                 else return bq_u4{0u, 0u, 0u, 0u};
             };
             // GNB_U pixels' loads in flight per thread, then their sums in pixel order (the same
@@ -939,7 +967,7 @@ __global__ __launch_bounds__(kBlock) void k_gnb_stats(const u16* __restrict__ x1
                 bq_u4 xv[GNB_U], dzv[GNB_U];
 #pragma unroll
                 for (int u = 0; u < GNB_U; ++u) {
-                    xv[u] = gnb_ld(x1, x2, c1, c2, nn, hw, p + u * rows_here, j);
+                    xv[u] = gnb_ld<NT>(x1, x2, c1, c2, nn, hw, p + u * rows_here, j);
                     dzv[u] = ldz(p + u * rows_here);
                 }
 #pragma unroll
@@ -1124,7 +1152,7 @@ __global__ __launch_bounds__(64) void k_gnb_final_bwd(const float* __restrict__ 
 // forward apply: z = act(x sc + sh) over the concatenated channels.  Grid (chunks, batch) as the
 // stats pass: a thread owns one 8-channel column of the sample, keeps its (n, c) coefficients in
 // registers and walks the chunk's pixels (the block reads rows of C channels contiguously).
-template <bool ACT>
+template <bool ACT, bool NT = false>
 __global__ __launch_bounds__(kBlock) void k_gnb_apply(const u16* __restrict__ x1, const u16* __restrict__ x2, int c1,
                                                       int c2, const float* __restrict__ co, int64_t hw, int chunk_px,
                                                       u16* __restrict__ z, int blk) {
@@ -1152,13 +1180,13 @@ __global__ __launch_bounds__(kBlock) void k_gnb_apply(const u16* __restrict__ x1
             // blk: z in the channel-blocked layout [n][c / 16][hw][16] the conv tile reads best
             const int64_t zo = blk ? (((int64_t)nn * (c >> 4) + (j >> 1)) * hw + p) * 16 + 8 * (j & 1)
                                    : ((int64_t)nn * hw + p) * c + 8 * j;
-            *reinterpret_cast<bq_u4*>(z + zo) = pack8(f);
+            gnb_store<NT>(z + zo, pack8(f));
         };
         int64_t p = p0 + row;
         for (; p + (GNB_U - 1) * rows < p1; p += GNB_U * rows) {  // GNB_U pixels' loads in flight
             bq_u4 xv[GNB_U];
 #pragma unroll
-            for (int u = 0; u < GNB_U; ++u) xv[u] = gnb_ld(x1, x2, c1, c2, nn, hw, p + u * rows, j);
+            for (int u = 0; u < GNB_U; ++u) xv[u] = gnb_ld<NT>(x1, x2, c1, c2, nn, hw, p + u * rows, j);
 #pragma unroll
             for (int u = 0; u < GNB_U; ++u) one(xv[u], p + u * rows);
         }
@@ -1173,7 +1201,7 @@ __device__ __forceinline__ void ld8f(const float* p, float (&f)[8]) {
 
 // VJP apply: dx = A dy' + B x + D (+ add1 / add2 / add1b), written to the parts' layouts; grid
 // and column ownership as k_gnb_apply (the five (n, c) coefficient rows held in registers)
-template <bool ACT>
+template <bool ACT, bool NT = false>
 __global__ __launch_bounds__(kBlock) void k_gnb_bwd_apply(const u16* __restrict__ dz, const u16* __restrict__ x1,
                                                           const u16* __restrict__ x2, int c1, int c2,
                                                           const float* __restrict__ co, const float* __restrict__ co2,
@@ -1233,11 +1261,11 @@ __global__ __launch_bounds__(kBlock) void k_gnb_bwd_apply(const u16* __restrict_
             }
             // blk (one part): dx in the channel-blocked layout [n][c / 16][hw][16]
             const int64_t oo = blk ? (((int64_t)nn * (cp >> 4) + (chp >> 4)) * hw + p) * 16 + (chp & 15) : off;
-            *reinterpret_cast<bq_u4*>(dst + oo) = pack8(o);
+            gnb_store<NT>(dst + oo, pack8(o));
         };
         const bq_u4 zero4 = {0u, 0u, 0u, 0u};
         auto ld = [&](const u16* __restrict__ src, int64_t off) {
-            return src ? *reinterpret_cast<const bq_u4*>(src + off) : zero4;
+            return src ? gnb_load<NT>(src + off) : zero4;
         };
         int64_t p = p0 + row;
         for (; p + (GNB_U - 1) * rows < p1; p += GNB_U * rows) {  // GNB_U pixels' loads in flight
@@ -1245,8 +1273,8 @@ __global__ __launch_bounds__(kBlock) void k_gnb_bwd_apply(const u16* __restrict_
 #pragma unroll
             for (int u = 0; u < GNB_U; ++u) {
                 const int64_t pp = p + u * rows, off = ((int64_t)nn * hw + pp) * cp + chp;
-                xv[u] = *reinterpret_cast<const bq_u4*>(xs + off);
-                dv[u] = *reinterpret_cast<const bq_u4*>(dz + ((int64_t)nn * hw + pp) * c + ch);
+                xv[u] = gnb_load<NT>(xs + off);
+                dv[u] = gnb_load<NT>(dz + ((int64_t)nn * hw + pp) * c + ch);
                 av[u] = ld(a, off);
                 bv[u] = ld(ab, off);
             }
@@ -2125,18 +2153,22 @@ int sp_groupnorm_bf16_fwd_ex(const void* x1, const void* x2, int32_t c1, int32_t
     float* co = part + n * g.chunks * 2 * (int64_t)c;
     const u16* a = static_cast<const u16*>(x1);
     const u16* b = static_cast<const u16*>(x2);
-    launch(0, k_gnb_stats<0, false>, dim3(g.chunks, static_cast<unsigned>(n)), dim3(kBlock), s, a, b, c1, c2,
-           chan_bias, static_cast<const u16*>(nullptr), static_cast<const float*>(nullptr),
-           static_cast<const float*>(nullptr), hw, g.chunk_px, part);
+    const bool nt = gnb_nt(n, c, hw);
+    const dim3 grid(g.chunks, static_cast<unsigned>(n));
+    auto stats_pass = [&](auto kern) {
+        launch(0, kern, grid, dim3(kBlock), s, a, b, c1, c2, chan_bias, static_cast<const u16*>(nullptr),
+               static_cast<const float*>(nullptr), static_cast<const float*>(nullptr), hw, g.chunk_px, part);
+    };
+    if (nt) stats_pass(k_gnb_stats<0, false, true>);
+    else stats_pass(k_gnb_stats<0, false, false>);
     launch(0, k_gnb_final_fwd, dim3(groups, static_cast<unsigned>(n)), dim3(64), s, a, b, c1, c2, chan_bias,
            static_cast<const float*>(part), g.chunks, hw, groups, eps, gamma, beta, stats, co);
-    const dim3 grid(g.chunks, static_cast<unsigned>(n));
-    if (act)
-        launch(0, k_gnb_apply<true>, grid, dim3(kBlock), s, a, b, c1, c2, static_cast<const float*>(co), hw, g.chunk_px,
+    auto apply_pass = [&](auto kern) {
+        launch(0, kern, grid, dim3(kBlock), s, a, b, c1, c2, static_cast<const float*>(co), hw, g.chunk_px,
                static_cast<u16*>(z), static_cast<int>(z_layout));
-    else
-        launch(0, k_gnb_apply<false>, grid, dim3(kBlock), s, a, b, c1, c2, static_cast<const float*>(co), hw,
-               g.chunk_px, static_cast<u16*>(z), static_cast<int>(z_layout));
+    };
+    if (act) nt ? apply_pass(k_gnb_apply<true, true>) : apply_pass(k_gnb_apply<true, false>);
+    else nt ? apply_pass(k_gnb_apply<false, true>) : apply_pass(k_gnb_apply<false, false>);
     return check_launch("sp_groupnorm_bf16_fwd");
 }
 
@@ -2175,25 +2207,24 @@ int sp_groupnorm_bf16_bwd_ex(const void* dz, const void* x1, const void* x2, int
     const int64_t nc = n * c;
     launch(0, k_gnb_coefs, dim3(static_cast<unsigned>((nc + kBlock - 1) / kBlock)), dim3(kBlock), s, stats, chan_bias,
            gamma, beta, static_cast<int>(n), c, groups, co);
-    if (act)
-        launch(0, k_gnb_stats<1, true>, dim3(g.chunks, static_cast<unsigned>(n)), dim3(kBlock), s, a, b, c1, c2,
-               chan_bias, d, static_cast<const float*>(co), gamma, hw, g.chunk_px, part);
-    else
-        launch(0, k_gnb_stats<1, false>, dim3(g.chunks, static_cast<unsigned>(n)), dim3(kBlock), s, a, b, c1, c2,
-               chan_bias, d, static_cast<const float*>(co), gamma, hw, g.chunk_px, part);
+    const bool nt = gnb_nt(n, c, hw);
+    const dim3 grid(g.chunks, static_cast<unsigned>(n));
+    auto stats_pass = [&](auto kern) {
+        launch(0, kern, grid, dim3(kBlock), s, a, b, c1, c2, chan_bias, d, static_cast<const float*>(co), gamma, hw,
+               g.chunk_px, part);
+    };
+    if (act) nt ? stats_pass(k_gnb_stats<1, true, true>) : stats_pass(k_gnb_stats<1, true, false>);
+    else nt ? stats_pass(k_gnb_stats<1, false, true>) : stats_pass(k_gnb_stats<1, false, false>);
     launch(0, k_gnb_final_bwd, dim3(groups, static_cast<unsigned>(n)), dim3(64), s, static_cast<const float*>(part),
            g.chunks, hw, c, groups, stats, gamma, static_cast<const float*>(co), co2);
-    const dim3 grid(g.chunks, static_cast<unsigned>(n));
-    if (act)
-        launch(0, k_gnb_bwd_apply<true>, grid, dim3(kBlock), s, d, a, b, c1, c2, static_cast<const float*>(co),
+    auto apply_pass = [&](auto kern) {
+        launch(0, kern, grid, dim3(kBlock), s, d, a, b, c1, c2, static_cast<const float*>(co),
                static_cast<const float*>(co2), hw, g.chunk_px, static_cast<u16*>(dx1), static_cast<u16*>(dx2),
                static_cast<const u16*>(add1), static_cast<const u16*>(add2), static_cast<const u16*>(add1b),
                static_cast<int>(dx_layout));
-    else
-        launch(0, k_gnb_bwd_apply<false>, grid, dim3(kBlock), s, d, a, b, c1, c2, static_cast<const float*>(co),
-               static_cast<const float*>(co2), hw, g.chunk_px, static_cast<u16*>(dx1), static_cast<u16*>(dx2),
-               static_cast<const u16*>(add1), static_cast<const u16*>(add2), static_cast<const u16*>(add1b),
-               static_cast<int>(dx_layout));
+    };
+    if (act) nt ? apply_pass(k_gnb_bwd_apply<true, true>) : apply_pass(k_gnb_bwd_apply<true, false>);
+    else nt ? apply_pass(k_gnb_bwd_apply<false, true>) : apply_pass(k_gnb_bwd_apply<false, false>);
     return check_launch("sp_groupnorm_bf16_bwd");
 }
 
