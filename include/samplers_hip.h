@@ -614,7 +614,8 @@ int sp_groupnorm_bf16_bwd(const void* dz, const void* x1, const void* x2, int32_
                           const void* add2, const void* add1b, void* ws, int64_t ws_bytes, sp_stream_t stream);
 /* The same with a chosen layout for z (z_layout 1: channel-blocked [n][c/16][hw][16], c % 16 == 0:
  * the conv tile's preferred input, sp_conv3x3_bf16_ex) / for dx1 (dx_layout 1: one part, c1 % 16 == 0;
- * the addends stay NHWC). */
+ * the addends stay NHWC; dx_layout 2: dx1 / dx2 NHWC, add1 one addend over the concatenated channels
+ * [n][hw][c1 + c2] and add2 NULL — a 1x1 shortcut's input gradient from one GEMM). */
 int sp_groupnorm_bf16_fwd_ex(const void* x1, const void* x2, int32_t c1, int32_t c2, const float* chan_bias,
                              const float* gamma, const float* beta, int64_t n, int64_t hw, int32_t groups, float eps,
                              int32_t act, void* z, int32_t z_layout, float* stats, void* ws, int64_t ws_bytes,

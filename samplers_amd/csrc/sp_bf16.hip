@@ -1229,7 +1229,10 @@ __global__ __launch_bounds__(kBlock) void k_gnb_bwd_apply(const u16* __restrict_
         const bool first = ch < c1;
         const int cp = first ? c1 : c2, chp = first ? ch : ch - c1;
         u16* __restrict__ dst = first ? dx1 : dx2;
-        const u16* __restrict__ a = first ? add1 : add2;
+        // blk & 2: add1 is one addend over the concatenated channels ([n][hw][c1 + c2], e.g. the
+        // 1x1 shortcut's input gradient from one GEMM), add2 unused
+        const bool acat = (blk & 2) != 0;
+        const u16* __restrict__ a = acat ? add1 : first ? add1 : add2;
         const u16* __restrict__ ab = first ? add1b : nullptr;
         const u16* __restrict__ xs = first ? x1 : x2;
         // one pixel from its loaded vectors (x, dy', and the addends or zeros)
@@ -1259,8 +1262,8 @@ __global__ __launch_bounds__(kBlock) void k_gnb_bwd_apply(const u16* __restrict_
 #pragma unroll
                 for (int e = 0; e < 8; ++e) o[e] += t[e];
             }
-            // blk (one part): dx in the channel-blocked layout [n][c / 16][hw][16]
-            const int64_t oo = blk ? (((int64_t)nn * (cp >> 4) + (chp >> 4)) * hw + p) * 16 + (chp & 15) : off;
+            // blk & 1 (one part): dx in the channel-blocked layout [n][c / 16][hw][16]
+            const int64_t oo = (blk & 1) ? (((int64_t)nn * (cp >> 4) + (chp >> 4)) * hw + p) * 16 + (chp & 15) : off;
             gnb_store<NT>(dst + oo, pack8(o));
         };
         const bq_u4 zero4 = {0u, 0u, 0u, 0u};
@@ -1275,7 +1278,7 @@ __global__ __launch_bounds__(kBlock) void k_gnb_bwd_apply(const u16* __restrict_
                 const int64_t pp = p + u * rows, off = ((int64_t)nn * hw + pp) * cp + chp;
                 xv[u] = gnb_load<NT>(xs + off);
                 dv[u] = gnb_load<NT>(dz + ((int64_t)nn * hw + pp) * c + ch);
-                av[u] = ld(a, off);
+                av[u] = ld(a, acat ? ((int64_t)nn * hw + pp) * c + ch : off);
                 bv[u] = ld(ab, off);
             }
 #pragma unroll
@@ -1284,8 +1287,8 @@ __global__ __launch_bounds__(kBlock) void k_gnb_bwd_apply(const u16* __restrict_
         }
         for (; p < p1; p += rows) {
             const int64_t off = ((int64_t)nn * hw + p) * cp + chp;
-            one(*reinterpret_cast<const bq_u4*>(xs + off),
-                *reinterpret_cast<const bq_u4*>(dz + ((int64_t)nn * hw + p) * c + ch), ld(a, off), ld(ab, off), off, p);
+            one(*reinterpret_cast<const bq_u4*>(xs + off), *reinterpret_cast<const bq_u4*>(dz + ((int64_t)nn * hw + p) * c + ch),
+                ld(a, acat ? ((int64_t)nn * hw + p) * c + ch : off), ld(ab, off), off, p);
         }
     }
 }
@@ -2183,7 +2186,8 @@ int sp_groupnorm_bf16_bwd(const void* dz, const void* x1, const void* x2, int32_
 }
 
 // dx_layout 1 (one part, c2 == 0, c1 % 16 == 0): dx1 in the channel-blocked layout [n][c / 16][hw][16]
-// (the addends stay NHWC)
+// (the addends stay NHWC); dx_layout 2: dx1 / dx2 NHWC and add1 one addend over the concatenated
+// channels [n][hw][c1 + c2] (add2 NULL; the outputs must not alias it)
 int sp_groupnorm_bf16_bwd_ex(const void* dz, const void* x1, const void* x2, int32_t c1, int32_t c2,
                              const float* chan_bias, const float* gamma, const float* beta, const float* stats,
                              int64_t n, int64_t hw, int32_t groups, int32_t act, void* dx1, void* dx2, int32_t dx_layout,
@@ -2192,7 +2196,7 @@ int sp_groupnorm_bf16_bwd_ex(const void* dz, const void* x1, const void* x2, int
     if (!dz || !x1 || (c2 && (!x2 || !dx2)) || !dx1 || !stats || !ws || n <= 0 || hw <= 0 ||
         !sp_groupnorm_bf16_supported(c1, c2, groups))
         return SP_EINVAL;
-    if (dx_layout != 0 && (dx_layout != 1 || c2 || c1 % 16)) return SP_EINVAL;
+    if (dx_layout != 0 && (dx_layout != 1 || c2 || c1 % 16) && (dx_layout != 2 || add2)) return SP_EINVAL;
     const int c = c1 + c2;
     if (ws_bytes < sp_groupnorm_bf16_workspace(n, c, hw) || n * hw * c >= (int64_t(1) << 40) || n > 65535)
         return SP_EINVAL;

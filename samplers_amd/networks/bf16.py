@@ -365,10 +365,11 @@ def _gn_fwd_raw(norm: nn.GroupNorm, x1: Tensor, x2: Tensor | None, cb: Tensor | 
 def _gn_bwd_raw(norm: nn.GroupNorm, dz: Tensor, x1: Tensor, x2: Tensor | None, cb: Tensor | None, stats: Tensor,
                 add1: Tensor | None = None, add2: Tensor | None = None, out1: Tensor | None = None,
                 out2: Tensor | None = None, blocked: bool = False,
-                add1b: Tensor | None = None) -> tuple[Tensor, Tensor | None]:
+                add1b: Tensor | None = None, add_cat: bool = False) -> tuple[Tensor, Tensor | None]:
     """Input VJP of ``_gn_fwd_raw`` into the parts' layouts, + the addends (channels-last, shaped
     like the parts) added in the kernel; ``out1`` / ``out2`` may be the addends (in place);
     ``add1b``: a second addend of dx1 (a skip tensor's up-block gradient, layers.SkipGrad);
+    ``add_cat``: ``add1`` is one channels-last addend over cat(x1, x2)'s channels (``add2`` None);
     ``blocked`` (one part): dx1 as a flat channel-blocked buffer for the next conv VJP."""
     lib = _hip.load_library()
     n, c1, h, w = x1.shape
@@ -385,7 +386,8 @@ def _gn_bwd_raw(norm: nn.GroupNorm, dz: Tensor, x1: Tensor, x2: Tensor | None, c
                                             None if gamma is None else gamma.data_ptr(),
                                             None if beta is None else beta.data_ptr(), stats.data_ptr(), n, h * w,
                                             norm.num_groups, int(norm.act), _p(dx1, cl=not blocked), _p(dx2),
-                                            int(blocked), _p(add1), _p(add2), _p(add1b), ws.data_ptr(), nb,
+                                            2 if add_cat else int(blocked), _p(add1), _p(add2), _p(add1b),
+                                            ws.data_ptr(), nb,
                                             _hip.stream_of(dz)), "sp_groupnorm_bf16_bwd_ex")
     return dx1, dx2
 
@@ -708,6 +710,8 @@ class _ResnetBlockBf16Fn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dout):
+        import os
+
         x1, x2, h1, tb, st1, st2 = ctx.saved_tensors
         blk = ctx.block
         dout = nhwc(dout.to(BF16))
@@ -730,15 +734,22 @@ class _ResnetBlockBf16Fn(torch.autograd.Function):
         extra = ctx.box_in.take() if ctx.box_in is not None else None
         if extra is not None:
             extra = nhwc(extra.to(BF16))
+        fused_gn1 = cmid % 16 == 0 and gnvjp_ok(n, cmid, cin, hh, ww, c1, blk.norm1.num_groups)
         if blk.conv_shortcut is None:  # identity shortcut: dx1 = GN1^T dz1 + dout (+ skip grad)
             adds = dict(add1=dout, add1b=extra)
-        else:  # s = shortcut^T dout per part (pixel rows), then += GN1^T dz1 in place
+        elif fused_gn1 or os.environ.get("SAMPLERS_AMD_BF16_SCVJP", "1") == "0":
+            # s = shortcut^T dout per part (pixel rows), then += GN1^T dz1 in place
             w1, w2 = _shortcut_w(blk, c1)
             d = _rows(dout)
             s1 = (d @ w1).reshape(n, hh, ww, c1).permute(0, 3, 1, 2)
             s2 = None if x2 is None else (d @ w2).reshape(n, hh, ww, x2.shape[1]).permute(0, 3, 1, 2)
             adds = dict(add1=s1, add2=s2, out1=s1, out2=s2, add1b=extra)
-        if cmid % 16 == 0 and gnvjp_ok(n, cmid, cin, hh, ww, c1, blk.norm1.num_groups):  # GN1 sums: conv1^T's epilogue
+        else:  # shortcut^T dout over cat(x1, x2)'s channels as one GEMM (dout read once), added by GN1's VJP
+            wfull = _cached(blk.conv_shortcut, "w2d", _wkey(blk.conv_shortcut.weight),
+                            lambda: blk.conv_shortcut.weight.detach().reshape(cout, cin).contiguous())
+            sc = (_rows(dout) @ wfull).reshape(n, hh, ww, cin).permute(0, 3, 1, 2)
+            adds = dict(add1=sc, add1b=extra, add_cat=True)
+        if fused_gn1:  # GN1 sums: conv1^T's epilogue
             dx1, dx2 = _conv_gn_vjp(dh1, conv_pack(blk.conv1, True), cmid, blk.norm1, x1, x2, None, st1,
                                     dy_blocked=bl, **adds)
         else:
